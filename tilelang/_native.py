@@ -1,0 +1,31 @@
+"""Loader for the in-tree native runtime extension (``tilelang/_tl_runtime*.so``, built from csrc/).
+
+There is deliberately no Python fallback: if the extension is missing, kernels cannot run and the
+error says how to build it (``python setup.py build_ext --inplace``).
+"""
+_rt = None
+
+
+class NativeRuntimeMissing(ImportError):
+    pass
+
+
+def runtime():
+    global _rt
+    if _rt is None:
+        try:
+            from . import _tl_runtime as m  # noqa: F401
+        except ImportError as e:
+            raise NativeRuntimeMissing(
+                "tilelang native runtime not built: run `python setup.py build_ext --inplace` "
+                f"in the repository root ({e})") from e
+        _rt = m
+    return _rt
+
+
+def available() -> bool:
+    try:
+        runtime()
+        return True
+    except ImportError:
+        return False

@@ -1,0 +1,509 @@
+"""gfx950 HIP C++ emitter (and the CPU C++ emitter used by the plumbing target).
+
+Reference: ``src/target/codegen_hip.cc`` (``CodeGenTileLangHIP``: ``extern "C"
+__global__`` with ``__launch_bounds__``, dynamic LDS, MFMA intrinsics) and
+``src/target/codegen_cpp.cc`` / ``codegen_c_host.cc`` for CPU.  Unlike the
+reference there is no separate host stub: the kernel is launched by the native
+runtime (``csrc/tl_runtime.cpp``) through ``hipModuleLaunchKernel`` with a packed
+argument array, and CPU kernels are called through a generated ``tl_entry(void**)``.
+"""
+from __future__ import annotations
+
+import math
+import re
+from typing import Dict, List, Optional
+
+from ..ir import stmt as S
+from ..ir import lowered as L
+from ..ir import dtypes as _dt
+from ..ir.buffer import Buffer
+from ..ir.expr import (BinOp, BufferLoad, Call, Cast, FloatImm, IntImm, PrimExpr, Select, StringImm, UnOp, Var,
+                       is_nonneg, as_int, free_vars)
+
+_MATH = {
+    "exp", "exp2", "exp10", "log", "log2", "log10", "log1p", "expm1", "sqrt", "rsqrt", "rcp", "sin", "cos", "tan",
+    "asin", "acos", "atan", "sinh", "cosh", "tanh", "erf", "floor", "ceil", "trunc", "round", "nearbyint", "sigmoid",
+    "abs", "pow", "fmod", "atan2", "fma", "isnan", "isinf", "isfinite", "fast_exp", "fast_exp2", "fast_exp10",
+    "fast_log", "fast_log2", "fast_log10", "fast_sin", "fast_cos", "fast_tan"
+}
+
+_C_KEYWORDS = {"int", "float", "double", "char", "long", "short", "void", "for", "if", "else", "while", "do",
+               "return", "break", "continue", "switch", "case", "default", "auto", "const", "static", "signed",
+               "unsigned", "struct", "union", "enum", "typedef", "goto", "sizeof", "volatile", "register", "extern",
+               "inline", "new", "delete", "class", "template", "this", "half", "bool", "true", "false", "min", "max",
+               "abs", "exp", "log", "tid", "lane", "wave", "tl", "smem", "tl_smem"}
+
+
+class CodeGenError(Exception):
+    pass
+
+
+class KernelSource:
+    """Result of code generation."""
+
+    def __init__(self):
+        self.source = ""
+        self.kernel_name = ""
+        self.params: List[dict] = []      # runtime argument spec
+        self.grid: List[PrimExpr] = []
+        self.block: List[int] = []
+        self.lds_bytes = 0
+        self.is_cpu = False
+        self.dyn_vars: List[Var] = []
+
+
+class CodeGen:
+
+    def __init__(self, func: S.PrimFunc, kernel: S.KernelStmt, target, lds_offsets: Dict[Buffer, int],
+                 lds_total: int, pass_cfg=None):
+        self.func = func
+        self.kernel = kernel
+        self.target = target
+        self.is_cpu = kernel.is_cpu or getattr(target, "kind", "hip") == "cpu"
+        self.lds_offsets = lds_offsets
+        self.lds_total = lds_total
+        self.lines: List[str] = []
+        self.ind = 1
+        self.names: Dict[int, str] = {}
+        self.used_names = set()
+        self.pass_cfg = pass_cfg or {}
+        self.fast_math = bool(self.pass_cfg.get("tl.enable_fast_math", False))
+        self.param_ptr: Dict[Buffer, str] = {}
+
+    # -- names ------------------------------------------------------------------------
+    def name_of(self, obj, base: str) -> str:
+        k = id(obj)
+        if k in self.names:
+            return self.names[k]
+        base = re.sub(r"[^A-Za-z0-9_]", "_", base) or "v"
+        if base[0].isdigit():
+            base = "v" + base
+        if base in _C_KEYWORDS:
+            base = base + "_"
+        name = base
+        i = 1
+        while name in self.used_names:
+            name = f"{base}_{i}"
+            i += 1
+        self.used_names.add(name)
+        self.names[k] = name
+        self._keep = getattr(self, "_keep", [])
+        self._keep.append(obj)
+        return name
+
+    def buf_name(self, b: Buffer) -> str:
+        key = getattr(b, "orig", None)
+        return self.name_of(b, b.name)
+
+    # -- expressions ---------------------------------------------------------------------
+    def ctype(self, dt) -> str:
+        return _dt.cpu_type(dt) if self.is_cpu else _dt.hip_type(dt)
+
+    def e(self, x) -> str:
+        if isinstance(x, bool):
+            return "true" if x else "false"
+        if isinstance(x, int):
+            return str(x)
+        if isinstance(x, str):
+            return x
+        if isinstance(x, IntImm):
+            dt = x.dtype
+            if dt.is_bool:
+                return "true" if x.value else "false"
+            if dt.name == "int64":
+                return f"{x.value}LL"
+            if dt.name in ("uint32", ):
+                return f"{x.value}u"
+            if dt.name == "uint64":
+                return f"{x.value}ULL"
+            if dt.name == "int32":
+                return str(x.value) if x.value >= -2**31 + 1 else f"({x.value + 1} - 1)"
+            return f"(({self.ctype(dt)}){x.value})"
+        if isinstance(x, FloatImm):
+            return self.float_lit(x.value, x.dtype)
+        if isinstance(x, StringImm):
+            return '"' + x.value.replace('"', '\\"') + '"'
+        if isinstance(x, Var):
+            return self.name_of(x, x.name)
+        if isinstance(x, L.BufferPtr):
+            return f"(&{self.buf_ref(x.buffer)}[{self.e(x.offset)}])"
+        if isinstance(x, BinOp):
+            return self.binop(x)
+        if isinstance(x, UnOp):
+            return f"({x.op}{self.e(x.a)})"
+        if isinstance(x, Cast):
+            return self.cast(x.value, x.dtype)
+        if isinstance(x, Select):
+            return f"({self.e(x.cond)} ? {self.e(x.t)} : {self.e(x.f)})"
+        if isinstance(x, BufferLoad):
+            return f"{self.buf_ref(x.buffer)}[{self.e(x.indices[0])}]"
+        if isinstance(x, Call):
+            return self.call(x)
+        raise CodeGenError(f"cannot emit expression {type(x).__name__}: {x}")
+
+    def float_lit(self, v: float, dt) -> str:
+        if math.isinf(v):
+            s = ("-" if v < 0 else "") + ("__builtin_huge_valf()" if dt.bits <= 32 else "__builtin_huge_val()")
+        elif math.isnan(v):
+            s = "__builtin_nanf(\"\")"
+        else:
+            s = repr(float(v))
+            if "e" not in s and "." not in s:
+                s += ".0"
+            if dt.bits <= 32:
+                s += "f"
+        if dt.name in ("float32", "float64"):
+            return s if not s.startswith("-") else f"({s})"
+        return self.cast_str(s, _dt.float32, dt)
+
+    def cast_str(self, s: str, src, dst) -> str:
+        if dst.is_fp8 and not self.is_cpu:
+            return f"{self.ctype(dst)}((float)({s}))"
+        if src.is_fp8 and not self.is_cpu:
+            return f"(({self.ctype(dst)})(float)({s}))"
+        if self.is_cpu and (dst.name in ("float16", "bfloat16") or src.name in ("float16", "bfloat16")):
+            if dst.name in ("float16", "bfloat16"):
+                return f"{self.ctype(dst)}((float)({s}))"
+            return f"(({self.ctype(dst)})(float)({s}))"
+        if dst.is_bool:
+            return f"(bool)({s})"
+        return f"(({self.ctype(dst)})({s}))"
+
+    def cast(self, v, dt) -> str:
+        return self.cast_str(self.e(v), v.dtype, dt)
+
+    def binop(self, x: BinOp) -> str:
+        a, b = self.e(x.a), self.e(x.b)
+        op = x.op
+        if op in ("min", "max"):
+            if x.dtype.is_float and x.dtype.bits == 32:
+                return f"__builtin_f{op}f({a}, {b})"
+            return f"tl::{op}_({a}, {b})"
+        if op == "//":
+            if x.dtype.is_float:
+                return f"floorf({a} / {b})" if not self.is_cpu else f"std::floor({a} / {b})"
+            if is_nonneg(x.a) and is_nonneg(x.b):
+                return f"({a} / {b})"
+            return f"tl::floordiv({a}, {b})"
+        if op == "%":
+            if x.dtype.is_float:
+                return f"fmodf({a}, {b})"
+            if is_nonneg(x.a) and is_nonneg(x.b):
+                return f"({a} % {b})"
+            return f"tl::floormod({a}, {b})"
+        if op in ("&&", "||"):
+            return f"({a} {op} {b})"
+        return f"({a} {op} {b})"
+
+    def call(self, x: Call) -> str:
+        op = x.op
+        args = x.args
+        if op in _MATH:
+            if self.fast_math and op in ("exp", "log", "exp2", "log2", "sin", "cos") and \
+                    x.dtype.name == "float32":
+                op = "fast_" + op
+            return f"tl::{op}({', '.join(self.e(a) for a in args)})"
+        if op == "extern":
+            name = args[0].value if isinstance(args[0], StringImm) else args[0]
+            return f"{name}({', '.join(self.e(a) for a in args[1:])})"
+        if op == "tl.lane_id":
+            return "tl::lane_id()" if not self.is_cpu else "0"
+        if op == "tl.wave_id":
+            return "tl::wave_id()" if not self.is_cpu else "0"
+        if op in ("tl.shfl_xor", "tl.shfl_down", "tl.shfl_up", "tl.shfl"):
+            fn = op.split(".")[1]
+            return f"tl::{fn}({', '.join(self.e(a) for a in args)})"
+        if op.startswith("tl.wave_reduce_"):
+            return f"tl::{op[3:]}({self.e(args[0])})"
+        if op.startswith("tl.atomic_"):
+            kind = op[len("tl.atomic_"):]
+            if kind in ("add", "max", "min"):
+                return f"tl::atomic_{kind}(&{self.e(args[0])}, {self.e(args[1])})"
+            if kind == "load":
+                return f"tl::atomic_load(&{self.e(args[0])})"
+            if kind == "store":
+                return f"tl::atomic_store(&{self.e(args[0])}, {self.e(args[1])})"
+        if op == "tl.clock":
+            return "clock64()" if not self.is_cpu else "0"
+        if op == "tl.ballot":
+            return f"__ballot({self.e(args[0])})"
+        if op == "tl.dp4a":
+            return f"__builtin_amdgcn_sdot4({self.e(args[0])}, {self.e(args[1])}, {self.e(args[2])}, false)"
+        if op == "tl.reinterpret":
+            return f"__builtin_bit_cast({self.ctype(x.dtype)}, {self.e(args[0])})"
+        if op == "tl.pack_b16":
+            return (f"((uint32_t)__builtin_bit_cast(uint16_t, {self.e(args[0])}) | "
+                    f"((uint32_t)__builtin_bit_cast(uint16_t, {self.e(args[1])}) << 16))")
+        if op == "tl.address_of":
+            return f"(&{self.e(args[0])})"
+        if op == "tl.mesh_rank":
+            return "tl_mesh_rank"
+        if op == "tl.sync_threads":
+            return "__syncthreads()"
+        if op == "tl.fence":
+            return "tl::fence_agent()"
+        raise CodeGenError(f"unknown intrinsic {op}")
+
+    def buf_ref(self, b: Buffer) -> str:
+        return self.buf_name(b)
+
+    # -- statements -----------------------------------------------------------------------
+    def w(self, line: str):
+        self.lines.append("  " * self.ind + line)
+
+    def s(self, st):
+        if st is None:
+            return
+        if isinstance(st, S.SeqStmt):
+            scoped = getattr(st, "scoped", False)
+            if scoped:
+                self.w("{")
+                self.ind += 1
+            for c in st.stmts:
+                self.s(c)
+            if scoped:
+                self.ind -= 1
+                self.w("}")
+        elif isinstance(st, S.ForStmt):
+            v = self.e(st.var)
+            mn, ext = st.min, st.extent
+            end = mn + ext
+            if st.kind == "unroll" or (as_int(ext) is not None and as_int(ext) <= 8 and st.kind != "serial"):
+                self.w("#pragma unroll")
+            elif st.annotations.get("unroll_factor"):
+                self.w(f"#pragma unroll {int(st.annotations['unroll_factor'])}")
+            self.w(f"for (int {v} = {self.e(mn)}; {v} < {self.e(end)}; ++{v}) {{")
+            self.ind += 1
+            self.s(st.body)
+            self.ind -= 1
+            self.w("}")
+        elif isinstance(st, S.WhileStmt):
+            self.w(f"while ({self.e(st.cond)}) {{")
+            self.ind += 1
+            self.s(st.body)
+            self.ind -= 1
+            self.w("}")
+        elif isinstance(st, S.IfStmt):
+            self.w(f"if ({self.e(st.cond)}) {{")
+            self.ind += 1
+            self.s(st.then_body)
+            self.ind -= 1
+            if st.else_body is not None:
+                self.w("} else {")
+                self.ind += 1
+                self.s(st.else_body)
+                self.ind -= 1
+            self.w("}")
+        elif isinstance(st, S.StoreStmt):
+            b = st.buffer
+            self.w(f"{self.buf_ref(b)}[{self.e(st.indices[0])}] = {self.e(st.value)};")
+        elif isinstance(st, S.LetStmt):
+            self.w(f"const {self.ctype(st.var.dtype)} {self.e(st.var)} = {self.e(st.value)};")
+        elif isinstance(st, S.EvaluateStmt):
+            self.w(f"{self.e(st.expr)};")
+        elif isinstance(st, S.AllocStmt):
+            self.alloc(st.buffer)
+        elif isinstance(st, S.BreakStmt):
+            self.w("break;")
+        elif isinstance(st, S.ContinueStmt):
+            self.w("continue;")
+        elif isinstance(st, S.AssertStmt):
+            if not self.is_cpu:
+                self.w(f'tl::device_assert({self.e(st.cond)}, "{st.msg}");')
+            else:
+                self.w(f'if (!({self.e(st.cond)})) {{ return; }}')
+        elif isinstance(st, S.AttrStmt):
+            self.s(st.body)
+        elif isinstance(st, S.RawStmt):
+            for ln in st.code.splitlines():
+                self.w(ln)
+        elif isinstance(st, L.CallStmt):
+            t = f"<{', '.join(st.targs)}>" if st.targs else ""
+            self.w(f"{st.name}{t}({', '.join(self.e(a) for a in st.args)});")
+        elif isinstance(st, L.VecStoreStmt):
+            b = st.buffer
+            n = len(st.values)
+            ct = self.ctype(b.dtype)
+            vals = ", ".join(self.e(v) for v in st.values)
+            self.w(f"{{ {ct} _v[{n}] = {{{vals}}}; tl::store_vec<{ct}, {n}>(&{self.buf_ref(b)}[{self.e(st.index)}], _v); }}")
+        elif isinstance(st, L.VecLoadStmt):
+            ct = self.ctype(st.src.dtype)
+            self.w(f"tl::load_vec<{ct}, {st.n}>(*reinterpret_cast<{ct}(*)[{st.n}]>(&{self.buf_ref(st.dst)}[{st.dst_index}]), "
+                   f"&{self.buf_ref(st.src)}[{self.e(st.src_index)}]);")
+        elif isinstance(st, L.CopyBytesStmt):
+            self.w(f"tl::copy_bytes<{st.nbytes}>(&{self.buf_ref(st.dst)}[{self.e(st.dst_index)}], "
+                   f"&{self.buf_ref(st.src)}[{self.e(st.src_index)}]);")
+        elif isinstance(st, L.CommentStmt):
+            self.w(f"// {st.text}")
+        elif isinstance(st, S.KernelStmt):
+            raise CodeGenError("nested kernel")
+        elif isinstance(st, S.TileOpStmt):
+            raise CodeGenError(f"unlowered tile op {st.op.kind}")
+        else:
+            raise CodeGenError(f"cannot emit {type(st).__name__}")
+
+    def alloc(self, b: Buffer):
+        ct = self.ctype(b.dtype)
+        name = self.buf_name(b)
+        if b.scope == "shared":
+            if self.is_cpu:
+                self.w(f"static {ct} {name}[{int(b.shape[0])}];")
+                return
+            off = self.lds_offsets[b]
+            self.w(f"{ct}* {name} = reinterpret_cast<{ct}*>(tl_smem + {off});")
+        elif b.scope in ("local", "var", "fragment"):
+            n = as_int(b.numel())
+            if n is None:
+                raise CodeGenError(f"local buffer {b.name} needs a static size")
+            init = ""
+            if b.init_value is not None and False:
+                init = ""
+            self.w(f"{ct} {name}[{n}];")
+        else:
+            raise CodeGenError(f"cannot allocate {b.scope} buffer {b.name} inside a kernel")
+
+    # -- kernel ------------------------------------------------------------------------------
+    def generate(self, name: str) -> KernelSource:
+        ks = KernelSource()
+        ks.is_cpu = self.is_cpu
+        k = self.kernel
+        kname = self.name_of(k, name)
+        ks.kernel_name = kname
+        params = []
+        sig = []
+        # parameters: buffers and scalars of the PrimFunc, then dynamic shape symbols
+        flat = k.attrs.get("flat", {})
+        dyn_vars = []
+        seen = set()
+        for p in self.func.params:
+            if isinstance(p, Buffer):
+                for s in list(p.shape) + list(p.strides or []):
+                    if isinstance(s, PrimExpr):
+                        for v in free_vars(s):
+                            if id(v) not in seen and not any(v is q for q in self.func.params):
+                                seen.add(id(v))
+                                dyn_vars.append(v)
+        for p in self.func.params:
+            if isinstance(p, Buffer):
+                fb = flat.get(p)
+                target_buf = fb if fb is not None else p
+                pname = self.name_of(target_buf, p.name)
+                if fb is not None:
+                    self.names[id(p)] = pname
+                ct = self.ctype(p.dtype)
+                sig.append(f"{ct}* __restrict__ {pname}")
+                params.append(dict(kind="buffer", name=p.name, dtype=p.dtype.name, shape=list(p.shape),
+                                   strides=p.strides, buffer=p))
+            else:
+                sig.append(f"{self.ctype(p.dtype)} {self.name_of(p, p.name)}")
+                params.append(dict(kind="scalar", name=p.name, dtype=p.dtype.name, var=p))
+        for v in dyn_vars:
+            sig.append(f"{self.ctype(v.dtype)} {self.name_of(v, v.name)}")
+            params.append(dict(kind="dyn", name=v.name, dtype=v.dtype.name, var=v))
+        for extra in k.attrs.get("extra_params", []):
+            sig.append(extra["decl"])
+            params.append(extra)
+        ks.params = params
+        ks.dyn_vars = dyn_vars
+        ks.grid = list(k.grid)
+        ks.block = list(k.threads)
+        ks.lds_bytes = self.lds_total
+        self.ind = 1
+        body_lines_start = len(self.lines)
+        self.preamble(k)
+        self.s(k.body)
+        body = self.lines[body_lines_start:]
+        hdr = []
+        if self.is_cpu:
+            hdr.append('#include "tl/cpu.h"')
+        else:
+            hdr.append('#include "tl/tl.h"')
+        for src in self.func.attrs.get("import_source", []):
+            hdr.append(src)
+        if k.prelude:
+            hdr.append(k.prelude)
+        nthreads = k.num_threads
+        out = hdr + [""]
+        if self.is_cpu:
+            out.append(f'extern "C" void {kname}({", ".join(sig)}) {{')
+            # grid loops
+            depth = 0
+            for i, (v, g) in enumerate(zip(k.block_vars, k.grid)):
+                vn = self.name_of(v, v.name)
+                out.append("  " * (1 + depth) + f"for (int {vn} = 0; {vn} < {self.e(g)}; ++{vn}) {{")
+                depth += 1
+            out += ["  " * depth + ln for ln in body]
+            for _ in range(depth):
+                depth -= 1
+                out.append("  " * (1 + depth) + "}")
+            out.append("}")
+            # generic entry point
+            unpack = []
+            for i, p in enumerate(params):
+                decl = sig[i]
+                ty = decl.rsplit(" ", 1)[0].replace("__restrict__", "").strip()
+                unpack.append(f"*reinterpret_cast<{ty}*>(args[{i}])")
+            out.append(f'extern "C" void tl_entry(void** args) {{ {kname}({", ".join(unpack)}); }}')
+        else:
+            wpe = max(1, min(8, 2048 // max(nthreads, 64) // 4 if nthreads else 1))
+            lb = f"__launch_bounds__({nthreads})"
+            if self.pass_cfg.get("tl.min_waves_per_eu"):
+                lb = f"__launch_bounds__({nthreads}, {int(self.pass_cfg['tl.min_waves_per_eu'])})"
+            out.append(f'extern "C" __global__ void {lb} {kname}({", ".join(sig)}) {{')
+            if self.lds_total:
+                out.append(f"  __shared__ __attribute__((aligned(1024))) char tl_smem[{self.lds_total}];")
+            out += body
+            out.append("}")
+        ks.source = "\n".join(out) + "\n"
+        return ks
+
+    def preamble(self, k: S.KernelStmt):
+        tid = k.attrs.get("tid")
+        if self.is_cpu:
+            if tid is not None:
+                self.w(f"const int {self.e(tid)} = 0;")
+            for v in k.thread_vars:
+                self.w(f"const int {self.e(v)} = 0;")
+            if k.attrs.get("lane") is not None:
+                self.w(f"const int {self.e(k.attrs['lane'])} = 0;")
+            if k.attrs.get("wave") is not None:
+                self.w(f"const int {self.e(k.attrs['wave'])} = 0;")
+            return
+        dims = ["x", "y", "z"]
+        for v, d in zip(k.thread_vars, dims):
+            self.w(f"const int {self.e(v)} = threadIdx.{d};")
+        if tid is not None:
+            if len(k.threads) == 1:
+                self.w(f"const int {self.e(tid)} = threadIdx.x;")
+            else:
+                t = "threadIdx.x"
+                mul = k.threads[0]
+                for i in range(1, len(k.threads)):
+                    t += f" + threadIdx.{dims[i]} * {mul}"
+                    mul *= k.threads[i]
+                self.w(f"const int {self.e(tid)} = {t};")
+        if k.attrs.get("lane") is not None:
+            self.w(f"const int {self.e(k.attrs['lane'])} = {self.e(tid)} & 63;")
+        if k.attrs.get("wave") is not None:
+            self.w(f"const int {self.e(k.attrs['wave'])} = __builtin_amdgcn_readfirstlane({self.e(tid)} >> 6);")
+        sw = self.func.attrs.get("use_swizzle")
+        if sw and len(k.block_vars) >= 2:
+            panel = int(sw.get("panel_size", 8))
+            order = sw.get("order", "row")
+            bxn, byn = self.e(k.block_vars[0]), self.e(k.block_vars[1])
+            self.w("int tl_bid = blockIdx.x + blockIdx.y * gridDim.x;")
+            self.w("tl_bid = tl::xcd_remap(tl_bid, gridDim.x * gridDim.y);")
+            self.w(f"int {bxn}, {byn};")
+            fn = "rasterize_row" if order == "row" else "rasterize_col"
+            self.w(f"tl::{fn}<{panel}>(tl_bid, gridDim.x, gridDim.y, {bxn}, {byn});")
+            for v, d in list(zip(k.block_vars, dims))[2:]:
+                self.w(f"const int {self.e(v)} = blockIdx.{d};")
+        else:
+            for v, d in zip(k.block_vars, dims):
+                self.w(f"const int {self.e(v)} = blockIdx.{d};")
+        for b in self.func.params:
+            pass
+
+
+def generate(func, kernel, target, lds_offsets, lds_total, name, pass_cfg=None) -> KernelSource:
+    return CodeGen(func, kernel, target, lds_offsets, lds_total, pass_cfg).generate(name)

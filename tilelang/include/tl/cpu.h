@@ -1,0 +1,109 @@
+// tl/cpu.h — prelude for kernels compiled for the CPU plumbing target (host clang++).
+//
+// Counterpart of the reference's src/tl_templates/cpp/{common,gemm}.h (which vendors a 5.6k
+// line half.hpp); host clang provides _Float16 and __bf16 natively.
+#pragma once
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+#include <cmath>
+
+typedef _Float16 half_t;
+typedef __bf16 bfloat16_t;
+
+namespace tl {
+
+template <typename T> inline T max_(T a, T b) { return a > b ? a : b; }
+template <typename T> inline T min_(T a, T b) { return a < b ? a : b; }
+template <typename T> inline T floordiv(T a, T b) {
+  T q = a / b;
+  return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
+}
+template <typename T> inline T floormod(T a, T b) {
+  T r = a % b;
+  return (r != 0 && ((r < 0) != (b < 0))) ? r + b : r;
+}
+
+#define TL_CPU_UNARY(NAME, EXPR)                                         \
+  template <typename T> inline T NAME(T x) {                             \
+    float v = (float)x;                                                  \
+    return (T)(EXPR);                                                    \
+  }
+TL_CPU_UNARY(exp, std::exp(v))
+TL_CPU_UNARY(exp2, std::exp2(v))
+TL_CPU_UNARY(exp10, std::pow(10.0f, v))
+TL_CPU_UNARY(log, std::log(v))
+TL_CPU_UNARY(log2, std::log2(v))
+TL_CPU_UNARY(log10, std::log10(v))
+TL_CPU_UNARY(log1p, std::log1p(v))
+TL_CPU_UNARY(expm1, std::expm1(v))
+TL_CPU_UNARY(sqrt, std::sqrt(v))
+TL_CPU_UNARY(rsqrt, 1.0f / std::sqrt(v))
+TL_CPU_UNARY(rcp, 1.0f / v)
+TL_CPU_UNARY(sin, std::sin(v))
+TL_CPU_UNARY(cos, std::cos(v))
+TL_CPU_UNARY(tan, std::tan(v))
+TL_CPU_UNARY(asin, std::asin(v))
+TL_CPU_UNARY(acos, std::acos(v))
+TL_CPU_UNARY(atan, std::atan(v))
+TL_CPU_UNARY(sinh, std::sinh(v))
+TL_CPU_UNARY(cosh, std::cosh(v))
+TL_CPU_UNARY(tanh, std::tanh(v))
+TL_CPU_UNARY(erf, std::erf(v))
+TL_CPU_UNARY(floor, std::floor(v))
+TL_CPU_UNARY(ceil, std::ceil(v))
+TL_CPU_UNARY(trunc, std::trunc(v))
+TL_CPU_UNARY(round, std::round(v))
+TL_CPU_UNARY(nearbyint, std::nearbyint(v))
+TL_CPU_UNARY(sigmoid, 1.0f / (1.0f + std::exp(-v)))
+TL_CPU_UNARY(fast_exp, std::exp(v))
+TL_CPU_UNARY(fast_exp2, std::exp2(v))
+TL_CPU_UNARY(fast_log, std::log(v))
+TL_CPU_UNARY(fast_log2, std::log2(v))
+TL_CPU_UNARY(fast_sin, std::sin(v))
+TL_CPU_UNARY(fast_cos, std::cos(v))
+#undef TL_CPU_UNARY
+template <typename T> inline T abs(T x) { return x < (T)0 ? (T)(-x) : x; }
+template <typename T, typename U> inline T pow(T x, U y) { return (T)std::pow((float)x, (float)y); }
+template <typename T, typename U> inline T fmod(T x, U y) { return (T)std::fmod((float)x, (float)y); }
+template <typename T> inline T fma(T a, T b, T c) { return (T)std::fma((float)a, (float)b, (float)c); }
+template <typename T> inline bool isnan(T x) { return std::isnan((float)x); }
+template <typename T> inline bool isinf(T x) { return std::isinf((float)x); }
+
+template <typename T, int N> inline void store_vec(T* dst, const T (&vals)[N]) { memcpy(dst, vals, sizeof(T) * N); }
+template <typename T, int N> inline void load_vec(T (&vals)[N], const T* src) { memcpy(vals, src, sizeof(T) * N); }
+template <int B> inline void copy_bytes(void* dst, const void* src) { memcpy(dst, src, B); }
+
+inline void sync_threads() {}
+inline void barrier_raw() {}
+template <int N> inline void wait_vmcnt() {}
+
+struct SumOp {};
+struct MaxOp {};
+struct MinOp {};
+struct BitAndOp {};
+struct BitOrOp {};
+struct BitXorOp {};
+template <typename Op, int M, typename T> inline T lane_allreduce(T v) { return v; }
+template <typename T> inline T wave_reduce_sum(T v) { return v; }
+template <typename T> inline T wave_reduce_max(T v) { return v; }
+template <typename T> inline T wave_reduce_min(T v) { return v; }
+
+template <typename T, typename V> inline T atomic_add(T* p, V v) { T o = *p; *p = (T)((float)o + (float)v); return o; }
+template <typename T, typename V> inline T atomic_max(T* p, V v) { T o = *p; if ((T)v > o) *p = (T)v; return o; }
+template <typename T, typename V> inline T atomic_min(T* p, V v) { T o = *p; if ((T)v < o) *p = (T)v; return o; }
+
+// C[M,N] += op(A) * op(B); C is the thread-local fp32 accumulator (row-major M x N).
+template <typename T, int M, int N, int K, int TA, int TB, int A_COLS, int B_COLS>
+inline void cpu_gemm(const T* A, const T* B, float* C) {
+  for (int i = 0; i < M; ++i)
+    for (int k = 0; k < K; ++k) {
+      const float a = TA ? (float)A[k * A_COLS + i] : (float)A[i * A_COLS + k];
+      for (int j = 0; j < N; ++j) {
+        const float b = TB ? (float)B[j * B_COLS + k] : (float)B[k * B_COLS + j];
+        C[i * N + j] += a * b;
+      }
+    }
+}
+
+}  // namespace tl

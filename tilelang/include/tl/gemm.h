@@ -1,0 +1,169 @@
+// tl/gemm.h — CDNA4 MFMA tile GEMM micro-kernels (wave64).
+//
+// Counterpart of src/tl_templates/hip/gemm.h (CDNA3, 16x16x16 MFMA, kPack) and the
+// Python MFMA emitter tilelang/intrinsics/mfma_macro_generator.py.  gfx950 specifics:
+//   * v_mfma_f32_16x16x32_{f16,bf16}: 8 K-consecutive operands per lane (one ds_read_b128);
+//   * MN-contiguous operands ([K][N] B, [K][M] A^T) are read with ds_read_b64_tr_b16
+//     (hardware transpose) instead of scalar LDS gathers;
+//   * operands are SWAPPED at issue (mfma(B, A)) so every lane holds a row segment of C:
+//     C[m = lane&15][n = 4*(lane>>4) + v]  -> 8/16-byte vector epilogue stores and a
+//     register-resident accumulator that can feed the next GEMM as its A operand (KPERM=1);
+//   * LDS tiles are XOR-swizzled in 16-byte chunks: chunk' = chunk ^ gather(row bits),
+//     encoded in a 32-bit SWZ (nibble cb = 1 + row bit XORed into chunk bit cb, 0 = none).
+#pragma once
+
+namespace tl {
+
+template <uint32_t SWZ> TL_DEVICE int swz_term(int row) {
+  int t = 0;
+#pragma unroll
+  for (int cb = 0; cb < 8; ++cb) {
+    const int rb = (int)((SWZ >> (4 * cb)) & 15u);
+    if (rb) t |= ((row >> (rb - 1)) & 1) << cb;
+  }
+  return t;
+}
+
+// element offset of (row, col) inside a swizzled [*][COLS] tile of T
+template <typename T, int COLS, uint32_t SWZ> TL_DEVICE int swz_offset(int row, int col) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  if constexpr (SWZ == 0u) {
+    return row * COLS + col;
+  } else {
+    return row * COLS + (((col / EPC) ^ swz_term<SWZ>(row)) * EPC) + (col % EPC);
+  }
+}
+
+template <typename T> struct mfma_traits;
+
+template <> struct mfma_traits<half_t> {
+  typedef halfx8 frag;
+  TL_DEVICE static floatx4 mma16(frag a, frag b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct mfma_traits<bfloat16_t> {
+  typedef bf16x8 frag;
+  TL_DEVICE static floatx4 mma16(frag a, frag b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+
+// 8 consecutive elements of a row (K-contiguous operand): one ds_read_b128
+template <typename T, int COLS, uint32_t SWZ>
+TL_DEVICE typename mfma_traits<T>::frag ld_rows8(const T* base, int row, int col) {
+  return *reinterpret_cast<const typename mfma_traits<T>::frag*>(base + swz_offset<T, COLS, SWZ>(row, col));
+}
+
+// 2x4 K-consecutive elements at cols col0 and col0+16 (k-permuted K-contiguous operand)
+template <typename T, int COLS, uint32_t SWZ>
+TL_DEVICE typename mfma_traits<T>::frag ld_rows4x2(const T* base, int row, int col0) {
+  typedef typename mfma_traits<T>::frag F;
+  shortx4 lo = *reinterpret_cast<const shortx4*>(base + swz_offset<T, COLS, SWZ>(row, col0));
+  shortx4 hi = *reinterpret_cast<const shortx4*>(base + swz_offset<T, COLS, SWZ>(row, col0 + 16));
+  shortx8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(F, v);
+}
+
+// transposed read: lane (g=lane>>4, i=lane&15) receives column c0+i of rows r0+q (q=0..3)
+// where each lane supplies the address of row rows_of(q) and columns c0 + 4*(i&3).
+template <typename T, int COLS, uint32_t SWZ>
+TL_DEVICE shortx4 ld_tr4(const T* base, int row, int col) {
+  const T* p = base + swz_offset<T, COLS, SWZ>(row, col);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) shortx4*)((__attribute__((address_space(3))) char*)(p)));
+}
+
+// MN-contiguous operand fragment for MFMA column c (=lane&15) of tile column c0:
+// KPERM=0: rows k0 + 8g + {0..7};   KPERM=1: rows k0 + 4g + {0..3} and k0 + 16 + 4g + {0..3}
+template <typename T, int COLS, uint32_t SWZ, int KPERM>
+TL_DEVICE typename mfma_traits<T>::frag ld_tr8(const T* base, int k0, int c0, int lane) {
+  typedef typename mfma_traits<T>::frag F;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int r0 = KPERM ? (k0 + 4 * g + q) : (k0 + 8 * g + q);
+  const int r1 = KPERM ? (r0 + 16) : (r0 + 4);
+  shortx4 lo = ld_tr4<T, COLS, SWZ>(base, r0, c0 + 4 * p);
+  shortx4 hi = ld_tr4<T, COLS, SWZ>(base, r1, c0 + 4 * p);
+  shortx8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(F, v);
+}
+
+// Operand fragment of an [MN][K] (K-contiguous) or [K][MN] (MN-contiguous) LDS tile for the
+// 16-wide MFMA block starting at mn0 and K step k0.
+template <typename T, int ROWS, int COLS, uint32_t SWZ, bool MN_CONTIG, int KPERM>
+TL_DEVICE typename mfma_traits<T>::frag ld_operand(const T* base, int mn0, int k0, int lane) {
+  if constexpr (!MN_CONTIG) {
+    const int row = mn0 + (lane & 15);
+    if constexpr (KPERM == 0) {
+      return ld_rows8<T, COLS, SWZ>(base, row, k0 + 8 * (lane >> 4));
+    } else {
+      return ld_rows4x2<T, COLS, SWZ>(base, row, k0 + 4 * (lane >> 4));
+    }
+  } else {
+    return ld_tr8<T, COLS, SWZ, KPERM>(base, k0, mn0, lane);
+  }
+}
+
+// C[M x N] (+)= A * B for one block; each of the WARP_M*WARP_N waves owns a (M/WARP_M)x(N/WARP_N)
+// sub-tile held in registers as floatx4 [M_REP][N_REP] (local index (mi*N_REP+ni)*4+v).
+// A: LDS tile [M][K] (TA=false) or [K][M] (TA=true); B: [K][N] (TB=false) or [N][K] (TB=true).
+template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TA, bool TB, int A_COLS, uint32_t SWZ_A,
+          int B_COLS, uint32_t SWZ_B>
+TL_DEVICE void gemm_ss(const T* __restrict__ A, const T* __restrict__ B, float* __restrict__ C) {
+  typedef mfma_traits<T> MT;
+  typedef typename MT::frag F;
+  constexpr int WM = M / WARP_M, WN = N / WARP_N;
+  constexpr int M_REP = WM / 16, N_REP = WN / 16, KSTEPS = K / 32;
+  static_assert(WM % 16 == 0 && WN % 16 == 0 && K % 32 == 0, "MFMA 16x16x32 tiling");
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wm = wave / WARP_N, wn = wave % WARP_N;
+  floatx4* acc = reinterpret_cast<floatx4*>(C);
+#pragma unroll
+  for (int kk = 0; kk < KSTEPS; ++kk) {
+    F a[M_REP], b[N_REP];
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi)
+      a[mi] = ld_operand<T, (TA ? K : M), A_COLS, SWZ_A, TA, 0>(A, wm * WM + mi * 16, kk * 32, lane);
+#pragma unroll
+    for (int ni = 0; ni < N_REP; ++ni)
+      b[ni] = ld_operand<T, (TB ? N : K), B_COLS, SWZ_B, !TB, 0>(B, wn * WN + ni * 16, kk * 32, lane);
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < N_REP; ++ni)
+        acc[mi * N_REP + ni] = MT::mma16(b[ni], a[mi], acc[mi * N_REP + ni]);
+  }
+}
+
+// A operand in registers (gemm_rs): a_regs holds the A fragment, 8 elements per (mi, kk) at
+// a_regs + (mi*KSTEPS + kk)*8.  KPERM=1 when the fragment came from an accumulator layout.
+template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TB, int B_COLS, uint32_t SWZ_B, int KPERM>
+TL_DEVICE void gemm_rs(const T* __restrict__ a_regs, const T* __restrict__ B, float* __restrict__ C) {
+  typedef mfma_traits<T> MT;
+  typedef typename MT::frag F;
+  constexpr int WM = M / WARP_M, WN = N / WARP_N;
+  constexpr int M_REP = WM / 16, N_REP = WN / 16, KSTEPS = K / 32;
+  static_assert(WM % 16 == 0 && WN % 16 == 0 && K % 32 == 0, "MFMA 16x16x32 tiling");
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wn = wave % WARP_N;
+  floatx4* acc = reinterpret_cast<floatx4*>(C);
+#pragma unroll
+  for (int kk = 0; kk < KSTEPS; ++kk) {
+    F b[N_REP];
+#pragma unroll
+    for (int ni = 0; ni < N_REP; ++ni)
+      b[ni] = ld_operand<T, (TB ? N : K), B_COLS, SWZ_B, !TB, KPERM>(B, wn * WN + ni * 16, kk * 32, lane);
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi) {
+      F a;
+      __builtin_memcpy(&a, a_regs + (mi * KSTEPS + kk) * 8, sizeof(F));
+#pragma unroll
+      for (int ni = 0; ni < N_REP; ++ni)
+        acc[mi * N_REP + ni] = MT::mma16(b[ni], a, acc[mi * N_REP + ni]);
+    }
+  }
+}
+
+}  // namespace tl

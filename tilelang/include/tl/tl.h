@@ -1,0 +1,9 @@
+// tl/tl.h — umbrella header included by every generated gfx950 kernel.
+#pragma once
+#include "common.h"
+#include "copy.h"
+#include "gemm.h"
+#include "reduce.h"
+#include "atomic.h"
+#include "swizzle.h"
+#include "debug.h"

@@ -1,0 +1,188 @@
+"""``tilelang.jit`` / ``lazy_jit`` / ``compile`` / ``par_compile``.
+
+Reference: ``tilelang/jit/__init__.py:48-585``.  ``@tilelang.jit`` wraps a kernel
+*factory* (a Python function returning a ``T.prim_func``); calling the factory with
+compile-time parameters returns a cached ``JITKernel``.  ``@tilelang.lazy_jit``
+wraps a kernel *body* whose parameters are annotated tensors: calling it with
+tensors specialises, compiles (cached) and runs it.
+"""
+from __future__ import annotations
+
+import functools
+import inspect
+from concurrent.futures import ThreadPoolExecutor
+from typing import Any, Callable, Dict, List, Optional, Union
+
+from ..ir import stmt as S
+from .kernel import JITKernel
+
+
+def _freeze(x):
+    if isinstance(x, (list, tuple)):
+        return tuple(_freeze(i) for i in x)
+    if isinstance(x, dict):
+        return tuple(sorted((k, _freeze(v)) for k, v in x.items()))
+    try:
+        hash(x)
+        return x
+    except TypeError:
+        return repr(x)
+
+
+_GLOBAL_JIT_CACHE: Dict[Any, JITKernel] = {}
+
+
+def compile(func: S.PrimFunc = None, out_idx=None, execution_backend: str = "auto", target="auto",
+            target_host=None, verbose: bool = False, pass_configs: Optional[dict] = None,
+            compile_flags: Optional[List[str]] = None) -> JITKernel:  # noqa: A001
+    """Compile a PrimFunc into a callable kernel (memoised on the printed IR + options)."""
+    key = (func.script(), _freeze(out_idx), str(target), _freeze(pass_configs), _freeze(compile_flags))
+    k = _GLOBAL_JIT_CACHE.get(key)
+    if k is None:
+        k = JITKernel(func, out_idx=out_idx, target=target, target_host=target_host,
+                      execution_backend=execution_backend, verbose=verbose, pass_configs=pass_configs,
+                      compile_flags=compile_flags)
+        _GLOBAL_JIT_CACHE[key] = k
+    return k
+
+
+def par_compile(funcs: List[S.PrimFunc], out_idx=None, execution_backend="auto", target="auto",
+                target_host=None, verbose=False, pass_configs=None, compile_flags=None, num_workers=None,
+                ignore_error=False) -> List[Optional[JITKernel]]:
+    """Compile many PrimFuncs concurrently (hipcc runs as subprocesses, so threads scale)."""
+    import os
+    workers = num_workers or min(16, max(1, (os.cpu_count() or 4)))
+
+    def one(f):
+        try:
+            return compile(f, out_idx, execution_backend, target, target_host, verbose, pass_configs, compile_flags)
+        except Exception:
+            if ignore_error:
+                return None
+            raise
+
+    with ThreadPoolExecutor(workers) as ex:
+        return list(ex.map(one, funcs))
+
+
+class JITImpl:
+
+    def __init__(self, fn: Callable, out_idx=None, target="auto", target_host=None, execution_backend="auto",
+                 verbose=False, pass_configs=None, debug_root_path=None, compile_flags=None):
+        self.fn = fn
+        self.out_idx = out_idx
+        self.target = target
+        self.target_host = target_host
+        self.execution_backend = execution_backend
+        self.verbose = verbose
+        self.pass_configs = pass_configs
+        self.debug_root_path = debug_root_path
+        self.compile_flags = compile_flags
+        self._kernel_cache: Dict[Any, JITKernel] = {}
+        functools.update_wrapper(self, fn)
+
+    def get_tir(self, *args, **kwargs) -> S.PrimFunc:
+        f = self.fn(*args, **kwargs)
+        if not isinstance(f, S.PrimFunc):
+            raise TypeError(f"@tilelang.jit function {self.fn.__name__} must return a T.prim_func, got {type(f)}")
+        return f
+
+    def compile(self, *args, **kwargs) -> JITKernel:
+        func = self.get_tir(*args, **kwargs)
+        k = compile(func, self.out_idx, self.execution_backend, self.target, self.target_host, self.verbose,
+                    self.pass_configs, self.compile_flags)
+        if self.debug_root_path:
+            import os
+            d = os.path.join(self.debug_root_path, func.name)
+            k.export_sources(d)
+            with open(os.path.join(d, "tir.py"), "w") as f:
+                f.write(func.script())
+        return k
+
+    def par_compile(self, configs: List[Dict[str, Any]], num_workers=None, ignore_error=False):
+        funcs = []
+        for c in configs:
+            funcs.append(self.get_tir(**c))
+        return par_compile(funcs, self.out_idx, self.execution_backend, self.target, self.target_host,
+                           self.verbose, self.pass_configs, self.compile_flags, num_workers, ignore_error)
+
+    def __call__(self, *args, **kwargs) -> JITKernel:
+        key = (_freeze(args), _freeze(kwargs))
+        k = self._kernel_cache.get(key)
+        if k is None:
+            k = self.compile(*args, **kwargs)
+            self._kernel_cache[key] = k
+        return k
+
+
+def jit(func: Callable = None, *, out_idx=None, target="auto", target_host=None, execution_backend="auto",
+        verbose=False, pass_configs=None, debug_root_path=None, compile_flags=None):
+
+    def deco(fn):
+        return JITImpl(fn, out_idx, target, target_host, execution_backend, verbose, pass_configs, debug_root_path,
+                       compile_flags)
+
+    if func is not None and callable(func):
+        return deco(func)
+    return deco
+
+
+class LazyJITImpl:
+    """Kernel body with tensor annotations; specialised per call from the argument tensors."""
+
+    def __init__(self, fn, out_idx=None, target="auto", pass_configs=None, compile_flags=None, verbose=False):
+        self.fn = fn
+        self.out_idx = out_idx
+        self.target = target
+        self.pass_configs = pass_configs
+        self.compile_flags = compile_flags
+        self.verbose = verbose
+        self._cache = {}
+        functools.update_wrapper(self, fn)
+
+    def _spec(self, args):
+        key = []
+        for a in args:
+            if hasattr(a, "shape") and hasattr(a, "dtype"):
+                key.append(("T", tuple(a.shape), str(a.dtype)))
+            else:
+                key.append(("S", _freeze(a)))
+        return tuple(key)
+
+    def get_kernel(self, *args) -> JITKernel:
+        key = self._spec(args)
+        k = self._cache.get(key)
+        if k is None:
+            from ..language.parser import trace_prim_func
+            func = trace_prim_func(self.fn, _lazy_overrides(self.fn, args))
+            out_idx = self.out_idx
+            if out_idx is None:
+                out_idx = [i for i, p in enumerate(func.params) if getattr(p, "is_empty_output", False)] or None
+            k = compile(func, out_idx, "auto", self.target, None, self.verbose, self.pass_configs,
+                        self.compile_flags)
+            self._cache[key] = k
+        return k
+
+    def __call__(self, *args):
+        k = self.get_kernel(*args)
+        inputs = [a for i, a in enumerate(args) if i not in (k.out_idx or [])]
+        return k(*inputs)
+
+
+def _lazy_overrides(fn, args):
+    """Bind dynamic (``T.dyn``) dims of annotations to the concrete call-site values when static."""
+    return None
+
+
+def lazy_jit(func: Callable = None, *, out_idx=None, target="auto", pass_configs=None, compile_flags=None,
+             verbose=False):
+
+    def deco(fn):
+        return LazyJITImpl(fn, out_idx, target, pass_configs, compile_flags, verbose)
+
+    if func is not None and callable(func):
+        return deco(func)
+    return deco
+
+
+__all__ = ["jit", "lazy_jit", "compile", "par_compile", "JITKernel", "JITImpl"]

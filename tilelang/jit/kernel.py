@@ -1,0 +1,222 @@
+"""``JITKernel``: a compiled tilelang kernel callable on torch tensors.
+
+Reference: ``tilelang/jit/kernel.py:31-758`` (compile + adapter + profiler +
+source export) and the Cython adapter (``jit/adapter/cython``).  Execution goes
+through the native runtime ``tilelang._tl_runtime.Kernel`` (C++: argument
+validation, dynamic-shape binding, output allocation, ``hipModuleLaunchKernel`` on
+the current stream).
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+from pathlib import Path
+from typing import Any, List, Optional, Sequence, Union
+
+from ..engine.lower import lower, CompiledArtifact
+from ..ir import dtypes as _dt
+from ..ir import stmt as S
+from ..ir.buffer import Buffer
+from ..ir.expr import BinOp, IntImm, PrimExpr, Var, as_int
+from ..utils.target import Target, determine_target
+from ..contrib import hipcc
+from .. import cache as _cache
+
+_OP = {"+": 2, "-": 3, "*": 4, "//": 5, "/": 5, "%": 6, "min": 8, "max": 9}
+
+
+def _prog(e, symtab) -> List[int]:
+    if isinstance(e, int):
+        return [0, e]
+    if isinstance(e, IntImm):
+        return [0, e.value]
+    if isinstance(e, Var):
+        if e not in symtab:
+            raise ValueError(f"grid expression uses {e.name}, which is neither a tensor shape symbol nor an int "
+                             f"scalar parameter")
+        return [1, symtab[e]]
+    if isinstance(e, BinOp) and e.op in _OP:
+        return _prog(e.a, symtab) + _prog(e.b, symtab) + [_OP[e.op]]
+    from ..ir.expr import Cast
+    if isinstance(e, Cast):
+        return _prog(e.value, symtab)
+    raise ValueError(f"unsupported grid expression {e}")
+
+
+_SCALAR_TYPES = {}
+
+
+def _scalar_type_code(dtype) -> int:
+    import torch
+    from .. import _native
+    key = str(dtype)
+    if key not in _SCALAR_TYPES:
+        _SCALAR_TYPES[key] = _native.runtime().scalar_type_of(torch.empty(0, dtype=_dt.to_torch(dtype)))
+    return _SCALAR_TYPES[key]
+
+
+class JITKernel:
+
+    def __init__(self, func: S.PrimFunc = None, out_idx: Union[List[int], int, None] = None, target="auto",
+                 target_host=None, execution_backend: str = "native", verbose: bool = False,
+                 pass_configs: Optional[dict] = None, compile_flags: Optional[List[str]] = None,
+                 from_database: bool = False, artifact: Optional[CompiledArtifact] = None, code=None):
+        self.func = func
+        self.verbose = verbose
+        self.pass_configs = dict(pass_configs or {})
+        self.compile_flags = list(compile_flags or [])
+        self.execution_backend = execution_backend
+        self.target = determine_target(target)
+        self._rt = None
+        self._lock = threading.Lock()
+        self.config = None
+        self.latency = None
+        self.ref_latency = None
+        if artifact is None:
+            artifact = lower(func, self.target, pass_configs=self.pass_configs)
+        self.artifact = artifact
+        self.target = artifact.target
+        nparams = len(func.params)
+        if out_idx is None:
+            out_idx = []
+        elif isinstance(out_idx, int):
+            out_idx = [out_idx]
+        self.out_idx = sorted(i % nparams for i in out_idx)
+        for i in self.out_idx:
+            if not isinstance(func.params[i], Buffer):
+                raise ValueError(f"out_idx {i} refers to a scalar parameter")
+        self.code = code if code is not None else self._compile()
+
+    # -- compilation -------------------------------------------------------------------
+    def _compile(self):
+        a = self.artifact
+        if a.is_cpu:
+            return _cache.compile_cpu_cached(a.kernel_source, self.compile_flags, self.verbose)
+        return _cache.compile_hip_cached(a.kernel_source, self.compile_flags, self.verbose)
+
+    def _param_specs(self):
+        a = self.artifact
+        symtab = {}
+        for p in a.params:
+            if p["kind"] == "dyn":
+                symtab[p["var"]] = len(symtab)
+        for p in a.params:
+            if p["kind"] == "scalar" and p["var"].dtype.is_int:
+                symtab[p["var"]] = len(symtab)
+        specs = []
+        for i, p in enumerate(a.params):
+            d = dict(kind={"buffer": 0, "scalar": 1, "dyn": 2}.get(p["kind"], 1), name=p["name"], scalar_type=0,
+                     nbytes=8, is_float=False, shape=[], strides=[], is_output=False, sym=-1)
+            if p["kind"] == "buffer":
+                b: Buffer = p["buffer"]
+                d["scalar_type"] = _scalar_type_code(b.dtype)
+                d["is_output"] = (b.param_index in self.out_idx)
+                for s in b.shape:
+                    v = as_int(s)
+                    if v is not None:
+                        d["shape"].append((True, v))
+                    elif isinstance(s, Var) and s in symtab:
+                        d["shape"].append((False, symtab[s]))
+                    else:
+                        raise ValueError(f"unsupported dynamic shape expression {s} for {b.name}")
+                if b.strides is not None:
+                    for s in b.strides:
+                        v = as_int(s)
+                        d["strides"].append((True, v) if v is not None else (False, symtab[s]))
+            elif p["kind"] == "scalar":
+                v = p["var"]
+                d["nbytes"] = max(1, v.dtype.bits // 8)
+                d["is_float"] = v.dtype.is_float
+                d["sym"] = symtab.get(v, -1)
+            elif p["kind"] == "dyn":
+                v = p["var"]
+                d["nbytes"] = max(1, v.dtype.bits // 8)
+                d["sym"] = symtab[v]
+            else:  # extra (runtime-provided) params, e.g. mesh pointers
+                d["kind"] = 1
+                d["nbytes"] = p.get("nbytes", 8)
+                d["is_float"] = False
+            specs.append(d)
+        grid = [_prog(g, symtab) for g in a.grid]
+        return specs, len(symtab), grid
+
+    @property
+    def runtime(self):
+        if self._rt is None:
+            with self._lock:
+                if self._rt is None:
+                    from .. import _native
+                    rt = _native.runtime()
+                    specs, nsyms, grid = self._param_specs()
+                    a = self.artifact
+                    code = self.code.encode() if isinstance(self.code, str) else self.code
+                    self._rt = rt.Kernel(code, a.kernel_name, a.is_cpu, specs, nsyms, grid,
+                                         [int(b) for b in a.block], int(a.lds_bytes), a.kernel_name)
+        return self._rt
+
+    # -- execution -----------------------------------------------------------------------
+    def __call__(self, *args, **kwargs):
+        if kwargs:
+            names = [p.name for p in self.func.params]
+            full = list(args)
+            for n in names[len(args):]:
+                if n in kwargs:
+                    full.append(kwargs[n])
+            args = tuple(full)
+        return self.runtime(*args)
+
+    def set_validation(self, enabled: bool):
+        self.runtime.set_validate(enabled)
+
+    # -- introspection (reference API) -----------------------------------------------------
+    def get_kernel_source(self) -> str:
+        return self.artifact.kernel_source
+
+    def get_host_source(self) -> str:
+        a = self.artifact
+        lines = [f"// native launcher: hipModuleLaunchKernel({a.kernel_name}, grid={a.grid}, block={a.block}, "
+                 f"lds={a.lds_bytes}B)"]
+        for p in a.params:
+            lines.append(f"//   {p['kind']:6s} {p['name']} {p.get('dtype', '')}")
+        return "\n".join(lines)
+
+    def show_source(self, which: str = "kernel"):
+        print(self.get_kernel_source() if which == "kernel" else self.get_host_source())
+
+    def get_assembly(self) -> str:
+        if self.artifact.is_cpu:
+            return ""
+        return hipcc.compile_hip(self.artifact.kernel_source, options=self.compile_flags, asm=True).decode()
+
+    def export_sources(self, directory: str):
+        Path(directory).mkdir(parents=True, exist_ok=True)
+        (Path(directory) / "kernel.hip").write_text(self.get_kernel_source())
+        (Path(directory) / "host.txt").write_text(self.get_host_source())
+
+    def export_library(self, path: str):
+        if self.artifact.is_cpu:
+            import shutil
+            shutil.copy(self.code, path)
+        else:
+            Path(path).write_bytes(self.code)
+
+    def get_profiler(self, tensor_supply_type=None):
+        from ..profiler import Profiler
+        from ..utils.tensor import TensorSupplyType
+        return Profiler(self, tensor_supply_type or TensorSupplyType.Auto)
+
+    @property
+    def params(self):
+        return self.func.params
+
+    @property
+    def kernel_source(self):
+        return self.artifact.kernel_source
+
+    def update_tuner_result(self, latency, config, ref_latency=None):
+        self.latency, self.config, self.ref_latency = latency, config, ref_latency
+        return self
+
+    def __repr__(self):
+        return f"JITKernel({self.artifact.kernel_name}, target={self.target})"

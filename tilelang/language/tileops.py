@@ -1,0 +1,242 @@
+"""Tile operators: ``T.copy``, ``T.gemm``, ``T.fill``, ``T.reduce_*``, ``T.cumsum``, atomics.
+
+Reference frontends: ``tilelang/language/{copy,gemm,fill,reduce,atomic,customize}.py``.
+"""
+from __future__ import annotations
+
+from enum import IntEnum
+from typing import Optional
+
+from ..ir import stmt as S
+from ..ir import tileop as O
+from ..ir.buffer import Buffer, BufferRegion, to_region
+from ..ir.expr import BufferLoad, PrimExpr, convert, call, const, as_int, cast, IntImm
+from ..ir import dtypes as _dt
+from .builder import current_builder
+
+
+def _emit(op):
+    current_builder().emit(S.TileOpStmt(op))
+    return None
+
+
+def _extents_of(x):
+    if isinstance(x, Buffer):
+        return list(x.shape)
+    if isinstance(x, BufferRegion):
+        return list(x.extents)
+    return None
+
+
+def _pair_regions(src, dst):
+    """Resolve point loads against the other operand's extents (legalize_pairwise_extents)."""
+    se, de = _extents_of(src), _extents_of(dst)
+    if se is None and de is None:
+        # both points: a single-element copy
+        return to_region(src), to_region(dst)
+    s = to_region(src, de if se is None else None)
+    d = to_region(dst, se if de is None else None)
+    return s, d
+
+
+def copy(src, dst, coalesced_width: Optional[int] = None, disable_tma: bool = False,
+         eviction_policy: Optional[str] = None, loop_layout=None):
+    if isinstance(src, (int, float, PrimExpr)) and not isinstance(src, BufferLoad):
+        # T.copy(scalar, dst) == fill
+        return fill(dst, src)
+    s, d = _pair_regions(src, dst)
+    return _emit(O.CopyOp(s, d, coalesced_width, disable_tma, eviction_policy))
+
+
+def c2d_im2col(img, col, nhw_step, c_step, kernel, stride, dilation, pad, eviction_policy=None):
+    return _emit(O.Im2ColOp(to_region(img), to_region(col), convert(nhw_step), convert(c_step), kernel, stride,
+                            dilation, pad))
+
+
+class GemmWarpPolicy(IntEnum):
+    """Warp partition policy (reference ``tilelang/primitives/gemm/base.py:8-15``)."""
+    Square = 0
+    FullRow = 1
+    FullCol = 2
+
+    def compute_warp_partition(self, M: int, N: int, num_warps: int):
+        from ..transform.gemm_lower import compute_warp_partition
+        return compute_warp_partition(M, N, num_warps, int(self))
+
+
+def gemm(A, B, C, transpose_A: bool = False, transpose_B: bool = False, policy=GemmWarpPolicy.Square,
+         clear_accum=False, k_pack: int = 1, wg_wait: int = 0, mbar=None):
+    A, B, C = to_region(A), to_region(B), to_region(C)
+    return _emit(O.GemmOp(A, B, C, transpose_A, transpose_B, int(policy), clear_accum, k_pack, wg_wait))
+
+
+gemm_v1 = gemm
+gemm_v2 = gemm
+
+
+def gemm_scaled(A, B, C, scale_A, scale_B, transpose_A=False, transpose_B=True, policy=GemmWarpPolicy.Square,
+                clear_accum=False):
+    """Block-scaled MX GEMM (gfx950 ``v_mfma_scale_f32_*_f8f6f4``): A/B fp8, e8m0 scales per 32 K."""
+    op = O.GemmOp(to_region(A), to_region(B), to_region(C), transpose_A, transpose_B, int(policy), clear_accum, 1,
+                  0, to_region(scale_A), to_region(scale_B))
+    return _emit(op)
+
+
+def fill(buffer, value):
+    r = to_region(buffer)
+    return _emit(O.FillOp(r, convert(value)))
+
+
+def clear(buffer):
+    r = to_region(buffer)
+    return fill(r, const(0, r.dtype))
+
+
+def reduce(buffer, out, reduce_type: str, dim: int = -1, clear: bool = True):
+    src, dst = to_region(buffer), to_region(out)
+    nd = len(src.region)
+    if dim < 0:
+        dim += nd
+    if not (0 <= dim < nd):
+        raise ValueError(f"reduce dim {dim} out of range for a {nd}-d tile")
+    return _emit(O.ReduceOp(src, dst, reduce_type, dim, clear))
+
+
+def reduce_max(buffer, out, dim: int = -1, clear: bool = True):
+    return reduce(buffer, out, "max", dim, clear)
+
+
+def reduce_min(buffer, out, dim: int = -1, clear: bool = True):
+    return reduce(buffer, out, "min", dim, clear)
+
+
+def reduce_sum(buffer, out, dim: int = -1, clear: bool = True):
+    return reduce(buffer, out, "sum", dim, clear)
+
+
+def reduce_abssum(buffer, out, dim: int = -1, clear: bool = True):
+    return reduce(buffer, out, "abssum", dim, clear)
+
+
+def reduce_absmax(buffer, out, dim: int = -1, clear: bool = True):
+    return reduce(buffer, out, "absmax", dim, clear)
+
+
+def reduce_bitand(buffer, out, dim: int = -1, clear: bool = True):
+    return reduce(buffer, out, "bitand", dim, clear)
+
+
+def reduce_bitor(buffer, out, dim: int = -1, clear: bool = True):
+    return reduce(buffer, out, "bitor", dim, clear)
+
+
+def reduce_bitxor(buffer, out, dim: int = -1, clear: bool = True):
+    return reduce(buffer, out, "bitxor", dim, clear)
+
+
+def cumsum(src, dst=None, dim: int = 0, reverse: bool = False):
+    s = to_region(src)
+    d = to_region(dst) if dst is not None else s
+    nd = len(s.region)
+    if dim < 0:
+        dim += nd
+    return _emit(O.CumSumOp(s, d, dim, reverse))
+
+
+def finalize_reducer(reducer):
+    return _emit(O.FinalizeReducerOp(to_region(reducer)))
+
+
+# ---- warp (wave64) reductions on scalars ------------------------------------------------
+
+
+def _wave_reduce(kind, value):
+    value = convert(value)
+    return call(f"tl.wave_reduce_{kind}", [value], value.dtype)
+
+
+def warp_reduce_sum(value):
+    return _wave_reduce("sum", value)
+
+
+def warp_reduce_max(value):
+    return _wave_reduce("max", value)
+
+
+def warp_reduce_min(value):
+    return _wave_reduce("min", value)
+
+
+def warp_reduce_bitand(value):
+    return _wave_reduce("bitand", value)
+
+
+def warp_reduce_bitor(value):
+    return _wave_reduce("bitor", value)
+
+
+# ---- atomics ------------------------------------------------------------------------------
+
+
+def _atomic(op, dst, value, memory_order=None, return_prev=False):
+    if isinstance(dst, BufferLoad):
+        # scalar atomic on one element
+        e = call(f"tl.atomic_{op}", [dst, convert(value)], dst.dtype, memory_order=memory_order,
+                 return_prev=return_prev)
+        if return_prev:
+            return e
+        current_builder().emit(S.EvaluateStmt(e))
+        return None
+    d = to_region(dst)
+    if isinstance(value, (Buffer, BufferRegion, BufferLoad)):
+        src = to_region(value, d.extents)
+    else:
+        src = convert(value)
+    return _emit(O.AtomicOp(op, d, src, return_prev, memory_order))
+
+
+def atomic_add(dst, value, memory_order=None, return_prev=False, use_tma=False):
+    return _atomic("add", dst, value, memory_order, return_prev)
+
+
+def atomic_max(dst, value, memory_order=None, return_prev=False):
+    return _atomic("max", dst, value, memory_order, return_prev)
+
+
+def atomic_min(dst, value, memory_order=None, return_prev=False):
+    return _atomic("min", dst, value, memory_order, return_prev)
+
+
+def atomic_addx2(dst, value, return_prev=False):
+    return _atomic("add", dst, value, None, return_prev)
+
+
+def atomic_addx4(dst, value, return_prev=False):
+    return _atomic("add", dst, value, None, return_prev)
+
+
+def atomic_load(src, memory_order="seq_cst"):
+    return call("tl.atomic_load", [src], src.dtype, memory_order=memory_order)
+
+
+def atomic_store(dst, value, memory_order="seq_cst"):
+    current_builder().emit(S.EvaluateStmt(call("tl.atomic_store", [dst, convert(value)], dst.dtype,
+                                               memory_order=memory_order)))
+
+
+# ---- views --------------------------------------------------------------------------------
+
+
+def reshape(src: Buffer, shape):
+    """A view of ``src`` with a new row-major shape (same storage)."""
+    b = Buffer(src.name + "_view", list(shape), src.dtype, src.scope)
+    b.alias_of = (src, 0)
+    b._auto_name = False
+    return b
+
+
+def view(src: Buffer, shape=None, dtype=None):
+    shape = list(shape) if shape is not None else list(src.shape)
+    b = Buffer(src.name + "_view", shape, dtype or src.dtype, src.scope)
+    b.alias_of = (src, 0)
+    return b

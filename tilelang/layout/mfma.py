@@ -1,0 +1,235 @@
+"""CDNA4 (gfx950) MFMA fragment layouts and operand LDS swizzles.
+
+Reference counterparts (CDNA3 16x16x16 only): ``src/layout/gemm_layouts.cc:62-298``
+(``makeGemmFragmentCCDNA``, ``makeGemmFragmentACDNA``) and
+``tilelang/intrinsics/mfma_layout.py``.  gfx950 doubles K per instruction:
+
+* ``v_mfma_f32_16x16x32_{f16,bf16}`` — lane ``l`` holds ``A[l&15][8(l>>4)+j]`` and
+  ``B[8(l>>4)+j][l&15]`` (j<8); C/D: ``col = l&15, row = 4(l>>4)+v``.
+* ``v_mfma_f32_32x32x16_{f16,bf16}`` — lane holds ``A[l&31][8(l>>5)+j]``; C/D:
+  ``col = l&31, row = (v&3) + 8(v>>2) + 4(l>>5)``.
+
+The emitter issues ``mfma(B_frag, A_frag, acc)`` (operands swapped), so every
+lane holds a *row* segment of C: ``C[m = l&15][n = 4(l>>4)+v]``.  That makes the
+accumulator directly usable as the A operand of a following GEMM with the
+k-permutation ``k = 16h + 4(l>>4) + v`` (``kperm=1``), the B side of which is read
+with ``ds_read_b64_tr_b16`` from the same rows (guide §3 "An accumulator tile as
+the next MFMA's operand").  This is what keeps FlashAttention's P in registers.
+"""
+from __future__ import annotations
+
+import functools
+import itertools
+from typing import List, Optional, Sequence, Tuple
+
+from .fragment import Digit, Fragment
+from .layout import SwizzleLayout
+from ..analysis import lds_bank
+
+WAVE = 64
+
+
+def mfma_shape(dtype_bits: int, prefer_32: bool = False) -> Tuple[int, int, int]:
+    """(m, n, k) of the MFMA instruction used for an input element width."""
+    if dtype_bits == 16:
+        return (32, 32, 16) if prefer_32 else (16, 16, 32)
+    if dtype_bits == 8:
+        return (32, 32, 16) if prefer_32 else (16, 16, 32)
+    if dtype_bits == 32:
+        return (16, 16, 4)
+    raise ValueError(f"no MFMA for {dtype_bits}-bit inputs")
+
+
+def compute_warp_partition(M: int, N: int, num_warps: int, policy: int = 0, mtile: int = 16,
+                           ntile: int = 16) -> Tuple[int, int]:
+    """Split ``num_warps`` waves into ``warp_m x warp_n`` (reference gemm.cc:144-354).
+
+    policy: 0 = Square (balance per-wave tile), 1 = FullRow (waves along M), 2 = FullCol (along N).
+    """
+    cands = []
+    for wm in range(1, num_warps + 1):
+        if num_warps % wm:
+            continue
+        wn = num_warps // wm
+        if M % (wm * mtile) or N % (wn * ntile):
+            continue
+        cands.append((wm, wn))
+    if not cands:
+        raise ValueError(f"cannot partition a {M}x{N} GEMM tile over {num_warps} waves "
+                         f"(needs M%(warp_m*{mtile})==0 and N%(warp_n*{ntile})==0)")
+    if policy == 1:
+        return max(cands, key=lambda c: (c[0], -c[1]))
+    if policy == 2:
+        return max(cands, key=lambda c: (c[1], -c[0]))
+
+    def score(c):
+        wm, wn = c
+        tm, tn = M // wm, N // wn
+        # prefer square per-wave tiles, then more waves along M (A-operand reuse)
+        return (abs(tm - tn) / max(tm, tn), -wm)
+
+    return min(cands, key=score)
+
+
+def mfma_c_fragment(M: int, N: int, warp_m: int, warp_n: int, mn: Tuple[int, int] = (16, 16)) -> Fragment:
+    """Accumulator layout of a ``M x N`` tile computed by ``warp_m x warp_n`` waves (swapped operands)."""
+    WM, WN = M // warp_m, N // warp_n
+    if mn == (16, 16):
+        m_rep, n_rep = WM // 16, WN // 16
+        thread = [Digit(0, WM, warp_m), Digit(1, WN, warp_n), Digit(1, 4, 4), Digit(0, 1, 16)]
+        local = [Digit(0, 16, m_rep), Digit(1, 16, n_rep), Digit(1, 1, 4)]
+    elif mn == (32, 32):
+        m_rep, n_rep = WM // 32, WN // 32
+        thread = [Digit(0, WM, warp_m), Digit(1, WN, warp_n), Digit(1, 4, 2), Digit(0, 1, 32)]
+        local = [Digit(0, 32, m_rep), Digit(1, 32, n_rep), Digit(1, 8, 4), Digit(1, 1, 4)]
+    else:
+        raise ValueError(mn)
+    return Fragment([M, N], _drop_unit(thread), _drop_unit(local), f"mfma_c{mn[0]}")
+
+
+def mfma_a_fragment(M: int, K: int, warp_m: int, warp_n: int, kperm: int = 0, mn=(16, 16)) -> Fragment:
+    """A operand held in registers (gemm_rs).  Replicated over the ``warp_n`` waves.
+
+    kperm=0: natural  k = 32*kk + 8*g + j
+    kperm=1: C-layout compatible  k = 32*kk + 16*h + 4*g + v   (local order kk, h, v)
+    """
+    WM = M // warp_m
+    if mn != (16, 16):
+        raise NotImplementedError("register A operand is implemented for 16x16x32 MFMA")
+    m_rep = WM // 16
+    kk = K // 32
+    thread = [Digit(0, WM, warp_m), Digit(-1, 1, warp_n)]
+    if kperm == 0:
+        thread += [Digit(1, 8, 4), Digit(0, 1, 16)]
+        local = [Digit(0, 16, m_rep), Digit(1, 32, kk), Digit(1, 1, 8)]
+    else:
+        thread += [Digit(1, 4, 4), Digit(0, 1, 16)]
+        local = [Digit(0, 16, m_rep), Digit(1, 16, 2 * kk), Digit(1, 1, 4)]
+    return Fragment([M, K], _drop_unit(thread), _drop_unit(local), f"mfma_a_kperm{kperm}")
+
+
+def _drop_unit(digs: List[Digit]) -> List[Digit]:
+    return [d for d in digs if d.size > 1]
+
+
+# ---------------------------------------------------------------------------
+# LDS operand swizzles, searched against the gfx950 bank model
+# ---------------------------------------------------------------------------
+
+
+def _read_patterns(kind: str, rows: int, cols: int, elem_bytes: int, row_base_step: int = 16) -> List[List[tuple]]:
+    """Per-instruction lists of 64 (row, col) lane addresses for an operand read pattern.
+
+    kind:
+      'k_rows'  : K-contiguous operand, each lane reads 8 consecutive k (16 B for 16-bit data,
+                  8 B for 8-bit) of row (l&15) at k-chunk (l>>4)    -> ds_read_b128 / b64
+      'tr'      : MN-contiguous operand read with ds_read_b64_tr_b16 (natural k order)
+      'tr_kperm': same, C-layout compatible k order (16h + 4g + q)
+    """
+    pats = []
+    if kind == "k_rows":
+        k_per_lane = 8
+        kstep = 4 * k_per_lane
+        for r0 in range(0, min(rows, 64), row_base_step):
+            for k0 in range(0, cols, kstep):
+                pats.append([(r0 + (l & 15), k0 + (l >> 4) * k_per_lane) for l in range(64)])
+    elif kind in ("tr", "tr_kperm"):
+        # rows are k, cols are m/n; 16 columns per MFMA tile
+        for c0 in range(0, min(cols, 64), 16):
+            for k0 in range(0, rows, 32):
+                for h in range(2):
+                    p = []
+                    for l in range(64):
+                        g, i = l >> 4, l & 15
+                        q, pp = i >> 2, i & 3
+                        if kind == "tr":
+                            r = k0 + 8 * g + 4 * h + q
+                        else:
+                            r = k0 + 16 * h + 4 * g + q
+                        p.append((r, c0 + 4 * pp))
+                    pats.append(p)
+    else:
+        raise ValueError(kind)
+    return pats
+
+
+def _instr_for(kind: str, elem_bytes: int) -> str:
+    if kind == "k_rows":
+        return "ds_read_b128" if elem_bytes == 2 else "ds_read_b64"
+    return "ds_read_b64_tr_b16"
+
+
+def _candidates(cpr: int, max_row_bit: int = 6):
+    nbits = max(0, cpr.bit_length() - 1)
+    choices = [None] + list(range(max_row_bit))
+    for combo in itertools.product(choices, repeat=nbits):
+        bits = [(rb, cb) for cb, rb in enumerate(combo) if rb is not None]
+        yield bits
+
+
+def _batched_cycles(instr: str, addrs):
+    """Vectorised ``lds_bank.instruction_cycles``: addrs is int array [C, P, 64] (bytes)."""
+    import numpy as np
+    groups, width, mod = lds_bank.INSTRUCTIONS[instr]
+    C, P, _ = addrs.shape
+    total = np.zeros(C, dtype=np.int64)
+    nw = width // 4
+    for g in groups:
+        a = addrs[:, :, g] // 4                                   # [C, P, L]
+        dw = (a[..., None] + np.arange(nw)).reshape(C * P, -1)    # [C*P, L*nw]
+        dw = np.sort(dw, axis=1)
+        uniq = np.ones_like(dw, dtype=bool)
+        uniq[:, 1:] = dw[:, 1:] != dw[:, :-1]
+        banks = dw % mod
+        cnt = np.zeros((C * P, mod), dtype=np.int64)
+        rows_idx = np.repeat(np.arange(C * P), dw.shape[1]).reshape(dw.shape)
+        np.add.at(cnt, (rows_idx[uniq], banks[uniq]), 1)
+        total += np.maximum(cnt.max(axis=1), 1).reshape(C, P).sum(axis=1)
+    return total
+
+
+@functools.lru_cache(maxsize=None)
+def choose_swizzle(kind: str, rows: int, cols: int, elem_bytes: int) -> Tuple[Tuple[int, int], ...]:
+    """Pick the chunk-XOR swizzle with the fewest modelled LDS cycles for this read pattern
+    (exhaustive over row-bit -> chunk-bit assignments, scored with the gfx950 bank model)."""
+    import numpy as np
+    cpr = cols * elem_bytes // 16
+    if cpr <= 1:
+        return ()
+    pats = _read_patterns(kind, rows, cols, elem_bytes)
+    instr = _instr_for(kind, elem_bytes)
+    cands = [tuple(b) for b in _candidates(cpr, max_row_bit=min(6, max(1, rows.bit_length() - 1)))]
+    R = np.array([[r for r, c in p] for p in pats], dtype=np.int64)      # [P, 64]
+    Cc = np.array([[c for r, c in p] for p in pats], dtype=np.int64)
+    byte = Cc * elem_bytes
+    chunk = byte // 16
+    within = byte % 16
+    xs = np.zeros((len(cands), ) + R.shape, dtype=np.int64)
+    for i, bits in enumerate(cands):
+        for rb, cb in bits:
+            xs[i] |= ((R >> rb) & 1) << cb
+    addrs = R[None] * (cols * elem_bytes) + ((chunk[None] ^ xs) * 16) + within[None]
+    cost = _batched_cycles(instr, addrs)
+    best = min(range(len(cands)), key=lambda i: (int(cost[i]), len(cands[i])))
+    return cands[best]
+
+
+def swizzle_report(kind: str, rows: int, cols: int, elem_bytes: int, bits) -> dict:
+    pats = _read_patterns(kind, rows, cols, elem_bytes)
+    instr = _instr_for(kind, elem_bytes)
+    lay = SwizzleLayout([rows, cols], elem_bytes, list(bits))
+    base = SwizzleLayout([rows, cols], elem_bytes, [])
+    cyc = sum(lds_bank.instruction_cycles(instr, [lay.forward(r, c)[0] * elem_bytes for r, c in p]) for p in pats)
+    cyc0 = sum(lds_bank.instruction_cycles(instr, [base.forward(r, c)[0] * elem_bytes for r, c in p]) for p in pats)
+    ideal = len(pats) * len(lds_bank.INSTRUCTIONS[instr][0])
+    return {"instruction": instr, "cycles": cyc, "cycles_unswizzled": cyc0, "conflict_free": ideal}
+
+
+def operand_swizzle(kind: str, shape: Sequence[int], elem_bytes: int) -> SwizzleLayout:
+    rows, cols = int(shape[-2]), int(shape[-1])
+    bits = choose_swizzle(kind, rows, cols, elem_bytes)
+    return SwizzleLayout(list(shape), elem_bytes, list(bits), name=f"swz_{kind}")
+
+
+def default_operand_swizzle(shape, elem_bytes: int) -> SwizzleLayout:
+    return operand_swizzle("k_rows", shape, elem_bytes)

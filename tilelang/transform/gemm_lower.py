@@ -1,0 +1,97 @@
+"""``T.gemm`` planning and lowering for gfx950 MFMA.
+
+Reference: ``src/op/gemm.cc`` (instruction choice ``:129-141``, warp partition
+``:144-354``, CDNA ``tl::gemm_ss/rs`` template call ``:437-592``) and the Python
+``GemmMFMA`` lowering (``tilelang/tileop/gemm/gemm_mfma.py:62-233``).
+
+The plan fixes: MFMA shape (16x16x32 for f16/bf16), warp partition, the
+accumulator fragment (swapped-operand CDNA4 C layout), the LDS swizzle of each
+shared operand (searched against the gfx950 bank model for the exact read
+instruction: ``ds_read_b128`` for K-contiguous, ``ds_read_b64_tr_b16`` for
+MN-contiguous operands) and whether a register A operand uses the k-permuted
+order of an accumulator (``kperm``).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+from ..ir import tileop as O
+from ..ir.buffer import Buffer
+from ..ir.expr import as_int
+from ..layout import mfma as MF
+from ..layout.fragment import make_linear_fragment, Fragment
+from ..layout.layout import LinearLayout, SwizzleLayout
+
+compute_warp_partition = MF.compute_warp_partition
+
+
+def _trailing2(region):
+    ext = region.static_extents()
+    if ext is None:
+        raise ValueError("T.gemm operands need static tile shapes")
+    # drop leading unit dims (e.g. a pipeline stage index)
+    while len(ext) > 2 and ext[0] == 1:
+        ext = ext[1:]
+    if len(ext) != 2:
+        raise ValueError(f"T.gemm operand must be 2-D, got extents {region.static_extents()}")
+    return ext
+
+
+def encode_swizzle(layout) -> int:
+    if not isinstance(layout, SwizzleLayout):
+        return 0
+    v = 0
+    for rb, cb in layout.bits:
+        v |= (rb + 1) << (4 * cb)
+    return v
+
+
+def gemm_plan(op: O.GemmOp, num_threads: int, target=None, a_layout: Optional[Fragment] = None) -> Dict:
+    a_ext, b_ext, c_ext = _trailing2(op.A), _trailing2(op.B), _trailing2(op.C)
+    M, N = c_ext
+    K = a_ext[0] if op.trans_A else a_ext[1]
+    kb = b_ext[1] if op.trans_B else b_ext[0]
+    am = a_ext[1] if op.trans_A else a_ext[0]
+    bn = b_ext[0] if op.trans_B else b_ext[1]
+    if kb != K or am != M or bn != N:
+        raise ValueError(f"T.gemm shape mismatch: A{a_ext} B{b_ext} C{c_ext} "
+                         f"(transpose_A={op.trans_A}, transpose_B={op.trans_B})")
+    is_cpu = target is not None and getattr(target, "kind", "hip") == "cpu"
+    A, B, C = op.A.buffer, op.B.buffer, op.C.buffer
+    plan = dict(M=M, N=N, K=K, a_kperm=0)
+    if is_cpu:
+        plan.update(warp_m=1, warp_n=1, mfma=None, c_layout=make_linear_fragment([M, N], num_threads, 1, "cpu_c"),
+                    a_smem_layout=LinearLayout(A.static_shape() or a_ext),
+                    b_smem_layout=LinearLayout(B.static_shape() or b_ext))
+        return plan
+    eb = A.dtype.bits
+    if A.dtype != B.dtype:
+        raise ValueError(f"T.gemm needs matching A/B dtypes, got {A.dtype} and {B.dtype}")
+    if eb not in (16, 8):
+        raise ValueError(f"T.gemm on gfx950 supports 16-bit (f16/bf16) and 8-bit (fp8) inputs, got {A.dtype}")
+    if num_threads % 64:
+        raise ValueError(f"block size {num_threads} is not a multiple of the 64-lane wavefront")
+    nw = num_threads // 64
+    warp_m, warp_n = MF.compute_warp_partition(M, N, nw, op.policy)
+    plan.update(warp_m=warp_m, warp_n=warp_n, mfma=(16, 16, 32))
+    plan["c_layout"] = MF.mfma_c_fragment(M, N, warp_m, warp_n)
+    if K % 32:
+        raise ValueError(f"T.gemm K={K} must be a multiple of 32 on gfx950 (MFMA 16x16x32)")
+    if a_layout is not None and A.scope == "fragment":
+        k1 = MF.mfma_a_fragment(M, K, warp_m, warp_n, 1)
+        k1r = k1 if k1.num_threads == num_threads else k1.replicate(num_threads // k1.num_threads)
+        if a_layout.is_equal(k1r) or a_layout.is_equal(k1):
+            plan["a_kperm"] = 1
+    ebytes = A.dtype.bytes
+    if A.scope == "shared":
+        shp = A.static_shape()
+        kind = "tr" if op.trans_A else "k_rows"
+        plan["a_smem_layout"] = MF.operand_swizzle(kind, shp, ebytes) if ebytes == 2 else LinearLayout(shp)
+    if B.scope == "shared":
+        shp = B.static_shape()
+        if op.trans_B:
+            kind = "k_rows"
+        else:
+            kind = "tr_kperm" if plan["a_kperm"] == 1 else "tr"
+        plan["b_smem_layout"] = MF.operand_swizzle(kind, shp, ebytes) if ebytes == 2 else LinearLayout(shp)
+    return plan

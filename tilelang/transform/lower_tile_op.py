@@ -1,0 +1,1313 @@
+"""Lower tile operators and ``T.Parallel`` nests into per-thread (SIMT) code.
+
+Reference: ``src/transform/lower_tile_op.cc`` (calls each op's ``Lower``),
+``src/op/parallel.cc`` + ``loop_partition.cc`` + ``loop_vectorize.cc`` (partition
+a parallel nest over threads using the fragment layout and vectorise it),
+``src/op/copy.cc`` (SIMT copy), ``src/op/reduce.cc`` (thread-local reduce +
+``tl::AllReduce``), ``src/op/fill.cc``.
+
+After this pass:
+  * fragments are per-thread ``local`` arrays indexed by compile-time register numbers
+    (register index of logical element = Fragment.forward_index, proven uniform over
+    the block's threads by enumeration — so nothing is indexed at run time and the
+    arrays stay in VGPRs/AGPRs);
+  * every buffer access is flat (global: strides applied; shared: swizzled physical
+    offset inside the buffer's LDS slot);
+  * contiguous accesses are vectorised up to 16 B per lane.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+from ..ir import stmt as S
+from ..ir import tileop as O
+from ..ir import lowered as L
+from ..ir import dtypes as _dt
+from ..ir.buffer import Buffer, BufferRegion
+from ..ir.expr import (BufferLoad, Call, IntImm, PrimExpr, Var, as_int, binop, call, cast, compile_py, const,
+                       convert, divisible_by, evaluate, free_vars, logical_and, select, substitute, transform,
+                       post_order, loads_of, modular)
+from ..layout.fragment import Fragment, make_linear_fragment
+from ..layout.layout import Layout, LinearLayout, SwizzleLayout
+from .layout_inference import ParallelNest, collect_nests, lift_layout, _index_map
+from .pipeline import AsyncCopyOp, StagedCopyOp
+from .utils import Mutator, Substituter, bound, flatten_seq
+from . import gemm_lower
+
+
+class LoweringError(Exception):
+    pass
+
+
+_REDUCE_OPS = {
+    "sum": ("tl::SumOp", "+"),
+    "abssum": ("tl::SumOp", "+"),
+    "max": ("tl::MaxOp", "max"),
+    "absmax": ("tl::MaxOp", "max"),
+    "min": ("tl::MinOp", "min"),
+    "bitand": ("tl::BitAndOp", "&"),
+    "bitor": ("tl::BitOrOp", "|"),
+    "bitxor": ("tl::BitXorOp", "^"),
+}
+
+
+def _reduce_init(kind, dtype):
+    if kind in ("sum", "abssum", "bitor", "bitxor"):
+        return const(0, dtype)
+    if kind in ("max", "absmax"):
+        return const(-float("inf") if dtype.is_float else _dt.min_value(dtype), dtype) if kind == "max" \
+            else const(0, dtype)
+    if kind == "min":
+        return const(float("inf") if dtype.is_float else _dt.max_value(dtype), dtype)
+    if kind == "bitand":
+        return const(-1, dtype)
+    raise ValueError(kind)
+
+
+def _combine(kind, a, b):
+    if kind in ("sum", "abssum"):
+        return a + b
+    if kind in ("max", "absmax"):
+        return binop("max", a, b)
+    if kind == "min":
+        return binop("min", a, b)
+    if kind == "bitand":
+        return a & b
+    if kind == "bitor":
+        return a | b
+    if kind == "bitxor":
+        return a ^ b
+    raise ValueError(kind)
+
+
+def _prod(xs):
+    n = 1
+    for x in xs:
+        n *= x
+    return n
+
+
+class LowerCtx:
+
+    def __init__(self, kernel: S.KernelStmt, target, pass_cfg=None):
+        self.kernel = kernel
+        self.T = kernel.num_threads
+        self.target = target
+        self.is_cpu = kernel.is_cpu or getattr(target, "kind", "hip") == "cpu"
+        self.tid = Var("tid")
+        self.tid.nonneg = True
+        self.lane = Var("lane")
+        self.wave = Var("wave")
+        self.frag_local: Dict[Buffer, Buffer] = {}
+        self.flat: Dict[Buffer, Buffer] = {}
+        self.extra_allocs: List[Buffer] = []
+        self.staging: Dict[int, Buffer] = {}
+        self.pass_cfg = pass_cfg or {}
+        self.known_div: Dict[Var, tuple] = {}
+        self.ranges = {}
+        for v, g in zip(kernel.block_vars, kernel.grid):
+            gv = as_int(g)
+            if gv is not None:
+                self.ranges[v] = (0, gv - 1)
+        self.ranges[self.tid] = (0, self.T - 1)
+        self.uses_lane = False
+        self.uses_wave = False
+        self.ws_counter = 0
+
+    # -- buffers ---------------------------------------------------------------------
+    def flat_of(self, b: Buffer) -> Buffer:
+        if b.scope == "fragment":
+            return self.local_of(b)
+        fb = self.flat.get(b)
+        if fb is None:
+            if b.alias_of is not None:
+                base = self.flat_of(b.alias_of[0])
+                self.flat[b] = base
+                return base
+            size = None
+            if b.scope == "shared":
+                from ..layout.layout import physical_size
+                size = physical_size(b.layout, b.shape)
+            fb = Buffer(b.name, [size] if size is not None else [b.numel()], b.dtype, b.scope)
+            fb.orig = b
+            fb.param_index = b.param_index
+            fb._auto_name = False
+            self.flat[b] = fb
+        return fb
+
+    def local_of(self, b: Buffer) -> Buffer:
+        lb = self.frag_local.get(b)
+        if lb is None:
+            lay = b.layout
+            if not isinstance(lay, Fragment):
+                raise LoweringError(f"fragment {b.name} has no inferred layout")
+            lb = Buffer(b.name, [lay.local_size], b.dtype, "local")
+            lb.orig = b
+            lb._auto_name = False
+            self.frag_local[b] = lb
+        return lb
+
+    def flat_index(self, b: Buffer, indices) -> PrimExpr:
+        if b.scope == "shared":
+            lay = b.layout
+            if lay is None:
+                return b.offset_of(indices)
+            return convert(lay.offset(*indices))
+        if b.scope in ("local", "var"):
+            return b.offset_of(indices)
+        if b.scope == "global":
+            return b.offset_of(indices)
+        raise LoweringError(f"cannot flatten access to {b.scope} buffer {b.name}")
+
+    def lane_expr(self):
+        self.uses_lane = True
+        return self.lane
+
+    def wave_expr(self):
+        self.uses_wave = True
+        return self.wave
+
+    def new_local(self, name, n, dtype) -> Buffer:
+        b = Buffer(name, [n], dtype, "local")
+        b._auto_name = False
+        self.extra_allocs.append(b)
+        return b
+
+    def new_workspace(self, n, dtype) -> Buffer:
+        self.ws_counter += 1
+        b = Buffer(f"red_ws{self.ws_counter}", [n], dtype, "shared")
+        b.layout = LinearLayout([n])
+        b._auto_name = False
+        self.extra_allocs.append(b)
+        return b
+
+
+# ---------------------------------------------------------------------------
+# per-element fragment resolution
+# ---------------------------------------------------------------------------
+
+
+class _FragResolver:
+    """Resolves ``frag[idx(loop vars)]`` to a constant register index for iteration r of a
+    loop partitioned by ``loop_layout`` (checked for every thread of the block)."""
+
+    def __init__(self, ctx: LowerCtx, loop_vars: List[Var], loop_mins: List[PrimExpr], loop_layout: Fragment):
+        self.ctx = ctx
+        self.vars = loop_vars
+        self.mins = [as_int(m) or 0 for m in loop_mins]
+        self.layout = loop_layout
+        self.cache = {}
+        # loop-var values per (thread, r)
+        T = loop_layout.num_threads
+        self.T = T
+
+    def local_index(self, buf: Buffer, idx_exprs: List[PrimExpr], r: int) -> int:
+        key = (id(buf), tuple(id(e) for e in idx_exprs), r)
+        if key in self.cache:
+            return self.cache[key]
+        blay: Fragment = buf.layout
+        try:
+            fns = [compile_py(e, self.vars) for e in idx_exprs]
+        except Exception as ex:  # noqa: BLE001
+            raise LoweringError(f"fragment {buf.name} indexed by {idx_exprs}: indices must depend only on the "
+                                f"T.Parallel loop variables ({ex})") from None
+        result = None
+        tl_cache = getattr(blay, "_tlmap", None)
+        if tl_cache is None:
+            tl_cache = {}
+            blay._tlmap = tl_cache
+        for t in range(self.T):
+            vals = self.layout.inverse(t, r)
+            vals = [v + m for v, m in zip(vals, self.mins)]
+            bidx = tuple(int(f(*vals)) for f in fns)
+            m = tl_cache.get(t)
+            if m is None:
+                m = blay.thread_local_map(t)
+                tl_cache[t] = m
+            li = m.get(bidx)
+            if li is None:
+                raise LoweringError(
+                    f"layout conflict: thread {t} iterates element {bidx} of fragment {buf.name} it does not own "
+                    f"(loop layout {self.layout}, buffer layout {blay})")
+            if result is None:
+                result = li
+            elif result != li:
+                raise LoweringError(f"fragment {buf.name}: register index of element differs across threads "
+                                    f"(non-uniform access {idx_exprs})")
+        self.cache[key] = result
+        return result
+
+
+class _IterRewriter(Mutator):
+    """Rewrite one iteration (register r) of a fragment-partitioned nest."""
+
+    def __init__(self, ctx: LowerCtx, resolver: _FragResolver, r: int, vmap):
+        self.ctx = ctx
+        self.res = resolver
+        self.r = r
+        self.vmap = vmap
+        self.sub = Substituter(vmap)
+
+    def _load(self, n):
+        if isinstance(n, BufferLoad):
+            return self._access(n.buffer, n.indices)
+        return None
+
+    def _access(self, b: Buffer, idx):
+        if b.scope == "fragment":
+            li = self.res.local_index(b, idx, self.r)
+            return BufferLoad(self.ctx.local_of(b), [IntImm(li)])
+        idx2 = [substitute(i, self.vmap) for i in idx]
+        idx2 = [transform(i, self._load_sub) for i in idx2]
+        return BufferLoad(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx2)])
+
+    def _load_sub(self, n):
+        return None
+
+    def expr(self, e):
+        if not isinstance(e, PrimExpr):
+            return e
+
+        def fn(n):
+            if isinstance(n, BufferLoad):
+                return self._access(n.buffer, n.indices)
+            return None
+
+        # fragments must be resolved on the ORIGINAL (loop-var) indices, so transform first,
+        # then substitute the loop vars in what is left.
+        e2 = transform(e, fn)
+        return substitute(e2, self.vmap)
+
+    def store(self, s: S.StoreStmt):
+        val = self.expr(s.value)
+        b = s.buffer
+        if b.scope == "fragment":
+            li = self.res.local_index(b, s.indices, self.r)
+            return S.StoreStmt(self.ctx.local_of(b), [IntImm(li)], val)
+        idx = [self.expr(i) for i in s.indices]
+        return S.StoreStmt(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)], val)
+
+    def visit_LetStmt(self, s):
+        return S.LetStmt(s.var, self.expr(s.value))
+
+    def visit_ForStmt(self, s):
+        return S.ForStmt(s.var, self.expr(s.min), self.expr(s.extent), s.kind, self.stmt(s.body), s.annotations)
+
+
+# ---------------------------------------------------------------------------
+# vectorisation of a group of per-element statements
+# ---------------------------------------------------------------------------
+
+
+def _const_diff(a: PrimExpr, b: PrimExpr, probe_vars: List[Var]) -> Optional[int]:
+    """a - b if it is the same constant for sampled values of probe_vars (else None)."""
+    d = binop("-", a, b)
+    v = as_int(d)
+    if v is not None:
+        return v
+    try:
+        fv = free_vars(d)
+        f = compile_py(d, fv)
+    except Exception:  # noqa: BLE001
+        return None
+    import random
+    rnd = random.Random(7)
+    vals = None
+    for _ in range(6):
+        args = [rnd.randrange(0, 4096) for _ in fv]
+        try:
+            x = f(*args)
+        except Exception:  # noqa: BLE001
+            return None
+        if vals is None:
+            vals = x
+        elif x != vals:
+            return None
+    return int(vals) if vals is not None else None
+
+
+def vectorize_group(ctx: LowerCtx, stmts: List[S.Stmt], known_div) -> Optional[List[S.Stmt]]:
+    """``stmts[i]`` are the per-element copies (i = 0..W-1) of a single-store body.  If the
+    stores (and the loads feeding them) are contiguous and aligned, emit vector accesses."""
+    W = len(stmts)
+    if W == 1 or not all(isinstance(s, S.StoreStmt) for s in stmts):
+        return None
+    b = stmts[0].buffer
+    if any(s.buffer is not b for s in stmts):
+        return None
+    eb = b.dtype.bytes
+    if W * eb > 16 or (W * eb) not in (2, 4, 8, 16):
+        return None
+    base = stmts[0].indices[0]
+    probe = []
+    for i, s in enumerate(stmts):
+        d = _const_diff(s.indices[0], base, probe)
+        if d != i:
+            return None
+    if b.scope != "local" and not divisible_by(base, W, known_div):
+        return None
+    # vectorise the loads feeding the stores: the i-th load (in post-order) of every group
+    # member is the same access shifted by i elements when the body is contiguous
+    vals = [s.value for s in stmts]
+    pre = []
+    po = [[n for n in post_order(v) if isinstance(n, BufferLoad)] for v in vals]
+    if all(len(p) == len(po[0]) for p in po):
+        if len(po[0]) == 1 and vals[0] is po[0][0] and po[0][0].buffer.dtype == b.dtype and \
+                po[0][0].buffer.scope in ("global", "shared") and b.scope != "local":
+            ld0 = po[0][0]
+            if all(_const_diff(po[i][0].indices[0], ld0.indices[0], []) == i for i in range(W)) and \
+                    divisible_by(ld0.indices[0], W, known_div):
+                return [L.CopyBytesStmt(b, base, ld0.buffer, ld0.indices[0], W * eb)]
+        repl = [dict() for _ in range(W)]
+        for j, ld0 in enumerate(po[0]):
+            if ld0.buffer.scope not in ("global", "shared"):
+                continue
+            leb = ld0.buffer.dtype.bytes
+            if W * leb not in (2, 4, 8, 16):
+                continue
+            if not all(po[i][j].buffer is ld0.buffer and
+                       _const_diff(po[i][j].indices[0], ld0.indices[0], []) == i for i in range(W)):
+                continue
+            if not divisible_by(ld0.indices[0], W, known_div):
+                continue
+            tmp = ctx.new_local(f"vtmp{len(ctx.extra_allocs)}", W, ld0.buffer.dtype)
+            pre.append(L.VecLoadStmt(tmp, 0, ld0.buffer, ld0.indices[0], W))
+            for i in range(W):
+                repl[i][id(po[i][j])] = BufferLoad(tmp, [IntImm(i)])
+        if pre:
+            vals = [transform(v, lambda n, r=repl[i]: r.get(id(n))) for i, v in enumerate(vals)]
+    if b.scope == "local":
+        # stores into a register array need no vector op
+        return pre + [S.StoreStmt(b, [s.indices[0]], v) for s, v in zip(stmts, vals)] if pre else None
+    return pre + [L.VecStoreStmt(b, base, vals)]
+
+
+def _is_cast_of(v, ld):
+    from ..ir.expr import Cast
+    return isinstance(v, Cast) and v.value is ld
+
+
+# ---------------------------------------------------------------------------
+# the pass
+# ---------------------------------------------------------------------------
+
+
+class TileOpLowerer(Mutator):
+
+    def __init__(self, ctx: LowerCtx):
+        self.ctx = ctx
+        self.known_div = {}
+
+    # -- helpers -------------------------------------------------------------------
+    def flat_access_expr(self, e):
+        """Flatten non-fragment buffer loads inside a scalar expression (outside nests)."""
+        ctx = self.ctx
+
+        def fn(n):
+            if isinstance(n, BufferLoad):
+                b = n.buffer
+                if b.scope == "fragment":
+                    lay = b.layout
+                    if isinstance(lay, Fragment) and lay.local_size == _prod(b.static_shape() or [0]) and \
+                            lay.replicate_size == lay.num_threads:
+                        return BufferLoad(ctx.local_of(b), [b.offset_of(n.indices)])
+                    raise LoweringError(f"fragment {b.name} accessed outside T.Parallel; use a T.Parallel loop or "
+                                        f"T.alloc_local for per-thread arrays")
+                if b.scope in ("local", "var") and b.alias_of is None:
+                    return BufferLoad(b, [b.offset_of(n.indices)] if b.ndim != 1 else n.indices)
+                return BufferLoad(ctx.flat_of(b), [ctx.flat_index(b, n.indices)])
+            return None
+
+        return transform(e, fn)
+
+    def expr(self, e):
+        if isinstance(e, PrimExpr):
+            return self.flat_access_expr(e)
+        return e
+
+    def store(self, s):
+        b = s.buffer
+        val = self.expr(s.value)
+        idx = [self.expr(i) for i in s.indices]
+        if b.scope == "fragment":
+            lay = b.layout
+            if isinstance(lay, Fragment) and lay.replicate_size == lay.num_threads:
+                return S.StoreStmt(self.ctx.local_of(b), [b.offset_of(idx)], val)
+            raise LoweringError(f"store to fragment {b.name} outside T.Parallel")
+        if b.scope in ("local", "var"):
+            return S.StoreStmt(b, [b.offset_of(idx)] if b.ndim != 1 else idx, val)
+        return S.StoreStmt(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)], val)
+
+    def visit_AllocStmt(self, s):
+        b = s.buffer
+        if b.scope == "fragment":
+            return S.AllocStmt(self.ctx.local_of(b))
+        if b.scope == "shared":
+            return S.AllocStmt(self.ctx.flat_of(b))
+        return s
+
+    def visit_ForStmt(self, s: S.ForStmt):
+        if s.kind == "parallel":
+            return self.lower_nest(s)
+        mn, ext = as_int(s.min), as_int(s.extent)
+        if mn is not None and ext is not None and ext > 0:
+            self.ctx.ranges[s.var] = (mn, mn + ext - 1)
+        body = self.stmt(s.body)
+        kind = s.kind if s.kind in ("serial", "unroll") else "serial"
+        return S.ForStmt(s.var, self.expr(s.min), self.expr(s.extent), kind, body, s.annotations)
+
+    def visit_TileOpStmt(self, s):
+        op = s.op
+        fn = getattr(self, "lower_" + type(op).__name__, None)
+        if fn is None:
+            raise LoweringError(f"no lowering for tile op {type(op).__name__}")
+        return fn(op)
+
+    # -- parallel nests ----------------------------------------------------------------
+    def lower_nest(self, outer: S.ForStmt, layout: Optional[Fragment] = None):
+        nest = ParallelNest(_nest_loops(outer))
+        if self.ctx.is_cpu:
+            return self.lower_cpu_nest(nest)
+        layout = layout or outer.annotations.get("_layout")
+        if layout is not None:
+            return self.lower_frag_nest(nest, layout)
+        if nest.fragment_accesses():
+            raise LoweringError("T.Parallel over fragments without an inferred layout")
+        return self.lower_simt_nest(nest)
+
+    def lower_cpu_nest(self, nest: ParallelNest) -> S.Stmt:
+        """CPU target: one thread owns every fragment element (row-major local arrays), so a
+        parallel nest is a plain loop nest."""
+        ctx = self.ctx
+
+        class _Cpu(_SimtRewriter):
+
+            def _acc(self, n):
+                if isinstance(n, BufferLoad) and n.buffer.scope == "fragment":
+                    return BufferLoad(ctx.local_of(n.buffer), [n.buffer.offset_of(n.indices)])
+                return _SimtRewriter._acc(self, n)
+
+            def store(self, s):
+                if s.buffer.scope == "fragment":
+                    return S.StoreStmt(ctx.local_of(s.buffer), [s.buffer.offset_of([self.expr(i) for i in s.indices])],
+                                       self.expr(s.value))
+                return _SimtRewriter.store(self, s)
+
+        body = _Cpu(ctx, {}).stmt(nest.body)
+        for l in reversed(nest.loops):
+            body = S.ForStmt(l.var, l.min, l.extent, "serial", body)
+        return body
+
+    def lower_frag_nest(self, nest: ParallelNest, layout: Fragment) -> S.Stmt:
+        ctx = self.ctx
+        res = _FragResolver(ctx, nest.vars, nest.mins, layout)
+        W = layout.inner_vector_width(len(nest.vars) - 1)
+        out = []
+        body_is_single_store = isinstance(nest.body, S.StoreStmt)
+        for r0 in range(0, layout.local_size, W):
+            group = []
+            for r in range(r0, r0 + W):
+                idx = layout.inverse(ctx.tid, r)
+                vmap = {v: binop("+", m, i) for v, m, i in zip(nest.vars, nest.mins, idx)}
+                rw = _IterRewriter(ctx, res, r, vmap)
+                group.append(rw.stmt(nest.body))
+            if body_is_single_store and W > 1:
+                vec = vectorize_group(ctx, group, self.known_div)
+                if vec is not None:
+                    out.extend(vec)
+                    continue
+            if not body_is_single_store:
+                # scope each iteration (let bindings are per-iteration)
+                out.extend(_scoped(g) for g in group)
+            else:
+                out.extend(group)
+        return S.SeqStmt(out)
+
+    def lower_simt_nest(self, nest: ParallelNest) -> S.Stmt:
+        """Partition a nest over plain (global/shared/local) buffers across the block's threads."""
+        ctx = self.ctx
+        exts = nest.extents
+        if any(e is None for e in exts):
+            return self.lower_dynamic_nest(nest)
+        total = _prod(exts)
+        T = ctx.T
+        inner_var = nest.vars[-1]
+        # vector width: contiguous along the innermost loop var for every access
+        vec = 1
+        cw = nest.outer.annotations.get("coalesced_width")
+        accs = nest.accesses()
+        max_eb = max([b.dtype.bytes for b, _, _ in accs] or [4])
+        cand = cw if cw else max(1, 16 // max_eb)
+        while cand > 1:
+            if exts[-1] % cand == 0 and total // cand >= 1 and self._vec_ok(nest, cand):
+                vec = cand
+                break
+            cand //= 2
+        slots = total // vec
+        steps = -(-slots // T)
+        out = []
+        single_store = isinstance(nest.body, S.StoreStmt)
+        for o in range(steps):
+            slot = binop("+", binop("*", o, T), ctx.tid) if steps > 1 else ctx.tid
+            guard = None
+            if (o + 1) * T > slots:
+                guard = binop("<", slot, slots)
+            group = []
+            for v in range(vec):
+                lin = binop("+", binop("*", slot, vec), v) if vec > 1 else slot
+                vals = _unflatten(lin, exts)
+                vmap = {var: binop("+", m, x) for var, m, x in zip(nest.vars, nest.mins, vals)}
+                rw = _SimtRewriter(ctx, vmap)
+                group.append(rw.stmt(nest.body))
+            stmts = None
+            if single_store and vec > 1:
+                kd = dict(self.known_div)
+                kd[ctx.tid] = (1, 0)
+                stmts = vectorize_group(ctx, group, _slot_div(kd, ctx.tid, o, T, vec))
+            if stmts is None:
+                stmts = [_scoped(g) for g in group] if not single_store else group
+            blk = S.SeqStmt(stmts)
+            out.append(S.IfStmt(guard, blk) if guard is not None else blk)
+        return S.SeqStmt(out)
+
+    def lower_dynamic_nest(self, nest: ParallelNest) -> S.Stmt:
+        ctx = self.ctx
+        total = const(1)
+        for l in nest.loops:
+            total = total * l.extent
+        it = Var("it")
+        lin = binop("+", binop("*", it, ctx.T), ctx.tid)
+        vals = _unflatten_dyn(lin, [l.extent for l in nest.loops])
+        vmap = {var: binop("+", m, x) for var, m, x in zip(nest.vars, nest.mins, vals)}
+        body = _SimtRewriter(ctx, vmap).stmt(nest.body)
+        from ..ir.expr import ceildiv
+        n_it = ceildiv(total, ctx.T)
+        return S.ForStmt(it, 0, n_it, "serial", S.IfStmt(binop("<", lin, total), body))
+
+    def _vec_ok(self, nest: ParallelNest, vec: int) -> bool:
+        v = nest.vars[-1]
+        for b, idx, _ in nest.accesses():
+            if b.scope == "fragment":
+                return False
+            if not idx:
+                continue
+            # innermost buffer index must be v (+ something not involving v); other dims free of v
+            for d, e in enumerate(idx):
+                uses = any(n is v for n in post_order(e))
+                if d < len(idx) - 1 and uses:
+                    return False
+            last = idx[-1]
+            if any(n is v for n in post_order(last)):
+                rest = substitute(last, {v: IntImm(0)})
+                if _const_diff(last, rest, []) is None:
+                    # coefficient of v must be exactly 1
+                    d1 = _const_diff(substitute(last, {v: IntImm(1)}), rest, [])
+                    if d1 != 1:
+                        return False
+                d1 = _const_diff(substitute(last, {v: IntImm(1)}), rest, [])
+                if d1 != 1:
+                    return False
+                if b.scope == "global":
+                    st = b.get_strides()
+                    if as_int(st[-1]) != 1:
+                        return False
+                    for s_ in st[:-1]:
+                        if not divisible_by(convert(s_), vec):
+                            return False
+                    if not divisible_by(rest, vec, self.known_div):
+                        return False
+                if b.scope == "shared" and b.layout is not None and isinstance(b.layout, SwizzleLayout):
+                    if (vec * b.dtype.bytes) > 16 or (b.layout.epc % vec and vec % b.layout.epc):
+                        return False
+        return True
+
+    # -- tile ops ---------------------------------------------------------------------
+    def lower_FillOp(self, op: O.FillOp):
+        b = op.dst.buffer
+        val = self.expr(op.value)
+        if b.scope == "fragment":
+            lb = self.ctx.local_of(b)
+            if not _full(op.dst):
+                raise LoweringError("T.fill on a fragment must cover the whole fragment")
+            v = cast(val, b.dtype)
+            if ctx_is_cpu(self.ctx):
+                i = Var("fi")
+                return S.ForStmt(i, 0, lb.shape[0], "serial", S.StoreStmt(lb, [i], v))
+            return S.SeqStmt([S.StoreStmt(lb, [IntImm(i)], v) for i in range(lb.shape[0])])
+        if b.scope in ("local", "var"):
+            n = as_int(b.numel())
+            return S.SeqStmt([S.StoreStmt(b, [IntImm(i)], cast(val, b.dtype)) for i in range(n)])
+        nest = _region_nest(op.dst, lambda idx: (op.dst.buffer, idx, cast(val, b.dtype)))
+        return self.lower_nest(nest)
+
+    def lower_CopyOp(self, op: O.CopyOp):
+        src, dst = op.src, op.dst
+        sf, df = src.buffer.scope == "fragment", dst.buffer.scope == "fragment"
+        if sf or df:
+            return self.lower_frag_copy(op)
+        if src.buffer.scope == "local" and dst.buffer.scope == "local":
+            pass
+        nest = _copy_nest(src, dst, op.coalesced_width)
+        return self.lower_nest(nest)
+
+    def lower_frag_copy(self, op: O.CopyOp):
+        src, dst = op.src, op.dst
+        frag_side = dst if dst.buffer.scope == "fragment" else src
+        fb = frag_side.buffer
+        if not _full(frag_side):
+            raise LoweringError(f"T.copy to/from fragment {fb.name} must cover the whole fragment")
+        nest = _copy_nest(src, dst, None)
+        loops = _nest_loops(nest)
+        fshape = fb.static_shape()
+        # loop dims correspond to the squeezed extents; map fragment dims onto loop vars
+        lay = fb.layout
+        squeezed_lay = _squeeze_fragment(lay, fshape)
+        loop_lay = squeezed_lay
+        if [as_int(l.extent) for l in loops] != squeezed_lay.shape:
+            raise LoweringError(f"T.copy shape mismatch for fragment {fb.name}")
+        return self.lower_nest(nest, loop_lay)
+
+    def lower_GemmOp(self, op: O.GemmOp):
+        ctx = self.ctx
+        plan = getattr(op, "plan", None)
+        if plan is None:
+            plan = gemm_lower.gemm_plan(op, ctx.T, ctx.target,
+                                        op.A.buffer.layout if op.A.buffer.scope == "fragment" else None)
+        A, B, C = op.A.buffer, op.B.buffer, op.C.buffer
+        if C.scope != "fragment":
+            raise LoweringError("T.gemm accumulator must be a fragment (T.alloc_fragment)")
+        out = []
+        cl = ctx.local_of(C)
+        if op.clear_accum is not False and op.clear_accum is not None:
+            zero = S.SeqStmt([S.StoreStmt(cl, [IntImm(i)], const(0.0, C.dtype)) for i in range(cl.shape[0])])
+            ca = op.clear_accum
+            if isinstance(ca, bool) or as_int(ca) is not None:
+                if bool(as_int(ca) if not isinstance(ca, bool) else ca):
+                    out.append(zero)
+            else:
+                out.append(S.IfStmt(self.expr(ca), zero))
+        ctype = _dt.hip_type(A.dtype)
+        if ctx.is_cpu:
+            pa = self._operand_ptr(op.A)
+            pb = self._operand_ptr(op.B)
+            a_cols = (A.static_shape() or [0])[-1]
+            b_cols = (B.static_shape() or [0])[-1]
+            out.append(L.CallStmt("tl::cpu_gemm", [pa, pb, L.BufferPtr(cl, 0)],
+                                  [_dt.cpu_type(A.dtype), plan["M"], plan["N"], plan["K"], int(op.trans_A),
+                                   int(op.trans_B), a_cols, b_cols]))
+            return S.SeqStmt(out)
+        if B.scope != "shared":
+            raise LoweringError("T.gemm: B operand must be in shared memory on gfx950")
+        pb = self._operand_ptr(op.B)
+        b_cols = B.static_shape()[-1]
+        swz_b = gemm_lower.encode_swizzle(B.layout)
+        if A.scope == "shared":
+            pa = self._operand_ptr(op.A)
+            a_cols = A.static_shape()[-1]
+            swz_a = gemm_lower.encode_swizzle(A.layout)
+            out.append(L.CallStmt("tl::gemm_ss", [pa, pb, L.BufferPtr(cl, 0)], [
+                ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_A),
+                _b(op.trans_B), a_cols, f"{swz_a}u", b_cols, f"{swz_b}u"
+            ]))
+        elif A.scope == "fragment":
+            al = ctx.local_of(A)
+            if op.trans_A:
+                raise LoweringError("register A operand cannot be transposed")
+            out.append(L.CallStmt("tl::gemm_rs", [L.BufferPtr(al, 0), pb, L.BufferPtr(cl, 0)], [
+                ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_B), b_cols,
+                f"{swz_b}u", plan.get("a_kperm", 0)
+            ]))
+        else:
+            raise LoweringError(f"T.gemm: A operand scope {A.scope} unsupported")
+        return S.SeqStmt(out)
+
+    def _operand_ptr(self, r: BufferRegion):
+        b = r.buffer
+        mins = [self.expr(m) for m in r.mins]
+        if b.scope == "fragment":
+            return L.BufferPtr(self.ctx.local_of(b), 0)
+        off = self.ctx.flat_index(b, mins)
+        return L.BufferPtr(self.ctx.flat_of(b), off)
+
+    def lower_ReduceOp(self, op: O.ReduceOp):
+        ctx = self.ctx
+        sb, db = op.src.buffer, op.dst.buffer
+        if sb.scope != "fragment" or db.scope != "fragment":
+            return self.lower_reduce_simt(op)
+        S_lay: Fragment = sb.layout
+        D_lay: Fragment = db.layout
+        kind = op.reduce_type
+        dim = op.dim
+        sl, dl = ctx.local_of(sb), ctx.local_of(db)
+        dshape = db.static_shape()
+        squeeze_dim = len(dshape) == len(S_lay.shape)  # dst keeps a unit dim
+        # group source registers by destination register (must be thread-uniform)
+        groups: Dict[int, List[int]] = {}
+        for t in range(0, ctx.T, max(1, ctx.T // 16)):
+            pass
+        dmap0 = D_lay.thread_local_map(0)
+        for r in range(S_lay.local_size):
+            owners = set()
+            for t in _sample_threads(ctx.T):
+                idx = S_lay.inverse(t, r)
+                didx = list(idx)
+                if squeeze_dim:
+                    didx[dim] = 0
+                else:
+                    didx.pop(dim)
+                m = D_lay.thread_local_map(t)
+                li = m.get(tuple(didx))
+                if li is None:
+                    raise LoweringError(f"reduce: thread {t} lacks destination element {didx} of {db.name}")
+                owners.add(li)
+            if len(owners) != 1:
+                raise LoweringError("reduce: non-uniform register mapping")
+            groups.setdefault(owners.pop(), []).append(r)
+        out = []
+        accs = {}
+        dt = sb.dtype
+        for d, rs in sorted(groups.items()):
+            acc = None
+            for r in rs:
+                x = BufferLoad(sl, [IntImm(r)])
+                if kind in ("abssum", "absmax"):
+                    x = call("abs", [x], dt)
+                acc = x if acc is None else _combine(kind, acc, x)
+            accs[d] = acc
+        # cross-thread: thread digits of the reduced dim
+        lane_mask, wave_digits = _reduce_thread_masks(S_lay, dim)
+        opname = _REDUCE_OPS[kind][0]
+        tmp_vars = {}
+        for d, acc in accs.items():
+            v = Var(f"red{d}", dt, nonneg=False)
+            out.append(S.LetStmt(v, acc))
+            tmp_vars[d] = v
+        red_vals = {}
+        if lane_mask:
+            for d, v in tmp_vars.items():
+                v2 = Var(f"redl{d}", dt, nonneg=False)
+                out.append(S.LetStmt(v2, call("extern", ["tl::lane_allreduce<%s, %d>" % (opname, lane_mask), v], dt)))
+                red_vals[d] = v2
+        else:
+            red_vals = dict(tmp_vars)
+        if wave_digits:
+            # cross-wave through an LDS workspace: ws[d][tid]
+            nd = len(red_vals)
+            ws = ctx.new_workspace(nd * ctx.T, dt)
+            wsf = ctx.flat_of(ws)
+            keys = sorted(red_vals)
+            out.append(L.CallStmt("tl::sync_threads", []))
+            for j, d in enumerate(keys):
+                out.append(S.StoreStmt(wsf, [binop("+", j * ctx.T, ctx.tid)], red_vals[d]))
+            out.append(L.CallStmt("tl::sync_threads", []))
+            partners = _partner_offsets(ctx.tid, wave_digits)
+            new_vals = {}
+            for j, d in enumerate(keys):
+                acc = None
+                for p in partners:
+                    x = BufferLoad(wsf, [binop("+", j * ctx.T, p)])
+                    acc = x if acc is None else _combine(kind, acc, x)
+                v3 = Var(f"redw{d}", dt, nonneg=False)
+                out.append(S.LetStmt(v3, acc))
+                new_vals[d] = v3
+            out.append(L.CallStmt("tl::sync_threads", []))
+            red_vals = new_vals
+        for d, v in red_vals.items():
+            if op.clear:
+                out.append(S.StoreStmt(dl, [IntImm(d)], cast(v, db.dtype)))
+            else:
+                out.append(S.StoreStmt(dl, [IntImm(d)], cast(_combine(kind, BufferLoad(dl, [IntImm(d)]), v),
+                                                             db.dtype)))
+        return _scoped(S.SeqStmt(out))
+
+    def lower_reduce_simt(self, op: O.ReduceOp):
+        """Reduction over shared/local buffers: each thread reduces whole rows serially."""
+        ctx = self.ctx
+        src, dst = op.src, op.dst
+        sext = src.static_extents()
+        if sext is None:
+            raise LoweringError("reduce needs static extents")
+        dim = op.dim
+        outer = [e for d, e in enumerate(sext) if d != dim]
+        n_out = _prod(outer)
+        red_n = sext[dim]
+        dt = src.buffer.dtype
+        steps = -(-n_out // ctx.T)
+        out = []
+        for o in range(steps):
+            slot = binop("+", o * ctx.T, ctx.tid)
+            oidx = _unflatten(slot, outer)
+            k = Var("rk")
+            sidx = list(oidx)
+            sidx.insert(dim, k)
+            sidx = [binop("+", m, i) for m, i in zip(src.mins, sidx)]
+            didx = list(oidx)
+            if len(dst.region) == len(src.region):
+                didx.insert(dim, IntImm(0))
+            didx = [binop("+", m, i) for m, i in zip(dst.mins, didx)]
+            acc = Var("racc", dt, nonneg=False)
+            accb = ctx.new_local(f"racc{ctx.ws_counter}_{o}", 1, dt)
+            ctx.ws_counter += 1
+            x = BufferLoad(src.buffer, sidx)
+            if op.reduce_type in ("abssum", "absmax"):
+                x = call("abs", [x], dt)
+            body = [S.StoreStmt(accb, [IntImm(0)], _reduce_init(op.reduce_type, dt)),
+                    S.ForStmt(k, 0, red_n, "serial",
+                              S.StoreStmt(accb, [IntImm(0)], _combine(op.reduce_type, BufferLoad(accb, [IntImm(0)]),
+                                                                      x)))]
+            res = BufferLoad(accb, [IntImm(0)])
+            if not op.clear:
+                res = _combine(op.reduce_type, BufferLoad(dst.buffer, didx), res)
+            body.append(S.StoreStmt(dst.buffer, didx, cast(res, dst.buffer.dtype)))
+            blk = self.stmt(S.SeqStmt(body))
+            out.append(S.IfStmt(binop("<", slot, n_out), blk) if (o + 1) * ctx.T > n_out else blk)
+        return S.SeqStmt(out)
+
+    def lower_CumSumOp(self, op: O.CumSumOp):
+        """Inclusive scan along ``dim`` for shared/global buffers (one thread per row)."""
+        ctx = self.ctx
+        src, dst = op.src, op.dst
+        if src.buffer.scope == "fragment" or dst.buffer.scope == "fragment":
+            raise LoweringError("T.cumsum on fragments is not supported yet; stage through shared memory")
+        sext = src.static_extents()
+        dim = op.dim
+        outer = [e for d, e in enumerate(sext) if d != dim]
+        n_out = _prod(outer)
+        n = sext[dim]
+        dt = dst.buffer.dtype
+        out = [L.CallStmt("tl::sync_threads", [])]
+        steps = -(-n_out // ctx.T)
+        for o in range(steps):
+            slot = binop("+", o * ctx.T, ctx.tid)
+            oidx = _unflatten(slot, outer)
+            k = Var("ck")
+            kk = binop("-", n - 1, k) if op.reverse else k
+            sidx = list(oidx)
+            sidx.insert(dim, kk)
+            didx = list(sidx)
+            sidx = [binop("+", m, i) for m, i in zip(src.mins, sidx)]
+            didx = [binop("+", m, i) for m, i in zip(dst.mins, didx)]
+            accb = ctx.new_local(f"cacc{ctx.ws_counter}", 1, dt)
+            ctx.ws_counter += 1
+            body = [S.StoreStmt(accb, [IntImm(0)], const(0, dt)),
+                    S.ForStmt(k, 0, n, "serial", S.SeqStmt([
+                        S.StoreStmt(accb, [IntImm(0)], BufferLoad(accb, [IntImm(0)]) +
+                                    cast(BufferLoad(src.buffer, sidx), dt)),
+                        S.StoreStmt(dst.buffer, didx, BufferLoad(accb, [IntImm(0)]))]))]
+            blk = self.stmt(S.SeqStmt(body))
+            out.append(S.IfStmt(binop("<", slot, n_out), blk) if (o + 1) * ctx.T > n_out else blk)
+        out.append(L.CallStmt("tl::sync_threads", []))
+        return S.SeqStmt(out)
+
+    def lower_AtomicOp(self, op: O.AtomicOp):
+        dst = op.dst
+        if isinstance(op.src, BufferRegion):
+            src = op.src
+            nest = _copy_nest(src, dst, None, atomic=op.op)
+            lay = None
+            if src.buffer.scope == "fragment":
+                lay = _squeeze_fragment(src.buffer.layout, src.buffer.static_shape())
+            return self.lower_nest(nest, lay)
+        val = op.src
+        nest = _region_nest(dst, lambda idx: None, atomic=(op.op, val))
+        return self.lower_nest(nest)
+
+    def lower_FinalizeReducerOp(self, op):
+        b = op.buf.buffer
+        kind = getattr(b, "reducer_op", "sum")
+        lay = b.layout
+        # combine replicas: all-reduce over replication digits of the layout
+        lane_mask, wave_digits = _replica_masks(lay)
+        ctx = self.ctx
+        lb = ctx.local_of(b)
+        out = []
+        opname = _REDUCE_OPS[kind][0]
+        if wave_digits:
+            raise LoweringError("finalize_reducer across waves is not supported; keep replicas within a wave")
+        if lane_mask:
+            for i in range(lb.shape[0]):
+                out.append(S.StoreStmt(lb, [IntImm(i)], call("extern", ["tl::lane_allreduce<%s, %d>" % (opname,
+                                                                                                       lane_mask),
+                                                                         BufferLoad(lb, [IntImm(i)])], b.dtype)))
+        return S.SeqStmt(out)
+
+    def lower_AsyncCopyOp(self, op: AsyncCopyOp):
+        ctx = self.ctx
+        p = op.plan
+        src, dst = op.src, op.dst
+        NB = dst.buffer
+        lay = NB.layout
+        epc = 16 // p["eb"]
+        nw = p["nwaves"]
+        wave = ctx.wave_expr()
+        lane = ctx.lane_expr()
+        stage = self.expr(dst.mins[0])
+        base_off = ctx.flat_index(NB, [stage, 0, 0])
+        out = []
+        smins = [self.expr(m) for m in src.mins]
+        for i in range(p["instrs"]):
+            chunk_base = binop("*", binop("+", i * nw, wave), 64)
+            P = binop("+", chunk_base, lane)
+            row = binop("//", P, p["cpr"])
+            pch = binop("%", P, p["cpr"])
+            if isinstance(lay, SwizzleLayout) and lay.bits:
+                lch = binop("^", pch, lay._xor_term(row))
+            else:
+                lch = pch
+            col = binop("*", lch, epc)
+            idx = list(smins)
+            if p["rdim"] is not None:
+                idx[p["rdim"]] = binop("+", idx[p["rdim"]], row)
+            idx[p["cdim"]] = binop("+", idx[p["cdim"]], col)
+            gidx = ctx.flat_index(src.buffer, idx)
+            lds_off = binop("+", base_off, binop("*", chunk_base, epc))
+            out.append(L.CallStmt("tl::glds16", [L.BufferPtr(ctx.flat_of(src.buffer), gidx),
+                                                 L.BufferPtr(ctx.flat_of(NB), lds_off)]))
+        return S.SeqStmt(out)
+
+    def lower_StagedCopyOp(self, op: StagedCopyOp):
+        """Register-staged copy: phase 'load' fills a staging array, 'store' writes it to LDS."""
+        ctx = self.ctx
+        steps = _simt_copy_steps(ctx, op.src, op.dst, self.known_div)
+        nelem = sum(st["vec"] for st in steps)
+        stage = ctx.staging.get(op.key)
+        if stage is None:
+            stage = ctx.new_local(f"stage{op.key}", max(1, nelem), op.src.buffer.dtype)
+            ctx.staging[op.key] = stage
+        out = []
+        pos = 0
+        for st in steps:
+            vec = st["vec"]
+            if op.phase == "load":
+                sidx = [self.expr(i) for i in st["src_idx"]]
+                sflat = ctx.flat_index(op.src.buffer, sidx)
+                if st["guard"] is not None:
+                    # out-of-range lanes load zeros (keeps the staging array defined)
+                    zero = S.SeqStmt([S.StoreStmt(stage, [IntImm(pos + j)], const(0, stage.dtype))
+                                      for j in range(vec)])
+                    body = L.VecLoadStmt(stage, pos, ctx.flat_of(op.src.buffer), sflat, vec) if vec > 1 else \
+                        S.StoreStmt(stage, [IntImm(pos)], BufferLoad(ctx.flat_of(op.src.buffer), [sflat]))
+                    out.append(S.IfStmt(self.expr(st["guard"]), body, zero))
+                else:
+                    out.append(L.VecLoadStmt(stage, pos, ctx.flat_of(op.src.buffer), sflat, vec) if vec > 1 else
+                               S.StoreStmt(stage, [IntImm(pos)], BufferLoad(ctx.flat_of(op.src.buffer), [sflat])))
+            else:
+                didx = [self.expr(i) for i in st["dst_idx"]]
+                dflat = ctx.flat_index(op.dst.buffer, didx)
+                vals = [cast(BufferLoad(stage, [IntImm(pos + j)]), op.dst.buffer.dtype) for j in range(vec)]
+                s_ = L.VecStoreStmt(ctx.flat_of(op.dst.buffer), dflat, vals) if vec > 1 else \
+                    S.StoreStmt(ctx.flat_of(op.dst.buffer), [dflat], vals[0])
+                if st["dst_guard"] is not None:
+                    s_ = S.IfStmt(self.expr(st["dst_guard"]), s_)
+                out.append(s_)
+            pos += vec
+        return S.SeqStmt(out)
+
+    def lower_CommBroadcastOp(self, op):
+        from ..parallel.comm_lower import lower_comm
+        return lower_comm(self, op)
+
+    lower_CommPutOp = lower_CommBroadcastOp
+    lower_CommAllGatherOp = lower_CommBroadcastOp
+    lower_CommAllReduceOp = lower_CommBroadcastOp
+    lower_CommBarrierOp = lower_CommBroadcastOp
+    lower_CommFenceOp = lower_CommBroadcastOp
+
+    def lower_Im2ColOp(self, op):
+        raise LoweringError("T.c2d_im2col lowering: use the convolution example's explicit gather instead")
+
+
+# ---------------------------------------------------------------------------
+# helpers
+# ---------------------------------------------------------------------------
+
+
+def ctx_is_cpu(ctx):
+    return ctx.is_cpu
+
+
+def _b(x):
+    return "true" if x else "false"
+
+
+def _scoped(s):
+    s = S.SeqStmt([s]) if not isinstance(s, S.SeqStmt) else s
+    s.scoped = True
+    return s
+
+
+def _nest_loops(outer: S.ForStmt) -> List[S.ForStmt]:
+    loops = [outer]
+    cur = outer
+    while isinstance(cur.body, S.ForStmt) and cur.body.kind == "parallel":
+        cur = cur.body
+        loops.append(cur)
+    return loops
+
+
+def _unflatten(lin, exts):
+    vals = []
+    rem = lin
+    for i, e in enumerate(reversed(exts)):
+        if i == len(exts) - 1:
+            vals.append(rem)
+        else:
+            vals.append(binop("%", rem, e))
+            rem = binop("//", rem, e)
+    return list(reversed(vals))
+
+
+def _unflatten_dyn(lin, exts):
+    return _unflatten(lin, exts)
+
+
+def _slot_div(kd, tid, o, T, vec):
+    return kd
+
+
+def _full(r: BufferRegion) -> bool:
+    ext = r.static_extents()
+    shp = r.buffer.static_shape()
+    return ext is not None and shp is not None and ext == shp and all(as_int(m) == 0 for m in r.mins)
+
+
+def _squeeze_pairs(src: BufferRegion, dst: BufferRegion):
+    se, de = src.extents, dst.extents
+    sd = [d for d, e in enumerate(se) if as_int(e) != 1]
+    dd = [d for d, e in enumerate(de) if as_int(e) != 1]
+    sv = [as_int(se[d]) for d in sd]
+    dv = [as_int(de[d]) for d in dd]
+    if len(sd) != len(dd):
+        raise LoweringError(f"T.copy: incompatible regions {src} -> {dst}")
+    for a, b in zip(sv, dv):
+        if a is not None and b is not None and a != b:
+            raise LoweringError(f"T.copy: extent mismatch {src} -> {dst}")
+    return sd, dd
+
+
+def _copy_nest(src: BufferRegion, dst: BufferRegion, coalesced_width, atomic=None) -> S.ForStmt:
+    sd, dd = _squeeze_pairs(src, dst)
+    exts = [dst.extents[d] for d in dd] if dd else []
+    vars_ = [Var(f"c{i}") for i in range(len(exts))]
+    sidx = [m for m in src.mins]
+    didx = [m for m in dst.mins]
+    for v, s, d in zip(vars_, sd, dd):
+        sidx[s] = binop("+", sidx[s], v)
+        didx[d] = binop("+", didx[d], v)
+    val = BufferLoad(src.buffer, sidx)
+    if atomic is not None:
+        body = S.EvaluateStmt(call(f"tl.atomic_{atomic}", [BufferLoad(dst.buffer, didx), val], dst.buffer.dtype))
+    else:
+        body = S.StoreStmt(dst.buffer, didx, cast(val, dst.buffer.dtype))
+    if not exts:
+        vars_ = [Var("c0")]
+        exts = [1]
+    ann = {"coalesced_width": coalesced_width} if coalesced_width else {}
+    for v, e in reversed(list(zip(vars_, exts))):
+        body = S.ForStmt(v, 0, e, "parallel", body, ann)
+    return body
+
+
+def _region_nest(r: BufferRegion, mk, atomic=None) -> S.ForStmt:
+    exts = list(r.extents)
+    vars_ = [Var(f"f{i}") for i in range(len(exts))]
+    idx = [binop("+", m, v) for m, v in zip(r.mins, vars_)]
+    if atomic is not None:
+        kind, val = atomic
+        body = S.EvaluateStmt(call(f"tl.atomic_{kind}", [BufferLoad(r.buffer, idx), convert(val)], r.buffer.dtype))
+    else:
+        b, _, val = mk(idx)
+        body = S.StoreStmt(b, idx, val)
+    for v, e in reversed(list(zip(vars_, exts))):
+        body = S.ForStmt(v, 0, e, "parallel", body)
+    return body
+
+
+def _squeeze_fragment(lay: Fragment, shape) -> Fragment:
+    """Drop unit dims of a fragment layout (so it matches a squeezed copy nest)."""
+    keep = [d for d, s in enumerate(shape) if s != 1]
+    if len(keep) == len(shape):
+        return lay
+    from ..layout.fragment import Digit
+    remap = {old: new for new, old in enumerate(keep)}
+    td = [Digit(remap[d.dim], d.stride, d.size) if d.dim >= 0 else d for d in lay.thread_digits]
+    ld = [Digit(remap[d.dim], d.stride, d.size) for d in lay.local_digits]
+    return Fragment([shape[d] for d in keep], td, ld, lay.name)
+
+
+class _SimtRewriter(Mutator):
+
+    def __init__(self, ctx, vmap):
+        self.ctx = ctx
+        self.vmap = vmap
+
+    def _acc(self, n):
+        if isinstance(n, BufferLoad):
+            b = n.buffer
+            idx = [substitute(i, self.vmap) for i in n.indices]
+            if b.scope in ("local", "var"):
+                return BufferLoad(b, [b.offset_of(idx)] if b.ndim != 1 else idx)
+            if b.scope == "fragment":
+                raise LoweringError(f"fragment {b.name} in a non-fragment T.Parallel nest")
+            return BufferLoad(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)])
+        return None
+
+    def expr(self, e):
+        if not isinstance(e, PrimExpr):
+            return e
+        return substitute(transform(e, self._acc), self.vmap)
+
+    def store(self, s):
+        b = s.buffer
+        val = self.expr(s.value)
+        idx = [self.expr(i) for i in s.indices]
+        if b.scope in ("local", "var"):
+            return S.StoreStmt(b, [b.offset_of(idx)] if b.ndim != 1 else idx, val)
+        return S.StoreStmt(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)], val)
+
+
+def _sample_threads(T):
+    if T <= 256:
+        return range(T)
+    return list(range(0, T, 1))
+
+
+def _thread_digit_weights(lay: Fragment):
+    weights = []
+    w = 1
+    for d in reversed(lay.thread_digits):
+        weights.append((d, w))
+        w *= d.size
+    return list(reversed(weights))
+
+
+def _reduce_thread_masks(lay: Fragment, dim: int):
+    lane_mask = 0
+    wave_digits = []
+    for d, w in _thread_digit_weights(lay):
+        if d.dim != dim:
+            continue
+        if w * d.size <= 64:
+            for b in range(int(math.log2(d.size))):
+                lane_mask |= w << b
+        elif w >= 64:
+            wave_digits.append((d, w))
+        else:
+            raise LoweringError("reduction digit straddles the wave boundary")
+    return lane_mask, wave_digits
+
+
+def _replica_masks(lay: Fragment):
+    lane_mask = 0
+    wave_digits = []
+    for d, w in _thread_digit_weights(lay):
+        if d.dim >= 0:
+            continue
+        if w * d.size <= 64:
+            for b in range(int(math.log2(d.size))):
+                lane_mask |= w << b
+        else:
+            wave_digits.append((d, w))
+    return lane_mask, wave_digits
+
+
+def _partner_offsets(tid, wave_digits):
+    """Thread ids of all partners (including self) that differ only in the given digits."""
+    exprs = [tid]
+    for d, w in wave_digits:
+        new = []
+        for e in exprs:
+            cur = binop("%", binop("//", e, w), d.size)
+            for v in range(d.size):
+                new.append(binop("+", e, binop("*", binop("-", v, cur), w)))
+        exprs = new
+    return exprs
+
+
+def _simt_copy_steps(ctx: LowerCtx, src: BufferRegion, dst: BufferRegion, known_div) -> List[dict]:
+    """Thread mapping of a plain copy: list of per-step {src_idx, dst_idx, vec, guard}."""
+    sd, dd = _squeeze_pairs(src, dst)
+    exts = [as_int(dst.extents[d]) for d in dd]
+    if any(e is None for e in exts):
+        raise LoweringError("register-staged copy needs static extents")
+    total = _prod(exts) if exts else 1
+    eb = max(src.buffer.dtype.bytes, dst.buffer.dtype.bytes)
+    vec = max(1, 16 // eb)
+    while vec > 1:
+        if exts and exts[-1] % vec == 0 and _copy_vec_ok(src, dst, sd, dd, vec, known_div):
+            break
+        vec //= 2
+    slots = total // vec
+    steps = -(-slots // ctx.T)
+    out = []
+    for o in range(steps):
+        slot = binop("+", o * ctx.T, ctx.tid) if steps > 1 else ctx.tid
+        lin = binop("*", slot, vec)
+        vals = _unflatten(lin, exts) if exts else []
+        sidx = list(src.mins)
+        didx = list(dst.mins)
+        for v, s, d in zip(vals, sd, dd):
+            sidx[s] = binop("+", sidx[s], v)
+            didx[d] = binop("+", didx[d], v)
+        guard = binop("<", slot, slots) if (o + 1) * ctx.T > slots else None
+        # source bounds (zero-fill) for ragged tiles
+        sg = _bounds_guard(src, sidx, sd, vals, vec)
+        g = guard if sg is None else (sg if guard is None else logical_and(guard, sg))
+        dg = guard
+        out.append(dict(src_idx=sidx, dst_idx=didx, vec=vec, guard=g, dst_guard=dg))
+    return out
+
+
+def _bounds_guard(r: BufferRegion, idx, dims, vals, vec):
+    b = r.buffer
+    if b.scope != "global":
+        return None
+    conds = None
+    for d, i in enumerate(idx):
+        s = b.shape[d]
+        ext = r.extents[d]
+        # skip dims provably in range
+        c = binop("<", binop("+", i, vec - 1) if d == len(idx) - 1 else i, s)
+        if as_int(c) == 1:
+            continue
+        conds = c if conds is None else logical_and(conds, c)
+    return conds
+
+
+def _copy_vec_ok(src, dst, sd, dd, vec, known_div) -> bool:
+    for r, dims in ((src, sd), (dst, dd)):
+        b = r.buffer
+        if not dims:
+            return False
+        last = dims[-1]
+        if last != len(r.region) - 1:
+            return False
+        if b.scope == "global":
+            st = b.get_strides()
+            if as_int(st[-1]) != 1:
+                return False
+            for s_ in st[:-1]:
+                if not divisible_by(convert(s_), vec):
+                    return False
+        if not divisible_by(r.region[last][0], vec, known_div):
+            return False
+        if b.scope == "shared" and isinstance(b.layout, SwizzleLayout):
+            if vec > b.layout.epc:
+                return False
+    return True
+
+
+def lower_tile_ops(kernel: S.KernelStmt, target, pass_cfg=None):
+    ctx = LowerCtx(kernel, target, pass_cfg)
+    lw = TileOpLowerer(ctx)
+    body = lw.stmt(kernel.body)
+    allocs = [S.AllocStmt(b) for b in ctx.extra_allocs]
+    k = S.KernelStmt(kernel.grid, kernel.threads, kernel.block_vars, kernel.thread_vars,
+                     S.SeqStmt(allocs + [body]), kernel.is_cpu, kernel.prelude)
+    k.attrs = dict(kernel.attrs)
+    k.attrs["tid"] = ctx.tid
+    k.attrs["lane"] = ctx.lane if ctx.uses_lane else None
+    k.attrs["wave"] = ctx.wave if ctx.uses_wave else None
+    k.attrs["flat"] = ctx.flat
+    return k, ctx

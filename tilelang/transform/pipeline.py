@@ -1,0 +1,349 @@
+"""Software pipelining of ``T.Pipelined`` loops (tile level).
+
+Reference: ``src/transform/pipeline_planning.cc`` (derives stage/order from
+``num_stages``; async stages when the target has async copy) and
+``inject_pipeline.cc`` (prologue/body/epilogue, multi-versioned buffers).
+
+MI355X design (guide §5 "Pipelining across barriers", T3/T4):
+  * every global->shared ``T.copy`` in the loop body is a *producer*; its shared
+    buffer is multi-versioned ``num_stages`` deep (one LDS arena slot per stage);
+  * producers that are eligible become **LDS-DMA** (``global_load_lds_dwordx4``)
+    issued ``num_stages-1`` iterations ahead; the loop waits with a *counted*
+    ``s_waitcnt vmcnt(N)`` and a raw ``s_barrier`` (no ``vmcnt(0)`` drain), so
+    ``num_stages-2`` tiles stay in flight across every barrier;
+  * other producers are **register staged** (T14 "issue-early / write-late"): the
+    global loads of tile k+1 are issued before the compute of tile k and written
+    to LDS after it;
+  * one barrier per iteration orders both the RAW hazard on tile k and the WAR
+    hazard on the slot being refilled.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+from ..ir import stmt as S
+from ..ir import tileop as O
+from ..ir import lowered as L
+from ..ir.buffer import Buffer, BufferRegion
+from ..ir.expr import (PrimExpr, Var, IntImm, as_int, binop, const, convert, divisible_by, free_vars, substitute,
+                       call)
+from ..ir import dtypes as _dt
+from ..layout.layout import Layout, LinearLayout, SwizzleLayout
+from .utils import BufferReplacer, Mutator, Substituter, bound, flatten_seq
+
+
+class AsyncCopyOp(O.TileOp):
+    """Global->LDS DMA copy (lowered to ``tl::glds16``)."""
+    kind = "async_copy"
+
+    def __init__(self, src: BufferRegion, dst: BufferRegion, plan: dict):
+        self.src, self.dst, self.plan = src, dst, plan
+
+    def regions(self):
+        return [self.src, self.dst]
+
+    def reads(self):
+        return [self.src]
+
+    def writes(self):
+        return [self.dst]
+
+
+class StagedCopyOp(O.TileOp):
+    """Register-staged copy split in two phases sharing a staging register array."""
+    kind = "staged_copy"
+
+    def __init__(self, src: BufferRegion, dst: BufferRegion, phase: str, key: int):
+        self.src, self.dst, self.phase, self.key = src, dst, phase, key
+
+    def regions(self):
+        return [self.src, self.dst]
+
+    def reads(self):
+        return [self.src] if self.phase == "load" else []
+
+    def writes(self):
+        return [self.dst] if self.phase == "store" else []
+
+
+def stage_layout(layout: Optional[Layout], shape: List[int], stages: int) -> Layout:
+    if layout is None:
+        return LinearLayout([stages] + list(shape))
+    if isinstance(layout, SwizzleLayout):
+        return SwizzleLayout([stages] + list(layout.shape), layout.elem_bytes, layout.bits, layout.name)
+    if isinstance(layout, LinearLayout):
+        return LinearLayout([stages] + list(layout.shape))
+    size = 1
+    for s in (layout.output_shape or shape):
+        size *= int(s)
+    inner = layout
+
+    def fwd(s, *idx):
+        return [s * size + inner.offset(*idx)]
+
+    return Layout([stages] + list(shape), fwd, None, [stages * size], name=f"stage_{layout.name}")
+
+
+def _squeeze(ext):
+    ext = list(ext)
+    while len(ext) > 2 and ext[0] == 1:
+        ext = ext[1:]
+    return ext
+
+
+def glds_plan(op: O.CopyOp, num_threads: int, ranges, target) -> Optional[dict]:
+    """Decide whether a global->shared copy can be a lane-linear LDS-DMA; return its geometry."""
+    if target is not None and getattr(target, "kind", "hip") != "hip":
+        return None
+    if getattr(target, "disable_glds", False):
+        return None
+    src, dst = op.src, op.dst
+    sb, db = src.buffer, dst.buffer
+    if sb.scope != "global" or db.scope != "shared" or sb.dtype != db.dtype:
+        return None
+    eb = sb.dtype.bytes
+    dext = dst.static_extents()
+    dshape = db.static_shape()
+    if dext is None or dshape is None or dext != dshape or len(dshape) != 2:
+        return None
+    R, C = dshape
+    if (C * eb) % 16 or (R * C * eb) % (1024 * (num_threads // 64)):
+        return None
+    lay = db.layout
+    if lay is not None and not isinstance(lay, (SwizzleLayout, LinearLayout)):
+        return None
+    # map the two tile dims onto source dims (skip unit dims)
+    sext = src.static_extents()
+    if sext is None:
+        return None
+    nonunit = [d for d, e in enumerate(sext) if e != 1]
+    if R == 1:
+        if len(nonunit) != 1 or sext[nonunit[0]] != C:
+            return None
+        rdim, cdim = None, nonunit[0]
+    else:
+        if len(nonunit) != 2 or sext[nonunit[0]] != R or sext[nonunit[1]] != C:
+            return None
+        rdim, cdim = nonunit
+    strides = sb.get_strides()
+    if as_int(strides[cdim]) != 1:
+        return None
+    # 16-byte alignment of every source chunk: row stride and column start
+    epc = 16 // eb
+    if rdim is not None:
+        rs = strides[rdim]
+        if not divisible_by(convert(rs), epc):
+            return None
+    if not divisible_by(src.region[cdim][0], epc):
+        return None
+    # in-bounds proof for every dim
+    shape = sb.shape
+    for d, (m, e) in enumerate(src.region):
+        b = bound(m, ranges)
+        s = as_int(shape[d])
+        ev = as_int(e)
+        if b is None or s is None or ev is None or b[0] < 0 or b[1] + ev > s:
+            return None
+    n_chunks = R * C * eb // 16
+    nw = num_threads // 64
+    return dict(R=R, C=C, eb=eb, rdim=rdim, cdim=cdim, instrs=n_chunks // 64 // nw, nwaves=nw, cpr=C * eb // 16)
+
+
+class _Ranges:
+
+    def __init__(self):
+        self.r: Dict[Var, tuple] = {}
+
+
+def _var_ranges_for_kernel(k: S.KernelStmt) -> Dict[Var, tuple]:
+    r = {}
+    for v, g in zip(k.block_vars, k.grid):
+        gv = as_int(g)
+        if gv is not None:
+            r[v] = (0, gv - 1)
+    tot = k.num_threads
+    for v, t in zip(k.thread_vars, k.threads):
+        r[v] = (0, int(t) - 1)
+    return r
+
+
+class PipelineInjector(Mutator):
+
+    def __init__(self, kernel: S.KernelStmt, num_threads: int, target):
+        self.kernel = kernel
+        self.T = num_threads
+        self.target = target
+        self.ranges = _var_ranges_for_kernel(kernel)
+        self.key = 0
+
+    def visit_ForStmt(self, s: S.ForStmt):
+        mn, ext = as_int(s.min), as_int(s.extent)
+        if mn is not None and ext is not None and ext > 0:
+            self.ranges[s.var] = (mn, mn + ext - 1)
+        body = self.stmt(s.body)
+        if s.kind != "pipelined":
+            return S.ForStmt(s.var, s.min, s.extent, s.kind, body, s.annotations)
+        return self.pipeline(S.ForStmt(s.var, s.min, s.extent, s.kind, body, s.annotations))
+
+    def visit_LetStmt(self, s):
+        return s
+
+    def pipeline(self, loop: S.ForStmt):
+        nstages = int(loop.annotations.get("num_stages", 0))
+        stmts = flatten_seq(loop.body)
+        serial = S.ForStmt(loop.var, loop.min, loop.extent, "serial", loop.body,
+                           {k: v for k, v in loop.annotations.items() if k != "num_stages"})
+        if nstages < 2 or getattr(self.target, "kind", "hip") == "cpu":
+            return serial
+        k, n = loop.var, loop.extent
+        lets: Dict[Var, PrimExpr] = {}
+        producers = []
+        written_elsewhere = set()
+        for st in stmts:
+            if isinstance(st, S.LetStmt):
+                lets[st.var] = substitute(st.value, lets)
+            elif isinstance(st, S.TileOpStmt) and isinstance(st.op, O.CopyOp) and \
+                    st.op.src.buffer.scope == "global" and st.op.dst.buffer.scope == "shared":
+                producers.append(st)
+            else:
+                for w in S.walk(st):
+                    if isinstance(w, S.TileOpStmt):
+                        for r in w.op.writes():
+                            written_elsewhere.add(r.buffer)
+                    if isinstance(w, S.StoreStmt):
+                        written_elsewhere.add(w.buffer)
+        producers = [p for p in producers if p.op.dst.buffer not in written_elsewhere]
+        if not producers:
+            return serial
+        allowed = set(free_vars_stmt_outer(self.kernel)) | {k}
+        prods = []
+        for p in producers:
+            src = _subst_region(p.op.src, lets)
+            fv = set()
+            for m, e in src.region:
+                fv |= {id(v) for v in free_vars(m)}
+            loop_local = {id(v) for v in lets}  # unresolved lets would appear as themselves
+            prods.append((p, src))
+        # multi-version the shared buffers
+        mapping = {}
+        newbufs = {}
+        for p, _ in prods:
+            B = p.op.dst.buffer
+            if B in newbufs:
+                continue
+            shp = B.static_shape()
+            NB = Buffer(B.name, [nstages] + shp, B.dtype, "shared")
+            NB.layout = stage_layout(B.layout, shp, nstages)
+            NB._auto_name = False
+            NB.stages_of = B
+            newbufs[B] = NB
+        kk = binop("-", k, loop.min)
+        stage = binop("%", kk, nstages)
+        for B, NB in newbufs.items():
+            mapping[B] = (NB, [stage])
+        # classify producers
+        rng = dict(self.ranges)
+        if as_int(loop.min) is not None and as_int(loop.extent) is not None:
+            rng[k] = (as_int(loop.min), as_int(loop.min) + as_int(loop.extent) - 1)
+        asyncs, staged = [], []
+        for p, src in prods:
+            plan = glds_plan(O.CopyOp(src, p.op.dst), self.T, rng, self.target)
+            if plan is not None:
+                asyncs.append((p, src, plan))
+            else:
+                staged.append((p, src))
+        L_instr = sum(pl["instrs"] for _, _, pl in asyncs)
+
+        def issue_async(j, stg):
+            out = []
+            for p, src, plan in asyncs:
+                srcj = _subst_region(src, {k: binop("+", loop.min, j)})
+                NB = newbufs[p.op.dst.buffer]
+                dst = BufferRegion(NB, [(stg, 1)] + list(p.op.dst.region))
+                out.append(S.TileOpStmt(AsyncCopyOp(srcj, dst, plan)))
+            return out
+
+        keys = {}
+
+        def staged_phase(j, stg, phase):
+            out = []
+            for p, src in staged:
+                if id(p) not in keys:
+                    self.key += 1
+                    keys[id(p)] = self.key
+                srcj = _subst_region(src, {k: binop("+", loop.min, j)})
+                NB = newbufs[p.op.dst.buffer]
+                dst = BufferRegion(NB, [(stg, 1)] + list(p.op.dst.region))
+                out.append(S.TileOpStmt(StagedCopyOp(srcj, dst, phase, keys[id(p)])))
+            return out
+
+        prologue = []
+        nv = as_int(n)
+        for j in range(nstages - 1):
+            st = issue_async(j, j)
+            if not st:
+                break
+            if nv is not None and j >= nv:
+                break
+            prologue.append(S.seq(*st) if nv is not None else S.IfStmt(binop("<", j, n), S.seq(*st)))
+        if staged:
+            st = staged_phase(0, 0, "load") + staged_phase(0, 0, "store")
+            prologue.append(S.seq(*st) if nv is not None and nv > 0 else S.IfStmt(binop("<", 0, n), S.seq(*st)))
+
+        consumer_stmts = [st for st in stmts if not any(st is p for p, _ in prods)]
+        consumers = BufferReplacer(mapping).stmt(S.SeqStmt(consumer_stmts))
+        body = []
+        if asyncs:
+            if nstages > 2:
+                body.append(S.IfStmt(binop("<", binop("+", kk, nstages - 2), n),
+                                     L.CallStmt("tl::wait_vmcnt", [], [L_instr * (nstages - 2)]),
+                                     L.CallStmt("tl::wait_vmcnt", [], [0])))
+            else:
+                body.append(L.CallStmt("tl::wait_vmcnt", [], [0]))
+        body.append(L.CallStmt("tl::barrier_raw", []))
+        if asyncs:
+            j = binop("+", kk, nstages - 1)
+            body.append(S.IfStmt(binop("<", j, n), S.seq(*issue_async(j, binop("%", j, nstages)))))
+        if staged:
+            j1 = binop("+", kk, 1)
+            body.append(S.IfStmt(binop("<", j1, n), S.seq(*staged_phase(j1, binop("%", j1, nstages), "load"))))
+        body.append(consumers)
+        if staged:
+            j1 = binop("+", kk, 1)
+            body.append(S.IfStmt(binop("<", j1, n), S.seq(*staged_phase(j1, binop("%", j1, nstages), "store"))))
+        new_loop = S.ForStmt(k, loop.min, loop.extent, "serial", S.SeqStmt(body),
+                             {"pipelined": nstages, "_lets": lets})
+        # allocations for the new multi-versioned buffers replace the old ones (done by caller)
+        self.replaced = getattr(self, "replaced", {})
+        self.replaced.update(newbufs)
+        tail = [L.CallStmt("tl::barrier_raw", [])]
+        return S.SeqStmt(prologue + [new_loop] + tail)
+
+
+def free_vars_stmt_outer(kernel):
+    return list(kernel.block_vars) + list(kernel.thread_vars)
+
+
+def _subst_region(r: BufferRegion, vmap) -> BufferRegion:
+    return BufferRegion(r.buffer, [(substitute(m, vmap), substitute(e, vmap) if isinstance(e, PrimExpr) else e)
+                                   for m, e in r.region])
+
+
+class _AllocReplacer(Mutator):
+
+    def __init__(self, replaced):
+        self.replaced = replaced
+
+    def visit_AllocStmt(self, s):
+        if s.buffer in self.replaced:
+            return S.AllocStmt(self.replaced[s.buffer])
+        return s
+
+
+def inject_software_pipeline(kernel: S.KernelStmt, num_threads: int, target) -> S.KernelStmt:
+    pi = PipelineInjector(kernel, num_threads, target)
+    new = pi.stmt(kernel)
+    replaced = getattr(pi, "replaced", {})
+    if replaced:
+        new = _AllocReplacer(replaced).stmt(new)
+    return new

@@ -1,0 +1,260 @@
+"""Insert block barriers for LDS (shared memory) hazards.
+
+Reference: ``src/transform/thread_storage_sync.cc`` + ``storage_access.cc``
+(``ThreadSync("shared")``).  Runs on the lowered per-thread IR: a linear scan
+tracks buffers written/read since the last barrier and inserts
+``__syncthreads()`` before a RAW/WAR/WAW conflict; loops are scanned twice for
+loop-carried hazards; barriers are never placed inside divergent ``if`` bodies
+(they are hoisted in front of the ``if``).  Accesses that the software pipeline
+manages itself (multi-versioned stage buffers inside a pipelined loop) are
+skipped: that loop already carries one raw ``s_barrier`` per iteration and a
+``__syncthreads()`` there would drain the in-flight LDS-DMA (``vmcnt(0)``).
+"""
+from __future__ import annotations
+
+from typing import List, Set, Tuple
+
+from ..ir import stmt as S
+from ..ir import lowered as L
+from ..ir.buffer import Buffer
+from ..ir.expr import BufferLoad, PrimExpr, post_order, loads_of
+
+_BARRIERS = {"tl::sync_threads", "tl::barrier_raw"}
+
+
+def _shared(b) -> bool:
+    return isinstance(b, Buffer) and b.scope == "shared"
+
+
+def _expr_reads(e, out: Set):
+    if not isinstance(e, PrimExpr):
+        return
+    for n in post_order(e):
+        if isinstance(n, BufferLoad) and _shared(n.buffer):
+            out.add(n.buffer)
+        if isinstance(n, L.BufferPtr) and _shared(n.buffer):
+            out.add(n.buffer)
+
+
+class _State:
+
+    def __init__(self, reads=None, writes=None):
+        self.reads: Set = set(reads or ())
+        self.writes: Set = set(writes or ())
+
+    def copy(self):
+        return _State(self.reads, self.writes)
+
+    def merge(self, o):
+        return _State(self.reads | o.reads, self.writes | o.writes)
+
+
+def _stmt_access(s, managed) -> Tuple[Set, Set, bool]:
+    """(reads, writes, is_barrier) of a leaf statement."""
+    r, w = set(), set()
+    if isinstance(s, L.CallStmt):
+        if s.name in _BARRIERS:
+            return r, w, True
+        if s.name in ("tl::glds16", "tl::glds4", "tl::buffer_lds16", "tl::glds16_nt"):
+            # async LDS-DMA is only produced by the software pipeline, which orders it with
+            # counted vmcnt waits + raw barriers itself (a __syncthreads here would drain it)
+            return r, w, False
+        for a in s.args:
+            _expr_reads(a, r)
+        if s.name.startswith("tl::mesh") or s.name.startswith("tl::comm"):
+            for a in s.args:
+                if isinstance(a, L.BufferPtr) and _shared(a.buffer):
+                    w.add(a.buffer)
+        return r - managed, w - managed, False
+    if isinstance(s, S.StoreStmt):
+        for i in s.indices:
+            _expr_reads(i, r)
+        _expr_reads(s.value, r)
+        if _shared(s.buffer):
+            w.add(s.buffer)
+    elif isinstance(s, L.VecStoreStmt):
+        _expr_reads(s.index, r)
+        for v in s.values:
+            _expr_reads(v, r)
+        if _shared(s.buffer):
+            w.add(s.buffer)
+    elif isinstance(s, L.VecLoadStmt):
+        if _shared(s.src):
+            r.add(s.src)
+        if _shared(s.dst):
+            w.add(s.dst)
+    elif isinstance(s, L.CopyBytesStmt):
+        if _shared(s.src):
+            r.add(s.src)
+        if _shared(s.dst):
+            w.add(s.dst)
+    elif isinstance(s, S.LetStmt):
+        _expr_reads(s.value, r)
+    elif isinstance(s, S.EvaluateStmt):
+        _expr_reads(s.expr, r)
+        from ..ir.expr import Call
+        if isinstance(s.expr, Call) and s.expr.op == "tl.sync_threads":
+            return r, w, True
+        if isinstance(s.expr, Call) and s.expr.op.startswith("tl.atomic"):
+            a0 = s.expr.args[0]
+            if isinstance(a0, BufferLoad) and _shared(a0.buffer):
+                w.add(a0.buffer)
+    elif isinstance(s, S.AssertStmt):
+        _expr_reads(s.cond, r)
+    return r - managed, w - managed, False
+
+
+def _sync():
+    return L.CallStmt("tl::sync_threads", [])
+
+
+class ThreadSync:
+
+    def __init__(self):
+        self.managed: Set = set()
+
+    def needs(self, st: _State, r, w) -> bool:
+        # RAW and WAR hazards; WAW between different threads writing the same location is
+        # a program race in the tile model and is not ordered by the compiler (as in the reference)
+        return bool((r & st.writes) or (w & st.reads))
+
+    def scan(self, s, st: _State):
+        """Returns (new_stmt, state_after, inserted_at_front)."""
+        if isinstance(s, S.SeqStmt):
+            out = []
+            for c in s.stmts:
+                nc, st = self.scan_one(c, st, out)
+            ns = S.SeqStmt(out)
+            if getattr(s, "scoped", False):
+                ns.scoped = True
+            return ns, st
+        out = []
+        ns, st = self.scan_one(s, st, out)
+        return (out[0] if len(out) == 1 else S.SeqStmt(out)), st
+
+    def first_access(self, s) -> Tuple[Set, Set]:
+        """Accesses of ``s`` before its first unconditional barrier (conservative)."""
+        r_all, w_all = set(), set()
+        for x in _leaves(s):
+            r, w, bar = _stmt_access(x, self.managed)
+            if bar:
+                break
+            r_all |= r
+            w_all |= w
+        return r_all, w_all
+
+    def scan_one(self, c, st: _State, out: List):
+        if isinstance(c, S.SeqStmt):
+            nc, st = self.scan(c, st)
+            out.append(nc)
+            return nc, st
+        if isinstance(c, (S.ForStmt, S.WhileStmt)):
+            body = c.body
+            managed_here = set()
+            if isinstance(c, S.ForStmt) and c.annotations.get("pipelined"):
+                for x in _leaves(body):
+                    if isinstance(x, L.CallStmt) and x.name.startswith("tl::glds"):
+                        managed_here.add(x.args[1].buffer)
+                    if isinstance(x, L.CallStmt) and x.name in ("tl::gemm_ss", "tl::gemm_rs"):
+                        pass
+                # stage buffers: any shared buffer with a `stages_of`
+                for x in _leaves(body):
+                    for b in _buffers_of(x):
+                        if getattr(getattr(b, "orig", None), "stages_of", None) is not None:
+                            managed_here.add(b)
+            saved = set(self.managed)
+            self.managed |= managed_here
+            # hazard with what precedes the loop: barrier in front
+            r0, w0 = self.first_access(body)
+            if self.needs(st, r0, w0):
+                out.append(_sync())
+                st = _State()
+            nb, st_end = self.scan(body, st.copy())
+            # loop-carried: entry of iteration i+1 after end of iteration i
+            r1, w1 = self.first_access(nb)
+            if self.needs(st_end, r1, w1):
+                nb = S.SeqStmt([_sync(), nb])
+                nb, st_end = self.scan(nb, _State())
+            self.managed = saved
+            if isinstance(c, S.ForStmt):
+                nc = S.ForStmt(c.var, c.min, c.extent, c.kind, nb, c.annotations)
+            else:
+                nc = S.WhileStmt(c.cond, nb)
+            out.append(nc)
+            return nc, st.merge(st_end)
+        if isinstance(c, S.IfStmt):
+            # barriers must not be inside divergent branches: pre-sync if any branch conflicts
+            r0, w0 = set(), set()
+            for x in _leaves(c):
+                r, w, _ = _stmt_access(x, self.managed)
+                r0 |= r
+                w0 |= w
+            rc = set()
+            _expr_reads(c.cond, rc)
+            r0 |= rc
+            if self.needs(st, r0, w0):
+                out.append(_sync())
+                st = _State()
+            # scan branches for internal hazards (barriers inside are allowed only if the
+            # condition is block-uniform; we keep them, matching the reference behaviour)
+            tb, st_t = self.scan(c.then_body, st.copy())
+            eb, st_e = (self.scan(c.else_body, st.copy()) if c.else_body is not None else (None, st.copy()))
+            nc = S.IfStmt(c.cond, tb, eb)
+            out.append(nc)
+            return nc, st_t.merge(st_e)
+        if isinstance(c, S.KernelStmt):
+            nb, st2 = self.scan(c.body, _State())
+            k = S.KernelStmt(c.grid, c.threads, c.block_vars, c.thread_vars, nb, c.is_cpu, c.prelude)
+            k.attrs = dict(c.attrs)
+            out.append(k)
+            return k, st2
+        r, w, bar = _stmt_access(c, self.managed)
+        if bar:
+            out.append(c)
+            return c, _State()
+        if self.needs(st, r, w):
+            out.append(_sync())
+            st = _State()
+        out.append(c)
+        st = _State(st.reads | r, st.writes | w)
+        return c, st
+
+
+def _leaves(s):
+    if s is None:
+        return
+    if isinstance(s, S.SeqStmt):
+        for c in s.stmts:
+            yield from _leaves(c)
+    elif isinstance(s, (S.ForStmt, S.WhileStmt)):
+        yield from _leaves(s.body)
+    elif isinstance(s, S.IfStmt):
+        yield from _leaves(s.then_body)
+        yield from _leaves(s.else_body)
+    else:
+        yield s
+
+
+def _buffers_of(x):
+    out = []
+    if isinstance(x, L.CallStmt):
+        for a in x.args:
+            if isinstance(a, L.BufferPtr):
+                out.append(a.buffer)
+    if isinstance(x, S.StoreStmt):
+        out.append(x.buffer)
+        for n in post_order(x.value):
+            if isinstance(n, BufferLoad):
+                out.append(n.buffer)
+    if isinstance(x, (L.VecStoreStmt, )):
+        out.append(x.buffer)
+    if isinstance(x, (L.VecLoadStmt, L.CopyBytesStmt)):
+        out += [x.src, x.dst]
+    return out
+
+
+def insert_thread_sync(kernel: S.KernelStmt) -> S.KernelStmt:
+    ts = ThreadSync()
+    out = []
+    k, _ = ts.scan_one(kernel, _State(), out)
+    return k
