@@ -442,6 +442,18 @@ def binop(op: str, a, b) -> PrimExpr:
             return a
         if structural_equal(a, b) and not rdt.is_float:
             return const(0, rdt)
+        if not rdt.is_float:
+            la, lb = _linear_form(a), _linear_form(b)
+            if la is not None and lb is not None:
+                diff = dict(la)
+                for k, (t, c) in lb.items():
+                    if k in diff:
+                        diff[k] = (diff[k][0], diff[k][1] - c)
+                    else:
+                        diff[k] = (t, -c)
+                diff = {k: v for k, v in diff.items() if v[1] != 0}
+                if all(k == "__const__" for k in diff):
+                    return const(diff.get("__const__", (None, 0))[1], rdt)
     elif op == "*":
         if av == 1:
             return b
@@ -477,6 +489,53 @@ def binop(op: str, a, b) -> PrimExpr:
         if bv is not None:
             return const(True) if bv else a
     return BinOp(op, a, b, rdt)
+
+
+def _term_key(e) -> str:
+    from .printer import Printer
+    p = Printer()
+    p.names = _IdNames()
+    return p.e(e)
+
+
+class _IdNames:
+    """Name vars by identity so structurally-equal keys mean the same variables."""
+
+    def __call__(self, obj, base):
+        return f"{base}#{id(obj)}"
+
+
+def _linear_form(e, depth=0):
+    """{key: (term, coeff)} with '__const__' for the constant, for +,-,*const trees (ints only)."""
+    if depth > 24:
+        return None
+    if isinstance(e, IntImm):
+        return {"__const__": (None, e.value)}
+    if isinstance(e, BinOp) and e.op in ("+", "-"):
+        la, lb = _linear_form(e.a, depth + 1), _linear_form(e.b, depth + 1)
+        if la is None or lb is None:
+            return None
+        out = dict(la)
+        sign = 1 if e.op == "+" else -1
+        for k, (t, c) in lb.items():
+            if k in out:
+                out[k] = (out[k][0], out[k][1] + sign * c)
+            else:
+                out[k] = (t, sign * c)
+        return out
+    if isinstance(e, BinOp) and e.op == "*":
+        cb, ca = const_value(e.b), const_value(e.a)
+        if cb is not None and isinstance(cb, int):
+            la = _linear_form(e.a, depth + 1)
+            return None if la is None else {k: (t, c * cb) for k, (t, c) in la.items()}
+        if ca is not None and isinstance(ca, int):
+            lb = _linear_form(e.b, depth + 1)
+            return None if lb is None else {k: (t, c * ca) for k, (t, c) in lb.items()}
+    if isinstance(e, (Var, BinOp, Cast, Call, BufferLoad, Select, UnOp)):
+        if not e.dtype.is_int:
+            return None
+        return {_term_key(e): (e, 1)}
+    return None
 
 
 def _unify(a: PrimExpr, b: PrimExpr):

@@ -1,0 +1,82 @@
+"""Kernel timing (reference ``tilelang/profiler/bench.py:63-204``).
+
+MI355X specifics: the cache flush before every timed launch writes a 512 MiB buffer so
+that both the per-XCD L2s (8 x 4 MiB) and the 256 MiB Infinity Cache are evicted
+(the reference flushes 256 MB, sized for NVIDIA L2).  Timing uses HIP events on the
+current stream; ``backend="profiler"`` uses torch.profiler device time (rocprofiler).
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional
+
+_FLUSH = {}
+
+
+def _flush_buffer(device):
+    import torch
+    b = _FLUSH.get(device)
+    if b is None:
+        b = torch.empty(512 * 1024 * 1024 // 4, dtype=torch.int32, device=device)
+        _FLUSH[device] = b
+    return b
+
+
+def do_bench(fn: Callable, warmup: float = 25, rep: float = 100, _n_warmup: int = 0, _n_repeat: int = 0,
+             quantiles: Optional[List[float]] = None, fast_flush: bool = True, return_mode: str = "mean",
+             backend: str = "event", flush_l2: bool = True) -> float:
+    """Median/mean runtime of ``fn`` in milliseconds."""
+    import torch
+    assert return_mode in ("min", "max", "mean", "median")
+    if backend in ("cupti", "profiler"):
+        return _bench_profiler(fn, warmup, rep)
+    fn()
+    torch.cuda.synchronize()
+    dev = torch.cuda.current_device()
+    cache = _flush_buffer(dev) if flush_l2 else None
+    # estimate
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(5):
+        if cache is not None:
+            cache.zero_()
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    est = max(s.elapsed_time(e) / 5, 1e-4)
+    n_warmup = _n_warmup or max(1, int(warmup / est))
+    n_repeat = _n_repeat or max(1, int(rep / est))
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(n_repeat)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(n_repeat)]
+    for _ in range(n_warmup):
+        fn()
+    for i in range(n_repeat):
+        if cache is not None:
+            cache.zero_()
+        starts[i].record()
+        fn()
+        ends[i].record()
+    torch.cuda.synchronize()
+    times = torch.tensor([a.elapsed_time(b) for a, b in zip(starts, ends)], dtype=torch.float)
+    if quantiles is not None:
+        ret = torch.quantile(times, torch.tensor(quantiles, dtype=torch.float)).tolist()
+        return ret[0] if len(ret) == 1 else ret
+    return getattr(torch, return_mode)(times).item()
+
+
+def _bench_profiler(fn, warmup, rep):
+    import torch
+    from torch.profiler import profile, ProfilerActivity
+    fn()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    n = 20
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+    total = 0.0
+    for evt in prof.key_averages():
+        total += evt.device_time_total if hasattr(evt, "device_time_total") else evt.cuda_time_total
+    return total / n / 1e3
