@@ -260,7 +260,11 @@ class _IterRewriter(Mutator):
             return BufferLoad(self.ctx.local_of(b), [IntImm(li)])
         idx2 = [substitute(i, self.vmap) for i in idx]
         idx2 = [transform(i, self._load_sub) for i in idx2]
-        return BufferLoad(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx2)])
+        ld = BufferLoad(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx2)])
+        g = safe_guard(self.ctx, b, idx2)
+        if g is not None:
+            return select(g, ld, const(0, b.dtype))
+        return ld
 
     def _load_sub(self, n):
         return None
@@ -286,7 +290,9 @@ class _IterRewriter(Mutator):
             li = self.res.local_index(b, s.indices, self.r)
             return S.StoreStmt(self.ctx.local_of(b), [IntImm(li)], val)
         idx = [self.expr(i) for i in s.indices]
-        return S.StoreStmt(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)], val)
+        st = S.StoreStmt(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)], val)
+        g = safe_guard(self.ctx, b, idx)
+        return S.IfStmt(g, st) if g is not None else st
 
     def visit_LetStmt(self, s):
         return S.LetStmt(s.var, self.expr(s.value))
@@ -327,10 +333,35 @@ def _const_diff(a: PrimExpr, b: PrimExpr, probe_vars: List[Var]) -> Optional[int
     return int(vals) if vals is not None else None
 
 
+def safe_guard(ctx: LowerCtx, b: Buffer, idx) -> Optional[PrimExpr]:
+    """Bounds condition for a global access that cannot be proven in range (ragged tiles,
+    dynamic shapes); None when every index is provably inside the tensor."""
+    if b.scope != "global" or ctx.pass_cfg.get("tl.disable_safe_memory_legalize"):
+        return None
+    cond = None
+    for i, s in zip(idx, b.shape):
+        bd = bound(i, ctx.ranges)
+        sv = as_int(s)
+        if bd is not None and sv is not None and bd[0] >= 0 and bd[1] < sv:
+            continue
+        c = binop("<", i, s)
+        if as_int(c) == 1:
+            continue
+        cond = c if cond is None else logical_and(cond, c)
+    return cond
+
+
 def vectorize_group(ctx: LowerCtx, stmts: List[S.Stmt], known_div) -> Optional[List[S.Stmt]]:
     """``stmts[i]`` are the per-element copies (i = 0..W-1) of a single-store body.  If the
     stores (and the loads feeding them) are contiguous and aligned, emit vector accesses."""
     W = len(stmts)
+    from ..ir.expr import structural_equal
+    if W > 1 and all(isinstance(s, S.IfStmt) and s.else_body is None for s in stmts):
+        c0 = stmts[0].cond
+        if all(structural_equal(s.cond, c0) for s in stmts):
+            inner = vectorize_group(ctx, [s.then_body for s in stmts], known_div)
+            return [S.IfStmt(c0, S.SeqStmt(inner))] if inner is not None else None
+        return None
     if W == 1 or not all(isinstance(s, S.StoreStmt) for s in stmts):
         return None
     b = stmts[0].buffer
@@ -1150,7 +1181,9 @@ class _SimtRewriter(Mutator):
                 return BufferLoad(b, [b.offset_of(idx)] if b.ndim != 1 else idx)
             if b.scope == "fragment":
                 raise LoweringError(f"fragment {b.name} in a non-fragment T.Parallel nest")
-            return BufferLoad(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)])
+            ld = BufferLoad(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)])
+            g = safe_guard(self.ctx, b, idx)
+            return select(g, ld, const(0, b.dtype)) if g is not None else ld
         return None
 
     def expr(self, e):
@@ -1164,7 +1197,9 @@ class _SimtRewriter(Mutator):
         idx = [self.expr(i) for i in s.indices]
         if b.scope in ("local", "var"):
             return S.StoreStmt(b, [b.offset_of(idx)] if b.ndim != 1 else idx, val)
-        return S.StoreStmt(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)], val)
+        st = S.StoreStmt(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)], val)
+        g = safe_guard(self.ctx, b, idx)
+        return S.IfStmt(g, st) if g is not None else st
 
 
 def _sample_threads(T):
