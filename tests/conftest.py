@@ -28,3 +28,7 @@ def _seed():
     except ImportError:
         pass
     yield
+for _p in ("gemm_fp8", "deepseek_mla"):
+    _d = os.path.join(ROOT, "examples", _p)
+    if _d not in sys.path:
+        sys.path.insert(0, _d)

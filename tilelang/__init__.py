@@ -47,3 +47,5 @@ def __getattr__(name):
         from .utils.tensor import TensorSupplyType
         return TensorSupplyType
     raise AttributeError(name)
+
+from .transform.pass_config import PassConfigKey  # noqa: E402,F401

@@ -2,7 +2,7 @@
 
 Reference: ``tilelang/engine/lower.py:217-272`` and the pass pipeline in
 ``tilelang/engine/phase.py`` (``PreLowerSemanticCheck`` -> ``LowerAndLegalize`` ->
-``OptimizeForTarget``).  The MI355X pipeline:
+``OptimizeForTarget``).  The MI355X pipeline, run per ``T.Kernel`` of the program:
 
   1. semantic checks (nested-loop / fragment-loop legality)
   2. layout inference (fragments + LDS swizzles)              transform/layout_inference.py
@@ -11,6 +11,10 @@ Reference: ``tilelang/engine/lower.py:217-272`` and the pass pipeline in
   5. barrier insertion                                         transform/thread_sync.py
   6. LDS arena planning (one __shared__ array, <=160 KiB)       transform/lds_plan.py
   7. code generation                                           codegen/hip.py
+
+A program may contain several ``T.Kernel`` scopes (e.g. split-KV attention + combine):
+each becomes its own gfx950 kernel and the runtime launches them in program order on the
+current stream.
 """
 from __future__ import annotations
 
@@ -22,7 +26,7 @@ from ..ir import stmt as S
 from ..ir.buffer import Buffer
 from ..ir.expr import PrimExpr, Var
 from ..utils.target import Target, determine_target
-from ..analysis.checks import semantic_check
+from ..analysis.checks import semantic_check, SemanticError
 from ..transform.layout_inference import infer_layouts
 from ..transform.pipeline import inject_software_pipeline
 from ..transform.lower_tile_op import lower_tile_ops
@@ -32,66 +36,115 @@ from ..codegen.hip import generate, KernelSource
 
 
 @dataclass
+class DeviceKernel:
+    source: str
+    name: str
+    grid: list
+    block: list
+    lds_bytes: int
+    params: list
+    lowered_ir: Optional[S.Stmt] = None
+    layout_info: Dict[str, str] = field(default_factory=dict)
+
+
+@dataclass
 class CompiledArtifact:
     """Reference ``tilelang/engine/param.py:106-116``."""
     func: S.PrimFunc
     target: Target
-    kernel_source: str
-    kernel_name: str
-    params: list
-    grid: list
-    block: list
-    lds_bytes: int
+    kernels: List[DeviceKernel]
     is_cpu: bool
-    lowered_ir: Optional[S.Stmt] = None
     timings: Dict[str, float] = field(default_factory=dict)
-    layout_info: Dict[str, str] = field(default_factory=dict)
+
+    # single-kernel conveniences (first kernel)
+    @property
+    def kernel_source(self) -> str:
+        if len(self.kernels) == 1:
+            return self.kernels[0].source
+        return "\n// ---- next kernel ----\n".join(k.source for k in self.kernels)
+
+    @property
+    def kernel_name(self) -> str:
+        return self.kernels[0].name
+
+    @property
+    def params(self):
+        return self.kernels[0].params
+
+    @property
+    def grid(self):
+        return self.kernels[0].grid
+
+    @property
+    def block(self):
+        return self.kernels[0].block
+
+    @property
+    def lds_bytes(self):
+        return max(k.lds_bytes for k in self.kernels)
+
+    @property
+    def lowered_ir(self):
+        return self.kernels[0].lowered_ir
+
+    @property
+    def layout_info(self):
+        out = {}
+        for k in self.kernels:
+            out.update(k.layout_info)
+        return out
 
 
-def _find_kernel(body) -> S.KernelStmt:
+def _find_kernels(body) -> List[S.KernelStmt]:
     ks = [s for s in S.walk(body) if isinstance(s, S.KernelStmt)]
-    if len(ks) != 1:
-        raise ValueError(f"a prim_func must contain exactly one T.Kernel launch (found {len(ks)})")
-    return ks[0]
+    if not ks:
+        raise SemanticError("a prim_func must contain at least one T.Kernel launch")
+    return ks
+
+
+def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timings):
+    if target.kind == "cpu" and not kernel.is_cpu:
+        # a GPU-style kernel compiled for the CPU target runs one "thread" per block
+        kernel = S.KernelStmt(kernel.grid, [1], kernel.block_vars, kernel.thread_vars, kernel.body, True,
+                              kernel.prelude)
+    if target.kind == "hip" and kernel.num_threads % 64 != 0:
+        raise ValueError(f"T.Kernel threads={kernel.threads}: the block size must be a multiple of the 64-lane "
+                         f"CDNA wavefront")
+    T = kernel.num_threads if target.kind == "hip" else 1
+    semantic_check(func, kernel)
+    t = time.perf_counter()
+    li = infer_layouts(S.PrimFunc(func.name, func.params, kernel, func.attrs), T, target)
+    timings["layout_inference"] = timings.get("layout_inference", 0) + time.perf_counter() - t
+    t = time.perf_counter()
+    kernel = inject_software_pipeline(kernel, T, target)
+    timings["pipeline"] = timings.get("pipeline", 0) + time.perf_counter() - t
+    t = time.perf_counter()
+    lk, ctx = lower_tile_ops(kernel, target, cfg)
+    timings["lower_tile_op"] = timings.get("lower_tile_op", 0) + time.perf_counter() - t
+    if target.kind == "hip" and not cfg.get("tl.disable_thread_storage_sync", False):
+        lk = insert_thread_sync(lk)
+    offsets, total = plan_lds(lk)
+    t = time.perf_counter()
+    ks: KernelSource = generate(func, lk, target, offsets, total, name, cfg)
+    timings["codegen"] = timings.get("codegen", 0) + time.perf_counter() - t
+    layout_info = {b.name: repr(lay) for b, lay in li.frag.items()}
+    return DeviceKernel(ks.source, ks.kernel_name, ks.grid, ks.block, ks.lds_bytes, ks.params, lk, layout_info)
 
 
 def lower(func: S.PrimFunc, target="auto", target_host=None, pass_configs: Optional[dict] = None,
           enable_host_codegen=False, enable_device_compile=False, runtime_only=False) -> CompiledArtifact:
     t0 = time.perf_counter()
     target = determine_target(target)
-    cfg = dict(pass_configs or {})
-    kernel = _find_kernel(func.body)
-    if target.kind == "cpu" and not kernel.is_cpu:
-        # a GPU-style kernel compiled for the CPU target runs one "thread" per block
-        kernel = S.KernelStmt(kernel.grid, [1], kernel.block_vars, kernel.thread_vars, kernel.body, True,
-                              kernel.prelude)
-    if kernel.is_cpu and target.kind != "cpu":
+    cfg = {str(k): v for k, v in dict(pass_configs or {}).items()}
+    kernels = _find_kernels(func.body)
+    if any(k.is_cpu for k in kernels) and target.kind != "cpu":
         target = Target("cpu", "host", target.mesh)
-    if target.kind == "hip" and kernel.num_threads % 64 != 0:
-        raise ValueError(f"T.Kernel threads={kernel.threads}: the block size must be a multiple of the 64-lane "
-                         f"CDNA wavefront")
     if cfg.get("tl.disable_glds"):
         target.disable_glds = True
-    T = kernel.num_threads if target.kind == "hip" else 1
-    timings = {}
-    semantic_check(func, kernel)
-    t = time.perf_counter()
-    li = infer_layouts(S.PrimFunc(func.name, func.params, kernel, func.attrs), T, target)
-    timings["layout_inference"] = time.perf_counter() - t
-    t = time.perf_counter()
-    kernel = inject_software_pipeline(kernel, T, target)
-    timings["pipeline"] = time.perf_counter() - t
-    t = time.perf_counter()
-    lk, ctx = lower_tile_ops(kernel, target, cfg)
-    timings["lower_tile_op"] = time.perf_counter() - t
-    if target.kind == "hip" and not cfg.get("tl.disable_thread_storage_sync", False):
-        lk = insert_thread_sync(lk)
-    offsets, total = plan_lds(lk)
-    t = time.perf_counter()
-    ks: KernelSource = generate(func, lk, target, offsets, total, func.name + "_kernel", cfg)
-    timings["codegen"] = time.perf_counter() - t
+    timings: Dict[str, float] = {}
+    dks = []
+    for i, k in enumerate(kernels):
+        name = f"{func.name}_kernel" if i == 0 else f"{func.name}_kernel_{i}"
+        dks.append(_lower_one(func, k, target, cfg, name, timings))
     timings["total"] = time.perf_counter() - t0
-    layout_info = {b.name: repr(lay) for b, lay in li.frag.items()}
-    return CompiledArtifact(func=func, target=target, kernel_source=ks.source, kernel_name=ks.kernel_name,
-                            params=ks.params, grid=ks.grid, block=ks.block, lds_bytes=ks.lds_bytes,
-                            is_cpu=ks.is_cpu, lowered_ir=lk, timings=timings, layout_info=layout_info)
+    return CompiledArtifact(func=func, target=target, kernels=dks, is_cpu=target.kind == "cpu", timings=timings)

@@ -166,4 +166,85 @@ TL_DEVICE void gemm_rs(const T* __restrict__ a_regs, const T* __restrict__ B, fl
   }
 }
 
+// ---------------------------------------------------------------------------
+// 8-bit (OCP fp8 e4m3 / e5m2) GEMM, both operands K-contiguous ([M][K] and [N][K] in LDS).
+// K % 128 == 0: v_mfma_scale_f32_16x16x128_f8f6f4 with unit e8m0 scales (2x the bf16 MFMA
+//               rate); each lane feeds 32 consecutive k (two ds_read_b128).  The operand
+//               k-assignment only has to agree between A and B (verified on gfx950 with exact
+//               integer data: csrc/probes/mfma_fp8_layout.hip).
+// otherwise:    v_mfma_f32_16x16x32_{fp8,bf8}_{fp8,bf8}, 8 consecutive k per lane (ds_read_b64).
+// ---------------------------------------------------------------------------
+template <typename T> struct fp8_fmt;
+template <> struct fp8_fmt<fp8_e4_t> { static constexpr int code = 0; };
+template <> struct fp8_fmt<fp8_e5_t> { static constexpr int code = 1; };
+
+template <typename TA, typename TB> TL_DEVICE floatx4 mma_f8_32(long a, long b, floatx4 c) {
+  if constexpr (fp8_fmt<TA>::code == 0 && fp8_fmt<TB>::code == 0)
+    return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0);
+  else if constexpr (fp8_fmt<TA>::code == 0)
+    return __builtin_amdgcn_mfma_f32_16x16x32_fp8_bf8(a, b, c, 0, 0, 0);
+  else if constexpr (fp8_fmt<TB>::code == 0)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf8_fp8(a, b, c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf8_bf8(a, b, c, 0, 0, 0);
+}
+
+template <int COLS, uint32_t SWZ>
+TL_DEVICE intx8 ld_rows32_b8(const uint8_t* base, int row, int col) {
+  intx4 lo = *reinterpret_cast<const intx4*>(base + swz_offset<uint8_t, COLS, SWZ>(row, col));
+  intx4 hi = *reinterpret_cast<const intx4*>(base + swz_offset<uint8_t, COLS, SWZ>(row, col + 16));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int COLS, uint32_t SWZ>
+TL_DEVICE long ld_rows8_b8(const uint8_t* base, int row, int col) {
+  return *reinterpret_cast<const long*>(base + swz_offset<uint8_t, COLS, SWZ>(row, col));
+}
+
+// A: [M][K] (K contiguous), B: [N][K] (K contiguous)
+template <typename TA, typename TB, int M, int N, int K, int WARP_M, int WARP_N, int A_COLS, uint32_t SWZ_A,
+          int B_COLS, uint32_t SWZ_B>
+TL_DEVICE void gemm_ss_f8(const TA* __restrict__ A_, const TB* __restrict__ B_, float* __restrict__ C) {
+  constexpr int WM = M / WARP_M, WN = N / WARP_N;
+  constexpr int M_REP = WM / 16, N_REP = WN / 16;
+  const uint8_t* A = reinterpret_cast<const uint8_t*>(A_);
+  const uint8_t* B = reinterpret_cast<const uint8_t*>(B_);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wm = wave / WARP_N, wn = wave % WARP_N;
+  const int r = lane & 15, g = lane >> 4;
+  floatx4* acc = reinterpret_cast<floatx4*>(C);
+  if constexpr (K % 128 == 0) {
+#pragma unroll
+    for (int kk = 0; kk < K / 128; ++kk) {
+      intx8 a[M_REP], b[N_REP];
+#pragma unroll
+      for (int mi = 0; mi < M_REP; ++mi) a[mi] = ld_rows32_b8<A_COLS, SWZ_A>(A, wm * WM + mi * 16 + r, kk * 128 + 32 * g);
+#pragma unroll
+      for (int ni = 0; ni < N_REP; ++ni) b[ni] = ld_rows32_b8<B_COLS, SWZ_B>(B, wn * WN + ni * 16 + r, kk * 128 + 32 * g);
+#pragma unroll
+      for (int mi = 0; mi < M_REP; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < N_REP; ++ni)
+          acc[mi * N_REP + ni] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              b[ni], a[mi], acc[mi * N_REP + ni], fp8_fmt<TB>::code, fp8_fmt<TA>::code, 0, 127, 0, 127);
+    }
+  } else {
+    static_assert(K % 32 == 0, "fp8 MFMA needs K % 32 == 0");
+#pragma unroll
+    for (int kk = 0; kk < K / 32; ++kk) {
+      long a[M_REP], b[N_REP];
+#pragma unroll
+      for (int mi = 0; mi < M_REP; ++mi) a[mi] = ld_rows8_b8<A_COLS, SWZ_A>(A, wm * WM + mi * 16 + r, kk * 32 + 8 * g);
+#pragma unroll
+      for (int ni = 0; ni < N_REP; ++ni) b[ni] = ld_rows8_b8<B_COLS, SWZ_B>(B, wn * WN + ni * 16 + r, kk * 32 + 8 * g);
+#pragma unroll
+      for (int mi = 0; mi < M_REP; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < N_REP; ++ni)
+          acc[mi * N_REP + ni] = mma_f8_32<TB, TA>(b[ni], a[mi], acc[mi * N_REP + ni]);
+    }
+  }
+}
+
 }  // namespace tl

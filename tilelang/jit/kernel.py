@@ -90,28 +90,32 @@ class JITKernel:
 
     # -- compilation -------------------------------------------------------------------
     def _compile(self):
+        """One code object (gfx950) or shared object (cpu) per device kernel of the program."""
         a = self.artifact
-        if a.is_cpu:
-            return _cache.compile_cpu_cached(a.kernel_source, self.compile_flags, self.verbose)
-        return _cache.compile_hip_cached(a.kernel_source, self.compile_flags, self.verbose)
+        out = []
+        for dk in a.kernels:
+            if a.is_cpu:
+                out.append(_cache.compile_cpu_cached(dk.source, self.compile_flags, self.verbose))
+            else:
+                out.append(_cache.compile_hip_cached(dk.source, self.compile_flags, self.verbose))
+        return out
 
-    def _param_specs(self):
-        a = self.artifact
+    def _param_specs(self, dk, with_outputs: bool):
         symtab = {}
-        for p in a.params:
+        for p in dk.params:
             if p["kind"] == "dyn":
                 symtab[p["var"]] = len(symtab)
-        for p in a.params:
+        for p in dk.params:
             if p["kind"] == "scalar" and p["var"].dtype.is_int:
                 symtab[p["var"]] = len(symtab)
         specs = []
-        for i, p in enumerate(a.params):
+        for i, p in enumerate(dk.params):
             d = dict(kind={"buffer": 0, "scalar": 1, "dyn": 2}.get(p["kind"], 1), name=p["name"], scalar_type=0,
                      nbytes=8, is_float=False, shape=[], strides=[], is_output=False, sym=-1)
             if p["kind"] == "buffer":
                 b: Buffer = p["buffer"]
                 d["scalar_type"] = _scalar_type_code(b.dtype)
-                d["is_output"] = (b.param_index in self.out_idx)
+                d["is_output"] = with_outputs and (b.param_index in self.out_idx)
                 for s in b.shape:
                     v = as_int(s)
                     if v is not None:
@@ -138,36 +142,60 @@ class JITKernel:
                 d["nbytes"] = p.get("nbytes", 8)
                 d["is_float"] = False
             specs.append(d)
-        grid = [_prog(g, symtab) for g in a.grid]
+        grid = [_prog(g, symtab) for g in dk.grid]
         return specs, len(symtab), grid
 
     @property
-    def runtime(self):
+    def runtimes(self):
         if self._rt is None:
             with self._lock:
                 if self._rt is None:
                     from .. import _native
                     rt = _native.runtime()
-                    specs, nsyms, grid = self._param_specs()
                     a = self.artifact
-                    code = self.code.encode() if isinstance(self.code, str) else self.code
-                    self._rt = rt.Kernel(code, a.kernel_name, a.is_cpu, specs, nsyms, grid,
-                                         [int(b) for b in a.block], int(a.lds_bytes), a.kernel_name)
+                    rts = []
+                    for i, (dk, code) in enumerate(zip(a.kernels, self.code)):
+                        specs, nsyms, grid = self._param_specs(dk, with_outputs=(i == 0))
+                        blob = code.encode() if isinstance(code, str) else code
+                        rts.append(rt.Kernel(blob, dk.name, a.is_cpu, specs, nsyms, grid, [int(b) for b in dk.block],
+                                             int(dk.lds_bytes), dk.name))
+                    self._rt = rts
         return self._rt
+
+    @property
+    def runtime(self):
+        return self.runtimes[0]
 
     # -- execution -----------------------------------------------------------------------
     def __call__(self, *args, **kwargs):
         if kwargs:
-            names = [p.name for p in self.func.params]
+            names = [p.name for i, p in enumerate(self.func.params) if i not in self.out_idx]
             full = list(args)
             for n in names[len(args):]:
                 if n in kwargs:
                     full.append(kwargs[n])
             args = tuple(full)
-        return self.runtime(*args)
+        rts = self.runtimes
+        out = rts[0](*args)
+        if len(rts) == 1:
+            return out
+        # later kernels of the program see the outputs of the first as ordinary arguments
+        outs = list(out) if isinstance(out, tuple) else ([out] if out is not None else [])
+        full, ai, oi = [], 0, 0
+        for i, p in enumerate(self.func.params):
+            if i in self.out_idx:
+                full.append(outs[oi])
+                oi += 1
+            else:
+                full.append(args[ai])
+                ai += 1
+        for r in rts[1:]:
+            r(*full)
+        return out
 
     def set_validation(self, enabled: bool):
-        self.runtime.set_validate(enabled)
+        for r in self.runtimes:
+            r.set_validate(enabled)
 
     # -- introspection (reference API) -----------------------------------------------------
     def get_kernel_source(self) -> str:
@@ -197,9 +225,9 @@ class JITKernel:
     def export_library(self, path: str):
         if self.artifact.is_cpu:
             import shutil
-            shutil.copy(self.code, path)
+            shutil.copy(self.code[0], path)
         else:
-            Path(path).write_bytes(self.code)
+            Path(path).write_bytes(self.code[0])
 
     def get_profiler(self, tensor_supply_type=None):
         from ..profiler import Profiler

@@ -127,6 +127,13 @@ def _read_patterns(kind: str, rows: int, cols: int, elem_bytes: int, row_base_st
       'tr_kperm': same, C-layout compatible k order (16h + 4g + q)
     """
     pats = []
+    if kind == "k_rows32":
+        # 8-bit operand of the scaled 16x16x128 MFMA: 32 consecutive bytes per lane, two b128 reads
+        for r0 in range(0, min(rows, 64), row_base_step):
+            for k0 in range(0, cols, 128):
+                for half in range(2):
+                    pats.append([(r0 + (l & 15), k0 + (l >> 4) * 32 + 16 * half) for l in range(64)])
+        return pats
     if kind == "k_rows":
         k_per_lane = 8
         kstep = 4 * k_per_lane
@@ -154,13 +161,17 @@ def _read_patterns(kind: str, rows: int, cols: int, elem_bytes: int, row_base_st
 
 
 def _instr_for(kind: str, elem_bytes: int) -> str:
+    if kind == "k_rows32":
+        return "ds_read_b128"
     if kind == "k_rows":
         return "ds_read_b128" if elem_bytes == 2 else "ds_read_b64"
     return "ds_read_b64_tr_b16"
 
 
 def _candidates(cpr: int, max_row_bit: int = 6):
-    nbits = max(0, cpr.bit_length() - 1)
+    # only chunk bits below the 256-byte bank row (16 chunks) change the bank of an access
+    nbits = min(4, max(0, cpr.bit_length() - 1))
+    max_row_bit = min(max_row_bit, 5)
     choices = [None] + list(range(max_row_bit))
     for combo in itertools.product(choices, repeat=nbits):
         bits = [(rb, cb) for cb, rb in enumerate(combo) if rb is not None]
@@ -223,6 +234,41 @@ def swizzle_report(kind: str, rows: int, cols: int, elem_bytes: int, bits) -> di
     cyc0 = sum(lds_bank.instruction_cycles(instr, [base.forward(r, c)[0] * elem_bytes for r, c in p]) for p in pats)
     ideal = len(pats) * len(lds_bank.INSTRUCTIONS[instr][0])
     return {"instruction": instr, "cycles": cyc, "cycles_unswizzled": cyc0, "conflict_free": ideal}
+
+
+@functools.lru_cache(maxsize=None)
+def choose_swizzle_multi(kinds: Tuple[str, ...], rows: int, cols: int, elem_bytes: int):
+    """Best swizzle for a tile read with several patterns (e.g. MLA's KV tile, read row-wise by
+    Q.KV^T and transposed by P.KV): minimise the summed modelled cycles."""
+    import numpy as np
+    if len(kinds) == 1:
+        return choose_swizzle(kinds[0], rows, cols, elem_bytes)
+    cpr = cols * elem_bytes // 16
+    if cpr <= 1:
+        return ()
+    cands = [tuple(b) for b in _candidates(cpr, max_row_bit=min(6, max(1, rows.bit_length() - 1)))]
+    total = np.zeros(len(cands), dtype=np.int64)
+    for kind in kinds:
+        pats = _read_patterns(kind, rows, cols, elem_bytes)
+        instr = _instr_for(kind, elem_bytes)
+        R = np.array([[r for r, c in p] for p in pats], dtype=np.int64)
+        Cc = np.array([[c for r, c in p] for p in pats], dtype=np.int64)
+        byte = Cc * elem_bytes
+        xs = np.zeros((len(cands), ) + R.shape, dtype=np.int64)
+        for i, bits in enumerate(cands):
+            for rb, cb in bits:
+                xs[i] |= ((R >> rb) & 1) << cb
+        addrs = R[None] * (cols * elem_bytes) + (((byte // 16)[None] ^ xs) * 16) + (byte % 16)[None]
+        total += _batched_cycles(instr, addrs)
+    best = min(range(len(cands)), key=lambda i: (int(total[i]), len(cands[i])))
+    return cands[best]
+
+
+def operand_swizzle_multi(kinds, shape: Sequence[int], elem_bytes: int) -> SwizzleLayout:
+    rows, cols = int(shape[-2]), int(shape[-1])
+    kinds = tuple(sorted(set(kinds)))
+    bits = choose_swizzle_multi(kinds, rows, cols, elem_bytes)
+    return SwizzleLayout(list(shape), elem_bytes, list(bits), name="swz_" + "+".join(kinds))
 
 
 def operand_swizzle(kind: str, shape: Sequence[int], elem_bytes: int) -> SwizzleLayout:

@@ -83,9 +83,20 @@ def gemm_plan(op: O.GemmOp, num_threads: int, target=None, a_layout: Optional[Fr
         if a_layout.is_equal(k1r) or a_layout.is_equal(k1):
             plan["a_kperm"] = 1
     ebytes = A.dtype.bytes
+    if eb == 8:
+        if op.trans_A or not op.trans_B or A.scope != "shared" or B.scope != "shared":
+            raise ValueError("fp8 T.gemm on gfx950 needs K-contiguous shared operands: A [M,K] and B [N,K] "
+                             "(transpose_B=True)")
+        kind = "k_rows32" if K % 128 == 0 else "k_rows"
+        plan["f8_kind"] = kind
+        plan["a_kind"] = plan["b_kind"] = kind
+        plan["a_smem_layout"] = MF.operand_swizzle(kind, A.static_shape(), 1)
+        plan["b_smem_layout"] = MF.operand_swizzle(kind, B.static_shape(), 1)
+        return plan
     if A.scope == "shared":
         shp = A.static_shape()
         kind = "tr" if op.trans_A else "k_rows"
+        plan["a_kind"] = kind
         plan["a_smem_layout"] = MF.operand_swizzle(kind, shp, ebytes) if ebytes == 2 else LinearLayout(shp)
     if B.scope == "shared":
         shp = B.static_shape()
@@ -93,5 +104,6 @@ def gemm_plan(op: O.GemmOp, num_threads: int, target=None, a_layout: Optional[Fr
             kind = "k_rows"
         else:
             kind = "tr_kperm" if plan["a_kperm"] == 1 else "tr"
+        plan["b_kind"] = kind
         plan["b_smem_layout"] = MF.operand_swizzle(kind, shp, ebytes) if ebytes == 2 else LinearLayout(shp)
     return plan

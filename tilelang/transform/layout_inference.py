@@ -193,6 +193,7 @@ class LayoutInference:
         self.strict: set = set()
         self.gemm_info: Dict[int, dict] = {}
         self.nest_layouts: Dict[int, Fragment] = {}
+        self.smem_reads: Dict[Buffer, dict] = {}
 
     # ------------------------------------------------------------------------------
     def set_frag(self, buf: Buffer, lay: Fragment, why: str, strict: bool = False):
@@ -268,6 +269,12 @@ class LayoutInference:
                         break
             else:
                 break
+        # final gemm plans (register-A k-permutation is known now) -> shared operand swizzles
+        self.smem_reads = {}
+        for op in ops:
+            if isinstance(op, O.GemmOp):
+                self.infer_gemm(op, level="final")
+        self.assign_shared_layouts()
         for b, lay in self.frag.items():
             b.layout = lay
         for n in nests:
@@ -317,19 +324,26 @@ class LayoutInference:
                 # prefer the layout that matches an accumulator source (checked later), else natural
                 changed |= self.set_frag(A, k0, "gemm A", strict=True)
                 plan["a_kperm"] = 0
-        for reg, role in ((op.A, "A"), (op.B, "B")):
+        for reg, role in ((op.A, "a"), (op.B, "b")):
             b = reg.buffer
-            if b.scope == "shared" and not getattr(b, "layout_annotated", False):
-                lay = plan[f"{role.lower()}_smem_layout"]
-                if b.layout is None or not _same_layout(b.layout, lay):
-                    if b.layout is not None and getattr(b, "_layout_owner", None) not in (None, id(op)):
-                        # shared buffer consumed by two GEMMs with different read patterns: keep linear
-                        b.layout = LinearLayout(b.static_shape())
-                        b._layout_owner = -1
-                    elif getattr(b, "_layout_owner", None) != -1:
-                        b.layout = lay
-                        b._layout_owner = id(op)
+            if b.scope == "shared" and plan.get(f"{role}_kind"):
+                self.smem_reads.setdefault(b, {})[(id(op), role)] = plan[f"{role}_kind"]
         return changed
+
+    def assign_shared_layouts(self):
+        """One swizzle per shared operand tile, chosen against ALL its MFMA read patterns."""
+        for b, kinds in self.smem_reads.items():
+            if getattr(b, "layout_annotated", False):
+                continue
+            shp = b.static_shape()
+            if len(shp) != 2:
+                b.layout = LinearLayout(shp)
+                continue
+            eb = b.dtype.bytes
+            if eb not in (1, 2):
+                b.layout = LinearLayout(shp)
+                continue
+            b.layout = MF.operand_swizzle_multi(tuple(kinds.values()), shp, eb)
 
     def infer_op(self, op) -> bool:
         changed = False

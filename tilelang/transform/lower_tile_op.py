@@ -260,6 +260,8 @@ class _IterRewriter(Mutator):
             return BufferLoad(self.ctx.local_of(b), [IntImm(li)])
         idx2 = [substitute(i, self.vmap) for i in idx]
         idx2 = [transform(i, self._load_sub) for i in idx2]
+        if b.scope in ("local", "var"):
+            return BufferLoad(b, [b.offset_of(idx2)] if b.ndim != 1 else idx2)
         ld = BufferLoad(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx2)])
         g = safe_guard(self.ctx, b, idx2)
         if g is not None:
@@ -290,6 +292,8 @@ class _IterRewriter(Mutator):
             li = self.res.local_index(b, s.indices, self.r)
             return S.StoreStmt(self.ctx.local_of(b), [IntImm(li)], val)
         idx = [self.expr(i) for i in s.indices]
+        if b.scope in ("local", "var"):
+            return S.StoreStmt(b, [b.offset_of(idx)] if b.ndim != 1 else idx, val)
         st = S.StoreStmt(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)], val)
         g = safe_guard(self.ctx, b, idx)
         return S.IfStmt(g, st) if g is not None else st
@@ -731,6 +735,14 @@ class TileOpLowerer(Mutator):
         if B.scope != "shared":
             raise LoweringError("T.gemm: B operand must be in shared memory on gfx950")
         pb = self._operand_ptr(op.B)
+        if A.dtype.bits == 8:
+            pa = self._operand_ptr(op.A)
+            out.append(L.CallStmt("tl::gemm_ss_f8", [pa, pb, L.BufferPtr(cl, 0)], [
+                _dt.hip_type(A.dtype), _dt.hip_type(B.dtype), plan["M"], plan["N"], plan["K"], plan["warp_m"],
+                plan["warp_n"], A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
+                B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u"
+            ]))
+            return S.SeqStmt(out)
         b_cols = B.static_shape()[-1]
         swz_b = gemm_lower.encode_swizzle(B.layout)
         if A.scope == "shared":
