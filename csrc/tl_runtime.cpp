@@ -336,6 +336,8 @@ class Kernel {
     int64_t gx = g.size() > 0 ? g[0] : 1, gy = g.size() > 1 ? g[1] : 1, gz = g.size() > 2 ? g[2] : 1;
     if (gx <= 0 || gy <= 0 || gz <= 0) return;  // empty launch
     if (is_cpu_) {
+      // CPU kernels may spin on peers (virtual mesh ranks run in other Python threads)
+      py::gil_scoped_release nogil;
       cpu_entry_(ptrs);
       return;
     }
@@ -379,9 +381,80 @@ py::dict device_info(int dev) {
   return d;
 }
 
+// ---- mesh workspaces: symmetric device memory shared across processes over xGMI ----------
+// flags: 0 = hipMalloc (coarse-grained; the protocol uses system-scope fences),
+//        1 = uncached fine-grained (hipDeviceMallocUncached) for debugging coherence issues.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    TL_HIP_CHECK(hipGetDevice(&prev));
+    if (dev >= 0 && dev != prev) TL_HIP_CHECK(hipSetDevice(dev));
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int64_t ws_alloc(int64_t nbytes, int device, int flags) {
+  DeviceGuard g(device);
+  void* p = nullptr;
+  if (flags == 1) TL_HIP_CHECK(hipExtMallocWithFlags(&p, (size_t)nbytes, hipDeviceMallocUncached));
+  else TL_HIP_CHECK(hipMalloc(&p, (size_t)nbytes));
+  TL_HIP_CHECK(hipMemset(p, 0, (size_t)nbytes));
+  TL_HIP_CHECK(hipDeviceSynchronize());
+  return reinterpret_cast<int64_t>(p);
+}
+
+void ws_free(int64_t ptr, int device) {
+  DeviceGuard g(device);
+  TL_HIP_CHECK(hipFree(reinterpret_cast<void*>(ptr)));
+}
+
+void ws_zero(int64_t ptr, int64_t nbytes, int device) {
+  DeviceGuard g(device);
+  TL_HIP_CHECK(hipMemset(reinterpret_cast<void*>(ptr), 0, (size_t)nbytes));
+  TL_HIP_CHECK(hipDeviceSynchronize());
+}
+
+py::bytes ipc_get_handle(int64_t ptr, int device) {
+  DeviceGuard g(device);
+  hipIpcMemHandle_t h;
+  TL_HIP_CHECK(hipIpcGetMemHandle(&h, reinterpret_cast<void*>(ptr)));
+  return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+int64_t ipc_open_handle(py::bytes handle, int device) {
+  std::string s = handle;
+  if (s.size() != sizeof(hipIpcMemHandle_t)) throw py::value_error("bad IPC handle size");
+  DeviceGuard g(device);
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, s.data(), sizeof(h));
+  void* p = nullptr;
+  TL_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  return reinterpret_cast<int64_t>(p);
+}
+
+void ipc_close_handle(int64_t ptr, int device) {
+  DeviceGuard g(device);
+  TL_HIP_CHECK(hipIpcCloseMemHandle(reinterpret_cast<void*>(ptr)));
+}
+
+bool can_access_peer(int dev, int peer) {
+  int ok = 0;
+  TL_HIP_CHECK(hipDeviceCanAccessPeer(&ok, dev, peer));
+  return ok != 0;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_tl_runtime, m) {
+  m.def("ws_alloc", &ws_alloc, py::arg("nbytes"), py::arg("device"), py::arg("flags") = 0);
+  m.def("ws_free", &ws_free);
+  m.def("ws_zero", &ws_zero);
+  m.def("ipc_get_handle", &ipc_get_handle);
+  m.def("ipc_open_handle", &ipc_open_handle);
+  m.def("ipc_close_handle", &ipc_close_handle);
+  m.def("can_access_peer", &can_access_peer);
   m.doc() = "tilelang native kernel runtime for MI355X (gfx950)";
   py::class_<Kernel, std::shared_ptr<Kernel>>(m, "Kernel")
       .def(py::init<py::bytes, std::string, bool, py::list, int, std::vector<std::vector<int64_t>>,

@@ -1,0 +1,116 @@
+"""T.comm on MI355X: the gfx950 protocol (peer stores into IPC/virtual workspaces, system-scope
+flags) on a real GPU.  One GPU per box here, so the ranks share it: a VirtualMesh (one HIP
+stream per rank) and two processes that exchange HIP IPC handles over gloo.  Results are
+compared with plain PyTorch."""
+import os
+import socket
+
+import pytest
+import torch
+
+import tilelang
+import tilelang.language as T
+from tilelang.parallel import VirtualMesh, device_mesh_config
+
+pytestmark = pytest.mark.gpu
+
+
+def _program(nrow, ncol, M=64, N=128, blocks=2):
+    world = nrow * ncol
+    with device_mesh_config(nrow, ncol):
+
+        @T.prim_func
+        def main(A: T.Tensor((M * blocks, N), "float16"), B: T.Tensor((M * blocks, N), "float16"),
+                 G: T.Tensor((world, M * blocks, N), "float16"), R: T.Tensor((M * blocks,), "float32")):
+            with T.Kernel(blocks, threads=256) as bx:
+                a = T.alloc_fragment((M, N), "float16")
+                b = T.alloc_fragment((M, N), "float16")
+                f = T.alloc_fragment((M, N), "float32")
+                g = T.alloc_shared((world, M, N), "float16")
+                r = T.alloc_fragment((M,), "float32")
+                T.copy(A[bx * M, 0], a)
+                T.comm.broadcast(a, b, (0, ncol - 1), direction="all")
+                T.copy(b, B[bx * M, 0])
+                T.comm.all_gather(a, g, direction="all")
+                T.copy(g, G[0:world, bx * M:(bx + 1) * M, 0:N])
+                for i, j in T.Parallel(M, N):
+                    f[i, j] = a[i, j]
+                T.comm.all_reduce(f, r, "sum", "all", dim=1)
+                T.copy(r, R[bx * M])
+
+        return tilelang.compile(main, target="hip")
+
+
+def _check(rank, world, As, B, G, R, src):
+    torch.testing.assert_close(B, As[src])
+    torch.testing.assert_close(G, torch.stack(As))
+    ref = sum(a.float().sum(1) for a in As)
+    torch.testing.assert_close(R, ref, rtol=1e-4, atol=1e-3)
+
+
+def test_virtual_mesh_gpu_1x2():
+    k = _program(1, 2)
+    vm = VirtualMesh(1, 2, "cuda", workspace_bytes=16 << 20)
+    torch.manual_seed(0)
+    As = [torch.randn(128, 128, device="cuda", dtype=torch.float16) for _ in range(2)]
+    outs = [(torch.zeros(128, 128, device="cuda", dtype=torch.float16),
+             torch.zeros(2, 128, 128, device="cuda", dtype=torch.float16),
+             torch.zeros(128, device="cuda")) for _ in range(2)]
+
+    def fn(ctx):
+        k(As[ctx.rank], *outs[ctx.rank])
+
+    for _ in range(3):  # several launches: epochs advance, no workspace reset
+        vm.run(fn)
+        vm.check()
+    for r in range(2):
+        _check(r, 2, As, *outs[r], src=1)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from tilelang.parallel import init_mesh, shutdown_mesh
+        ctx = init_mesh(1, world, device="cuda:0")  # both ranks on the box's one GPU, HIP IPC workspaces
+        k = _program(1, world)
+        torch.manual_seed(rank)
+        A = torch.randn(128, 128, device="cuda", dtype=torch.float16)
+        B = torch.zeros_like(A)
+        G = torch.zeros(world, 128, 128, device="cuda", dtype=torch.float16)
+        R = torch.zeros(128, device="cuda")
+        for _ in range(3):
+            k(A, B, G, R)
+        ctx.check()
+        allA = [torch.zeros_like(A.cpu()) for _ in range(world)]
+        dist.all_gather(allA, A.cpu())
+        As = [a.cuda() for a in allA]
+        _check(rank, world, As, B, G, R, src=world - 1)
+        shutdown_mesh()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_process_mesh_ipc_gpu():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=400) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}, res

@@ -237,7 +237,10 @@ class CodeGen:
         if op == "tl.address_of":
             return f"(&{self.e(args[0])})"
         if op == "tl.mesh_rank":
-            return "tl_mesh_rank"
+            v = self.kernel.attrs.get("mesh_rank_var")
+            if v is None:
+                raise CodeGenError("T.comm.current_core() used in a kernel without mesh parameters")
+            return self.e(v)
         if op == "tl.sync_threads":
             return "__syncthreads()"
         if op == "tl.fence":
@@ -335,6 +338,11 @@ class CodeGen:
                    f"&{self.buf_ref(st.src)}[{self.e(st.src_index)}]);")
         elif isinstance(st, L.CommentStmt):
             self.w(f"// {st.text}")
+        elif isinstance(st, L.PtrDeclStmt):
+            ct = self.ctype(st.buffer.dtype)
+            self.w(f"{ct}* {self.buf_name(st.buffer)} = reinterpret_cast<{ct}*>({self.e(st.ptr)});")
+        elif isinstance(st, L.AutoLetStmt):
+            self.w(f"const auto {self.e(st.var)} = {self.e(st.value)};")
         elif isinstance(st, S.KernelStmt):
             raise CodeGenError("nested kernel")
         elif isinstance(st, S.TileOpStmt):
@@ -347,7 +355,7 @@ class CodeGen:
         name = self.buf_name(b)
         if b.scope == "shared":
             if self.is_cpu:
-                self.w(f"static {ct} {name}[{int(b.shape[0])}];")
+                self.w(f"static thread_local {ct} {name}[{int(b.shape[0])}];")
                 return
             off = self.lds_offsets[b]
             self.w(f"{ct}* {name} = reinterpret_cast<{ct}*>(tl_smem + {off});")
@@ -401,7 +409,7 @@ class CodeGen:
             sig.append(f"{self.ctype(v.dtype)} {self.name_of(v, v.name)}")
             params.append(dict(kind="dyn", name=v.name, dtype=v.dtype.name, var=v))
         for extra in k.attrs.get("extra_params", []):
-            sig.append(extra["decl"])
+            sig.append(f"{extra['ctype']} {self.name_of(extra['var'], extra['name'])}")
             params.append(extra)
         ks.params = params
         ks.dyn_vars = dyn_vars

@@ -45,6 +45,7 @@ class DeviceKernel:
     params: list
     lowered_ir: Optional[S.Stmt] = None
     layout_info: Dict[str, str] = field(default_factory=dict)
+    mesh: Optional[dict] = None   # T.comm kernels: mesh shape, op count, workspace bytes
 
 
 @dataclass
@@ -128,7 +129,8 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
     ks: KernelSource = generate(func, lk, target, offsets, total, name, cfg)
     timings["codegen"] = timings.get("codegen", 0) + time.perf_counter() - t
     layout_info = {b.name: repr(lay) for b, lay in li.frag.items()}
-    return DeviceKernel(ks.source, ks.kernel_name, ks.grid, ks.block, ks.lds_bytes, ks.params, lk, layout_info)
+    return DeviceKernel(ks.source, ks.kernel_name, ks.grid, ks.block, ks.lds_bytes, ks.params, lk, layout_info,
+                        lk.attrs.get("mesh"))
 
 
 def lower(func: S.PrimFunc, target="auto", target_host=None, pass_configs: Optional[dict] = None,

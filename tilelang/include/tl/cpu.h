@@ -107,3 +107,4 @@ inline void cpu_gemm(const T* A, const T* B, float* C) {
 }
 
 }  // namespace tl
+#include "mesh_cpu.h"

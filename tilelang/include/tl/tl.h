@@ -7,3 +7,4 @@
 #include "atomic.h"
 #include "swizzle.h"
 #include "debug.h"
+#include "mesh.h"

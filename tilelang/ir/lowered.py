@@ -68,3 +68,20 @@ class CommentStmt(Stmt):
 
     def __init__(self, text: str):
         self.text = text
+
+
+class PtrDeclStmt(Stmt):
+    """``T* name = reinterpret_cast<T*>(ptr);`` — a flat global view at a runtime address
+    (e.g. a peer GPU's mesh workspace slot)."""
+
+    def __init__(self, buffer, ptr):
+        self.buffer = buffer
+        self.ptr = ptr
+
+
+class AutoLetStmt(Stmt):
+    """``const auto name = value;`` for values of device-library struct type."""
+
+    def __init__(self, var, value):
+        self.var = var
+        self.value = value

@@ -207,6 +207,7 @@ class FinalizeReducerOp(TileOp):
 
 class CommOp(TileOp):
     kind = "comm"
+    mesh = None  # (nrow, ncol) the op was traced for
 
 
 class CommBroadcastOp(CommOp):
@@ -264,9 +265,10 @@ class CommAllReduceOp(CommOp):
                  clear: bool):
         self.src, self.dst, self.reduce_type = src, dst, reduce_type
         self.direction, self.dim, self.clear = direction, dim, clear
+        self.tmp = None  # per-core partial reduction (allocated by T.comm.all_reduce)
 
     def regions(self):
-        return [self.src, self.dst]
+        return [self.src, self.dst] + ([self.tmp] if self.tmp is not None else [])
 
     def reads(self):
         return [self.src]

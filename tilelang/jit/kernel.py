@@ -176,7 +176,20 @@ class JITKernel:
                     full.append(kwargs[n])
             args = tuple(full)
         rts = self.runtimes
-        out = rts[0](*args)
+        kernels = self.artifact.kernels
+        mesh_ctx = None
+        if any(dk.mesh is not None for dk in kernels):
+            from ..parallel.mesh import current_mesh, MeshError
+            mesh_ctx = current_mesh()
+            if mesh_ctx is None:
+                raise MeshError(f"{self.artifact.kernel_name} uses T.comm / current_core but no mesh is active: call "
+                                f"tilelang.parallel.init_mesh() (one process per GPU) or run it inside "
+                                f"VirtualMesh.run()")
+
+        def _margs(dk):
+            return mesh_ctx.launch_args(dk.mesh) if dk.mesh is not None else []
+
+        out = rts[0](*args, *_margs(kernels[0]))
         if len(rts) == 1:
             return out
         # later kernels of the program see the outputs of the first as ordinary arguments
@@ -189,8 +202,8 @@ class JITKernel:
             else:
                 full.append(args[ai])
                 ai += 1
-        for r in rts[1:]:
-            r(*full)
+        for r, dk in zip(rts[1:], kernels[1:]):
+            r(*full, *_margs(dk))
         return out
 
     def set_validation(self, enabled: bool):

@@ -67,6 +67,16 @@ def is_current_core(core):
     return current_core() == convert(core)
 
 
+def _mesh_tuple():
+    m = get_target_mesh_shape()
+    return (m["x"], m["y"])
+
+
+def _emit(op):
+    op.mesh = _mesh_tuple()
+    current_builder().emit(S.TileOpStmt(op))
+
+
 def _shape(b):
     return list(b.shape) if isinstance(b, Buffer) else list(b.extents)
 
@@ -104,7 +114,7 @@ def broadcast(src, dst, src_core, direction: str = "all", size: int = -1):
     assert direction.lower() in DIRECTION_MAP, f"Invalid direction string: {direction}"
     op = O.CommBroadcastOp(to_region(src), to_region(dst), core_tuple_to_id(src_core),
                            DIRECTION_NAMES[DIRECTION_MAP[direction.lower()]], n if size == -1 else size)
-    current_builder().emit(S.TileOpStmt(op))
+    _emit(op)
 
 
 def put(src, dst, src_core, dst_core, size: int = -1):
@@ -117,7 +127,7 @@ def put(src, dst, src_core, dst_core, size: int = -1):
     assert size <= n, f"size {size} exceeds source buffer size {n}."
     op = O.CommPutOp(to_region(src), to_region(dst), core_tuple_to_id(src_core), core_tuple_to_id(dst_core),
                      n if size == -1 else size)
-    current_builder().emit(S.TileOpStmt(op))
+    _emit(op)
 
 
 def all_gather(send_buffer, recv_buffer, direction: str = "all", size: int = -1):
@@ -135,7 +145,7 @@ def all_gather(send_buffer, recv_buffer, direction: str = "all", size: int = -1)
     assert size <= n, f"size {size} exceeds send buffer size {n}."
     op = O.CommAllGatherOp(to_region(send_buffer), to_region(recv_buffer), DIRECTION_NAMES[d],
                            n if size == -1 else size)
-    current_builder().emit(S.TileOpStmt(op))
+    _emit(op)
 
 
 def all_reduce(buffer, out, reduce_type: str, direction: str = "all", dim: int = -1, clear: bool = True):
@@ -154,12 +164,32 @@ def all_reduce(buffer, out, reduce_type: str, direction: str = "all", dim: int =
     assert clear in (True, False), "clear must be a boolean value."
     op = O.CommAllReduceOp(to_region(buffer), to_region(out), reduce_type,
                            DIRECTION_NAMES[DIRECTION_MAP[direction.lower()]], dim, clear)
-    current_builder().emit(S.TileOpStmt(op))
+    # per-core partial (local reduce along `dim`), same scope as `out` — the reference allocates
+    # its row/col gather fragments here too (language/comm.py:340-433)
+    ob = out if isinstance(out, Buffer) else out.buffer
+    from .allocate import alloc_fragment, alloc_shared
+    alloc = alloc_shared if ob.scope == "shared" else alloc_fragment
+    tmp = alloc(oshape, ob.dtype)
+    tmp.name = f"{ob.name}_partial"
+    tmp._auto_name = False
+    op.tmp = to_region(tmp)
+    _emit(op)
 
 
 def barrier(group=None):
-    current_builder().emit(S.TileOpStmt(O.CommBarrierOp(group)))
+    """Synchronise a group of cores (default: the whole mesh).  ``group`` is an iterable of
+    ``(row, col)`` tuples (reference ``language/comm.py:436-459``)."""
+    m = get_target_mesh_shape()
+    ids = None
+    if group is not None:
+        ids = []
+        for c in group:
+            _check_core(tuple(c), m, "barrier core")
+            ids.append(core_tuple_to_id(tuple(c)))
+        if len(set(ids)) != len(ids):
+            raise ValueError(f"duplicate core in barrier group {group}")
+    _emit(O.CommBarrierOp(ids))
 
 
 def fence():
-    current_builder().emit(S.TileOpStmt(O.CommFenceOp()))
+    _emit(O.CommFenceOp())

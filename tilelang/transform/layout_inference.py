@@ -363,6 +363,32 @@ class LayoutInference:
                     changed |= self.set_frag(s, self.frag[d], "copy")
         elif isinstance(op, O.CumSumOp):
             pass
+        elif isinstance(op, O.CommAllReduceOp) and op.tmp is not None:
+            # partial = reduce(src, dim) gets the reduce layout; out follows the partial
+            s, t, d = op.src.buffer, op.tmp.buffer, op.dst.buffer
+            if _is_frag(s) and _is_frag(t) and s in self.frag and t not in self.frag:
+                if not _full_region(op.src):
+                    raise LayoutConflictError("T.comm.all_reduce on a fragment must cover the whole fragment")
+                changed |= self.set_frag(t, reduce_dst_layout(self.frag[s], op.dim, t.static_shape()), "comm reduce")
+            if _is_frag(t) and _is_frag(d) and t in self.frag and d not in self.frag:
+                changed |= self.set_frag(d, self.frag[t], "comm all_reduce out")
+        elif isinstance(op, O.CommAllGatherOp):
+            # recv[k] is laid out like send: each thread holds slice k of the elements it sends
+            s, r = op.send.buffer, op.recv.buffer
+            if _is_frag(s) and _is_frag(r) and s in self.frag and r not in self.frag and _full_region(op.send):
+                sl = self.frag[s]
+                G = r.static_shape()[0]
+                td = [Digit(d.dim + 1, d.stride, d.size) if d.dim >= 0 else d for d in sl.thread_digits]
+                ld = [Digit(0, 1, G)] + [Digit(d.dim + 1, d.stride, d.size) for d in sl.local_digits]
+                changed |= self.set_frag(r, Fragment([G] + list(sl.shape), td, ld, sl.name + "_gather"), "all_gather")
+        elif isinstance(op, (O.CommBroadcastOp, O.CommPutOp)):
+            s, d = op.src.buffer, op.dst.buffer
+            if _is_frag(s) and _is_frag(d) and _full_region(op.src) and _full_region(op.dst) and \
+                    s.static_shape() == d.static_shape():
+                if s in self.frag and d not in self.frag:
+                    changed |= self.set_frag(d, self.frag[s], "comm")
+                elif d in self.frag and s not in self.frag:
+                    changed |= self.set_frag(s, self.frag[d], "comm")
         return changed
 
     def infer_nest(self, n: ParallelNest, free: bool) -> bool:
@@ -403,7 +429,10 @@ class LayoutInference:
                 if dm is None:
                     continue
                 bshape = b.static_shape()
-                lay = project_layout(n.layout, dm, bshape)
+                try:
+                    lay = project_layout(n.layout, dm, bshape)
+                except ValueError:
+                    continue  # the nest covers only part of b (constant index); b is laid out elsewhere
                 changed |= self.set_frag(b, lay, "parallel")
         return changed
 

@@ -340,7 +340,7 @@ def _const_diff(a: PrimExpr, b: PrimExpr, probe_vars: List[Var]) -> Optional[int
 def safe_guard(ctx: LowerCtx, b: Buffer, idx) -> Optional[PrimExpr]:
     """Bounds condition for a global access that cannot be proven in range (ragged tiles,
     dynamic shapes); None when every index is provably inside the tensor."""
-    if b.scope != "global" or ctx.pass_cfg.get("tl.disable_safe_memory_legalize"):
+    if b.scope != "global" or ctx.pass_cfg.get("tl.disable_safe_memory_legalize") or getattr(b, "no_guard", False):
         return None
     cond = None
     for i, s in zip(idx, b.shape):
@@ -1345,14 +1345,48 @@ def _copy_vec_ok(src, dst, sd, dd, vec, known_div) -> bool:
     return True
 
 
+def _mesh_usage(kernel: S.KernelStmt):
+    """(comm ops, uses T.comm.current_core) of a kernel, before lowering."""
+    comm = [s.op for s in S.walk(kernel) if isinstance(s, S.TileOpStmt) and isinstance(s.op, O.CommOp)]
+    found = []
+
+    class _F(Mutator):
+
+        def expr(self, e):
+            if isinstance(e, PrimExpr) and not found:
+                for n in post_order(e):
+                    if isinstance(n, Call) and n.op == "tl.mesh_rank":
+                        found.append(n)
+                        break
+            return e
+
+    _F().stmt(kernel.body)
+    return comm, bool(found)
+
+
 def lower_tile_ops(kernel: S.KernelStmt, target, pass_cfg=None):
     ctx = LowerCtx(kernel, target, pass_cfg)
+    comm_ops, uses_rank = _mesh_usage(kernel)
+    ctx.mesh = None
+    if comm_ops or uses_rank:
+        from ..parallel import comm_lower
+        ctx.mesh_slot_bytes = max([comm_lower.op_slot_bytes(o) for o in comm_ops] or [256])
+        shapes = {tuple(o.mesh) for o in comm_ops if o.mesh is not None}
+        if len(shapes) > 1:
+            raise LoweringError(f"T.comm ops of one kernel were traced for different mesh shapes: {sorted(shapes)}")
+        comm_lower.mesh_state(ctx, shapes.pop() if shapes else None)
     lw = TileOpLowerer(ctx)
     body = lw.stmt(kernel.body)
     allocs = [S.AllocStmt(b) for b in ctx.extra_allocs]
+    if ctx.mesh is not None:
+        allocs = allocs + ctx.mesh.prologue()
     k = S.KernelStmt(kernel.grid, kernel.threads, kernel.block_vars, kernel.thread_vars,
                      S.SeqStmt(allocs + [body]), kernel.is_cpu, kernel.prelude)
     k.attrs = dict(kernel.attrs)
+    if ctx.mesh is not None:
+        k.attrs["extra_params"] = list(k.attrs.get("extra_params", [])) + ctx.mesh.extra_params()
+        k.attrs["mesh"] = ctx.mesh.meta()
+        k.attrs["mesh_rank_var"] = ctx.mesh.rank
     k.attrs["tid"] = ctx.tid
     k.attrs["lane"] = ctx.lane if ctx.uses_lane else None
     k.attrs["wave"] = ctx.wave if ctx.uses_wave else None
