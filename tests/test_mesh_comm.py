@@ -303,3 +303,30 @@ def test_process_mesh_gloo_cpu():
     for p in ps:
         p.join(timeout=60)
     assert res == {0: "ok", 1: "ok"}, res
+
+
+@pytest.mark.parametrize("direction,clear", [("all", True), ("h", False)])
+def test_all_reduce_tile_cpu(direction, clear):
+    """Tensor-parallel partial sums: element-wise tile reduction across cores."""
+    nrow, ncol = 2, 2
+    M, N = 16, 8
+    with device_mesh_config(nrow, ncol):
+
+        @T.prim_func
+        def main(A: T.Tensor((M, N), "float32"), O_: T.Tensor((M, N), "float32")):
+            with T.Kernel(1, threads=64) as bx:
+                a = T.alloc_fragment((M, N), "float32")
+                o = T.alloc_fragment((M, N), "float32")
+                T.copy(A, a)
+                T.fill(o, 2.0)
+                T.comm.all_reduce_tile(a, o, "sum", direction, clear=clear)
+                T.copy(o, O_)
+
+        k = tilelang.compile(main, target="cpu")
+    vm = VirtualMesh(nrow, ncol, "cpu", workspace_bytes=1 << 20)
+    As = [torch.randn(M, N) for _ in range(4)]
+    Os = [torch.zeros(M, N) for _ in range(4)]
+    _run(vm, k, [(a,) for a in As], [(o,) for o in Os])
+    for r in range(4):
+        exp = sum(As[m] for m in _dirs(nrow, ncol, r, direction)) + (0 if clear else 2.0)
+        torch.testing.assert_close(Os[r], exp)

@@ -176,6 +176,21 @@ def all_reduce(buffer, out, reduce_type: str, direction: str = "all", dim: int =
     _emit(op)
 
 
+def all_reduce_tile(src, dst, reduce_type: str = "sum", direction: str = "all", clear: bool = True):
+    """Element-wise reduction of a whole tile across the cores of a group (no local reduce):
+    ``dst = op_{c in group} src@c`` (``clear=False``: ``dst = dst op ...``).  Extension over the
+    reference API for tensor-parallel partial sums (e.g. a row-parallel GEMM's output tile)."""
+    assert src.dtype == dst.dtype if isinstance(src, Buffer) and isinstance(dst, Buffer) else True
+    if [int(x) for x in _shape(src)] != [int(x) for x in _shape(dst)]:
+        raise ValueError(f"all_reduce_tile: src shape {_shape(src)} != dst shape {_shape(dst)}")
+    reduce_type = reduce_type.lower()
+    assert reduce_type in ("sum", "max", "min", "bitand", "bitor", "bitxor"), f"bad reduce type {reduce_type}"
+    assert direction.lower() in DIRECTION_MAP, f"Invalid direction string: {direction}"
+    op = O.CommAllReduceOp(to_region(src), to_region(dst), reduce_type,
+                           DIRECTION_NAMES[DIRECTION_MAP[direction.lower()]], None, clear)
+    _emit(op)
+
+
 def barrier(group=None):
     """Synchronise a group of cores (default: the whole mesh).  ``group`` is an iterable of
     ``(row, col)`` tuples (reference ``language/comm.py:436-459``)."""

@@ -20,6 +20,7 @@ from __future__ import annotations
 import ast
 import functools
 import inspect
+import sys
 import textwrap
 from typing import Any, Dict, List, Optional
 
@@ -315,6 +316,10 @@ def _resolve_annotations(fn) -> Dict[str, Any]:
         if isinstance(v, str):  # from __future__ import annotations
             if ns is None:
                 ns = _closure_namespace(fn)
+                # names used only in annotations are not captured by the closure: use the
+                # locals of the frame that applied the decorator
+                for name, val in (getattr(fn, "__tl_def_locals__", None) or {}).items():
+                    ns.setdefault(name, val)
             anns[k] = eval(v, ns)  # noqa: S307 - user annotation
     return anns
 
@@ -322,14 +327,18 @@ def _resolve_annotations(fn) -> Dict[str, Any]:
 def prim_func(fn=None, *, private: bool = False, generator: bool = False):
     """Decorator turning a kernel definition into a ``PrimFunc`` (eagerly traced)."""
 
-    def deco(f):
+    def deco(f, depth=1):
+        try:
+            f.__tl_def_locals__ = dict(sys._getframe(depth).f_locals)
+        except (AttributeError, ValueError):
+            pass
         if generator:
             return _PrimFuncGenerator(f)
         return trace_prim_func(f)
 
     if fn is None:
         return deco
-    return deco(fn)
+    return deco(fn, depth=2)
 
 
 def trace_prim_func(f, arg_overrides: Optional[Dict[str, Any]] = None) -> S.PrimFunc:

@@ -1,0 +1,139 @@
+"""Mixture-of-Experts FFN layer on the mesh (BASELINE config 5: grouped-GEMM MoE, 8 experts,
+1/2/4/8 MI355X over xGMI).
+
+Per layer: router (softmax top-k) -> dispatch -> SwiGLU experts (tilelang grouped GEMMs,
+``tilelang.ops.moe``) -> weighted combine.  Parallel modes over the active mesh:
+
+* ``"local"`` — all experts on this rank (single GPU, or plain data parallel);
+* ``"ep"``    — expert parallel: rank r owns experts ``[r*E/W, (r+1)*E/W)``; tokens travel to
+                their experts and back with two variable-size all-to-alls (RCCL over xGMI,
+                ``parallel.collectives.all_to_all_v``) — the reference DeepSeek-V3.2
+                example's EP (``examples/deepseek_v32/inference/model.py:787-850``) uses an
+                all-reduce of the full output instead, moving W x more bytes;
+* ``"tp"``    — tensor parallel ("mesh cross-GPU tiles"): every rank holds 1/W of every
+                expert's FFN width, the down-projection's fp32 output tiles are summed across
+                the mesh INSIDE the GEMM kernel (``T.comm.all_reduce_tile``), so the reduction
+                of one tile overlaps the MMA of the next on the same GPU.
+
+Weights are random-initialised (no checkpoints are available); ``moe_reference`` is the
+plain PyTorch fp32 definition the kernels are tested against.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from ..ops.moe import expert_ffn
+
+
+@dataclass
+class MoEConfig:
+    hidden: int = 4096
+    ffn: int = 14336
+    n_experts: int = 8
+    topk: int = 2
+    dtype: torch.dtype = torch.bfloat16
+    block_M: int = 128
+
+
+def route(x: torch.Tensor, gate_w: torch.Tensor, topk: int):
+    """softmax(x Wg^T) top-k with renormalised weights -> (expert ids [T, k], weights [T, k])."""
+    logits = (x.float() @ gate_w.float().t())
+    probs = torch.softmax(logits, -1)
+    w, ids = torch.topk(probs, topk, dim=-1)
+    w = w / w.sum(-1, keepdim=True)
+    return ids, w
+
+
+def moe_reference(x, gate_w, w1, w2, topk):
+    """fp32 PyTorch definition (w1: [E, 2F, H] = [gate | up], w2: [E, H, F])."""
+    ids, wts = route(x, gate_w, topk)
+    xf = x.float()
+    out = torch.zeros_like(xf)
+    F = w1.shape[1] // 2
+    for e in range(w1.shape[0]):
+        tok, slot = torch.nonzero(ids == e, as_tuple=True)
+        if tok.numel() == 0:
+            continue
+        h = xf[tok] @ w1[e].float().t()
+        a = torch.nn.functional.silu(h[:, :F]) * h[:, F:]
+        out.index_add_(0, tok, (a @ w2[e].float().t()) * wts[tok, slot, None])
+    return out
+
+
+def init_moe_weights(cfg: MoEConfig, seed: int = 0):
+    """Full (gate [E, H], w1 [E, 2F, H], w2 [E, H, F]) on the CPU, deterministic in ``seed``."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    E, H, F = cfg.n_experts, cfg.hidden, cfg.ffn
+
+    def rnd(*shape, scale):
+        return (torch.randn(*shape, generator=g) * scale).to(cfg.dtype)
+
+    return rnd(E, H, scale=H ** -0.5), rnd(E, 2 * F, H, scale=H ** -0.5), rnd(E, H, F, scale=F ** -0.5)
+
+
+class MoELayer(torch.nn.Module):
+
+    def __init__(self, cfg: MoEConfig, parallel: str = "local", mesh=None, device="cuda", seed: int = 0):
+        super().__init__()
+        from ..parallel.mesh import current_mesh
+        self.cfg = cfg
+        self.parallel = parallel
+        self.mesh = mesh or (current_mesh() if parallel != "local" else None)
+        W = self.mesh.world if self.mesh is not None else 1
+        E, H, F = cfg.n_experts, cfg.hidden, cfg.ffn
+        if parallel == "ep" and E % W:
+            raise ValueError(f"{E} experts do not split over {W} ranks")
+        if parallel == "tp" and F % W:
+            raise ValueError(f"ffn {F} does not split over {W} ranks")
+        # full weights are generated identically on every rank, then sliced
+        gate_w, w1, w2 = init_moe_weights(cfg, seed)
+        self.gate_w = gate_w.to(device)
+        if parallel == "ep":
+            r = self.mesh.rank
+            n = E // W
+            self.local_experts = range(r * n, (r + 1) * n)
+            w1, w2 = w1[r * n:(r + 1) * n], w2[r * n:(r + 1) * n]
+        elif parallel == "tp":
+            r = self.mesh.rank
+            f = F // W
+            w1 = torch.cat([w1[:, r * f:(r + 1) * f], w1[:, F + r * f:F + (r + 1) * f]], 1)
+            w2 = w2[:, :, r * f:(r + 1) * f]
+        self.w1 = w1.contiguous().to(device)
+        self.w2 = w2.contiguous().to(device)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        cfg = self.cfg
+        T_, H = x.shape
+        ids, wts = route(x, self.gate_w, cfg.topk)
+        flat_ids = ids.reshape(-1)
+        tok = torch.arange(T_, device=x.device).repeat_interleave(cfg.topk)
+        rows = x[tok]
+        if self.parallel in ("local", "tp"):
+            y = expert_ffn(rows, flat_ids, self.w1, self.w2, cfg.block_M,
+                           reduce_mesh="all" if self.parallel == "tp" else None)
+        else:
+            y = self._ep(rows, flat_ids)
+        out = torch.zeros(T_, H, dtype=torch.float32, device=x.device)
+        out.index_add_(0, tok, y.float() * wts.reshape(-1, 1))
+        return out.to(x.dtype)
+
+    def _ep(self, rows, flat_ids):
+        from ..parallel import collectives as C
+        m = self.mesh
+        W = m.world
+        n = self.cfg.n_experts // W
+        dest = torch.div(flat_ids, n, rounding_mode="floor")
+        order = torch.argsort(dest, stable=True)
+        send_counts = torch.bincount(dest, minlength=W).tolist()
+        payload = rows[order]
+        local_e = (flat_ids[order] - dest[order] * n).to(torch.int32)
+        recv_rows, rc = C.all_to_all_v(payload, send_counts)
+        recv_e, _ = C.all_to_all_v(local_e.unsqueeze(1), send_counts)
+        y_local = expert_ffn(recv_rows, recv_e.squeeze(1).long(), self.w1, self.w2, self.cfg.block_M)
+        y_back, _ = C.all_to_all_v(y_local, rc)
+        y = torch.empty_like(y_back)
+        y[order] = y_back
+        return y

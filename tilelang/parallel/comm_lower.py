@@ -54,7 +54,7 @@ def op_slot_bytes(op) -> int:
     if isinstance(op, O.CommAllGatherOp):
         return op.size * op.send.buffer.dtype.bytes
     if isinstance(op, O.CommAllReduceOp):
-        ext = op.dst.static_extents()
+        ext = op.dst.static_extents()  # (whole tile when dim is None)
         n = 1
         for e in ext:
             n *= e
@@ -360,19 +360,22 @@ def lower_all_reduce(lw, op: O.CommAllReduceOp):
     from ..transform.lower_tile_op import _combine
     st = mesh_state(lw.ctx, op.mesh)
     cpu = lw.ctx.is_cpu
-    if op.tmp is None:
+    tile = op.dim is None  # all_reduce_tile: element-wise across cores, no local reduce
+    if op.tmp is None and not tile:
         raise CommLoweringError("T.comm.all_reduce without a partial buffer")
     _check_region(op.src, "all_reduce", cpu)
     _check_region(op.dst, "all_reduce", cpu)
     dirn = DIR[op.direction]
-    oi, tag, out = _begin(st, "all_reduce")
-    # 1) local reduce along dim into the partial
-    out.append(lw.lower_ReduceOp(O.ReduceOp(op.src, op.tmp, op.reduce_type, op.dim, True)))
+    oi, tag, out = _begin(st, "all_reduce_tile" if tile else "all_reduce")
+    part = op.src if tile else op.tmp
+    if not tile:
+        # 1) local reduce along dim into the partial
+        out.append(lw.lower_ReduceOp(O.ReduceOp(op.src, op.tmp, op.reduce_type, op.dim, True)))
     # 2) all-gather the partials into the workspace
     n = 1
-    for e in op.tmp.static_extents():
+    for e in part.static_extents():
         n *= e
-    out += _gather_phases(lw, st, oi, tag, op.tmp, n, dirn)
+    out += _gather_phases(lw, st, oi, tag, part, n, dirn)
     # 3) combine in member (core-id) order — identical on every rank
     view, decl, stride = _gathered_view(lw, st, oi, dirn, op.dst.buffer.dtype)
     G = _group_size(st, dirn)

@@ -363,6 +363,13 @@ class LayoutInference:
                     changed |= self.set_frag(s, self.frag[d], "copy")
         elif isinstance(op, O.CumSumOp):
             pass
+        elif isinstance(op, O.CommAllReduceOp) and op.dim is None:
+            s, d = op.src.buffer, op.dst.buffer
+            if _is_frag(s) and _is_frag(d):
+                if s in self.frag and d not in self.frag:
+                    changed |= self.set_frag(d, self.frag[s], "comm all_reduce_tile")
+                elif d in self.frag and s not in self.frag:
+                    changed |= self.set_frag(s, self.frag[d], "comm all_reduce_tile")
         elif isinstance(op, O.CommAllReduceOp) and op.tmp is not None:
             # partial = reduce(src, dim) gets the reduce layout; out follows the partial
             s, t, d = op.src.buffer, op.tmp.buffer, op.dst.buffer

@@ -1005,6 +1005,13 @@ class TileOpLowerer(Mutator):
             idx[p["cdim"]] = binop("+", idx[p["cdim"]], col)
             gidx = ctx.flat_index(src.buffer, idx)
             lds_off = binop("+", base_off, binop("*", chunk_base, epc))
+            if p.get("oob_bytes"):
+                # ragged outer dim: buffer LDS-DMA, lanes past the tensor end write zeros
+                rsrc = call("extern", ["tl::make_rsrc", L.BufferPtr(ctx.flat_of(src.buffer), 0),
+                                       IntImm(p["oob_bytes"], _dt.uint32)], _dt.handle)
+                voff = cast(binop("*", gidx, p["eb"]), _dt.uint32)
+                out.append(L.CallStmt("tl::buffer_lds16", [rsrc, voff, L.BufferPtr(ctx.flat_of(NB), lds_off)]))
+                continue
             out.append(L.CallStmt("tl::glds16", [L.BufferPtr(ctx.flat_of(src.buffer), gidx),
                                                  L.BufferPtr(ctx.flat_of(NB), lds_off)]))
         return S.SeqStmt(out)

@@ -136,17 +136,36 @@ def glds_plan(op: O.CopyOp, num_threads: int, ranges, target) -> Optional[dict]:
             return None
     if not divisible_by(src.region[cdim][0], epc):
         return None
-    # in-bounds proof for every dim
+    # in-bounds proof for every dim.  A data-dependent offset along the OUTERMOST tensor dim
+    # (MoE expert rows, expert ids) is still fine: leaving that dim leaves the tensor, so a
+    # buffer-resource LDS-DMA (hardware zero fill past num_records) gives exactly the
+    # zero-padded tile — no register staging needed.
     shape = sb.shape
+    oob = False
     for d, (m, e) in enumerate(src.region):
         b = bound(m, ranges)
         s = as_int(shape[d])
         ev = as_int(e)
         if b is None or s is None or ev is None or b[0] < 0 or b[1] + ev > s:
+            if d == 0 and ev is not None:
+                oob = True
+                continue
             return None
+    nbytes = None
+    if oob:
+        numel = 1
+        for s in shape:
+            if as_int(s) is None:
+                return None
+            numel *= as_int(s)
+        st0 = as_int(strides[0])
+        if st0 is None or sb.strides is not None or numel * eb >= (1 << 31):
+            return None
+        nbytes = numel * eb
     n_chunks = R * C * eb // 16
     nw = num_threads // 64
-    return dict(R=R, C=C, eb=eb, rdim=rdim, cdim=cdim, instrs=n_chunks // 64 // nw, nwaves=nw, cpr=C * eb // 16)
+    return dict(R=R, C=C, eb=eb, rdim=rdim, cdim=cdim, instrs=n_chunks // 64 // nw, nwaves=nw, cpr=C * eb // 16,
+                oob_bytes=nbytes)
 
 
 class _Ranges:
