@@ -1,3 +1,4 @@
+import glob
 import os
 import random
 import sys
@@ -5,7 +6,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (ROOT, os.path.join(ROOT, "examples", "gemm"), os.path.join(ROOT, "examples", "flash_attention")):
+# the repo root and every examples/<family> directory (examples are imported by module name)
+for p in [ROOT] + sorted(d for d in glob.glob(os.path.join(ROOT, "examples", "*")) if os.path.isdir(d)):
     if p not in sys.path:
         sys.path.insert(0, p)
 
@@ -28,7 +30,3 @@ def _seed():
     except ImportError:
         pass
     yield
-for _p in ("gemm_fp8", "deepseek_mla"):
-    _d = os.path.join(ROOT, "examples", _p)
-    if _d not in sys.path:
-        sys.path.insert(0, _d)

@@ -1,0 +1,87 @@
+"""MI355X numerics of the memory-bound / utility example kernels against PyTorch fp32 references."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _native():
+    from tilelang import _native
+    _native.runtime()
+
+
+def test_elementwise_add():
+    import example_elementwise_add as m
+    for dt in ("float32", "float16"):
+        k = m.elementwise_add(1024, 1024, in_dtype=dt, out_dtype=dt)
+        a = torch.randn(1024, 1024, device="cuda", dtype=getattr(torch, dt))
+        b = torch.randn(1024, 1024, device="cuda", dtype=getattr(torch, dt))
+        torch.testing.assert_close(k(a, b), a + b)
+
+
+def test_rms_norm():
+    import rms_norm as m
+    k = m.rms_norm(1024, 4096, 4)
+    x = torch.randn(1024, 4096, device="cuda")
+    torch.testing.assert_close(k(x), m.ref_program(x), rtol=1e-4, atol=1e-4)
+    k = m.rms_norm_splitk(256, 8192, 4, 512)
+    x = torch.randn(256, 8192, device="cuda")
+    torch.testing.assert_close(k(x), m.ref_program(x), rtol=1e-4, atol=1e-4)
+
+
+def test_online_softmax():
+    import online_softmax as m
+    k = m.online_softmax(512, 8192)
+    x = torch.randn(512, 8192, device="cuda")
+    torch.testing.assert_close(k(x), m.ref_program(x), rtol=1e-4, atol=1e-6)
+    k = m.softmax_rows(512, 1024)
+    x = torch.randn(512, 1024, device="cuda")
+    torch.testing.assert_close(k(x), m.ref_program(x), rtol=1e-4, atol=1e-6)
+
+
+def test_topk():
+    import example_topk as m
+    k = m.tl_topk(320, 128, 6, 16)
+    x = torch.rand(320, 128, device="cuda")
+    g, i = k(x)
+    rg, ri = m.ref_program(x, 6)
+    torch.testing.assert_close(g, rg)
+    torch.testing.assert_close(i, ri)
+
+
+def test_per_token_cast_fp8():
+    import example_per_token_cast_to_fp8 as m
+    k = m.per_token_cast_to_fp8(1024, 1024, 8)
+    x = torch.randn(1024, 1024, device="cuda")
+    q, s = k(x)
+    rq, rs = m.ref_program(x)
+    torch.testing.assert_close(s, rs)
+    torch.testing.assert_close(q.float(), rq.float(), rtol=0, atol=0)
+
+
+def test_gemv():
+    import example_gemv as m
+    k = m.gemv(4096, 4096)
+    A = torch.randn(4096, 4096, device="cuda", dtype=torch.float16)
+    x = torch.randn(4096, device="cuda", dtype=torch.float16)
+    torch.testing.assert_close(k(A, x).float(), m.ref_program(A, x).float(), rtol=1e-2, atol=1e-1)
+
+
+@pytest.mark.parametrize("variant", ["tile", "elementwise"])
+def test_splitk(variant):
+    import example_tilelang_gemm_splitk as m
+    fn = m.matmul_splitk if variant == "tile" else m.matmul_splitk_elementwise
+    k = fn(512, 512, 4096, split_k=4)
+    a = torch.randn(512, 4096, device="cuda", dtype=torch.float16)
+    b = torch.randn(4096, 512, device="cuda", dtype=torch.float16)
+    c = torch.zeros(512, 512, device="cuda")
+    k(a, b, c)
+    torch.testing.assert_close(c, a.float() @ b.float(), rtol=1e-2, atol=1e-1)
+
+
+def test_hadamard():
+    import example_hadamard as m
+    k = m.hadamard(8, 4096)
+    x = torch.randn(8, 4096, device="cuda")
+    torch.testing.assert_close(k(x), m.ref_program(x), rtol=1e-3, atol=1e-2)

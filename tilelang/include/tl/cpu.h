@@ -11,6 +11,60 @@
 typedef _Float16 half_t;
 typedef __bf16 bfloat16_t;
 
+// OCP fp8 on the host: E exponent bits, M mantissa bits, FN = "finite" (no inf, NaN=S.1111.111).
+// Round-to-nearest-even; overflow -> NaN (fn) / inf (e5m2), as torch's float8 casts.
+template <int E, int M, bool FN> struct fp8_host_t {
+  uint8_t v;
+  static constexpr int kBias = (1 << (E - 1)) - 1;
+  fp8_host_t() = default;
+  fp8_host_t(float f) { v = encode(f); }
+  fp8_host_t(double f) { v = encode((float)f); }
+  fp8_host_t(int f) { v = encode((float)f); }
+  operator float() const { return decode(v); }
+  static float max_finite() {
+    return FN ? std::ldexp(1.0f + (float)((1 << M) - 2) / (1 << M), (1 << E) - 1 - kBias)
+              : std::ldexp(1.0f + (float)((1 << M) - 1) / (1 << M), (1 << E) - 2 - kBias);
+  }
+  static uint8_t encode(float f) {
+    const uint8_t sign = std::signbit(f) ? 0x80 : 0;
+    const uint8_t nan = FN ? 0x7F : (uint8_t)((((1 << E) - 1) << M) | 1);
+    const uint8_t inf = FN ? nan : (uint8_t)(((1 << E) - 1) << M);
+    if (std::isnan(f)) return sign | nan;
+    float a = std::fabs(f);
+    if (std::isinf(a)) return sign | inf;
+    int e;
+    (void)std::frexp(a, &e);  // a = m * 2^e, m in [0.5, 1)
+    e -= 1;                   // a = 1.x * 2^e
+    uint32_t code;
+    if (a == 0.0f) return sign;
+    if (e < 1 - kBias) {  // subnormal
+      float q = std::nearbyint(std::ldexp(a, kBias - 1 + M));
+      code = (uint32_t)q;  // may round up into the smallest normal (code == 1 << M)
+    } else {
+      float q = std::nearbyint((std::ldexp(a, -e) - 1.0f) * (1 << M));
+      if (q >= (float)(1 << M)) {
+        q = 0;
+        ++e;
+      }
+      code = ((uint32_t)(e + kBias) << M) | (uint32_t)q;
+    }
+    const uint32_t max_code = FN ? ((1u << (E + M)) - 2) : (((1u << E) - 2) << M | ((1u << M) - 1));
+    if (code > max_code) return sign | inf;
+    return sign | (uint8_t)code;
+  }
+  static float decode(uint8_t c) {
+    const float s = (c & 0x80) ? -1.0f : 1.0f;
+    const int ex = (c >> M) & ((1 << E) - 1);
+    const int mt = c & ((1 << M) - 1);
+    if (FN && ex == (1 << E) - 1 && mt == (1 << M) - 1) return NAN;
+    if (!FN && ex == (1 << E) - 1) return mt ? NAN : s * INFINITY;
+    if (ex == 0) return s * std::ldexp((float)mt, 1 - kBias - M);
+    return s * std::ldexp(1.0f + (float)mt / (1 << M), ex - kBias);
+  }
+};
+typedef fp8_host_t<4, 3, true> fp8_e4_t;
+typedef fp8_host_t<5, 2, false> fp8_e5_t;
+
 namespace tl {
 
 template <typename T> inline T max_(T a, T b) { return a > b ? a : b; }

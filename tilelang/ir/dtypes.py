@@ -213,8 +213,8 @@ _HIP_NAMES = {
 
 # CPU C++ spellings (include/tl/cpu.h)
 _CPU_NAMES = dict(_HIP_NAMES)
-_CPU_NAMES.update({"float16": "half_t", "bfloat16": "bfloat16_t", "float8_e4m3fn": "uint8_t",
-                   "float8_e5m2": "uint8_t"})
+_CPU_NAMES.update({"float16": "half_t", "bfloat16": "bfloat16_t", "float8_e4m3fn": "fp8_e4_t",
+                   "float8_e5m2": "fp8_e5_t"})
 
 
 def hip_type(dt) -> str:

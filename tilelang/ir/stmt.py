@@ -23,7 +23,7 @@ class SeqStmt(Stmt):
     def __init__(self, stmts: List[Stmt]):
         flat = []
         for s in stmts:
-            if isinstance(s, SeqStmt):
+            if isinstance(s, SeqStmt) and not getattr(s, "scoped", False):
                 flat.extend(s.stmts)
             elif s is not None:
                 flat.append(s)

@@ -179,6 +179,9 @@ def warp_reduce_bitor(value):
 
 
 def _atomic(op, dst, value, memory_order=None, return_prev=False):
+    if isinstance(dst, BufferLoad) and isinstance(value, (Buffer, BufferRegion)):
+        # tile form with a point destination: T.atomic_add(C[by * bm, bx * bn], C_local)
+        dst = to_region(dst, _extents_of(value))
     if isinstance(dst, BufferLoad):
         # scalar atomic on one element
         e = call(f"tl.atomic_{op}", [dst, convert(value)], dst.dtype, memory_order=memory_order,

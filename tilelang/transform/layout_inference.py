@@ -157,6 +157,57 @@ def lift_layout(buf_layout: Fragment, dim_map: List[Optional[int]], loop_shape: 
         return None
 
 
+def extend_layout(buf_layout: Fragment, dim_map: List[Optional[int]], loop_shape: List[int],
+                  vec: int = 4) -> Optional[Fragment]:
+    """Loop partition for a nest whose only laid-out fragment covers a *subset* of the loop
+    dims (e.g. ``x[i, j] * row_scale[i]``): keep the buffer's placement of its dims, spread
+    the missing loop dims over the buffer's replication threads (lane-fastest) and registers
+    (innermost ``vec`` elements contiguous), so every thread owns what it iterates."""
+    used = {ld: bd for bd, ld in enumerate(dim_map) if ld is not None}
+    if len(used) != len([d for d in dim_map if d is not None]):
+        return None
+    missing = [ld for ld in range(len(loop_shape)) if ld not in used and loop_shape[ld] > 1]
+    td = []
+    for d in buf_layout.thread_digits:
+        if d.dim < 0:
+            td.append(["rep", d.size])
+        else:
+            td.append(Digit(dim_map[d.dim], d.stride, d.size))
+    ld_ = [Digit(dim_map[d.dim], d.stride, d.size) for d in buf_layout.local_digits]
+    import math as _m
+    tail_local = []
+    for md in reversed(missing):
+        E = loop_shape[md]
+        stride = 1
+        v = _m.gcd(E, max(1, vec)) if md == len(loop_shape) - 1 else 1
+        if v > 1:
+            tail_local.insert(0, Digit(md, 1, v))
+            stride = v
+        rem = E // v
+        # fill replication thread digits, least significant first
+        for k in range(len(td) - 1, -1, -1):
+            if rem == 1:
+                break
+            ent = td[k]
+            if isinstance(ent, list):
+                t = _m.gcd(ent[1], rem)
+                if t > 1:
+                    new = []
+                    if ent[1] // t > 1:
+                        new.append(["rep", ent[1] // t])
+                    new.append(Digit(md, stride, t))
+                    td[k:k + 1] = new
+                    stride *= t
+                    rem //= t
+        if rem > 1:
+            ld_.insert(0, Digit(md, stride, rem))
+    thread = [Digit(-1, 1, e[1]) if isinstance(e, list) else e for e in td]
+    try:
+        return Fragment(loop_shape, thread, ld_ + tail_local, buf_layout.name + "_ext")
+    except ValueError:
+        return None
+
+
 def reduce_dst_layout(src: Fragment, dim: int, dst_shape: List[int]) -> Fragment:
     """Layout of reduce(src, dim): the reduced dim's digits become replication (threads)
     or disappear (registers)."""
@@ -221,6 +272,12 @@ class LayoutInference:
         if not kernel:
             return {}
         kernel = kernel[0]
+        # layouts are per-compilation results: forget those of an earlier lowering of the same
+        # PrimFunc (e.g. for another target); only user annotations persist
+        for s in S.walk(kernel):
+            if isinstance(s, S.AllocStmt) and not getattr(s.buffer, "layout_annotated", False):
+                if s.buffer.scope in ("fragment", "shared"):
+                    s.buffer.layout = None
         frags = [s.buffer for s in S.walk(kernel) if isinstance(s, S.AllocStmt) and _is_frag(s.buffer)]
         for b in frags:
             if getattr(b, "layout_annotated", False) and isinstance(b.layout, Fragment):
@@ -245,10 +302,18 @@ class LayoutInference:
                     changed |= self.infer_gemm(op, level="common")
             if not changed:
                 break
-        # free: unconstrained fragments in nests/copies get default layouts
-        for _ in range(32):
+        # free: unconstrained fragments in nests/copies get default layouts.  Larger iteration
+        # domains choose first (the reference's per-component root search): a 2-D tile nest
+        # fixes the partition its 1-D row statistics then inherit, not the other way round.
+        def _domain(n):
+            sz = 1
+            for e in n.extents:
+                sz *= e if e is not None else 1
+            return -sz
+        free_order = sorted(nests, key=_domain)
+        for _ in range(64):
             changed = False
-            for n in nests:
+            for n in free_order:
                 changed |= self.infer_nest(n, free=True)
                 if changed:
                     break
@@ -417,6 +482,19 @@ class LayoutInference:
                         n.layout = lifted
                         changed = True
                         break
+            if n.layout is None and free and n.fragment_accesses():
+                # a laid-out fragment covering part of the loop dims: extend its partition
+                eb = max(b.dtype.bytes for b, _, _ in n.fragment_accesses())
+                for b, idx, _ in n.fragment_accesses():
+                    if b in self.frag and all(as_int(m) == 0 for m in n.mins):
+                        dm = _index_map(idx, n.vars)
+                        if dm is None:
+                            continue
+                        ext = extend_layout(self.frag[b], dm, shape, max(1, 16 // eb))
+                        if ext is not None and ext.num_threads == self.T:
+                            n.layout = ext
+                            changed = True
+                            break
             if n.layout is None and free and n.fragment_accesses():
                 # choose a default partition for the nest
                 unknown = [b for b, _, _ in n.fragment_accesses() if b not in self.frag]

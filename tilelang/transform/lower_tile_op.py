@@ -28,7 +28,7 @@ from ..ir.buffer import Buffer, BufferRegion
 from ..ir.expr import (BufferLoad, Call, IntImm, PrimExpr, Var, as_int, binop, call, cast, compile_py, const,
                        convert, divisible_by, evaluate, free_vars, logical_and, select, substitute, transform,
                        post_order, loads_of, modular)
-from ..layout.fragment import Fragment, make_linear_fragment
+from ..layout.fragment import Digit, Fragment, make_linear_fragment
 from ..layout.layout import Layout, LinearLayout, SwizzleLayout
 from .layout_inference import ParallelNest, collect_nests, lift_layout, _index_map
 from .pipeline import AsyncCopyOp, StagedCopyOp
@@ -79,6 +79,17 @@ def _combine(kind, a, b):
     if kind == "bitxor":
         return a ^ b
     raise ValueError(kind)
+
+
+def _tree_combine(kind, xs):
+    """Balanced reduction tree: log-depth dependency chains (ILP) and shallow expressions."""
+    xs = list(xs)
+    while len(xs) > 1:
+        nxt = [_combine(kind, xs[i], xs[i + 1]) for i in range(0, len(xs) - 1, 2)]
+        if len(xs) % 2:
+            nxt.append(xs[-1])
+        xs = nxt
+    return xs[0]
 
 
 def _prod(xs):
@@ -179,6 +190,7 @@ class LowerCtx:
         b = Buffer(f"red_ws{self.ws_counter}", [n], dtype, "shared")
         b.layout = LinearLayout([n])
         b._auto_name = False
+        self.flat[b] = b  # already flat: accesses and the allocation are the same buffer
         self.extra_allocs.append(b)
         return b
 
@@ -300,6 +312,10 @@ class _IterRewriter(Mutator):
 
     def visit_LetStmt(self, s):
         return S.LetStmt(s.var, self.expr(s.value))
+
+    def visit_EvaluateStmt(self, s):
+        r = _rewrite_atomic(self, s)
+        return r if r is not None else S.EvaluateStmt(self.expr(s.expr))
 
     def visit_ForStmt(self, s):
         return S.ForStmt(s.var, self.expr(s.min), self.expr(s.extent), s.kind, self.stmt(s.body), s.annotations)
@@ -785,39 +801,31 @@ class TileOpLowerer(Mutator):
         sl, dl = ctx.local_of(sb), ctx.local_of(db)
         dshape = db.static_shape()
         squeeze_dim = len(dshape) == len(S_lay.shape)  # dst keeps a unit dim
-        # group source registers by destination register (must be thread-uniform)
-        groups: Dict[int, List[int]] = {}
-        for t in range(0, ctx.T, max(1, ctx.T // 16)):
-            pass
-        dmap0 = D_lay.thread_local_map(0)
-        for r in range(S_lay.local_size):
-            owners = set()
-            for t in _sample_threads(ctx.T):
-                idx = S_lay.inverse(t, r)
-                didx = list(idx)
-                if squeeze_dim:
-                    didx[dim] = 0
-                else:
-                    didx.pop(dim)
-                m = D_lay.thread_local_map(t)
-                li = m.get(tuple(didx))
-                if li is None:
-                    raise LoweringError(f"reduce: thread {t} lacks destination element {didx} of {db.name}")
-                owners.add(li)
-            if len(owners) != 1:
-                raise LoweringError("reduce: non-uniform register mapping")
-            groups.setdefault(owners.pop(), []).append(r)
+        # group source registers by destination register (must be thread-uniform).  When the
+        # destination was laid out by another consumer first, reduce into the natural layout
+        # (the reduced dim's digits dropped) and redistribute through LDS afterwards.
+        groups = self._reduce_groups(S_lay, D_lay, dim, squeeze_dim)
+        redistribute = None
+        if groups is None:
+            from .layout_inference import reduce_dst_layout
+            redistribute = D_lay
+            D_lay = reduce_dst_layout(S_lay, dim, dshape)
+            if D_lay.num_threads < ctx.T:
+                D_lay = D_lay.replicate(ctx.T // D_lay.num_threads)
+            groups = self._reduce_groups(S_lay, D_lay, dim, squeeze_dim)
+            if groups is None:
+                raise LoweringError(f"reduce: cannot map {sb.name} onto a reduced layout")
         out = []
         accs = {}
         dt = sb.dtype
         for d, rs in sorted(groups.items()):
-            acc = None
+            xs = []
             for r in rs:
                 x = BufferLoad(sl, [IntImm(r)])
                 if kind in ("abssum", "absmax"):
                     x = call("abs", [x], dt)
-                acc = x if acc is None else _combine(kind, acc, x)
-            accs[d] = acc
+                xs.append(x)
+            accs[d] = _tree_combine(kind, xs)
         # cross-thread: thread digits of the reduced dim
         lane_mask, wave_digits = _reduce_thread_masks(S_lay, dim)
         opname = _REDUCE_OPS[kind][0]
@@ -856,6 +864,23 @@ class TileOpLowerer(Mutator):
                 new_vals[d] = v3
             out.append(L.CallStmt("tl::sync_threads", []))
             red_vals = new_vals
+        if redistribute is not None:
+            # natural-layout results -> LDS (logical row-major) -> the consumer's layout
+            n = _prod(dshape)
+            ws = ctx.new_workspace(n, dt)
+            wsf = ctx.flat_of(ws)
+            out.append(L.CallStmt("tl::sync_threads", []))
+            for d, v in red_vals.items():
+                idx = D_lay.inverse(ctx.tid, d)
+                out.append(S.StoreStmt(wsf, [_row_major(idx, dshape)], v))
+            out.append(L.CallStmt("tl::sync_threads", []))
+            red_vals = {}
+            for r in range(redistribute.local_size):
+                idx = redistribute.inverse(ctx.tid, r)
+                v = Var(f"redx{r}", dt, nonneg=False)
+                out.append(S.LetStmt(v, BufferLoad(wsf, [_row_major(idx, dshape)])))
+                red_vals[r] = v
+            out.append(L.CallStmt("tl::sync_threads", []))
         for d, v in red_vals.items():
             if op.clear:
                 out.append(S.StoreStmt(dl, [IntImm(d)], cast(v, db.dtype)))
@@ -863,6 +888,32 @@ class TileOpLowerer(Mutator):
                 out.append(S.StoreStmt(dl, [IntImm(d)], cast(_combine(kind, BufferLoad(dl, [IntImm(d)]), v),
                                                              db.dtype)))
         return _scoped(S.SeqStmt(out))
+
+    def _reduce_groups(self, S_lay: Fragment, D_lay: Fragment, dim: int, squeeze_dim: bool):
+        """src register -> dst register grouping, or None when some thread does not own the
+        destination of an element it holds (the layouts are not reduce-compatible)."""
+        groups: Dict[int, List[int]] = {}
+        dmaps = {}
+        for r in range(S_lay.local_size):
+            owners = set()
+            for t in _sample_threads(self.ctx.T):
+                idx = S_lay.inverse(t, r)
+                didx = list(idx)
+                if squeeze_dim:
+                    didx[dim] = 0
+                else:
+                    didx.pop(dim)
+                m = dmaps.get(t)
+                if m is None:
+                    m = dmaps[t] = D_lay.thread_local_map(t)
+                li = m.get(tuple(didx))
+                if li is None:
+                    return None
+                owners.add(li)
+            if len(owners) != 1:
+                return None
+            groups.setdefault(owners.pop(), []).append(r)
+        return groups
 
     def lower_reduce_simt(self, op: O.ReduceOp):
         """Reduction over shared/local buffers: each thread reduces whole rows serially."""
@@ -1186,11 +1237,33 @@ def _squeeze_fragment(lay: Fragment, shape) -> Fragment:
     return Fragment([shape[d] for d in keep], td, ld, lay.name)
 
 
+def _rewrite_atomic(rw, s: S.EvaluateStmt):
+    """``tl.atomic_*(buf[idx], v)``: the destination is an address, never a guarded load --
+    an out-of-bounds destination skips the whole atomic instead."""
+    e = s.expr
+    if not (isinstance(e, Call) and isinstance(e.op, str) and e.op.startswith("tl.atomic_") and e.args
+            and isinstance(e.args[0], BufferLoad)):
+        return None
+    ld = e.args[0]
+    b = ld.buffer
+    if b.scope in ("fragment", "local", "var"):
+        return None
+    idx = [rw.expr(i) for i in ld.indices]
+    dst = BufferLoad(rw.ctx.flat_of(b), [rw.ctx.flat_index(b, idx)])
+    new = S.EvaluateStmt(Call(e.op, [dst] + [rw.expr(a) for a in e.args[1:]], e.dtype, dict(e.attrs)))
+    g = safe_guard(rw.ctx, b, idx)
+    return S.IfStmt(g, new) if g is not None else new
+
+
 class _SimtRewriter(Mutator):
 
     def __init__(self, ctx, vmap):
         self.ctx = ctx
         self.vmap = vmap
+
+    def visit_EvaluateStmt(self, s):
+        r = _rewrite_atomic(self, s)
+        return r if r is not None else S.EvaluateStmt(self.expr(s.expr))
 
     def _acc(self, n):
         if isinstance(n, BufferLoad):
@@ -1247,9 +1320,23 @@ def _reduce_thread_masks(lay: Fragment, dim: int):
                 lane_mask |= w << b
         elif w >= 64:
             wave_digits.append((d, w))
+        elif 64 % w == 0 and d.size % (64 // w) == 0:
+            # the digit straddles the wave boundary: its low part is reduced with lane
+            # shuffles, its high part across waves through LDS
+            lo = 64 // w
+            for b in range(int(math.log2(lo))):
+                lane_mask |= w << b
+            wave_digits.append((Digit(d.dim, d.stride * lo, d.size // lo), 64))
         else:
             raise LoweringError("reduction digit straddles the wave boundary")
     return lane_mask, wave_digits
+
+
+def _row_major(idx, shape) -> PrimExpr:
+    acc = None
+    for i, s in zip(idx, shape):
+        acc = convert(i) if acc is None else binop("+", binop("*", acc, s), i)
+    return acc if acc is not None else IntImm(0)
 
 
 def _replica_masks(lay: Fragment):
