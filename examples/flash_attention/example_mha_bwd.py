@@ -1,0 +1,273 @@
+"""FlashAttention-2 backward (reference: examples/flash_attention/example_mha_bwd_bshd.py,
+examples/amd/example_amd_flash_attn_bwd.py) on MI355X, wired into ``torch.autograd``.
+
+Three kernels, Q/K/V/O/dO all [batch, seq, heads, dim] (bshd):
+
+* ``flashattn_fwd``       -- forward that also writes the base-2 log-sum-exp per row;
+* ``flashattn_bwd_preprocess`` -- Delta = rowsum(O * dO) (one HBM pass);
+* ``flashattn_bwd``       -- one block per (KV tile, head, batch).  K and V stay resident in
+  LDS; Q/dO tiles stream through the LDS-DMA pipeline.  Per step (everything transposed so the
+  KV rows are the MFMA M dimension and the per-KV-row accumulators dK/dV stay in AGPRs):
+      P^T  = exp2(K Q^T * scale - lse)           (ss GEMM, FullRow: whole rows per wave)
+      dP^T = V dO^T
+      dV  += P^T dO                               (register-A GEMM: accumulator reused as operand)
+      dS^T = P^T * (dP^T - Delta) * sm_scale
+      dK  += dS^T Q
+      dQ  += dS K     (dS^T staged through LDS, read transposed with ds_read_b64_tr_b16,
+                       fp32 atomics into dQ -- many KV blocks contribute to one Q row)
+* dQ (fp32) is cast back to the input dtype by a copy kernel.
+"""
+import argparse
+
+import tilelang
+import tilelang.language as T
+
+LOG2E = 1.44269504
+
+
+@tilelang.jit(out_idx=[3, 4])
+def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=256, dtype="float16"):
+    scale = (1.0 / dim)**0.5 * LOG2E
+    shape = [batch, seq_len, heads, dim]
+    accum_dtype = "float"
+
+    @T.prim_func
+    def flash_fwd(Q: T.Tensor(shape, dtype), K: T.Tensor(shape, dtype), V: T.Tensor(shape, dtype),
+                  Output: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype)):
+        with T.Kernel(T.ceildiv(seq_len, block_M), heads, batch, threads=threads) as (bx, by, bz):
+            Q_shared = T.alloc_shared([block_M, dim], dtype)
+            K_shared = T.alloc_shared([block_N, dim], dtype)
+            V_shared = T.alloc_shared([block_N, dim], dtype)
+            acc_s = T.alloc_fragment([block_M, block_N], accum_dtype)
+            acc_s_cast = T.alloc_fragment([block_M, block_N], dtype)
+            acc_o = T.alloc_fragment([block_M, dim], accum_dtype)
+            scores_max = T.alloc_fragment([block_M], accum_dtype)
+            scores_max_prev = T.alloc_fragment([block_M], accum_dtype)
+            scores_scale = T.alloc_fragment([block_M], accum_dtype)
+            scores_sum = T.alloc_fragment([block_M], accum_dtype)
+            logsum = T.alloc_fragment([block_M], accum_dtype)
+            T.copy(Q[bz, bx * block_M:(bx + 1) * block_M, by, :], Q_shared)
+            T.fill(acc_o, 0)
+            T.fill(logsum, 0)
+            T.fill(scores_max, -T.infinity(accum_dtype))
+            loop_range = T.ceildiv((bx + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N)
+            for k in T.Pipelined(loop_range, num_stages=2):
+                T.copy(K[bz, k * block_N:(k + 1) * block_N, by, :], K_shared)
+                if is_causal:
+                    for i, j in T.Parallel(block_M, block_N):
+                        acc_s[i, j] = T.if_then_else(bx * block_M + i >= k * block_N + j, 0, -T.infinity(accum_dtype))
+                else:
+                    T.clear(acc_s)
+                T.gemm(Q_shared, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.copy(V[bz, k * block_N:(k + 1) * block_N, by, :], V_shared)
+                T.copy(scores_max, scores_max_prev)
+                T.reduce_max(acc_s, scores_max, dim=1, clear=False)
+                for i in T.Parallel(block_M):
+                    scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
+                for i, j in T.Parallel(block_M, dim):
+                    acc_o[i, j] *= scores_scale[i]
+                for i, j in T.Parallel(block_M, block_N):
+                    acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
+                T.reduce_sum(acc_s, scores_sum, dim=1)
+                for i in T.Parallel(block_M):
+                    logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
+                T.copy(acc_s, acc_s_cast)
+                T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
+            for i, j in T.Parallel(block_M, dim):
+                acc_o[i, j] /= logsum[i]
+            T.copy(acc_o, Output[bz, bx * block_M:(bx + 1) * block_M, by, :])
+            for i in T.Parallel(block_M):
+                logsum[i] = T.log2(logsum[i]) + scores_max[i] * scale
+            T.copy(logsum, lse[bz, by, bx * block_M:(bx + 1) * block_M])
+
+    return flash_fwd
+
+
+@tilelang.jit(out_idx=[2])
+def flashattn_bwd_preprocess(batch, heads, seq_len, dim, blk=32, threads=256, dtype="float16"):
+    shape = [batch, seq_len, heads, dim]
+
+    @T.prim_func
+    def flash_bwd_prep(O: T.Tensor(shape, dtype), dO: T.Tensor(shape, dtype),
+                       Delta: T.Tensor([batch, heads, seq_len], "float")):
+        with T.Kernel(heads, T.ceildiv(seq_len, blk), batch, threads=threads) as (bx, by, bz):
+            o = T.alloc_fragment([blk, dim], dtype)
+            do = T.alloc_fragment([blk, dim], dtype)
+            acc = T.alloc_fragment([blk, dim], "float")
+            delta = T.alloc_fragment([blk], "float")
+            T.copy(O[bz, by * blk:(by + 1) * blk, bx, :], o)
+            T.copy(dO[bz, by * blk:(by + 1) * blk, bx, :], do)
+            for i, j in T.Parallel(blk, dim):
+                acc[i, j] = T.Cast("float", o[i, j]) * T.Cast("float", do[i, j])
+            T.reduce_sum(acc, delta, 1)
+            T.copy(delta, Delta[bz, bx, by * blk:(by + 1) * blk])
+
+    return flash_bwd_prep
+
+
+@tilelang.jit(out_idx=[1])
+def flashattn_bwd_postprocess(batch, heads, seq_len, dim, blk=64, threads=256, dtype="float16"):
+    shape = [batch, seq_len, heads, dim]
+
+    @T.prim_func
+    def flash_bwd_post(dQ: T.Tensor(shape, "float"), dQ_out: T.Tensor(shape, dtype)):
+        with T.Kernel(T.ceildiv(seq_len, blk), heads, batch, threads=threads) as (bx, by, bz):
+            t = T.alloc_fragment([blk, dim], "float")
+            tc = T.alloc_fragment([blk, dim], dtype)
+            T.copy(dQ[bz, bx * blk:(bx + 1) * blk, by, :], t)
+            T.copy(t, tc)
+            T.copy(tc, dQ_out[bz, bx * blk:(bx + 1) * blk, by, :])
+
+    return flash_bwd_post
+
+
+@tilelang.jit
+def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=64, block_N=64, threads=256, num_stages=2,
+                  dtype="float16"):
+    sm_scale = (1.0 / dim)**0.5
+    scale = sm_scale * LOG2E
+    shape = [batch, seq_len, heads, dim]
+    accum_dtype = "float"
+
+    @T.prim_func
+    def flash_bwd(Q: T.Tensor(shape, dtype), K: T.Tensor(shape, dtype), V: T.Tensor(shape, dtype),
+                  dO: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
+                  Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dQ: T.Tensor(shape, accum_dtype),
+                  dK: T.Tensor(shape, dtype), dV: T.Tensor(shape, dtype)):
+        with T.Kernel(heads, T.ceildiv(seq_len, block_M), batch, threads=threads) as (bx, by, bz):
+            K_shared = T.alloc_shared([block_M, dim], dtype)
+            V_shared = T.alloc_shared([block_M, dim], dtype)
+            q = T.alloc_shared([block_N, dim], dtype)
+            do = T.alloc_shared([block_N, dim], dtype)
+            dsT_shared = T.alloc_shared([block_M, block_N], dtype)
+            lse_shared = T.alloc_shared([block_N], accum_dtype)
+            delta = T.alloc_shared([block_N], accum_dtype)
+            qkT = T.alloc_fragment([block_M, block_N], accum_dtype)
+            dsT = T.alloc_fragment([block_M, block_N], accum_dtype)
+            qkT_cast = T.alloc_fragment([block_M, block_N], dtype)
+            dsT_cast = T.alloc_fragment([block_M, block_N], dtype)
+            dv = T.alloc_fragment([block_M, dim], accum_dtype)
+            dk = T.alloc_fragment([block_M, dim], accum_dtype)
+            dq = T.alloc_fragment([block_N, dim], accum_dtype)
+            dv_cast = T.alloc_fragment([block_M, dim], dtype)
+            dk_cast = T.alloc_fragment([block_M, dim], dtype)
+
+            T.copy(K[bz, by * block_M:(by + 1) * block_M, bx, :], K_shared)
+            T.copy(V[bz, by * block_M:(by + 1) * block_M, bx, :], V_shared)
+            T.clear(dv)
+            T.clear(dk)
+            loop_st = T.floordiv(by * block_M, block_N) if is_causal else 0
+            loop_ed = T.ceildiv(seq_len, block_N)
+            for k in T.Pipelined(loop_st, loop_ed, num_stages=num_stages):
+                T.copy(Q[bz, k * block_N:(k + 1) * block_N, bx, :], q)
+                T.clear(qkT)
+                T.gemm(K_shared, q, qkT, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.copy(lse[bz, bx, k * block_N:(k + 1) * block_N], lse_shared)
+                for i, j in T.Parallel(block_M, block_N):
+                    qkT[i, j] = T.exp2(qkT[i, j] * scale - lse_shared[j])
+                if is_causal:
+                    for i, j in T.Parallel(block_M, block_N):
+                        qkT[i, j] = T.if_then_else(by * block_M + i <= k * block_N + j, qkT[i, j], 0)
+                T.copy(dO[bz, k * block_N:(k + 1) * block_N, bx, :], do)
+                T.clear(dsT)
+                T.gemm(V_shared, do, dsT, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.copy(qkT, qkT_cast)
+                T.gemm(qkT_cast, do, dv, policy=T.GemmWarpPolicy.FullRow)
+                T.copy(Delta[bz, bx, k * block_N:(k + 1) * block_N], delta)
+                for i, j in T.Parallel(block_M, block_N):
+                    dsT_cast[i, j] = qkT[i, j] * (dsT[i, j] - delta[j]) * sm_scale
+                T.gemm(dsT_cast, q, dk, policy=T.GemmWarpPolicy.FullRow)
+                T.copy(dsT_cast, dsT_shared)
+                T.clear(dq)
+                T.gemm(dsT_shared, K_shared, dq, transpose_A=True)
+                T.atomic_add(dQ[bz, k * block_N:(k + 1) * block_N, bx, :], dq)
+            T.copy(dv, dv_cast)
+            T.copy(dk, dk_cast)
+            T.copy(dv_cast, dV[bz, by * block_M:(by + 1) * block_M, bx, :])
+            T.copy(dk_cast, dK[bz, by * block_M:(by + 1) * block_M, bx, :])
+
+    return flash_bwd
+
+
+class _attention:
+    """torch.autograd.Function built lazily (keeps this module importable without a GPU)."""
+    fn = None
+
+    @classmethod
+    def get(cls):
+        if cls.fn is None:
+            import torch
+
+            class Attn(torch.autograd.Function):
+
+                @staticmethod
+                def forward(ctx, q, k, v, causal):
+                    B, S, H, D = q.shape
+                    dt = "bfloat16" if q.dtype == torch.bfloat16 else "float16"
+                    o, lse = flashattn_fwd(B, H, S, D, causal, dtype=dt)(q, k, v)
+                    ctx.save_for_backward(q, k, v, o, lse)
+                    ctx.causal = causal
+                    return o
+
+                @staticmethod
+                def backward(ctx, do):
+                    q, k, v, o, lse = ctx.saved_tensors
+                    B, S, H, D = q.shape
+                    dt = "bfloat16" if q.dtype == torch.bfloat16 else "float16"
+                    do = do.contiguous()
+                    delta = flashattn_bwd_preprocess(B, H, S, D, dtype=dt)(o, do)
+                    dq = torch.zeros(B, S, H, D, dtype=torch.float32, device=q.device)
+                    dk = torch.empty_like(q)
+                    dv = torch.empty_like(q)
+                    flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt)(q, k, v, do, lse, delta, dq, dk, dv)
+                    return flashattn_bwd_postprocess(B, H, S, D, dtype=dt)(dq), dk, dv, None
+
+            cls.fn = Attn
+        return cls.fn
+
+
+def attention(q, k, v, causal=False):
+    return _attention.get().apply(q, k, v, causal)
+
+
+def ref_program(Q, K, V, is_causal):
+    import torch
+    dim = Q.size(-1)
+    scores = torch.einsum("bqhd,bkhd->bhqk", Q.float(), K.float()) / dim**0.5
+    if is_causal:
+        s = Q.size(1)
+        mask = torch.tril(torch.ones(s, s, device=scores.device))
+        scores = scores.masked_fill(mask == 0, float("-inf"))
+    return torch.einsum("bhqk,bkhd->bqhd", torch.softmax(scores, dim=-1), V.float()).to(Q.dtype)
+
+
+def main(batch=8, heads=32, seq_len=1024, dim=64, causal=False):
+    import torch
+    flops = 5 * 2.0 * batch * heads * seq_len * seq_len * dim * (0.5 if causal else 1.0)
+    Q = torch.randn(batch, seq_len, heads, dim, dtype=torch.half, device="cuda").requires_grad_()
+    K = torch.randn_like(Q).requires_grad_()
+    V = torch.randn_like(Q).requires_grad_()
+    dO = torch.randn_like(Q)
+    O = attention(Q, K, V, causal)
+    O.backward(dO)
+    grads = [t.grad.clone() for t in (Q, K, V)]
+    for t in (Q, K, V):
+        t.grad = None
+    ref_program(Q, K, V, causal).backward(dO)
+    for g, t in zip(grads, (Q, K, V)):
+        torch.testing.assert_close(g, t.grad, rtol=2e-2, atol=2e-2)
+    print("All checks pass.")
+    from tilelang.profiler import do_bench
+    lat = do_bench(lambda: O.backward(dO, retain_graph=True))
+    print(f"flash attention bwd: {lat:.3f} ms, {flops / lat * 1e-9:.1f} TFLOPS")
+
+
+if __name__ == "__main__":
+    p = argparse.ArgumentParser()
+    p.add_argument("--batch", type=int, default=8)
+    p.add_argument("--h", type=int, default=32)
+    p.add_argument("--n_ctx", type=int, default=1024)
+    p.add_argument("--d_head", type=int, default=64)
+    p.add_argument("--causal", action="store_true")
+    a = p.parse_args()
+    main(a.batch, a.h, a.n_ctx, a.d_head, a.causal)

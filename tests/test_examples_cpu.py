@@ -85,3 +85,22 @@ def test_hadamard():
     k = _both(m.hadamard, 4, 1024)
     x = torch.randn(4, 1024)
     torch.testing.assert_close(k(x), m.ref_program(x), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_flash_attention_bwd(causal):
+    import example_mha_bwd as m
+    B, S, H, D = 1, 128, 2, 64
+    q, k, v, do = [torch.randn(B, S, H, D).half() for _ in range(4)]
+    o, lse = _both(m.flashattn_fwd, B, H, S, D, causal, 64, 64)(q, k, v)
+    qf, kf, vf = [t.float().requires_grad_() for t in (q, k, v)]
+    ro = m.ref_program(qf, kf, vf, causal)
+    ro.backward(do.float())
+    torch.testing.assert_close(o.float(), ro.detach(), rtol=1e-2, atol=1e-2)
+    delta = _both(m.flashattn_bwd_preprocess, B, H, S, D)(o, do)
+    dq = torch.zeros(B, S, H, D)
+    dk, dv = torch.empty_like(q), torch.empty_like(q)
+    _both(m.flashattn_bwd, B, H, S, D, causal, 64, 64)(q, k, v, do, lse, delta, dq, dk, dv)
+    dqh = _both(m.flashattn_bwd_postprocess, B, H, S, D)(dq)
+    for a, r in ((dqh, qf.grad), (dk, kf.grad), (dv, vf.grad)):
+        torch.testing.assert_close(a.float(), r, rtol=1e-2, atol=1e-2)

@@ -85,3 +85,22 @@ def test_hadamard():
     k = m.hadamard(8, 4096)
     x = torch.randn(8, 4096, device="cuda")
     torch.testing.assert_close(k(x), m.ref_program(x), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+def test_flash_attention_bwd(causal, dtype):
+    import example_mha_bwd as m
+    tdt = getattr(torch, dtype)
+    B, S, H, D = 2, 512, 4, 64
+    Q = torch.randn(B, S, H, D, dtype=tdt, device="cuda").requires_grad_()
+    K = torch.randn_like(Q).requires_grad_()
+    V = torch.randn_like(Q).requires_grad_()
+    dO = torch.randn_like(Q)
+    m.attention(Q, K, V, causal).backward(dO)
+    grads = [t.grad.clone() for t in (Q, K, V)]
+    for t in (Q, K, V):
+        t.grad = None
+    m.ref_program(Q, K, V, causal).backward(dO)
+    for g, t in zip(grads, (Q, K, V)):
+        torch.testing.assert_close(g.float(), t.grad.float(), rtol=3e-2, atol=3e-2)
