@@ -104,3 +104,20 @@ def test_flash_attention_bwd(causal):
     dqh = _both(m.flashattn_bwd_postprocess, B, H, S, D)(dq)
     for a, r in ((dqh, qf.grad), (dk, kf.grad), (dv, vf.grad)):
         torch.testing.assert_close(a.float(), r, rtol=1e-2, atol=1e-2)
+
+
+def test_gqa_decode_contiguous_and_paged():
+    import example_gqa_decode as m
+    b, h, g, s, d, ns = 2, 8, 2, 256, 64, 2
+    q = torch.randn(b, h, d).half()
+    k, v = torch.randn(b, s, g, d).half(), torch.randn(b, s, g, d).half()
+    lens = torch.tensor([200, 256], dtype=torch.int32)
+    glse, part = torch.empty(b, h, ns), torch.empty(b, h, ns, d)
+    o = _both(m.gqa_decode, b, h, g, s, d, 64, 16, ns)(q, k, v, lens, glse, part)
+    torch.testing.assert_close(o, m.ref_program(q, k, v, lens), rtol=1e-2, atol=1e-2)
+    ps, mp, npg = 64, 4, 10
+    table = torch.randperm(npg)[:b * mp].view(b, mp).int()
+    kc, vc = torch.randn(npg, ps, g, d).half(), torch.randn(npg, ps, g, d).half()
+    o = _both(m.gqa_decode_paged, b, h, g, npg, ps, mp, d, 64, 16, ns)(q, kc, vc, lens, table, glse, part)
+    ref = m.ref_program(q, m.paged_to_contiguous(kc, table, mp, ps), m.paged_to_contiguous(vc, table, mp, ps), lens)
+    torch.testing.assert_close(o, ref, rtol=1e-2, atol=1e-2)

@@ -104,3 +104,23 @@ def test_flash_attention_bwd(causal, dtype):
     m.ref_program(Q, K, V, causal).backward(dO)
     for g, t in zip(grads, (Q, K, V)):
         torch.testing.assert_close(g.float(), t.grad.float(), rtol=3e-2, atol=3e-2)
+
+
+def test_gqa_decode_contiguous_and_paged():
+    import example_gqa_decode as m
+    b, h, g, s, d, ns = 4, 32, 8, 2048, 128, 4
+    q = torch.randn(b, h, d, device="cuda", dtype=torch.float16)
+    k = torch.randn(b, s, g, d, device="cuda", dtype=torch.float16)
+    v = torch.randn_like(k)
+    lens = torch.tensor([2048, 1500, 700, 1], dtype=torch.int32, device="cuda")
+    glse = torch.empty(b, h, ns, device="cuda")
+    part = torch.empty(b, h, ns, d, device="cuda")
+    o = m.gqa_decode(b, h, g, s, d, num_split=ns)(q, k, v, lens, glse, part)
+    torch.testing.assert_close(o, m.ref_program(q, k, v, lens), rtol=2e-2, atol=2e-2)
+    ps, mp, npg = 64, 32, 160
+    table = torch.randperm(npg, device="cuda")[:b * mp].view(b, mp).int()
+    kc = torch.randn(npg, ps, g, d, device="cuda", dtype=torch.float16)
+    vc = torch.randn_like(kc)
+    o = m.gqa_decode_paged(b, h, g, npg, ps, mp, d, num_split=ns)(q, kc, vc, lens, table, glse, part)
+    ref = m.ref_program(q, m.paged_to_contiguous(kc, table, mp, ps), m.paged_to_contiguous(vc, table, mp, ps), lens)
+    torch.testing.assert_close(o, ref, rtol=2e-2, atol=2e-2)

@@ -707,7 +707,7 @@ class TileOpLowerer(Mutator):
         frag_side = dst if dst.buffer.scope == "fragment" else src
         fb = frag_side.buffer
         if not _full(frag_side):
-            raise LoweringError(f"T.copy to/from fragment {fb.name} must cover the whole fragment")
+            return self.lower_partial_frag_copy(op, frag_side is dst)
         nest = _copy_nest(src, dst, None)
         loops = _nest_loops(nest)
         fshape = fb.static_shape()
@@ -718,6 +718,48 @@ class TileOpLowerer(Mutator):
         if [as_int(l.extent) for l in loops] != squeezed_lay.shape:
             raise LoweringError(f"T.copy shape mismatch for fragment {fb.name}")
         return self.lower_nest(nest, loop_lay)
+
+    def lower_partial_frag_copy(self, op: O.CopyOp, into_frag: bool):
+        """Copy between a sub-tile of a fragment and another buffer (e.g. the valid rows of a
+        padded MFMA tile): iterate the whole fragment with its own partition and predicate the
+        elements that fall inside the region."""
+        fr, other = (op.dst, op.src) if into_frag else (op.src, op.dst)
+        fb = fr.buffer
+        fshape = fb.static_shape()
+        fext, oext = fr.static_extents(), other.static_extents()
+        fmins = [as_int(m) for m in fr.mins]
+        if fext is None or oext is None or any(m is None for m in fmins):
+            raise LoweringError(f"T.copy on a sub-tile of fragment {fb.name} needs static bounds")
+        fd = [d for d, e in enumerate(fext) if e != 1]
+        od = [d for d, e in enumerate(oext) if e != 1]
+        if [fext[d] for d in fd] != [oext[d] for d in od]:
+            raise LoweringError(f"T.copy extents mismatch: {fb.name}{fext} vs {other.buffer.name}{oext}")
+        vars_ = [Var(f"pf{d}") for d in range(len(fshape))]
+        conds = []
+        for d, (m, e, s) in enumerate(zip(fmins, fext, fshape)):
+            if m == 0 and e == s:
+                continue
+            if e == 1:
+                conds.append(binop("==", vars_[d], m))
+            else:
+                conds.append(logical_and(binop(">=", vars_[d], m), binop("<", vars_[d], m + e)))
+        oidx = list(other.mins)
+        for k, d in enumerate(od):
+            oidx[d] = binop("+", other.mins[d], binop("-", vars_[fd[k]], fmins[fd[k]]))
+        fl = BufferLoad(fb, list(vars_))
+        ol = BufferLoad(other.buffer, oidx)
+        if into_frag:
+            body = S.StoreStmt(fb, list(vars_), cast(ol, fb.dtype))
+        else:
+            body = S.StoreStmt(other.buffer, oidx, cast(fl, other.buffer.dtype))
+        cond = None
+        for c in conds:
+            cond = c if cond is None else logical_and(cond, c)
+        if cond is not None:
+            body = S.IfStmt(cond, body)
+        for v, s in reversed(list(zip(vars_, fshape))):
+            body = S.ForStmt(v, 0, s, "parallel", body)
+        return self.lower_nest(body, fb.layout)
 
     def lower_GemmOp(self, op: O.GemmOp):
         ctx = self.ctx
