@@ -118,6 +118,34 @@ def b_hadamard():
     _emit("hadamard 64x32768 fp32", ms)
 
 
+def b_sink():
+    import example_gqa_sink_fwd_bhsd as m
+    B, H, S, D, G = 1, 64, 4096, 128, 8
+    k = m.flashattn_sink(B, H, S, S, D, G)
+    q = torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16)
+    kk = torch.randn(B, H // G, S, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn_like(kk)
+    s = torch.randn(H, device="cuda", dtype=torch.bfloat16)
+    ms = do_bench(lambda: k(q, kk, v, s))
+    _emit("gqa+sink fwd causal bf16 b1 h64 kvh8 s4096 d128 (reference headline 497 TF on H800)", ms,
+          TFLOPS=round(m.flops(B, H, S, S, D) / ms * 1e-9, 1))
+
+
+def b_decode():
+    import example_gqa_decode as m
+    b, h, g, s, d, ns = 32, 32, 8, 8192, 128, 8
+    k = m.gqa_decode(b, h, g, s, d, num_split=ns)
+    q = torch.randn(b, h, d, device="cuda", dtype=torch.float16)
+    kk = torch.randn(b, s, g, d, device="cuda", dtype=torch.float16)
+    v = torch.randn_like(kk)
+    lens = torch.full((b, ), s, dtype=torch.int32, device="cuda")
+    glse = torch.empty(b, h, ns, device="cuda")
+    part = torch.empty(b, h, ns, d, device="cuda")
+    ms = do_bench(lambda: k(q, kk, v, lens, glse, part))
+    gbs = 2 * b * s * g * d * 2 / ms * 1e-6
+    _emit("gqa decode fp16 b32 h32 g8 kv8192 d128", ms, GBs=round(gbs, 1), pct_hbm=round(100 * gbs / HBM_PEAK_GBS, 1))
+
+
 BENCHES = {n[2:]: f for n, f in globals().items() if n.startswith("b_")}
 
 if __name__ == "__main__":

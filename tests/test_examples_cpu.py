@@ -121,3 +121,13 @@ def test_gqa_decode_contiguous_and_paged():
     o = _both(m.gqa_decode_paged, b, h, g, npg, ps, mp, d, 64, 16, ns)(q, kc, vc, lens, table, glse, part)
     ref = m.ref_program(q, m.paged_to_contiguous(kc, table, mp, ps), m.paged_to_contiguous(vc, table, mp, ps), lens)
     torch.testing.assert_close(o, ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("sq,skv,win", [(256, 256, None), (192, 320, None), (256, 256, 128)])
+def test_attention_sink(sq, skv, win):
+    import example_gqa_sink_fwd_bhsd as m
+    k = _both(m.flashattn_sink, 1, 8, sq, skv, 64, 4, win, None, 64, 64, 2, 256, "float16")
+    q = torch.randn(1, 8, sq, 64).half()
+    kk, v = torch.randn(1, 2, skv, 64).half(), torch.randn(1, 2, skv, 64).half()
+    s = torch.randn(8).half()
+    torch.testing.assert_close(k(q, kk, v, s).float(), m.ref_program(q, kk, v, s, win).float(), rtol=1e-2, atol=1e-2)

@@ -124,3 +124,14 @@ def test_gqa_decode_contiguous_and_paged():
     o = m.gqa_decode_paged(b, h, g, npg, ps, mp, d, num_split=ns)(q, kc, vc, lens, table, glse, part)
     ref = m.ref_program(q, m.paged_to_contiguous(kc, table, mp, ps), m.paged_to_contiguous(vc, table, mp, ps), lens)
     torch.testing.assert_close(o, ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("sq,skv,win", [(1024, 1024, None), (512, 1536, None), (1024, 1024, 256)])
+def test_attention_sink(sq, skv, win):
+    import example_gqa_sink_fwd_bhsd as m
+    k = m.flashattn_sink(2, 16, sq, skv, 128, 8, win)
+    q = torch.randn(2, 16, sq, 128, device="cuda", dtype=torch.bfloat16)
+    kk = torch.randn(2, 2, skv, 128, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn_like(kk)
+    s = torch.randn(16, device="cuda", dtype=torch.bfloat16)
+    torch.testing.assert_close(k(q, kk, v, s).float(), m.ref_program(q, kk, v, s, win).float(), rtol=2e-2, atol=2e-2)

@@ -246,15 +246,23 @@ class PipelineInjector(Mutator):
         # multi-version the shared buffers
         mapping = {}
         newbufs = {}
+        versions = getattr(self, "versions", None)
+        if versions is None:
+            versions = self.versions = {}
         for p, _ in prods:
             B = p.op.dst.buffer
             if B in newbufs:
                 continue
-            shp = B.static_shape()
-            NB = Buffer(B.name, [nstages] + shp, B.dtype, "shared")
-            NB.layout = stage_layout(B.layout, shp, nstages)
-            NB._auto_name = False
-            NB.stages_of = B
+            # several pipelined loops over the same tile (e.g. an unmasked main loop and a masked
+            # tail) share one multi-versioned LDS ring per stage count
+            NB = versions.get((B, nstages))
+            if NB is None:
+                shp = B.static_shape()
+                NB = Buffer(B.name, [nstages] + shp, B.dtype, "shared")
+                NB.layout = stage_layout(B.layout, shp, nstages)
+                NB._auto_name = False
+                NB.stages_of = B
+                versions[(B, nstages)] = NB
             newbufs[B] = NB
         kk = binop("-", k, loop.min)
         stage = binop("%", kk, nstages)
@@ -334,7 +342,10 @@ class PipelineInjector(Mutator):
                              {"pipelined": nstages, "_lets": lets})
         # allocations for the new multi-versioned buffers replace the old ones (done by caller)
         self.replaced = getattr(self, "replaced", {})
-        self.replaced.update(newbufs)
+        for B, NB in newbufs.items():
+            lst = self.replaced.setdefault(B, [])
+            if NB not in lst:
+                lst.append(NB)
         tail = [L.CallStmt("tl::barrier_raw", [])]
         return S.SeqStmt(prologue + [new_loop] + tail)
 
@@ -355,7 +366,8 @@ class _AllocReplacer(Mutator):
 
     def visit_AllocStmt(self, s):
         if s.buffer in self.replaced:
-            return S.AllocStmt(self.replaced[s.buffer])
+            nbs = self.replaced[s.buffer]
+            return S.seq(*[S.AllocStmt(nb) for nb in nbs])
         return s
 
 
