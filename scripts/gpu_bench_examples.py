@@ -146,6 +146,28 @@ def b_decode():
     _emit("gqa decode fp16 b32 h32 g8 kv8192 d128", ms, GBs=round(gbs, 1), pct_hbm=round(100 * gbs / HBM_PEAK_GBS, 1))
 
 
+def b_mamba():
+    import example_mamba_chunk_scan as m
+    for seq in (1024, 4096, 16384):
+        args = m.make_inputs(8, seq, 256, 1, 80, 64, 128)
+        k = m.chunk_scan_fwd(8, seq, 256, 1, 80, 64, 128)
+        ms = do_bench(lambda: k(*args))
+        _emit(f"mamba2 chunk scan b8 h80 chunk256 d64 dstate128 seq{seq} (reference 126-136 TF on H800)", ms,
+              TFLOPS=round(m.flops(8, seq, 256, 80, 64, 128) / ms * 1e-9, 1))
+
+
+def b_linear_attn():
+    import example_linear_attn_fwd as m
+    B, S, H, D = 1, 8192, 32, 128
+    k = m.linear_attn_fwd(B, S, H, D, D)
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.float16) * 0.1
+    kk = torch.randn_like(q) * 0.1
+    v = torch.randn_like(q)
+    ms = do_bench(lambda: k(q, kk, v))
+    flops = B * H * (S // 64) * (2 * 64 * 64 * D * 2 + 2 * 64 * D * D * 2)
+    _emit("linear attention fwd b1 s8192 h32 d128", ms, TFLOPS=round(flops / ms * 1e-9, 1))
+
+
 BENCHES = {n[2:]: f for n, f in globals().items() if n.startswith("b_")}
 
 if __name__ == "__main__":

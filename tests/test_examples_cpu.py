@@ -131,3 +131,22 @@ def test_attention_sink(sq, skv, win):
     kk, v = torch.randn(1, 2, skv, 64).half(), torch.randn(1, 2, skv, 64).half()
     s = torch.randn(8).half()
     torch.testing.assert_close(k(q, kk, v, s).float(), m.ref_program(q, kk, v, s, win).float(), rtol=1e-2, atol=1e-2)
+
+
+def test_linear_attention_fwd():
+    import example_linear_attn_fwd as m
+    k = _both(m.linear_attn_fwd, 1, 256, 2, 64, 64)
+    q = torch.nn.functional.normalize(torch.randn(1, 256, 2, 64), dim=-1).half()
+    kk = torch.nn.functional.normalize(torch.randn(1, 256, 2, 64), dim=-1).half()
+    v = torch.randn(1, 256, 2, 64).half()
+    o, h = k(q, kk, v)
+    ro, rh = m.ref_program(q, kk, v)
+    torch.testing.assert_close(o.float(), ro, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(h, rh, rtol=1e-3, atol=1e-3)
+
+
+def test_mamba_chunk_scan():
+    import example_mamba_chunk_scan as m
+    args = m.make_inputs(1, 512, 128, 1, 2, 64, 64, device="cpu")
+    k = _both(m.chunk_scan_fwd, 1, 512, 128, 1, 2, 64, 64)
+    torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=1e-2, atol=2e-2)

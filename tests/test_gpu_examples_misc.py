@@ -135,3 +135,23 @@ def test_attention_sink(sq, skv, win):
     v = torch.randn_like(kk)
     s = torch.randn(16, device="cuda", dtype=torch.bfloat16)
     torch.testing.assert_close(k(q, kk, v, s).float(), m.ref_program(q, kk, v, s, win).float(), rtol=2e-2, atol=2e-2)
+
+
+def test_linear_attention_fwd():
+    import example_linear_attn_fwd as m
+    B, S, H, D = 2, 1024, 4, 128
+    k = m.linear_attn_fwd(B, S, H, D, D)
+    q = torch.nn.functional.normalize(torch.randn(B, S, H, D, device="cuda"), dim=-1).half()
+    kk = torch.nn.functional.normalize(torch.randn(B, S, H, D, device="cuda"), dim=-1).half()
+    v = torch.randn(B, S, H, D, device="cuda", dtype=torch.float16)
+    o, h = k(q, kk, v)
+    ro, rh = m.ref_program(q, kk, v)
+    torch.testing.assert_close(o.float(), ro, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(h, rh, rtol=1e-2, atol=2e-2)
+
+
+def test_mamba_chunk_scan():
+    import example_mamba_chunk_scan as m
+    args = m.make_inputs(2, 1024, 256, 1, 8, 64, 128)
+    k = m.chunk_scan_fwd(2, 1024, 256, 1, 8, 64, 128)
+    torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=2e-2, atol=5e-2)
