@@ -4,7 +4,8 @@ The extension is plain C++ (compiled by the host compiler) that links the HIP ru
 PyTorch's c10_hip directly — no hipify step, no CUDA sources.
 """
 import os
-from setuptools import setup, find_packages
+import pybind11
+from setuptools import Extension, setup, find_packages
 from torch.utils.cpp_extension import BuildExtension, CppExtension
 
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
@@ -19,11 +20,21 @@ ext = CppExtension(
     extra_compile_args=["-O2", "-std=c++17", "-Wno-unused-function"],
 )
 
+# host-only compiler core (fragment algebra, LDS model, arena planner, hierarchical layouts)
+# (plain pybind11, no torch linkage: the compiler runs without loading the torch/HIP runtime)
+core = Extension(
+    "tilelang._tl_core",
+    ["csrc/core/bindings.cc", "csrc/core/fragment.cc", "csrc/core/lds.cc", "csrc/core/hier.cc"],
+    include_dirs=[pybind11.get_include()],
+    language="c++",
+    extra_compile_args=["-O2", "-std=c++17", "-fvisibility=hidden"],
+)
+
 setup(
     name="tilelang-mi355x",
     version="0.1.7+mi355x",
     packages=find_packages(include=["tilelang", "tilelang.*"]),
     package_data={"tilelang": ["include/tl/*.h"]},
-    ext_modules=[ext],
+    ext_modules=[ext, core],
     cmdclass={"build_ext": BuildExtension.with_options(use_ninja=False)},
 )

@@ -29,3 +29,21 @@ def available() -> bool:
         return True
     except ImportError:
         return False
+
+
+_core = None
+
+
+def core():
+    """The native compiler core (``tilelang/_tl_core*.so`` from csrc/core).  Mandatory: layout
+    inference, lowering and LDS planning run their numeric work in it."""
+    global _core
+    if _core is None:
+        try:
+            from . import _tl_core as m  # noqa: F401
+        except ImportError as e:
+            raise NativeRuntimeMissing(
+                "tilelang native compiler core not built: run `python setup.py build_ext --inplace` "
+                f"in the repository root ({e})") from e
+        _core = m
+    return _core

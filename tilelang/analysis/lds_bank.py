@@ -31,7 +31,14 @@ INSTRUCTIONS: Dict[str, tuple] = {
 
 
 def instruction_cycles(instr: str, byte_addrs: Sequence[int]) -> int:
-    """LDS-array cycles one wave-instruction costs (conflict-free == number of groups)."""
+    """LDS-array cycles one wave-instruction costs (conflict-free == number of groups).
+    Evaluated by the native model (``tilelang._tl_core.lds_instruction_cycles``, csrc/core/lds.cc)."""
+    from .._native import core
+    return core().lds_instruction_cycles(instr, [-1 if a is None else int(a) for a in byte_addrs])
+
+
+def instruction_cycles_py(instr: str, byte_addrs: Sequence[int]) -> int:
+    """Pure-Python twin of the native model (kept as the executable specification for tests)."""
     groups, width, mod = INSTRUCTIONS[instr]
     total = 0
     for g in groups:

@@ -163,16 +163,10 @@ class MeshTensorAnnot:
                 factors.append((policy.y, nrows))
             if policy.x is not None:
                 factors.append((policy.x, ncols))
+        from .._native import core
+        groups = [tuple(g) for g in hgroups]
         for dim, f in factors:
-            if f == 1:
-                continue
-            start, end = hgroups[dim]
-            if start >= end:
-                continue
-            if hdims[start] % f != 0:
-                raise ValueError(f"The most significant hierarchical dimension ({hdims[start]}) of logical dimension "
-                                 f"{dim} is not divisible by the shard factor ({f}).")
-            out[start] = hdims[start] // f
+            out = core().shard_hier(out, groups, dim, f)  # csrc/core/hier.cc
         return tuple(out)
 
     @staticmethod

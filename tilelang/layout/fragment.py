@@ -159,6 +159,18 @@ class Fragment:
             idx[d.dim] = term if (isinstance(idx[d.dim], int) and idx[d.dim] == 0) else idx[d.dim] + term
         return idx
 
+    # -- native engine ---------------------------------------------------------------
+    @property
+    def native(self):
+        """The C++ twin (``tilelang._tl_core.Fragment``) used for whole-layout numeric work."""
+        nf = self.__dict__.get("_native_frag")
+        if nf is None:
+            from .._native import core
+            nf = core().Fragment(self.shape, [(d.dim, d.stride, d.size) for d in self.thread_digits],
+                                 [(d.dim, d.stride, d.size) for d in self.local_digits], self.thread_offset)
+            self.__dict__["_native_frag"] = nf
+        return nf
+
     # -- structure queries ---------------------------------------------------------
     def signature(self) -> Tuple:
         return (tuple(self.shape), tuple(self.thread_digits), tuple(self.local_digits), self.thread_offset)
@@ -172,23 +184,24 @@ class Fragment:
                 self.local_size != other.local_size:
             return False
         # numeric comparison (digit structure may differ but the map be identical)
-        for t in range(self.num_threads):
-            for r in range(self.local_size):
-                if self.inverse(t, r) != other.inverse(t, r):
-                    return False
-        return True
+        return self.native.equals(other.native)
 
     def table(self) -> Dict[Tuple[int, ...], List[Tuple[int, int]]]:
         """logical idx -> list of (thread, local) (replicas)."""
         out = {}
+        flat = self.native.table()
+        nd = len(self.shape)
+        L = self.local_size
         for t in range(self.num_threads):
-            for r in range(self.local_size):
-                key = tuple(self.inverse(t, r))
-                out.setdefault(key, []).append((t + self.thread_offset, r))
+            for r in range(L):
+                o = (t * L + r) * nd
+                out.setdefault(tuple(flat[o:o + nd]), []).append((t + self.thread_offset, r))
         return out
 
     def thread_local_map(self, thread: int) -> Dict[Tuple[int, ...], int]:
         """For one thread: logical idx -> local index."""
+        if isinstance(thread, int):
+            return self.native.thread_local_map(thread)
         return {tuple(self.inverse(thread, r)): r for r in range(self.local_size)}
 
     def inner_vector_width(self, dim: Optional[int] = None) -> int:

@@ -40,6 +40,9 @@ class HierarchicalLayout:
             shape.append(n)
         if sorted(covered) != list(range(len(self.hdims))):
             raise ValueError("hierarchical groups must partition the hierarchical dims")
+        # the native twin validates the same invariants and evaluates integer offsets
+        from .._native import core
+        self._native = core().HierarchicalLayout(list(self.hdims), list(self.hstrides), list(self.hgroups))
         if self.logical_shape is None:
             self.logical_shape = tuple(shape)
         elif tuple(self.logical_shape) != tuple(shape):
@@ -68,11 +71,20 @@ class HierarchicalLayout:
         return out
 
     def offset(self, idx: Sequence):
+        if all(isinstance(i, int) for i in idx):
+            return self._native.offset([int(i) for i in idx])
         h = self.logical_to_hierarchical(idx)
         off = 0
         for hi, s in zip(h, self.hstrides):
             off = off + hi * s
         return off
+
+    def offsets(self) -> List[int]:
+        """Offset of every logical element in row-major order (native)."""
+        return self._native.offsets()
+
+    def is_bijective(self) -> bool:
+        return self._native.is_bijective()
 
     def offset_to_logical(self, off: int) -> List[int]:
         """Inverse (numeric): requires the strides to describe a bijection."""

@@ -178,49 +178,24 @@ def _candidates(cpr: int, max_row_bit: int = 6):
         yield bits
 
 
-def _batched_cycles(instr: str, addrs):
-    """Vectorised ``lds_bank.instruction_cycles``: addrs is int array [C, P, 64] (bytes)."""
-    import numpy as np
-    groups, width, mod = lds_bank.INSTRUCTIONS[instr]
-    C, P, _ = addrs.shape
-    total = np.zeros(C, dtype=np.int64)
-    nw = width // 4
-    for g in groups:
-        a = addrs[:, :, g] // 4                                   # [C, P, L]
-        dw = (a[..., None] + np.arange(nw)).reshape(C * P, -1)    # [C*P, L*nw]
-        dw = np.sort(dw, axis=1)
-        uniq = np.ones_like(dw, dtype=bool)
-        uniq[:, 1:] = dw[:, 1:] != dw[:, :-1]
-        banks = dw % mod
-        cnt = np.zeros((C * P, mod), dtype=np.int64)
-        rows_idx = np.repeat(np.arange(C * P), dw.shape[1]).reshape(dw.shape)
-        np.add.at(cnt, (rows_idx[uniq], banks[uniq]), 1)
-        total += np.maximum(cnt.max(axis=1), 1).reshape(C, P).sum(axis=1)
-    return total
+def _native_costs(kind: str, rows: int, cols: int, elem_bytes: int, cands):
+    """Modelled cycles of every candidate swizzle for one read pattern (csrc/core/lds.cc)."""
+    from .._native import core
+    pats = _read_patterns(kind, rows, cols, elem_bytes)
+    flat = [v for p in pats for rc in p for v in rc]
+    return core().swizzle_costs(_instr_for(kind, elem_bytes), flat, len(pats), cols, elem_bytes,
+                                [list(c) for c in cands])
 
 
 @functools.lru_cache(maxsize=None)
 def choose_swizzle(kind: str, rows: int, cols: int, elem_bytes: int) -> Tuple[Tuple[int, int], ...]:
     """Pick the chunk-XOR swizzle with the fewest modelled LDS cycles for this read pattern
     (exhaustive over row-bit -> chunk-bit assignments, scored with the gfx950 bank model)."""
-    import numpy as np
     cpr = cols * elem_bytes // 16
     if cpr <= 1:
         return ()
-    pats = _read_patterns(kind, rows, cols, elem_bytes)
-    instr = _instr_for(kind, elem_bytes)
     cands = [tuple(b) for b in _candidates(cpr, max_row_bit=min(6, max(1, rows.bit_length() - 1)))]
-    R = np.array([[r for r, c in p] for p in pats], dtype=np.int64)      # [P, 64]
-    Cc = np.array([[c for r, c in p] for p in pats], dtype=np.int64)
-    byte = Cc * elem_bytes
-    chunk = byte // 16
-    within = byte % 16
-    xs = np.zeros((len(cands), ) + R.shape, dtype=np.int64)
-    for i, bits in enumerate(cands):
-        for rb, cb in bits:
-            xs[i] |= ((R >> rb) & 1) << cb
-    addrs = R[None] * (cols * elem_bytes) + ((chunk[None] ^ xs) * 16) + within[None]
-    cost = _batched_cycles(instr, addrs)
+    cost = _native_costs(kind, rows, cols, elem_bytes, cands)
     best = min(range(len(cands)), key=lambda i: (int(cost[i]), len(cands[i])))
     return cands[best]
 
@@ -240,26 +215,16 @@ def swizzle_report(kind: str, rows: int, cols: int, elem_bytes: int, bits) -> di
 def choose_swizzle_multi(kinds: Tuple[str, ...], rows: int, cols: int, elem_bytes: int):
     """Best swizzle for a tile read with several patterns (e.g. MLA's KV tile, read row-wise by
     Q.KV^T and transposed by P.KV): minimise the summed modelled cycles."""
-    import numpy as np
     if len(kinds) == 1:
         return choose_swizzle(kinds[0], rows, cols, elem_bytes)
     cpr = cols * elem_bytes // 16
     if cpr <= 1:
         return ()
     cands = [tuple(b) for b in _candidates(cpr, max_row_bit=min(6, max(1, rows.bit_length() - 1)))]
-    total = np.zeros(len(cands), dtype=np.int64)
+    total = [0] * len(cands)
     for kind in kinds:
-        pats = _read_patterns(kind, rows, cols, elem_bytes)
-        instr = _instr_for(kind, elem_bytes)
-        R = np.array([[r for r, c in p] for p in pats], dtype=np.int64)
-        Cc = np.array([[c for r, c in p] for p in pats], dtype=np.int64)
-        byte = Cc * elem_bytes
-        xs = np.zeros((len(cands), ) + R.shape, dtype=np.int64)
-        for i, bits in enumerate(cands):
-            for rb, cb in bits:
-                xs[i] |= ((R >> rb) & 1) << cb
-        addrs = R[None] * (cols * elem_bytes) + (((byte // 16)[None] ^ xs) * 16) + (byte % 16)[None]
-        total += _batched_cycles(instr, addrs)
+        for i, c in enumerate(_native_costs(kind, rows, cols, elem_bytes, cands)):
+            total[i] += c
     best = min(range(len(cands)), key=lambda i: (int(total[i]), len(cands[i])))
     return cands[best]
 

@@ -87,25 +87,12 @@ def plan_lds(kernel: S.KernelStmt, reuse: bool = False) -> Tuple[Dict[Buffer, in
         for b in t:
             first.setdefault(b, i)
             last[b] = i
-    offsets: Dict[Buffer, int] = {}
-    placed: List[Tuple[int, int, int, int]] = []  # (off, size, first, last)
-    total = 0
-    for b in sorted(shared, key=lambda x: -sizes[x]):
-        sz = (sizes[b] + ALIGN - 1) // ALIGN * ALIGN
-        f, l = first.get(b, 0), last.get(b, len(top))
-        off = 0
-        if reuse:
-            cands = sorted(p for p in placed if not (p[3] < f or l < p[2]))
-            for p in cands:
-                if off + sz <= p[0]:
-                    break
-                off = max(off, p[0] + p[1])
-        else:
-            off = total
-        offsets[b] = off
-        placed.append((off, sz, f, l))
-        total = max(total, off + sz)
-    if total > LDS_LIMIT:
-        raise LDSPlanError(f"kernel needs {total} bytes of LDS, MI355X has {LDS_LIMIT} per CU; "
-                           f"reduce tile sizes or num_stages")
+    # placement by the native arena planner (csrc/core/lds.cc plan_arena)
+    from .._native import core
+    try:
+        offs, total = core().plan_arena([sizes[b] for b in shared], [first.get(b, 0) for b in shared],
+                                        [last.get(b, len(top)) for b in shared], ALIGN, bool(reuse), LDS_LIMIT)
+    except ValueError as e:  # std::length_error -> ValueError
+        raise LDSPlanError(str(e)) from None
+    offsets: Dict[Buffer, int] = dict(zip(shared, offs))
     return offsets, total

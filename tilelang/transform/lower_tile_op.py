@@ -25,7 +25,7 @@ from ..ir import tileop as O
 from ..ir import lowered as L
 from ..ir import dtypes as _dt
 from ..ir.buffer import Buffer, BufferRegion
-from ..ir.expr import (BufferLoad, Call, IntImm, PrimExpr, Var, as_int, binop, call, cast, compile_py, const,
+from ..ir.expr import (BinOp, BufferLoad, Call, IntImm, PrimExpr, Var, as_int, binop, call, cast, compile_py, const,
                        convert, divisible_by, evaluate, free_vars, logical_and, select, substitute, transform,
                        post_order, loads_of, modular)
 from ..layout.fragment import Digit, Fragment, make_linear_fragment
@@ -200,6 +200,34 @@ class LowerCtx:
 # ---------------------------------------------------------------------------
 
 
+def _affine(e, vars_: List[Var]):
+    """``e`` as (coefficients over ``vars_``, constant) when it is an integer affine form of them."""
+    v = as_int(e)
+    if v is not None:
+        return [0] * len(vars_), v
+    if isinstance(e, Var):
+        for i, x in enumerate(vars_):
+            if x is e:
+                c = [0] * len(vars_)
+                c[i] = 1
+                return c, 0
+        return None
+    if isinstance(e, BinOp) and e.op in ("+", "-", "*"):
+        a, b = _affine(e.a, vars_), _affine(e.b, vars_)
+        if a is None or b is None:
+            return None
+        if e.op == "+":
+            return [x + y for x, y in zip(a[0], b[0])], a[1] + b[1]
+        if e.op == "-":
+            return [x - y for x, y in zip(a[0], b[0])], a[1] - b[1]
+        if not any(a[0]):
+            return [a[1] * y for y in b[0]], a[1] * b[1]
+        if not any(b[0]):
+            return [b[1] * x for x in a[0]], a[1] * b[1]
+        return None
+    return None
+
+
 class _FragResolver:
     """Resolves ``frag[idx(loop vars)]`` to a constant register index for iteration r of a
     loop partitioned by ``loop_layout`` (checked for every thread of the block)."""
@@ -219,6 +247,21 @@ class _FragResolver:
         if key in self.cache:
             return self.cache[key]
         blay: Fragment = buf.layout
+        aff = [_affine(e, self.vars) for e in idx_exprs]
+        if all(a is not None for a in aff) and blay.num_threads == self.T:
+            # native proof over every lane of the block (tilelang._tl_core.Fragment.resolve_affine)
+            A = [c for a in aff for c in a[0]]
+            b = [a[1] + sum(c * m for c, m in zip(a[0], self.mins)) for a in aff]
+            li = self.layout.native.resolve_affine(blay.native, A, b, r)
+            if li == -1:
+                raise LoweringError(
+                    f"layout conflict: a thread iterates an element of fragment {buf.name} it does not own "
+                    f"(loop layout {self.layout}, buffer layout {blay})")
+            if li == -2:
+                raise LoweringError(f"fragment {buf.name}: register index of element differs across threads "
+                                    f"(non-uniform access {idx_exprs})")
+            self.cache[key] = li
+            return li
         try:
             fns = [compile_py(e, self.vars) for e in idx_exprs]
         except Exception as ex:  # noqa: BLE001
