@@ -24,8 +24,8 @@ LOG2E = 1.44269504
 
 
 @tilelang.jit(out_idx=[3])
-def flashattn_sink(batch, heads, seq_q, seq_kv, dim, groups=1, window_size=None, sm_scale=None, block_M=128,
-                   block_N=64, num_stages=2, threads=512, dtype="bfloat16"):
+def flashattn_sink(batch, heads, seq_q, seq_kv, dim, groups=1, window_size=None, sm_scale=None, block_M=256,
+                   block_N=64, num_stages=2, threads=512, dtype="bfloat16", causal=True):
     if window_size is not None:
         assert window_size % block_N == 0, "window_size must be divisible by block_N"
     if sm_scale is None:
@@ -51,7 +51,8 @@ def flashattn_sink(batch, heads, seq_q, seq_kv, dim, groups=1, window_size=None,
                     acc_s[i, j] = T.if_then_else((q_idx >= k_idx) & (q_idx < k_idx + window_size), 0,
                                                  -T.infinity(accum_dtype))
                 else:
-                    acc_s[i, j] = T.if_then_else((q_idx >= k_idx) & (k_idx < seq_kv), 0, -T.infinity(accum_dtype))
+                    acc_s[i, j] = T.if_then_else(((q_idx >= k_idx) | (not causal)) & (k_idx < seq_kv), 0,
+                                                 -T.infinity(accum_dtype))
         else:
             T.clear(acc_s)
         T.gemm(Q_shared, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
@@ -99,8 +100,12 @@ def flashattn_sink(batch, heads, seq_q, seq_kv, dim, groups=1, window_size=None,
             T.fill(scores_max, -T.infinity(accum_dtype))
             # KV tiles [start, full_end) lie entirely below the diagonal (and inside the window's
             # far edge when windowed); [full_end, end) need the mask
-            end = T.min(T.ceildiv(seq_kv, block_N), T.ceildiv((qt + 1) * block_M + past_len, block_N))
-            full_end = T.max(T.min((qt * block_M + past_len + 1) // block_N, end), 0)
+            if causal:
+                end = T.min(T.ceildiv(seq_kv, block_N), T.ceildiv((qt + 1) * block_M + past_len, block_N))
+                full_end = T.max(T.min((qt * block_M + past_len + 1) // block_N, end), 0)
+            else:
+                end = T.ceildiv(seq_kv, block_N)
+                full_end = seq_kv // block_N
             if window_size is not None:
                 start = T.max(0, (qt * block_M + past_len - window_size) // block_N)
                 for k in T.Pipelined(start, end, num_stages=num_stages):
