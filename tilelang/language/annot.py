@@ -42,6 +42,15 @@ class _TensorFactory:
 
     def __call__(self, shape, dtype="float32", data=None, strides=None, elem_offset=None, scope=None,
                  align=0, offset_factor=0, buffer_type="", axis_separators=None):
+        if data is not None:
+            # inside a kernel: a new view of an existing buffer's storage, e.g.
+            # T.Tensor((KH * KW * C, F), dtype, kernel.data)
+            from ..ir.buffer import DATA_OWNERS
+            owner = data if isinstance(data, Buffer) else DATA_OWNERS.get(getattr(data, "uid", None))
+            if owner is None:
+                raise ValueError("T.Tensor(..., data=...) needs the .data of a buffer")
+            from .tileops import view
+            return view(owner, shape, dtype)
         return TensorAnnot(shape, dtype, strides=strides, scope=scope or self.scope)
 
     def __getitem__(self, key):

@@ -272,6 +272,18 @@ class PipelineInjector(Mutator):
         rng = dict(self.ranges)
         if as_int(loop.min) is not None and as_int(loop.extent) is not None:
             rng[k] = (as_int(loop.min), as_int(loop.min) + as_int(loop.extent) - 1)
+        else:
+            # data-dependent trip counts (causal / windowed attention): interval of the loop
+            # var from the bounds of its start and end, so LDS-DMA stays provably in bounds
+            lo = bound(loop.min, self.ranges)
+            ext = loop.extent
+            from ..ir.expr import BinOp, structural_equal
+            if isinstance(ext, BinOp) and ext.op == "-" and structural_equal(ext.b, loop.min):
+                hi = bound(ext.a, self.ranges)  # T.Pipelined(start, end): extent = end - start
+            else:
+                hi = bound(binop("+", loop.min, ext), self.ranges)
+            if lo is not None and hi is not None:
+                rng[k] = (lo[0], max(lo[0], hi[1] - 1))
         asyncs, staged = [], []
         for p, src in prods:
             plan = glds_plan(O.CopyOp(src, p.op.dst), self.T, rng, self.target)
