@@ -6,13 +6,14 @@ s4096 d128 -- is this kernel).
 softmax is taken over [scores, sink]: the sink adds exp(sink - max) to each row's normaliser
 and contributes nothing to the output.  MI355X schedule:
 
-* one block per (128-query tile, head, batch), 8 waves (FullRow: each wave owns 16 query rows
+* one block per (head, 256-query tile, batch), 8 waves (FullRow: each wave owns 32 query rows
   of S = Q K^T, so row max/sum are in-wave shuffles and P feeds the P V MFMA from registers);
 * K/V tiles stream through the 2-stage LDS-DMA ring;
 * causal masking is applied only on the diagonal tiles: the KV loop is split into an unmasked
   main loop and a short masked tail, so the main loop has no per-element selects;
-* query tiles are issued longest-first (``bx`` reversed) so the tail of the grid is the
-  cheap tiles (causal work is triangular).
+* query tiles are issued longest-first across ALL heads (grid = (heads, q-tiles) with the
+  tile index reversed), so the tail of the grid is the cheap tiles (causal work is
+  triangular; measured 0.75 -> see docs/RESULTS.md).
 """
 import argparse
 from typing import Optional
@@ -79,7 +80,9 @@ def flashattn_sink(batch, heads, seq_q, seq_kv, dim, groups=1, window_size=None,
     @T.prim_func
     def main(Q: T.Tensor(q_shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
              Output: T.Tensor(q_shape, dtype), Sinks: T.Tensor([heads], dtype)):
-        with T.Kernel(n_qt, heads, batch, threads=threads) as (bx, by, bz):
+        # heads on the fastest grid axis: every head's heaviest (last) query tile is dispatched
+        # before any lighter one -- global longest-first order for the triangular causal work
+        with T.Kernel(heads, n_qt, batch, threads=threads) as (by, bx, bz):
             Q_shared = T.alloc_shared([block_M, dim], dtype)
             K_shared = T.alloc_shared([block_N, dim], dtype)
             V_shared = T.alloc_shared([block_N, dim], dtype)

@@ -122,7 +122,7 @@ def flashattn_bwd_postprocess(batch, heads, seq_len, dim, blk=64, threads=256, d
 
 
 @tilelang.jit
-def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=64, block_N=64, threads=256, num_stages=2,
+def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=512, num_stages=2,
                   dtype="float16"):
     sm_scale = (1.0 / dim)**0.5
     scale = sm_scale * LOG2E

@@ -18,8 +18,8 @@ LOG2E = 1.44269504
 
 
 @tilelang.jit(out_idx=[7])
-def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, block_M=64, block_N=64,
-                   block_K=64, num_stages=2, threads=256, dtype="float16"):
+def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, block_M=128, block_N=64,
+                   block_K=32, num_stages=2, threads=256, dtype="float16"):
     accum_dtype = "float"
     nchunks = seqlen // chunk_size
     assert seqlen % chunk_size == 0 and chunk_size % block_M == 0 and chunk_size % block_K == 0

@@ -150,3 +150,20 @@ def test_mamba_chunk_scan():
     args = m.make_inputs(1, 512, 128, 1, 2, 64, 64, device="cpu")
     k = _both(m.chunk_scan_fwd, 1, 512, 128, 1, 2, 64, 64)
     torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=1e-2, atol=2e-2)
+
+
+def test_dequant_gemm_w4a16():
+    import example_dequant_gemm_w4a16 as m
+    k = _both(m.dequant_gemm_w4a16, 64, 256, 256)
+    A, W = torch.randn(64, 256).half(), torch.randn(256, 256).half()
+    Bq, s = m.quantize_int4(W)
+    assert (m.dequantize_int4(Bq, s) - W.float()).abs().max() < 0.5
+    torch.testing.assert_close(k(A, Bq, s).float(), m.ref_program(A, Bq, s).float(), rtol=1e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("n,c,h,w,f,k,s,d,p", [(2, 32, 8, 8, 64, 3, 1, 1, 1), (1, 32, 9, 9, 64, 3, 2, 2, 2)])
+def test_convolution_im2col(n, c, h, w, f, k, s, d, p):
+    import example_convolution as m
+    kern = _both(m.convolution, n, c, h, w, f, k, s, d, p, 64, 64, 32)
+    a, b = torch.randn(n, h, w, c).half(), torch.randn(k, k, c, f).half()
+    torch.testing.assert_close(kern(a, b).float(), m.ref_program(s, p, d)(a, b).float(), rtol=1e-2, atol=2e-2)

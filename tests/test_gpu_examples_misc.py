@@ -155,3 +155,22 @@ def test_mamba_chunk_scan():
     args = m.make_inputs(2, 1024, 256, 1, 8, 64, 128)
     k = m.chunk_scan_fwd(2, 1024, 256, 1, 8, 64, 128)
     torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=2e-2, atol=5e-2)
+
+
+def test_dequant_gemm_w4a16():
+    import example_dequant_gemm_w4a16 as m
+    for M in (16, 256):
+        k = m.dequant_gemm_w4a16(M, 1024, 2048)
+        A = torch.randn(M, 2048, device="cuda", dtype=torch.float16)
+        W = torch.randn(1024, 2048, device="cuda", dtype=torch.float16)
+        Bq, s = m.quantize_int4(W)
+        torch.testing.assert_close(k(A, Bq, s).float(), m.ref_program(A, Bq, s).float(), rtol=1e-2, atol=5e-1)
+
+
+def test_convolution_im2col():
+    import example_convolution as m
+    for (n, c, h, w, f, k, s, d, p) in ((8, 64, 32, 32, 128, 3, 1, 1, 1), (4, 64, 33, 33, 128, 3, 2, 1, 1)):
+        kern = m.convolution(n, c, h, w, f, k, s, d, p)
+        a = torch.randn(n, h, w, c, device="cuda", dtype=torch.float16)
+        b = torch.randn(k, k, c, f, device="cuda", dtype=torch.float16)
+        torch.testing.assert_close(kern(a, b).float(), m.ref_program(s, p, d)(a, b).float(), rtol=1e-2, atol=1e-1)

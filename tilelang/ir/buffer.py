@@ -28,6 +28,10 @@ def _norm_scope(scope: str) -> str:
     return scope
 
 
+# data-pointer var uid -> buffer (``T.Tensor(shape, dtype, buf.data)`` re-views a buffer's storage)
+DATA_OWNERS = {}
+
+
 class Buffer:
     """A typed n-d buffer.  Indexing builds loads/stores/regions."""
 
@@ -42,6 +46,7 @@ class Buffer:
         self.strides = list(strides) if strides is not None else None
         self.offset = offset
         self.data = Var(name, _dt.handle)
+        DATA_OWNERS[self.data.uid] = self
         # filled by passes
         self.layout = None       # Layout for shared buffers (swizzle) / Fragment for fragments
         self.param_index = None  # position in the kernel signature (global buffers)

@@ -1201,7 +1201,43 @@ class TileOpLowerer(Mutator):
     lower_CommFenceOp = lower_CommBroadcastOp
 
     def lower_Im2ColOp(self, op):
-        raise LoweringError("T.c2d_im2col lowering: use the convolution example's explicit gather instead")
+        """``T.c2d_im2col(img[N,H,W,C], col[bm, bk], nhw_step, c_step, K, S, D, P)``: gather one
+        implicit-GEMM A tile (rows = output pixels, cols = (kh, kw, c)) with zero padding
+        (reference src/op/copy.cc:1878 Conv2DIm2ColOpNode::Lower)."""
+        img, col = op.img.buffer, op.col
+        shp = img.static_shape()
+        if shp is None or len(shp) != 4:
+            raise LoweringError("T.c2d_im2col needs a static NHWC image tensor")
+        _, H, W, C = shp
+        KH = KW = int(op.kernel)
+        Sd, Dd, Pd = int(op.stride), int(op.dilation), int(op.pad)
+        OH = (H + 2 * Pd - Dd * (KH - 1) - 1) // Sd + 1
+        OW = (W + 2 * Pd - Dd * (KW - 1) - 1) // Sd + 1
+        ext = col.static_extents()
+        if ext is None or len([e for e in ext if e != 1]) != 2:
+            raise LoweringError("T.c2d_im2col destination must be a 2-D tile")
+        bm, bk = [e for e in ext if e != 1]
+        i, j = Var("ic_i"), Var("ic_j")
+        m = binop("+", binop("*", op.nhw_step, bm), i)
+        k = binop("+", binop("*", op.c_step, bk), j)
+        n = binop("//", m, OH * OW)
+        oh = binop("//", binop("%", m, OH * OW), OW)
+        ow = binop("%", m, OW)
+        h = binop("-", binop("+", binop("*", oh, Sd), binop("*", binop("//", k, KW * C), Dd)), Pd)
+        w = binop("-", binop("+", binop("*", ow, Sd), binop("*", binop("%", binop("//", k, C), KW), Dd)), Pd)
+        inb = logical_and(logical_and(binop(">=", h, 0), binop("<", h, H)),
+                          logical_and(binop(">=", w, 0), binop("<", w, W)))
+        # clamp the gather address so the load itself stays inside the image
+        hc = binop("min", binop("max", h, 0), H - 1)
+        wc = binop("min", binop("max", w, 0), W - 1)
+        val = select(inb, BufferLoad(img, [n, hc, wc, binop("%", k, C)]), const(0, img.dtype))
+        cidx = list(col.mins)
+        nz = [d for d, e in enumerate(ext) if e != 1]
+        cidx[nz[0]] = binop("+", cidx[nz[0]], i)
+        cidx[nz[1]] = binop("+", cidx[nz[1]], j)
+        body = S.StoreStmt(col.buffer, cidx, cast(val, col.buffer.dtype))
+        nest = S.ForStmt(i, 0, bm, "parallel", S.ForStmt(j, 0, bk, "parallel", body))
+        return self.lower_nest(nest)
 
 
 # ---------------------------------------------------------------------------
