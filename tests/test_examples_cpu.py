@@ -100,7 +100,7 @@ def test_flash_attention_bwd(causal):
     delta = _both(m.flashattn_bwd_preprocess, B, H, S, D)(o, do)
     dq = torch.zeros(B, S, H, D)
     dk, dv = torch.empty_like(q), torch.empty_like(q)
-    _both(m.flashattn_bwd, B, H, S, D, causal, 64, 64)(q, k, v, do, lse, delta, dq, dk, dv)
+    _both(m.flashattn_bwd, B, H, S, D, causal, 64, 64, 256)(q, k, v, do, lse, delta, dq, dk, dv)
     dqh = _both(m.flashattn_bwd_postprocess, B, H, S, D)(dq)
     for a, r in ((dqh, qf.grad), (dk, kf.grad), (dv, vf.grad)):
         torch.testing.assert_close(a.float(), r, rtol=1e-2, atol=1e-2)
