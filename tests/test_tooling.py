@@ -1,0 +1,99 @@
+"""Carver (config recommender), static analyzer, layout plotting and quantisation helpers (CPU)."""
+import os
+
+import pytest
+import torch
+
+import tilelang
+import tilelang.language as T
+from tilelang import quantize as Q
+from tilelang.carver.arch import CDNA
+from tilelang.carver.template import (ElementwiseTemplate, FlashAttentionTemplate, GEMVTemplate, MatmulTemplate)
+
+
+def test_carver_matmul_hints_fit_hardware():
+    arch = CDNA("hip")
+    hints = MatmulTemplate(M=4096, N=4096, K=4096).with_arch(arch).recommend_hints(topk=8)
+    assert hints and all(h.estimated_us > 0 for h in hints)
+    for h in hints:
+        cfg = h.to_config()
+        eb = 2
+        assert cfg["num_stages"] * (cfg["block_M"] + cfg["block_N"]) * cfg["block_K"] * eb <= 160 * 1024
+        assert cfg["threads"] % 64 == 0
+    assert hints == sorted(hints, key=lambda h: h.estimated_us)
+    # big square GEMMs want big tiles and rasterisation
+    assert hints[0].block[0] * hints[0].block[1] >= 128 * 128
+    small = MatmulTemplate(M=16, N=8192, K=8192).with_arch(arch).recommend_hints(topk=3)
+    assert small[0].block[0] <= 64
+
+
+def test_carver_other_templates():
+    arch = CDNA("hip")
+    assert FlashAttentionTemplate(heads=64, seq_len=4096).with_arch(arch).recommend_hints(3)
+    g = GEMVTemplate(N=16384, K=16384).with_arch(arch).recommend_hints(3)
+    assert set(g[0].to_config()) >= {"block_N", "block_K", "threads"}
+    e = ElementwiseTemplate(shape=[8192, 8192], dtype="float32").with_arch(arch).recommend_hints(3)
+    assert e and e[0].threads in (128, 256, 512)
+
+
+def test_carver_hints_drive_a_kernel_factory():
+    from example_gemm import matmul
+    hint = MatmulTemplate(M=256, N=256, K=256).with_arch(CDNA()).recommend_hints(topk=1)[0]
+    c = hint.to_config()
+    f = matmul.get_tir(256, 256, 256, c["block_M"], c["block_N"], c["block_K"], c["threads"], c["num_stages"])
+    k = tilelang.compile(f, out_idx=[-1], target="cpu")
+    a, b = torch.randn(256, 256).half(), torch.randn(256, 256).half()
+    torch.testing.assert_close(k(a, b).float(), a.float() @ b.float(), rtol=1e-2, atol=1e-2)
+
+
+def test_static_analyzer_counts_gemm_flops_and_bytes():
+    from tilelang.tools import Analyzer
+    from example_gemm import matmul
+    f = matmul.get_tir(1024, 1024, 1024, 128, 128, 32, 256, 2)
+    r = Analyzer.analysis(f, "MI355X")
+    assert r.total_flops == pytest.approx(2 * 1024**3)
+    # A and B tiles are re-read once per output tile; C written once
+    assert r.total_global_bytes == pytest.approx((1024 * 1024 * 2) * (1024 // 128) * 2 + 1024 * 1024 * 2)
+    assert r.bound == "memory" and r.estimated_time_us > 0  # tile re-reads counted as HBM traffic (no L2 model)
+
+
+def test_plot_layout_writes_grid(tmp_path):
+    from tilelang.layout import mfma as MF
+    from tilelang.tools import plot_layout, layout_text
+    frag = MF.mfma_c_fragment(16, 16, 1, 1)
+    txt = layout_text(frag)
+    assert txt.count("T") == 16 * 16
+    p = plot_layout(frag, str(tmp_path), "c16", "txt,svg")
+    assert os.path.exists(p) and os.path.exists(os.path.join(tmp_path, "c16.svg"))
+
+
+def test_int4_and_mxfp4_roundtrip():
+    W = torch.randn(64, 256)
+    packed, s = Q.quantize_int4_groupwise(W, 128)
+    assert packed.shape == (64, 128) and packed.dtype == torch.uint8
+    assert (Q.dequantize_int4_groupwise(packed, s, 128) - W).abs().max() <= s.max() * 0.51
+    pk, e = Q.quantize_mxfp4(W, 32)
+    deq = Q.dequantize_mxfp4(pk, e, 32)
+    rel = (deq - W).abs() / W.abs().clamp(min=1e-3)
+    assert rel.median() < 0.15
+    codes = torch.arange(16, dtype=torch.uint8)
+    assert torch.equal(Q.float_to_e2m1(Q.e2m1_to_float_torch(codes)) & 0xF, torch.where(codes == 8, 0, codes).to(torch.uint8))
+
+
+@tilelang.jit(out_idx=[-1], target="cpu")
+def _deq_kernel(N, K):
+
+    @T.prim_func
+    def main(P: T.Tensor((N, K // 2), "uint8"), E: T.Tensor((N, K // 32), "uint8"), O: T.Tensor((N, K), "float32")):
+        with T.Kernel(1, is_cpu=True):
+            for n, k in T.Parallel(N, K):
+                O[n, k] = Q.fp4_to_float(P[n, k // 2], k % 2) * Q.e8m0_to_float(E[n, k // 32])
+
+    return main
+
+
+def test_dsl_dequant_expressions_match_host():
+    W = torch.randn(8, 64)
+    pk, e = Q.quantize_mxfp4(W, 32)
+    out = _deq_kernel(8, 64)(pk, e)
+    torch.testing.assert_close(out, Q.dequantize_mxfp4(pk, e, 32))

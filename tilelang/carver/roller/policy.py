@@ -1,0 +1,152 @@
+"""CDNA4 tile-config policies (reference ``tilelang/carver/roller/policy/{default,tensorcore}.py``).
+
+``TensorCorePolicy`` ranks GEMM-shaped tilings with an MI355X model:
+
+* MFMA peak per CU = peak / CUs (4096 fp16 FLOP/clk/CU at 2.4 GHz);
+* LDS feed: a wave computing a ``wm x wn`` tile reads ``(wm + wn) * bk`` operand elements
+  per ``2 * wm * wn * bk`` FLOPs through ds_read_b128 at 128 B/clk/CU, so small wave tiles
+  are LDS-bound (64x64 per wave is the break-even point for fp16);
+* latency hiding from resident waves (LDS / accumulator-register limited occupancy);
+* HBM traffic with L2 reuse inside a rasterisation panel, and wave quantisation over the CUs.
+
+``DefaultPolicy`` sizes memory-bound (elementwise / GEMV / reduction) tiles for 16-byte
+lanes and enough blocks to cover every CU several times.
+"""
+from __future__ import annotations
+
+import itertools
+import math
+from typing import List, Optional, Sequence
+
+from .hint import Hint
+from .rasterization import NoRasterization, Rasterization2DRow
+
+_EB = {"float16": 2, "bfloat16": 2, "float8_e4m3fn": 1, "float8_e5m2": 1, "int8": 1, "float32": 4, "float": 4}
+
+
+def _eb(dtype) -> int:
+    return _EB.get(str(dtype), 2)
+
+
+def gemm_cost(arch, M, N, K, bm, bn, bk, threads, stages, in_dtype="float16", warp=None) -> Optional[dict]:
+    """Modelled time (us) of one tiling, or None if it does not fit the hardware."""
+    eb = _eb(in_dtype)
+    waves = threads // 64
+    if threads % 64 or waves not in (1, 2, 4, 8, 16):
+        return None
+    if bk * eb < 32 or (bk * eb) % 64 and eb == 1:
+        return None
+    lds = stages * (bm + bn) * bk * eb
+    if lds > arch.smem_cap:
+        return None
+    acc_regs = bm * bn // threads  # fp32 accumulators per lane
+    if acc_regs > 256 or acc_regs < 4:
+        return None
+    if warp is None:
+        from ...layout.mfma import compute_warp_partition
+        try:
+            wpm, wpn = compute_warp_partition(bm, bn, waves, 0)
+        except Exception:  # noqa: BLE001
+            return None
+        wm, wn = bm // wpm, bn // wpn
+    else:
+        wm, wn = warp
+    if wm < 16 or wn < 16:
+        return None
+    per_cu_flops = arch.peak_tflops.get(str(in_dtype), 2500.0) * 1e12 / arch.compute_max_core
+    clk = arch.clock_ghz * 1e9
+    mfma_per_clk = per_cu_flops / clk
+    # LDS-feed bound (ds_read 128 B/clk/CU shared by the resident waves)
+    lds_eff = min(1.0, (2.0 * wm * wn / ((wm + wn) * eb)) * 128.0 / mfma_per_clk)
+    # residency: LDS, registers (accumulators + ~64 operand/address VGPRs of the 512 per lane)
+    # and the 8-waves-per-SIMD cap
+    waves_per_simd_by_regs = min(8, 512 // (acc_regs + 64))
+    blocks_by_regs = (waves_per_simd_by_regs * 4) // waves
+    blocks_per_cu = max(1, min(arch.smem_cap // max(lds, 1), blocks_by_regs, 32 // waves))
+    resident_waves = blocks_per_cu * waves
+    occ_eff = 0.55 + 0.45 * min(1.0, resident_waves / 8.0)
+    pipe_eff = 0.85 if stages >= 2 else 0.65
+    eff = lds_eff * occ_eff * pipe_eff
+    tiles_m, tiles_n = math.ceil(M / bm), math.ceil(N / bn)
+    n_tiles = tiles_m * tiles_n
+    concurrent = arch.compute_max_core * blocks_per_cu
+    rounds = math.ceil(n_tiles / concurrent)
+    tile_flops = 2.0 * bm * bn * K
+    t_compute = rounds * tile_flops / (per_cu_flops * eff / blocks_per_cu)
+    # HBM traffic: inside a panel of 8 tile rows the B panel is reused from L2
+    panel = 8 if n_tiles > arch.compute_max_core else 1
+    traffic = (M * K * tiles_n / max(1, min(panel, tiles_n)) + N * K * tiles_m / max(1, min(panel, tiles_m))) * eb
+    traffic += M * N * 2
+    t_mem = traffic / (arch.bandwidth[0] * 1e9)
+    t = max(t_compute, t_mem)
+    return dict(us=t * 1e6, eff=eff, lds_eff=lds_eff, occ=resident_waves, rounds=rounds, warp=(wm, wn),
+                raster=panel > 1, lds_bytes=lds, t_compute_us=t_compute * 1e6, t_mem_us=t_mem * 1e6)
+
+
+class TensorCorePolicy:
+
+    def __init__(self, arch, M, N, K, in_dtype="float16", trans_b=False):
+        self.arch, self.M, self.N, self.K = arch, M, N, K
+        self.in_dtype = in_dtype
+        self.trans_b = trans_b
+
+    def candidates(self):
+        bms = [b for b in (32, 64, 128, 256) if b <= max(32, self.M * 2)]
+        bns = [b for b in (32, 64, 128, 256) if b <= max(32, self.N * 2)]
+        eb = _eb(self.in_dtype)
+        bks = [b for b in ((32, 64, 128) if eb == 2 else (64, 128, 256)) if self.K % b == 0] or [32 // eb * 2]
+        return itertools.product(bms, bns, bks, (256, 512), (2, 3))
+
+    def emit_config(self, topk: int = 10) -> List[Hint]:
+        hints = []
+        for bm, bn, bk, th, st in self.candidates():
+            c = gemm_cost(self.arch, self.M, self.N, self.K, bm, bn, bk, th, st, self.in_dtype)
+            if c is None:
+                continue
+            hints.append(Hint(block=[bm, bn], warp=list(c["warp"]), rstep=[bk], pipeline_stage=st, threads=th,
+                              rasterization_plan=Rasterization2DRow(8) if c["raster"] else NoRasterization(),
+                              estimated_us=c["us"], score=c))
+        hints.sort(key=lambda h: (h.estimated_us, -h.block[0] * h.block[1]))
+        return hints[:topk]
+
+
+class DefaultPolicy:
+    """Memory-bound tiles: ``shape`` is the output iteration space, ``reduce_len`` the per-output
+    reduction length (GEMV / row reductions), 0 for elementwise."""
+
+    def __init__(self, arch, shape: Sequence[int], dtype="float16", reduce_len: int = 0, bytes_per_elem=None):
+        self.arch = arch
+        self.shape = list(shape)
+        self.dtype = dtype
+        self.reduce_len = reduce_len
+        self.eb = bytes_per_elem or _eb(dtype)
+
+    def emit_config(self, topk: int = 10) -> List[Hint]:
+        vec = max(1, 16 // self.eb)
+        total = 1
+        for s in self.shape:
+            total *= s
+        hints = []
+        rows = self.shape[0] if len(self.shape) > 1 else 1
+        cols = self.shape[-1]
+        for th in (128, 256, 512):
+            for bm in (1, 2, 4, 8, 16, 32, 64):
+                if bm > rows:
+                    continue
+                for bn in (64, 128, 256, 512, 1024, 2048):
+                    if bn > max(cols, vec) or (bm * bn) % (th * vec) and bm * bn >= th * vec:
+                        continue
+                    blocks = math.ceil(rows / bm) * math.ceil(cols / bn)
+                    cover = blocks / (self.arch.compute_max_core * max(1, 2048 // th))
+                    per_lane = bm * bn / th
+                    if per_lane > 64 or per_lane < 1:
+                        continue
+                    moved = total * self.eb * (2 if not self.reduce_len else 1) + (
+                        total * self.reduce_len * self.eb if self.reduce_len else 0)
+                    t = moved / (self.arch.bandwidth[0] * 1e9) * 1e6
+                    # under-filled chips and long per-lane serial chains both cost bandwidth
+                    t /= min(1.0, 0.3 + 0.7 * min(1.0, cover)) * (1.0 if per_lane <= 32 else 0.8)
+                    hints.append(Hint(block=[bm, bn], warp=[bm, bn], rstep=[], pipeline_stage=1, threads=th,
+                                      estimated_us=t, score=dict(blocks=blocks, cover=cover)))
+        hints.sort(key=lambda h: (h.estimated_us, -h.threads))
+        return hints[:topk]

@@ -1,1 +1,143 @@
+"""Low-bit weight formats: packing on the host (PyTorch) and dequantisation expressions for use
+inside kernels (reference ``tilelang/quantize/{quantization,mxfp,utils}.py``).
 
+Formats (gfx950-relevant):
+  * int4 (signed, two per byte, low nibble first) with group-wise scales  (W4A16 GEMM);
+  * fp4 e2m1 (OCP MX) with e8m0 block scales (MXFP4, 32 elements per scale) -- the operand
+    format of the gfx950 ``v_mfma_scale_f32_*_f8f6f4`` instructions;
+  * e8m0 scales (power-of-two, bias 127).
+
+The DSL helpers return ``PrimExpr``s, e.g. inside ``T.Parallel``::
+
+    B_shared[n, k] = T.Cast("float16", Q.int4_to_float(Bq_shared[n, k // 2], k % 2) * scale)
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+# ---------------------------------------------------------------------------------------------
+# DSL expressions
+# ---------------------------------------------------------------------------------------------
+
+
+def _T():
+    import tilelang.language as T
+    return T
+
+
+def int4_to_float(byte, hi):
+    """Signed int4 nibble ``hi`` (0 = low, 1 = high; may be an expression) of ``byte`` as fp32."""
+    T = _T()
+    nib = (byte >> (hi * 4)) & 15
+    return T.Cast("float32", T.Cast("int32", nib) - T.if_then_else(nib >= 8, 16, 0))
+
+
+def uint4_to_float(byte, hi, zero=8):
+    """Unsigned int4 with a zero point (AWQ/GPTQ style)."""
+    T = _T()
+    nib = (byte >> (hi * 4)) & 15
+    return T.Cast("float32", T.Cast("int32", nib) - zero)
+
+
+def e2m1_to_float(nib):
+    """OCP fp4 e2m1 -> fp32: magnitudes {0, .5, 1, 1.5, 2, 3, 4, 6} with a sign bit."""
+    T = _T()
+    e = (nib >> 1) & 3
+    m = nib & 1
+    mag = T.if_then_else(e == 0, T.Cast("float32", m) * 0.5,
+                         T.exp2(T.Cast("float32", e) - 1.0) * (1.0 + T.Cast("float32", m) * 0.5))
+    return T.if_then_else((nib & 8) != 0, -mag, mag)
+
+
+def fp4_to_float(byte, hi):
+    return e2m1_to_float((byte >> (hi * 4)) & 15)
+
+
+def e8m0_to_float(byte):
+    """e8m0 block scale -> fp32 (2^(byte - 127))."""
+    T = _T()
+    return T.exp2(T.Cast("float32", byte) - 127.0)
+
+
+# ---------------------------------------------------------------------------------------------
+# host-side packing (PyTorch)
+# ---------------------------------------------------------------------------------------------
+
+
+def pack_int4(q):
+    """int tensor in [-8, 7] of shape [..., K] -> uint8 [..., K/2] (low nibble = even k)."""
+    import torch
+    u = (q.to(torch.int32) & 0xF).to(torch.uint8)
+    return (u[..., 0::2] | (u[..., 1::2] << 4)).contiguous()
+
+
+def unpack_int4(packed):
+    import torch
+    lo = (packed & 0xF).to(torch.int32)
+    hi = (packed >> 4).to(torch.int32)
+    q = torch.stack([lo, hi], -1).flatten(-2)
+    return q - (q >= 8).to(torch.int32) * 16
+
+
+def quantize_int4_groupwise(W, group_size: int = 128) -> Tuple:
+    """Symmetric int4 with one scale per ``group_size`` along the last dim."""
+    import torch
+    shp = W.shape
+    g = W.float().reshape(*shp[:-1], shp[-1] // group_size, group_size)
+    scales = (g.abs().amax(-1) / 7.0).clamp(min=1e-8)
+    q = torch.clamp(torch.round(g / scales.unsqueeze(-1)), -8, 7).reshape(shp)
+    return pack_int4(q), scales.to(W.dtype)
+
+
+def dequantize_int4_groupwise(packed, scales, group_size: int = 128):
+    q = unpack_int4(packed).float()
+    shp = q.shape
+    g = q.reshape(*shp[:-1], shp[-1] // group_size, group_size)
+    return (g * scales.float().unsqueeze(-1)).reshape(shp)
+
+
+_E2M1 = [0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0]
+
+
+def float_to_e2m1(x):
+    """Round-to-nearest onto the e2m1 grid (saturating at 6); returns uint8 codes."""
+    import torch
+    grid = torch.tensor(_E2M1, device=x.device)
+    mag = x.abs().clamp(max=6.0)
+    code = (mag.unsqueeze(-1) - grid).abs().argmin(-1).to(torch.uint8)
+    return code | ((x < 0).to(torch.uint8) << 3)
+
+
+def e2m1_to_float_torch(code):
+    import torch
+    grid = torch.tensor(_E2M1, device=code.device)
+    mag = grid[(code & 7).long()]
+    return torch.where((code & 8) != 0, -mag, mag)
+
+
+def quantize_mxfp4(W, block: int = 32) -> Tuple:
+    """OCP MXFP4: per 32 elements an e8m0 scale 2^floor(log2(amax)) - 2 (so amax/scale <= 6)."""
+    import torch
+    shp = W.shape
+    g = W.float().reshape(*shp[:-1], shp[-1] // block, block)
+    amax = g.abs().amax(-1).clamp(min=2.0**-126)
+    e = torch.floor(torch.log2(amax)) - 2
+    scale = torch.exp2(e)
+    codes = float_to_e2m1(g / scale.unsqueeze(-1)).reshape(shp)
+    packed = (codes[..., 0::2] | (codes[..., 1::2] << 4)).contiguous()
+    return packed, (e + 127).clamp(0, 254).to(torch.uint8)
+
+
+def dequantize_mxfp4(packed, scales_e8m0, block: int = 32):
+    import torch
+    lo = e2m1_to_float_torch(packed & 0xF)
+    hi = e2m1_to_float_torch(packed >> 4)
+    v = torch.stack([lo, hi], -1).flatten(-2)
+    shp = v.shape
+    s = torch.exp2(scales_e8m0.float() - 127.0)
+    return (v.reshape(*shp[:-1], shp[-1] // block, block) * s.unsqueeze(-1)).reshape(shp)
+
+
+__all__ = ["int4_to_float", "uint4_to_float", "e2m1_to_float", "fp4_to_float", "e8m0_to_float", "pack_int4",
+           "unpack_int4", "quantize_int4_groupwise", "dequantize_int4_groupwise", "float_to_e2m1",
+           "e2m1_to_float_torch", "quantize_mxfp4", "dequantize_mxfp4"]
