@@ -123,7 +123,8 @@ def flashattn_bwd_postprocess(batch, heads, seq_len, dim, blk=64, threads=256, d
 
 @tilelang.jit
 def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=512, num_stages=2,
-                  dtype="float16"):
+                  dtype="float16", dq_mode="atomic"):
+    """``dq_mode``: "atomic" (fp32 atomics into dQ) or "none" (skip dQ: profiling the dK/dV part)."""
     sm_scale = (1.0 / dim)**0.5
     scale = sm_scale * LOG2E
     shape = [batch, seq_len, heads, dim]
@@ -177,10 +178,11 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
                 for i, j in T.Parallel(block_M, block_N):
                     dsT_cast[i, j] = qkT[i, j] * (dsT[i, j] - delta[j]) * sm_scale
                 T.gemm(dsT_cast, q, dk, policy=T.GemmWarpPolicy.FullRow)
-                T.copy(dsT_cast, dsT_shared)
-                T.clear(dq)
-                T.gemm(dsT_shared, K_shared, dq, transpose_A=True)
-                T.atomic_add(dQ[bz, k * block_N:(k + 1) * block_N, bx, :], dq)
+                if dq_mode == "atomic":
+                    T.copy(dsT_cast, dsT_shared)
+                    T.clear(dq)
+                    T.gemm(dsT_shared, K_shared, dq, transpose_A=True)
+                    T.atomic_add(dQ[bz, k * block_N:(k + 1) * block_N, bx, :], dq)
             T.copy(dv, dv_cast)
             T.copy(dk, dk_cast)
             T.copy(dv_cast, dV[bz, by * block_M:(by + 1) * block_M, bx, :])

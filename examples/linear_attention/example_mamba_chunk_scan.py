@@ -7,7 +7,8 @@ out[c, l] = exp(dA_l) * C_l . prev_state_c                                   (in
           + D * x_l
 Block = (head, (m-tile, n-tile), batch*chunk).  The decay-weighted, causally masked CB tile is
 built in registers in the MFMA A-operand layout and fed straight to the x-tile MFMA (no LDS
-round trip); the decays use exp2 with log2(e) folded in.
+round trip); the per-column dA/dt slices ride the same LDS-DMA pipeline as the CB and x tiles
+(no register loads from HBM inside the loop); the decays use exp2 with log2(e) folded in.
 """
 import argparse
 
@@ -44,8 +45,8 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
             st_shared = T.alloc_shared((block_N, dstate), dtype)
             dA_m = T.alloc_fragment((block_M, ), accum_dtype)
             scale_m = T.alloc_fragment((block_M, ), accum_dtype)
-            dA_k = T.alloc_fragment((block_K, ), accum_dtype)
-            dt_k = T.alloc_fragment((block_K, ), accum_dtype)
+            dA_k = T.alloc_shared((block_K, ), dtype)
+            dt_k = T.alloc_shared((block_K, ), dtype)
             x_res = T.alloc_fragment((block_M, block_N), dtype)
             o_cast = T.alloc_fragment((block_M, block_N), dtype)
             b = by % batch
@@ -73,7 +74,8 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
                 for i, j in T.Parallel(block_M, block_K):
                     cb_local[i, j] = T.if_then_else(
                         m_idx * block_M + i >= k * block_K + j,
-                        cb_shared[i, j] * T.exp2(dA_m[i] * LOG2E - dA_k[j] * LOG2E) * dt_k[j], 0)
+                        cb_shared[i, j] * T.exp2(dA_m[i] * LOG2E - T.Cast(accum_dtype, dA_k[j]) * LOG2E) *
+                        T.Cast(accum_dtype, dt_k[j]), 0)
                 T.gemm(cb_local, x_shared, acc_o)
             T.copy(x[b, row0:row0 + block_M, bz, n_idx * block_N:(n_idx + 1) * block_N], x_res)
             for i, j in T.Parallel(block_M, block_N):
