@@ -124,17 +124,15 @@ def flashattn_bwd_postprocess(batch, heads, seq_len, dim, blk=64, threads=256, d
 @tilelang.jit
 def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=512, num_stages=2,
                   dtype="float16", dq_mode="atomic"):
-    """``dq_mode``: "atomic" (fp32 atomics into dQ) or "none" (skip dQ: profiling the dK/dV part)."""
+    """``dq_mode``: "atomic" (fp32 atomics into dQ, one kernel) or "none" (dK/dV only; dQ comes from
+    ``flashattn_bwd_dq``) -- the dQ atomics were 85% of the single-kernel time on MI355X."""
     sm_scale = (1.0 / dim)**0.5
     scale = sm_scale * LOG2E
     shape = [batch, seq_len, heads, dim]
     accum_dtype = "float"
 
-    @T.prim_func
-    def flash_bwd(Q: T.Tensor(shape, dtype), K: T.Tensor(shape, dtype), V: T.Tensor(shape, dtype),
-                  dO: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
-                  Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dQ: T.Tensor(shape, accum_dtype),
-                  dK: T.Tensor(shape, dtype), dV: T.Tensor(shape, dtype)):
+    @T.macro
+    def body(Q, K, V, dO, lse, Delta, dQ, dK, dV):
         with T.Kernel(heads, T.ceildiv(seq_len, block_M), batch, threads=threads) as (bx, by, bz):
             K_shared = T.alloc_shared([block_M, dim], dtype)
             V_shared = T.alloc_shared([block_M, dim], dtype)
@@ -188,7 +186,78 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
             T.copy(dv_cast, dV[bz, by * block_M:(by + 1) * block_M, bx, :])
             T.copy(dk_cast, dK[bz, by * block_M:(by + 1) * block_M, bx, :])
 
+    if dq_mode == "atomic":
+
+        @T.prim_func
+        def flash_bwd(Q: T.Tensor(shape, dtype), K: T.Tensor(shape, dtype), V: T.Tensor(shape, dtype),
+                      dO: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
+                      Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dQ: T.Tensor(shape, accum_dtype),
+                      dK: T.Tensor(shape, dtype), dV: T.Tensor(shape, dtype)):
+            body(Q, K, V, dO, lse, Delta, dQ, dK, dV)
+    else:
+
+        @T.prim_func
+        def flash_bwd(Q: T.Tensor(shape, dtype), K: T.Tensor(shape, dtype), V: T.Tensor(shape, dtype),
+                      dO: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
+                      Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dK: T.Tensor(shape, dtype),
+                      dV: T.Tensor(shape, dtype)):
+            body(Q, K, V, dO, lse, Delta, None, dK, dV)
+
     return flash_bwd
+
+
+@tilelang.jit(out_idx=[6])
+def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=256, num_stages=2,
+                     dtype="float16"):
+    """dQ without atomics: one block per (query tile, head, batch) walks the KV tiles, recomputing
+    P and dP (2 extra GEMMs) and accumulating dQ = dS K in registers -- on MI355X this is ~4x
+    faster than fp32 atomics from every KV block (measured: docs/RESULTS.md)."""
+    sm_scale = (1.0 / dim)**0.5
+    scale = sm_scale * LOG2E
+    shape = [batch, seq_len, heads, dim]
+    accum_dtype = "float"
+
+    @T.prim_func
+    def flash_bwd_dq(Q: T.Tensor(shape, dtype), K: T.Tensor(shape, dtype), V: T.Tensor(shape, dtype),
+                     dO: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
+                     Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dQ: T.Tensor(shape, dtype)):
+        with T.Kernel(heads, T.ceildiv(seq_len, block_M), batch, threads=threads) as (bx, by, bz):
+            q = T.alloc_shared([block_M, dim], dtype)
+            do = T.alloc_shared([block_M, dim], dtype)
+            K_shared = T.alloc_shared([block_N, dim], dtype)
+            V_shared = T.alloc_shared([block_N, dim], dtype)
+            lse_f = T.alloc_fragment([block_M], accum_dtype)
+            delta_f = T.alloc_fragment([block_M], accum_dtype)
+            s = T.alloc_fragment([block_M, block_N], accum_dtype)
+            dp = T.alloc_fragment([block_M, block_N], accum_dtype)
+            ds_cast = T.alloc_fragment([block_M, block_N], dtype)
+            dq = T.alloc_fragment([block_M, dim], accum_dtype)
+            dq_cast = T.alloc_fragment([block_M, dim], dtype)
+            T.copy(Q[bz, by * block_M:(by + 1) * block_M, bx, :], q)
+            T.copy(dO[bz, by * block_M:(by + 1) * block_M, bx, :], do)
+            T.copy(lse[bz, bx, by * block_M:(by + 1) * block_M], lse_f)
+            T.copy(Delta[bz, bx, by * block_M:(by + 1) * block_M], delta_f)
+            T.clear(dq)
+            loop_ed = T.ceildiv((by + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N)
+            for k in T.Pipelined(loop_ed, num_stages=num_stages):
+                T.copy(K[bz, k * block_N:(k + 1) * block_N, bx, :], K_shared)
+                T.copy(V[bz, k * block_N:(k + 1) * block_N, bx, :], V_shared)
+                T.clear(s)
+                T.gemm(q, K_shared, s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.clear(dp)
+                T.gemm(do, V_shared, dp, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                for i, j in T.Parallel(block_M, block_N):
+                    ds_cast[i, j] = T.if_then_else(
+                        (by * block_M + i >= k * block_N + j) | (not is_causal),
+                        T.exp2(s[i, j] * scale - lse_f[i]) * (dp[i, j] - delta_f[i]) * sm_scale, 0)
+                T.gemm(ds_cast, K_shared, dq, policy=T.GemmWarpPolicy.FullRow)
+            T.copy(dq, dq_cast)
+            T.copy(dq_cast, dQ[bz, by * block_M:(by + 1) * block_M, bx, :])
+
+    return flash_bwd_dq
+
+
+BWD_DQ_MODE = "separate"  # or "atomic" (single kernel, fp32 atomics into dQ)
 
 
 class _attention:
@@ -218,11 +287,17 @@ class _attention:
                     dt = "bfloat16" if q.dtype == torch.bfloat16 else "float16"
                     do = do.contiguous()
                     delta = flashattn_bwd_preprocess(B, H, S, D, dtype=dt)(o, do)
-                    dq = torch.zeros(B, S, H, D, dtype=torch.float32, device=q.device)
                     dk = torch.empty_like(q)
                     dv = torch.empty_like(q)
-                    flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt)(q, k, v, do, lse, delta, dq, dk, dv)
-                    return flashattn_bwd_postprocess(B, H, S, D, dtype=dt)(dq), dk, dv, None
+                    if BWD_DQ_MODE == "atomic":
+                        dq = torch.zeros(B, S, H, D, dtype=torch.float32, device=q.device)
+                        flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt)(q, k, v, do, lse, delta, dq, dk, dv)
+                        return flashattn_bwd_postprocess(B, H, S, D, dtype=dt)(dq), dk, dv, None
+                    # dK/dV kernel without dQ + an atomic-free dQ kernel (the two could run on
+                    # separate streams; they only share read-only inputs)
+                    flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, dq_mode="none")(q, k, v, do, lse, delta, dk, dv)
+                    dq = flashattn_bwd_dq(B, H, S, D, ctx.causal, dtype=dt)(q, k, v, do, lse, delta)
+                    return dq, dk, dv, None
 
             cls.fn = Attn
         return cls.fn

@@ -167,3 +167,29 @@ def test_convolution_im2col(n, c, h, w, f, k, s, d, p):
     kern = _both(m.convolution, n, c, h, w, f, k, s, d, p, 64, 64, 32)
     a, b = torch.randn(n, h, w, c).half(), torch.randn(k, k, c, f).half()
     torch.testing.assert_close(kern(a, b).float(), m.ref_program(s, p, d)(a, b).float(), rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_flash_attention_bwd_atomic_free_dq(causal):
+    import example_mha_bwd as m
+    B, S, H, D = 1, 256, 2, 64
+    q, k, v, do = [torch.randn(B, S, H, D).half() for _ in range(4)]
+    o, lse = _both(m.flashattn_fwd, B, H, S, D, causal, 64, 64)(q, k, v)
+    delta = _both(m.flashattn_bwd_preprocess, B, H, S, D)(o, do)
+    dq = _both(m.flashattn_bwd_dq, B, H, S, D, causal, 64, 64, 256)(q, k, v, do, lse, delta)
+    dk, dv = torch.empty_like(q), torch.empty_like(q)
+    f = m.flashattn_bwd.get_tir(B, H, S, D, causal, 64, 64, 256, dq_mode="none")
+    tilelang.compile(f, target="hip")
+    tilelang.compile(f, target="cpu")(q, k, v, do, lse, delta, dk, dv)
+    qf, kf, vf = [t.float().requires_grad_() for t in (q, k, v)]
+    m.ref_program(qf, kf, vf, causal).backward(do.float())
+    for a, r in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
+        torch.testing.assert_close(a.float(), r, rtol=1e-2, atol=1e-2)
+
+
+def test_fused_moe_shared_plus_routed():
+    import example_fusedmoe_tilelang as m
+    w = m.init_weights(256, 128, 4, 1, device="cpu")
+    x = torch.randn(2, 64, 256).half()
+    out = m.FusedMoE(w, 2, block_M=64)(x)
+    torch.testing.assert_close(out.float(), m.ref_program(x, w, 2).float(), rtol=1e-2, atol=1e-2)

@@ -174,3 +174,11 @@ def test_convolution_im2col():
         a = torch.randn(n, h, w, c, device="cuda", dtype=torch.float16)
         b = torch.randn(k, k, c, f, device="cuda", dtype=torch.float16)
         torch.testing.assert_close(kern(a, b).float(), m.ref_program(s, p, d)(a, b).float(), rtol=1e-2, atol=1e-1)
+
+
+def test_fused_moe_shared_plus_routed():
+    import example_fusedmoe_tilelang as m
+    w = m.init_weights(1024, 512, 8, 1)
+    x = torch.randn(1, 512, 1024, device="cuda", dtype=torch.float16)
+    out = m.FusedMoE(w, 4)(x)
+    torch.testing.assert_close(out.float(), m.ref_program(x, w, 4).float(), rtol=2e-2, atol=2e-2)
