@@ -193,3 +193,34 @@ def test_fused_moe_shared_plus_routed():
     x = torch.randn(2, 64, 256).half()
     out = m.FusedMoE(w, 2, block_M=64)(x)
     torch.testing.assert_close(out.float(), m.ref_program(x, w, 2).float(), rtol=1e-2, atol=1e-2)
+
+
+def test_deepseek_v32_sparse_mla_fwd():
+    import sparse_mla_fwd as m
+    B, S, SKV, H, D, DT, topk = 1, 8, 64, 16, 64, 32, 64
+    k = _both(m.sparse_mla_fwd, B, S, SKV, H, D, DT, topk, 1, None, 32, 64, "float16")
+    q, kv = torch.randn(B, S, H, D + DT).half(), torch.randn(B, SKV, 1, D + DT).half()
+    idx = m.make_indices(B, S, SKV, 1, topk)
+    o, _ = k(q, kv, idx)
+    torch.testing.assert_close(o.float(), m.ref_program(q, kv, idx, D).float(), rtol=1e-2, atol=1e-2)
+
+
+def test_deepseek_v32_lightning_indexer():
+    import fp8_lighting_indexer as m
+    S, SKV, H, D = 8, 128, 16, 128
+    k = _both(m.mqa_attn_return_logits, S, SKV, H, D)
+    q, kv, sc, w, ks, ke = m.make_inputs(S, SKV, H, D, "cpu")
+    out = k(q.view(S * H, D), kv, sc, w, ks, ke)
+    ref = m.ref_program(q, kv, sc, w, ks, ke)
+    fin = torch.isfinite(ref)
+    assert torch.equal(torch.isfinite(out), fin)
+    torch.testing.assert_close(out[fin], ref[fin], rtol=1e-4, atol=1e-4)
+
+
+def test_deepseek_v32_topk_selector():
+    import topk_selector as m
+    x = torch.randn(4, 1024)
+    x[0, :10] = float("-inf")
+    x[1, 5:20] = 1.0  # ties at the threshold
+    idx = _both(m.topk_selector, 4, 1024, 64)(x)
+    m.check(x, idx, 64)

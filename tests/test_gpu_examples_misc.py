@@ -182,3 +182,25 @@ def test_fused_moe_shared_plus_routed():
     x = torch.randn(1, 512, 1024, device="cuda", dtype=torch.float16)
     out = m.FusedMoE(w, 4)(x)
     torch.testing.assert_close(out.float(), m.ref_program(x, w, 4).float(), rtol=2e-2, atol=2e-2)
+
+
+def test_deepseek_v32_kernels():
+    import fp8_lighting_indexer as li
+    import sparse_mla_fwd as sm
+    import topk_selector as ts
+    S, SKV, H, D = 256, 1024, 64, 128
+    q, kv, sc, w, ks, ke = li.make_inputs(S, SKV, H, D)
+    logits = li.mqa_attn_return_logits(S, SKV, H, D)(q.view(S * H, D), kv, sc, w, ks, ke)
+    ref = li.ref_program(q, kv, sc, w, ks, ke)
+    fin = torch.isfinite(ref)
+    assert torch.equal(torch.isfinite(logits), fin)
+    torch.testing.assert_close(logits[fin], ref[fin], rtol=2e-2, atol=2e-2)
+    x = torch.randn(512, 4096, device="cuda")
+    ts.check(x, ts.topk_selector(512, 4096, 512)(x), 512)
+    B, S2, SKV2, H2, topk = 1, 16, 512, 128, 256
+    qq = torch.randn(B, S2, H2, 576, device="cuda", dtype=torch.bfloat16)
+    kv2 = torch.randn(B, SKV2, 1, 576, device="cuda", dtype=torch.bfloat16)
+    idx = sm.make_indices(B, S2, SKV2, 1, topk, "cuda")
+    o, _ = sm.sparse_mla_fwd(B, S2, SKV2, H2, 512, 64, topk)(qq, kv2, idx)
+    torch.testing.assert_close(o.float().cpu(), sm.ref_program(qq.cpu(), kv2.cpu(), idx.cpu(), 512).float(),
+                               rtol=3e-2, atol=3e-2)

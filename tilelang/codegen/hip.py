@@ -242,7 +242,7 @@ class CodeGen:
                 raise CodeGenError("T.comm.current_core() used in a kernel without mesh parameters")
             return self.e(v)
         if op == "tl.sync_threads":
-            return "__syncthreads()"
+            return "tl::sync_threads()" if self.is_cpu else "__syncthreads()"
         if op == "tl.fence":
             return "tl::fence_agent()"
         raise CodeGenError(f"unknown intrinsic {op}")

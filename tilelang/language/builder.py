@@ -197,8 +197,10 @@ def assign(name: str, value, prev_thunk):
         value.data.name = value.name
         value._auto_name = False
         return value
-    if isinstance(prev, Buffer) and prev.scope == "var" and not isinstance(value, Buffer):
-        b.store(prev, [IntImm(0)], value)
+    if isinstance(prev, Buffer) and prev.scope == "var" and prev is not value and \
+            (not isinstance(value, Buffer) or value.scope == "var"):
+        # `x = y` / `x = expr` with x a T.alloc_var: store (y's current value when y is a var too)
+        b.store(prev, [IntImm(0)], value.as_scalar() if isinstance(value, Buffer) else value)
         return prev
     if isinstance(value, Buffer) and value.scope == "var" and b.in_kernel and prev is not value:
         value = value.as_scalar()   # `y = x` with x a T.alloc_var: capture x's current value
