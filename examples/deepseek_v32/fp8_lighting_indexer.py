@@ -15,44 +15,7 @@ import tilelang
 import tilelang.language as T
 
 
-@tilelang.jit(out_idx=[3])
-def mqa_attn_return_logits(seq_len, seq_len_kv, heads, index_dim, block_N=64, threads=256, block_Q=None):
-    if block_Q is None:
-        block_Q = max(1, 128 // heads)
-    QH = block_Q * heads
-    dtype = "float8_e4m3fn"
-    accum_dtype = "float"
-
-    @T.prim_func
-    def main(IndexQ: T.Tensor([seq_len * heads, index_dim], dtype), IndexK: T.Tensor([seq_len_kv, index_dim], dtype),
-             IndexKScale: T.Tensor([seq_len_kv], accum_dtype), Logits: T.Tensor([seq_len, seq_len_kv], accum_dtype),
-             Weights: T.Tensor([seq_len, heads], accum_dtype), CuSeqLenKS: T.Tensor([seq_len], "int32"),
-             CuSeqLenKE: T.Tensor([seq_len], "int32")):
-        with T.Kernel(T.ceildiv(seq_len, block_Q), threads=threads) as bx:
-            q_shared = T.alloc_shared([QH, index_dim], dtype)
-            k_shared = T.alloc_shared([block_N, index_dim], dtype)
-            s = T.alloc_fragment([block_N, QH], accum_dtype)
-            s_shared = T.alloc_shared([block_N, QH], accum_dtype)
-            q0 = bx * block_Q
-            T.copy(IndexQ[q0 * heads, 0], q_shared)
-            for nb in T.Pipelined(T.ceildiv(seq_len_kv, block_N), num_stages=2):
-                T.copy(IndexK[nb * block_N, 0], k_shared)
-                T.clear(s)
-                T.gemm(k_shared, q_shared, s, transpose_B=True)
-                for n, c in T.Parallel(block_N, QH):
-                    s_shared[n, c] = T.max(s[n, c], 0) * Weights[q0 + c // heads, c % heads] * \
-                        IndexKScale[nb * block_N + n]
-                for bq, n in T.Parallel(block_Q, block_N):
-                    acc = T.alloc_var(accum_dtype)
-                    acc = 0.0
-                    for h in T.serial(heads):
-                        acc += s_shared[n, bq * heads + h]
-                    kv_pos = nb * block_N + n
-                    Logits[q0 + bq, kv_pos] = T.if_then_else(
-                        (kv_pos >= CuSeqLenKS[q0 + bq]) & (kv_pos < CuSeqLenKE[q0 + bq]), acc,
-                        -T.infinity(accum_dtype))
-
-    return main
+from tilelang.ops.dsa import mqa_attn_return_logits  # noqa: E402,F401  (kernel lives in the library)
 
 
 def ref_program(q, kv, kv_scale, weights, ks, ke):

@@ -17,90 +17,7 @@ import tilelang.language as T
 LOG2E = 1.44269504
 
 
-@tilelang.jit(out_idx=[3, 4])
-def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_group=1, sm_scale=None, block_I=64,
-                   threads=256, dtype="bfloat16"):
-    assert topk % block_I == 0
-    if sm_scale is None:
-        sm_scale = (1.0 / (dim + tail_dim))**0.5
-    scale = sm_scale * LOG2E
-    accum_dtype = "float"
-    G = kv_group
-    H = heads // G
-    H_blk = min(64, max(16, H))
-    assert H % H_blk == 0 or H < 16
-    n_hblk = max(1, H // H_blk)
-    valid_h = min(H, H_blk)
-    D, DT = dim, tail_dim
-    NI = topk // block_I
-    past = seq_len_kv - seq_len
-
-    @T.prim_func
-    def main(Q: T.Tensor([batch, seq_len, heads, D + DT], dtype), KV: T.Tensor([batch, seq_len_kv, G, D + DT], dtype),
-             Indices: T.Tensor([batch, seq_len, G, topk], "int32"), Output: T.Tensor([batch, seq_len, heads, D], dtype),
-             Lse: T.Tensor([batch, seq_len, heads], accum_dtype)):
-        with T.Kernel(seq_len, n_hblk, batch * G, threads=threads) as (bx, by, bz):
-            b = bz // G
-            g = bz % G
-            h0 = g * H + by * H_blk
-            Q_shared = T.alloc_shared([H_blk, D], dtype)
-            Qt_shared = T.alloc_shared([H_blk, DT], dtype)
-            KV_shared = T.alloc_shared([block_I, D], dtype)
-            Kt_shared = T.alloc_shared([block_I, DT], dtype)
-            valid = T.alloc_shared([block_I], "int32")
-            acc_s = T.alloc_fragment([H_blk, block_I], accum_dtype)
-            acc_s_cast = T.alloc_fragment([H_blk, block_I], dtype)
-            acc_o = T.alloc_fragment([H_blk, D], accum_dtype)
-            o_cast = T.alloc_fragment([H_blk, D], dtype)
-            m_cur = T.alloc_fragment([H_blk], accum_dtype)
-            m_prev = T.alloc_fragment([H_blk], accum_dtype)
-            alpha = T.alloc_fragment([H_blk], accum_dtype)
-            l_sum = T.alloc_fragment([H_blk], accum_dtype)
-            r_sum = T.alloc_fragment([H_blk], accum_dtype)
-
-            T.clear(Q_shared)
-            T.clear(Qt_shared)
-            T.copy(Q[b, bx, h0:h0 + valid_h, 0:D], Q_shared[0:valid_h, :])
-            T.copy(Q[b, bx, h0:h0 + valid_h, D:D + DT], Qt_shared[0:valid_h, :])
-            T.fill(acc_o, 0)
-            T.fill(l_sum, 0)
-            T.fill(m_cur, -(2.0**30))
-            for i in T.serial(NI):
-                # gather the selected latent rows (masked rows read row 0 and are discarded)
-                for r in T.Parallel(block_I):
-                    idx = Indices[b, bx, g, i * block_I + r]
-                    valid[r] = T.if_then_else((idx <= bx + past) & (idx >= 0), 1, 0)
-                for r, d in T.Parallel(block_I, D):
-                    idx = Indices[b, bx, g, i * block_I + r]
-                    KV_shared[r, d] = KV[b, T.if_then_else((idx <= bx + past) & (idx >= 0), idx, 0), g, d]
-                for r, d in T.Parallel(block_I, DT):
-                    idx = Indices[b, bx, g, i * block_I + r]
-                    Kt_shared[r, d] = KV[b, T.if_then_else((idx <= bx + past) & (idx >= 0), idx, 0), g, D + d]
-                for h, r in T.Parallel(H_blk, block_I):
-                    acc_s[h, r] = T.if_then_else(valid[r] == 1, 0, -T.infinity(accum_dtype))
-                T.gemm(Q_shared, KV_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                T.gemm(Qt_shared, Kt_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                T.copy(m_cur, m_prev)
-                T.reduce_max(acc_s, m_cur, dim=1, clear=False)
-                for h in T.Parallel(H_blk):
-                    alpha[h] = T.exp2((m_prev[h] - m_cur[h]) * scale)
-                for h, r in T.Parallel(H_blk, block_I):
-                    acc_s[h, r] = T.exp2(acc_s[h, r] * scale - m_cur[h] * scale)
-                T.reduce_sum(acc_s, r_sum, dim=1)
-                for h in T.Parallel(H_blk):
-                    l_sum[h] = l_sum[h] * alpha[h] + r_sum[h]
-                for h, d in T.Parallel(H_blk, D):
-                    acc_o[h, d] *= alpha[h]
-                T.copy(acc_s, acc_s_cast)
-                T.gemm(acc_s_cast, KV_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
-            for h, d in T.Parallel(H_blk, D):
-                o_cast[h, d] = acc_o[h, d] / l_sum[h]
-            for h in T.Parallel(H_blk):
-                l_sum[h] = T.log2(l_sum[h]) + m_cur[h] * scale
-            T.copy(o_cast[0:valid_h, :], Output[b, bx, h0:h0 + valid_h, :])
-            T.copy(l_sum[0:valid_h], Lse[b, bx, h0:h0 + valid_h])
-
-    return main
+from tilelang.ops.dsa import sparse_mla_fwd  # noqa: E402,F401  (kernel lives in the library)
 
 
 def ref_program(q, kv, indices, dim=512, sm_scale=None):

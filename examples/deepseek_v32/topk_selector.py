@@ -15,52 +15,7 @@ import tilelang
 import tilelang.language as T
 
 
-@tilelang.jit(out_idx=[1])
-def topk_selector(M, N, topk, threads=256):
-    assert N % threads == 0
-
-    @T.prim_func
-    def main(Scores: T.Tensor([M, N], "float32"), Indices: T.Tensor([M, topk], "int32")):
-        with T.Kernel(M, threads=threads) as r:
-            keys = T.alloc_fragment([1, N], "int64")
-            hit = T.alloc_fragment([1, N], "int32")
-            cnt = T.alloc_fragment([1], "int32")
-            lo = T.alloc_var("int64")
-            hi = T.alloc_var("int64")
-            mid = T.alloc_var("int64")
-            pos = T.alloc_shared([2], "int32")
-            for z, j in T.Parallel(1, N):
-                bits = T.Cast("int64", T.reinterpret(Scores[r, j], "int32"))
-                keys[z, j] = T.if_then_else(bits >= 0, bits + 2147483648, 2147483647 - (bits & 2147483647))
-            lo = 0
-            hi = 4294967295
-            for _ in T.serial(32):
-                mid = (lo + hi + 1) // 2
-                for z, j in T.Parallel(1, N):
-                    hit[z, j] = T.if_then_else(keys[z, j] >= mid, 1, 0)
-                T.reduce_sum(hit, cnt, dim=1)
-                if cnt[0] >= topk:
-                    lo = mid
-                else:
-                    hi = mid - 1
-            # lo is the key of the k-th largest value: take everything above it, then fill
-            # the remaining slots with entries equal to it
-            for z, j in T.Parallel(1, N):
-                hit[z, j] = T.if_then_else(keys[z, j] > lo, 1, 0)
-            T.reduce_sum(hit, cnt, dim=1)
-            pos[0] = 0
-            pos[1] = cnt[0]
-            T.sync_threads()
-            for z, j in T.Parallel(1, N):
-                if keys[z, j] > lo:
-                    slot_gt = T.atomic_add(pos[0], 1, return_prev=True)
-                    Indices[r, slot_gt] = j
-                elif keys[z, j] == lo:
-                    slot = T.atomic_add(pos[1], 1, return_prev=True)
-                    if slot < topk:
-                        Indices[r, slot] = j
-
-    return main
+from tilelang.ops.dsa import topk_selector  # noqa: E402,F401  (kernel lives in the library)
 
 
 def ref_program(scores, topk):

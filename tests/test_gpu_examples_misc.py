@@ -204,3 +204,17 @@ def test_deepseek_v32_kernels():
     o, _ = sm.sparse_mla_fwd(B, S2, SKV2, H2, 512, 64, topk)(qq, kv2, idx)
     torch.testing.assert_close(o.float().cpu(), sm.ref_program(qq.cpu(), kv2.cpu(), idx.cpu(), 512).float(),
                                rtol=3e-2, atol=3e-2)
+
+
+def test_deepseek_v32_model_on_gpu():
+    from tilelang.models.deepseek_v32 import ModelArgs, Transformer, generate
+    args = ModelArgs.tiny()
+    m = Transformer(args, seed=0, device="cuda")
+    toks = torch.randint(0, args.vocab_size, (2, 12), generator=torch.Generator().manual_seed(1)).cuda()
+    full = m(toks, 0)
+    m2 = Transformer(args, seed=0, device="cuda")
+    m2(toks[:, :11], 0)
+    torch.testing.assert_close(m2(toks[:, 11:12], 11), full, rtol=3e-2, atol=3e-2)
+    cpu = Transformer(args, seed=0, device="cpu")(toks.cpu(), 0)
+    torch.testing.assert_close(full.cpu(), cpu, rtol=5e-2, atol=5e-2)
+    assert len(generate(m, [[1, 2, 3], [4, 5, 6, 7]], 4)[0]) == 4

@@ -1,0 +1,58 @@
+"""``linear(x, w)`` = x @ w^T on MFMA (reference counterpart: examples/deepseek_v32/inference/kernel.py
+``fp8_gemm`` / the model's ``linear``).  One compiled kernel per (M, N, K, dtype, target); the
+tile is chosen by M so decode-sized (skinny) and prefill-sized GEMMs both fill the CUs."""
+from __future__ import annotations
+
+import functools
+
+import torch
+
+import tilelang
+import tilelang.language as T
+
+
+def _tdt(dtype: torch.dtype) -> str:
+    return {torch.float16: "float16", torch.bfloat16: "bfloat16", torch.float32: "float32"}[dtype]
+
+
+def _tiles(M: int, N: int, K: int):
+    bm = 64 if M <= 64 else (128 if M <= 2048 else 256)
+    bn = 64 if N <= 256 else 128 if M <= 2048 else 256
+    bk = 64 if K % 64 == 0 else 32
+    threads = 256 if bm * bn <= 128 * 128 else 512
+    return bm, bn, bk, threads
+
+
+@functools.lru_cache(maxsize=None)
+def _linear_kernel(M, N, K, dtype, target):
+    bm, bn, bk, threads = _tiles(M, N, K)
+
+    @T.prim_func
+    def main(A: T.Tensor((M, K), dtype), W: T.Tensor((N, K), dtype), C: T.Tensor((M, N), dtype)):
+        with T.Kernel(T.ceildiv(N, bn), T.ceildiv(M, bm), threads=threads) as (bx, by):
+            A_s = T.alloc_shared((bm, bk), dtype)
+            W_s = T.alloc_shared((bn, bk), dtype)
+            acc = T.alloc_fragment((bm, bn), "float")
+            out = T.alloc_fragment((bm, bn), dtype)
+            T.use_swizzle(panel_size=8)
+            T.clear(acc)
+            for k in T.Pipelined(T.ceildiv(K, bk), num_stages=2):
+                T.copy(A[by * bm, k * bk], A_s)
+                T.copy(W[bx * bn, k * bk], W_s)
+                T.gemm(A_s, W_s, acc, transpose_B=True)
+            T.copy(acc, out)
+            T.copy(out, C[by * bm, bx * bn])
+
+    return tilelang.compile(main, out_idx=[-1], target=target)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """x [..., K] @ w[N, K]^T -> [..., N] in x's dtype (fp32 accumulation)."""
+    shp = x.shape
+    x2 = x.reshape(-1, shp[-1]).contiguous()
+    M, K = x2.shape
+    N = w.shape[0]
+    if K % 32 or x2.dtype == torch.float32:
+        return torch.nn.functional.linear(x, w)  # fp32 / odd K: not an MFMA shape (router logits etc.)
+    k = _linear_kernel(M, N, K, _tdt(x2.dtype), "cpu" if x2.device.type == "cpu" else "hip")
+    return k(x2, w.contiguous()).reshape(*shp[:-1], N)
