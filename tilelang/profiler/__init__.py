@@ -73,8 +73,12 @@ class Profiler:
     def do_bench(self, func: Optional[Callable] = None, warmup: int = 25, rep: int = 100, n_warmup: int = 0,
                  n_repeat: int = 0, input_tensors: Optional[List] = None, backend: str = "event",
                  quantiles=None, return_mode: str = "mean"):
-        ins = input_tensors or self._get_inputs()
         fn = func or self.kernel
+        if func is not None and _takes_no_args(func):
+            # ``profiler.do_bench(lambda: kernel(a, b))``: a closure over its own inputs
+            ins = []
+        else:
+            ins = input_tensors or self._get_inputs()
         if self.kernel.artifact.is_cpu:
             import time
             fn(*ins)
@@ -85,6 +89,16 @@ class Profiler:
             return (time.perf_counter() - t) / n * 1e3
         return do_bench(lambda: fn(*ins), warmup=warmup, rep=rep, _n_warmup=n_warmup, _n_repeat=n_repeat,
                         backend=backend, quantiles=quantiles, return_mode=return_mode)
+
+
+def _takes_no_args(fn) -> bool:
+    import inspect
+    try:
+        sig = inspect.signature(fn)
+    except (TypeError, ValueError):
+        return False
+    return all(p.default is not inspect.Parameter.empty or p.kind in (p.VAR_POSITIONAL, p.VAR_KEYWORD)
+               for p in sig.parameters.values())
 
 
 __all__ = ["Profiler", "do_bench"]
