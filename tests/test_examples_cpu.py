@@ -224,3 +224,28 @@ def test_deepseek_v32_topk_selector():
     x[1, 5:20] = 1.0  # ties at the threshold
     idx = _both(m.topk_selector, 4, 1024, 64)(x)
     m.check(x, idx, 64)
+
+
+def test_gemm_persistent():
+    import example_gemm_persistent as m
+    k = _both(m.matmul_persistent, 256, 384, 128, 64, 64, 32, 256, 2, 4)
+    a, b = torch.randn(256, 128).half(), torch.randn(128, 384).half()
+    torch.testing.assert_close(k(a, b).float(), a.float() @ b.float(), rtol=1e-2, atol=2e-2)
+
+
+def test_gemm_streamk():
+    import example_tilelang_gemm_streamk as m
+    k = _both(m.matmul_streamk, 128, 256, 256, 64, 64, 32, 5)
+    A, B = torch.randn(128, 256).half(), torch.randn(256, 256).half()
+    C = torch.zeros(128, 256)
+    k(A, B, C)
+    torch.testing.assert_close(C, A.float() @ B.float().t(), rtol=1e-3, atol=1e-3)
+
+
+def test_blocksparse_gemm():
+    import example_blocksparse_gemm as m
+    k = _both(m.blocksparse_matmul, 256, 256, 256, 64, 64, 32)
+    a, b = torch.randn(256, 256).half(), torch.randn(256, 256).half()
+    mask = torch.rand(4, 4, 8) > 0.5
+    torch.testing.assert_close(k(a, b, mask).float(), m.ref_program(a, b, mask, 64, 64, 32).float(), rtol=1e-2,
+                               atol=2e-2)

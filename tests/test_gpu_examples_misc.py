@@ -218,3 +218,21 @@ def test_deepseek_v32_model_on_gpu():
     cpu = Transformer(args, seed=0, device="cpu")(toks.cpu(), 0)
     torch.testing.assert_close(full.cpu(), cpu, rtol=5e-2, atol=5e-2)
     assert len(generate(m, [[1, 2, 3], [4, 5, 6, 7]], 4)[0]) == 4
+
+
+def test_gemm_persistent_streamk_blocksparse():
+    import example_gemm_persistent as gp
+    import example_tilelang_gemm_streamk as sk
+    import example_blocksparse_gemm as bs
+    a = torch.randn(1024, 512, device="cuda", dtype=torch.float16)
+    b = torch.randn(512, 768, device="cuda", dtype=torch.float16)
+    torch.testing.assert_close(gp.matmul_persistent(1024, 768, 512, 128, 128, 64, 256)(a, b).float(),
+                               a.float() @ b.float(), rtol=1e-2, atol=1e-1)
+    A = torch.rand(256, 512, device="cuda", dtype=torch.float16) * 2 - 1
+    B = torch.rand(1024, 512, device="cuda", dtype=torch.float16) * 2 - 1
+    C = torch.zeros(256, 1024, device="cuda")
+    sk.matmul_streamk(256, 1024, 512)(A, B, C)
+    torch.testing.assert_close(C, A.float() @ B.float().t(), rtol=1e-2, atol=1e-2)
+    mask = torch.rand(8, 6, 16, device="cuda") > 0.5
+    out = bs.blocksparse_matmul(1024, 768, 512)(a, b, mask)
+    torch.testing.assert_close(out.float(), bs.ref_program(a, b, mask, 128, 128, 32).float(), rtol=1e-2, atol=1e-1)

@@ -379,8 +379,36 @@ class _AllocReplacer(Mutator):
     def visit_AllocStmt(self, s):
         if s.buffer in self.replaced:
             nbs = self.replaced[s.buffer]
-            return S.seq(*[S.AllocStmt(nb) for nb in nbs])
+            keep = [s] if s.buffer in getattr(self, "still_used", ()) else []
+            return S.seq(*(keep + [S.AllocStmt(nb) for nb in nbs]))
         return s
+
+
+def _referenced_buffers(stmt) -> set:
+    """Buffers a (pre-lowering) statement reads or writes: tile-op regions, loads, stores."""
+    from ..ir.expr import post_order, BufferLoad
+    out = set()
+    for x in S.walk(stmt):
+        exprs = []
+        if isinstance(x, S.TileOpStmt):
+            for r in x.op.regions():
+                if hasattr(r, "buffer"):
+                    out.add(r.buffer)
+        elif isinstance(x, S.StoreStmt):
+            out.add(x.buffer)
+            exprs = [x.value] + list(x.indices)
+        elif isinstance(x, S.LetStmt):
+            exprs = [x.value]
+        elif isinstance(x, S.EvaluateStmt):
+            exprs = [x.expr]
+        elif isinstance(x, (S.IfStmt, S.WhileStmt)):
+            exprs = [x.cond]
+        for e in exprs:
+            if hasattr(e, "dtype"):
+                for n in post_order(e):
+                    if isinstance(n, BufferLoad):
+                        out.add(n.buffer)
+    return out
 
 
 def inject_software_pipeline(kernel: S.KernelStmt, num_threads: int, target) -> S.KernelStmt:
@@ -388,5 +416,10 @@ def inject_software_pipeline(kernel: S.KernelStmt, num_threads: int, target) -> 
     new = pi.stmt(kernel)
     replaced = getattr(pi, "replaced", {})
     if replaced:
-        new = _AllocReplacer(replaced).stmt(new)
+        ar = _AllocReplacer(replaced)
+        # a tile also used outside the pipelined loops (e.g. a stream-K partial loop next to a
+        # pipelined data-parallel loop) keeps its single-buffer allocation as well
+        used = _referenced_buffers(new)
+        ar.still_used = {b for b in replaced if b in used}
+        new = ar.stmt(new)
     return new
