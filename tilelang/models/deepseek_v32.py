@@ -295,7 +295,7 @@ class MLA(nn.Module):
         kvf = torch.cat([self.kv_cache[:b, :end], self.pe_cache[:b, :end]], -1).unsqueeze(2).contiguous()
         idx = self.indexer(x, qr, start_pos, freqs).unsqueeze(2).contiguous()    # [b, s, 1, topk]
         kern = dsa.sparse_mla_fwd(b, s, end, self.n_local_heads, self.kv_lora, self.rope, idx.shape[-1], 1,
-                                  self.softmax_scale, 64, 256, _tdt(x.dtype))
+                                  self.softmax_scale, 64, None, _tdt(x.dtype))
         o_lat, _ = kern(qf, kvf, idx)                                             # [b, s, h, 512]
         o = torch.einsum("bshc,hdc->bshd", o_lat.float(), wkv_b[:, -self.vdim:].float()).to(x.dtype)
         return self.wo(o.reshape(b, s, -1))

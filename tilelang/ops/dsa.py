@@ -12,7 +12,7 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[3, 4])
 def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_group=1, sm_scale=None, block_I=64,
-                   threads=256, dtype="bfloat16"):
+                   threads=None, dtype="bfloat16"):
     assert topk % block_I == 0
     if sm_scale is None:
         sm_scale = (1.0 / (dim + tail_dim))**0.5
@@ -24,6 +24,8 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
     assert H % H_blk == 0 or H < 16
     n_hblk = max(1, H // H_blk)
     valid_h = min(H, H_blk)
+    if threads is None:
+        threads = 64 * (H_blk // 16)  # FullRow: 16 head rows per wave, P stays in registers
     D, DT = dim, tail_dim
     NI = topk // block_I
     past = seq_len_kv - seq_len
