@@ -238,13 +238,13 @@ class Indexer(nn.Module):
         for bi in range(b):
             ks_ = torch.zeros(s, dtype=torch.int32, device=x.device)
             ke_ = torch.arange(start_pos + 1, end + 1, dtype=torch.int32, device=x.device)
-            logits = dsa.mqa_attn_return_logits(s, end, self.h, self.d)(
+            logits = dsa.for_target("mqa_attn_return_logits", _target(x), s, end, self.h, self.d)(
                 q8[bi].reshape(s * self.h, self.d).contiguous(), self.k_cache[bi, :end].contiguous(),
                 self.k_scale[bi, :end].contiguous(), w[bi].contiguous().float(), ks_, ke_)
             padded = torch.full((s, n_pad), float("-inf"), device=x.device)
             padded[:, :end] = logits
             # rows with fewer than topk_pad visible keys pick -inf slots: mark them invalid
-            idx = dsa.topk_selector(s, n_pad, topk_pad)(padded)
+            idx = dsa.for_target("topk_selector", _target(x), s, n_pad, topk_pad)(padded)
             val = torch.gather(padded, 1, idx.long())
             idx = torch.where(torch.isfinite(val), idx, torch.full_like(idx, end))
             idx_all.append(idx)
@@ -294,11 +294,15 @@ class MLA(nn.Module):
         qf = torch.cat([q_lat, q_pe], -1).contiguous()                          # [b, s, h, 576]
         kvf = torch.cat([self.kv_cache[:b, :end], self.pe_cache[:b, :end]], -1).unsqueeze(2).contiguous()
         idx = self.indexer(x, qr, start_pos, freqs).unsqueeze(2).contiguous()    # [b, s, 1, topk]
-        kern = dsa.sparse_mla_fwd(b, s, end, self.n_local_heads, self.kv_lora, self.rope, idx.shape[-1], 1,
-                                  self.softmax_scale, 64, None, _tdt(x.dtype))
+        kern = dsa.for_target("sparse_mla_fwd", _target(x), b, s, end, self.n_local_heads, self.kv_lora, self.rope,
+                              idx.shape[-1], 1, self.softmax_scale, 64, None, _tdt(x.dtype))
         o_lat, _ = kern(qf, kvf, idx)                                             # [b, s, h, 512]
         o = torch.einsum("bshc,hdc->bshd", o_lat.float(), wkv_b[:, -self.vdim:].float()).to(x.dtype)
         return self.wo(o.reshape(b, s, -1))
+
+
+def _target(x: torch.Tensor) -> str:
+    return "cpu" if x.device.type == "cpu" else "hip"
 
 
 def _tdt(dt):

@@ -4,6 +4,8 @@ Library home of the kernels used by ``tilelang.models.deepseek_v32`` and the exa
 ``examples/deepseek_v32`` (reference: examples/deepseek_v32/{sparse_mla_fwd,fp8_lighting_indexer,
 topk_selector}.py and inference/kernel.py).  Schedules are documented in the example files.
 """
+import functools
+
 import tilelang
 import tilelang.language as T
 
@@ -184,3 +186,11 @@ def topk_selector(M, N, topk, threads=256):
                         Indices[r, slot] = j
 
     return main
+
+
+@functools.lru_cache(maxsize=None)
+def for_target(name: str, target: str, *args):
+    """The kernel ``name`` (one of this module's jit functions) compiled for ``target`` ("hip" /
+    "cpu"): the model runs the same shapes on either device, the jit cache keys on shapes only."""
+    impl = globals()[name]
+    return tilelang.compile(impl.get_tir(*args), out_idx=impl.out_idx, target=target)

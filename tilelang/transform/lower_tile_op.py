@@ -414,6 +414,35 @@ def safe_guard(ctx: LowerCtx, b: Buffer, idx) -> Optional[PrimExpr]:
     return cond
 
 
+def _guard_conds(e, target) -> Optional[List[PrimExpr]]:
+    """Conditions under which ``target`` (a node of ``e``, by identity) is evaluated: the
+    conditions of the selects / short-circuit operators on its path.  None if not found."""
+    from ..ir.expr import Select, UnOp as _Un
+    if e is target:
+        return []
+    if isinstance(e, Select):
+        r = _guard_conds(e.cond, target)
+        if r is not None:
+            return r
+        r = _guard_conds(e.t, target)
+        if r is not None:
+            return [e.cond] + r
+        r = _guard_conds(e.f, target)
+        return None if r is None else [logical_not(e.cond)] + r
+    if isinstance(e, BinOp) and e.op in ("&&", "||"):
+        r = _guard_conds(e.a, target)
+        if r is not None:
+            return r
+        r = _guard_conds(e.b, target)
+        return None if r is None else [e.a if e.op == "&&" else logical_not(e.a)] + r
+    from ..ir.expr import children
+    for c in children(e):
+        r = _guard_conds(c, target)
+        if r is not None:
+            return r
+    return None
+
+
 def vectorize_group(ctx: LowerCtx, stmts: List[S.Stmt], known_div) -> Optional[List[S.Stmt]]:
     """``stmts[i]`` are the per-element copies (i = 0..W-1) of a single-store body.  If the
     stores (and the loads feeding them) are contiguous and aligned, emit vector accesses."""
@@ -466,7 +495,26 @@ def vectorize_group(ctx: LowerCtx, stmts: List[S.Stmt], known_div) -> Optional[L
             if not divisible_by(ld0.indices[0], W, known_div):
                 continue
             tmp = ctx.new_local(f"vtmp{len(ctx.extra_allocs)}", W, ld0.buffer.dtype)
-            pre.append(L.VecLoadStmt(tmp, 0, ld0.buffer, ld0.indices[0], W))
+            guards = [_guard_conds(vals[i], po[i][j]) for i in range(W)]
+            if any(g is None for g in guards):
+                continue
+            vload = L.VecLoadStmt(tmp, 0, ld0.buffer, ld0.indices[0], W)
+            if any(guards):
+                # the element loads sit under bounds guards (selects): the vector load may only
+                # run when every lane's guard holds, otherwise fall back to guarded scalar loads
+                pred = None
+                for g in guards:
+                    for c in g:
+                        pred = c if pred is None else logical_and(pred, c)
+                slow = []
+                for i in range(W):
+                    st = S.StoreStmt(tmp, [IntImm(i)], po[i][j])
+                    gc = None
+                    for c in guards[i]:
+                        gc = c if gc is None else logical_and(gc, c)
+                    slow.append(st if gc is None else S.IfStmt(gc, st))
+                vload = S.IfStmt(pred, vload, S.SeqStmt(slow))
+            pre.append(vload)
             for i in range(W):
                 repl[i][id(po[i][j])] = BufferLoad(tmp, [IntImm(i)])
         if pre:
