@@ -249,3 +249,38 @@ def test_blocksparse_gemm():
     mask = torch.rand(4, 4, 8) > 0.5
     torch.testing.assert_close(k(a, b, mask).float(), m.ref_program(a, b, mask, 64, 64, 32).float(), rtol=1e-2,
                                atol=2e-2)
+
+
+def _gather_rows_kernel(N, D, R, NT, target):
+    import tilelang
+    import tilelang.language as T
+
+    @T.prim_func
+    def k(X: T.Tensor((2, N, 1, D), "bfloat16"), I: T.Tensor((NT * R, ), "int32"),
+          Y: T.Tensor((2, NT * R, D), "bfloat16")):
+        with T.Kernel(2, threads=256) as b:
+            S = T.alloc_shared((R, D), "bfloat16")
+            for t in T.Pipelined(NT, num_stages=2):
+                T.gather_rows(X[b, :, 0, 0:D], I[t * R:(t + 1) * R], S)
+                T.copy(S, Y[b, t * R, 0])
+
+    return tilelang.compile(k, out_idx=[2], target=target)
+
+
+def _gather_rows_check(dev, target):
+    N, D, R, NT = 300, 256, 64, 4
+    k = _gather_rows_kernel(N, D, R, NT, target)
+    x = torch.randn(2, N, 1, D).bfloat16().to(dev)
+    i = torch.randint(-5, N + 5, (NT * R, ), dtype=torch.int32, generator=torch.Generator().manual_seed(0)).to(dev)
+    y = k(x, i)
+    ok = (i >= 0) & (i < N)
+    ref = torch.where(ok[None, :, None], x[:, i.clamp(0, N - 1).long(), 0], torch.zeros((), dtype=x.dtype, device=dev))
+    assert torch.equal(y, ref)
+    return k
+
+
+def test_gather_rows_cpu():
+    _gather_rows_check("cpu", "cpu")
+    # the HIP lowering is a lane-addressed buffer LDS-DMA inside the pipeline
+    src = _gather_rows_kernel(300, 256, 64, 4, "hip").get_kernel_source()
+    assert "tl::buffer_lds16" in src and "4294967280u" in src

@@ -236,3 +236,8 @@ def test_gemm_persistent_streamk_blocksparse():
     mask = torch.rand(8, 6, 16, device="cuda") > 0.5
     out = bs.blocksparse_matmul(1024, 768, 512)(a, b, mask)
     torch.testing.assert_close(out.float(), bs.ref_program(a, b, mask, 128, 128, 32).float(), rtol=1e-2, atol=1e-1)
+
+
+def test_gather_rows_gpu():
+    from test_examples_cpu import _gather_rows_check
+    _gather_rows_check("cuda", "hip")

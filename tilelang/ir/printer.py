@@ -219,6 +219,9 @@ class Printer:
             return f"T.comm.barrier({op.group!r})"
         if isinstance(op, O.CommFenceOp):
             return "T.comm.fence()"
+        if isinstance(op, O.GatherRowsOp):
+            return (f"T.gather_rows({self.region(op.src)}, {self.region(op.idx)}, {self.region(op.dst)}, "
+                    f"row_dim={op.row_dim})")
         if isinstance(op, O.Im2ColOp):
             return f"T.c2d_im2col({self.region(op.img)}, {self.region(op.col)})"
         return f"T.{k}(...)"

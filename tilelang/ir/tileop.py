@@ -48,6 +48,28 @@ class CopyOp(TileOp):
         return [self.dst]
 
 
+class GatherRowsOp(TileOp):
+    """``T.gather_rows(src, indices, dst)``: ``dst[r, :] = src[..., indices[r], ..., c0:c0+C]``;
+    rows whose index falls outside ``[0, src.shape[row_dim])`` read zeros.  Data-dependent row
+    gathers (sparse attention over selected KV rows, MoE token gathers) on MI355X map onto
+    lane-addressed buffer LDS-DMA, so inside ``T.Pipelined`` they are asynchronous producers
+    like a plain ``T.copy`` (no reference counterpart; the reference writes such gathers as
+    SIMT ``T.Parallel`` loops)."""
+    kind = "gather_rows"
+
+    def __init__(self, src: BufferRegion, idx: BufferRegion, dst: BufferRegion, row_dim: int):
+        self.src, self.idx, self.dst, self.row_dim = src, idx, dst, row_dim
+
+    def regions(self):
+        return [self.src, self.idx, self.dst]
+
+    def reads(self):
+        return [self.src, self.idx]
+
+    def writes(self):
+        return [self.dst]
+
+
 class Im2ColOp(TileOp):
     """``T.c2d_im2col`` (reference ``src/op/copy.cc:1878``)."""
     kind = "im2col"

@@ -48,6 +48,23 @@ def copy(src, dst, coalesced_width: Optional[int] = None, disable_tma: bool = Fa
     return _emit(O.CopyOp(s, d, coalesced_width, disable_tma, eviction_policy))
 
 
+def gather_rows(src, indices, dst, row_dim: Optional[int] = None):
+    """Row gather into a shared tile: ``dst[r, :] = src[..., indices[r], ..., cols]``.
+
+    ``src`` is a global tensor region whose ``row_dim`` is the gathered dimension (its region
+    start/extent are ignored; write ``:``) and whose last non-unit dim gives the columns;
+    ``indices`` is a 1-D region (global or shared int32) with one index per tile row.  Indices
+    outside ``[0, src.shape[row_dim])`` yield zero rows.  Inside ``T.Pipelined`` it is issued
+    asynchronously (buffer LDS-DMA with per-lane row addresses)."""
+    s, i, d = to_region(src), to_region(indices), to_region(dst)
+    if row_dim is None:
+        nonunit = [k for k, e in enumerate(s.extents) if as_int(e) != 1]
+        if len(nonunit) != 2:
+            raise ValueError("T.gather_rows: give row_dim (source region needs one row and one column dim)")
+        row_dim = nonunit[0]
+    return _emit(O.GatherRowsOp(s, i, d, int(row_dim)))
+
+
 def c2d_im2col(img, col, nhw_step, c_step, kernel, stride, dilation, pad, eviction_policy=None):
     return _emit(O.Im2ColOp(to_region(img), to_region(col), convert(nhw_step), convert(c_step), kernel, stride,
                             dilation, pad))

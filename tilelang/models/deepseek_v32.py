@@ -238,7 +238,7 @@ class Indexer(nn.Module):
         for bi in range(b):
             ks_ = torch.zeros(s, dtype=torch.int32, device=x.device)
             ke_ = torch.arange(start_pos + 1, end + 1, dtype=torch.int32, device=x.device)
-            logits = dsa.for_target("mqa_attn_return_logits", _target(x), s, end, self.h, self.d)(
+            logits = dsa.for_target("mqa_attn_return_logits", _target(x), s, None, self.h, self.d)(
                 q8[bi].reshape(s * self.h, self.d).contiguous(), self.k_cache[bi, :end].contiguous(),
                 self.k_scale[bi, :end].contiguous(), w[bi].contiguous().float(), ks_, ke_)
             padded = torch.full((s, n_pad), float("-inf"), device=x.device)
@@ -294,7 +294,7 @@ class MLA(nn.Module):
         qf = torch.cat([q_lat, q_pe], -1).contiguous()                          # [b, s, h, 576]
         kvf = torch.cat([self.kv_cache[:b, :end], self.pe_cache[:b, :end]], -1).unsqueeze(2).contiguous()
         idx = self.indexer(x, qr, start_pos, freqs).unsqueeze(2).contiguous()    # [b, s, 1, topk]
-        kern = dsa.for_target("sparse_mla_fwd", _target(x), b, s, end, self.n_local_heads, self.kv_lora, self.rope,
+        kern = dsa.for_target("sparse_mla_fwd", _target(x), b, s, None, self.n_local_heads, self.kv_lora, self.rope,
                               idx.shape[-1], 1, self.softmax_scale, 64, None, _tdt(x.dtype))
         o_lat, _ = kern(qf, kvf, idx)                                             # [b, s, h, 512]
         o = torch.einsum("bshc,hdc->bshd", o_lat.float(), wkv_b[:, -self.vdim:].float()).to(x.dtype)

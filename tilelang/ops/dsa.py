@@ -14,7 +14,14 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[3, 4])
 def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_group=1, sm_scale=None, block_I=64,
-                   threads=None, dtype="bfloat16"):
+                   threads=None, dtype="bfloat16", num_stages=2, block_H=None):
+    """Sparse MLA forward over the ``topk`` selected latent rows of every query token.
+
+    Schedule (MI355X): one block per (token, 64-head slice); Q stays in registers (it is the
+    MFMA A operand of both score GEMMs), so LDS holds only the gathered KV rows, double
+    buffered: ``T.gather_rows`` becomes a lane-addressed buffer LDS-DMA issued one tile ahead
+    of the MFMA work (``T.Pipelined``), i.e. the gather latency hides behind the GEMMs.
+    Each wave owns 16 head rows (FullRow), so P = softmax(S) never leaves registers."""
     assert topk % block_I == 0
     if sm_scale is None:
         sm_scale = (1.0 / (dim + tail_dim))**0.5
@@ -22,7 +29,7 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
     accum_dtype = "float"
     G = kv_group
     H = heads // G
-    H_blk = min(64, max(16, H))
+    H_blk = block_H or min(64, max(16, H))
     assert H % H_blk == 0 or H < 16
     n_hblk = max(1, H // H_blk)
     valid_h = min(H, H_blk)
@@ -30,6 +37,8 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
         threads = 64 * (H_blk // 16)  # FullRow: 16 head rows per wave, P stays in registers
     D, DT = dim, tail_dim
     NI = topk // block_I
+    if seq_len_kv is None:  # decode: one kernel for every cache length
+        seq_len_kv = T.dynamic("seq_len_kv")
     past = seq_len_kv - seq_len
 
     @T.prim_func
@@ -40,11 +49,10 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
             b = bz // G
             g = bz % G
             h0 = g * H + by * H_blk
-            Q_shared = T.alloc_shared([H_blk, D], dtype)
-            Qt_shared = T.alloc_shared([H_blk, DT], dtype)
+            Q_frag = T.alloc_fragment([H_blk, D], dtype)
+            Qt_frag = T.alloc_fragment([H_blk, DT], dtype)
             KV_shared = T.alloc_shared([block_I, D], dtype)
             Kt_shared = T.alloc_shared([block_I, DT], dtype)
-            valid = T.alloc_shared([block_I], "int32")
             acc_s = T.alloc_fragment([H_blk, block_I], accum_dtype)
             acc_s_cast = T.alloc_fragment([H_blk, block_I], dtype)
             acc_o = T.alloc_fragment([H_blk, D], accum_dtype)
@@ -55,28 +63,22 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
             l_sum = T.alloc_fragment([H_blk], accum_dtype)
             r_sum = T.alloc_fragment([H_blk], accum_dtype)
 
-            T.clear(Q_shared)
-            T.clear(Qt_shared)
-            T.copy(Q[b, bx, h0:h0 + valid_h, 0:D], Q_shared[0:valid_h, :])
-            T.copy(Q[b, bx, h0:h0 + valid_h, D:D + DT], Qt_shared[0:valid_h, :])
+            T.clear(Q_frag)
+            T.clear(Qt_frag)
+            T.copy(Q[b, bx, h0:h0 + valid_h, 0:D], Q_frag[0:valid_h, :])
+            T.copy(Q[b, bx, h0:h0 + valid_h, D:D + DT], Qt_frag[0:valid_h, :])
             T.fill(acc_o, 0)
             T.fill(l_sum, 0)
             T.fill(m_cur, -(2.0**30))
-            for i in T.serial(NI):
-                # gather the selected latent rows (masked rows read row 0 and are discarded)
-                for r in T.Parallel(block_I):
-                    idx = Indices[b, bx, g, i * block_I + r]
-                    valid[r] = T.if_then_else((idx <= bx + past) & (idx >= 0), 1, 0)
-                for r, d in T.Parallel(block_I, D):
-                    idx = Indices[b, bx, g, i * block_I + r]
-                    KV_shared[r, d] = KV[b, T.if_then_else((idx <= bx + past) & (idx >= 0), idx, 0), g, d]
-                for r, d in T.Parallel(block_I, DT):
-                    idx = Indices[b, bx, g, i * block_I + r]
-                    Kt_shared[r, d] = KV[b, T.if_then_else((idx <= bx + past) & (idx >= 0), idx, 0), g, D + d]
+            for i in T.Pipelined(NI, num_stages=num_stages):
+                # selected latent rows; indices outside the cache read zeros, causal ones are masked
+                T.gather_rows(KV[b, :, g, 0:D], Indices[b, bx, g, i * block_I:(i + 1) * block_I], KV_shared)
+                T.gather_rows(KV[b, :, g, D:D + DT], Indices[b, bx, g, i * block_I:(i + 1) * block_I], Kt_shared)
                 for h, r in T.Parallel(H_blk, block_I):
-                    acc_s[h, r] = T.if_then_else(valid[r] == 1, 0, -T.infinity(accum_dtype))
-                T.gemm(Q_shared, KV_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                T.gemm(Qt_shared, Kt_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                    idx = Indices[b, bx, g, i * block_I + r]
+                    acc_s[h, r] = T.if_then_else((idx <= bx + past) & (idx >= 0), 0, -T.infinity(accum_dtype))
+                T.gemm(Q_frag, KV_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.gemm(Qt_frag, Kt_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 T.copy(m_cur, m_prev)
                 T.reduce_max(acc_s, m_cur, dim=1, clear=False)
                 for h in T.Parallel(H_blk):
@@ -105,6 +107,8 @@ def mqa_attn_return_logits(seq_len, seq_len_kv, heads, index_dim, block_N=64, th
     if block_Q is None:
         block_Q = max(1, 128 // heads)
     QH = block_Q * heads
+    if seq_len_kv is None:
+        seq_len_kv = T.dynamic("seq_len_kv")
     dtype = "float8_e4m3fn"
     accum_dtype = "float"
 

@@ -26,7 +26,7 @@ from ..ir import lowered as L
 from ..ir import dtypes as _dt
 from ..ir.buffer import Buffer, BufferRegion
 from ..ir.expr import (BinOp, BufferLoad, Call, IntImm, PrimExpr, Var, as_int, binop, call, cast, compile_py, const,
-                       convert, divisible_by, evaluate, free_vars, logical_and, select, substitute, transform,
+                       convert, divisible_by, evaluate, free_vars, logical_and, logical_not, select, substitute, transform,
                        post_order, loads_of, modular)
 from ..layout.fragment import Digit, Fragment, make_linear_fragment
 from ..layout.layout import Layout, LinearLayout, SwizzleLayout
@@ -1162,6 +1162,8 @@ class TileOpLowerer(Mutator):
     def lower_AsyncCopyOp(self, op: AsyncCopyOp):
         ctx = self.ctx
         p = op.plan
+        if p.get("gather"):
+            return self.lower_async_gather(op)
         src, dst = op.src, op.dst
         NB = dst.buffer
         lay = NB.layout
@@ -1199,6 +1201,74 @@ class TileOpLowerer(Mutator):
             out.append(L.CallStmt("tl::glds16", [L.BufferPtr(ctx.flat_of(src.buffer), gidx),
                                                  L.BufferPtr(ctx.flat_of(NB), lds_off)]))
         return S.SeqStmt(out)
+
+    def lower_async_gather(self, op: AsyncCopyOp):
+        """Row gather as buffer LDS-DMA: each lane fetches the 16-byte chunk that lands at its
+        lane-linear LDS slot, from the row named by the index tensor.  The resource is based at
+        row 0 of the gathered dim (``num_records`` = whole dim), and invalid indices get an
+        offset past ``num_records`` so the hardware writes zeros."""
+        ctx = self.ctx
+        p = op.plan
+        src, dst = op.src, op.dst
+        NB = dst.buffer
+        lay = NB.layout
+        epc = 16 // p["eb"]
+        nw, cpr, rdim = p["nwaves"], p["cpr"], p["rdim"]
+        wave, lane = ctx.wave_expr(), ctx.lane_expr()
+        stage = self.expr(dst.mins[0])
+        base_off = ctx.flat_index(NB, [stage, 0, 0])
+        smins = [self.expr(m) for m in src.mins]
+        smins[rdim] = IntImm(0)
+        sb = src.buffer
+        base = ctx.flat_index(sb, smins)
+        stride_r = self.expr(convert(sb.get_strides()[rdim]))
+        nrows = self.expr(convert(sb.shape[rdim]))
+        rsrc = call("extern", ["tl::make_rsrc", L.BufferPtr(ctx.flat_of(sb), base),
+                               cast(binop("*", binop("*", nrows, stride_r), p["eb"]), _dt.uint32)], _dt.handle)
+        out = []
+        for i in range(p["instrs"]):
+            chunk_base = binop("*", binop("+", i * nw, wave), 64)
+            if cpr % 64 == 0:
+                row = binop("//", chunk_base, cpr)  # one row per wave instruction: uniform index
+                pch = binop("+", binop("%", chunk_base, cpr), lane)
+            else:
+                row = binop("+", binop("//", chunk_base, cpr), binop("//", lane, cpr))
+                pch = binop("%", lane, cpr)
+            if isinstance(lay, SwizzleLayout) and lay.bits:
+                lch = binop("^", pch, lay._xor_term(row))
+            else:
+                lch = pch
+            iv = self.expr(_gather_index(op.idx, row))
+            ok = logical_and(binop(">=", iv, 0), binop("<", iv, nrows))
+            off = binop("*", binop("+", binop("*", iv, stride_r), binop("*", lch, epc)), p["eb"])
+            voff = select(ok, cast(off, _dt.uint32), IntImm(0xFFFFFFF0, _dt.uint32))
+            lds_off = binop("+", base_off, binop("*", chunk_base, epc))
+            out.append(L.CallStmt("tl::buffer_lds16", [rsrc, voff, L.BufferPtr(ctx.flat_of(NB), lds_off)]))
+        return S.SeqStmt(out)
+
+    def lower_GatherRowsOp(self, op: O.GatherRowsOp):
+        """Synchronous row gather (outside pipelined loops / CPU): a SIMT copy nest."""
+        src, dst, rdim = op.src, op.dst, op.row_dim
+        dd = [d for d, e in enumerate(dst.extents) if as_int(e) != 1]
+        if len(dd) != 2:
+            raise LoweringError("T.gather_rows destination must be a 2-D tile")
+        cols = [d for d, e in enumerate(src.extents) if d != rdim and as_int(e) != 1]
+        if len(cols) != 1:
+            raise LoweringError("T.gather_rows source needs exactly one column dim besides row_dim")
+        cdim = cols[0]
+        r, c = Var("gr"), Var("gc")
+        iv = _gather_index(op.idx, r)
+        ok = logical_and(binop(">=", iv, 0), binop("<", iv, src.buffer.shape[rdim]))
+        sidx = list(src.mins)
+        sidx[rdim] = select(ok, iv, 0)
+        sidx[cdim] = binop("+", sidx[cdim], c)
+        didx = list(dst.mins)
+        didx[dd[0]] = binop("+", didx[dd[0]], r)
+        didx[dd[1]] = binop("+", didx[dd[1]], c)
+        val = select(ok, cast(BufferLoad(src.buffer, sidx), dst.buffer.dtype), const(0, dst.buffer.dtype))
+        body = S.StoreStmt(dst.buffer, didx, val)
+        nest = S.ForStmt(r, 0, dst.extents[dd[0]], "parallel", S.ForStmt(c, 0, dst.extents[dd[1]], "parallel", body))
+        return self.lower_nest(nest)
 
     def lower_StagedCopyOp(self, op: StagedCopyOp):
         """Register-staged copy: phase 'load' fills a staging array, 'store' writes it to LDS."""
@@ -1354,6 +1424,15 @@ def _squeeze_pairs(src: BufferRegion, dst: BufferRegion):
         if a is not None and b is not None and a != b:
             raise LoweringError(f"T.copy: extent mismatch {src} -> {dst}")
     return sd, dd
+
+
+def _gather_index(idx: BufferRegion, row) -> PrimExpr:
+    """``indices[row]`` for a 1-D index region (its single non-unit dim, else the last dim)."""
+    nonunit = [d for d, e in enumerate(idx.extents) if as_int(e) != 1]
+    d = nonunit[0] if nonunit else len(idx.extents) - 1
+    ii = list(idx.mins)
+    ii[d] = binop("+", ii[d], row)
+    return BufferLoad(idx.buffer, ii)
 
 
 def _copy_nest(src: BufferRegion, dst: BufferRegion, coalesced_width, atomic=None) -> S.ForStmt:

@@ -36,14 +36,14 @@ class AsyncCopyOp(O.TileOp):
     """Global->LDS DMA copy (lowered to ``tl::glds16``)."""
     kind = "async_copy"
 
-    def __init__(self, src: BufferRegion, dst: BufferRegion, plan: dict):
-        self.src, self.dst, self.plan = src, dst, plan
+    def __init__(self, src: BufferRegion, dst: BufferRegion, plan: dict, idx: Optional[BufferRegion] = None):
+        self.src, self.dst, self.plan, self.idx = src, dst, plan, idx  # idx: row indices of a gather
 
     def regions(self):
-        return [self.src, self.dst]
+        return [self.src, self.dst] + ([self.idx] if self.idx is not None else [])
 
     def reads(self):
-        return [self.src]
+        return [self.src] + ([self.idx] if self.idx is not None else [])
 
     def writes(self):
         return [self.dst]
@@ -168,6 +168,58 @@ def glds_plan(op: O.CopyOp, num_threads: int, ranges, target) -> Optional[dict]:
                 oob_bytes=nbytes)
 
 
+def gather_plan(op: O.GatherRowsOp, num_threads: int, target) -> Optional[dict]:
+    """LDS-DMA geometry of a row gather: every lane fetches one 16-byte chunk of the row its
+    chunk belongs to, addressed through a buffer resource (out-of-range rows -> zeros)."""
+    if target is not None and getattr(target, "kind", "hip") != "hip":
+        return None
+    if getattr(target, "disable_glds", False):
+        return None
+    src, dst = op.src, op.dst
+    sb, db = src.buffer, dst.buffer
+    if sb.scope != "global" or db.scope != "shared" or sb.dtype != db.dtype:
+        return None
+    eb = sb.dtype.bytes
+    dext, dshape = dst.static_extents(), db.static_shape()
+    if dext is None or dshape is None or dext != dshape or len(dshape) != 2:
+        return None
+    R, C = dshape
+    nw = num_threads // 64
+    if (C * eb) % 16 or (R * C * eb) % (1024 * nw):
+        return None
+    lay = db.layout
+    if lay is not None and not isinstance(lay, (SwizzleLayout, LinearLayout)):
+        return None
+    cpr = C * eb // 16
+    if cpr % 64 and 64 % cpr:
+        return None
+    rdim = op.row_dim
+    sext = src.static_extents()
+    if sext is None:
+        return None
+    cols = [d for d, e in enumerate(sext) if d != rdim and e != 1]
+    if len(cols) != 1 or sext[cols[0]] != C:
+        return None
+    cdim = cols[0]
+    strides = sb.get_strides()
+    epc = 16 // eb
+    if as_int(strides[cdim]) != 1 or not divisible_by(convert(strides[rdim]), epc) or \
+            not divisible_by(src.region[cdim][0], epc):
+        return None
+    iext = [as_int(e) for e in op.idx.extents]
+    if None in iext or [e for e in iext if e != 1] not in ([R], []) or _prod_i(iext) != R:
+        return None
+    return dict(R=R, C=C, eb=eb, rdim=rdim, cdim=cdim, instrs=R * C * eb // 16 // 64 // nw, nwaves=nw, cpr=cpr,
+                gather=True)
+
+
+def _prod_i(xs):
+    r = 1
+    for x in xs:
+        r *= x
+    return r
+
+
 class _Ranges:
 
     def __init__(self):
@@ -224,6 +276,9 @@ class PipelineInjector(Mutator):
             elif isinstance(st, S.TileOpStmt) and isinstance(st.op, O.CopyOp) and \
                     st.op.src.buffer.scope == "global" and st.op.dst.buffer.scope == "shared":
                 producers.append(st)
+            elif isinstance(st, S.TileOpStmt) and isinstance(st.op, O.GatherRowsOp) and \
+                    gather_plan(st.op, self.T, self.target) is not None:
+                producers.append(st)  # gathers have no register-staged form: async or in-loop
             else:
                 for w in S.walk(st):
                     if isinstance(w, S.TileOpStmt):
@@ -286,6 +341,9 @@ class PipelineInjector(Mutator):
                 rng[k] = (lo[0], max(lo[0], hi[1] - 1))
         asyncs, staged = [], []
         for p, src in prods:
+            if isinstance(p.op, O.GatherRowsOp):
+                asyncs.append((p, src, gather_plan(p.op, self.T, self.target)))
+                continue
             plan = glds_plan(O.CopyOp(src, p.op.dst), self.T, rng, self.target)
             if plan is not None:
                 asyncs.append((p, src, plan))
@@ -299,7 +357,10 @@ class PipelineInjector(Mutator):
                 srcj = _subst_region(src, {k: binop("+", loop.min, j)})
                 NB = newbufs[p.op.dst.buffer]
                 dst = BufferRegion(NB, [(stg, 1)] + list(p.op.dst.region))
-                out.append(S.TileOpStmt(AsyncCopyOp(srcj, dst, plan)))
+                idxj = None
+                if isinstance(p.op, O.GatherRowsOp):
+                    idxj = _subst_region(_subst_region(p.op.idx, lets), {k: binop("+", loop.min, j)})
+                out.append(S.TileOpStmt(AsyncCopyOp(srcj, dst, plan, idxj)))
             return out
 
         keys = {}
