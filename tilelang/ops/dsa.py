@@ -14,7 +14,7 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[3, 4])
 def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_group=1, sm_scale=None, block_I=64,
-                   threads=None, dtype="bfloat16", num_stages=2, block_H=None):
+                   threads=None, dtype="bfloat16", num_stages=2, block_H=None, xcd_pair=True):
     """Sparse MLA forward over the ``topk`` selected latent rows of every query token.
 
     Schedule (MI355X): one block per (token, 64-head slice); Q stays in registers (it is the
@@ -40,12 +40,22 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
     if seq_len_kv is None:  # decode: one kernel for every cache length
         seq_len_kv = T.dynamic("seq_len_kv")
     past = seq_len_kv - seq_len
+    pair_xcd = xcd_pair and n_hblk > 1 and seq_len % 8 == 0
 
     @T.prim_func
     def main(Q: T.Tensor([batch, seq_len, heads, D + DT], dtype), KV: T.Tensor([batch, seq_len_kv, G, D + DT], dtype),
              Indices: T.Tensor([batch, seq_len, G, topk], "int32"), Output: T.Tensor([batch, seq_len, heads, D], dtype),
              Lse: T.Tensor([batch, seq_len, heads], accum_dtype)):
-        with T.Kernel(seq_len, n_hblk, batch * G, threads=threads) as (bx, by, bz):
+        with T.Kernel(seq_len * n_hblk, batch * G, threads=threads) as (pid, bz):
+            if pair_xcd:
+                # the head slices of one token run back to back on one XCD (block ids 8 apart:
+                # workgroups go round-robin over the 8 XCDs), so the second slice's row gathers
+                # hit the L2 the first one filled
+                bx = (pid // (8 * n_hblk)) * 8 + pid % 8
+                by = (pid // 8) % n_hblk
+            else:
+                bx = pid % seq_len
+                by = pid // seq_len
             b = bz // G
             g = bz % G
             h0 = g * H + by * H_blk
@@ -53,6 +63,7 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
             Qt_frag = T.alloc_fragment([H_blk, DT], dtype)
             KV_shared = T.alloc_shared([block_I, D], dtype)
             Kt_shared = T.alloc_shared([block_I, DT], dtype)
+            idx_s = T.alloc_shared([block_I], "int32")
             acc_s = T.alloc_fragment([H_blk, block_I], accum_dtype)
             acc_s_cast = T.alloc_fragment([H_blk, block_I], dtype)
             acc_o = T.alloc_fragment([H_blk, D], accum_dtype)
@@ -74,9 +85,10 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
                 # selected latent rows; indices outside the cache read zeros, causal ones are masked
                 T.gather_rows(KV[b, :, g, 0:D], Indices[b, bx, g, i * block_I:(i + 1) * block_I], KV_shared)
                 T.gather_rows(KV[b, :, g, D:D + DT], Indices[b, bx, g, i * block_I:(i + 1) * block_I], Kt_shared)
+                T.copy(Indices[b, bx, g, i * block_I:(i + 1) * block_I], idx_s)  # prefetched a step ahead
                 for h, r in T.Parallel(H_blk, block_I):
-                    idx = Indices[b, bx, g, i * block_I + r]
-                    acc_s[h, r] = T.if_then_else((idx <= bx + past) & (idx >= 0), 0, -T.infinity(accum_dtype))
+                    acc_s[h, r] = T.if_then_else((idx_s[r] <= bx + past) & (idx_s[r] >= 0), 0,
+                                                 -T.infinity(accum_dtype))
                 T.gemm(Q_frag, KV_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 T.gemm(Qt_frag, Kt_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 T.copy(m_cur, m_prev)

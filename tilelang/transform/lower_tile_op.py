@@ -31,7 +31,7 @@ from ..ir.expr import (BinOp, BufferLoad, Call, IntImm, PrimExpr, Var, as_int, b
 from ..layout.fragment import Digit, Fragment, make_linear_fragment
 from ..layout.layout import Layout, LinearLayout, SwizzleLayout
 from .layout_inference import ParallelNest, collect_nests, lift_layout, _index_map
-from .pipeline import AsyncCopyOp, StagedCopyOp
+from .pipeline import AsyncCopyOp, GatherIndexOp, StagedCopyOp
 from .utils import Mutator, Substituter, bound, flatten_seq
 from . import gemm_lower
 
@@ -1226,24 +1226,38 @@ class TileOpLowerer(Mutator):
         rsrc = call("extern", ["tl::make_rsrc", L.BufferPtr(ctx.flat_of(sb), base),
                                cast(binop("*", binop("*", nrows, stride_r), p["eb"]), _dt.uint32)], _dt.handle)
         out = []
+        regs = ctx.staging.get(("gidx", op.key)) if op.key is not None else None
+        if op.key is not None and regs is None:
+            raise LoweringError("gather DMA issued before its index prefetch")
         for i in range(p["instrs"]):
-            chunk_base = binop("*", binop("+", i * nw, wave), 64)
-            if cpr % 64 == 0:
-                row = binop("//", chunk_base, cpr)  # one row per wave instruction: uniform index
-                pch = binop("+", binop("%", chunk_base, cpr), lane)
-            else:
-                row = binop("+", binop("//", chunk_base, cpr), binop("//", lane, cpr))
-                pch = binop("%", lane, cpr)
+            chunk_base, row, pch = _gather_geom(i, nw, cpr, wave, lane)
             if isinstance(lay, SwizzleLayout) and lay.bits:
                 lch = binop("^", pch, lay._xor_term(row))
             else:
                 lch = pch
-            iv = self.expr(_gather_index(op.idx, row))
+            if regs is not None:
+                iv = BufferLoad(regs, [IntImm(i)])
+            else:
+                iv = self.expr(_gather_index(op.idx, row))
             ok = logical_and(binop(">=", iv, 0), binop("<", iv, nrows))
             off = binop("*", binop("+", binop("*", iv, stride_r), binop("*", lch, epc)), p["eb"])
             voff = select(ok, cast(off, _dt.uint32), IntImm(0xFFFFFFF0, _dt.uint32))
             lds_off = binop("+", base_off, binop("*", chunk_base, epc))
             out.append(L.CallStmt("tl::buffer_lds16", [rsrc, voff, L.BufferPtr(ctx.flat_of(NB), lds_off)]))
+        return S.SeqStmt(out)
+
+    def lower_GatherIndexOp(self, op: GatherIndexOp):
+        ctx = self.ctx
+        p = op.plan
+        regs = ctx.staging.get(("gidx", op.key))
+        if regs is None:
+            regs = ctx.new_local(f"gidx{op.key}", p["instrs"], _dt.int32)
+            ctx.staging[("gidx", op.key)] = regs
+        wave, lane = ctx.wave_expr(), ctx.lane_expr()
+        out = []
+        for i in range(p["instrs"]):
+            _, row, _ = _gather_geom(i, p["nwaves"], p["cpr"], wave, lane)
+            out.append(S.StoreStmt(regs, [IntImm(i)], cast(self.expr(_gather_index(op.idx, row)), _dt.int32)))
         return S.SeqStmt(out)
 
     def lower_GatherRowsOp(self, op: O.GatherRowsOp):
@@ -1424,6 +1438,18 @@ def _squeeze_pairs(src: BufferRegion, dst: BufferRegion):
         if a is not None and b is not None and a != b:
             raise LoweringError(f"T.copy: extent mismatch {src} -> {dst}")
     return sd, dd
+
+
+def _gather_geom(i, nw, cpr, wave, lane):
+    """(chunk base, tile row, physical chunk in the row) of LDS-DMA instruction ``i`` of a gather."""
+    chunk_base = binop("*", binop("+", i * nw, wave), 64)
+    if cpr % 64 == 0:
+        row = binop("//", chunk_base, cpr)  # one row per wave instruction: uniform index
+        pch = binop("+", binop("%", chunk_base, cpr), lane)
+    else:
+        row = binop("+", binop("//", chunk_base, cpr), binop("//", lane, cpr))
+        pch = binop("%", lane, cpr)
+    return chunk_base, row, pch
 
 
 def _gather_index(idx: BufferRegion, row) -> PrimExpr:

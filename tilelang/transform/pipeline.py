@@ -36,8 +36,11 @@ class AsyncCopyOp(O.TileOp):
     """Global->LDS DMA copy (lowered to ``tl::glds16``)."""
     kind = "async_copy"
 
-    def __init__(self, src: BufferRegion, dst: BufferRegion, plan: dict, idx: Optional[BufferRegion] = None):
-        self.src, self.dst, self.plan, self.idx = src, dst, plan, idx  # idx: row indices of a gather
+    def __init__(self, src: BufferRegion, dst: BufferRegion, plan: dict, idx: Optional[BufferRegion] = None,
+                 key: Optional[int] = None):
+        # gathers: ``idx`` = the row indices; ``key`` names the register array they were
+        # prefetched into (GatherIndexOp, one pipeline step earlier), None = load at issue
+        self.src, self.dst, self.plan, self.idx, self.key = src, dst, plan, idx, key
 
     def regions(self):
         return [self.src, self.dst] + ([self.idx] if self.idx is not None else [])
@@ -47,6 +50,22 @@ class AsyncCopyOp(O.TileOp):
 
     def writes(self):
         return [self.dst]
+
+
+class GatherIndexOp(O.TileOp):
+    """Prefetch of a gather's row indices into registers (one per LDS-DMA instruction and lane),
+    issued a step ahead of the DMA that consumes them, so the index load latency never sits
+    between the barrier and the DMA issue."""
+    kind = "gather_index"
+
+    def __init__(self, idx: BufferRegion, plan: dict, key: int):
+        self.idx, self.plan, self.key = idx, plan, key
+
+    def regions(self):
+        return [self.idx]
+
+    def reads(self):
+        return [self.idx]
 
 
 class StagedCopyOp(O.TileOp):
@@ -351,6 +370,20 @@ class PipelineInjector(Mutator):
                 staged.append((p, src))
         L_instr = sum(pl["instrs"] for _, _, pl in asyncs)
 
+        gkeys = {}
+        for p, _, plan in asyncs:
+            if plan.get("gather"):
+                self.key += 1
+                gkeys[id(p)] = self.key
+
+        def gather_idx(j):
+            out = []
+            for p, src, plan in asyncs:
+                if id(p) in gkeys:
+                    idxj = _subst_region(_subst_region(p.op.idx, lets), {k: binop("+", loop.min, j)})
+                    out.append(S.TileOpStmt(GatherIndexOp(idxj, plan, gkeys[id(p)])))
+            return out
+
         def issue_async(j, stg):
             out = []
             for p, src, plan in asyncs:
@@ -360,7 +393,7 @@ class PipelineInjector(Mutator):
                 idxj = None
                 if isinstance(p.op, O.GatherRowsOp):
                     idxj = _subst_region(_subst_region(p.op.idx, lets), {k: binop("+", loop.min, j)})
-                out.append(S.TileOpStmt(AsyncCopyOp(srcj, dst, plan, idxj)))
+                out.append(S.TileOpStmt(AsyncCopyOp(srcj, dst, plan, idxj, gkeys.get(id(p)))))
             return out
 
         keys = {}
@@ -379,6 +412,14 @@ class PipelineInjector(Mutator):
 
         prologue = []
         nv = as_int(n)
+
+        def guarded(j, st):
+            if nv is not None:
+                return S.seq(*st) if j < nv else None
+            return S.IfStmt(binop("<", j, n), S.seq(*st))
+
+        if gkeys:
+            prologue.append(guarded(0, gather_idx(0)))
         for j in range(nstages - 1):
             st = issue_async(j, j)
             if not st:
@@ -386,6 +427,9 @@ class PipelineInjector(Mutator):
             if nv is not None and j >= nv:
                 break
             prologue.append(S.seq(*st) if nv is not None else S.IfStmt(binop("<", j, n), S.seq(*st)))
+            if gkeys:
+                prologue.append(guarded(j + 1, gather_idx(j + 1)))
+        prologue = [x for x in prologue if x is not None]
         if staged:
             st = staged_phase(0, 0, "load") + staged_phase(0, 0, "store")
             prologue.append(S.seq(*st) if nv is not None and nv > 0 else S.IfStmt(binop("<", 0, n), S.seq(*st)))
@@ -404,6 +448,9 @@ class PipelineInjector(Mutator):
         if asyncs:
             j = binop("+", kk, nstages - 1)
             body.append(S.IfStmt(binop("<", j, n), S.seq(*issue_async(j, binop("%", j, nstages)))))
+            if gkeys:
+                j2 = binop("+", kk, nstages)
+                body.append(S.IfStmt(binop("<", j2, n), S.seq(*gather_idx(j2))))
         if staged:
             j1 = binop("+", kk, 1)
             body.append(S.IfStmt(binop("<", j1, n), S.seq(*staged_phase(j1, binop("%", j1, nstages), "load"))))
