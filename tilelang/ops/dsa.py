@@ -14,7 +14,7 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[3, 4])
 def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_group=1, sm_scale=None, block_I=64,
-                   threads=None, dtype="bfloat16", num_stages=2, block_H=None, xcd_pair=True):
+                   threads=None, dtype="bfloat16", num_stages=2, block_H=None, xcd_pair=True, lazy_rescale=True):
     """Sparse MLA forward over the ``topk`` selected latent rows of every query token.
 
     Schedule (MI355X): one block per (token, 64-head slice); Q stays in registers (it is the
@@ -41,6 +41,7 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
         seq_len_kv = T.dynamic("seq_len_kv")
     past = seq_len_kv - seq_len
     pair_xcd = xcd_pair and n_hblk > 1 and seq_len % 8 == 0
+    tau = 8.0 if lazy_rescale else 0.0
 
     @T.prim_func
     def main(Q: T.Tensor([batch, seq_len, heads, D + DT], dtype), KV: T.Tensor([batch, seq_len_kv, G, D + DT], dtype),
@@ -92,16 +93,27 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
                 T.gemm(Q_frag, KV_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 T.gemm(Qt_frag, Kt_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 T.copy(m_cur, m_prev)
-                T.reduce_max(acc_s, m_cur, dim=1, clear=False)
+                T.reduce_max(acc_s, m_prev, dim=1, clear=False)
+                # lazy rescale: a row keeps its running max until a new score exceeds it by
+                # more than 2^8 (P <= 256 stays exact enough in fp32 / bf16), so after the
+                # first tiles the 128-register O accumulator is almost never rescaled
+                rescale = T.alloc_var("int32")
+                rescale = 0
                 for h in T.Parallel(H_blk):
-                    alpha[h] = T.exp2((m_prev[h] - m_cur[h]) * scale)
+                    if (m_prev[h] - m_cur[h]) * scale > tau:
+                        alpha[h] = T.exp2((m_cur[h] - m_prev[h]) * scale)
+                        m_cur[h] = m_prev[h]
+                        rescale = 1
+                    else:
+                        alpha[h] = 1.0
                 for h, r in T.Parallel(H_blk, block_I):
                     acc_s[h, r] = T.exp2(acc_s[h, r] * scale - m_cur[h] * scale)
                 T.reduce_sum(acc_s, r_sum, dim=1)
                 for h in T.Parallel(H_blk):
                     l_sum[h] = l_sum[h] * alpha[h] + r_sum[h]
-                for h, d in T.Parallel(H_blk, D):
-                    acc_o[h, d] *= alpha[h]
+                if rescale != 0:  # per-thread flag: waves whose rows all kept their max skip it
+                    for h, d in T.Parallel(H_blk, D):
+                        acc_o[h, d] *= alpha[h]
                 T.copy(acc_s, acc_s_cast)
                 T.gemm(acc_s_cast, KV_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
             for h, d in T.Parallel(H_blk, D):
