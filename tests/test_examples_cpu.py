@@ -284,3 +284,37 @@ def test_gather_rows_cpu():
     # the HIP lowering is a lane-addressed buffer LDS-DMA inside the pipeline
     src = _gather_rows_kernel(300, 256, 64, 4, "hip").get_kernel_source()
     assert "tl::buffer_lds16" in src and "4294967280u" in src
+
+
+def test_nsa_fwd_cpu():
+    from example_nsa_fwd import nsa_fwd, make_block_indices, ref_program
+    B, SQ, SKV, HQ, H, D, S, BS = 2, 48, 128, 32, 2, 64, 4, 16
+    for bt in (16, 8):
+        k = nsa_fwd.get_tir(B, HQ, SQ, SKV, D, True, None, BS, HQ // H, S, block_T=bt)
+        kc = tilelang.compile(k, out_idx=[-1], target="cpu")
+        q, kk, v = (torch.randn(B, n, h, D).bfloat16() for n, h in ((SQ, HQ), (SKV, H), (SKV, H)))
+        bi = make_block_indices(B, SQ, SKV, H, S, BS)
+        torch.testing.assert_close(kc(q, kk, v, bi).float(), ref_program(q, kk, v, bi, BS).float(), rtol=2e-2,
+                                   atol=2e-2)
+
+
+def test_block_sparse_attn_cpu():
+    from example_block_sparse_attn import blocksparse_attn, compact_mask, random_block_mask, ref_program
+    B, H, S, D = 1, 2, 256, 64
+    for causal in (True, False):
+        f = blocksparse_attn.get_tir(B, H, S, D, causal, block=32, threads=128)
+        kc = tilelang.compile(f, out_idx=[-1], target="cpu")
+        q, k, v = (torch.randn(B, H, S, D).bfloat16() for _ in range(3))
+        mask = random_block_mask(B, H, S // 32, 0.4, causal)
+        idx, cnt = compact_mask(mask)
+        torch.testing.assert_close(kc(q, k, v, idx, cnt).float(), ref_program(q, k, v, mask, 32, causal).float(),
+                                   rtol=2e-2, atol=2e-2)
+
+
+def test_gdn_chunked_matches_recurrence_cpu():
+    from example_gdn import chunk_gated_delta_rule, make_inputs, naive_recurrent
+    q, k, v, g, beta = make_inputs(1, 128, 2, 64, 32)
+    o, hf = chunk_gated_delta_rule(q, k, v, g, beta, C=64, block_DV=16)
+    o_ref, h_ref = naive_recurrent(q, k, v, g, beta)
+    torch.testing.assert_close(o.float(), o_ref, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(hf, h_ref, rtol=2e-2, atol=2e-2)

@@ -241,3 +241,35 @@ def test_gemm_persistent_streamk_blocksparse():
 def test_gather_rows_gpu():
     from test_examples_cpu import _gather_rows_check
     _gather_rows_check("cuda", "hip")
+
+
+def test_nsa_fwd_and_decode_gpu():
+    from example_nsa_fwd import nsa_fwd, make_block_indices, ref_program
+    B, SKV, HQ, H, D, S, BS = 2, 512, 32, 2, 128, 4, 64
+    for SQ in (256, 1):  # prefill and decode (one query at the end of the cache)
+        k = nsa_fwd(B, HQ, SQ, SKV, D, True, None, BS, HQ // H, S)
+        q = torch.randn(B, SQ, HQ, D, device="cuda", dtype=torch.bfloat16)
+        kk = torch.randn(B, SKV, H, D, device="cuda", dtype=torch.bfloat16)
+        v = torch.randn(B, SKV, H, D, device="cuda", dtype=torch.bfloat16)
+        bi = make_block_indices(B, SQ, SKV, H, S, BS, "cuda")
+        torch.testing.assert_close(k(q, kk, v, bi).float().cpu(), ref_program(q, kk, v, bi, BS).float(), rtol=2e-2,
+                                   atol=2e-2)
+
+
+def test_block_sparse_attn_gpu():
+    from example_block_sparse_attn import blocksparse_attn, compact_mask, random_block_mask, ref_program
+    B, H, S, D = 1, 4, 1024, 128
+    k_ = blocksparse_attn(B, H, S, D)
+    q, k, v = (torch.randn(B, H, S, D, device="cuda", dtype=torch.bfloat16) for _ in range(3))
+    mask = random_block_mask(B, H, S // 64, 0.3, True, "cuda")
+    idx, cnt = compact_mask(mask)
+    torch.testing.assert_close(k_(q, k, v, idx, cnt).float(), ref_program(q, k, v, mask).float(), rtol=2e-2, atol=2e-2)
+
+
+def test_gdn_chunked_gpu():
+    from example_gdn import chunk_gated_delta_rule, make_inputs, naive_recurrent
+    q, k, v, g, beta = make_inputs(2, 256, 2, 128, 64, "cuda")
+    o, hf = chunk_gated_delta_rule(q, k, v, g, beta)
+    o_ref, h_ref = naive_recurrent(q, k, v, g, beta)
+    torch.testing.assert_close(o.float().cpu(), o_ref, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(hf.cpu(), h_ref, rtol=3e-2, atol=3e-2)

@@ -170,7 +170,18 @@ def stmt_uses_var(s, var: Var) -> bool:
 
 
 def bound(e, ranges: Dict[Var, tuple]):
-    """Conservative integer interval [lo, hi] of ``e`` (None when unknown)."""
+    """Conservative integer interval [lo, hi] of ``e`` (None when unknown).  Data-dependent
+    values are unknown, but a clamp ``min(max(x, lo), hi)`` of one is still bounded."""
+    r = _bound(e, ranges)
+    if r is None or r[0] == -_INF or r[1] == _INF:
+        return None
+    return (int(r[0]), int(r[1]))
+
+
+_INF = float("inf")
+
+
+def _bound(e, ranges):
     if isinstance(e, int):
         return (e, e)
     if isinstance(e, IntImm):
@@ -178,11 +189,17 @@ def bound(e, ranges: Dict[Var, tuple]):
     if isinstance(e, Var):
         return ranges.get(e)
     if isinstance(e, Cast):
-        return bound(e.value, ranges)
+        return _bound(e.value, ranges)
     if isinstance(e, BinOp):
-        a = bound(e.a, ranges)
-        b = bound(e.b, ranges)
-        if a is None or b is None:
+        a = _bound(e.a, ranges)
+        b = _bound(e.b, ranges)
+        if e.op in ("min", "max"):
+            a = a if a is not None else (-_INF, _INF)
+            b = b if b is not None else (-_INF, _INF)
+            if e.op == "min":
+                return (min(a[0], b[0]), min(a[1], b[1]))
+            return (max(a[0], b[0]), max(a[1], b[1]))
+        if a is None or b is None or _INF in (abs(a[0]), abs(a[1]), abs(b[0]), abs(b[1])):
             return None
         if e.op == "+":
             return (a[0] + b[0], a[1] + b[1])
@@ -197,8 +214,4 @@ def bound(e, ranges: Dict[Var, tuple]):
             if a[0] >= 0:
                 return (0, min(b[0] - 1, a[1]))
             return (0, b[0] - 1)
-        if e.op == "min":
-            return (min(a[0], b[0]), min(a[1], b[1]))
-        if e.op == "max":
-            return (max(a[0], b[0]), max(a[1], b[1]))
     return None
