@@ -115,7 +115,7 @@ def main(B=1, H=32, S=8192, D=128, density=0.25):
     torch.testing.assert_close(o[:, :2].float(), ref.float(), rtol=2e-2, atol=2e-2)
     print("All checks pass.")
     lat = kernel.get_profiler().do_bench(lambda: kernel(q, k, v, idx, cnt))
-    flops = 4 * B * H * D * 64 * 64 * int(cnt.sum())
+    flops = 4 * D * 64 * 64 * int(cnt.sum())  # cnt sums over batch and heads
     print(f"block-sparse attn B{B} H{H} S{S} D{D} density {float(cnt.sum()) / mask.numel():.3f}: {lat:.3f} ms, "
           f"{flops / lat * 1e-9:.1f} TFLOPS (active blocks)")
 

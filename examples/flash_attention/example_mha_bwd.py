@@ -26,13 +26,15 @@ LOG2E = 1.44269504
 
 
 @tilelang.jit(out_idx=[3, 4])
-def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=256, dtype="float16"):
+def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=256, dtype="float16",
+                  groups=1):
     scale = (1.0 / dim)**0.5 * LOG2E
     shape = [batch, seq_len, heads, dim]
+    kv_shape = [batch, seq_len, heads // groups, dim]
     accum_dtype = "float"
 
     @T.prim_func
-    def flash_fwd(Q: T.Tensor(shape, dtype), K: T.Tensor(shape, dtype), V: T.Tensor(shape, dtype),
+    def flash_fwd(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
                   Output: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype)):
         with T.Kernel(T.ceildiv(seq_len, block_M), heads, batch, threads=threads) as (bx, by, bz):
             Q_shared = T.alloc_shared([block_M, dim], dtype)
@@ -52,14 +54,14 @@ def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
             T.fill(scores_max, -T.infinity(accum_dtype))
             loop_range = T.ceildiv((bx + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N)
             for k in T.Pipelined(loop_range, num_stages=2):
-                T.copy(K[bz, k * block_N:(k + 1) * block_N, by, :], K_shared)
+                T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
                 if is_causal:
                     for i, j in T.Parallel(block_M, block_N):
                         acc_s[i, j] = T.if_then_else(bx * block_M + i >= k * block_N + j, 0, -T.infinity(accum_dtype))
                 else:
                     T.clear(acc_s)
                 T.gemm(Q_shared, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                T.copy(V[bz, k * block_N:(k + 1) * block_N, by, :], V_shared)
+                T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
                 T.copy(scores_max, scores_max_prev)
                 T.reduce_max(acc_s, scores_max, dim=1, clear=False)
                 for i in T.Parallel(block_M):
@@ -123,17 +125,22 @@ def flashattn_bwd_postprocess(batch, heads, seq_len, dim, blk=64, threads=256, d
 
 @tilelang.jit
 def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=512, num_stages=2,
-                  dtype="float16", dq_mode="atomic"):
+                  dtype="float16", dq_mode="atomic", groups=1):
     """``dq_mode``: "atomic" (fp32 atomics into dQ, one kernel) or "none" (dK/dV only; dQ comes from
-    ``flashattn_bwd_dq``) -- the dQ atomics were 85% of the single-kernel time on MI355X."""
+    ``flashattn_bwd_dq``) -- the dQ atomics were 85% of the single-kernel time on MI355X.
+    GQA (``groups`` query heads per KV head): one block per KV head walks the Q/dO tiles of all
+    its query heads in ONE pipelined loop (head = it // n_q, tile = it % n_q), so dK/dV of the
+    group accumulate in registers -- no atomics, no per-query-head dK/dV buffers."""
     sm_scale = (1.0 / dim)**0.5
     scale = sm_scale * LOG2E
     shape = [batch, seq_len, heads, dim]
+    head_kv = heads // groups
+    kv_shape = [batch, seq_len, head_kv, dim]
     accum_dtype = "float"
 
     @T.macro
     def body(Q, K, V, dO, lse, Delta, dQ, dK, dV):
-        with T.Kernel(heads, T.ceildiv(seq_len, block_M), batch, threads=threads) as (bx, by, bz):
+        with T.Kernel(head_kv, T.ceildiv(seq_len, block_M), batch, threads=threads) as (bx, by, bz):
             K_shared = T.alloc_shared([block_M, dim], dtype)
             V_shared = T.alloc_shared([block_M, dim], dtype)
             q = T.alloc_shared([block_N, dim], dtype)
@@ -157,22 +164,25 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
             T.clear(dk)
             loop_st = T.floordiv(by * block_M, block_N) if is_causal else 0
             loop_ed = T.ceildiv(seq_len, block_N)
-            for k in T.Pipelined(loop_st, loop_ed, num_stages=num_stages):
-                T.copy(Q[bz, k * block_N:(k + 1) * block_N, bx, :], q)
+            n_q = loop_ed - loop_st
+            for it in T.Pipelined(n_q * groups, num_stages=num_stages):
+                hq = bx * groups + it // n_q
+                k = loop_st + it % n_q
+                T.copy(Q[bz, k * block_N:(k + 1) * block_N, hq, :], q)
                 T.clear(qkT)
                 T.gemm(K_shared, q, qkT, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                T.copy(lse[bz, bx, k * block_N:(k + 1) * block_N], lse_shared)
+                T.copy(lse[bz, hq, k * block_N:(k + 1) * block_N], lse_shared)
                 for i, j in T.Parallel(block_M, block_N):
                     qkT[i, j] = T.exp2(qkT[i, j] * scale - lse_shared[j])
                 if is_causal:
                     for i, j in T.Parallel(block_M, block_N):
                         qkT[i, j] = T.if_then_else(by * block_M + i <= k * block_N + j, qkT[i, j], 0)
-                T.copy(dO[bz, k * block_N:(k + 1) * block_N, bx, :], do)
+                T.copy(dO[bz, k * block_N:(k + 1) * block_N, hq, :], do)
                 T.clear(dsT)
                 T.gemm(V_shared, do, dsT, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 T.copy(qkT, qkT_cast)
                 T.gemm(qkT_cast, do, dv, policy=T.GemmWarpPolicy.FullRow)
-                T.copy(Delta[bz, bx, k * block_N:(k + 1) * block_N], delta)
+                T.copy(Delta[bz, hq, k * block_N:(k + 1) * block_N], delta)
                 for i, j in T.Parallel(block_M, block_N):
                     dsT_cast[i, j] = qkT[i, j] * (dsT[i, j] - delta[j]) * sm_scale
                 T.gemm(dsT_cast, q, dk, policy=T.GemmWarpPolicy.FullRow)
@@ -180,7 +190,7 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
                     T.copy(dsT_cast, dsT_shared)
                     T.clear(dq)
                     T.gemm(dsT_shared, K_shared, dq, transpose_A=True)
-                    T.atomic_add(dQ[bz, k * block_N:(k + 1) * block_N, bx, :], dq)
+                    T.atomic_add(dQ[bz, k * block_N:(k + 1) * block_N, hq, :], dq)
             T.copy(dv, dv_cast)
             T.copy(dk, dk_cast)
             T.copy(dv_cast, dV[bz, by * block_M:(by + 1) * block_M, bx, :])
@@ -189,18 +199,18 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
     if dq_mode == "atomic":
 
         @T.prim_func
-        def flash_bwd(Q: T.Tensor(shape, dtype), K: T.Tensor(shape, dtype), V: T.Tensor(shape, dtype),
+        def flash_bwd(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
                       dO: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
                       Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dQ: T.Tensor(shape, accum_dtype),
-                      dK: T.Tensor(shape, dtype), dV: T.Tensor(shape, dtype)):
+                      dK: T.Tensor(kv_shape, dtype), dV: T.Tensor(kv_shape, dtype)):
             body(Q, K, V, dO, lse, Delta, dQ, dK, dV)
     else:
 
         @T.prim_func
-        def flash_bwd(Q: T.Tensor(shape, dtype), K: T.Tensor(shape, dtype), V: T.Tensor(shape, dtype),
+        def flash_bwd(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
                       dO: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
-                      Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dK: T.Tensor(shape, dtype),
-                      dV: T.Tensor(shape, dtype)):
+                      Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dK: T.Tensor(kv_shape, dtype),
+                      dV: T.Tensor(kv_shape, dtype)):
             body(Q, K, V, dO, lse, Delta, None, dK, dV)
 
     return flash_bwd
@@ -208,17 +218,18 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
 
 @tilelang.jit(out_idx=[6])
 def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=256, num_stages=2,
-                     dtype="float16"):
+                     dtype="float16", groups=1):
     """dQ without atomics: one block per (query tile, head, batch) walks the KV tiles, recomputing
     P and dP (2 extra GEMMs) and accumulating dQ = dS K in registers -- on MI355X this is ~4x
     faster than fp32 atomics from every KV block (measured: docs/RESULTS.md)."""
     sm_scale = (1.0 / dim)**0.5
     scale = sm_scale * LOG2E
     shape = [batch, seq_len, heads, dim]
+    kv_shape = [batch, seq_len, heads // groups, dim]
     accum_dtype = "float"
 
     @T.prim_func
-    def flash_bwd_dq(Q: T.Tensor(shape, dtype), K: T.Tensor(shape, dtype), V: T.Tensor(shape, dtype),
+    def flash_bwd_dq(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
                      dO: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
                      Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dQ: T.Tensor(shape, dtype)):
         with T.Kernel(heads, T.ceildiv(seq_len, block_M), batch, threads=threads) as (bx, by, bz):
@@ -240,8 +251,8 @@ def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N
             T.clear(dq)
             loop_ed = T.ceildiv((by + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N)
             for k in T.Pipelined(loop_ed, num_stages=num_stages):
-                T.copy(K[bz, k * block_N:(k + 1) * block_N, bx, :], K_shared)
-                T.copy(V[bz, k * block_N:(k + 1) * block_N, bx, :], V_shared)
+                T.copy(K[bz, k * block_N:(k + 1) * block_N, bx // groups, :], K_shared)
+                T.copy(V[bz, k * block_N:(k + 1) * block_N, bx // groups, :], V_shared)
                 T.clear(s)
                 T.gemm(q, K_shared, s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 T.clear(dp)
@@ -274,8 +285,9 @@ class _attention:
                 @staticmethod
                 def forward(ctx, q, k, v, causal):
                     B, S, H, D = q.shape
+                    G = H // k.shape[2]
                     dt = "bfloat16" if q.dtype == torch.bfloat16 else "float16"
-                    o, lse = flashattn_fwd(B, H, S, D, causal, dtype=dt)(q, k, v)
+                    o, lse = flashattn_fwd(B, H, S, D, causal, dtype=dt, groups=G)(q, k, v)
                     ctx.save_for_backward(q, k, v, o, lse)
                     ctx.causal = causal
                     return o
@@ -284,19 +296,21 @@ class _attention:
                 def backward(ctx, do):
                     q, k, v, o, lse = ctx.saved_tensors
                     B, S, H, D = q.shape
+                    G = H // k.shape[2]
                     dt = "bfloat16" if q.dtype == torch.bfloat16 else "float16"
                     do = do.contiguous()
                     delta = flashattn_bwd_preprocess(B, H, S, D, dtype=dt)(o, do)
-                    dk = torch.empty_like(q)
-                    dv = torch.empty_like(q)
+                    dk = torch.empty_like(k)
+                    dv = torch.empty_like(v)
                     if BWD_DQ_MODE == "atomic":
                         dq = torch.zeros(B, S, H, D, dtype=torch.float32, device=q.device)
-                        flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt)(q, k, v, do, lse, delta, dq, dk, dv)
+                        flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, groups=G)(q, k, v, do, lse, delta, dq, dk, dv)
                         return flashattn_bwd_postprocess(B, H, S, D, dtype=dt)(dq), dk, dv, None
                     # dK/dV kernel without dQ + an atomic-free dQ kernel (the two could run on
                     # separate streams; they only share read-only inputs)
-                    flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, dq_mode="none")(q, k, v, do, lse, delta, dk, dv)
-                    dq = flashattn_bwd_dq(B, H, S, D, ctx.causal, dtype=dt)(q, k, v, do, lse, delta)
+                    flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, dq_mode="none", groups=G)(q, k, v, do, lse, delta,
+                                                                                              dk, dv)
+                    dq = flashattn_bwd_dq(B, H, S, D, ctx.causal, dtype=dt, groups=G)(q, k, v, do, lse, delta)
                     return dq, dk, dv, None
 
             cls.fn = Attn
@@ -310,6 +324,8 @@ def attention(q, k, v, causal=False):
 def ref_program(Q, K, V, is_causal):
     import torch
     dim = Q.size(-1)
+    G = Q.size(2) // K.size(2)
+    K, V = K.repeat_interleave(G, 2), V.repeat_interleave(G, 2)
     scores = torch.einsum("bqhd,bkhd->bhqk", Q.float(), K.float()) / dim**0.5
     if is_causal:
         s = Q.size(1)

@@ -14,6 +14,7 @@ Layouts are FLA's [B, T, H, D].  chunk_delta_h is the only sequential kernel: on
 operand); ``block_DV`` = 16 gives B*H*V/16 workgroups so a 32-head model fills the 256 CUs.
 """
 import argparse
+import functools
 
 import tilelang
 import tilelang.language as T
@@ -204,22 +205,30 @@ def chunk_o(B, S, H, DK, DV, C=64, scale=None, threads=256, dtype="bfloat16"):
     return main
 
 
+@functools.lru_cache(maxsize=None)
+def _kernels(B, S, H, DK, DV, C, block_DV, tgt):
+
+    def k_(impl, *args, out_idx):
+        return tilelang.compile(impl.get_tir(*args), out_idx=out_idx, target=tgt)
+
+    return (k_(chunk_cumsum, B, S, H, C, out_idx=[1]), k_(chunk_scaled_dot_kkt, B, S, H, DK, C, out_idx=[3]),
+            k_(solve_tril, B, S, H, C, out_idx=[1]), k_(wy_fast, B, S, H, DK, DV, C, out_idx=[5, 6]),
+            k_(chunk_delta_h, B, S, H, DK, DV, C, block_DV, out_idx=[4, 5, 6]),
+            k_(chunk_o, B, S, H, DK, DV, C, out_idx=[5]))
+
+
 def chunk_gated_delta_rule(q, k, v, g, beta, C=64, block_DV=16, target=None):
     """Full chunked GDN forward: (o [B,T,H,V], final state [B,H,K,V] fp32)."""
     B, S, H, DK = q.shape
     DV = v.shape[-1]
     tgt = target or ("cpu" if q.device.type == "cpu" else "hip")
-
-    def k_(impl, *args, out_idx, **kw):
-        return tilelang.compile(impl.get_tir(*args, **kw), out_idx=out_idx, target=tgt)
-
-    gc = k_(chunk_cumsum, B, S, H, C, out_idx=[1])(g.float().contiguous())
-    A = k_(chunk_scaled_dot_kkt, B, S, H, DK, C, out_idx=[3])(k, beta.float().contiguous(), gc)
-    Tm = k_(solve_tril, B, S, H, C, out_idx=[1])(A)
-    w, u = k_(wy_fast, B, S, H, DK, DV, C, out_idx=[5, 6])(k, v, beta.float().contiguous(), gc, Tm)
-    hs, vnew, hfin = k_(chunk_delta_h, B, S, H, DK, DV, C, block_DV, out_idx=[4, 5, 6])(k, w, u, gc)
-    o = k_(chunk_o, B, S, H, DK, DV, C, out_idx=[5])(q, k, vnew, hs, gc)
-    return o, hfin
+    k_cum, k_kkt, k_tril, k_wy, k_h, k_o = _kernels(B, S, H, DK, DV, C, block_DV, tgt)
+    beta = beta.float().contiguous()
+    gc = k_cum(g.float().contiguous())
+    Tm = k_tril(k_kkt(k, beta, gc))
+    w, u = k_wy(k, v, beta, gc, Tm)
+    hs, vnew, hfin = k_h(k, w, u, gc)
+    return k_o(q, k, vnew, hs, gc), hfin
 
 
 def naive_recurrent(q, k, v, g, beta, scale=None):
@@ -264,6 +273,16 @@ def main(B=1, S=32768, H=32, DK=128, DV=128):
     chunk_gated_delta_rule(q, k, v, g, beta)
     lat = do_bench(lambda: chunk_gated_delta_rule(q, k, v, g, beta))
     print(f"GDN chunked fwd B{B} S{S} H{H} K{DK} V{DV}: {lat:.3f} ms (all 6 kernels)")
+    k_cum, k_kkt, k_tril, k_wy, k_h, k_o = _kernels(B, S, H, DK, DV, 64, 16, "hip")
+    gc = k_cum(g)
+    A = k_kkt(k, beta, gc)
+    Tm = k_tril(A)
+    w, u = k_wy(k, v, beta, gc, Tm)
+    hs, vnew, _ = k_h(k, w, u, gc)
+    for name, fn in (("cumsum", lambda: k_cum(g)), ("scaled_dot_kkt", lambda: k_kkt(k, beta, gc)),
+                     ("solve_tril", lambda: k_tril(A)), ("wy_fast", lambda: k_wy(k, v, beta, gc, Tm)),
+                     ("chunk_delta_h", lambda: k_h(k, w, u, gc)), ("chunk_o", lambda: k_o(q, k, vnew, hs, gc))):
+        print(f"  {name}: {do_bench(fn):.3f} ms")
     # the critical sequential kernel alone
     gc = chunk_cumsum(B, S, H)(g)
     w = torch.randn(B, S, H, DK, device="cuda", dtype=torch.bfloat16) * 0.1

@@ -318,3 +318,25 @@ def test_gdn_chunked_matches_recurrence_cpu():
     o_ref, h_ref = naive_recurrent(q, k, v, g, beta)
     torch.testing.assert_close(o.float(), o_ref, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(hf, h_ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_gqa_attention_fwd_bwd_cpu(causal):
+    import example_mha_bwd as m
+    B, S, H, HKV, D = 1, 128, 4, 2, 64
+    G = H // HKV
+    q, do = torch.randn(B, S, H, D).half(), torch.randn(B, S, H, D).half()
+    k, v = torch.randn(B, S, HKV, D).half(), torch.randn(B, S, HKV, D).half()
+    o, lse = _both(m.flashattn_fwd, B, H, S, D, causal, 64, 64, groups=G)(q, k, v)
+    qf, kf, vf = [t.float().requires_grad_() for t in (q, k, v)]
+    ro = m.ref_program(qf, kf, vf, causal)
+    ro.backward(do.float())
+    torch.testing.assert_close(o.float(), ro.detach(), rtol=1e-2, atol=1e-2)
+    delta = _both(m.flashattn_bwd_preprocess, B, H, S, D)(o, do)
+    dq = _both(m.flashattn_bwd_dq, B, H, S, D, causal, 64, 64, 256, groups=G)(q, k, v, do, lse, delta)
+    dk, dv = torch.empty_like(k), torch.empty_like(v)
+    f = m.flashattn_bwd.get_tir(B, H, S, D, causal, 64, 64, 256, dq_mode="none", groups=G)
+    tilelang.compile(f, target="hip")
+    tilelang.compile(f, target="cpu")(q, k, v, do, lse, delta, dk, dv)
+    for a, r in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
+        torch.testing.assert_close(a.float(), r, rtol=1e-2, atol=1e-2)

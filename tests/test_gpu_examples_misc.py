@@ -273,3 +273,20 @@ def test_gdn_chunked_gpu():
     o_ref, h_ref = naive_recurrent(q, k, v, g, beta)
     torch.testing.assert_close(o.float().cpu(), o_ref, rtol=3e-2, atol=3e-2)
     torch.testing.assert_close(hf.cpu(), h_ref, rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_gqa_attention_bwd_gpu(causal):
+    import example_mha_bwd as m
+    B, S, H, HKV, D = 2, 512, 8, 2, 64
+    Q = torch.randn(B, S, H, D, dtype=torch.bfloat16, device="cuda").requires_grad_()
+    K = torch.randn(B, S, HKV, D, dtype=torch.bfloat16, device="cuda").requires_grad_()
+    V = torch.randn(B, S, HKV, D, dtype=torch.bfloat16, device="cuda").requires_grad_()
+    dO = torch.randn_like(Q)
+    m.attention(Q, K, V, causal).backward(dO)
+    grads = [t.grad.clone() for t in (Q, K, V)]
+    for t in (Q, K, V):
+        t.grad = None
+    m.ref_program(Q, K, V, causal).backward(dO)
+    for g, t in zip(grads, (Q, K, V)):
+        torch.testing.assert_close(g.float(), t.grad.float(), rtol=3e-2, atol=5e-2)
