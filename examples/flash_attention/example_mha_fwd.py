@@ -17,7 +17,10 @@ import tilelang.language as T
 
 @tilelang.jit(out_idx=[3])
 def flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=128, block_N=64, threads=256,
-              num_stages=2, dtype="bfloat16"):
+              num_stages=2, dtype="bfloat16", lazy_rescale=True):
+    """``lazy_rescale``: a row keeps its running max until a new score exceeds it by 2^8, so the
+    O accumulator is rescaled only on those (rare, after the first tiles) steps; a wave skips
+    the rescale when none of its rows moved."""
     scale = (1.0 / dim)**0.5 * 1.44269504  # log2(e): softmax via exp2
     head_kv = heads // groups
     q_shape = [batch, seq_len, heads, dim]
@@ -47,7 +50,10 @@ def flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=128
             T.copy(Q[bz, bx * block_M:(bx + 1) * block_M, by, :], Q_shared)
             T.fill(acc_o, 0)
             T.fill(logsum, 0)
-            T.fill(scores_max, -T.infinity(accum_dtype))
+            if lazy_rescale:
+                T.fill(scores_max, -(2.0**30))  # finite: a fully masked tile keeps it (no inf - inf)
+            else:
+                T.fill(scores_max, -T.infinity(accum_dtype))
 
             loop_range = (T.ceildiv((bx + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N))
 
@@ -62,11 +68,26 @@ def flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=128
                 T.gemm(Q_shared, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
                 T.copy(scores_max, scores_max_prev)
-                T.reduce_max(acc_s, scores_max, dim=1, clear=False)
-                for i in T.Parallel(block_M):
-                    scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
-                for i, j in T.Parallel(block_M, dim):
-                    acc_o[i, j] *= scores_scale[i]
+                if lazy_rescale:
+                    T.reduce_max(acc_s, scores_max_prev, dim=1, clear=False)  # candidate max
+                    rescale = T.alloc_var("int32")
+                    rescale = 0
+                    for i in T.Parallel(block_M):
+                        if (scores_max_prev[i] - scores_max[i]) * scale > 8.0:
+                            scores_scale[i] = T.exp2((scores_max[i] - scores_max_prev[i]) * scale)
+                            scores_max[i] = scores_max_prev[i]
+                            rescale = 1
+                        else:
+                            scores_scale[i] = 1.0
+                    if rescale != 0:
+                        for i, j in T.Parallel(block_M, dim):
+                            acc_o[i, j] *= scores_scale[i]
+                else:
+                    T.reduce_max(acc_s, scores_max, dim=1, clear=False)
+                    for i in T.Parallel(block_M):
+                        scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
+                    for i, j in T.Parallel(block_M, dim):
+                        acc_o[i, j] *= scores_scale[i]
                 for i, j in T.Parallel(block_M, block_N):
                     acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
                 T.reduce_sum(acc_s, scores_sum, dim=1)

@@ -67,24 +67,28 @@ def chunk_scaled_dot_kkt(B, S, H, DK, C=64, threads=256, dtype="bfloat16"):
 
 
 @tilelang.jit(out_idx=[1])
-def solve_tril(B, S, H, C=64, threads=64):
-    """Tm = (I + A)^-1 per chunk (A strictly lower): forward substitution in LDS, one row per
-    step, the C columns across the threads."""
+def solve_tril(B, S, H, C=64):
+    """Tm = (I + A)^-1 per chunk (A strictly lower) by forward substitution.  One thread per
+    column keeps its whole column of Tm in registers (fully unrolled, constant indices); the
+    row of A it needs is an LDS broadcast read, so each step is a register FMA chain."""
 
     @T.prim_func
     def main(A: T.Tensor([B, S, H, C], "float32"), Tm: T.Tensor([B, S, H, C], "float32")):
-        with T.Kernel(S // C, B * H, threads=threads) as (bc, bbh):
+        with T.Kernel(S // C, B * H, threads=C) as (bc, bbh):
             b, h = bbh // H, bbh % H
             a_s = T.alloc_shared([C, C], "float32")
             t_s = T.alloc_shared([C, C], "float32")
             T.copy(A[b, bc * C:(bc + 1) * C, h, :], a_s)
-            for i in T.serial(C):
-                for j in T.Parallel(C):
+            for j in T.Parallel(C, coalesced_width=1):  # one column per thread (no vectorising)
+                col = T.alloc_local([C], "float32")
+                for i in T.unroll(C):
                     acc = T.alloc_var("float32")
                     acc = T.if_then_else(i == j, 1.0, 0.0)
-                    for r in T.serial(i):
-                        acc = acc - a_s[i, r] * t_s[r, j]
-                    t_s[i, j] = acc
+                    for r in T.unroll(i):
+                        acc = acc - a_s[i, r] * col[r]
+                    col[i] = acc
+                for i in T.unroll(C):
+                    t_s[i, j] = col[i]
             T.copy(t_s, Tm[b, bc * C:(bc + 1) * C, h, :])
 
     return main

@@ -89,6 +89,22 @@ def w_decode(c):
     return ms, None, 2 * b * s * g * d * 2
 
 
+def w_fa_fwd(c):
+    import example_mha_fwd as m
+    B, H, S, D = 1, 64, 4096, 128
+    causal = c.pop("causal", False)
+    q, k_, v = [torch.randn(B, S, H, D, dtype=torch.bfloat16, device="cuda") for _ in range(3)]
+    k = m.flashattn(B, H, S, D, causal, 1, **c)
+    o = k(q, k_, v)
+    torch.testing.assert_close(o[:, :, :2].float(), m.ref_program(q[:, :, :2], k_[:, :, :2], v[:, :, :2], causal).float(),
+                               rtol=2e-2, atol=2e-2)
+    return do_bench(lambda: k(q, k_, v)), 4.0 * B * H * S * S * D * (0.5 if causal else 1.0)
+
+
+def w_sink_lazy(c):
+    return w_sink(c)
+
+
 if __name__ == "__main__":
     fn = globals()["w_" + sys.argv[1]]
     for a in sys.argv[2:]:
