@@ -26,7 +26,9 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[3])
 def flashattn_sink(batch, heads, seq_q, seq_kv, dim, groups=1, window_size=None, sm_scale=None, block_M=256,
-                   block_N=64, num_stages=2, threads=512, dtype="bfloat16", causal=True):
+                   block_N=64, num_stages=2, threads=512, dtype="bfloat16", causal=True, lazy_rescale=True):
+    """``lazy_rescale``: rows keep their running max until a score exceeds it by 2^8 (O is
+    rescaled only then, per wave), see example_mha_fwd.py."""
     if window_size is not None:
         assert window_size % block_N == 0, "window_size must be divisible by block_N"
     if sm_scale is None:
@@ -59,16 +61,32 @@ def flashattn_sink(batch, heads, seq_q, seq_kv, dim, groups=1, window_size=None,
         T.gemm(Q_shared, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
         T.copy(V[bz, by // groups, k * block_N:(k + 1) * block_N, :], V_shared)
         T.copy(scores_max, scores_max_prev)
-        T.reduce_max(acc_s, scores_max, dim=1, clear=False)
-        if masked:
-            # a row whose keys are all masked so far keeps a finite (0) running max: exp2 of
-            # -inf - 0 is 0, never inf - inf (softmax is shift invariant)
+        if lazy_rescale:
+            # running max starts finite (-2^30), so fully masked rows never see inf - inf
+            T.reduce_max(acc_s, scores_max_prev, dim=1, clear=False)
+            rescale = T.alloc_var("int32")
+            rescale = 0
             for i in T.Parallel(block_M):
-                scores_max[i] = T.if_then_else(scores_max[i] == -T.infinity(accum_dtype), 0, scores_max[i])
-        for i in T.Parallel(block_M):
-            scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
-        for i, j in T.Parallel(block_M, dim):
-            acc_o[i, j] *= scores_scale[i]
+                if (scores_max_prev[i] - scores_max[i]) * scale > 8.0:
+                    scores_scale[i] = T.exp2((scores_max[i] - scores_max_prev[i]) * scale)
+                    scores_max[i] = scores_max_prev[i]
+                    rescale = 1
+                else:
+                    scores_scale[i] = 1.0
+            if rescale != 0:
+                for i, j in T.Parallel(block_M, dim):
+                    acc_o[i, j] *= scores_scale[i]
+        else:
+            T.reduce_max(acc_s, scores_max, dim=1, clear=False)
+            if masked:
+                # a row whose keys are all masked so far keeps a finite (0) running max: exp2 of
+                # -inf - 0 is 0, never inf - inf (softmax is shift invariant)
+                for i in T.Parallel(block_M):
+                    scores_max[i] = T.if_then_else(scores_max[i] == -T.infinity(accum_dtype), 0, scores_max[i])
+            for i in T.Parallel(block_M):
+                scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
+            for i, j in T.Parallel(block_M, dim):
+                acc_o[i, j] *= scores_scale[i]
         for i, j in T.Parallel(block_M, block_N):
             acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
         T.reduce_sum(acc_s, scores_sum, dim=1)
@@ -100,7 +118,7 @@ def flashattn_sink(batch, heads, seq_q, seq_kv, dim, groups=1, window_size=None,
             T.copy(Q[bz, by, qt * block_M:(qt + 1) * block_M, :], Q_shared)
             T.fill(acc_o, 0)
             T.fill(logsum, 0)
-            T.fill(scores_max, -T.infinity(accum_dtype))
+            T.fill(scores_max, -(2.0**30) if lazy_rescale else -T.infinity(accum_dtype))
             # KV tiles [start, full_end) lie entirely below the diagonal (and inside the window's
             # far edge when windowed); [full_end, end) need the mask
             if causal:

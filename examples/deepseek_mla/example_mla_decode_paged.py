@@ -1,0 +1,166 @@
+"""DeepSeek MLA decode over a paged latent KV cache with per-sequence lengths (reference:
+examples/deepseek_mla/example_mla_decode_paged.py).
+
+KV pages [num_pages, page_size, 512] + K_pe pages [num_pages, page_size, 64]; ``BlockTable[b, i]``
+is the page holding tokens [i*page_size, (i+1)*page_size) of sequence b and ``CacheSeqlens[b]``
+its length.  Split-KV as in example_mla_decode.py: every split owns a contiguous token range
+(rounded to ``block_N``), each step reads one ``block_N`` slice of one page -- a data-dependent
+offset along the OUTERMOST (page) dim, which stays an LDS-DMA producer of ``T.Pipelined``
+(buffer resource over the whole pool).  Tokens past the sequence end are masked; a split with
+no tokens writes lse = -inf and is ignored by the combine kernel.
+"""
+import argparse
+
+import tilelang
+import tilelang.language as T
+
+
+@tilelang.jit(out_idx=[8])
+def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe_dim=64, block_N=64, block_H=64,
+                     num_split=4, threads=256, num_stages=2, dtype="bfloat16"):
+    scale = (1.0 / (dim + pe_dim))**0.5 * 1.44269504
+    accum_dtype = "float"
+    VALID_H = min(block_H, heads)
+    assert page_size % block_N == 0
+    max_pages = (max_seqlen + page_size - 1) // page_size
+
+    @T.prim_func
+    def main(Q: T.Tensor([batch, heads, dim], dtype), Q_pe: T.Tensor([batch, heads, pe_dim], dtype),
+             KV: T.Tensor([num_pages, page_size, dim], dtype), K_pe: T.Tensor([num_pages, page_size, pe_dim], dtype),
+             BlockTable: T.Tensor([batch, max_pages], "int32"), CacheSeqlens: T.Tensor([batch], "int32"),
+             glse: T.Tensor([batch, heads, num_split], accum_dtype),
+             Output_partial: T.Tensor([batch, heads, num_split, dim], accum_dtype),
+             Output: T.Tensor([batch, heads, dim], dtype)):
+        with T.Kernel(batch, heads // VALID_H, num_split, threads=threads) as (bx, by, bz):
+            Q_local = T.alloc_fragment([block_H, dim], dtype)
+            Q_pe_local = T.alloc_fragment([block_H, pe_dim], dtype)
+            KV_shared = T.alloc_shared([block_N, dim], dtype)
+            K_pe_shared = T.alloc_shared([block_N, pe_dim], dtype)
+            acc_s = T.alloc_fragment([block_H, block_N], accum_dtype)
+            acc_s_cast = T.alloc_fragment([block_H, block_N], dtype)
+            acc_o = T.alloc_fragment([block_H, dim], accum_dtype)
+            m = T.alloc_fragment([block_H], accum_dtype)
+            m_prev = T.alloc_fragment([block_H], accum_dtype)
+            alpha = T.alloc_fragment([block_H], accum_dtype)
+            r_sum = T.alloc_fragment([block_H], accum_dtype)
+            l_sum = T.alloc_fragment([block_H], accum_dtype)
+            seqlen = CacheSeqlens[bx]
+            # this split's token range, whole block_N tiles
+            n_tiles = T.ceildiv(seqlen, block_N)
+            per_split = T.ceildiv(n_tiles, num_split)
+            t_begin = T.min(bz * per_split, n_tiles)
+            t_end = T.min(t_begin + per_split, n_tiles)
+            T.copy(Q[bx, by * VALID_H:(by + 1) * VALID_H, :], Q_local)
+            T.copy(Q_pe[bx, by * VALID_H:(by + 1) * VALID_H, :], Q_pe_local)
+            T.fill(acc_o, 0)
+            T.fill(l_sum, 0)
+            T.fill(m, -(2.0**30))
+            for t in T.Pipelined(t_begin, t_end, num_stages=num_stages):
+                tok = t * block_N
+                page = BlockTable[bx, tok // page_size]
+                off = tok % page_size
+                T.copy(KV[page, off:off + block_N, :], KV_shared)
+                T.copy(K_pe[page, off:off + block_N, :], K_pe_shared)
+                for i, j in T.Parallel(block_H, block_N):
+                    acc_s[i, j] = T.if_then_else(tok + j < seqlen, 0, -T.infinity(accum_dtype))
+                T.gemm(Q_local, KV_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.gemm(Q_pe_local, K_pe_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.copy(m, m_prev)
+                T.reduce_max(acc_s, m, dim=1, clear=False)
+                for i in T.Parallel(block_H):
+                    alpha[i] = T.exp2((m_prev[i] - m[i]) * scale)
+                for i, j in T.Parallel(block_H, block_N):
+                    acc_s[i, j] = T.exp2(acc_s[i, j] * scale - m[i] * scale)
+                T.reduce_sum(acc_s, r_sum, dim=1)
+                T.copy(acc_s, acc_s_cast)
+                for i in T.Parallel(block_H):
+                    l_sum[i] = l_sum[i] * alpha[i] + r_sum[i]
+                for i, j in T.Parallel(block_H, dim):
+                    acc_o[i, j] *= alpha[i]
+                T.gemm(acc_s_cast, KV_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
+            for i, j in T.Parallel(block_H, dim):
+                acc_o[i, j] /= T.max(l_sum[i], 1e-30)
+            for i in T.Parallel(block_H):
+                l_sum[i] = T.if_then_else(l_sum[i] > 0, T.log2(l_sum[i]) + m[i] * scale, -T.infinity(accum_dtype))
+            T.copy(l_sum[0:VALID_H], glse[bx, by * VALID_H:(by + 1) * VALID_H, bz])
+            T.copy(acc_o[0:VALID_H, :], Output_partial[bx, by * VALID_H:(by + 1) * VALID_H, bz, :])
+
+        with T.Kernel(heads, batch, threads=128) as (hy, bz):
+            o_acc = T.alloc_fragment([dim], accum_dtype)
+            lse_max = T.alloc_var(accum_dtype)
+            lse_sum = T.alloc_var(accum_dtype)
+            sc = T.alloc_var(accum_dtype)
+            T.clear(o_acc)
+            lse_max = -(2.0**30)
+            for k in T.serial(num_split):
+                lse_max = T.max(lse_max, glse[bz, hy, k])
+            lse_sum = 0.0
+            for k in T.serial(num_split):
+                lse_sum += T.exp2(glse[bz, hy, k] - lse_max)
+            lse_sum = T.log2(lse_sum) + lse_max
+            for k in T.serial(num_split):
+                sc = T.exp2(glse[bz, hy, k] - lse_sum)
+                for i in T.Parallel(dim):
+                    o_acc[i] += T.if_then_else(sc > 0, Output_partial[bz, hy, k, i] * sc, 0.0)
+            for i in T.Parallel(dim):
+                Output[bz, hy, i] = o_acc[i]
+
+    return main
+
+
+def make_paged_cache(kv, k_pe, seqlens, page_size, num_pages=None, seed=0):
+    """Scatter contiguous caches [b, s, d] into a randomly permuted page pool."""
+    import torch
+    b, s, _ = kv.shape
+    max_pages = (s + page_size - 1) // page_size
+    num_pages = num_pages or b * max_pages
+    g = torch.Generator().manual_seed(seed)
+    perm = torch.randperm(num_pages, generator=g)[:b * max_pages].view(b, max_pages).int().to(kv.device)
+    kvp = torch.zeros(num_pages, page_size, kv.shape[-1], dtype=kv.dtype, device=kv.device)
+    pep = torch.zeros(num_pages, page_size, k_pe.shape[-1], dtype=kv.dtype, device=kv.device)
+    for i in range(b):
+        for p in range(max_pages):
+            n = min(page_size, s - p * page_size)
+            kvp[perm[i, p], :n] = kv[i, p * page_size:p * page_size + n]
+            pep[perm[i, p], :n] = k_pe[i, p * page_size:p * page_size + n]
+    return kvp, pep, perm
+
+
+def ref_program(q, q_pe, kv, k_pe, seqlens):
+    import torch
+    out = []
+    for i in range(q.shape[0]):
+        n = int(seqlens[i])
+        s = (q[i].float() @ kv[i, :n].float().t() + q_pe[i].float() @ k_pe[i, :n].float().t())
+        s = s / (q.shape[-1] + q_pe.shape[-1])**0.5
+        out.append(torch.softmax(s, -1) @ kv[i, :n].float())
+    return torch.stack(out).to(q.dtype)
+
+
+def main(batch=64, heads=128, max_seqlen=8192, page_size=64, num_split=4):
+    import torch
+    q = torch.randn(batch, heads, 512, device="cuda", dtype=torch.bfloat16)
+    q_pe = torch.randn(batch, heads, 64, device="cuda", dtype=torch.bfloat16)
+    kv = torch.randn(batch, max_seqlen, 512, device="cuda", dtype=torch.bfloat16)
+    k_pe = torch.randn(batch, max_seqlen, 64, device="cuda", dtype=torch.bfloat16)
+    seqlens = torch.randint(max_seqlen // 2, max_seqlen + 1, (batch, ), device="cuda", dtype=torch.int32)
+    kvp, pep, table = make_paged_cache(kv, k_pe, seqlens, page_size)
+    kernel = mla_decode_paged(batch, heads, max_seqlen, kvp.shape[0], page_size, num_split=num_split)
+    glse = torch.empty(batch, heads, num_split, device="cuda")
+    part = torch.empty(batch, heads, num_split, 512, device="cuda")
+    o = kernel(q, q_pe, kvp, pep, table, seqlens, glse, part)
+    torch.testing.assert_close(o[:2].float(), ref_program(q[:2], q_pe[:2], kv[:2], k_pe[:2], seqlens[:2]).float(),
+                               rtol=2e-2, atol=2e-2)
+    print("All checks pass.")
+    lat = kernel.get_profiler().do_bench(lambda: kernel(q, q_pe, kvp, pep, table, seqlens, glse, part))
+    toks = int(seqlens.sum())
+    flops = 2 * heads * toks * (512 + 64 + 512)
+    print(f"paged MLA decode b{batch} h{heads} avg ctx {toks // batch}: {lat:.3f} ms, {flops / lat * 1e-9:.1f} TFLOPS")
+
+
+if __name__ == "__main__":
+    p = argparse.ArgumentParser()
+    p.add_argument("--batch", type=int, default=64)
+    p.add_argument("--max_seqlen", type=int, default=8192)
+    a = p.parse_args()
+    main(a.batch, max_seqlen=a.max_seqlen)

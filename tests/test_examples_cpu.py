@@ -340,3 +340,17 @@ def test_gqa_attention_fwd_bwd_cpu(causal):
     tilelang.compile(f, target="cpu")(q, k, v, do, lse, delta, dk, dv)
     for a, r in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
         torch.testing.assert_close(a.float(), r, rtol=1e-2, atol=1e-2)
+
+
+def test_mla_decode_paged_cpu():
+    from example_mla_decode_paged import make_paged_cache, mla_decode_paged, ref_program
+    b, h, S, ps, ns = 3, 16, 200, 32, 3
+    q, qpe = torch.randn(b, h, 64).bfloat16(), torch.randn(b, h, 32).bfloat16()
+    kv, kpe = torch.randn(b, S, 64).bfloat16(), torch.randn(b, S, 32).bfloat16()
+    sl = torch.tensor([200, 37, 129], dtype=torch.int32)
+    kvp, pep, tab = make_paged_cache(kv, kpe, sl, ps)
+    f = mla_decode_paged.get_tir(b, h, S, kvp.shape[0], ps, 64, 32, 32, 16, ns, 64)
+    tilelang.compile(f, out_idx=[8], target="hip")
+    o = tilelang.compile(f, out_idx=[8], target="cpu")(q, qpe, kvp, pep, tab, sl, torch.empty(b, h, ns),
+                                                       torch.empty(b, h, ns, 64))
+    torch.testing.assert_close(o.float(), ref_program(q, qpe, kv, kpe, sl).float(), rtol=2e-2, atol=2e-2)

@@ -290,3 +290,17 @@ def test_gqa_attention_bwd_gpu(causal):
     m.ref_program(Q, K, V, causal).backward(dO)
     for g, t in zip(grads, (Q, K, V)):
         torch.testing.assert_close(g.float(), t.grad.float(), rtol=3e-2, atol=5e-2)
+
+
+def test_mla_decode_paged_gpu():
+    from example_mla_decode_paged import make_paged_cache, mla_decode_paged, ref_program
+    b, h, S, ps, ns = 4, 128, 1024, 64, 4
+    q = torch.randn(b, h, 512, device="cuda", dtype=torch.bfloat16)
+    qpe = torch.randn(b, h, 64, device="cuda", dtype=torch.bfloat16)
+    kv = torch.randn(b, S, 512, device="cuda", dtype=torch.bfloat16)
+    kpe = torch.randn(b, S, 64, device="cuda", dtype=torch.bfloat16)
+    sl = torch.tensor([1024, 77, 640, 300], dtype=torch.int32, device="cuda")
+    kvp, pep, tab = make_paged_cache(kv, kpe, sl, ps)
+    k = mla_decode_paged(b, h, S, kvp.shape[0], ps, num_split=ns)
+    o = k(q, qpe, kvp, pep, tab, sl, torch.empty(b, h, ns, device="cuda"), torch.empty(b, h, ns, 512, device="cuda"))
+    torch.testing.assert_close(o.float(), ref_program(q, qpe, kv, kpe, sl).float(), rtol=2e-2, atol=2e-2)
