@@ -354,3 +354,16 @@ def test_mla_decode_paged_cpu():
     o = tilelang.compile(f, out_idx=[8], target="cpu")(q, qpe, kvp, pep, tab, sl, torch.empty(b, h, ns),
                                                        torch.empty(b, h, ns, 64))
     torch.testing.assert_close(o.float(), ref_program(q, qpe, kv, kpe, sl).float(), rtol=2e-2, atol=2e-2)
+
+
+def test_grouped_gemm_bwd_cpu():
+    from example_grouped_gemm_bwd import construct_inputs, grouped_gemm, grouped_gemm_dw
+    sizes, K, N = (40, 100, 7), 64, 128
+    a, b, bs, bo, bpo = construct_inputs(list(sizes), K, N, False, 64, device="cpu")
+    dc = torch.randn(sum(sizes), N).half()
+    db = _both(grouped_gemm_dw, sizes, K, N, 64, 64, 32, 2, 128)(a, dc, bs, bo)
+    ref = torch.stack([a[s:s + n].float().t() @ dc[s:s + n].float() for s, n in zip(bo.tolist(), sizes)])
+    torch.testing.assert_close(db.float(), ref, rtol=1e-2, atol=5e-2)
+    da = _both(grouped_gemm, sizes, N, K, 64, 64, 64, 2, 128, "float16", True)(dc, b, bs, bo, bpo)
+    ref = torch.cat([dc[s:s + n].float() @ b[i].float().t() for i, (s, n) in enumerate(zip(bo.tolist(), sizes))])
+    torch.testing.assert_close(da.float(), ref, rtol=1e-2, atol=5e-2)

@@ -304,3 +304,8 @@ def test_mla_decode_paged_gpu():
     k = mla_decode_paged(b, h, S, kvp.shape[0], ps, num_split=ns)
     o = k(q, qpe, kvp, pep, tab, sl, torch.empty(b, h, ns, device="cuda"), torch.empty(b, h, ns, 512, device="cuda"))
     torch.testing.assert_close(o.float(), ref_program(q, qpe, kv, kpe, sl).float(), rtol=2e-2, atol=2e-2)
+
+
+def test_grouped_gemm_autograd_gpu():
+    import example_grouped_gemm_bwd as m
+    m.main((64, 300, 1024, 17), 512, 1024)
