@@ -1,0 +1,74 @@
+"""BF16 x MXFP4 weight-only GEMM (reference: examples/dequantize_gemm/
+example_dequant_gemm_bf16_mxfp4_hopper.py, example_dequant_gemm_fp4_hopper.py).
+
+C[M, N] = A[M, K] (bf16) @ dequant(Bq, S)^T with Bq [N, K/2] uint8 = two OCP e2m1 codes per byte
+(low nibble = even k) and S [N, K/32] uint8 e8m0 block scales (w = e2m1 * 2^(s-127)).  The
+packed tile (1/4 of a bf16 tile) and its scales stream through the LDS-DMA ring; the waves
+expand them into a bf16 LDS tile (the e2m1 decode is a 16-entry select, the e8m0 scale an
+exponent) and run bf16 MFMAs -- weight HBM traffic is 4.25 bits/element, which is what bounds
+the small-M (decode) shapes.  (gfx950 also has native fp4 MFMAs with e8m0 scales,
+v_mfma_scale_f32_16x16x128_f8f6f4; this example keeps the activations in bf16.)
+"""
+import argparse
+
+import tilelang
+import tilelang.language as T
+from tilelang.quantize import dequantize_mxfp4, e2m1_to_float, quantize_mxfp4
+
+
+@tilelang.jit(out_idx=[-1])
+def dequant_gemm_mxfp4(M, N, K, block_M=64, block_N=128, block_K=128, threads=256, num_stages=2,
+                       dtype="bfloat16", accum_dtype="float"):
+    assert K % block_K == 0 and block_K % 32 == 0
+
+    @T.prim_func
+    def main(A: T.Tensor((M, K), dtype), Bq: T.Tensor((N, K // 2), "uint8"), S: T.Tensor((N, K // 32), "uint8"),
+             C: T.Tensor((M, N), dtype)):
+        with T.Kernel(T.ceildiv(N, block_N), T.ceildiv(M, block_M), threads=threads) as (bx, by):
+            A_shared = T.alloc_shared((block_M, block_K), dtype)
+            Bq_shared = T.alloc_shared((block_N, block_K // 2), "uint8")
+            S_shared = T.alloc_shared((block_N, block_K // 32), "uint8")
+            B_shared = T.alloc_shared((block_N, block_K), dtype)
+            C_local = T.alloc_fragment((block_M, block_N), accum_dtype)
+            C_cast = T.alloc_fragment((block_M, block_N), dtype)
+            T.use_swizzle(panel_size=8)
+            T.clear(C_local)
+            for k in T.Pipelined(K // block_K, num_stages=num_stages):
+                T.copy(A[by * block_M, k * block_K], A_shared)
+                T.copy(Bq[bx * block_N, k * (block_K // 2)], Bq_shared)
+                T.copy(S[bx * block_N, k * (block_K // 32)], S_shared)
+                for n, kk in T.Parallel(block_N, block_K):
+                    nib = (Bq_shared[n, kk // 2] >> ((kk % 2) * 4)) & 15
+                    sc = T.exp2(T.Cast("float32", S_shared[n, kk // 32]) - 127.0)
+                    B_shared[n, kk] = T.Cast(dtype, e2m1_to_float(nib) * sc)
+                T.gemm(A_shared, B_shared, C_local, transpose_B=True)
+            T.copy(C_local, C_cast)
+            T.copy(C_cast, C[by * block_M, bx * block_N])
+
+    return main
+
+
+def ref_program(A, Bq, S):
+    return (A.float() @ dequantize_mxfp4(Bq, S).t()).to(A.dtype)
+
+
+def main(M=16, N=8192, K=8192):
+    import torch
+    kernel = dequant_gemm_mxfp4(M, N, K)
+    A = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    Bq, S = quantize_mxfp4(torch.randn(N, K, device="cuda"))
+    c = kernel(A, Bq, S)
+    torch.testing.assert_close(c.float(), ref_program(A, Bq, S).float(), rtol=2e-2, atol=1.0)
+    print("All checks pass.")
+    lat = kernel.get_profiler().do_bench(lambda: kernel(A, Bq, S))
+    print(f"bf16 x mxfp4 GEMM {M}x{N}x{K}: {lat:.4f} ms, {2 * M * N * K / lat * 1e-9:.1f} TFLOPS, "
+          f"{(N * K // 2 + N * K // 32 + M * K * 2) / lat * 1e-6:.1f} GB/s")
+
+
+if __name__ == "__main__":
+    p = argparse.ArgumentParser()
+    p.add_argument("--m", type=int, default=16)
+    p.add_argument("--n", type=int, default=8192)
+    p.add_argument("--k", type=int, default=8192)
+    a = p.parse_args()
+    main(a.m, a.n, a.k)

@@ -367,3 +367,13 @@ def test_grouped_gemm_bwd_cpu():
     da = _both(grouped_gemm, sizes, N, K, 64, 64, 64, 2, 128, "float16", True)(dc, b, bs, bo, bpo)
     ref = torch.cat([dc[s:s + n].float() @ b[i].float().t() for i, (s, n) in enumerate(zip(bo.tolist(), sizes))])
     torch.testing.assert_close(da.float(), ref, rtol=1e-2, atol=5e-2)
+
+
+def test_dequant_gemm_mxfp4_cpu():
+    from example_dequant_gemm_mxfp4 import dequant_gemm_mxfp4, ref_program
+    from tilelang.quantize import quantize_mxfp4
+    M, N, K = 32, 128, 256
+    k = _both(dequant_gemm_mxfp4, M, N, K, 32, 64, 128, 128)
+    A = torch.randn(M, K).bfloat16()
+    Bq, S = quantize_mxfp4(torch.randn(N, K))
+    torch.testing.assert_close(k(A, Bq, S).float(), ref_program(A, Bq, S).float(), rtol=2e-2, atol=0.5)

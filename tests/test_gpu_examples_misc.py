@@ -309,3 +309,13 @@ def test_mla_decode_paged_gpu():
 def test_grouped_gemm_autograd_gpu():
     import example_grouped_gemm_bwd as m
     m.main((64, 300, 1024, 17), 512, 1024)
+
+
+def test_dequant_gemm_mxfp4_gpu():
+    from example_dequant_gemm_mxfp4 import dequant_gemm_mxfp4, ref_program
+    from tilelang.quantize import quantize_mxfp4
+    M, N, K = 64, 1024, 2048
+    A = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    Bq, S = quantize_mxfp4(torch.randn(N, K, device="cuda"))
+    torch.testing.assert_close(dequant_gemm_mxfp4(M, N, K)(A, Bq, S).float(), ref_program(A, Bq, S).float(),
+                               rtol=2e-2, atol=1.0)
