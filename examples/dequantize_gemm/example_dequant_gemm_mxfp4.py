@@ -17,8 +17,15 @@ from tilelang.quantize import dequantize_mxfp4, e2m1_to_float, quantize_mxfp4
 
 
 @tilelang.jit(out_idx=[-1])
-def dequant_gemm_mxfp4(M, N, K, block_M=64, block_N=128, block_K=128, threads=256, num_stages=2,
+def dequant_gemm_mxfp4(M, N, K, block_M=None, block_N=None, block_K=128, threads=None, num_stages=2,
                        dtype="bfloat16", accum_dtype="float"):
+    # decode (small M): thin tiles so N/block_N workgroups fill the CUs; prefill: 128x128
+    if block_M is None:
+        block_M = 16 if M <= 16 else (64 if M <= 256 else 128)
+    if block_N is None:
+        block_N = 32 if M <= 16 else 128
+    if threads is None:
+        threads = 64 if M <= 16 else 256
     assert K % block_K == 0 and block_K % 32 == 0
 
     @T.prim_func
@@ -38,9 +45,19 @@ def dequant_gemm_mxfp4(M, N, K, block_M=64, block_N=128, block_K=128, threads=25
                 T.copy(Bq[bx * block_N, k * (block_K // 2)], Bq_shared)
                 T.copy(S[bx * block_N, k * (block_K // 32)], S_shared)
                 for n, kk in T.Parallel(block_N, block_K):
-                    nib = (Bq_shared[n, kk // 2] >> ((kk % 2) * 4)) & 15
-                    sc = T.exp2(T.Cast("float32", S_shared[n, kk // 32]) - 127.0)
-                    B_shared[n, kk] = T.Cast(dtype, e2m1_to_float(nib) * sc)
+                    nib = T.Cast("int32", (Bq_shared[n, kk // 2] >> ((kk % 2) * 4)) & 15)
+                    if dtype == "bfloat16":
+                        # integer decode straight into bf16 bits: the e8m0 scale only adds to
+                        # the exponent field (e2m1 e=0 is 0 or 0.5 -> exponent s-1)
+                        sc = T.Cast("int32", S_shared[n, kk // 32])
+                        e = (nib >> 1) & 3
+                        sgn = (nib & 8) << 12
+                        bits = T.if_then_else(e == 0, T.if_then_else((nib & 1) == 1, sgn | ((sc - 1) << 7), sgn),
+                                              sgn | ((e + sc - 1) << 7) | ((nib & 1) << 6))
+                        B_shared[n, kk] = T.reinterpret(T.Cast("uint16", bits), dtype)
+                    else:
+                        sc = T.exp2(T.Cast("float32", S_shared[n, kk // 32]) - 127.0)
+                        B_shared[n, kk] = T.Cast(dtype, e2m1_to_float(nib) * sc)
                 T.gemm(A_shared, B_shared, C_local, transpose_B=True)
             T.copy(C_local, C_cast)
             T.copy(C_cast, C[by * block_M, bx * block_N])

@@ -97,3 +97,36 @@ def test_dsl_dequant_expressions_match_host():
     pk, e = Q.quantize_mxfp4(W, 32)
     out = _deq_kernel(8, 64)(pk, e)
     torch.testing.assert_close(out, Q.dequantize_mxfp4(pk, e, 32))
+
+
+def test_math_testing_utils_libinfo():
+    import torch
+
+    import tilelang
+    import tilelang.language as T
+    from tilelang.utils.language import (is_fragment, is_global, is_shared, legalize_pairwise_extents,
+                                         retrieve_shape)
+    assert tilelang.cdiv(7, 2) == 4 and tilelang.math.next_power_of_2(33) == 64
+    assert tilelang.math.next_power_of_2(1) == 1 and tilelang.math.prev_power_of_2(33) == 32
+    tilelang.testing.set_random_seed(3)
+    a = torch.rand(4)
+    tilelang.testing.set_random_seed(3)
+    assert torch.equal(a, torch.rand(4))
+    tilelang.testing.torch_assert_close(a, a + 1e-4)
+    try:
+        tilelang.testing.torch_assert_close(a, a + 1)
+        raise RuntimeError("expected a mismatch")
+    except AssertionError as e:
+        assert "mismatched" in str(e)
+    assert tilelang.libinfo.find_lib_path("_tl_runtime")
+    assert legalize_pairwise_extents([1, 64, 32], [64, 32]) == ([64, 32], [64, 32])
+
+    @T.prim_func
+    def f(A: T.Tensor((64, 64), "float16")):
+        with T.Kernel(1, threads=64):
+            s = T.alloc_shared((16, 64), "float16")
+            r = T.alloc_fragment((16, 64), "float")
+            assert is_global(A) and is_shared(s) and is_fragment(r)
+            assert [int(x) for x in retrieve_shape(A[0:16, :])] == [16, 64]
+            T.copy(A[0:16, :], s)
+            T.copy(s, r)

@@ -15,6 +15,8 @@ from .engine.lower import lower  # noqa: F401
 from .cache import clear_cache, disable_cache, enable_cache  # noqa: F401
 from .utils.target import determine_target  # noqa: F401
 from . import layout  # noqa: F401
+from . import math  # noqa: F401,A004
+from .math import cdiv, next_power_of_2  # noqa: F401
 
 
 class _TqdmLoggingHandler(_logging.StreamHandler):
@@ -43,6 +45,10 @@ def __getattr__(name):
     if name == "Profiler":
         from .profiler import Profiler
         return Profiler
+    if name in ("testing", "carver", "tools", "quantize", "ops", "models", "parallel", "libinfo", "profiler",
+                "autotuner", "analysis"):
+        import importlib
+        return importlib.import_module(f"{__name__}.{name}")
     if name == "TensorSupplyType":
         from .utils.tensor import TensorSupplyType
         return TensorSupplyType
