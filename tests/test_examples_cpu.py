@@ -377,3 +377,13 @@ def test_dequant_gemm_mxfp4_cpu():
     A = torch.randn(M, K).bfloat16()
     Bq, S = quantize_mxfp4(torch.randn(N, K))
     torch.testing.assert_close(k(A, Bq, S).float(), ref_program(A, Bq, S).float(), rtol=2e-2, atol=0.5)
+
+
+def test_gemm_with_mesh_tensor_cpu():
+    from example_gemm_with_mesh_tensor import matmul
+    k = _both(matmul, 128, 128, 128, 64, 64, 32)
+    a, b = torch.randn(128, 128).half(), torch.randn(128, 128).half()
+    torch.testing.assert_close(k(a, b).float(), a.float() @ b.float(), rtol=1e-2, atol=1e-1)
+    # a (2, 2) mesh: every core sees its [64, 64] shard
+    f = matmul.get_tir(128, 128, 128, 64, 64, 32, (2, 2))
+    assert [int(x) for x in f.params[0].shape] == [64, 64]
