@@ -20,12 +20,13 @@ from tilelang.quantize import dequantize_mxfp4, e2m1_to_float, quantize_mxfp4
 def dequant_gemm_mxfp4(M, N, K, block_M=None, block_N=None, block_K=128, threads=None, num_stages=2,
                        dtype="bfloat16", accum_dtype="float"):
     # decode (small M): thin tiles so N/block_N workgroups fill the CUs; prefill: 128x128
+    # (prefill: a 256-row tile amortises the per-element decode over twice the MFMA work)
     if block_M is None:
-        block_M = 16 if M <= 16 else (64 if M <= 256 else 128)
+        block_M = 16 if M <= 16 else (64 if M <= 256 else 256)
     if block_N is None:
         block_N = 32 if M <= 16 else 128
     if threads is None:
-        threads = 64 if M <= 16 else 256
+        threads = 64 if M <= 16 else (256 if M <= 256 else 512)
     assert K % block_K == 0 and block_K % 32 == 0
 
     @T.prim_func
