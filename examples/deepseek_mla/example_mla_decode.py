@@ -14,7 +14,14 @@ import tilelang.language as T
 
 @tilelang.jit(out_idx=[6], pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True})
 def mla_decode(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, block_H=64, num_split=4,
-               threads=256, num_stages=2, dtype="float16"):
+               threads=None, num_stages=2, dtype="float16", wide=None):
+    """``wide`` (default for 64-head blocks): 8 waves, S on a 4x2 wave grid, P through LDS and
+    O = P KV split over the 512 latent columns (see tilelang/ops/dsa.py sparse_mla_fwd)."""
+    if wide is None:
+        wide = block_H == 64
+    if threads is None:
+        threads = 512 if wide else 256
+    s_policy = T.GemmWarpPolicy.Square if wide else T.GemmWarpPolicy.FullRow
     scale = (1.0 / (dim + pe_dim))**0.5 * 1.44269504  # softmax in base 2
     accum_dtype = "float"
     kv_group_num = heads // kv_head_num
@@ -31,6 +38,8 @@ def mla_decode(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, bl
             K_pe_shared = T.alloc_shared([block_N, pe_dim], dtype)
             acc_s = T.alloc_fragment([block_H, block_N], accum_dtype)
             acc_s_cast = T.alloc_fragment([block_H, block_N], dtype)
+            P_shared = T.alloc_shared([block_H, block_N], dtype)
+            sc_shared = T.alloc_shared([block_H], accum_dtype)
             acc_o = T.alloc_fragment([block_H, dim], accum_dtype)
             scores_max = T.alloc_fragment([block_H], accum_dtype)
             scores_max_prev = T.alloc_fragment([block_H], accum_dtype)
@@ -49,8 +58,8 @@ def mla_decode(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, bl
                 T.copy(KV[bx, kv_start:kv_start + block_N, 0, :], KV_shared)
                 T.copy(K_pe[bx, kv_start:kv_start + block_N, 0, :], K_pe_shared)
                 T.clear(acc_s)
-                T.gemm(Q_local, KV_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                T.gemm(Q_pe_local, K_pe_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.gemm(Q_local, KV_shared, acc_s, transpose_B=True, policy=s_policy)
+                T.gemm(Q_pe_local, K_pe_shared, acc_s, transpose_B=True, policy=s_policy)
                 T.copy(scores_max, scores_max_prev)
                 T.reduce_max(acc_s, scores_max, dim=1, clear=False)
                 for i in T.Parallel(block_H):
@@ -58,14 +67,26 @@ def mla_decode(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, bl
                 for i, j in T.Parallel(block_H, block_N):
                     acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
                 T.reduce_sum(acc_s, scores_sum, dim=1)
-                T.copy(acc_s, acc_s_cast)
                 for i in T.Parallel(block_H):
                     logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
+                if wide:
+                    T.copy(scores_scale, sc_shared)
+                    T.copy(acc_s, P_shared)
+                    for i, j in T.Parallel(block_H, dim):
+                        acc_o[i, j] *= sc_shared[i]
+                    T.gemm(P_shared, KV_shared, acc_o)
+                else:
+                    T.copy(acc_s, acc_s_cast)
+                    for i, j in T.Parallel(block_H, dim):
+                        acc_o[i, j] *= scores_scale[i]
+                    T.gemm(acc_s_cast, KV_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
+            if wide:
+                T.copy(logsum, sc_shared)
                 for i, j in T.Parallel(block_H, dim):
-                    acc_o[i, j] *= scores_scale[i]
-                T.gemm(acc_s_cast, KV_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
-            for i, j in T.Parallel(block_H, dim):
-                acc_o[i, j] /= logsum[i]
+                    acc_o[i, j] /= sc_shared[i]
+            else:
+                for i, j in T.Parallel(block_H, dim):
+                    acc_o[i, j] /= logsum[i]
             for i in T.Parallel(block_H):
                 logsum[i] = T.log2(logsum[i]) + scores_max[i] * scale
             T.copy(logsum, glse[bx, by * VALID_BLOCK_H:(by + 1) * VALID_BLOCK_H, bz])

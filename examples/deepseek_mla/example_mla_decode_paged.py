@@ -17,7 +17,12 @@ import tilelang.language as T
 
 @tilelang.jit(out_idx=[8])
 def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe_dim=64, block_N=64, block_H=64,
-                     num_split=4, threads=256, num_stages=2, dtype="bfloat16"):
+                     num_split=4, threads=None, num_stages=2, dtype="bfloat16", wide=None):
+    if wide is None:
+        wide = block_H == 64  # 8 waves, O split over the latent columns (example_mla_decode.py)
+    if threads is None:
+        threads = 512 if wide else 256
+    s_policy = T.GemmWarpPolicy.Square if wide else T.GemmWarpPolicy.FullRow
     scale = (1.0 / (dim + pe_dim))**0.5 * 1.44269504
     accum_dtype = "float"
     VALID_H = min(block_H, heads)
@@ -38,6 +43,8 @@ def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe
             K_pe_shared = T.alloc_shared([block_N, pe_dim], dtype)
             acc_s = T.alloc_fragment([block_H, block_N], accum_dtype)
             acc_s_cast = T.alloc_fragment([block_H, block_N], dtype)
+            P_shared = T.alloc_shared([block_H, block_N], dtype)
+            sc_shared = T.alloc_shared([block_H], accum_dtype)
             acc_o = T.alloc_fragment([block_H, dim], accum_dtype)
             m = T.alloc_fragment([block_H], accum_dtype)
             m_prev = T.alloc_fragment([block_H], accum_dtype)
@@ -63,8 +70,8 @@ def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe
                 T.copy(K_pe[page, off:off + block_N, :], K_pe_shared)
                 for i, j in T.Parallel(block_H, block_N):
                     acc_s[i, j] = T.if_then_else(tok + j < seqlen, 0, -T.infinity(accum_dtype))
-                T.gemm(Q_local, KV_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                T.gemm(Q_pe_local, K_pe_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.gemm(Q_local, KV_shared, acc_s, transpose_B=True, policy=s_policy)
+                T.gemm(Q_pe_local, K_pe_shared, acc_s, transpose_B=True, policy=s_policy)
                 T.copy(m, m_prev)
                 T.reduce_max(acc_s, m, dim=1, clear=False)
                 for i in T.Parallel(block_H):
@@ -72,14 +79,26 @@ def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe
                 for i, j in T.Parallel(block_H, block_N):
                     acc_s[i, j] = T.exp2(acc_s[i, j] * scale - m[i] * scale)
                 T.reduce_sum(acc_s, r_sum, dim=1)
-                T.copy(acc_s, acc_s_cast)
                 for i in T.Parallel(block_H):
                     l_sum[i] = l_sum[i] * alpha[i] + r_sum[i]
+                if wide:
+                    T.copy(alpha, sc_shared)
+                    T.copy(acc_s, P_shared)
+                    for i, j in T.Parallel(block_H, dim):
+                        acc_o[i, j] *= sc_shared[i]
+                    T.gemm(P_shared, KV_shared, acc_o)
+                else:
+                    T.copy(acc_s, acc_s_cast)
+                    for i, j in T.Parallel(block_H, dim):
+                        acc_o[i, j] *= alpha[i]
+                    T.gemm(acc_s_cast, KV_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
+            if wide:
+                T.copy(l_sum, sc_shared)
                 for i, j in T.Parallel(block_H, dim):
-                    acc_o[i, j] *= alpha[i]
-                T.gemm(acc_s_cast, KV_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
-            for i, j in T.Parallel(block_H, dim):
-                acc_o[i, j] /= T.max(l_sum[i], 1e-30)
+                    acc_o[i, j] /= T.max(sc_shared[i], 1e-30)
+            else:
+                for i, j in T.Parallel(block_H, dim):
+                    acc_o[i, j] /= T.max(l_sum[i], 1e-30)
             for i in T.Parallel(block_H):
                 l_sum[i] = T.if_then_else(l_sum[i] > 0, T.log2(l_sum[i]) + m[i] * scale, -T.infinity(accum_dtype))
             T.copy(l_sum[0:VALID_H], glse[bx, by * VALID_H:(by + 1) * VALID_H, bz])

@@ -387,3 +387,30 @@ def test_gemm_with_mesh_tensor_cpu():
     # a (2, 2) mesh: every core sees its [64, 64] shard
     f = matmul.get_tir(128, 128, 128, 64, 64, 32, (2, 2))
     assert [int(x) for x in f.params[0].shape] == [64, 64]
+
+
+def test_wide_mla_schedules_cpu():
+    """8-wave schedules (S on a 4x2 wave grid, P and the row scales through LDS)."""
+    import sparse_mla_fwd as sm
+    from example_mla_decode import mla_decode, ref_program as mla_ref
+    from example_mla_decode_paged import make_paged_cache, mla_decode_paged, ref_program
+    B, S, SKV, H, D, DT, topk = 1, 4, 128, 64, 64, 32, 64
+    k = _both(sm.sparse_mla_fwd, B, S, SKV, H, D, DT, topk, 1, None, 32, None, "float16", wide=True)
+    q, kv = torch.randn(B, S, H, D + DT).half(), torch.randn(B, SKV, 1, D + DT).half()
+    idx = sm.make_indices(B, S, SKV, 1, topk)
+    torch.testing.assert_close(k(q, kv, idx)[0].float(), sm.ref_program(q, kv, idx, D).float(), rtol=1e-2, atol=1e-2)
+    b, h, S2, ps, ns = 2, 64, 128, 32, 2
+    q, qpe = torch.randn(b, h, 64).bfloat16(), torch.randn(b, h, 32).bfloat16()
+    kv, kpe = torch.randn(b, S2, 64).bfloat16(), torch.randn(b, S2, 32).bfloat16()
+    sl = torch.tensor([128, 45], dtype=torch.int32)
+    kvp, pep, tab = make_paged_cache(kv, kpe, sl, ps)
+    f = mla_decode_paged.get_tir(b, h, S2, kvp.shape[0], ps, 64, 32, 32, 64, ns, wide=True)
+    tilelang.compile(f, out_idx=[8], target="hip")
+    o = tilelang.compile(f, out_idx=[8], target="cpu")(q, qpe, kvp, pep, tab, sl, torch.empty(b, h, ns),
+                                                       torch.empty(b, h, ns, 64))
+    torch.testing.assert_close(o.float(), ref_program(q, qpe, kv, kpe, sl).float(), rtol=2e-2, atol=2e-2)
+    kd = _both(mla_decode, b, h, 1, S2, 64, 32, 32, 64, ns, wide=True)
+    o = kd(q.half(), qpe.half(), kv.half().unsqueeze(2), kpe.half().unsqueeze(2), torch.empty(b, h, ns),
+           torch.empty(b, h, ns, 64))
+    torch.testing.assert_close(o.float(), mla_ref(q.half(), qpe.half(), kv.half().unsqueeze(2),
+                                                  kpe.half().unsqueeze(2)).float(), rtol=2e-2, atol=2e-2)
