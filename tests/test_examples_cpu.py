@@ -414,3 +414,21 @@ def test_wide_mla_schedules_cpu():
            torch.empty(b, h, ns, 64))
     torch.testing.assert_close(o.float(), mla_ref(q.half(), qpe.half(), kv.half().unsqueeze(2),
                                                   kpe.half().unsqueeze(2)).float(), rtol=2e-2, atol=2e-2)
+
+
+def test_sparse_mla_bwd_cpu():
+    import sparse_mla_bwd as m
+    from sparse_mla_fwd import make_indices
+    from tilelang.ops import dsa
+    B, S, SKV, H, D, DT, topk = 1, 8, 64, 16, 64, 32, 64
+    q, kv = torch.randn(B, S, H, D + DT).bfloat16(), torch.randn(B, SKV, 1, D + DT).bfloat16()
+    do = torch.randn(B, S, H, D).bfloat16()
+    idx = make_indices(B, S, SKV, 1, topk)
+    o, lse = dsa.for_target("sparse_mla_fwd", "cpu", B, S, SKV, H, D, DT, topk)(q, kv, idx)
+    dq, dkv = m.sparse_mla_bwd(q, kv, o, do, idx, lse)
+    rq, rkv = m.ref_bwd(q, kv, do, idx, D)
+    torch.testing.assert_close(dq.float(), rq, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(dkv, rkv, rtol=2e-2, atol=2e-2)
+    for impl, args in ((m.sparse_mla_bwd_dq, (1, 64, 256, 64, 512, 64, 128)),
+                       (m.sparse_mla_bwd_dkv, (1, 64, 256, 64, 512, 64, 128))):
+        tilelang.compile(impl.get_tir(*args), out_idx=impl.out_idx, target="hip")

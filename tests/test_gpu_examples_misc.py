@@ -319,3 +319,22 @@ def test_dequant_gemm_mxfp4_gpu():
     Bq, S = quantize_mxfp4(torch.randn(N, K, device="cuda"))
     torch.testing.assert_close(dequant_gemm_mxfp4(M, N, K)(A, Bq, S).float(), ref_program(A, Bq, S).float(),
                                rtol=2e-2, atol=1.0)
+
+
+def test_sparse_mla_bwd_gpu():
+    import sparse_mla_bwd as m
+    from tilelang.ops.dsa import sparse_mla_fwd
+    B, S, SKV, H, topk = 1, 64, 256, 64, 128
+    q = (torch.randn(B, S, H, 576, device="cuda") / 4).bfloat16()
+    kv = (torch.randn(B, SKV, 1, 576, device="cuda") / 4).bfloat16()
+    do = torch.randn(B, S, H, 512, device="cuda", dtype=torch.bfloat16)
+    r = torch.rand(S, SKV, device="cuda")
+    pos = torch.arange(S, device="cuda")[:, None] + SKV - S
+    r = torch.where(torch.arange(SKV, device="cuda")[None, :] <= pos, r, torch.full_like(r, -1.0))
+    idx = r.topk(topk, -1).indices.int()
+    idx = torch.where(torch.gather(r, 1, idx.long()) >= 0, idx, torch.full_like(idx, SKV)).view(B, S, 1, topk)
+    o, lse = sparse_mla_fwd(B, S, SKV, H, 512, 64, topk)(q, kv, idx)
+    dq, dkv = m.sparse_mla_bwd(q, kv, o, do, idx, lse)
+    rq, rkv = m.ref_bwd(q, kv, do, idx)
+    torch.testing.assert_close(dq.float().cpu(), rq, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(dkv.cpu(), rkv, rtol=3e-2, atol=3e-2)
