@@ -11,8 +11,9 @@ MI355X decomposition (LDS is 160 KB, so Q, dO and a KV tile cannot all stay resi
   dQ += dS K; P and dS
   (bf16) are written out for the second kernel.
 * ``sparse_mla_bwd_dkv``: one block per token keeps Q and dO in LDS (138 KB) and walks its
-  ``topk`` rows in 64-row tiles: acc = dS^T Q + P^T dO on MFMA, then fp32 atomics scatter
-  the 64 x 576 partial into dKV at the selected rows (different tokens select the same rows).
+  ``topk`` rows in 32-row tiles: acc = dS^T Q + P^T dO on MFMA, then fp32 atomics scatter
+  the 32 x 576 partial into dKV at the selected rows (different tokens select the same rows),
+  staged through LDS so each wave atomic covers 64 consecutive floats of one row.
 """
 import argparse
 
@@ -111,9 +112,16 @@ def sparse_mla_bwd_dq(B, S, SKV, H, D, DT, topk, sm_scale=None, block_I=32, num_
 
 
 @tilelang.jit
-def sparse_mla_bwd_dkv(B, S, SKV, H, D, DT, topk, block_I=64, threads=256, dtype="bfloat16"):
-    """dKV[b, idx, 0, :] += dS^T Q (+ P^T dO on [0, D)); dKV is fp32 and zeroed by the caller."""
+def sparse_mla_bwd_dkv(B, S, SKV, H, D, DT, topk, block_I=32, block_C=64, threads=256, dtype="bfloat16"):
+    """dKV[b, idx, 0, :] += dS^T Q (+ P^T dO on [0, D)); dKV is fp32 and zeroed by the caller.
+
+    The MFMA accumulator is scattered in ``block_C``-column slices staged through LDS so every
+    wave-wide fp32 atomic covers 64 consecutive floats of ONE selected row (two cache lines);
+    atomics issued straight from the MFMA layout touch 16+ lines per instruction and were ~20x
+    slower."""
     NI = topk // block_I
+    assert D % block_C == 0 and DT <= block_C
+    NC = D // block_C
     accum = "float"
 
     @T.prim_func
@@ -127,6 +135,7 @@ def sparse_mla_bwd_dkv(B, S, SKV, H, D, DT, topk, block_I=64, threads=256, dtype
             p_s = T.alloc_shared([H, block_I], dtype)
             ds_s = T.alloc_shared([H, block_I], dtype)
             idx_s = T.alloc_shared([block_I], "int32")
+            stage = T.alloc_shared([block_I, block_C], accum)
             acc = T.alloc_fragment([block_I, D], accum)
             acct = T.alloc_fragment([block_I, DT], accum)
             T.copy(Q[bz, bx, :, 0:D], Q_s)
@@ -141,12 +150,15 @@ def sparse_mla_bwd_dkv(B, S, SKV, H, D, DT, topk, block_I=64, threads=256, dtype
                 T.gemm(ds_s, Q_s, acc, transpose_A=True)
                 T.gemm(p_s, dO_s, acc, transpose_A=True)
                 T.gemm(ds_s, Qt_s, acct, transpose_A=True)
-                for r, d in T.Parallel(block_I, D):
+                for c in list(range(NC)):  # trace-time unrolled: static sub-tile bounds
+                    T.copy(acc[:, c * block_C:(c + 1) * block_C], stage)
+                    for r, j in T.Parallel(block_I, block_C, coalesced_width=1):  # lane j -> column j
+                        if (idx_s[r] >= 0) & (idx_s[r] < SKV):
+                            T.atomic_add(dKV[bz, idx_s[r], 0, c * block_C + j], stage[r, j])
+                T.copy(acct, stage[:, 0:DT])
+                for r, j in T.Parallel(block_I, DT, coalesced_width=1):
                     if (idx_s[r] >= 0) & (idx_s[r] < SKV):
-                        T.atomic_add(dKV[bz, idx_s[r], 0, d], acc[r, d])
-                for r, d in T.Parallel(block_I, DT):
-                    if (idx_s[r] >= 0) & (idx_s[r] < SKV):
-                        T.atomic_add(dKV[bz, idx_s[r], 0, D + d], acct[r, d])
+                        T.atomic_add(dKV[bz, idx_s[r], 0, D + j], stage[r, j])
 
     return main
 
