@@ -117,8 +117,8 @@ def sparse_mla_bwd_dkv(B, S, SKV, H, D, DT, topk, block_I=32, block_C=64, thread
 
     The MFMA accumulator is scattered in ``block_C``-column slices staged through LDS so every
     wave-wide fp32 atomic covers 64 consecutive floats of ONE selected row (two cache lines);
-    atomics issued straight from the MFMA layout touch 16+ lines per instruction and were ~20x
-    slower."""
+    atomics issued straight from the MFMA layout touch 16+ lines per instruction (measured at the
+    reference shape: 61 ms -> 16 ms for this kernel)."""
     NI = topk // block_I
     assert D % block_C == 0 and DT <= block_C
     NC = D // block_C
