@@ -85,6 +85,9 @@ class JITImpl:
         f = self.fn(*args, **kwargs)
         if not isinstance(f, S.PrimFunc):
             raise TypeError(f"@tilelang.jit function {self.fn.__name__} must return a T.prim_func, got {type(f)}")
+        if f.name in ("main", "kernel", "func") and self.fn.__name__.isidentifier():
+            # kernels are named after the factory, so profiles (rocprofv3) tell them apart
+            f.name = self.fn.__name__
         return f
 
     def compile(self, *args, **kwargs) -> JITKernel:
