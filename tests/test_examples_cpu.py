@@ -432,3 +432,25 @@ def test_sparse_mla_bwd_cpu():
     for impl, args in ((m.sparse_mla_bwd_dq, (1, 64, 256, 64, 512, 64, 128)),
                        (m.sparse_mla_bwd_dkv, (1, 64, 256, 64, 512, 64, 128))):
         tilelang.compile(impl.get_tir(*args), out_idx=impl.out_idx, target="hip")
+
+
+def test_attention_sink_bwd_cpu():
+    import example_gqa_sink_bwd as m
+    fa = m.fa
+    B, S, H, G, D = 1, 128, 4, 2, 64
+    q, do = torch.randn(B, S, H, D).half(), torch.randn(B, S, H, D).half()
+    k, v = torch.randn(B, S, H // G, D).half(), torch.randn(B, S, H // G, D).half()
+    sinks = torch.randn(H)
+    o, lse = _both(fa.flashattn_fwd, B, H, S, D, True, 64, 64, groups=G)(q, k, v)
+    o2, lse2 = _both(m.sink_fixup, B, S, H, D, dtype="float16")(o, lse, sinks)
+    delta = _both(fa.flashattn_bwd_preprocess, B, H, S, D)(o2, do)
+    dq = _both(fa.flashattn_bwd_dq, B, H, S, D, True, 64, 64, 256, groups=G)(q, k, v, do, lse2, delta)
+    dk, dv = torch.empty_like(k), torch.empty_like(v)
+    f = fa.flashattn_bwd.get_tir(B, H, S, D, True, 64, 64, 256, dq_mode="none", groups=G)
+    tilelang.compile(f, target="cpu")(q, k, v, do, lse2, delta, dk, dv)
+    ds = _both(m.sink_grad, B, S, H)(lse2, delta, sinks)
+    qf, kf, vf, sf = [t.float().requires_grad_() for t in (q, k, v, sinks)]
+    ro = m.ref_program(qf, kf, vf, sf)
+    ro.backward(do.float())
+    for a, r in ((o2, ro.detach()), (dq, qf.grad), (dk, kf.grad), (dv, vf.grad), (ds, sf.grad)):
+        torch.testing.assert_close(a.float(), r, rtol=1e-2, atol=1e-2)

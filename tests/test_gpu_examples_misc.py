@@ -338,3 +338,20 @@ def test_sparse_mla_bwd_gpu():
     rq, rkv = m.ref_bwd(q, kv, do, idx)
     torch.testing.assert_close(dq.float().cpu(), rq, rtol=3e-2, atol=3e-2)
     torch.testing.assert_close(dkv.cpu(), rkv, rtol=3e-2, atol=3e-2)
+
+
+def test_attention_sink_autograd_gpu():
+    import example_gqa_sink_bwd as m
+    B, S, H, G, D = 2, 512, 8, 4, 64
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16).requires_grad_()
+    k = torch.randn(B, S, H // G, D, device="cuda", dtype=torch.bfloat16).requires_grad_()
+    v = torch.randn(B, S, H // G, D, device="cuda", dtype=torch.bfloat16).requires_grad_()
+    sinks = torch.randn(H, device="cuda").requires_grad_()
+    do = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+    m.attention_sink(q, k, v, sinks).backward(do)
+    grads = [t.grad.clone() for t in (q, k, v, sinks)]
+    for t in (q, k, v, sinks):
+        t.grad = None
+    m.ref_program(q, k, v, sinks).backward(do)
+    for g, t in zip(grads, (q, k, v, sinks)):
+        torch.testing.assert_close(g.float(), t.grad.float(), rtol=3e-2, atol=5e-2)
