@@ -1,0 +1,138 @@
+"""Variable-length (packed) FlashAttention forward (reference: examples/flash_attention/
+example_mha_fwd_varlen.py).
+
+Q [total_q, H, D] and K/V [total_k, H/G, D] hold the sequences of a batch back to back;
+``cu_seqlens_q/k`` [B+1] are their prefix offsets.  One block per (query tile of ``block_M``
+rows, head, sequence); tiles past a sequence's end exit early.  Token offsets are data
+dependent along the OUTERMOST (token) dim, so the K/V tiles remain LDS-DMA producers of
+``T.Pipelined`` (buffer resource over the packed tensor; rows of the next sequence are masked,
+rows past the tensor read zeros).  Causal masking is bottom-right aligned (q_len <= k_len).
+"""
+import argparse
+
+import tilelang
+import tilelang.language as T
+
+LOG2E = 1.44269504
+
+
+@tilelang.jit(out_idx=[5])
+def flashattn_varlen(batch, heads, total_q, total_k, max_seqlen_q, dim, is_causal=True, groups=1, block_M=128,
+                     block_N=64, threads=256, num_stages=2, dtype="bfloat16"):
+    scale = (1.0 / dim)**0.5 * LOG2E
+    head_kv = heads // groups
+    accum = "float"
+
+    @T.prim_func
+    def main(Q: T.Tensor([total_q, heads, dim], dtype), K: T.Tensor([total_k, head_kv, dim], dtype),
+             V: T.Tensor([total_k, head_kv, dim], dtype), cu_q: T.Tensor([batch + 1], "int32"),
+             cu_k: T.Tensor([batch + 1], "int32"), Output: T.Tensor([total_q, heads, dim], dtype)):
+        with T.Kernel(T.ceildiv(max_seqlen_q, block_M), heads, batch, threads=threads) as (bx, by, bz):
+            Q_s = T.alloc_shared([block_M, dim], dtype)
+            K_s = T.alloc_shared([block_N, dim], dtype)
+            V_s = T.alloc_shared([block_N, dim], dtype)
+            acc_s = T.alloc_fragment([block_M, block_N], accum)
+            acc_s_cast = T.alloc_fragment([block_M, block_N], dtype)
+            acc_o = T.alloc_fragment([block_M, dim], accum)
+            m = T.alloc_fragment([block_M], accum)
+            m_prev = T.alloc_fragment([block_M], accum)
+            alpha = T.alloc_fragment([block_M], accum)
+            l_sum = T.alloc_fragment([block_M], accum)
+            r_sum = T.alloc_fragment([block_M], accum)
+            o_cast = T.alloc_fragment([block_M, dim], dtype)
+            q0 = cu_q[bz]
+            k0 = cu_k[bz]
+            q_len = cu_q[bz + 1] - q0
+            k_len = cu_k[bz + 1] - k0
+            off = k_len - q_len  # bottom-right causal alignment
+            if bx * block_M < q_len:
+                T.copy(Q[q0 + bx * block_M:q0 + (bx + 1) * block_M, by, :], Q_s)
+                T.fill(acc_o, 0)
+                T.fill(l_sum, 0)
+                T.fill(m, -(2.0**30))
+                n_kv = T.ceildiv(T.min(k_len, (bx + 1) * block_M + off), block_N) if is_causal else \
+                    T.ceildiv(k_len, block_N)
+                for k in T.Pipelined(n_kv, num_stages=num_stages):
+                    T.copy(K[k0 + k * block_N:k0 + (k + 1) * block_N, by // groups, :], K_s)
+                    T.copy(V[k0 + k * block_N:k0 + (k + 1) * block_N, by // groups, :], V_s)
+                    for i, j in T.Parallel(block_M, block_N):
+                        ok = k * block_N + j < k_len
+                        if is_causal:
+                            ok = ok & (bx * block_M + i + off >= k * block_N + j)
+                        acc_s[i, j] = T.if_then_else(ok, 0, -T.infinity(accum))
+                    T.gemm(Q_s, K_s, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                    T.copy(m, m_prev)
+                    T.reduce_max(acc_s, m, dim=1, clear=False)
+                    for i in T.Parallel(block_M):
+                        alpha[i] = T.exp2((m_prev[i] - m[i]) * scale)
+                    for i, j in T.Parallel(block_M, dim):
+                        acc_o[i, j] *= alpha[i]
+                    for i, j in T.Parallel(block_M, block_N):
+                        acc_s[i, j] = T.exp2(acc_s[i, j] * scale - m[i] * scale)
+                    T.reduce_sum(acc_s, r_sum, dim=1)
+                    for i in T.Parallel(block_M):
+                        l_sum[i] = l_sum[i] * alpha[i] + r_sum[i]
+                    T.copy(acc_s, acc_s_cast)
+                    T.gemm(acc_s_cast, V_s, acc_o, policy=T.GemmWarpPolicy.FullRow)
+                for i, j in T.Parallel(block_M, dim):
+                    o_cast[i, j] = acc_o[i, j] / T.max(l_sum[i], 1e-30)
+                for i, j in T.Parallel(block_M, dim):
+                    if bx * block_M + i < q_len:
+                        Output[q0 + bx * block_M + i, by, j] = o_cast[i, j]
+
+    return main
+
+
+def ref_program(q, k, v, cu_q, cu_k, is_causal=True):
+    import torch
+    H = q.shape[1]
+    G = H // k.shape[1]
+    out = torch.zeros_like(q, dtype=torch.float32)
+    for b in range(len(cu_q) - 1):
+        qs, qe, ks, ke = int(cu_q[b]), int(cu_q[b + 1]), int(cu_k[b]), int(cu_k[b + 1])
+        qq = q[qs:qe].float().transpose(0, 1)
+        kk = k[ks:ke].float().repeat_interleave(G, 1).transpose(0, 1)
+        vv = v[ks:ke].float().repeat_interleave(G, 1).transpose(0, 1)
+        s = qq @ kk.transpose(-1, -2) * q.shape[-1]**-0.5
+        if is_causal:
+            lq, lk = qe - qs, ke - ks
+            mask = torch.arange(lq, device=q.device)[:, None] + (lk - lq) >= torch.arange(lk, device=q.device)[None, :]
+            s = s.masked_fill(~mask, float("-inf"))
+        out[qs:qe] = (torch.softmax(s, -1) @ vv).transpose(0, 1)
+    return out.to(q.dtype)
+
+
+def make_varlen(lens_q, lens_k, H, HKV, D, device="cpu", dtype=None):
+    import torch
+    dtype = dtype or torch.bfloat16
+    cu_q = torch.tensor([0] + list(torch.tensor(lens_q).cumsum(0)), dtype=torch.int32, device=device)
+    cu_k = torch.tensor([0] + list(torch.tensor(lens_k).cumsum(0)), dtype=torch.int32, device=device)
+    q = torch.randn(int(cu_q[-1]), H, D, device=device, dtype=dtype)
+    k = torch.randn(int(cu_k[-1]), HKV, D, device=device, dtype=dtype)
+    v = torch.randn(int(cu_k[-1]), HKV, D, device=device, dtype=dtype)
+    return q, k, v, cu_q, cu_k
+
+
+def main(B=8, max_len=4096, H=32, G=4, D=128):
+    import torch
+    g = torch.Generator().manual_seed(0)
+    lens = torch.randint(max_len // 4, max_len + 1, (B, ), generator=g).tolist()
+    q, k, v, cu_q, cu_k = make_varlen(lens, lens, H, H // G, D, "cuda")
+    kern = flashattn_varlen(B, H, q.shape[0], k.shape[0], max(lens), D, True, G)
+    o = kern(q, k, v, cu_q, cu_k)
+    n = int(cu_q[2])
+    torch.testing.assert_close(o[:n].float(), ref_program(q[:n], k[:n], v[:n], cu_q[:3], cu_k[:3]).float(),
+                               rtol=2e-2, atol=2e-2)
+    print("All checks pass.")
+    lat = kern.get_profiler().do_bench(lambda: kern(q, k, v, cu_q, cu_k))
+    flops = sum(2 * 2.0 * H * L * L * D * 0.5 for L in lens)
+    print(f"varlen causal attention B{B} lens {min(lens)}..{max(lens)} H{H} G{G}: {lat:.3f} ms, "
+          f"{flops / lat * 1e-9:.1f} TFLOPS")
+
+
+if __name__ == "__main__":
+    p = argparse.ArgumentParser()
+    p.add_argument("--batch", type=int, default=8)
+    p.add_argument("--max_len", type=int, default=4096)
+    a = p.parse_args()
+    main(a.batch, a.max_len)

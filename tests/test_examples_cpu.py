@@ -454,3 +454,13 @@ def test_attention_sink_bwd_cpu():
     ro.backward(do.float())
     for a, r in ((o2, ro.detach()), (dq, qf.grad), (dk, kf.grad), (dv, vf.grad), (ds, sf.grad)):
         torch.testing.assert_close(a.float(), r, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_varlen_cpu(causal):
+    from example_mha_fwd_varlen import flashattn_varlen, make_varlen, ref_program
+    q, k, v, cq, ck = make_varlen([37, 128, 5], [60, 128, 90], 4, 2, 64)
+    f = flashattn_varlen.get_tir(3, 4, q.shape[0], k.shape[0], 128, 64, causal, 2, 64, 32, 256)
+    tilelang.compile(f, out_idx=[5], target="hip")
+    o = tilelang.compile(f, out_idx=[5], target="cpu")(q, k, v, cq, ck)
+    torch.testing.assert_close(o.float(), ref_program(q, k, v, cq, ck, causal).float(), rtol=2e-2, atol=2e-2)

@@ -355,3 +355,10 @@ def test_attention_sink_autograd_gpu():
     m.ref_program(q, k, v, sinks).backward(do)
     for g, t in zip(grads, (q, k, v, sinks)):
         torch.testing.assert_close(g.float(), t.grad.float(), rtol=3e-2, atol=5e-2)
+
+
+def test_flash_attention_varlen_gpu():
+    from example_mha_fwd_varlen import flashattn_varlen, make_varlen, ref_program
+    q, k, v, cq, ck = make_varlen([300, 1024, 77, 513], [300, 1100, 200, 513], 8, 2, 128, "cuda")
+    o = flashattn_varlen(4, 8, q.shape[0], k.shape[0], 1024, 128, True, 4)(q, k, v, cq, ck)
+    torch.testing.assert_close(o.float(), ref_program(q, k, v, cq, ck).float(), rtol=2e-2, atol=2e-2)
