@@ -134,7 +134,7 @@ def main(B=1, S=4096, H=64, G=8, D=128):
     sinks = torch.randn(H, device="cuda", dtype=torch.float32).requires_grad_()
     do = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
     o = attention_sink(q, k, v, sinks)
-    o.backward(do)
+    o.backward(do, retain_graph=True)
     grads = [t.grad.clone() for t in (q, k, v, sinks)]
     for t in (q, k, v, sinks):
         t.grad = None

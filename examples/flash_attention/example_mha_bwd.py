@@ -26,61 +26,93 @@ LOG2E = 1.44269504
 
 
 @tilelang.jit(out_idx=[3, 4])
-def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=256, dtype="float16",
-                  groups=1):
+def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=256, block_N=64, threads=None, dtype="float16",
+                  groups=1, num_stages=2):
+    """Forward that also writes the base-2 LSE (the training forward).  Schedule as the sink
+    kernel (examples/attention_sink): heads on the fastest grid axis and the heaviest causal
+    query tiles first, KV tiles below the diagonal in an unmasked loop and the diagonal ones
+    in a masked loop, lazy O rescale, 8 waves x 32 rows."""
+    if threads is None:
+        threads = min(512, 64 * (block_M // 16))  # FullRow: >= 16 query rows per wave
     scale = (1.0 / dim)**0.5 * LOG2E
     shape = [batch, seq_len, heads, dim]
     kv_shape = [batch, seq_len, heads // groups, dim]
     accum_dtype = "float"
+    n_qt = (seq_len + block_M - 1) // block_M
+
+    @T.macro
+    def step(K, V, Q_shared, K_shared, V_shared, acc_s, acc_s_cast, acc_o, m, m_prev, alpha, r_sum, l_sum, k, qt,
+             by, bz, masked):
+        T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
+        T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
+        if masked:
+            for i, j in T.Parallel(block_M, block_N):
+                acc_s[i, j] = T.if_then_else(((qt * block_M + i >= k * block_N + j) | (not is_causal)) &
+                                             (k * block_N + j < seq_len), 0, -T.infinity(accum_dtype))
+        else:
+            T.clear(acc_s)
+        T.gemm(Q_shared, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+        T.copy(m, m_prev)
+        T.reduce_max(acc_s, m_prev, dim=1, clear=False)
+        rescale = T.alloc_var("int32")
+        rescale = 0
+        for i in T.Parallel(block_M):
+            if (m_prev[i] - m[i]) * scale > 8.0:
+                alpha[i] = T.exp2((m[i] - m_prev[i]) * scale)
+                m[i] = m_prev[i]
+                rescale = 1
+            else:
+                alpha[i] = 1.0
+        if rescale != 0:
+            for i, j in T.Parallel(block_M, dim):
+                acc_o[i, j] *= alpha[i]
+        for i, j in T.Parallel(block_M, block_N):
+            acc_s[i, j] = T.exp2(acc_s[i, j] * scale - m[i] * scale)
+        T.reduce_sum(acc_s, r_sum, dim=1)
+        for i in T.Parallel(block_M):
+            l_sum[i] = l_sum[i] * alpha[i] + r_sum[i]
+        T.copy(acc_s, acc_s_cast)
+        T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
 
     @T.prim_func
     def flash_fwd(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
                   Output: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype)):
-        with T.Kernel(T.ceildiv(seq_len, block_M), heads, batch, threads=threads) as (bx, by, bz):
+        with T.Kernel(heads, n_qt, batch, threads=threads) as (by, bx, bz):
             Q_shared = T.alloc_shared([block_M, dim], dtype)
             K_shared = T.alloc_shared([block_N, dim], dtype)
             V_shared = T.alloc_shared([block_N, dim], dtype)
             acc_s = T.alloc_fragment([block_M, block_N], accum_dtype)
             acc_s_cast = T.alloc_fragment([block_M, block_N], dtype)
             acc_o = T.alloc_fragment([block_M, dim], accum_dtype)
-            scores_max = T.alloc_fragment([block_M], accum_dtype)
-            scores_max_prev = T.alloc_fragment([block_M], accum_dtype)
-            scores_scale = T.alloc_fragment([block_M], accum_dtype)
-            scores_sum = T.alloc_fragment([block_M], accum_dtype)
-            logsum = T.alloc_fragment([block_M], accum_dtype)
-            T.copy(Q[bz, bx * block_M:(bx + 1) * block_M, by, :], Q_shared)
+            o_cast = T.alloc_fragment([block_M, dim], dtype)
+            m = T.alloc_fragment([block_M], accum_dtype)
+            m_prev = T.alloc_fragment([block_M], accum_dtype)
+            alpha = T.alloc_fragment([block_M], accum_dtype)
+            r_sum = T.alloc_fragment([block_M], accum_dtype)
+            l_sum = T.alloc_fragment([block_M], accum_dtype)
+            qt = (n_qt - 1 - bx) if is_causal else bx  # heaviest causal tiles first
+            T.copy(Q[bz, qt * block_M:(qt + 1) * block_M, by, :], Q_shared)
             T.fill(acc_o, 0)
-            T.fill(logsum, 0)
-            T.fill(scores_max, -T.infinity(accum_dtype))
-            loop_range = T.ceildiv((bx + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N)
-            for k in T.Pipelined(loop_range, num_stages=2):
-                T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
-                if is_causal:
-                    for i, j in T.Parallel(block_M, block_N):
-                        acc_s[i, j] = T.if_then_else(bx * block_M + i >= k * block_N + j, 0, -T.infinity(accum_dtype))
-                else:
-                    T.clear(acc_s)
-                T.gemm(Q_shared, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
-                T.copy(scores_max, scores_max_prev)
-                T.reduce_max(acc_s, scores_max, dim=1, clear=False)
-                for i in T.Parallel(block_M):
-                    scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
-                for i, j in T.Parallel(block_M, dim):
-                    acc_o[i, j] *= scores_scale[i]
-                for i, j in T.Parallel(block_M, block_N):
-                    acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
-                T.reduce_sum(acc_s, scores_sum, dim=1)
-                for i in T.Parallel(block_M):
-                    logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
-                T.copy(acc_s, acc_s_cast)
-                T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
+            T.fill(l_sum, 0)
+            T.fill(m, -(2.0**30))
+            if is_causal:
+                end = T.min(T.ceildiv(seq_len, block_N), T.ceildiv((qt + 1) * block_M, block_N))
+                full_end = T.min((qt * block_M + 1) // block_N, end)
+            else:
+                end = T.ceildiv(seq_len, block_N)
+                full_end = seq_len // block_N
+            for k in T.Pipelined(full_end, num_stages=num_stages):
+                step(K, V, Q_shared, K_shared, V_shared, acc_s, acc_s_cast, acc_o, m, m_prev, alpha, r_sum, l_sum, k,
+                     qt, by, bz, False)
+            for k in T.Pipelined(full_end, end, num_stages=num_stages):
+                step(K, V, Q_shared, K_shared, V_shared, acc_s, acc_s_cast, acc_o, m, m_prev, alpha, r_sum, l_sum, k,
+                     qt, by, bz, True)
             for i, j in T.Parallel(block_M, dim):
-                acc_o[i, j] /= logsum[i]
-            T.copy(acc_o, Output[bz, bx * block_M:(bx + 1) * block_M, by, :])
+                o_cast[i, j] = acc_o[i, j] / l_sum[i]
+            T.copy(o_cast, Output[bz, qt * block_M:(qt + 1) * block_M, by, :])
             for i in T.Parallel(block_M):
-                logsum[i] = T.log2(logsum[i]) + scores_max[i] * scale
-            T.copy(logsum, lse[bz, by, bx * block_M:(bx + 1) * block_M])
+                l_sum[i] = T.log2(l_sum[i]) + m[i] * scale
+            T.copy(l_sum, lse[bz, by, qt * block_M:(qt + 1) * block_M])
 
     return flash_fwd
 

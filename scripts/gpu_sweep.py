@@ -101,6 +101,29 @@ def w_fa_fwd(c):
     return do_bench(lambda: k(q, k_, v)), 4.0 * B * H * S * S * D * (0.5 if causal else 1.0)
 
 
+def w_fa_fwd_lse(c):
+    import example_mha_bwd as m
+    B, H, S, D, G = 1, 64, 4096, 128, 8
+    q = torch.randn(B, S, H, D, dtype=torch.bfloat16, device="cuda")
+    k_, v = [torch.randn(B, S, H // G, D, dtype=torch.bfloat16, device="cuda") for _ in range(2)]
+    k = m.flashattn_fwd(B, H, S, D, True, dtype="bfloat16", groups=G, **c)
+    o, _ = k(q, k_, v)
+    torch.testing.assert_close(o[:, :256].float(), m.ref_program(q[:, :256], k_[:, :256], v[:, :256], True).float(),
+                               rtol=2e-2, atol=2e-2)
+    return do_bench(lambda: k(q, k_, v)), 4.0 * B * H * S * S * D * 0.5
+
+
+def w_varlen(c):
+    import example_mha_fwd_varlen as m
+    B, L, H, G, D = 8, 4096, 32, 4, 128
+    g = torch.Generator().manual_seed(0)
+    lens = torch.randint(L // 4, L + 1, (B, ), generator=g).tolist()
+    q, k_, v, cq, ck = m.make_varlen(lens, lens, H, H // G, D, "cuda")
+    k = m.flashattn_varlen(B, H, q.shape[0], k_.shape[0], max(lens), D, True, G, **c)
+    k(q, k_, v, cq, ck)
+    return do_bench(lambda: k(q, k_, v, cq, ck)), sum(2 * 2.0 * H * x * x * D * 0.5 for x in lens)
+
+
 def w_sink_lazy(c):
     return w_sink(c)
 
