@@ -1,0 +1,108 @@
+"""Chunked retention (RetNet) forward (reference: examples/linear_attention/example_retention_fwd.py:9-83).
+
+O_t = scale * sum_{s<=t} gamma_h^(t-s) (q_t . k_s) v_s,   gamma_h = 1 - 2^(-5-h)
+
+Same CDNA4 schedule as the linear-attention example: one block per (value tile, batch*head) walks
+the chunks in order with the full-DK state H [DK, BV] resident in fp32 registers (no NK split, so
+the reference's cross-block ``o.sum(0)`` postprocess disappears):
+
+    S   = Q_c K_c^T,  masked and decayed by gamma^(i-j) in registers -> register-A MFMA with V_c
+    O_c = scale * (D S) V_c + scale * gamma^(i+1) * Q_c H
+    H   = gamma^L H + K_c^T (gamma^(L-1-j) V_c)      (decayed V_c written once into LDS)
+"""
+import argparse
+
+import tilelang
+import tilelang.language as T
+
+
+@tilelang.jit(out_idx=[3])
+def chunk_retention_fwd(B, S, H, DK, DV, chunk_size=64, BV=64, threads=256, dtype="float16", scale=None):
+    if scale is None:
+        scale = DK**-0.5
+    accum_dtype = "float"
+    assert S % chunk_size == 0 and DV % BV == 0
+    NT = S // chunk_size
+
+    @T.prim_func
+    def main(Q: T.Tensor([B, S, H, DK], dtype), K: T.Tensor([B, S, H, DK], dtype), V: T.Tensor([B, S, H, DV], dtype),
+             O: T.Tensor([B, S, H, DV], dtype)):
+        with T.Kernel(DV // BV, B * H, threads=threads) as (i_v, i_bh):
+            i_b = i_bh // H
+            i_h = i_bh % H
+            log_decay = T.alloc_var(accum_dtype)
+            log_decay = T.log2(1.0 - T.exp2(-5.0 - T.Cast(accum_dtype, i_h)))
+            q = T.alloc_shared([chunk_size, DK], dtype)
+            k = T.alloc_shared([chunk_size, DK], dtype)
+            v = T.alloc_shared([chunk_size, BV], dtype)
+            vw = T.alloc_shared([chunk_size, BV], dtype)
+            h_shared = T.alloc_shared([DK, BV], dtype)
+            h = T.alloc_fragment([DK, BV], accum_dtype)
+            s = T.alloc_fragment([chunk_size, chunk_size], accum_dtype)
+            s_cast = T.alloc_fragment([chunk_size, chunk_size], dtype)
+            o = T.alloc_fragment([chunk_size, BV], accum_dtype)
+            o_inter = T.alloc_fragment([chunk_size, BV], accum_dtype)
+            o_cast = T.alloc_fragment([chunk_size, BV], dtype)
+            T.clear(h)
+            for c in T.Pipelined(NT, num_stages=2):
+                T.copy(Q[i_b, c * chunk_size:(c + 1) * chunk_size, i_h, :], q)
+                T.copy(K[i_b, c * chunk_size:(c + 1) * chunk_size, i_h, :], k)
+                T.copy(V[i_b, c * chunk_size:(c + 1) * chunk_size, i_h, i_v * BV:(i_v + 1) * BV], v)
+                T.clear(s)
+                T.gemm(q, k, s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                for i, j in T.Parallel(chunk_size, chunk_size):
+                    s_cast[i, j] = T.if_then_else(i >= j, s[i, j] * (T.exp2(T.Cast(accum_dtype, i - j) * log_decay) *
+                                                                     scale), 0)
+                T.clear(o)
+                T.gemm(s_cast, v, o, policy=T.GemmWarpPolicy.FullRow)
+                T.copy(h, h_shared)
+                T.clear(o_inter)
+                T.gemm(q, h_shared, o_inter, policy=T.GemmWarpPolicy.FullRow)
+                for i, j in T.Parallel(chunk_size, BV):
+                    o_cast[i, j] = o[i, j] + o_inter[i, j] * (T.exp2(T.Cast(accum_dtype, i + 1) * log_decay) * scale)
+                T.copy(o_cast, O[i_b, c * chunk_size:(c + 1) * chunk_size, i_h, i_v * BV:(i_v + 1) * BV])
+                for i, j in T.Parallel(chunk_size, BV):
+                    vw[i, j] = v[i, j] * T.exp2(T.Cast(accum_dtype, chunk_size - 1 - i) * log_decay)
+                for i, j in T.Parallel(DK, BV):
+                    h[i, j] *= T.exp2(chunk_size * log_decay)
+                T.gemm(k, vw, h, transpose_A=True)
+
+    return main
+
+
+def ref_program(q, k, v, scale=None):
+    import torch
+    q, k, v = q.float(), k.float(), v.float()
+    _, S, H, D = q.shape
+    scale = D**-0.5 if scale is None else scale
+    gamma = 1.0 - torch.exp2(-5.0 - torch.arange(H, dtype=torch.float32, device=q.device))
+    t = torch.arange(S, device=q.device, dtype=torch.float32)
+    dist = (t[:, None] - t[None, :])
+    decay = torch.where(dist >= 0, gamma[:, None, None]**dist.clamp(min=0), torch.zeros((), device=q.device))
+    att = torch.einsum("bshd,bthd->bhst", q * scale, k) * decay[None]
+    return torch.einsum("bhst,bthd->bshd", att, v)
+
+
+def main(B=8, S=4096, H=32, D=128):
+    import torch
+    kernel = chunk_retention_fwd(B, S, H, D, D)
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.float16)
+    k = torch.randn(B, S, H, D, device="cuda", dtype=torch.float16)
+    v = torch.randn(B, S, H, D, device="cuda", dtype=torch.float16)
+    o = kernel(q, k, v)
+    ro = ref_program(q[:1, :1024], k[:1, :1024], v[:1, :1024])
+    torch.testing.assert_close(o[:1, :1024].float(), ro, rtol=2e-2, atol=5e-2)
+    print("All checks pass.")
+    lat = kernel.get_profiler().do_bench(lambda: kernel(q, k, v))
+    flops = 2.0 * B * S * S * H * D  # the reference's (causal) count, example_retention_fwd.py:98
+    print(f"retention fwd b{B} s{S} h{H} d{D}: {lat:.3f} ms, {flops / lat * 1e-9:.1f} TFLOPS")
+
+
+if __name__ == "__main__":
+    p = argparse.ArgumentParser()
+    p.add_argument("--B", type=int, default=8)
+    p.add_argument("--S", type=int, default=4096)
+    p.add_argument("--H", type=int, default=32)
+    p.add_argument("--D", type=int, default=128)
+    a = p.parse_args()
+    main(a.B, a.S, a.H, a.D)

@@ -14,6 +14,7 @@ def runtime():
     global _rt
     if _rt is None:
         try:
+            import torch  # noqa: F401  (loads libc10_hip.so, which the extension links against)
             from . import _tl_runtime as m  # noqa: F401
         except ImportError as e:
             raise NativeRuntimeMissing(
