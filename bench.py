@@ -1,18 +1,30 @@
 #!/usr/bin/env python3
-"""Headline benchmark: achieved TFLOPS of the tilelang fp16 GEMM 4096^3 + MHA fwd seqlen 4096.
+"""Headline benchmark: achieved TFLOPS of fp16 GEMM 4096^3 + MHA seqlen 4096 + the config-5 MoE.
 
 BASELINE.json metric: "achieved TFLOPS: fp16 GEMM 4096^3 and MHA seqlen=4096; % of MFMA roofline".
-One *step* = one fp16 GEMM (M=N=K=4096) + one FlashAttention-2 forward (bf16, batch 1, 64 heads,
-seqlen 4096, head_dim 128), both compiled by tilelang from the DSL programs in examples/.
-Weak scaling: every rank (one process per GPU, RCCL/torch.distributed for the barriers and the
-max-over-ranks timing) runs one step's work; ``value`` is the whole-job aggregate TFLOPS.
+One *step* on every rank (one process per GPU) =
+  1. fp16 GEMM M=N=K=4096                                   (BASELINE config 2)
+  2. FlashAttention-2 forward bf16, b1 h64 s4096 d128        (BASELINE config 3)
+  3. MoE FFN layer, 8 SwiGLU experts, top-2, hidden 4096, expert ffn 2048, 2048 tokens/rank,
+     experts sharded over the ranks (expert parallel): the routed tokens travel to their
+     experts' GPU and back with two RCCL all-to-alls over xGMI (BASELINE config 5)
+all three compiled by tilelang from the DSL programs in examples/ and tilelang/ops.
+Weak scaling: per-rank work is fixed as N grows; ``value`` is the whole-job aggregate TFLOPS
+(useful FLOPs of all N ranks / the max-over-ranks wall time of the timed steps).
 
     python bench.py --gpus N --steps K --warmup W
-    (N>1 is launched by torch.distributed.run; rank/world come from the environment)
+    (--gpus N>1 without a torchrun environment re-launches itself under torch.distributed.run
+     as a CHILD process before touching the GPU; under torchrun WORLD_SIZE must equal N)
+
+``vs_baseline``: the reference's time for the same per-rank work at its published rates
+(736 TF fp16 GEMM; 497.13 TF attention; the MoE grouped GEMMs are priced at the
+GEMM rate, the reference publishes no MoE number) divided by our time.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -21,6 +33,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "examples", "gemm"))
 sys.path.insert(0, os.path.join(ROOT, "examples", "flash_attention"))
 
+METRIC = "achieved TFLOPS: fp16 GEMM 4096^3 and MHA seqlen=4096; % of MFMA roofline"
 # reference numbers: fp16 GEMM 736 TFLOPS (H800, 8192x8192x4096);
 # attention fwd bf16 hd128 seq4096 497.13 TFLOPS (H800, GQA+sink b1 h64 kvh8)
 REF_GEMM_TF = 736.0
@@ -29,6 +42,67 @@ PEAK_BF16_TF = 2500.0  # MI355X dense fp16/bf16 MFMA (AMD spec, no sparsity)
 
 GEMM_CFG = dict(M=4096, N=4096, K=4096, block_M=256, block_N=256, block_K=64, threads=512, num_stages=2)
 ATTN_CFG = dict(batch=1, heads=64, seq_len=4096, dim=128, block_M=256, block_N=64, threads=512, num_stages=2)
+MOE_CFG = dict(tokens=2048, hidden=4096, ffn=2048, experts=8, topk=2)
+# --device cpu (CI plumbing run on the CPU target under gloo): same program, tiny shapes
+TINY = dict(gemm=dict(M=128, N=128, K=128, block_M=64, block_N=64, block_K=32, threads=128, num_stages=2),
+            attn=dict(batch=1, heads=2, seq_len=128, dim=64, block_M=64, block_N=32, threads=128, num_stages=2),
+            moe=dict(tokens=32, hidden=64, ffn=64, experts=8, topk=2))
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch(args) -> int:
+    """Run this script under torch.distributed.run with one rank per GPU (child process)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def _target(device):
+    return "cpu" if device == "cpu" else "hip"
+
+
+def build_gemm(device="cuda", g=None):
+    import torch
+    import tilelang
+    from example_gemm import matmul
+    g = g or GEMM_CFG
+    f = matmul.get_tir(g["M"], g["N"], g["K"], g["block_M"], g["block_N"], g["block_K"], g["threads"],
+                       g["num_stages"], "float16")
+    k = tilelang.compile(f, out_idx=[-1], target=_target(device))
+    A = torch.randn(g["M"], g["K"], device=device).to(torch.float16)
+    B = torch.randn(g["K"], g["N"], device=device).to(torch.float16)
+    return k, (A, B)
+
+
+def build_attn(device="cuda", a=None):
+    import torch
+    import tilelang
+    from example_mha_fwd import flashattn
+    a = a or ATTN_CFG
+    f = flashattn.get_tir(a["batch"], a["heads"], a["seq_len"], a["dim"], False, 1, a["block_M"], a["block_N"],
+                          a["threads"], a["num_stages"], "bfloat16")
+    k = tilelang.compile(f, out_idx=[3], target=_target(device), pass_configs=flashattn.pass_configs)
+    shp = (a["batch"], a["seq_len"], a["heads"], a["dim"])
+    return k, tuple(torch.randn(shp, device=device).to(torch.bfloat16) for _ in range(3))
+
+
+def build_moe(mesh, device="cuda", m=None):
+    import torch
+    from tilelang.models.moe import MoEConfig, MoELayer
+    m = m or MOE_CFG
+    dt = torch.bfloat16 if device != "cpu" else torch.float32
+    bm = 128 if device != "cpu" else 16
+    cfg = MoEConfig(hidden=m["hidden"], ffn=m["ffn"], n_experts=m["experts"], topk=m["topk"], dtype=dt, block_M=bm)
+    layer = MoELayer(cfg, "ep" if mesh is not None else "local", mesh=mesh, device=device)
+    x = torch.randn(m["tokens"], m["hidden"], device=device).to(dt)
+    return layer, x
 
 
 def main():
@@ -36,92 +110,118 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-moe", action="store_true", help="time GEMM + attention only")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: tiny shapes on the CPU target under gloo (CI plumbing check)")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(relaunch(args))
+    world = int(env_world or 1)
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+
     import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    cpu = args.device == "cpu"
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
+    if not cpu:
+        torch.cuda.set_device(local_rank)
     dist = None
+    mesh = None
     if world > 1:
         import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        if cpu:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        world = dist.get_world_size()
+        from tilelang.parallel import init_mesh
+        mesh = init_mesh(1, world)
+    dev = "cpu" if cpu else "cuda"
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
 
-    from example_gemm import matmul
-    from example_mha_fwd import flashattn
-
-    g = GEMM_CFG
-    gemm = matmul(g["M"], g["N"], g["K"], g["block_M"], g["block_N"], g["block_K"], g["threads"], g["num_stages"],
-                  "float16")
-    a_ = ATTN_CFG
-    attn = flashattn(a_["batch"], a_["heads"], a_["seq_len"], a_["dim"], False, 1, a_["block_M"], a_["block_N"],
-                     a_["threads"], a_["num_stages"], "bfloat16")
-
-    torch.manual_seed(1234 + rank)
-    A = torch.randn(g["M"], g["K"], device="cuda", dtype=torch.float16)
-    B = torch.randn(g["K"], g["N"], device="cuda", dtype=torch.float16)
-    C = torch.empty(g["M"], g["N"], device="cuda", dtype=torch.float16)
-    shp = (a_["batch"], a_["seq_len"], a_["heads"], a_["dim"])
-    Q = torch.randn(shp, device="cuda", dtype=torch.bfloat16)
-    Kt = torch.randn(shp, device="cuda", dtype=torch.bfloat16)
-    V = torch.randn(shp, device="cuda", dtype=torch.bfloat16)
+    torch.manual_seed(1234)  # identical expert weights on every rank (EP slices them)
+    g, a_, m = (TINY["gemm"], TINY["attn"], TINY["moe"]) if cpu else (GEMM_CFG, ATTN_CFG, MOE_CFG)
+    gemm, (A, B) = build_gemm(dev, g)
+    attn, (Q, K, V) = build_attn(dev, a_)
+    moe = None
+    if not args.no_moe:
+        moe, X = build_moe(mesh, dev, m)
+        torch.manual_seed(1234 + rank)
+        X = torch.randn_like(X.float()).to(X.dtype)  # every rank brings its own tokens
 
     # correctness guard (cheap spot check so a broken kernel cannot post a number)
     C = gemm(A, B)
-    ref = (A[:256].float() @ B.float())
-    if not torch.allclose(C[:256].float(), ref, rtol=2e-2, atol=2e-1):
+    ref = A[:64].float() @ B.float()
+    if not torch.allclose(C[:64].float(), ref, rtol=2e-2, atol=2e-1):
         raise SystemExit("GEMM result check failed")
 
     gemm_flops = 2.0 * g["M"] * g["N"] * g["K"]
-    attn_flops = 4.0 * a_["batch"] * a_["heads"] * a_["seq_len"] ** 2 * a_["dim"]
+    attn_flops = 4.0 * a_["batch"] * a_["heads"] * a_["seq_len"]**2 * a_["dim"]
+    moe_flops = 0.0 if moe is None else 6.0 * m["tokens"] * m["topk"] * m["hidden"] * m["ffn"]
 
     def step():
         gemm(A, B)
-        attn(Q, Kt, V)
+        attn(Q, K, V)
+        if moe is not None:
+            moe(X)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
 
-    # per-kernel times (events) for the report, measured after the timed region
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    ev[0].record()
-    for _ in range(10):
-        gemm(A, B)
-    ev[1].record()
-    for _ in range(10):
-        attn(Q, Kt, V)
-    ev[2].record()
-    torch.cuda.synchronize()
-    gemm_ms = ev[0].elapsed_time(ev[1]) / 10
-    attn_ms = ev[1].elapsed_time(ev[2]) / 10
+    # per-phase times, measured after the timed region (MoE includes its all-to-alls)
+    def timed(fn, n):
+        sync()
+        if dist is not None:
+            dist.barrier()
+        t = time.perf_counter()
+        for _ in range(n):
+            fn()
+        sync()
+        return (time.perf_counter() - t) / n * 1e3
 
-    t = torch.tensor([elapsed, gemm_ms, attn_ms], device="cuda", dtype=torch.float64)
+    reps = 2 if cpu else 10
+    gemm_ms = timed(lambda: gemm(A, B), reps)
+    attn_ms = timed(lambda: attn(Q, K, V), reps)
+    moe_ms = timed(lambda: moe(X), reps) if moe is not None else 0.0
+    moe_comm_ms = 0.0
+    if moe is not None and mesh is not None:
+        # the two all-to-alls alone (same byte counts as the layer's dispatch + return)
+        from tilelang.parallel import collectives as Cl
+        rows = X.shape[0] * m["topk"]
+        per = [rows // world] * world
+        per[-1] += rows - sum(per)
+        payload = torch.randn(rows, m["hidden"], device=dev).to(X.dtype)
+        moe_comm_ms = timed(lambda: (Cl.all_to_all_v(payload, per), Cl.all_to_all_v(payload, per)), reps)
+
+    t = torch.tensor([elapsed, gemm_ms, attn_ms, moe_ms, moe_comm_ms], dtype=torch.float64,
+                     device="cpu" if cpu else "cuda")
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, gemm_ms, attn_ms = t.tolist()
+    elapsed, gemm_ms, attn_ms, moe_ms, moe_comm_ms = t.tolist()
     ms_per_step = elapsed / args.steps * 1e3
-    total_flops = (gemm_flops + attn_flops) * world * args.steps
-    tflops = total_flops / elapsed / 1e12
-    # the reference's time for the same per-GPU work at its published rates
-    ref_step_s = gemm_flops / (REF_GEMM_TF * 1e12) + attn_flops / (REF_ATTN_TF * 1e12)
-    ref_tflops = (gemm_flops + attn_flops) / ref_step_s / 1e12 * world
+    step_flops = gemm_flops + attn_flops + moe_flops
+    tflops = step_flops * world * args.steps / elapsed / 1e12
+    # the reference's time for the same per-rank work at its published rates
+    ref_step_s = (gemm_flops + moe_flops) / (REF_GEMM_TF * 1e12) + attn_flops / (REF_ATTN_TF * 1e12)
+    ref_tflops = step_flops / ref_step_s / 1e12 * world
     if rank == 0:
         out = {
-            "metric": "achieved TFLOPS: fp16 GEMM 4096^3 and MHA seqlen=4096; % of MFMA roofline",
+            "metric": METRIC,
             "value": round(tflops, 2),
             "unit": "TFLOPS",
             "n_gpus": world,
@@ -132,20 +232,30 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(tflops / ref_tflops, 4),
             "dtype": "bf16",
-            "data": "synthetic (torch.randn)",
+            "data": "synthetic (torch.randn inputs, random-init expert weights)",
             "config": {
-                "model": "fp16 GEMM 4096x4096x4096 + FlashAttention-2 fwd bf16 b1 h64 s4096 d128",
+                "model": (f"fp16 GEMM {g['M']}x{g['N']}x{g['K']} + FlashAttention-2 fwd bf16 b{a_['batch']} "
+                          f"h{a_['heads']} s{a_['seq_len']} d{a_['dim']}"
+                          + ("" if moe is None else f" + MoE FFN {m['experts']} experts top-{m['topk']} "
+                             f"h{m['hidden']} f{m['ffn']} {m['tokens']} tok/rank (EP)")),
                 "global_batch": world,
                 "seq_len": a_["seq_len"],
-                "parallelism": f"dp{world}",
+                "parallelism": (f"dp{world}" if moe is None or world == 1 else f"dp{world}+ep{world}"),
             },
             "gemm_tflops": round(gemm_flops / gemm_ms / 1e9, 1),
             "attn_tflops": round(attn_flops / attn_ms / 1e9, 1),
+            "moe_tflops_per_gpu": round(moe_flops / moe_ms / 1e9, 1) if moe is not None else None,
+            "moe_comm_fraction": round(moe_comm_ms / moe_ms, 3) if moe is not None and moe_ms > 0 else None,
             "pct_of_mfma_peak": round(100.0 * tflops / world / PEAK_BF16_TF, 1),
             "gemm_dtype": "float16",
             "attn_dtype": "bfloat16",
+            "moe_dtype": "bfloat16",
+            "device": args.device,
         }
         print(json.dumps(out), flush=True)
+    if mesh is not None:
+        from tilelang.parallel import shutdown_mesh
+        shutdown_mesh()
     if dist is not None:
         dist.destroy_process_group()
 

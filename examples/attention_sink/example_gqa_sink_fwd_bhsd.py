@@ -21,10 +21,14 @@ from typing import Optional
 import tilelang
 import tilelang.language as T
 
+# exp/exp2 on the hardware transcendental unit (v_exp_f32): differs from the precise
+# OCML expansion only for results below 2^-126, which softmax/decay terms never need
+FAST_MATH = {tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True}
+
 LOG2E = 1.44269504
 
 
-@tilelang.jit(out_idx=[3])
+@tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
 def flashattn_sink(batch, heads, seq_q, seq_kv, dim, groups=1, window_size=None, sm_scale=None, block_M=256,
                    block_N=64, num_stages=2, threads=512, dtype="bfloat16", causal=True, lazy_rescale=True):
     """``lazy_rescale``: rows keep their running max until a score exceeds it by 2^8 (O is

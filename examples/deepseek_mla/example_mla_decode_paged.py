@@ -14,8 +14,12 @@ import argparse
 import tilelang
 import tilelang.language as T
 
+# exp/exp2 on the hardware transcendental unit (v_exp_f32): differs from the precise
+# OCML expansion only for results below 2^-126, which softmax/decay terms never need
+FAST_MATH = {tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True}
 
-@tilelang.jit(out_idx=[8])
+
+@tilelang.jit(out_idx=[8], pass_configs=FAST_MATH)
 def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe_dim=64, block_N=64, block_H=64,
                      num_split=4, threads=None, num_stages=2, dtype="bfloat16", wide=None):
     if wide is None:

@@ -20,10 +20,14 @@ import argparse
 import tilelang
 import tilelang.language as T
 
+# exp/exp2 on the hardware transcendental unit (v_exp_f32): differs from the precise
+# OCML expansion only for results below 2^-126, which softmax/decay terms never need
+FAST_MATH = {tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True}
+
 LOG2E = 1.44269504
 
 
-@tilelang.jit(out_idx=[2])
+@tilelang.jit(out_idx=[2], pass_configs=FAST_MATH)
 def sparse_mla_bwd_preprocess(B, S, H, D=512, block=32, dtype="bfloat16"):
     """Delta[b, s, h] = sum_d O * dO."""
 
@@ -44,7 +48,7 @@ def sparse_mla_bwd_preprocess(B, S, H, D=512, block=32, dtype="bfloat16"):
     return main
 
 
-@tilelang.jit(out_idx=[6, 7, 8])
+@tilelang.jit(out_idx=[6, 7, 8], pass_configs=FAST_MATH)
 def sparse_mla_bwd_dq(B, S, SKV, H, D, DT, topk, sm_scale=None, block_I=32, num_stages=2, dtype="bfloat16"):
     """Q is read from LDS (not registers) and KV tiles are 32 rows: with dO (64) and the dQ
     accumulator (144 registers per lane) that fits the register file without spilling."""
@@ -111,7 +115,7 @@ def sparse_mla_bwd_dq(B, S, SKV, H, D, DT, topk, sm_scale=None, block_I=32, num_
     return main
 
 
-@tilelang.jit
+@tilelang.jit(pass_configs=FAST_MATH)
 def sparse_mla_bwd_dkv(B, S, SKV, H, D, DT, topk, block_I=32, block_C=64, threads=256, dtype="bfloat16"):
     """dKV[b, idx, 0, :] += dS^T Q (+ P^T dO on [0, D)); dKV is fp32 and zeroed by the caller.
 

@@ -22,10 +22,14 @@ import argparse
 import tilelang
 import tilelang.language as T
 
+# exp/exp2 on the hardware transcendental unit (v_exp_f32): differs from the precise
+# OCML expansion only for results below 2^-126, which softmax/decay terms never need
+FAST_MATH = {tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True}
+
 LOG2E = 1.44269504
 
 
-@tilelang.jit(out_idx=[3, 4])
+@tilelang.jit(out_idx=[3, 4], pass_configs=FAST_MATH)
 def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=256, block_N=64, threads=None, dtype="float16",
                   groups=1, num_stages=2):
     """Forward that also writes the base-2 LSE (the training forward).  Schedule as the sink
@@ -117,7 +121,7 @@ def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=256, block_N=64
     return flash_fwd
 
 
-@tilelang.jit(out_idx=[2])
+@tilelang.jit(out_idx=[2], pass_configs=FAST_MATH)
 def flashattn_bwd_preprocess(batch, heads, seq_len, dim, blk=32, threads=256, dtype="float16"):
     shape = [batch, seq_len, heads, dim]
 
@@ -139,7 +143,7 @@ def flashattn_bwd_preprocess(batch, heads, seq_len, dim, blk=32, threads=256, dt
     return flash_bwd_prep
 
 
-@tilelang.jit(out_idx=[1])
+@tilelang.jit(out_idx=[1], pass_configs=FAST_MATH)
 def flashattn_bwd_postprocess(batch, heads, seq_len, dim, blk=64, threads=256, dtype="float16"):
     shape = [batch, seq_len, heads, dim]
 
@@ -155,7 +159,7 @@ def flashattn_bwd_postprocess(batch, heads, seq_len, dim, blk=64, threads=256, d
     return flash_bwd_post
 
 
-@tilelang.jit
+@tilelang.jit(pass_configs=FAST_MATH)
 def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=512, num_stages=2,
                   dtype="float16", dq_mode="atomic", groups=1):
     """``dq_mode``: "atomic" (fp32 atomics into dQ, one kernel) or "none" (dK/dV only; dQ comes from
@@ -248,7 +252,7 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
     return flash_bwd
 
 
-@tilelang.jit(out_idx=[6])
+@tilelang.jit(out_idx=[6], pass_configs=FAST_MATH)
 def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=256, num_stages=2,
                      dtype="float16", groups=1):
     """dQ without atomics: one block per (query tile, head, batch) walks the KV tiles, recomputing

@@ -19,10 +19,14 @@ import functools
 import tilelang
 import tilelang.language as T
 
+# exp/exp2 on the hardware transcendental unit (v_exp_f32): differs from the precise
+# OCML expansion only for results below 2^-126, which softmax/decay terms never need
+FAST_MATH = {tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True}
+
 LOG2E = 1.44269504
 
 
-@tilelang.jit(out_idx=[1])
+@tilelang.jit(out_idx=[1], pass_configs=FAST_MATH)
 def chunk_cumsum(B, S, H, C=64, threads=64):
     """g [B, S, H] fp32 -> within-chunk inclusive cumulative sum."""
 
@@ -40,7 +44,7 @@ def chunk_cumsum(B, S, H, C=64, threads=64):
     return main
 
 
-@tilelang.jit(out_idx=[3])
+@tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
 def chunk_scaled_dot_kkt(B, S, H, DK, C=64, threads=256, dtype="bfloat16"):
     """A[b, s, h, t] = beta_s (k_s . k_t) exp(g_s - g_t) for t < s within each chunk (fp32)."""
 
@@ -66,7 +70,7 @@ def chunk_scaled_dot_kkt(B, S, H, DK, C=64, threads=256, dtype="bfloat16"):
     return main
 
 
-@tilelang.jit(out_idx=[1])
+@tilelang.jit(out_idx=[1], pass_configs=FAST_MATH)
 def solve_tril(B, S, H, C=64):
     """Tm = (I + A)^-1 per chunk (A strictly lower) by forward substitution.  One thread per
     column keeps its whole column of Tm in registers (fully unrolled, constant indices); the
@@ -94,7 +98,7 @@ def solve_tril(B, S, H, C=64):
     return main
 
 
-@tilelang.jit(out_idx=[5, 6])
+@tilelang.jit(out_idx=[5, 6], pass_configs=FAST_MATH)
 def wy_fast(B, S, H, DK, DV, C=64, threads=256, dtype="bfloat16"):
     """w = Tm (beta exp(g) k), u = Tm (beta v) per chunk."""
 
@@ -125,7 +129,7 @@ def wy_fast(B, S, H, DK, DV, C=64, threads=256, dtype="bfloat16"):
     return main
 
 
-@tilelang.jit(out_idx=[4, 5, 6])
+@tilelang.jit(out_idx=[4, 5, 6], pass_configs=FAST_MATH)
 def chunk_delta_h(B, S, H, DK, DV, C=64, block_DV=16, threads=256, dtype="bfloat16"):
     """Sequential chunk recurrence: h_c (state before chunk c) [B, NT, H, DK, DV], v_new, final h."""
     NT = S // C
@@ -168,7 +172,7 @@ def chunk_delta_h(B, S, H, DK, DV, C=64, block_DV=16, threads=256, dtype="bfloat
     return main
 
 
-@tilelang.jit(out_idx=[5])
+@tilelang.jit(out_idx=[5], pass_configs=FAST_MATH)
 def chunk_o(B, S, H, DK, DV, C=64, scale=None, threads=256, dtype="bfloat16"):
     """o = scale [exp(g) q h_c + tril(q k^T exp(g_s - g_t)) v_new] per chunk."""
     NT = S // C
