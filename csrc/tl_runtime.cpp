@@ -58,6 +58,7 @@ struct Param {
   std::vector<Dim> strides; // buffers (empty = contiguous)
   bool is_output;
   int sym;                  // dyn: symbol id
+  int64_t max_elems;        // buffers addressed with 32-bit offsets: numel must stay below (0 = any)
 };
 
 // postfix program: op codes
@@ -127,6 +128,7 @@ class Kernel {
       p.is_float = d["is_float"].cast<bool>();
       p.is_output = d["is_output"].cast<bool>();
       p.sym = d["sym"].cast<int>();
+      p.max_elems = d.contains("max_elems") ? d["max_elems"].cast<int64_t>() : 0;
       for (auto s : d["shape"].cast<py::list>()) {
         auto t = s.cast<std::pair<bool, int64_t>>();
         p.shape.push_back({t.first, t.second});
@@ -147,6 +149,21 @@ class Kernel {
   }
 
   void set_validate(bool v) { validate_ = v; }
+  // kernels with a grid-wide barrier: cooperative launch (the runtime refuses grids that do not
+  // fit on the device at once, instead of a barrier that never completes)
+  void set_cooperative(bool v) { cooperative_ = v; }
+  int64_t max_resident_blocks() {
+    if (is_cpu_) return 1 << 30;
+    int per_cu = 0;
+    int64_t threads = 1;
+    for (auto b : block_) threads *= b;
+    TL_HIP_CHECK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func_, (int)threads, 0));
+    int dev = 0;
+    TL_HIP_CHECK(hipGetDevice(&dev));
+    hipDeviceProp_t prop;
+    TL_HIP_CHECK(hipGetDeviceProperties(&prop, dev));
+    return (int64_t)per_cu * prop.multiProcessorCount;
+  }
 
   // args: the non-output buffers/scalars in signature order
   py::object call(py::args args) {
@@ -188,6 +205,9 @@ class Kernel {
       if (is_cpu_) opts = opts.device(at::kCPU);
       else opts = opts.device(at::Device(at::kCUDA, device < 0 ? c10::hip::current_device() : device));
       at::Tensor t = at::empty(shape, opts);
+      if (p.max_elems > 0 && t.numel() >= p.max_elems)
+        throw py::value_error(label_ + ": output '" + p.name + "' would have " + std::to_string(t.numel()) +
+                              " elements; the kernel was compiled with 32-bit offsets for it");
       tensors[i] = t;
       outs.push_back(py::reinterpret_steal<py::object>(THPVariable_Wrap(t)));
     }
@@ -209,6 +229,9 @@ class Kernel {
         if (v < 0) throw py::value_error(label_ + ": dynamic symbol '" + p.name + "' is not bound by any tensor");
         if (p.nbytes == 8) std::memcpy(&storage[i], &v, 8);
         else {
+          if (v > INT32_MAX)
+            throw py::value_error(label_ + ": dynamic symbol '" + p.name + "' = " + std::to_string(v) +
+                                  " does not fit the kernel's int32 argument");
           int32_t v32 = (int32_t)v;
           std::memcpy(&storage[i], &v32, 4);
         }
@@ -286,6 +309,12 @@ class Kernel {
         }
       }
     }
+    if (p.max_elems > 0 && t.numel() >= p.max_elems) {
+      std::ostringstream os;
+      os << label_ << ": argument '" << p.name << "' has " << t.numel() << " elements; the kernel was compiled with "
+         << "32-bit offsets for it (recompile with pass_configs={'tl.config_index_bitwidth': 64})";
+      throw py::value_error(os.str());
+    }
     if (validate_) {
       if (p.strides.empty()) {
         if (!t.is_contiguous()) throw py::value_error(label_ + ": argument '" + p.name + "' must be contiguous");
@@ -345,6 +374,11 @@ class Kernel {
     int64_t bx = block_.size() > 0 ? block_[0] : 1, by = block_.size() > 1 ? block_[1] : 1,
             bz = block_.size() > 2 ? block_[2] : 1;
     hipStream_t stream = c10::hip::getCurrentHIPStream(device < 0 ? -1 : (c10::DeviceIndex)device).stream();
+    if (cooperative_) {
+      TL_HIP_CHECK(hipModuleLaunchCooperativeKernel(func_, (unsigned)gx, (unsigned)gy, (unsigned)gz, (unsigned)bx,
+                                                    (unsigned)by, (unsigned)bz, 0, stream, ptrs));
+      return;
+    }
     TL_HIP_CHECK(hipModuleLaunchKernel(func_, (unsigned)gx, (unsigned)gy, (unsigned)gz, (unsigned)bx, (unsigned)by,
                                        (unsigned)bz, 0, stream, ptrs, nullptr));
   }
@@ -363,6 +397,7 @@ class Kernel {
   std::vector<Param> params_;
   int n_inputs_ = 0;
   bool validate_ = true;
+  bool cooperative_ = false;
 };
 
 py::dict device_info(int dev) {
@@ -462,7 +497,9 @@ PYBIND11_MODULE(_tl_runtime, m) {
       .def("__call__", &Kernel::call)
       .def("grid_for", &Kernel::grid_for)
       .def("lds_bytes", &Kernel::lds_bytes)
-      .def("set_validate", &Kernel::set_validate);
+      .def("set_validate", &Kernel::set_validate)
+      .def("set_cooperative", &Kernel::set_cooperative)
+      .def("max_resident_blocks", &Kernel::max_resident_blocks);
   m.def("device_info", &device_info);
   m.def("scalar_type_of", [](py::handle t) {
     if (!THPVariable_Check(t.ptr())) throw py::type_error("expected a tensor");

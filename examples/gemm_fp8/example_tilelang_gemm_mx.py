@@ -1,0 +1,117 @@
+"""Block-scaled MX GEMM (OCP MXFP8 / MXFP4) on the gfx950 scaled matrix cores.
+
+``T.gemm_scaled`` lowers to ``v_mfma_scale_f32_16x16x128_f8f6f4``: the hardware multiplies every
+32-element K block of each row of A and B by its e8m0 scale (2^(s-127)) inside the MFMA, so the
+MX tensors are consumed as stored — no dequantisation pass.  Peak rates (dense): fp8 ~5 PF,
+fp4 ~10 PF (4x bf16).  Operands are K-contiguous: A ``[M, K]`` and B ``[N, K]`` bytes (fp8), or
+``[M, K/2]`` / ``[N, K/2]`` packed e2m1 pairs (low nibble = even element); scales ``[M, K/32]``,
+``[N, K/32]`` read straight from global memory (a few bytes per 32 K per lane; L1/L2 resident).
+
+The reference has no MX path (its AMD fp8 GEMM is CDNA3 fnuz, ``examples/gemm_fp8/
+example_tilelang_gemm_amd.py``; its MXFP4 example dequantises to bf16,
+``examples/dequantize_gemm/example_dequant_gemm_bf16_mxfp4_hopper.py``).
+"""
+import argparse
+
+import tilelang
+import tilelang.language as T
+
+_DT = {"e4m3": "float8_e4m3fn", "e5m2": "float8_e5m2", "e2m1": "uint8"}
+
+
+@tilelang.jit(out_idx=[-1])
+def mx_matmul(M, N, K, block_M=256, block_N=256, block_K=None, threads=512, num_stages=2, a_fmt="e4m3",
+              b_fmt="e4m3", out_dtype="bfloat16", accum_dtype="float", panel=8):
+    if block_K is None:  # 64 KiB of operand bytes per pipeline stage
+        block_K = 256 if a_fmt == b_fmt == "e2m1" else 128
+    ac = K // 2 if a_fmt == "e2m1" else K
+    bc = K // 2 if b_fmt == "e2m1" else K
+    bka = block_K // 2 if a_fmt == "e2m1" else block_K
+    bkb = block_K // 2 if b_fmt == "e2m1" else block_K
+    sk = block_K // 32
+
+    @T.prim_func
+    def main(
+            A: T.Tensor((M, ac), _DT[a_fmt]),
+            B: T.Tensor((N, bc), _DT[b_fmt]),
+            SA: T.Tensor((M, K // 32), "uint8"),
+            SB: T.Tensor((N, K // 32), "uint8"),
+            C: T.Tensor((M, N), out_dtype),
+    ):
+        with T.Kernel(T.ceildiv(N, block_N), T.ceildiv(M, block_M), threads=threads) as (bx, by):
+            A_s = T.alloc_shared((block_M, bka), _DT[a_fmt])
+            B_s = T.alloc_shared((block_N, bkb), _DT[b_fmt])
+            C_l = T.alloc_fragment((block_M, block_N), accum_dtype)
+            T.use_swizzle(panel_size=panel)
+            T.clear(C_l)
+            for k in T.Pipelined(T.ceildiv(K, block_K), num_stages=num_stages):
+                T.copy(A[by * block_M, k * bka], A_s)
+                T.copy(B[bx * block_N, k * bkb], B_s)
+                T.gemm_scaled(A_s, B_s, C_l, SA[by * block_M:(by + 1) * block_M, k * sk:(k + 1) * sk],
+                              SB[bx * block_N:(bx + 1) * block_N, k * sk:(k + 1) * sk], transpose_B=True,
+                              a_format=a_fmt, b_format=b_fmt)
+            T.copy(C_l, C[by * block_M, bx * block_N])
+
+    return main
+
+
+E2M1 = [0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0, -0.0, -0.5, -1.0, -1.5, -2.0, -3.0, -4.0, -6.0]
+
+
+def quantize(x, fmt):
+    """fp32 [R, K] -> (MX elements as stored, e8m0 scales [R, K/32]) with per-block power-of-2 scales."""
+    import torch
+    R, K = x.shape
+    blk = x.float().reshape(R, K // 32, 32)
+    amax = blk.abs().amax(-1).clamp(min=1e-30)
+    vmax = {"e4m3": 448.0, "e5m2": 57344.0, "e2m1": 6.0}[fmt]  # largest representable element
+    e = torch.ceil(torch.log2(amax / vmax))
+    s = (e + 127).clamp(0, 254).to(torch.uint8)
+    q = blk / torch.exp2(s.float() - 127).unsqueeze(-1)
+    q = q.reshape(R, K)
+    if fmt == "e4m3":
+        return q.to(torch.float8_e4m3fn), s
+    if fmt == "e5m2":
+        return q.to(torch.float8_e5m2), s
+    lut = torch.tensor(E2M1[:8], device=x.device)
+    mag = (q.abs().unsqueeze(-1) - lut).abs().argmin(-1)
+    code = (mag | ((q < 0).long() << 3)).to(torch.uint8)
+    return (code[:, 0::2] | (code[:, 1::2] << 4)).contiguous(), s
+
+
+def dequantize(q, s, fmt):
+    import torch
+    if fmt == "e2m1":
+        lut = torch.tensor(E2M1, device=q.device)
+        lo, hi = (q & 15).long(), (q >> 4).long()
+        v = torch.stack([lut[lo], lut[hi]], -1).reshape(q.shape[0], -1)
+    else:
+        v = q.float()
+    return v * torch.exp2(s.float() - 127).repeat_interleave(32, 1)
+
+
+def ref_program(a, b, sa, sb, a_fmt, b_fmt):
+    return dequantize(a, sa, a_fmt) @ dequantize(b, sb, b_fmt).t()
+
+
+def main(M=8192, N=8192, K=8192, a_fmt="e4m3", b_fmt="e4m3"):
+    import torch
+    kernel = mx_matmul(M, N, K, a_fmt=a_fmt, b_fmt=b_fmt)
+    a, sa = quantize(torch.randn(M, K, device="cuda") * 3, a_fmt)
+    b, sb = quantize(torch.randn(N, K, device="cuda") * 0.2, b_fmt)
+    c = kernel(a, b, sa, sb)
+    ref = ref_program(a, b, sa, sb, a_fmt, b_fmt)
+    torch.testing.assert_close(c.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+    lat = kernel.get_profiler().do_bench(lambda: kernel(a, b, sa, sb))
+    print(f"MX {a_fmt}x{b_fmt} gemm {M}x{N}x{K}: {lat:.3f} ms, {2 * M * N * K / lat * 1e-9:.1f} TFLOPS")
+
+
+if __name__ == "__main__":
+    p = argparse.ArgumentParser()
+    p.add_argument("--m", type=int, default=8192)
+    p.add_argument("--n", type=int, default=8192)
+    p.add_argument("--k", type=int, default=8192)
+    p.add_argument("--a_fmt", default="e4m3")
+    p.add_argument("--b_fmt", default="e4m3")
+    a = p.parse_args()
+    main(a.m, a.n, a.k, a.a_fmt, a.b_fmt)

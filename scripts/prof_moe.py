@@ -1,4 +1,7 @@
-"""Run the bench.py MoE layer (local, 1 GPU) N times for rocprofv3 --kernel-trace --stats."""
+"""Time the bench.py MoE layer (local, 1 GPU); optional sweep of the expert GEMM tile.
+
+    python scripts/prof_moe.py [reps] [--sweep]
+"""
 import os
 import sys
 
@@ -8,18 +11,43 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-layer, x = bench.build_moe(None, "cuda")
-for _ in range(3):
-    layer(x)
-torch.cuda.synchronize()
-e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-e0.record()
-for _ in range(reps):
-    layer(x)
-e1.record()
-torch.cuda.synchronize()
-ms = e0.elapsed_time(e1) / reps
+reps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 10
 m = bench.MOE_CFG
 fl = 6.0 * m["tokens"] * m["topk"] * m["hidden"] * m["ffn"]
-print(f"moe layer {ms * 1e3:.1f} us = {fl / ms * 1e-9:.1f} TF", flush=True)
+
+
+def run(layer, x, tag):
+    for _ in range(3):
+        layer(x)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        layer(x)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    print(f"{tag}: moe layer {ms * 1e3:.1f} us = {fl / ms * 1e-9:.1f} TF", flush=True)
+
+
+layer, x = bench.build_moe(None, "cuda")
+from tilelang.models.moe import moe_reference, init_moe_weights  # noqa: E402
+
+run(layer, x, "default " + str(layer.cfg.gemm_cfg))
+if "--check" in sys.argv:
+    out = layer(x).float()
+    ref = moe_reference(x, layer.gate_w, layer.w1, layer.w2, layer.cfg.topk)
+    print("max abs err", (out - ref).abs().max().item(), "ref max", ref.abs().max().item(), flush=True)
+if "--sweep" in sys.argv:
+    for bm in (128, 256):
+        for cfg in (dict(block_N=128, block_K=64, num_stages=2, threads=256),
+                    dict(block_N=256, block_K=64, num_stages=2, threads=512),
+                    dict(block_N=256, block_K=64, num_stages=3, threads=512),
+                    dict(block_N=128, block_K=64, num_stages=3, threads=256),
+                    dict(block_N=256, block_K=32, num_stages=4, threads=512)):
+            try:
+                layer.cfg.block_M = bm
+                layer.cfg.gemm_cfg = cfg
+                run(layer, x, f"bm{bm} {cfg}")
+            except Exception as e:  # noqa: BLE001
+                print(f"bm{bm} {cfg}: failed {type(e).__name__}: {str(e)[:200]}", flush=True)

@@ -1,0 +1,86 @@
+"""T.print / T.sync_warp / T.sync_grid lower to real code (reference language/print.py,
+builtin.py:676-701): printed values are checked on the CPU target; the grid barrier is checked
+on the GPU (cooperative launch, every block sees every other block's pre-barrier writes)."""
+import pytest
+import torch
+
+import tilelang
+import tilelang.language as T
+
+
+def print_kernel():
+
+    @T.prim_func
+    def main(A: T.Tensor((4, ), "float32"), B: T.Tensor((4, ), "float32")):
+        with T.Kernel(1, threads=64):
+            S = T.alloc_shared((4, ), "float32")
+            T.copy(A, S)
+            T.print(S, msg="shared")
+            T.print(A[2], msg="scalar")
+            T.sync_warp()
+            T.copy(S, B)
+
+    return main
+
+
+def test_print_cpu(capfd):
+    k = tilelang.compile(print_kernel(), target="cpu")
+    a = torch.tensor([1.5, 2.5, 3.5, 4.5])
+    b = torch.zeros(4)
+    k(a, b)
+    out = capfd.readouterr().out
+    assert "shared S[3] = 4.5" in out and "scalar: 3.5" in out
+    assert torch.equal(a, b)
+
+
+def test_print_and_sync_hip_codegen():
+    k = tilelang.compile(print_kernel(), target="hip")
+    src = k.get_kernel_source()
+    assert "tl::print_buffer" in src and "tl::print_val" in src and "tl::sync_warp()" in src
+    assert len(k.code[0]) > 0
+
+
+def grid_sync_kernel(nb, threads=256):
+
+    @T.prim_func
+    def main(X: T.Tensor((nb, ), "int32"), Y: T.Tensor((nb, ), "int32")):
+        with T.Kernel(nb, threads=threads) as bx:
+            for z in T.Parallel(1):
+                X[bx + z] = bx + 1
+            T.sync_grid()
+            for z in T.Parallel(1):
+                # every block reads its neighbour's pre-barrier write
+                Y[bx + z] = X[(bx + 1) % nb]
+
+    return main
+
+
+def test_grid_sync_codegen():
+    k = tilelang.compile(grid_sync_kernel(64), target="hip")
+    assert "tl::sync_grid()" in k.get_kernel_source()
+    assert k.artifact.kernels[0].cooperative
+
+
+@pytest.mark.gpu
+def test_grid_sync_gpu():
+    nb = 256
+    k = tilelang.compile(grid_sync_kernel(nb), target="hip")
+    for _ in range(3):
+        x = torch.zeros(nb, dtype=torch.int32, device="cuda")
+        y = torch.zeros(nb, dtype=torch.int32, device="cuda")
+        k(x, y)
+        torch.cuda.synchronize()
+        exp = (torch.arange(nb, device="cuda") + 1) % nb + 1
+        assert torch.equal(y, exp.to(torch.int32))
+
+
+@pytest.mark.gpu
+def test_print_gpu(capfd):
+    k = tilelang.compile(print_kernel(), target="hip")
+    a = torch.tensor([1.5, 2.5, 3.5, 4.5], device="cuda")
+    b = torch.zeros(4, device="cuda")
+    k(a, b)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    out = capfd.readouterr().out
+    assert "S[3]" in out

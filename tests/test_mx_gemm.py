@@ -1,0 +1,64 @@
+"""Block-scaled MX GEMM (T.gemm_scaled -> v_mfma_scale_f32_16x16x128_f8f6f4) against an fp32 PyTorch
+dequantise-then-matmul reference, with non-unit e8m0 scales (MXFP8 e4m3/e5m2, MXFP4 e2m1, mixed)."""
+import pytest
+import torch
+
+import tilelang
+
+FMTS = [("e4m3", "e4m3"), ("e2m1", "e2m1"), ("e4m3", "e2m1"), ("e5m2", "e4m3")]
+
+
+def _check(c, a, b, sa, sb, af, bf):
+    import example_tilelang_gemm_mx as m
+    ref = m.ref_program(a.cpu(), b.cpu(), sa.cpu(), sb.cpu(), af, bf)
+    torch.testing.assert_close(c.float().cpu(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("af,bf", FMTS)
+def test_mx_gemm_cpu(af, bf):
+    import example_tilelang_gemm_mx as m
+    M = N = 64
+    K = 256
+    f = m.mx_matmul.get_tir(M, N, K, 64, 64, 128, 128, 2, af, bf)
+    k = tilelang.compile(f, out_idx=[-1], target="cpu")
+    a, sa = m.quantize(torch.randn(M, K) * 3, af)
+    b, sb = m.quantize(torch.randn(N, K) * 0.2, bf)
+    assert len(set(sa.flatten().tolist())) > 1  # genuinely non-unit, varying scales
+    _check(k(a, b, sa, sb), a, b, sa, sb, af, bf)
+    kh = tilelang.compile(f, out_idx=[-1], target="hip")
+    src = kh.get_kernel_source()
+    assert "gemm_ss_mx" in src and len(kh.code[0]) > 0
+
+
+def test_mx_gemm_rejects_bad_scales():
+    import example_tilelang_gemm_mx as m
+    import tilelang.language as T
+
+    @T.prim_func
+    def bad(A: T.Tensor((64, 128), "float8_e4m3fn"), B: T.Tensor((64, 128), "float8_e4m3fn"),
+            SA: T.Tensor((64, 8), "uint8"), SB: T.Tensor((64, 4), "uint8"), C: T.Tensor((64, 64), "float32")):
+        with T.Kernel(1, threads=256):
+            A_s = T.alloc_shared((64, 128), "float8_e4m3fn")
+            B_s = T.alloc_shared((64, 128), "float8_e4m3fn")
+            C_l = T.alloc_fragment((64, 64), "float32")
+            T.copy(A, A_s)
+            T.copy(B, B_s)
+            T.clear(C_l)
+            T.gemm_scaled(A_s, B_s, C_l, SA, SB, transpose_B=True)
+            T.copy(C_l, C)
+
+    with pytest.raises(Exception, match="scales must be"):
+        tilelang.compile(bad, target="hip")
+    assert m is not None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("af,bf", FMTS)
+def test_mx_gemm_gpu(af, bf):
+    import example_tilelang_gemm_mx as m
+    M, N, K = 512, 512, 1024
+    k = m.mx_matmul(M, N, K, 256, 256, 128, 512, 2, af, bf)
+    a, sa = m.quantize(torch.randn(M, K, device="cuda") * 3, af)
+    b, sb = m.quantize(torch.randn(N, K, device="cuda") * 0.2, bf)
+    assert len(set(sa.flatten().tolist())) > 1
+    _check(k(a, b, sa, sb), a, b, sa, sb, af, bf)

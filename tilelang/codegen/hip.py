@@ -245,6 +245,10 @@ class CodeGen:
             return "tl::sync_threads()" if self.is_cpu else "__syncthreads()"
         if op == "tl.fence":
             return "tl::fence_agent()"
+        if op == "tl.sync_warp":
+            return "tl::sync_warp()"
+        if op == "tl.sync_grid":
+            return "tl::sync_grid()"
         raise CodeGenError(f"unknown intrinsic {op}")
 
     def buf_ref(self, b: Buffer) -> str:

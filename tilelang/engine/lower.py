@@ -33,6 +33,7 @@ from ..transform.lower_tile_op import lower_tile_ops
 from ..transform.thread_sync import insert_thread_sync
 from ..transform.lds_plan import plan_lds
 from ..codegen.hip import generate, KernelSource
+from ..transform.pass_config import validate_pass_configs
 
 
 @dataclass
@@ -46,6 +47,8 @@ class DeviceKernel:
     lowered_ir: Optional[S.Stmt] = None
     layout_info: Dict[str, str] = field(default_factory=dict)
     mesh: Optional[dict] = None   # T.comm kernels: mesh shape, op count, workspace bytes
+    narrow_index: set = field(default_factory=set)  # global params addressed with int32 offsets
+    cooperative: bool = False     # uses T.sync_grid: launched cooperatively (all blocks resident)
 
 
 @dataclass
@@ -113,6 +116,9 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
                          f"CDNA wavefront")
     T = kernel.num_threads if target.kind == "hip" else 1
     semantic_check(func, kernel)
+    if cfg.get("tl.force_let_inline"):
+        from ..transform.let_inline import inline_lets
+        kernel = inline_lets(kernel)
     t = time.perf_counter()
     li = infer_layouts(S.PrimFunc(func.name, func.params, kernel, func.attrs), T, target)
     timings["layout_inference"] = timings.get("layout_inference", 0) + time.perf_counter() - t
@@ -124,20 +130,25 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
     timings["lower_tile_op"] = timings.get("lower_tile_op", 0) + time.perf_counter() - t
     if target.kind == "hip" and not cfg.get("tl.disable_thread_storage_sync", False):
         lk = insert_thread_sync(lk)
-    offsets, total = plan_lds(lk)
+    lk, offsets, total = plan_lds(lk, reuse=bool(cfg.get("tl.lds_reuse", True)),
+                                  aggressive=bool(cfg.get("tl.enable_aggressive_shared_memory_merge", False)))
+    if cfg.get("tl.layout_visualization_enable"):
+        from ..analysis.layout_visual import dump_layouts
+        dump_layouts(name, li, cfg.get("tl.layout_visualization_formats") or "txt")
     t = time.perf_counter()
     ks: KernelSource = generate(func, lk, target, offsets, total, name, cfg)
     timings["codegen"] = timings.get("codegen", 0) + time.perf_counter() - t
     layout_info = {b.name: repr(lay) for b, lay in li.frag.items()}
     return DeviceKernel(ks.source, ks.kernel_name, ks.grid, ks.block, ks.lds_bytes, ks.params, lk, layout_info,
-                        lk.attrs.get("mesh"))
+                        lk.attrs.get("mesh"), set(lk.attrs.get("narrow_index", ())),
+                        bool(lk.attrs.get("cooperative", False)))
 
 
 def lower(func: S.PrimFunc, target="auto", target_host=None, pass_configs: Optional[dict] = None,
           enable_host_codegen=False, enable_device_compile=False, runtime_only=False) -> CompiledArtifact:
     t0 = time.perf_counter()
     target = determine_target(target)
-    cfg = {str(k): v for k, v in dict(pass_configs or {}).items()}
+    cfg = validate_pass_configs({str(k): v for k, v in dict(pass_configs or {}).items()})
     kernels = _find_kernels(func.body)
     if any(k.is_cpu for k in kernels) and target.kind != "cpu":
         target = Target("cpu", "host", target.mesh)

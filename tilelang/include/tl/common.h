@@ -90,6 +90,50 @@ TL_DEVICE void barrier_raw() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Wave-level barrier (reference T.sync_warp): the 64 lanes of a wave issue in lockstep, so this
+// only has to order memory (LDS / global) among the wave's lanes and stop the compiler from
+// moving accesses across it.
+TL_DEVICE void sync_warp() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Grid-wide barrier (reference T.sync_grid / sync_global).  Needs every workgroup of the grid
+// resident at once: the launcher uses hipModuleLaunchCooperativeKernel for kernels that call it,
+// which refuses grids larger than the device can hold.  Sense-reversing counter barrier with
+// agent-scope release/acquire (MI355X guide, Guideline 16: per-XCD L2s are not coherent):
+// lane 0 of every workgroup publishes with a release fence, arrives, and the last arriver resets
+// the count and bumps the generation the others poll (relaxed loads + s_sleep, bounded).
+__device__ unsigned int tl_grid_bar_count = 0;
+__device__ unsigned int tl_grid_bar_gen = 0;
+TL_DEVICE void sync_grid() {
+  __syncthreads();
+  if (threadIdx.x == 0 && threadIdx.y == 0 && threadIdx.z == 0) {
+    const unsigned nblocks = gridDim.x * gridDim.y * gridDim.z;
+    const unsigned gen = __hip_atomic_load(&tl_grid_bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned arrived =
+        __hip_atomic_fetch_add(&tl_grid_bar_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    if (arrived == nblocks) {
+      __hip_atomic_store(&tl_grid_bar_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&tl_grid_bar_gen, gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      // bounded spin (~seconds): a grid that is not fully resident must not hang the device
+      for (long it = 0; it < (1l << 26); ++it) {
+        if (__hip_atomic_load(&tl_grid_bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
 template <int N> TL_DEVICE void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

@@ -4,6 +4,7 @@
 // line half.hpp); host clang provides _Float16 and __bf16 natively.
 #pragma once
 #include <math.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <string.h>
 #include <cmath>
@@ -129,6 +130,21 @@ template <typename T, int N> inline void load_vec(T (&vals)[N], const T* src) { 
 template <int B> inline void copy_bytes(void* dst, const void* src) { memcpy(dst, src, B); }
 
 inline void sync_threads() {}
+inline void sync_warp() {}
+inline void sync_grid() {}  // CPU target: blocks run one after another (no co-residency)
+inline void print_val(const char* msg, double v) { printf("%s: %g\n", msg, v); fflush(stdout); }
+inline void print_val(const char* msg, float v) { print_val(msg, (double)v); }
+inline void print_val(const char* msg, half_t v) { print_val(msg, (double)(float)v); }
+inline void print_val(const char* msg, bfloat16_t v) { print_val(msg, (double)(float)v); }
+inline void print_val(const char* msg, long long v) { printf("%s: %lld\n", msg, v); fflush(stdout); }
+inline void print_val(const char* msg, long v) { print_val(msg, (long long)v); }
+inline void print_val(const char* msg, int v) { print_val(msg, (long long)v); }
+inline void print_val(const char* msg, unsigned v) { print_val(msg, (long long)v); }
+inline void print_val(const char* msg, bool v) { print_val(msg, (long long)v); }
+template <typename T> inline void print_buffer(const char* msg, const char* name, const T* buf, int n) {
+  for (int i = 0; i < n; ++i) printf("%s %s[%d] = %g\n", msg, name, i, (double)(float)buf[i]);
+  fflush(stdout);
+}
 inline void barrier_raw() {}
 template <int N> inline void wait_vmcnt() {}
 
@@ -157,6 +173,45 @@ inline void cpu_gemm(const T* A, const T* B, float* C) {
         const float b = TB ? (float)B[j * B_COLS + k] : (float)B[k * B_COLS + j];
         C[i * N + j] += a * b;
       }
+    }
+}
+
+// OCP MX element decode (FMT: 0 e4m3, 1 e5m2, 4 e2m1 packed two per byte, low nibble first)
+template <int FMT> inline float mx_elem(const uint8_t* row, int k) {
+  if constexpr (FMT == 0) {
+    fp8_e4_t v;
+    v.v = row[k];
+    return (float)v;
+  } else if constexpr (FMT == 1) {
+    fp8_e5_t v;
+    v.v = row[k];
+    return (float)v;
+  } else {
+    static const float lut[8] = {0.0f, 0.5f, 1.0f, 1.5f, 2.0f, 3.0f, 4.0f, 6.0f};
+    const uint8_t nib = (row[k >> 1] >> (4 * (k & 1))) & 15;
+    return (nib & 8 ? -1.0f : 1.0f) * lut[nib & 7];
+  }
+}
+
+inline float e8m0(uint8_t s) { return s == 255 ? NAN : std::ldexp(1.0f, (int)s - 127); }
+
+// C[M][N] += sum_k (A[m][k] * 2^(SA[m][k/32]-127)) * (B[n][k] * 2^(SB[n][k/32]-127))
+template <int FA, int FB, int M, int N, int K, int A_COLS, int B_COLS, int SA_STRIDE, int SB_STRIDE>
+inline void cpu_gemm_mx(const void* A_, const void* B_, const void* SA_, const void* SB_, float* C) {
+  const uint8_t* A = (const uint8_t*)A_;
+  const uint8_t* B = (const uint8_t*)B_;
+  const uint8_t* SA = (const uint8_t*)SA_;
+  const uint8_t* SB = (const uint8_t*)SB_;
+  for (int i = 0; i < M; ++i)
+    for (int j = 0; j < N; ++j) {
+      float acc = 0.0f;
+      for (int kb = 0; kb < K / 32; ++kb) {
+        float part = 0.0f;
+        for (int k = kb * 32; k < kb * 32 + 32; ++k)
+          part += mx_elem<FA>(A + i * A_COLS, k) * mx_elem<FB>(B + j * B_COLS, k);
+        acc += part * e8m0(SA[i * SA_STRIDE + kb]) * e8m0(SB[j * SB_STRIDE + kb]);
+      }
+      C[i * N + j] += acc;
     }
 }
 

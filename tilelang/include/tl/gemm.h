@@ -248,3 +248,78 @@ TL_DEVICE void gemm_ss_f8(const TA* __restrict__ A_, const TB* __restrict__ B_, 
 }
 
 }  // namespace tl
+
+namespace tl {
+
+// ---------------------------------------------------------------------------
+// Block-scaled MX GEMM (OCP MX: one e8m0 scale per 32 K of each row), both operands
+// K-contiguous byte tiles in LDS: fp8 rows hold K bytes, packed fp4 rows K/2 bytes.
+// v_mfma_scale_f32_16x16x128_f8f6f4, lane l = (row r = l&15, group g = l>>4), one 128-K step,
+// measured on gfx950 with exact data and per-lane scales (csrc/probes/mfma_scale_probe.hip):
+//   fp8 : bytes 0-15 of the lane are k = 16g..16g+15, bytes 16-31 are k = 64+16g..64+16g+15;
+//   fp4 : the 16 bytes are k = 32g..32g+31 (low nibble = even k);
+//   scale: lane l's e8m0 byte (bits 7:0, opsel 0) scales K block g = k 32g..32g+31 of row r.
+//   For fp8 block g therefore spans bytes 0-15 (g < 2) or 16-31 (g >= 2) of lane groups 2(g&1)
+//   and 2(g&1)+1, not the scale lane's own bytes: the data is fetched in the hardware K order
+//   above (two 16-byte reads at 16g and 64+16g) so contiguous MX blocks line up with the scales.
+// FMT codes: 0 e4m3, 1 e5m2, 4 e2m1.  Operands are swapped at issue like gemm_ss.
+// ---------------------------------------------------------------------------
+template <int FMT> struct mx_fmt { static constexpr int lane_bytes = FMT == 4 ? 16 : 32; };
+
+// bcol0: byte column of the 128-K step in the row
+template <int FMT, int COLS, uint32_t SWZ>
+TL_DEVICE intx8 ld_mx_operand(const uint8_t* base, int row, int bcol0, int g) {
+  if constexpr (mx_fmt<FMT>::lane_bytes == 32) {
+    intx4 lo = *reinterpret_cast<const intx4*>(base + swz_offset<uint8_t, COLS, SWZ>(row, bcol0 + 16 * g));
+    intx4 hi = *reinterpret_cast<const intx4*>(base + swz_offset<uint8_t, COLS, SWZ>(row, bcol0 + 64 + 16 * g));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  } else {
+    intx4 lo = *reinterpret_cast<const intx4*>(base + swz_offset<uint8_t, COLS, SWZ>(row, bcol0 + 16 * g));
+    intx4 z = {0, 0, 0, 0};
+    return __builtin_shufflevector(lo, z, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
+template <int FA, int FB, int M, int N, int K, int WARP_M, int WARP_N, int A_COLS, uint32_t SWZ_A, int B_COLS,
+          uint32_t SWZ_B, int SA_STRIDE, int SB_STRIDE>
+TL_DEVICE void gemm_ss_mx(const void* __restrict__ A_, const void* __restrict__ B_, const void* __restrict__ SA_,
+                          const void* __restrict__ SB_, float* __restrict__ C) {
+  constexpr int WM = M / WARP_M, WN = N / WARP_N;
+  constexpr int M_REP = WM / 16, N_REP = WN / 16;
+  constexpr int BA = mx_fmt<FA>::lane_bytes, BB = mx_fmt<FB>::lane_bytes;  // bytes per lane per step
+  static_assert(WM % 16 == 0 && WN % 16 == 0 && K % 128 == 0, "scaled MFMA 16x16x128 tiling");
+  const uint8_t* A = reinterpret_cast<const uint8_t*>(A_);
+  const uint8_t* B = reinterpret_cast<const uint8_t*>(B_);
+  const uint8_t* SA = reinterpret_cast<const uint8_t*>(SA_);
+  const uint8_t* SB = reinterpret_cast<const uint8_t*>(SB_);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wm = wave / WARP_N, wn = wave % WARP_N;
+  const int r = lane & 15, g = lane >> 4;
+  floatx4* acc = reinterpret_cast<floatx4*>(C);
+#pragma unroll
+  for (int kk = 0; kk < K / 128; ++kk) {
+    intx8 a[M_REP], b[N_REP];
+    int sa[M_REP], sb[N_REP];
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi) {
+      const int row = wm * WM + mi * 16 + r;
+      a[mi] = ld_mx_operand<FA, A_COLS, SWZ_A>(A, row, kk * 4 * BA, g);
+      sa[mi] = (int)SA[row * SA_STRIDE + kk * 4 + g];
+    }
+#pragma unroll
+    for (int ni = 0; ni < N_REP; ++ni) {
+      const int row = wn * WN + ni * 16 + r;
+      b[ni] = ld_mx_operand<FB, B_COLS, SWZ_B>(B, row, kk * 4 * BB, g);
+      sb[ni] = (int)SB[row * SB_STRIDE + kk * 4 + g];
+    }
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < N_REP; ++ni)
+        acc[mi * N_REP + ni] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            b[ni], a[mi], acc[mi * N_REP + ni], FB, FA, 0, sb[ni], 0, sa[mi]);
+  }
+}
+
+}  // namespace tl

@@ -83,13 +83,30 @@ class Buffer:
             acc = acc * s if not (isinstance(acc, int) and isinstance(s, int)) else acc * s
         return list(reversed(st))
 
-    def offset_of(self, indices) -> PrimExpr:
-        """Row-major linear element offset of ``indices``."""
+    def offset_of(self, indices, wide: bool = False) -> PrimExpr:
+        """Row-major linear element offset of ``indices``.  ``wide``: computed in int64 (tensors
+        of 2^31 elements or more; reference ``src/transform/config_index_bitwidth.cc``)."""
+        from .expr import cast
+        from . import dtypes as _dt
         strides = self.get_strides()
         off = convert(self.offset) if not isinstance(self.offset, int) or self.offset else const(0)
+        if wide:
+            off = cast(off, _dt.int64)
         for i, s in zip(indices, strides):
-            off = off + convert(i) * s
+            t = convert(i)
+            if wide and t.dtype.bits < 64:
+                t = cast(t, _dt.int64)
+            off = off + t * s
         return off
+
+    def static_numel(self) -> Optional[int]:
+        shp = self.static_shape()
+        if shp is None:
+            return None
+        n = 1
+        for s in shp:
+            n *= s
+        return n
 
     def is_scope(self, *scopes) -> bool:
         return self.scope in scopes

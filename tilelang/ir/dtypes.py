@@ -106,6 +106,7 @@ float8_e4m3fnuz = _reg("float8_e4m3fnuz", "float", 8)
 float8_e5m2fnuz = _reg("float8_e5m2fnuz", "float", 8)
 float8_e8m0fnu = _reg("float8_e8m0fnu", "float", 8, "e8m0")
 float4_e2m1fn = _reg("float4_e2m1fn", "float", 4, "fp4")
+float4_e2m1fn_x2 = _reg("float4_e2m1fn_x2", "float", 8, "fp4x2")  # two e2m1 per byte (low nibble first)
 int8 = _reg("int8", "int", 8)
 int16 = _reg("int16", "int", 16)
 int32 = _reg("int32", "int", 32, "int")
@@ -156,6 +157,7 @@ _TORCH_NAMES = {
     "float8_e4m3fnuz": "float8_e4m3fnuz",
     "float8_e5m2fnuz": "float8_e5m2fnuz",
     "float8_e8m0fnu": "float8_e8m0fnu",
+    "float4_e2m1fn_x2": "float4_e2m1fn_x2",
     "int8": "int8",
     "int16": "int16",
     "int32": "int32",
@@ -173,7 +175,7 @@ def to_torch(dt):
     dt = as_dtype(dt)
     name = _TORCH_NAMES.get(dt.name)
     if name is None or not hasattr(torch, name):
-        if dt.name == "float4_e2m1fn":
+        if dt.name in ("float4_e2m1fn", "float4_e2m1fn_x2"):
             return torch.uint8
         raise TypeError(f"dtype {dt} has no torch equivalent")
     return getattr(torch, name)
@@ -198,6 +200,7 @@ _HIP_NAMES = {
     "float8_e5m2": "fp8_e5_t",
     "float8_e8m0fnu": "uint8_t",
     "float4_e2m1fn": "uint8_t",
+    "float4_e2m1fn_x2": "uint8_t",
     "int8": "int8_t",
     "int16": "int16_t",
     "int32": "int",

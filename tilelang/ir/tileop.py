@@ -104,12 +104,17 @@ class GemmOp(TileOp):
         self.wg_wait = wg_wait
         self.scale_A = scale_A  # block-scaled MX gemm (e8m0 scales), gfx950 only
         self.scale_B = scale_B
+        self.a_fmt = self.b_fmt = None  # MX element formats ("e4m3", "e5m2", "e2m1")
+
+    @property
+    def is_mx(self) -> bool:
+        return self.scale_A is not None
 
     def regions(self):
-        return [self.A, self.B, self.C]
+        return [self.A, self.B, self.C] + ([self.scale_A, self.scale_B] if self.is_mx else [])
 
     def reads(self):
-        return [self.A, self.B, self.C]
+        return [self.A, self.B, self.C] + ([self.scale_A, self.scale_B] if self.is_mx else [])
 
     def writes(self):
         return [self.C]
@@ -127,7 +132,8 @@ class GemmOp(TileOp):
     @property
     def K(self):
         e = self.A.static_extents()
-        return e[-2] if self.trans_A else e[-1]
+        k = e[-2] if self.trans_A else e[-1]
+        return 2 * k if self.a_fmt == "e2m1" else k
 
 
 class FillOp(TileOp):

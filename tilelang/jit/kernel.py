@@ -111,9 +111,11 @@ class JITKernel:
         specs = []
         for i, p in enumerate(dk.params):
             d = dict(kind={"buffer": 0, "scalar": 1, "dyn": 2}.get(p["kind"], 1), name=p["name"], scalar_type=0,
-                     nbytes=8, is_float=False, shape=[], strides=[], is_output=False, sym=-1)
+                     nbytes=8, is_float=False, shape=[], strides=[], is_output=False, sym=-1, max_elems=0)
             if p["kind"] == "buffer":
                 b: Buffer = p["buffer"]
+                if b.name in getattr(dk, "narrow_index", ()):
+                    d["max_elems"] = 1 << 31  # compiled with 32-bit offsets: refuse larger tensors
                 d["scalar_type"] = _scalar_type_code(b.dtype)
                 d["is_output"] = with_outputs and (b.param_index in self.out_idx)
                 for s in b.shape:
@@ -157,8 +159,11 @@ class JITKernel:
                     for i, (dk, code) in enumerate(zip(a.kernels, self.code)):
                         specs, nsyms, grid = self._param_specs(dk, with_outputs=(i == 0))
                         blob = code.encode() if isinstance(code, str) else code
-                        rts.append(rt.Kernel(blob, dk.name, a.is_cpu, specs, nsyms, grid, [int(b) for b in dk.block],
-                                             int(dk.lds_bytes), dk.name))
+                        k = rt.Kernel(blob, dk.name, a.is_cpu, specs, nsyms, grid, [int(b) for b in dk.block],
+                                      int(dk.lds_bytes), dk.name)
+                        if getattr(dk, "cooperative", False) and not a.is_cpu:
+                            k.set_cooperative(True)
+                        rts.append(k)
                     self._rt = rts
         return self._rt
 

@@ -91,11 +91,42 @@ gemm_v1 = gemm
 gemm_v2 = gemm
 
 
+_MX_FORMATS = {"e4m3": 0, "e5m2": 1, "e2m3": 2, "e3m2": 3, "e2m1": 4}
+
+
+def _mx_format(region, fmt):
+    dt = region.buffer.dtype
+    if fmt is None:
+        fmt = {"float8_e4m3fn": "e4m3", "float8_e5m2": "e5m2", "float4_e2m1fn_x2": "e2m1"}.get(dt.name)
+        if fmt is None:
+            raise ValueError(f"T.gemm_scaled: cannot infer the MX element format of a {dt} operand; pass "
+                             f"a_format/b_format (one of {sorted(_MX_FORMATS)})")
+    if fmt not in _MX_FORMATS:
+        raise ValueError(f"T.gemm_scaled: unknown MX format {fmt!r} (one of {sorted(_MX_FORMATS)})")
+    if fmt in ("e2m3", "e3m2"):
+        raise NotImplementedError("T.gemm_scaled: fp6 operands (e2m3/e3m2) are not lowered yet; use fp8 or fp4")
+    if dt.bits != 8:
+        raise ValueError(f"T.gemm_scaled: MX operands are byte buffers (fp8, or packed fp4 pairs), got {dt}")
+    return fmt
+
+
 def gemm_scaled(A, B, C, scale_A, scale_B, transpose_A=False, transpose_B=True, policy=GemmWarpPolicy.Square,
-                clear_accum=False):
-    """Block-scaled MX GEMM (gfx950 ``v_mfma_scale_f32_*_f8f6f4``): A/B fp8, e8m0 scales per 32 K."""
-    op = O.GemmOp(to_region(A), to_region(B), to_region(C), transpose_A, transpose_B, int(policy), clear_accum, 1,
-                  0, to_region(scale_A), to_region(scale_B))
+                clear_accum=False, a_format=None, b_format=None):
+    """Block-scaled MX GEMM: ``C (+)= (A * 2^(scale_A-127)) @ (B * 2^(scale_B-127))^T``.
+
+    gfx950 ``v_mfma_scale_f32_16x16x128_f8f6f4``: the hardware applies one e8m0 scale per
+    32 consecutive K elements of every row.  ``A``: ``[M, K]`` fp8 (e4m3/e5m2) or ``[M, K/2]``
+    packed fp4 pairs (``float4_e2m1fn_x2`` / uint8 with ``a_format="e2m1"``, low nibble =
+    even element); ``B``: ``[N, K]`` likewise (``transpose_B=True``, both K-contiguous);
+    ``scale_A``: ``[M, K/32]`` and ``scale_B``: ``[N, K/32]`` e8m0 bytes (shared or global).
+    K must be a multiple of 128."""
+    A, B, C = to_region(A), to_region(B), to_region(C)
+    fa, fb = _mx_format(A, a_format), _mx_format(B, b_format)
+    if transpose_A or not transpose_B:
+        raise ValueError("T.gemm_scaled needs K-contiguous operands: A [M, K] and B [N, K] (transpose_B=True)")
+    op = O.GemmOp(A, B, C, transpose_A, transpose_B, int(policy), clear_accum, 1, 0, to_region(scale_A),
+                  to_region(scale_B))
+    op.a_fmt, op.b_fmt = fa, fb
     return _emit(op)
 
 

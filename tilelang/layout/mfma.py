@@ -127,6 +127,21 @@ def _read_patterns(kind: str, rows: int, cols: int, elem_bytes: int, row_base_st
       'tr_kperm': same, C-layout compatible k order (16h + 4g + q)
     """
     pats = []
+    if kind == "k_rows16":
+        # packed-fp4 operand of the scaled 16x16x128 MFMA: 64 bytes per row per K step, 16
+        # consecutive bytes (32 e2m1) per lane -> one b128 read
+        for r0 in range(0, min(rows, 64), row_base_step):
+            for k0 in range(0, cols, 64):
+                pats.append([(r0 + (l & 15), k0 + (l >> 4) * 16) for l in range(64)])
+        return pats
+    if kind == "k_rows32mx":
+        # fp8 operand of the block-scaled 16x16x128 MFMA in hardware K order: two b128 reads per
+        # lane at byte 16g and 64 + 16g of the 128-byte K step (see tl/gemm.h gemm_ss_mx)
+        for r0 in range(0, min(rows, 64), row_base_step):
+            for k0 in range(0, cols, 128):
+                for half in range(2):
+                    pats.append([(r0 + (l & 15), k0 + (l >> 4) * 16 + 64 * half) for l in range(64)])
+        return pats
     if kind == "k_rows32":
         # 8-bit operand of the scaled 16x16x128 MFMA: 32 consecutive bytes per lane, two b128 reads
         for r0 in range(0, min(rows, 64), row_base_step):
@@ -161,7 +176,7 @@ def _read_patterns(kind: str, rows: int, cols: int, elem_bytes: int, row_base_st
 
 
 def _instr_for(kind: str, elem_bytes: int) -> str:
-    if kind == "k_rows32":
+    if kind in ("k_rows32", "k_rows16", "k_rows32mx"):
         return "ds_read_b128"
     if kind == "k_rows":
         return "ds_read_b128" if elem_bytes == 2 else "ds_read_b64"

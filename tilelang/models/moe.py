@@ -36,11 +36,15 @@ class MoEConfig:
     topk: int = 2
     dtype: torch.dtype = torch.bfloat16
     block_M: int = 128
+    gemm_cfg: Optional[dict] = None  # expert GEMM tile: block_N, block_K, num_stages, threads
 
 
 def route(x: torch.Tensor, gate_w: torch.Tensor, topk: int):
-    """softmax(x Wg^T) top-k with renormalised weights -> (expert ids [T, k], weights [T, k])."""
-    logits = (x.float() @ gate_w.float().t())
+    """softmax(x Wg^T) top-k with renormalised weights -> (expert ids [T, k], weights [T, k]).
+
+    On the GPU / CPU target this is the tilelang router kernel (``ops.moe.route``); this
+    PyTorch definition is the reference it is tested against."""
+    logits = torch.nn.functional.linear(x, gate_w).float()
     probs = torch.softmax(logits, -1)
     w, ids = torch.topk(probs, topk, dim=-1)
     w = w / w.sum(-1, keepdim=True)
@@ -105,34 +109,37 @@ class MoELayer(torch.nn.Module):
         self.w2 = w2.contiguous().to(device)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from ..ops import moe as K
         cfg = self.cfg
-        T_, H = x.shape
-        ids, wts = route(x, self.gate_w, cfg.topk)
-        flat_ids = ids.reshape(-1)
-        tok = torch.arange(T_, device=x.device).repeat_interleave(cfg.topk)
-        rows = x[tok]
+        ids, wts = K.route(x, self.gate_w, cfg.topk)
         if self.parallel in ("local", "tp"):
-            y = expert_ffn(rows, flat_ids, self.w1, self.w2, cfg.block_M,
-                           reduce_mesh="all" if self.parallel == "tp" else None)
-        else:
-            y = self._ep(rows, flat_ids)
-        out = torch.zeros(T_, H, dtype=torch.float32, device=x.device)
-        out.index_add_(0, tok, y.float() * wts.reshape(-1, 1))
-        return out.to(x.dtype)
+            y, dest = K.expert_ffn_padded(x, ids, cfg.topk, self.w1, self.w2, cfg.block_M,
+                                          reduce_mesh="all" if self.parallel == "tp" else None, cfg=cfg.gemm_cfg)
+            return K.combine(y, dest, wts)
+        y = self._ep(x, ids)
+        return K.combine(y, torch.arange(y.shape[0], device=x.device, dtype=torch.int32), wts)
 
-    def _ep(self, rows, flat_ids):
+    def _ep(self, x, ids):
+        """Expert parallel: (token, expert) pairs travel to the expert's rank and back (two
+        variable-size all-to-alls; one host sync for the split sizes)."""
+        from ..ops import moe as K
         from ..parallel import collectives as C
         m = self.mesh
         W = m.world
         n = self.cfg.n_experts // W
-        dest = torch.div(flat_ids, n, rounding_mode="floor")
-        order = torch.argsort(dest, stable=True)
-        send_counts = torch.bincount(dest, minlength=W).tolist()
-        payload = rows[order]
-        local_e = (flat_ids[order] - dest[order] * n).to(torch.int32)
-        recv_rows, rc = C.all_to_all_v(payload, send_counts)
-        recv_e, _ = C.all_to_all_v(local_e.unsqueeze(1), send_counts)
-        y_local = expert_ffn(recv_rows, recv_e.squeeze(1).long(), self.w1, self.w2, self.cfg.block_M)
+        flat_ids = ids.reshape(-1).long()
+        dest_rank = torch.div(flat_ids, n, rounding_mode="floor")
+        order = torch.argsort(dest_rank, stable=True)
+        send_counts = torch.bincount(dest_rank, minlength=W)
+        tok = torch.div(order, self.cfg.topk, rounding_mode="floor")
+        payload = x[tok]
+        local_e = (flat_ids[order] - dest_rank[order] * n).to(payload.dtype).unsqueeze(1)
+        # expert id rides along as one extra column (exact in bf16/fp32 for < 256 experts)
+        recv, rc = C.all_to_all_v(torch.cat([payload, local_e], 1), send_counts)
+        recv_rows, recv_e = recv[:, :-1].contiguous(), recv[:, -1].round().to(torch.int32)
+        y_pad, dest = K.expert_ffn_padded(recv_rows, recv_e, 1, self.w1, self.w2, self.cfg.block_M,
+                                          cfg=self.cfg.gemm_cfg)
+        y_local = y_pad[dest.long()]
         y_back, _ = C.all_to_all_v(y_local, rc)
         y = torch.empty_like(y_back)
         y[order] = y_back

@@ -1,10 +1,23 @@
-"""MoE expert-FFN kernels (tilelang DSL) and the token dispatch around them.
+"""MoE expert-FFN kernels (tilelang DSL) and the device-side token dispatch around them.
 
-Layout (MI355X-first): tokens routed to expert ``e`` are packed into a row block of the
-``padded`` activation matrix whose start is a multiple of ``block_M``; a ``tile_expert``
-table gives the expert of every ``block_M`` row tile (``-1`` = empty tile, the block exits at
-once).  Shapes are therefore static (``max_rows`` is the worst case), one compiled kernel
-serves every routing, and the launches are hipGraph-capturable.
+Layout (MI355X-first): tokens routed to expert ``e`` occupy a row block of a *padded* row
+space whose start is a multiple of ``block_M``; a ``tile_expert`` table gives the expert of
+every ``block_M`` row tile (``-1`` = empty tile, the block exits at once) and ``row_src`` the
+source row of every padded row (``-1`` = padding).  Shapes are therefore static (``max_rows``
+is the worst case), one compiled kernel serves every routing, nothing syncs with the host and
+the launches are hipGraph-capturable.
+
+One layer = 6 launches, all tilelang kernels except the router logits GEMM:
+  router_topk   softmax-free top-k over the logits (renormalised weights cancel the softmax
+                denominator), one thread per token
+  moe_align     one workgroup: per-expert histogram (LDS atomics), padded prefix offsets,
+                slot of every assignment, ``row_src`` / ``tile_expert`` tables
+  gemm1         ``[g | u] = x[row_src] @ W1[e]^T`` — the A rows are gathered straight from
+                the token matrix into LDS by per-lane LDS-DMA (``T.gather_rows``); no
+                dispatch copy of the activations is ever materialised
+  silu_mul      ``act = silu(g) * u``
+  gemm2         ``y = act @ W2[e]^T`` (optionally summed across the mesh in-kernel)
+  combine       ``out[t] = sum_k w[t, k] * y[dest[t, k]]`` in fp32, one pass, no atomics
 
 Reference: ``examples/grouped_gemm/example_grouped_gemm_fwd.py`` (group search per tile) and
 ``examples/fusedmoe/example_fusedmoe_tilelang.py`` (routed SwiGLU experts).
@@ -28,20 +41,161 @@ def _tdt(dtype: torch.dtype) -> str:
     return {torch.float16: "float16", torch.bfloat16: "bfloat16", torch.float32: "float32"}[dtype]
 
 
+def _bucket(n: int, lo: int = 256) -> int:
+    """Power-of-two bucket >= n: data-dependent row counts reuse a handful of compiled kernels."""
+    nb = lo
+    while nb < n:
+        nb *= 2
+    return nb
+
+
+@functools.lru_cache(maxsize=None)
+def router_topk_kernel(n_tok: int, E: int, topk: int, target: str, threads: int = 256):
+    """``ids[t] = topk(logits[t])``, ``w[t] = softmax(logits[t])[ids] / sum`` — the renormalised
+    top-k weights equal ``exp(l_k - m) / sum_k' exp(l_k' - m)`` (the softmax denominator cancels)."""
+
+    @T.prim_func
+    def main(L: T.Tensor((n_tok, E), "float32"), ids: T.Tensor((n_tok, topk), "int32"),
+             w: T.Tensor((n_tok, topk), "float32")):
+        with T.Kernel(T.ceildiv(n_tok, threads), threads=threads) as bx:
+            for i in T.Parallel(threads):
+                v = T.alloc_local((E,), "float32")
+                sel = T.alloc_local((topk,), "int32")
+                p = T.alloc_local((topk,), "float32")
+                best = T.alloc_var("float32")
+                bi = T.alloc_var("int32")
+                tot = T.alloc_var("float32")
+                if bx * threads + i < n_tok:
+                    for e in T.serial(E):
+                        v[e] = L[bx * threads + i, e]
+                    for k in T.serial(topk):
+                        best = -T.infinity("float32")
+                        bi = 0
+                        for e in T.serial(E):
+                            if v[e] > best:
+                                best = v[e]
+                                bi = e
+                        sel[k] = bi
+                        p[k] = best
+                        v[bi] = -T.infinity("float32")
+                    tot = 0.0
+                    best = p[0]
+                    for k in T.serial(topk):
+                        p[k] = T.exp(p[k] - best)
+                        tot = tot + p[k]
+                    for k in T.serial(topk):
+                        ids[bx * threads + i, k] = sel[k]
+                        w[bx * threads + i, k] = p[k] / tot
+
+    return tilelang.compile(main, out_idx=None, target=target)
+
+
+def max_padded_rows(n_assign: int, E: int, block_M: int) -> int:
+    """Worst-case rows of the padded layout for ``n_assign`` (row, expert) pairs."""
+    rows = n_assign + E * (block_M - 1)
+    return (rows + block_M - 1) // block_M * block_M
+
+
+@functools.lru_cache(maxsize=None)
+def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: str, stable: bool = False,
+                 threads: int = 1024):
+    """Dispatch plan of ``n`` assignments (``expert_ids[n]``; assignment ``j`` reads source row
+    ``j // div``): ``dest[j]`` (its padded row), ``row_src[max_rows]``, ``tile_expert``, ``counts[E]``.
+
+    One workgroup.  ``stable=False``: rows of one expert are placed in LDS-atomic order (each
+    row's result is independent of its position, so the layer output does not depend on it).
+    ``stable=True``: assignment order is kept inside every expert (per-thread runs + a scan of
+    the per-thread counts) — identical placement on every rank, which the tensor-parallel
+    in-kernel reduction needs."""
+    n_tiles = max_rows // block_M
+    if stable:
+        threads = 256
+    c = -(-n // threads)
+
+    @T.prim_func
+    def main(expert_ids: T.Tensor((n,), "int32"), dest: T.Tensor((n,), "int32"),
+             row_src: T.Tensor((max_rows,), "int32"), tile_expert: T.Tensor((n_tiles,), "int32"),
+             counts: T.Tensor((E,), "int32")):
+        # written with T.Parallel (one iteration per thread on the GPU, a serial loop on the
+        # CPU target), never with raw thread ids, so the same program runs on both
+        with T.Kernel(1, threads=threads):
+            cnt = T.alloc_shared((E,), "int32")
+            start = T.alloc_shared((E + 1,), "int32")
+            fill = T.alloc_shared((E,), "int32")
+            acc = T.alloc_var("int32")
+            if stable:
+                tc = T.alloc_shared((threads, E), "int32")
+                run = T.alloc_shared((threads, E), "int32")
+                for t in T.Parallel(threads):
+                    for e in T.serial(E):
+                        tc[t, e] = 0
+                    for i in T.serial(c):
+                        if t * c + i < n:
+                            tc[t, expert_ids[t * c + i]] = tc[t, expert_ids[t * c + i]] + 1
+                T.cumsum(tc, run, dim=0)
+                for e in T.Parallel(E):
+                    cnt[e] = run[threads - 1, e]
+            else:
+                for e in T.Parallel(E):
+                    cnt[e] = 0
+                    fill[e] = 0
+                for j in T.Parallel(n):
+                    T.atomic_add(cnt[expert_ids[j]], 1)
+            for r in T.Parallel(max_rows):
+                row_src[r] = -1
+            for z in T.Parallel(1):
+                acc = 0
+                for e in T.serial(E):
+                    start[e] = acc
+                    acc = acc + (cnt[e] + block_M - 1) // block_M * block_M
+                start[E] = acc + z
+            for e in T.Parallel(E):
+                counts[e] = cnt[e]
+            for tt in T.Parallel(n_tiles):
+                te = T.alloc_var("int32")
+                te = -1
+                for e in T.serial(E):
+                    if tt * block_M >= start[e] and tt * block_M < start[e] + cnt[e]:
+                        te = e
+                tile_expert[tt] = te
+            if stable:
+                for t in T.Parallel(threads):
+                    for e in T.serial(E):
+                        run[t, e] = start[e] + run[t, e] - tc[t, e]
+                    for i in T.serial(c):
+                        if t * c + i < n:
+                            d = run[t, expert_ids[t * c + i]]
+                            run[t, expert_ids[t * c + i]] = d + 1
+                            dest[t * c + i] = d
+                            row_src[d] = (t * c + i) // div
+            else:
+                for j in T.Parallel(n):
+                    slot = T.atomic_add(fill[expert_ids[j]], 1, return_prev=True)
+                    dest[j] = start[expert_ids[j]] + slot
+                    row_src[start[expert_ids[j]] + slot] = j // div
+
+    return tilelang.compile(main, out_idx=None, target=target)
+
+
 @functools.lru_cache(maxsize=None)
 def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target: str, block_M: int = 128,
                        block_N: int = 128, block_K: int = 64, num_stages: int = 2, threads: int = 256,
-                       reduce_mesh: Optional[str] = None, mesh_shape: Optional[Tuple[int, int]] = None):
-    """``C[r, :] = A[r, :] @ W[tile_expert[r // block_M]].T`` for every non-empty row tile.
+                       reduce_mesh: Optional[str] = None, mesh_shape: Optional[Tuple[int, int]] = None,
+                       n_src: Optional[int] = None):
+    """``C[r, :] = A[src(r), :] @ W[tile_expert[r // block_M]].T`` for every non-empty row tile.
 
+    ``n_src`` given: A is the ``[n_src, K]`` source-row matrix and row ``r`` of the padded row
+    space reads ``A[row_src[r]]`` (``-1`` = padding = zeros), gathered straight into LDS.
     ``reduce_mesh`` ("all"/"h"/"v"): tensor-parallel partial products are summed across the
     mesh inside the kernel (``T.comm.all_reduce_tile`` on the fp32 accumulator tile)."""
     n_tiles = max_rows // block_M
     accum = "float32"
+    a_rows = n_src if n_src is not None else max_rows
 
     @T.prim_func
-    def main(A: T.Tensor((max_rows, K), dtype), W: T.Tensor((E, N, K), dtype),
-             tile_expert: T.Tensor((n_tiles,), "int32"), C: T.Tensor((max_rows, N), dtype)):
+    def main(A: T.Tensor((a_rows, K), dtype), W: T.Tensor((E, N, K), dtype),
+             tile_expert: T.Tensor((n_tiles,), "int32"), row_src: T.Tensor((max_rows,), "int32"),
+             C: T.Tensor((max_rows, N), dtype)):
         with T.Kernel(n_tiles, T.ceildiv(N, block_N), threads=threads) as (bx, by):
             A_s = T.alloc_shared((block_M, block_K), dtype)
             W_s = T.alloc_shared((block_N, block_K), dtype)
@@ -51,7 +205,11 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
                 if e >= 0:
                     T.clear(C_l)
                     for k in T.Pipelined(T.ceildiv(K, block_K), num_stages=num_stages):
-                        T.copy(A[bx * block_M, k * block_K], A_s)
+                        if n_src is not None:
+                            T.gather_rows(A[:, k * block_K:(k + 1) * block_K],
+                                          row_src[bx * block_M:(bx + 1) * block_M], A_s, row_dim=0)
+                        else:
+                            T.copy(A[bx * block_M, k * block_K], A_s)
                         T.copy(W[e, by * block_N, k * block_K], W_s)
                         T.gemm(A_s, W_s, C_l, transpose_B=True)
                     T.copy(C_l, C[bx * block_M, by * block_N])
@@ -62,7 +220,11 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
                 if e >= 0:
                     T.clear(C_l)
                     for k in T.Pipelined(T.ceildiv(K, block_K), num_stages=num_stages):
-                        T.copy(A[bx * block_M, k * block_K], A_s)
+                        if n_src is not None:
+                            T.gather_rows(A[:, k * block_K:(k + 1) * block_K],
+                                          row_src[bx * block_M:(bx + 1) * block_M], A_s, row_dim=0)
+                        else:
+                            T.copy(A[bx * block_M, k * block_K], A_s)
                         T.copy(W[e, by * block_N, k * block_K], W_s)
                         T.gemm(A_s, W_s, C_l, transpose_B=True)
                     T.comm.all_reduce_tile(C_l, C_r, "sum", reduce_mesh)
@@ -90,72 +252,107 @@ def silu_mul_kernel(rows: int, F: int, dtype: str, target: str, block_R: int = 3
                 u = T.Cast("float32", H[bx * block_R + i, F + by * block_F + j])
                 O[bx * block_R + i, by * block_F + j] = T.Cast(dtype, g / (1.0 + T.exp(-g)) * u)
 
+    return tilelang.compile(main, out_idx=None, target=target,
+                            pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True})
+
+
+@functools.lru_cache(maxsize=None)
+def combine_kernel(n_tok: int, H: int, topk: int, max_rows: int, dtype: str, target: str, block_H: int = 1024,
+                   threads: int = 128):
+    """``out[t, :] = sum_k w[t, k] * Y[dest[t * topk + k], :]`` (fp32 sum, one pass, no atomics)."""
+    block_H = min(block_H, H)
+    assert H % block_H == 0
+
+    @T.prim_func
+    def main(Y: T.Tensor((max_rows, H), dtype), dest: T.Tensor((n_tok * topk,), "int32"),
+             w: T.Tensor((n_tok, topk), "float32"), out: T.Tensor((n_tok, H), dtype)):
+        with T.Kernel(n_tok, H // block_H, threads=threads) as (bx, by):
+            acc = T.alloc_fragment((block_H,), "float32")
+            T.clear(acc)
+            for k in T.serial(topk):
+                r = dest[bx * topk + k]
+                wk = w[bx, k]
+                for h in T.Parallel(block_H):
+                    acc[h] += wk * T.Cast("float32", Y[r, by * block_H + h])
+            for h in T.Parallel(block_H):
+                out[bx, by * block_H + h] = T.Cast(dtype, acc[h])
+
     return tilelang.compile(main, out_idx=None, target=target)
 
 
-def max_padded_rows(n_assign: int, E: int, block_M: int) -> int:
-    """Worst-case rows of the padded layout for ``n_assign`` (token, expert) pairs."""
-    rows = n_assign + E * (block_M - 1)
-    return (rows + block_M - 1) // block_M * block_M
+def route(x: torch.Tensor, gate_w: torch.Tensor, topk: int):
+    """Router: logits (vendor GEMM, fp32 out) -> top-k ids [T, k] int32 + renormalised weights [T, k]."""
+    logits = torch.nn.functional.linear(x, gate_w).float()
+    n_tok, E = logits.shape
+    ids = torch.empty(n_tok, topk, dtype=torch.int32, device=x.device)
+    w = torch.empty(n_tok, topk, dtype=torch.float32, device=x.device)
+    router_topk_kernel(n_tok, E, topk, _target(x.device))(logits, ids, w)
+    return ids, w
+
+
+def dispatch_plan(expert_ids: torch.Tensor, E: int, block_M: int, max_rows: int, div: int = 1,
+                  stable: bool = False):
+    """Device-side padded placement: ``(dest[n], row_src[max_rows], tile_expert, counts[E])``."""
+    dev = expert_ids.device
+    n = expert_ids.numel()
+    ids = expert_ids.reshape(-1).to(torch.int32).contiguous()
+    dest = torch.empty(n, dtype=torch.int32, device=dev)
+    row_src = torch.empty(max_rows, dtype=torch.int32, device=dev)
+    te = torch.empty(max_rows // block_M, dtype=torch.int32, device=dev)
+    counts = torch.empty(E, dtype=torch.int32, device=dev)
+    align_kernel(n, E, block_M, max_rows, div, _target(dev), stable)(ids, dest, row_src, te, counts)
+    return dest, row_src, te, counts
 
 
 def pack_by_expert(expert_ids: torch.Tensor, E: int, block_M: int, max_rows: int):
-    """Padded placement of assignments grouped by expert.
+    """``(dest[n], tile_expert[max_rows // block_M], counts[E])`` (see ``dispatch_plan``)."""
+    dest, _, te, counts = dispatch_plan(expert_ids, E, block_M, max_rows, stable=True)
+    return dest.long(), te, counts.long()
 
-    Returns ``(dest_row[n], tile_expert[max_rows // block_M], counts[E])``: assignment i goes
-    to row ``dest_row[i]``; expert e's rows start at a multiple of ``block_M``."""
-    dev = expert_ids.device
+
+def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int, w1: torch.Tensor,
+                      w2: torch.Tensor, block_M: int = 128, reduce_mesh: Optional[str] = None,
+                      cfg: Optional[dict] = None):
+    """SwiGLU experts for the assignments ``expert_ids[n]`` (assignment j reads ``src_rows[j // div]``).
+    Returns ``(Y [max_rows, H], dest [n])``: assignment j's result is row ``dest[j]`` of Y."""
+    cfg = dict(cfg or {})
+    E, F2, H = w1.shape
+    F = F2 // 2
     n = expert_ids.numel()
-    counts = torch.bincount(expert_ids, minlength=E)
-    padded = (counts + block_M - 1) // block_M * block_M
-    starts = torch.cumsum(padded, 0) - padded
-    order = torch.argsort(expert_ids, stable=True)
-    sorted_e = expert_ids[order]
-    first = torch.cumsum(counts, 0) - counts
-    rank_in_e = torch.arange(n, device=dev) - first[sorted_e]
-    dest_sorted = starts[sorted_e] + rank_in_e
-    dest = torch.empty_like(dest_sorted)
-    dest[order] = dest_sorted
-    n_tiles = max_rows // block_M
-    tile_starts = torch.arange(n_tiles, device=dev) * block_M
-    ends = starts + padded
-    te = torch.full((n_tiles,), -1, dtype=torch.int32, device=dev)
-    # tile t belongs to expert e if starts[e] <= t*block_M < ends[e]
-    idx = torch.searchsorted(ends, tile_starts, right=True)
-    valid = idx < E
-    idx_c = idx.clamp(max=E - 1)
-    valid &= (tile_starts >= starts[idx_c]) & (padded[idx_c] > 0)
-    te[valid] = idx_c[valid].to(torch.int32)
-    return dest, te, counts
+    dev = src_rows.device
+    tgt = _tdt(src_rows.dtype)
+    target = _target(dev)
+    max_rows = max_padded_rows(_bucket(n), E, block_M)
+    n_src = _bucket(src_rows.shape[0])
+    if src_rows.shape[0] != n_src:
+        src_rows = torch.cat([src_rows, src_rows.new_zeros(n_src - src_rows.shape[0], src_rows.shape[1])])
+    dest, row_src, te, _ = dispatch_plan(expert_ids, E, block_M, max_rows, div, stable=reduce_mesh is not None)
+    k1 = expert_gemm_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, **cfg)
+    h = torch.empty(max_rows, F2, dtype=src_rows.dtype, device=dev)
+    k1(src_rows.contiguous(), w1, te, row_src, h)
+    act = torch.empty(max_rows, F, dtype=src_rows.dtype, device=dev)
+    silu_mul_kernel(max_rows, F, tgt, target)(h, act)
+    k2 = expert_gemm_kernel(max_rows, F, H, E, tgt, target, block_M, reduce_mesh=reduce_mesh,
+                            mesh_shape=_mesh_shape() if reduce_mesh else None, **cfg)
+    y = torch.empty(max_rows, H, dtype=src_rows.dtype, device=dev)
+    k2(act, w2, te, row_src, y)
+    return y, dest
 
 
 def expert_ffn(x_rows: torch.Tensor, expert_ids: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor,
                block_M: int = 128, reduce_mesh: Optional[str] = None, cfg: Optional[dict] = None) -> torch.Tensor:
     """SwiGLU experts on already-dispatched rows: ``y_i = W2[e_i] (silu(g) * u)``, with
     ``[g | u] = W1[e_i] x_i``.  ``w1``: ``[E, 2F, H]``, ``w2``: ``[E, H, F]``."""
-    cfg = dict(cfg or {})
-    E, F2, H = w1.shape
-    F = F2 // 2
-    n = x_rows.shape[0]
-    dev = x_rows.device
-    tgt = _tdt(x_rows.dtype)
-    target = _target(dev)
-    # bucket the row count (power of two >= 256) so data-dependent EP receive sizes reuse a
-    # handful of compiled kernels
-    nb = 256
-    while nb < n:
-        nb *= 2
-    max_rows = max_padded_rows(nb, E, block_M)
-    dest, te, _ = pack_by_expert(expert_ids, E, block_M, max_rows)
-    A = torch.zeros(max_rows, H, dtype=x_rows.dtype, device=dev)
-    A[dest] = x_rows
-    k1 = expert_gemm_kernel(max_rows, H, F2, E, tgt, target, block_M, **cfg)
-    h = torch.empty(max_rows, F2, dtype=x_rows.dtype, device=dev)
-    k1(A, w1, te, h)
-    act = torch.empty(max_rows, F, dtype=x_rows.dtype, device=dev)
-    silu_mul_kernel(max_rows, F, tgt, target)(h, act)
-    k2 = expert_gemm_kernel(max_rows, F, H, E, tgt, target, block_M, reduce_mesh=reduce_mesh,
-                            mesh_shape=_mesh_shape() if reduce_mesh else None, **cfg)
-    y = torch.empty(max_rows, H, dtype=x_rows.dtype, device=dev)
-    k2(act, w2, te, y)
-    return y[dest]
+    y, dest = expert_ffn_padded(x_rows, expert_ids, 1, w1, w2, block_M, reduce_mesh, cfg)
+    return y[dest.long()]
+
+
+def combine(y: torch.Tensor, dest: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``out[t] = sum_k w[t, k] * y[dest[t * topk + k]]``."""
+    n_tok, topk = w.shape
+    H = y.shape[1]
+    bh = 1024 if H % 1024 == 0 else H
+    out = torch.empty(n_tok, H, dtype=y.dtype, device=y.device)
+    combine_kernel(n_tok, H, topk, y.shape[0], _tdt(y.dtype), _target(y.device), block_H=bh)(
+        y, dest.to(torch.int32).contiguous(), w.float().contiguous(), out)
+    return out

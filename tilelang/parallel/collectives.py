@@ -206,16 +206,23 @@ def all_to_all_v(t: torch.Tensor, send_counts: List[int], direction: str = "all"
     ctx = _ctx(ctx)
     members = ctx.group_ranks(direction)
     G = len(members)
-    if len(send_counts) != G or sum(send_counts) != t.shape[0]:
-        raise ValueError("send_counts must have one entry per group member and sum to t.shape[0]")
-    cnt = torch.tensor(send_counts, dtype=torch.int64, device=t.device)
+    if len(send_counts) != G:
+        raise ValueError("send_counts must have one entry per group member")
+    if isinstance(send_counts, torch.Tensor):
+        cnt = send_counts.to(device=t.device, dtype=torch.int64)
+    else:
+        cnt = torch.tensor(send_counts, dtype=torch.int64, device=t.device)
     all_cnt = all_gather(cnt, direction, ctx)          # [G (src), G (dst)]
     k = members.index(ctx.rank)
-    recv_counts = [int(x) for x in all_cnt[:, k].tolist()]
+    both = torch.cat([all_cnt[:, k], cnt]).tolist()     # the one host sync of the exchange
+    recv_counts = [int(x) for x in both[:G]]
+    send_counts = [int(x) for x in both[G:]]
     if isinstance(ctx, ProcessMesh) and t.is_cuda:
         import torch.distributed as dist
         out = torch.empty((sum(recv_counts),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        dist.all_to_all_single(out, t.contiguous(), output_split_sizes=recv_counts, input_split_sizes=list(send_counts),
+        if sum(send_counts) != t.shape[0]:
+            raise ValueError("send_counts must sum to t.shape[0]")
+        dist.all_to_all_single(out, t.contiguous(), output_split_sizes=recv_counts, input_split_sizes=send_counts,
                                group=ctx.group(direction))
         return out, recv_counts
     if isinstance(ctx, ProcessMesh):

@@ -46,6 +46,50 @@ def encode_swizzle(layout) -> int:
     return v
 
 
+MX_CODES = {"e4m3": 0, "e5m2": 1, "e2m3": 2, "e3m2": 3, "e2m1": 4}
+
+
+def _mx_plan(op: O.GemmOp, plan: Dict, num_threads: int, a_ext, b_ext, is_cpu: bool = False) -> Dict:
+    """Block-scaled MX GEMM (v_mfma_scale_f32_16x16x128_f8f6f4): both operands K-contiguous in LDS,
+    one e8m0 scale per 32 K of every row of A and of B."""
+    A, B = op.A.buffer, op.B.buffer
+    M, N = plan["M"], plan["N"]
+    ka = a_ext[1] * (2 if op.a_fmt == "e2m1" else 1)
+    kb = b_ext[1] * (2 if op.b_fmt == "e2m1" else 1)
+    if ka != kb:
+        raise ValueError(f"T.gemm_scaled: A holds K={ka} and B holds K={kb} elements")
+    K = ka
+    if K % 128:
+        raise ValueError(f"T.gemm_scaled: K={K} must be a multiple of 128 (one scaled MFMA step)")
+    if A.scope != "shared" or B.scope != "shared":
+        raise ValueError("T.gemm_scaled: A and B must be shared-memory tiles")
+    sa, sb = _trailing2(op.scale_A), _trailing2(op.scale_B)
+    if tuple(sa) != (M, K // 32) or tuple(sb) != (N, K // 32):
+        raise ValueError(f"T.gemm_scaled: scales must be [M, K/32]=[{M}, {K // 32}] and [N, K/32]=[{N}, {K // 32}], "
+                         f"got {sa} and {sb}")
+    for r in (op.scale_A, op.scale_B):
+        if r.buffer.dtype.bits != 8 or r.buffer.scope not in ("shared", "global"):
+            raise ValueError("T.gemm_scaled: scales are e8m0 bytes in shared or global memory")
+    plan.update(a_code=MX_CODES[op.a_fmt], b_code=MX_CODES[op.b_fmt], K=K)
+    if is_cpu:
+        plan.update(warp_m=1, warp_n=1, mfma=None, mx=True,
+                    c_layout=make_linear_fragment([M, N], num_threads, 1, "cpu_c"),
+                    a_smem_layout=LinearLayout(A.static_shape()), b_smem_layout=LinearLayout(B.static_shape()))
+        return plan
+    if num_threads % 64:
+        raise ValueError(f"block size {num_threads} is not a multiple of the 64-lane wavefront")
+    warp_m, warp_n = MF.compute_warp_partition(M, N, num_threads // 64, op.policy)
+    plan.update(K=K, warp_m=warp_m, warp_n=warp_n, mfma=(16, 16, 128), mx=True,
+                a_code=MX_CODES[op.a_fmt], b_code=MX_CODES[op.b_fmt])
+    plan["c_layout"] = MF.mfma_c_fragment(M, N, warp_m, warp_n)
+    ka_kind = "k_rows16" if op.a_fmt == "e2m1" else "k_rows32mx"
+    kb_kind = "k_rows16" if op.b_fmt == "e2m1" else "k_rows32mx"
+    plan["a_kind"], plan["b_kind"] = ka_kind, kb_kind
+    plan["a_smem_layout"] = MF.operand_swizzle(ka_kind, A.static_shape(), 1)
+    plan["b_smem_layout"] = MF.operand_swizzle(kb_kind, B.static_shape(), 1)
+    return plan
+
+
 def gemm_plan(op: O.GemmOp, num_threads: int, target=None, a_layout: Optional[Fragment] = None) -> Dict:
     a_ext, b_ext, c_ext = _trailing2(op.A), _trailing2(op.B), _trailing2(op.C)
     M, N = c_ext
@@ -53,17 +97,21 @@ def gemm_plan(op: O.GemmOp, num_threads: int, target=None, a_layout: Optional[Fr
     kb = b_ext[1] if op.trans_B else b_ext[0]
     am = a_ext[1] if op.trans_A else a_ext[0]
     bn = b_ext[0] if op.trans_B else b_ext[1]
+    if op.is_mx:
+        kb = K  # packed fp4 rows hold 2 elements per byte: _mx_plan checks the logical K
     if kb != K or am != M or bn != N:
         raise ValueError(f"T.gemm shape mismatch: A{a_ext} B{b_ext} C{c_ext} "
                          f"(transpose_A={op.trans_A}, transpose_B={op.trans_B})")
     is_cpu = target is not None and getattr(target, "kind", "hip") == "cpu"
     A, B, C = op.A.buffer, op.B.buffer, op.C.buffer
     plan = dict(M=M, N=N, K=K, a_kperm=0)
-    if is_cpu:
+    if is_cpu and not op.is_mx:
         plan.update(warp_m=1, warp_n=1, mfma=None, c_layout=make_linear_fragment([M, N], num_threads, 1, "cpu_c"),
                     a_smem_layout=LinearLayout(A.static_shape() or a_ext),
                     b_smem_layout=LinearLayout(B.static_shape() or b_ext))
         return plan
+    if op.is_mx:
+        return _mx_plan(op, plan, num_threads, a_ext, b_ext, is_cpu)
     eb = A.dtype.bits
     if A.dtype != B.dtype:
         raise ValueError(f"T.gemm needs matching A/B dtypes, got {A.dtype} and {B.dtype}")

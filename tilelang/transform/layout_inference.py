@@ -540,4 +540,6 @@ def _equal_rep(a: Fragment, b: Fragment, T: int) -> bool:
 def infer_layouts(func: S.PrimFunc, num_threads: int, target=None) -> LayoutInference:
     li = LayoutInference(func, num_threads, target)
     li.run()
+    li.shared_buffers = [s.buffer for s in S.walk(func.body)
+                         if isinstance(s, S.AllocStmt) and s.buffer.scope == "shared"]
     return li

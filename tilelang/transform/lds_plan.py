@@ -61,25 +61,46 @@ def _touches(s, out: set):
                 out.add(e.buffer)
 
 
-def plan_lds(kernel: S.KernelStmt, reuse: bool = False) -> Tuple[Dict[Buffer, int], int]:
-    """``reuse`` (liveness-based sharing) is off by default: the barrier pass tracks hazards per
-    buffer, so aliasing two buffers also needs ``tl.enable_aggressive_shared_memory_merge``
-    (which re-runs the barrier pass on the merged arena)."""
+def _top_level(body) -> List:
+    """Flattened top-level statement list (scoped blocks stay whole: their declarations)."""
+    top = []
+    stack = [body]
+    while stack:
+        b = stack.pop(0)
+        if isinstance(b, S.SeqStmt) and not getattr(b, "scoped", False):
+            stack = list(b.stmts) + stack
+        else:
+            top.append(b)
+    return top
+
+
+def _dma_targets(s) -> set:
+    out = set()
+    for x in S.walk(s):
+        if isinstance(x, L.CallStmt) and x.name.startswith(("tl::glds", "tl::buffer_lds")):
+            for a in x.args:
+                if isinstance(a, L.BufferPtr) and a.buffer.scope == "shared":
+                    out.add(a.buffer)
+    return out
+
+
+def plan_lds(kernel: S.KernelStmt, reuse: bool = True, aggressive: bool = False):
+    """Place every shared buffer in one arena.
+
+    ``reuse``: buffers whose live ranges (first/last top-level statement of the kernel body that
+    touches them) do not overlap share bytes; a ``__syncthreads()`` is inserted in front of the
+    first statement that touches a buffer re-using bytes of a buffer that died earlier, so every
+    access of the old tenant (any thread) is ordered before the new tenant's first access.
+    LDS-DMA (pipeline stage) buffers keep their bytes for the whole kernel unless ``aggressive``
+    (``tl.enable_aggressive_shared_memory_merge``).
+
+    Returns ``(kernel, offsets, total_bytes)``."""
     shared = []
     for s in S.walk(kernel):
         if isinstance(s, S.AllocStmt) and s.buffer.scope == "shared" and s.buffer not in shared:
             shared.append(s.buffer)
     sizes = {b: int(b.shape[0]) * b.dtype.bytes for b in shared}
-    # live ranges over the top-level statements of the kernel body
-    top = []
-    body = kernel.body
-    stack = [body]
-    while stack:
-        b = stack.pop(0)
-        if isinstance(b, S.SeqStmt):
-            stack = list(b.stmts) + stack
-        else:
-            top.append(b)
+    top = _top_level(kernel.body)
     first, last = {}, {}
     for i, st in enumerate(top):
         t = set()
@@ -87,12 +108,37 @@ def plan_lds(kernel: S.KernelStmt, reuse: bool = False) -> Tuple[Dict[Buffer, in
         for b in t:
             first.setdefault(b, i)
             last[b] = i
+    pinned = set() if aggressive else _dma_targets(kernel)
+    n_top = len(top)
+    f = [0 if (b in pinned or b not in first) else first[b] for b in shared]
+    l_ = [n_top if (b in pinned or b not in last) else last[b] for b in shared]
     # placement by the native arena planner (csrc/core/lds.cc plan_arena)
     from .._native import core
     try:
-        offs, total = core().plan_arena([sizes[b] for b in shared], [first.get(b, 0) for b in shared],
-                                        [last.get(b, len(top)) for b in shared], ALIGN, bool(reuse), LDS_LIMIT)
+        offs, total = core().plan_arena([sizes[b] for b in shared], f, l_, ALIGN, bool(reuse), LDS_LIMIT)
     except ValueError as e:  # std::length_error -> ValueError
         raise LDSPlanError(str(e)) from None
     offsets: Dict[Buffer, int] = dict(zip(shared, offs))
-    return offsets, total
+    if not reuse or kernel.is_cpu:
+        return kernel, offsets, total
+    # region switches: statement index -> needs a barrier in front
+    switch = set()
+    for i, b in enumerate(shared):
+        for j, a in enumerate(shared):
+            if a is b or l_[j] >= f[i]:
+                continue
+            oa, ob = offsets[a], offsets[b]
+            if oa < ob + sizes[b] and ob < oa + sizes[a]:
+                switch.add(f[i])
+    if not switch:
+        return kernel, offsets, total
+    from .thread_sync import _sync
+    new_top = []
+    for i, st in enumerate(top):
+        if i in switch:
+            new_top.append(_sync())
+        new_top.append(st)
+    k = S.KernelStmt(kernel.grid, kernel.threads, kernel.block_vars, kernel.thread_vars, S.SeqStmt(new_top),
+                     kernel.is_cpu, kernel.prelude)
+    k.attrs = dict(kernel.attrs)
+    return k, offsets, total

@@ -115,6 +115,18 @@ class LowerCtx:
         self.extra_allocs: List[Buffer] = []
         self.staging: Dict[int, Buffer] = {}
         self.pass_cfg = pass_cfg or {}
+        self.narrow_index = set()  # global buffers addressed with 32-bit offsets
+        self.no_vectorize = bool(self.pass_cfg.get("tir.disable_vectorize", False))
+        # tl.dynamic_alignment: dynamic extents are multiples of this (enables vector accesses)
+        self.dynamic_alignment = int(self.pass_cfg.get("tl.dynamic_alignment", 0) or 0)
+        self.uses_grid_sync = False
+        self.dynamic_vars = set()
+        if self.dynamic_alignment > 1:
+            from .pipeline import _referenced_buffers
+            for b in _referenced_buffers(kernel):
+                for d in b.shape:
+                    if isinstance(d, Var):
+                        self.dynamic_vars.add(d)
         self.known_div: Dict[Var, tuple] = {}
         self.ranges = {}
         for v, g in zip(kernel.block_vars, kernel.grid):
@@ -168,8 +180,23 @@ class LowerCtx:
         if b.scope in ("local", "var"):
             return b.offset_of(indices)
         if b.scope == "global":
-            return b.offset_of(indices)
+            return b.offset_of(indices, wide=self.wide_index(b))
         raise LoweringError(f"cannot flatten access to {b.scope} buffer {b.name}")
+
+    def wide_index(self, b: Buffer) -> bool:
+        """int64 offsets for a global buffer: ``tl.config_index_bitwidth`` (32/64) decides; by
+        default a statically sized tensor of >= 2^31 elements gets int64, everything else int32
+        and the launcher refuses tensors that would overflow it (``narrow_index`` params)."""
+        bits = int(self.pass_cfg.get("tl.config_index_bitwidth", 0) or 0)
+        if bits == 64:
+            return True
+        n = b.static_numel()
+        if bits != 32 and n is not None and n >= (1 << 31):
+            return True
+        if bits == 32 and n is not None and n >= (1 << 31):
+            raise LoweringError(f"{b.name} has {n} elements but tl.config_index_bitwidth=32")
+        self.narrow_index.add(b)
+        return False
 
     def lane_expr(self):
         self.uses_lane = True
@@ -453,7 +480,15 @@ def vectorize_group(ctx: LowerCtx, stmts: List[S.Stmt], known_div) -> Optional[L
         if all(structural_equal(s.cond, c0) for s in stmts):
             inner = vectorize_group(ctx, [s.then_body for s in stmts], known_div)
             return [S.IfStmt(c0, S.SeqStmt(inner))] if inner is not None else None
-        return None
+        # per-element bounds guards (dynamic tails): the vector body runs when every element is
+        # in range, the guarded scalar copies otherwise
+        inner = vectorize_group(ctx, [s.then_body for s in stmts], known_div)
+        if inner is None:
+            return None
+        pred = None
+        for st in stmts:
+            pred = st.cond if pred is None else logical_and(pred, st.cond)
+        return [S.IfStmt(pred, S.SeqStmt(inner), S.SeqStmt(list(stmts)))]
     if W == 1 or not all(isinstance(s, S.StoreStmt) for s in stmts):
         return None
     b = stmts[0].buffer
@@ -540,6 +575,9 @@ class TileOpLowerer(Mutator):
     def __init__(self, ctx: LowerCtx):
         self.ctx = ctx
         self.known_div = {}
+        if ctx.dynamic_alignment > 1:
+            for v in ctx.dynamic_vars:
+                self.known_div[v] = (ctx.dynamic_alignment, 0)
 
     # -- helpers -------------------------------------------------------------------
     def flat_access_expr(self, e):
@@ -580,6 +618,42 @@ class TileOpLowerer(Mutator):
         if b.scope in ("local", "var"):
             return S.StoreStmt(b, [b.offset_of(idx)] if b.ndim != 1 else idx, val)
         return S.StoreStmt(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)], val)
+
+    def visit_EvaluateStmt(self, s):
+        e = s.expr
+        if isinstance(e, Call) and e.op == "tl.print_buffer":
+            return self._lower_print_buffer(e)
+        if isinstance(e, Call) and e.op == "tl.print":
+            msg, v = e.args[0], self.expr(e.args[1])
+            return L.CallStmt("tl::print_val", [msg, v])
+        if isinstance(e, Call) and e.op == "tl.sync_grid":
+            self.ctx.uses_grid_sync = True
+        return S.EvaluateStmt(self.expr(e))
+
+    def _lower_print_buffer(self, e):
+        """``T.print(buffer)`` (reference ``language/print.py:144-238``): a fragment prints every
+        thread's registers (``thread t: name[i]`` in local order); a shared / global / local
+        buffer is printed whole by one thread of the block."""
+        ctx = self.ctx
+        msg, name = e.args[0], e.args[1]
+        b = e.attrs.get("buffer")
+        if b is None:
+            raise LoweringError("T.print of a buffer lost its buffer reference")
+        if b.scope == "fragment":
+            lb = ctx.local_of(b)
+            n = int(lb.shape[0])
+            return L.CallStmt("tl::print_buffer", [msg, name, L.BufferPtr(lb, 0), IntImm(n)])
+        n = b.static_numel()
+        if n is None:
+            raise LoweringError(f"T.print({b.name}): needs a static shape")
+        if b.scope in ("local", "var"):
+            return L.CallStmt("tl::print_buffer", [msg, name, L.BufferPtr(b, 0), IntImm(n)])
+        ptr = L.BufferPtr(ctx.flat_of(b), ctx.flat_index(b, [IntImm(0)] * b.ndim))
+        st = L.CallStmt("tl::print_buffer", [msg, name, ptr, IntImm(n)])
+        if ctx.is_cpu:
+            return st
+        return S.SeqStmt([L.CallStmt("tl::sync_threads", []),
+                          S.IfStmt(binop("==", ctx.tid, IntImm(0)), st)])
 
     def visit_AllocStmt(self, s):
         b = s.buffer
@@ -654,7 +728,7 @@ class TileOpLowerer(Mutator):
                 vmap = {v: binop("+", m, i) for v, m, i in zip(nest.vars, nest.mins, idx)}
                 rw = _IterRewriter(ctx, res, r, vmap)
                 group.append(rw.stmt(nest.body))
-            if body_is_single_store and W > 1:
+            if body_is_single_store and W > 1 and not ctx.no_vectorize:
                 vec = vectorize_group(ctx, group, self.known_div)
                 if vec is not None:
                     out.extend(vec)
@@ -681,6 +755,8 @@ class TileOpLowerer(Mutator):
         accs = nest.accesses()
         max_eb = max([b.dtype.bytes for b, _, _ in accs] or [4])
         cand = cw if cw else max(1, 16 // max_eb)
+        if ctx.no_vectorize:
+            cand = 1
         while cand > 1:
             if exts[-1] % cand == 0 and total // cand >= 1 and self._vec_ok(nest, cand):
                 vec = cand
@@ -755,7 +831,7 @@ class TileOpLowerer(Mutator):
                     if as_int(st[-1]) != 1:
                         return False
                     for s_ in st[:-1]:
-                        if not divisible_by(convert(s_), vec):
+                        if not divisible_by(convert(s_), vec, self.known_div):
                             return False
                     if not divisible_by(rest, vec, self.known_div):
                         return False
@@ -872,6 +948,8 @@ class TileOpLowerer(Mutator):
             else:
                 out.append(S.IfStmt(self.expr(ca), zero))
         ctype = _dt.hip_type(A.dtype)
+        if op.is_mx:
+            return self._lower_mx_gemm(op, plan, cl, out)
         if ctx.is_cpu:
             pa = self._operand_ptr(op.A)
             pb = self._operand_ptr(op.B)
@@ -912,6 +990,24 @@ class TileOpLowerer(Mutator):
             ]))
         else:
             raise LoweringError(f"T.gemm: A operand scope {A.scope} unsupported")
+        return S.SeqStmt(out)
+
+    def _lower_mx_gemm(self, op: O.GemmOp, plan, cl, out):
+        """``tl::gemm_ss_mx`` / ``tl::cpu_gemm_mx``: block-scaled (e8m0) fp8/fp4 GEMM."""
+        A, B = op.A.buffer, op.B.buffer
+        pa, pb = self._operand_ptr(op.A), self._operand_ptr(op.B)
+        psa, psb = self._operand_ptr(op.scale_A), self._operand_ptr(op.scale_B)
+        sa_shape, sb_shape = op.scale_A.buffer.static_shape(), op.scale_B.buffer.static_shape()
+        if sa_shape is None or sb_shape is None:
+            raise LoweringError("T.gemm_scaled: scale buffers need static shapes (row stride)")
+        targs = [plan["a_code"], plan["b_code"], plan["M"], plan["N"], plan["K"]]
+        if self.ctx.is_cpu:
+            targs += [A.static_shape()[-1], B.static_shape()[-1], sa_shape[-1], sb_shape[-1]]
+            out.append(L.CallStmt("tl::cpu_gemm_mx", [pa, pb, psa, psb, L.BufferPtr(cl, 0)], targs))
+            return S.SeqStmt(out)
+        targs += [plan["warp_m"], plan["warp_n"], A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
+                  B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u", sa_shape[-1], sb_shape[-1]]
+        out.append(L.CallStmt("tl::gemm_ss_mx", [pa, pb, psa, psb, L.BufferPtr(cl, 0)], targs))
         return S.SeqStmt(out)
 
     def _operand_ptr(self, r: BufferRegion):
@@ -1651,7 +1747,7 @@ def _simt_copy_steps(ctx: LowerCtx, src: BufferRegion, dst: BufferRegion, known_
         raise LoweringError("register-staged copy needs static extents")
     total = _prod(exts) if exts else 1
     eb = max(src.buffer.dtype.bytes, dst.buffer.dtype.bytes)
-    vec = max(1, 16 // eb)
+    vec = 1 if ctx.no_vectorize else max(1, 16 // eb)
     while vec > 1:
         if exts and exts[-1] % vec == 0 and _copy_vec_ok(src, dst, sd, dd, vec, known_div):
             break
@@ -1754,6 +1850,8 @@ def lower_tile_ops(kernel: S.KernelStmt, target, pass_cfg=None):
     k = S.KernelStmt(kernel.grid, kernel.threads, kernel.block_vars, kernel.thread_vars,
                      S.SeqStmt(allocs + [body]), kernel.is_cpu, kernel.prelude)
     k.attrs = dict(kernel.attrs)
+    k.attrs["narrow_index"] = {b.name for b in ctx.narrow_index}
+    k.attrs["cooperative"] = ctx.uses_grid_sync
     if ctx.mesh is not None:
         k.attrs["extra_params"] = list(k.attrs.get("extra_params", [])) + ctx.mesh.extra_params()
         k.attrs["mesh"] = ctx.mesh.meta()

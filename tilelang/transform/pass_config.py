@@ -1,7 +1,14 @@
 """Pass configuration keys (reference ``tilelang/transform/pass_config.py:6-153``).
 
-Keys that only make sense on NVIDIA (TMA, WGMMA, warp specialisation, ptxas) are accepted and
-ignored so reference programs run unchanged; gfx950-specific keys are added at the end.
+Every key is either implemented on gfx950 or rejected (``validate_pass_configs``, run by
+``tilelang.lower``): a program never gets a silently different compile.  Three kinds:
+
+* implemented — changes what the compiler does (table ``EFFECT`` below says how);
+* satisfied by construction — the reference uses the key to switch OFF an NVIDIA-only feature
+  (TMA, WGMMA, warp specialisation, 256-bit vectors) or a TVM pass this compiler does not have;
+  the "off" value is what gfx950 always does and is accepted, asking for the feature raises;
+* unsupported — raises ``NotImplementedError`` (``tl.ptxas_register_usage_level``,
+  ``tl.storage_rewrite_detect_inplace``) with the gfx950 alternative in the message.
 """
 from enum import Enum
 
@@ -31,6 +38,80 @@ class PassConfigKey(str, Enum):
     # gfx950 additions
     TL_DISABLE_GLDS = "tl.disable_glds"            # stage through registers instead of LDS-DMA
     TL_MIN_WAVES_PER_EU = "tl.min_waves_per_eu"    # second __launch_bounds__ argument
+    TL_LDS_REUSE = "tl.lds_reuse"                  # liveness-based LDS arena sharing (default on)
 
     def __str__(self):
         return self.value
+
+
+# what each implemented key does on gfx950
+EFFECT = {
+    "tl.enable_fast_math": "exp/log/exp2/log2/sin/cos on the hardware transcendental unit (codegen/hip.py)",
+    "tl.disable_fast_math": "forces the precise OCML math even if tl.enable_fast_math is set",
+    "tl.config_index_bitwidth": "32 or 64: width of global-memory offsets (default: 64 only for tensors of "
+                                ">= 2^31 elements; the launcher refuses tensors too large for a 32-bit kernel)",
+    "tl.disable_safe_memory_legalize": "no bounds guards on global accesses",
+    "tl.enable_aggressive_shared_memory_merge": "LDS buffers of disjoint live ranges share the arena even "
+                                                "across pipelined loops' stage buffers",
+    "tl.lds_reuse": "liveness-based LDS arena sharing (False: every shared buffer gets its own bytes)",
+    "tl.disable_thread_storage_sync": "no automatic __syncthreads insertion",
+    "tl.force_let_inline": "every let binding inside a kernel is substituted into its uses",
+    "tl.layout_visualization_enable": "dump the inferred fragment / LDS layouts (tilelang.analysis.layout_visual)",
+    "tl.layout_visualization_formats": "'txt' (default), 'svg', 'png' or 'all' for the layout dump",
+    "tl.dynamic_alignment": "dynamic shape extents are multiples of N (vectorised accesses on dynamic dims)",
+    "tir.disable_vectorize": "scalar (1-element) accesses in every lowered loop and copy",
+    "tir.use_async_copy": "False: stage tiles through registers instead of LDS-DMA (= tl.disable_glds)",
+    "tl.disable_glds": "stage tiles through registers instead of LDS-DMA",
+    "tl.min_waves_per_eu": "second __launch_bounds__ argument (register budget for N waves per SIMD)",
+}
+
+# NVIDIA-only features / TVM passes that do not exist here: the value meaning "off" is what
+# gfx950 always does
+SATISFIED = {
+    "tl.disable_warp_specialized": True,
+    "tl.disable_tma_lower": True,
+    "tl.disable_wgmma": True,
+    "tl.disable_vectorize_256": True,     # gfx950 vector memory accesses are at most 128 bits
+    "tir.merge_static_smem": True,        # all LDS is always one arena
+    "tir.disable_cse_tir": True,          # no TIR CSE pass (clang does CSE on the HIP source)
+    "tl.disable_dynamic_tail_split": True,  # dynamic tails use guarded accesses, never a split loop
+}
+
+UNSUPPORTED = {
+    "tl.ptxas_register_usage_level": "ptxas is NVIDIA-only; bound gfx950 registers with "
+                                     "pass_configs={'tl.min_waves_per_eu': N}",
+    "tl.storage_rewrite_detect_inplace": "in-place buffer reuse detection is not implemented; LDS reuse is "
+                                         "liveness based ('tl.lds_reuse')",
+}
+
+DEFAULTS = {"tl.disable_dynamic_tail_split": False, "tir.merge_static_smem": False,
+            "tir.disable_cse_tir": False, "tl.disable_warp_specialized": False,
+            "tl.disable_tma_lower": False, "tl.disable_wgmma": False, "tl.disable_vectorize_256": False}
+
+
+def validate_pass_configs(cfg: dict) -> dict:
+    """Normalise and check ``pass_configs``; raises for unknown keys and unsupported values."""
+    out = {}
+    known = {k.value for k in PassConfigKey}
+    for k, v in dict(cfg or {}).items():
+        k = str(k)
+        if k not in known:
+            if k.startswith("cuda."):
+                raise ValueError(f"pass config {k!r} is CUDA-only; this compiler targets gfx950 only")
+            raise ValueError(f"unknown pass config key {k!r}; valid keys: {sorted(known)}")
+        if k in UNSUPPORTED and v not in (None, False, 0):
+            raise NotImplementedError(f"pass config {k!r}: {UNSUPPORTED[k]}")
+        if k in SATISFIED and v is not None and bool(v) != SATISFIED[k] and bool(v) != DEFAULTS.get(k, False):
+            raise NotImplementedError(f"pass config {k}={v!r} asks for an NVIDIA-only feature that gfx950 does not have")
+        if k == "tl.config_index_bitwidth" and v not in (None, 0, 32, 64):
+            raise ValueError(f"tl.config_index_bitwidth must be 32 or 64, got {v!r}")
+        if k == "tl.layout_visualization_formats" and v is not None:
+            fmts = {f.strip() for f in str(v).split(",")}
+            if not fmts <= {"txt", "svg", "png", "pdf", "all"}:
+                raise ValueError(f"tl.layout_visualization_formats: unknown format in {v!r}")
+        out[k] = v
+    if out.get("tir.use_async_copy") is False:
+        out["tl.disable_glds"] = True
+    if out.get("tl.disable_fast_math"):
+        out["tl.enable_fast_math"] = False
+    return out

@@ -93,7 +93,7 @@ def _stmt_access(s, managed) -> Tuple[Set, Set, bool]:
     elif isinstance(s, S.EvaluateStmt):
         _expr_reads(s.expr, r)
         from ..ir.expr import Call
-        if isinstance(s.expr, Call) and s.expr.op == "tl.sync_threads":
+        if isinstance(s.expr, Call) and s.expr.op in ("tl.sync_threads", "tl.sync_grid"):
             return r, w, True
         if isinstance(s.expr, Call) and s.expr.op.startswith("tl.atomic"):
             a0 = s.expr.args[0]
@@ -221,18 +221,81 @@ class ThreadSync:
 
 
 def _leaves(s):
+    """Leaf statements in program order; control expressions (if / while conditions, loop
+    bounds) appear as ``EvaluateStmt`` pseudo-leaves so their LDS reads are seen too."""
     if s is None:
         return
     if isinstance(s, S.SeqStmt):
         for c in s.stmts:
             yield from _leaves(c)
-    elif isinstance(s, (S.ForStmt, S.WhileStmt)):
+    elif isinstance(s, S.ForStmt):
+        yield S.EvaluateStmt(s.min)
+        yield S.EvaluateStmt(s.extent)
+        yield from _leaves(s.body)
+    elif isinstance(s, S.WhileStmt):
+        yield S.EvaluateStmt(s.cond)
         yield from _leaves(s.body)
     elif isinstance(s, S.IfStmt):
+        yield S.EvaluateStmt(s.cond)
         yield from _leaves(s.then_body)
         yield from _leaves(s.else_body)
+    elif isinstance(s, S.AttrStmt):
+        yield from _leaves(s.body)
     else:
         yield s
+
+
+_THREAD_NAMES = {"tid_", "tx", "ty", "tz", "lane_", "wave_"}
+
+
+def _thread_dependent(e, tvars) -> bool:
+    from ..ir.expr import Var
+    if not isinstance(e, PrimExpr):
+        return False
+    for n in post_order(e):
+        if isinstance(n, Var) and (n in tvars or n.name in _THREAD_NAMES):
+            return True
+        if isinstance(n, BufferLoad) and not _shared(n.buffer) and getattr(n.buffer, "scope", "") != "global":
+            return True  # a register value may differ per thread
+    return False
+
+
+def _has_barrier(s) -> bool:
+    for x in _leaves(s):
+        if isinstance(x, L.CallStmt) and x.name in _BARRIERS:
+            return True
+        if isinstance(x, S.EvaluateStmt):
+            from ..ir.expr import Call
+            if isinstance(x.expr, Call) and x.expr.op in ("tl.sync_threads", "tl.sync_grid"):
+                return True
+    return False
+
+
+def check_divergent_barriers(s, tvars=(), where="kernel"):
+    """A block barrier inside a thread-dependent branch or loop deadlocks the workgroup on the
+    GPU: refuse to emit such code (the reference's ThreadSync has the same rule)."""
+    if s is None:
+        return
+    if isinstance(s, S.SeqStmt):
+        for c in s.stmts:
+            check_divergent_barriers(c, tvars, where)
+    elif isinstance(s, S.KernelStmt):
+        check_divergent_barriers(s.body, tuple(s.thread_vars or ()), where)
+    elif isinstance(s, S.IfStmt):
+        if _thread_dependent(s.cond, tvars) and (_has_barrier(s.then_body) or _has_barrier(s.else_body)):
+            raise RuntimeError(f"{where}: a block barrier is required inside a thread-dependent branch "
+                               f"(if {s.cond}); move the shared-memory communication out of the branch")
+        check_divergent_barriers(s.then_body, tvars, where)
+        check_divergent_barriers(s.else_body, tvars, where)
+    elif isinstance(s, S.ForStmt):
+        if (_thread_dependent(s.min, tvars) or _thread_dependent(s.extent, tvars)) and _has_barrier(s.body):
+            raise RuntimeError(f"{where}: a block barrier is required inside a loop with a thread-dependent "
+                               f"trip count ({s.var})")
+        check_divergent_barriers(s.body, tvars, where)
+    elif isinstance(s, S.WhileStmt):
+        check_divergent_barriers(s.body, tvars, where)
+    elif isinstance(s, S.AttrStmt):
+        check_divergent_barriers(s.body, tvars, where)
 
 
 def _buffers_of(x):
@@ -257,4 +320,6 @@ def insert_thread_sync(kernel: S.KernelStmt) -> S.KernelStmt:
     ts = ThreadSync()
     out = []
     k, _ = ts.scan_one(kernel, _State(), out)
+    if not getattr(k, "is_cpu", False):
+        check_divergent_barriers(k)
     return k
