@@ -41,11 +41,14 @@ REF_ATTN_TF = 497.13
 PEAK_BF16_TF = 2500.0  # MI355X dense fp16/bf16 MFMA (AMD spec, no sparsity)
 
 GEMM_CFG = dict(M=4096, N=4096, K=4096, block_M=256, block_N=256, block_K=64, threads=512, num_stages=2)
-ATTN_CFG = dict(batch=1, heads=64, seq_len=4096, dim=128, block_M=256, block_N=64, threads=512, num_stages=2)
+# FA tile (scripts/sweep_fa.py, profiles/r2/fa_sweep.log): 256x64, 8 waves, Q in registers, 3-stage K/V ring
+ATTN_CFG = dict(batch=1, heads=64, seq_len=4096, dim=128, block_M=256, block_N=64, threads=512, num_stages=3,
+                q_in_regs=True)
 MOE_CFG = dict(tokens=2048, hidden=4096, ffn=2048, experts=8, topk=2)
 # --device cpu (CI plumbing run on the CPU target under gloo): same program, tiny shapes
 TINY = dict(gemm=dict(M=128, N=128, K=128, block_M=64, block_N=64, block_K=32, threads=128, num_stages=2),
-            attn=dict(batch=1, heads=2, seq_len=128, dim=64, block_M=64, block_N=32, threads=128, num_stages=2),
+            attn=dict(batch=1, heads=2, seq_len=128, dim=64, block_M=64, block_N=32, threads=128, num_stages=2,
+                      q_in_regs=True),
             moe=dict(tokens=32, hidden=64, ffn=64, experts=8, topk=2))
 
 
@@ -87,7 +90,7 @@ def build_attn(device="cuda", a=None):
     from example_mha_fwd import flashattn
     a = a or ATTN_CFG
     f = flashattn.get_tir(a["batch"], a["heads"], a["seq_len"], a["dim"], False, 1, a["block_M"], a["block_N"],
-                          a["threads"], a["num_stages"], "bfloat16")
+                          a["threads"], a["num_stages"], "bfloat16", True, a.get("q_in_regs", False))
     k = tilelang.compile(f, out_idx=[3], target=_target(device), pass_configs=flashattn.pass_configs)
     shp = (a["batch"], a["seq_len"], a["heads"], a["dim"])
     return k, tuple(torch.randn(shp, device=device).to(torch.bfloat16) for _ in range(3))
@@ -98,8 +101,11 @@ def build_moe(mesh, device="cuda", m=None):
     from tilelang.models.moe import MoEConfig, MoELayer
     m = m or MOE_CFG
     dt = torch.bfloat16 if device != "cpu" else torch.float32
-    bm = 128 if device != "cpu" else 16
-    cfg = MoEConfig(hidden=m["hidden"], ffn=m["ffn"], n_experts=m["experts"], topk=m["topk"], dtype=dt, block_M=bm)
+    bm = 256 if device != "cpu" else 16
+    # expert GEMM tile: 256x256x64, 8 waves, 2-stage LDS-DMA (scripts/prof_moe.py --sweep, profiles/r2)
+    gc = dict(block_N=256, block_K=64, num_stages=2, threads=512) if device != "cpu" else None
+    cfg = MoEConfig(hidden=m["hidden"], ffn=m["ffn"], n_experts=m["experts"], topk=m["topk"], dtype=dt, block_M=bm,
+                    gemm_cfg=gc)
     layer = MoELayer(cfg, "ep" if mesh is not None else "local", mesh=mesh, device=device)
     x = torch.randn(m["tokens"], m["hidden"], device=device).to(dt)
     return layer, x

@@ -21,10 +21,12 @@ FAST_MATH = {tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True}
 
 @tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
 def flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=128, block_N=64, threads=256,
-              num_stages=2, dtype="bfloat16", lazy_rescale=True):
+              num_stages=2, dtype="bfloat16", lazy_rescale=True, q_in_regs=False):
     """``lazy_rescale``: a row keeps its running max until a new score exceeds it by 2^8, so the
     O accumulator is rescaled only on those (rare, after the first tiles) steps; a wave skips
-    the rescale when none of its rows moved."""
+    the rescale when none of its rows moved.  ``q_in_regs``: Q is loaded once into the MFMA
+    A-operand registers of the wave that owns its rows (no per-tile LDS re-read of Q, and the
+    LDS it used goes to deeper K/V staging)."""
     scale = (1.0 / dim)**0.5 * 1.44269504  # log2(e): softmax via exp2
     head_kv = heads // groups
     q_shape = [batch, seq_len, heads, dim]
@@ -39,7 +41,10 @@ def flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=128
             Output: T.Tensor(q_shape, dtype),
     ):
         with T.Kernel(T.ceildiv(seq_len, block_M), heads, batch, threads=threads) as (bx, by, bz):
-            Q_shared = T.alloc_shared([block_M, dim], dtype)
+            if q_in_regs:
+                Q_shared = T.alloc_fragment([block_M, dim], dtype)
+            else:
+                Q_shared = T.alloc_shared([block_M, dim], dtype)
             K_shared = T.alloc_shared([block_N, dim], dtype)
             V_shared = T.alloc_shared([block_N, dim], dtype)
             acc_s = T.alloc_fragment([block_M, block_N], accum_dtype)

@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/${TAG:-moe}
 mkdir -p $OUT
-timeout -k 10 500 python scripts/prof_moe.py 20 --check --sweep > $OUT/moe.log 2>&1 || { tail -30 $OUT/moe.log; exit 1; }
+timeout -k 10 500 python scripts/prof_moe.py 20 --check > $OUT/moe.log 2>&1 || { tail -30 $OUT/moe.log; exit 1; }
 cat $OUT/moe.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o moe --output-format csv -- python3 $ROOT/scripts/prof_moe.py 10 > $OUT/prof.log 2>&1 || { tail -30 $OUT/prof.log; exit 1; }

@@ -36,7 +36,8 @@ from tilelang.models.moe import moe_reference, init_moe_weights  # noqa: E402
 run(layer, x, "default " + str(layer.cfg.gemm_cfg))
 if "--check" in sys.argv:
     out = layer(x).float()
-    ref = moe_reference(x, layer.gate_w, layer.w1, layer.w2, layer.cfg.topk)
+    g, w1, w2 = (t.to("cuda") for t in init_moe_weights(layer.cfg))
+    ref = moe_reference(x, g, w1, w2, layer.cfg.topk)
     print("max abs err", (out - ref).abs().max().item(), "ref max", ref.abs().max().item(), flush=True)
 if "--sweep" in sys.argv:
     for bm in (128, 256):

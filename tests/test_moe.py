@@ -80,6 +80,6 @@ def test_moe_layer_gpu():
     x = torch.randn(1000, cfg.hidden, device="cuda").to(cfg.dtype)
     layer = MoELayer(cfg, "local", device="cuda")
     out = layer(x).float()
-    g, w1, w2 = layer.gate_w, layer.w1, layer.w2
+    g, w1, w2 = (t.to("cuda") for t in init_moe_weights(cfg))
     ref = moe_reference(x, g, w1, w2, cfg.topk)
     torch.testing.assert_close(out, ref, rtol=3e-2, atol=3e-2 * ref.abs().max().item())

@@ -105,7 +105,9 @@ class MoELayer(torch.nn.Module):
             f = F // W
             w1 = torch.cat([w1[:, r * f:(r + 1) * f], w1[:, F + r * f:F + (r + 1) * f]], 1)
             w2 = w2[:, :, r * f:(r + 1) * f]
-        self.w1 = w1.contiguous().to(device)
+        # kernel layout: gate/up rows interleaved so the SwiGLU activation fuses into GEMM-1
+        from ..ops.moe import swiglu_interleave
+        self.w1 = swiglu_interleave(w1.contiguous()).to(device)
         self.w2 = w2.contiguous().to(device)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -114,7 +116,8 @@ class MoELayer(torch.nn.Module):
         ids, wts = K.route(x, self.gate_w, cfg.topk)
         if self.parallel in ("local", "tp"):
             y, dest = K.expert_ffn_padded(x, ids, cfg.topk, self.w1, self.w2, cfg.block_M,
-                                          reduce_mesh="all" if self.parallel == "tp" else None, cfg=cfg.gemm_cfg)
+                                          reduce_mesh="all" if self.parallel == "tp" else None, cfg=cfg.gemm_cfg,
+                                          w1_interleaved=True)
             return K.combine(y, dest, wts)
         y = self._ep(x, ids)
         return K.combine(y, torch.arange(y.shape[0], device=x.device, dtype=torch.int32), wts)
@@ -138,7 +141,7 @@ class MoELayer(torch.nn.Module):
         recv, rc = C.all_to_all_v(torch.cat([payload, local_e], 1), send_counts)
         recv_rows, recv_e = recv[:, :-1].contiguous(), recv[:, -1].round().to(torch.int32)
         y_pad, dest = K.expert_ffn_padded(recv_rows, recv_e, 1, self.w1, self.w2, self.cfg.block_M,
-                                          cfg=self.cfg.gemm_cfg)
+                                          cfg=self.cfg.gemm_cfg, w1_interleaved=True)
         y_local = y_pad[dest.long()]
         y_back, _ = C.all_to_all_v(y_local, rc)
         y = torch.empty_like(y_back)

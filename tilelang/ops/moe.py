@@ -55,7 +55,7 @@ def router_topk_kernel(n_tok: int, E: int, topk: int, target: str, threads: int 
     top-k weights equal ``exp(l_k - m) / sum_k' exp(l_k' - m)`` (the softmax denominator cancels)."""
 
     @T.prim_func
-    def main(L: T.Tensor((n_tok, E), "float32"), ids: T.Tensor((n_tok, topk), "int32"),
+    def moe_router_topk(L: T.Tensor((n_tok, E), "float32"), ids: T.Tensor((n_tok, topk), "int32"),
              w: T.Tensor((n_tok, topk), "float32")):
         with T.Kernel(T.ceildiv(n_tok, threads), threads=threads) as bx:
             for i in T.Parallel(threads):
@@ -87,7 +87,7 @@ def router_topk_kernel(n_tok: int, E: int, topk: int, target: str, threads: int 
                         ids[bx * threads + i, k] = sel[k]
                         w[bx * threads + i, k] = p[k] / tot
 
-    return tilelang.compile(main, out_idx=None, target=target)
+    return tilelang.compile(moe_router_topk, out_idx=None, target=target)
 
 
 def max_padded_rows(n_assign: int, E: int, block_M: int) -> int:
@@ -113,7 +113,7 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
     c = -(-n // threads)
 
     @T.prim_func
-    def main(expert_ids: T.Tensor((n,), "int32"), dest: T.Tensor((n,), "int32"),
+    def moe_align(expert_ids: T.Tensor((n,), "int32"), dest: T.Tensor((n,), "int32"),
              row_src: T.Tensor((max_rows,), "int32"), tile_expert: T.Tensor((n_tiles,), "int32"),
              counts: T.Tensor((E,), "int32")):
         # written with T.Parallel (one iteration per thread on the GPU, a serial loop on the
@@ -174,28 +174,34 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                     dest[j] = start[expert_ids[j]] + slot
                     row_src[start[expert_ids[j]] + slot] = j // div
 
-    return tilelang.compile(main, out_idx=None, target=target)
+    return tilelang.compile(moe_align, out_idx=None, target=target)
 
 
 @functools.lru_cache(maxsize=None)
 def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target: str, block_M: int = 128,
                        block_N: int = 128, block_K: int = 64, num_stages: int = 2, threads: int = 256,
                        reduce_mesh: Optional[str] = None, mesh_shape: Optional[Tuple[int, int]] = None,
-                       n_src: Optional[int] = None):
+                       n_src: Optional[int] = None, swiglu: bool = False):
     """``C[r, :] = A[src(r), :] @ W[tile_expert[r // block_M]].T`` for every non-empty row tile.
 
     ``n_src`` given: A is the ``[n_src, K]`` source-row matrix and row ``r`` of the padded row
     space reads ``A[row_src[r]]`` (``-1`` = padding = zeros), gathered straight into LDS.
     ``reduce_mesh`` ("all"/"h"/"v"): tensor-parallel partial products are summed across the
-    mesh inside the kernel (``T.comm.all_reduce_tile`` on the fp32 accumulator tile)."""
+    mesh inside the kernel (``T.comm.all_reduce_tile`` on the fp32 accumulator tile).
+    ``swiglu``: W's rows are interleaved in groups of 4 (gate 2p, gate 2p+1, up 2p, up 2p+1, see
+    ``swiglu_interleave``) and the epilogue writes ``C[r, p] = silu(gate) * up`` ([max_rows, N/2]):
+    the 4 columns of such a group sit in the registers of ONE lane (MFMA C layout), so the
+    activation needs no data movement and no separate kernel."""
     n_tiles = max_rows // block_M
     accum = "float32"
     a_rows = n_src if n_src is not None else max_rows
+    n_out = N // 2 if swiglu else N
+    assert not (swiglu and reduce_mesh), "the SwiGLU epilogue belongs to the first expert GEMM"
 
     @T.prim_func
-    def main(A: T.Tensor((a_rows, K), dtype), W: T.Tensor((E, N, K), dtype),
+    def moe_expert_gemm(A: T.Tensor((a_rows, K), dtype), W: T.Tensor((E, N, K), dtype),
              tile_expert: T.Tensor((n_tiles,), "int32"), row_src: T.Tensor((max_rows,), "int32"),
-             C: T.Tensor((max_rows, N), dtype)):
+             C: T.Tensor((max_rows, n_out), dtype)):
         with T.Kernel(n_tiles, T.ceildiv(N, block_N), threads=threads) as (bx, by):
             A_s = T.alloc_shared((block_M, block_K), dtype)
             W_s = T.alloc_shared((block_N, block_K), dtype)
@@ -212,7 +218,13 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
                             T.copy(A[bx * block_M, k * block_K], A_s)
                         T.copy(W[e, by * block_N, k * block_K], W_s)
                         T.gemm(A_s, W_s, C_l, transpose_B=True)
-                    T.copy(C_l, C[bx * block_M, by * block_N])
+                    if swiglu:
+                        for i, j in T.Parallel(block_M, block_N):
+                            if j % 4 < 2:
+                                C[bx * block_M + i, by * (block_N // 2) + (j // 4) * 2 + j % 4] = T.Cast(
+                                    dtype, C_l[i, j] / (1.0 + T.exp(-C_l[i, j])) * C_l[i, j + 2])
+                    else:
+                        T.copy(C_l, C[bx * block_M, by * block_N])
             else:
                 # every rank holds the same tile table (replicated tokens), so all ranks take
                 # the same branch and meet at the same mesh op
@@ -230,7 +242,18 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
                     T.comm.all_reduce_tile(C_l, C_r, "sum", reduce_mesh)
                     T.copy(C_r, C[bx * block_M, by * block_N])
 
-    return tilelang.compile(main, out_idx=None, target=target)
+    return tilelang.compile(moe_expert_gemm, out_idx=None, target=target,
+                            pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True} if swiglu else None)
+
+
+def swiglu_interleave(w1: torch.Tensor) -> torch.Tensor:
+    """``[E, 2F, H]`` (gate rows then up rows) -> the row order of the fused SwiGLU GEMM:
+    groups of 4 rows (gate 2p, gate 2p+1, up 2p, up 2p+1)."""
+    E, F2, H = w1.shape
+    F = F2 // 2
+    g = w1[:, :F].reshape(E, F // 2, 2, H)
+    u = w1[:, F:].reshape(E, F // 2, 2, H)
+    return torch.cat([g, u], 2).reshape(E, F2, H).contiguous()
 
 
 def _mesh_shape():
@@ -245,14 +268,14 @@ def silu_mul_kernel(rows: int, F: int, dtype: str, target: str, block_R: int = 3
     assert F % block_F == 0 and rows % block_R == 0
 
     @T.prim_func
-    def main(H: T.Tensor((rows, 2 * F), dtype), O: T.Tensor((rows, F), dtype)):
+    def moe_silu_mul(H: T.Tensor((rows, 2 * F), dtype), O: T.Tensor((rows, F), dtype)):
         with T.Kernel(rows // block_R, F // block_F, threads=threads) as (bx, by):
             for i, j in T.Parallel(block_R, block_F):
                 g = T.Cast("float32", H[bx * block_R + i, by * block_F + j])
                 u = T.Cast("float32", H[bx * block_R + i, F + by * block_F + j])
                 O[bx * block_R + i, by * block_F + j] = T.Cast(dtype, g / (1.0 + T.exp(-g)) * u)
 
-    return tilelang.compile(main, out_idx=None, target=target,
+    return tilelang.compile(moe_silu_mul, out_idx=None, target=target,
                             pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True})
 
 
@@ -264,7 +287,7 @@ def combine_kernel(n_tok: int, H: int, topk: int, max_rows: int, dtype: str, tar
     assert H % block_H == 0
 
     @T.prim_func
-    def main(Y: T.Tensor((max_rows, H), dtype), dest: T.Tensor((n_tok * topk,), "int32"),
+    def moe_combine(Y: T.Tensor((max_rows, H), dtype), dest: T.Tensor((n_tok * topk,), "int32"),
              w: T.Tensor((n_tok, topk), "float32"), out: T.Tensor((n_tok, H), dtype)):
         with T.Kernel(n_tok, H // block_H, threads=threads) as (bx, by):
             acc = T.alloc_fragment((block_H,), "float32")
@@ -277,7 +300,7 @@ def combine_kernel(n_tok: int, H: int, topk: int, max_rows: int, dtype: str, tar
             for h in T.Parallel(block_H):
                 out[bx, by * block_H + h] = T.Cast(dtype, acc[h])
 
-    return tilelang.compile(main, out_idx=None, target=target)
+    return tilelang.compile(moe_combine, out_idx=None, target=target)
 
 
 def route(x: torch.Tensor, gate_w: torch.Tensor, topk: int):
@@ -312,9 +335,10 @@ def pack_by_expert(expert_ids: torch.Tensor, E: int, block_M: int, max_rows: int
 
 def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int, w1: torch.Tensor,
                       w2: torch.Tensor, block_M: int = 128, reduce_mesh: Optional[str] = None,
-                      cfg: Optional[dict] = None):
+                      cfg: Optional[dict] = None, w1_interleaved: bool = False):
     """SwiGLU experts for the assignments ``expert_ids[n]`` (assignment j reads ``src_rows[j // div]``).
-    Returns ``(Y [max_rows, H], dest [n])``: assignment j's result is row ``dest[j]`` of Y."""
+    Returns ``(Y [max_rows, H], dest [n])``: assignment j's result is row ``dest[j]`` of Y.
+    ``w1_interleaved``: ``w1`` is in ``swiglu_interleave`` row order (fused activation)."""
     cfg = dict(cfg or {})
     E, F2, H = w1.shape
     F = F2 // 2
@@ -327,11 +351,16 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
     if src_rows.shape[0] != n_src:
         src_rows = torch.cat([src_rows, src_rows.new_zeros(n_src - src_rows.shape[0], src_rows.shape[1])])
     dest, row_src, te, _ = dispatch_plan(expert_ids, E, block_M, max_rows, div, stable=reduce_mesh is not None)
-    k1 = expert_gemm_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, **cfg)
-    h = torch.empty(max_rows, F2, dtype=src_rows.dtype, device=dev)
-    k1(src_rows.contiguous(), w1, te, row_src, h)
     act = torch.empty(max_rows, F, dtype=src_rows.dtype, device=dev)
-    silu_mul_kernel(max_rows, F, tgt, target)(h, act)
+    if w1_interleaved:
+        # gate/up rows interleaved: the activation is the first GEMM's epilogue
+        k1 = expert_gemm_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, swiglu=True, **cfg)
+        k1(src_rows.contiguous(), w1, te, row_src, act)
+    else:
+        k1 = expert_gemm_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, **cfg)
+        h = torch.empty(max_rows, F2, dtype=src_rows.dtype, device=dev)
+        k1(src_rows.contiguous(), w1, te, row_src, h)
+        silu_mul_kernel(max_rows, F, tgt, target)(h, act)
     k2 = expert_gemm_kernel(max_rows, F, H, E, tgt, target, block_M, reduce_mesh=reduce_mesh,
                             mesh_shape=_mesh_shape() if reduce_mesh else None, **cfg)
     y = torch.empty(max_rows, H, dtype=src_rows.dtype, device=dev)

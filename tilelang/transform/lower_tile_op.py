@@ -321,6 +321,25 @@ class _FragResolver:
         return result
 
 
+def _fold_guard(c):
+    """True / False when a guard condition is decided regardless of the thread, else None."""
+    from ..ir.expr import modular
+    v = as_int(c)
+    if v is not None:
+        return bool(v)
+    if isinstance(c, BinOp) and c.op in ("<", "<=", ">", ">=", "==", "!=") and as_int(c.b) is not None:
+        a = c.a
+        if isinstance(a, BinOp) and a.op == "%" and as_int(a.b) is not None:
+            m = as_int(a.b)
+            coeff, base = modular(a.a)
+            if coeff % m == 0:  # a.a == base (mod m) for every thread
+                lhs = base % m
+                rhs = as_int(c.b)
+                return {"<": lhs < rhs, "<=": lhs <= rhs, ">": lhs > rhs, ">=": lhs >= rhs, "==": lhs == rhs,
+                        "!=": lhs != rhs}[c.op]
+    return None
+
+
 class _IterRewriter(Mutator):
     """Rewrite one iteration (register r) of a fragment-partitioned nest."""
 
@@ -352,6 +371,18 @@ class _IterRewriter(Mutator):
 
     def _load_sub(self, n):
         return None
+
+    def visit_IfStmt(self, s):
+        # a guard that is decided by the register index alone (e.g. ``j % 4 < 2`` where the 4
+        # columns of a lane are its registers) folds away per iteration, so an access it protects
+        # (``C[i, j + 2]``, owned by this thread only when the guard holds) is never lowered
+        # for the registers where it does not hold
+        c = _fold_guard(substitute(s.cond, self.vmap))
+        if c is False:
+            return self.stmt(s.else_body) if s.else_body is not None else S.SeqStmt([])
+        if c is True:
+            return self.stmt(s.then_body)
+        return S.IfStmt(self.expr(s.cond), self.stmt(s.then_body), self.stmt(s.else_body))
 
     def expr(self, e):
         if not isinstance(e, PrimExpr):

@@ -248,16 +248,40 @@ def _leaves(s):
 _THREAD_NAMES = {"tid_", "tx", "ty", "tz", "lane_", "wave_"}
 
 
-def _thread_dependent(e, tvars) -> bool:
+def _thread_dependent(e, tvars, uniform=()) -> bool:
+    """May ``e`` differ between the threads of a block?  Thread ids do; a register variable does
+    unless every store to it is block-uniform (``uniform``); a memory load does iff its address does."""
     from ..ir.expr import Var
     if not isinstance(e, PrimExpr):
         return False
     for n in post_order(e):
         if isinstance(n, Var) and (n in tvars or n.name in _THREAD_NAMES):
             return True
-        if isinstance(n, BufferLoad) and not _shared(n.buffer) and getattr(n.buffer, "scope", "") != "global":
-            return True  # a register value may differ per thread
+        if isinstance(n, BufferLoad):
+            sc = getattr(n.buffer, "scope", "")
+            if sc not in ("global", "shared") and n.buffer not in uniform:
+                return True  # a register value may differ per thread
     return False
+
+
+def _uniform_registers(k: S.KernelStmt, tvars) -> set:
+    """Register buffers (``T.alloc_var`` / locals) whose every store is block-uniform (fixpoint)."""
+    stores = {}
+    for x in S.walk(k):
+        if isinstance(x, S.StoreStmt) and getattr(x.buffer, "scope", "") not in ("global", "shared"):
+            stores.setdefault(x.buffer, []).append(x)
+    uniform = set(stores)
+    changed = True
+    while changed:
+        changed = False
+        for b in list(uniform):
+            for st in stores[b]:
+                if _thread_dependent(st.value, tvars, uniform) or \
+                        any(_thread_dependent(i, tvars, uniform) for i in st.indices):
+                    uniform.discard(b)
+                    changed = True
+                    break
+    return uniform
 
 
 def _has_barrier(s) -> bool:
@@ -271,31 +295,36 @@ def _has_barrier(s) -> bool:
     return False
 
 
-def check_divergent_barriers(s, tvars=(), where="kernel"):
+def check_divergent_barriers(s, tvars=(), where="kernel", uniform=()):
     """A block barrier inside a thread-dependent branch or loop deadlocks the workgroup on the
     GPU: refuse to emit such code (the reference's ThreadSync has the same rule)."""
     if s is None:
         return
     if isinstance(s, S.SeqStmt):
         for c in s.stmts:
-            check_divergent_barriers(c, tvars, where)
+            check_divergent_barriers(c, tvars, where, uniform)
     elif isinstance(s, S.KernelStmt):
-        check_divergent_barriers(s.body, tuple(s.thread_vars or ()), where)
+        tv = tuple(s.thread_vars or ())
+        check_divergent_barriers(s.body, tv, where, _uniform_registers(s, tv))
     elif isinstance(s, S.IfStmt):
-        if _thread_dependent(s.cond, tvars) and (_has_barrier(s.then_body) or _has_barrier(s.else_body)):
+        if _thread_dependent(s.cond, tvars, uniform) and (_has_barrier(s.then_body) or _has_barrier(s.else_body)):
             raise RuntimeError(f"{where}: a block barrier is required inside a thread-dependent branch "
                                f"(if {s.cond}); move the shared-memory communication out of the branch")
-        check_divergent_barriers(s.then_body, tvars, where)
-        check_divergent_barriers(s.else_body, tvars, where)
+        check_divergent_barriers(s.then_body, tvars, where, uniform)
+        check_divergent_barriers(s.else_body, tvars, where, uniform)
     elif isinstance(s, S.ForStmt):
-        if (_thread_dependent(s.min, tvars) or _thread_dependent(s.extent, tvars)) and _has_barrier(s.body):
+        if (_thread_dependent(s.min, tvars, uniform) or _thread_dependent(s.extent, tvars, uniform)) and \
+                _has_barrier(s.body):
             raise RuntimeError(f"{where}: a block barrier is required inside a loop with a thread-dependent "
                                f"trip count ({s.var})")
-        check_divergent_barriers(s.body, tvars, where)
+        check_divergent_barriers(s.body, tvars, where, uniform)
     elif isinstance(s, S.WhileStmt):
-        check_divergent_barriers(s.body, tvars, where)
+        if _thread_dependent(s.cond, tvars, uniform) and _has_barrier(s.body):
+            raise RuntimeError(f"{where}: a block barrier is required inside a loop with a thread-dependent "
+                               f"condition ({s.cond})")
+        check_divergent_barriers(s.body, tvars, where, uniform)
     elif isinstance(s, S.AttrStmt):
-        check_divergent_barriers(s.body, tvars, where)
+        check_divergent_barriers(s.body, tvars, where, uniform)
 
 
 def _buffers_of(x):
