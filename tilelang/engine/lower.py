@@ -147,13 +147,15 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
 def lower(func: S.PrimFunc, target="auto", target_host=None, pass_configs: Optional[dict] = None,
           enable_host_codegen=False, enable_device_compile=False, runtime_only=False) -> CompiledArtifact:
     t0 = time.perf_counter()
-    target = determine_target(target)
+    import copy
+    target = copy.copy(determine_target(target))  # per-compile options are set on the target below
     cfg = validate_pass_configs({str(k): v for k, v in dict(pass_configs or {}).items()})
     kernels = _find_kernels(func.body)
     if any(k.is_cpu for k in kernels) and target.kind != "cpu":
         target = Target("cpu", "host", target.mesh)
     if cfg.get("tl.disable_glds"):
         target.disable_glds = True
+    target.mfma_shape = cfg.get("tl.mfma_shape")
     timings: Dict[str, float] = {}
     dks = []
     for i, k in enumerate(kernels):

@@ -34,6 +34,7 @@ typedef bfloat16_t bf16x4 __attribute__((ext_vector_type(4)));
 typedef short shortx4 __attribute__((ext_vector_type(4)));
 typedef short shortx8 __attribute__((ext_vector_type(8)));
 typedef int intx4 __attribute__((ext_vector_type(4)));
+typedef int intx16 __attribute__((ext_vector_type(16)));
 typedef int intx8 __attribute__((ext_vector_type(8)));
 typedef int intx2 __attribute__((ext_vector_type(2)));
 typedef unsigned uintx4 __attribute__((ext_vector_type(4)));

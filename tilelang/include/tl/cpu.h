@@ -8,6 +8,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <cmath>
+#include <type_traits>
 
 typedef _Float16 half_t;
 typedef __bf16 bfloat16_t;
@@ -164,14 +165,16 @@ template <typename T, typename V> inline T atomic_max(T* p, V v) { T o = *p; if 
 template <typename T, typename V> inline T atomic_min(T* p, V v) { T o = *p; if ((T)v < o) *p = (T)v; return o; }
 
 // C[M,N] += op(A) * op(B); C is the thread-local fp32 accumulator (row-major M x N).
-template <typename T, int M, int N, int K, int TA, int TB, int A_COLS, int B_COLS>
-inline void cpu_gemm(const T* A, const T* B, float* C) {
+template <typename T, int M, int N, int K, int TA, int TB, int A_COLS, int B_COLS, typename TC>
+inline void cpu_gemm(const T* A, const T* B, TC* C) {
+  // integer operands (int8 MFMA semantics) accumulate exactly in integers
+  typedef typename std::conditional<std::is_integral<TC>::value, long long, float>::type acc_t;
   for (int i = 0; i < M; ++i)
     for (int k = 0; k < K; ++k) {
-      const float a = TA ? (float)A[k * A_COLS + i] : (float)A[i * A_COLS + k];
+      const acc_t a = TA ? (acc_t)(float)A[k * A_COLS + i] : (acc_t)(float)A[i * A_COLS + k];
       for (int j = 0; j < N; ++j) {
-        const float b = TB ? (float)B[j * B_COLS + k] : (float)B[k * B_COLS + j];
-        C[i * N + j] += a * b;
+        const acc_t b = TB ? (acc_t)(float)B[j * B_COLS + k] : (acc_t)(float)B[k * B_COLS + j];
+        C[i * N + j] = (TC)((acc_t)C[i * N + j] + a * b);
       }
     }
 }

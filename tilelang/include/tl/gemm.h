@@ -323,3 +323,154 @@ TL_DEVICE void gemm_ss_mx(const void* __restrict__ A_, const void* __restrict__ 
 }
 
 }  // namespace tl
+
+namespace tl {
+
+// ---------------------------------------------------------------------------
+// 32x32 MFMA tiles (v_mfma_f32_32x32x16_{f16,bf16}, v_mfma_i32_32x32x32_i8) and the 16x16 int8 /
+// fp32 forms.  Operand maps (swapped issue, as gemm_ss): lane l holds operand rows (m or n)
+// l & 31 and 8 (16-bit) / 16 (8-bit) consecutive k starting at (l >> 5) * 8 / 16; the accumulator
+// (16 registers) is C[m = l & 31][n = (v & 3) + 8 (v >> 2) + 4 (l >> 5)].
+// ---------------------------------------------------------------------------
+template <typename T> struct mfma32_traits;
+template <> struct mfma32_traits<half_t> {
+  typedef halfx8 frag;
+  TL_DEVICE static floatx16 mma(frag a, frag b, floatx16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct mfma32_traits<bfloat16_t> {
+  typedef bf16x8 frag;
+  TL_DEVICE static floatx16 mma(frag a, frag b, floatx16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+
+// MN-contiguous operand of the 32x32x16 MFMA: lane (g = l >> 4, i = l & 15) needs column
+// c0 + 16 (g & 1) + i, rows k0 + 8 (g >> 1) + 0..7: two ds_read_b64_tr_b16 of 4 rows each
+template <typename T, int COLS, uint32_t SWZ>
+TL_DEVICE typename mfma32_traits<T>::frag ld_tr8_32(const T* base, int k0, int c0, int lane) {
+  typedef typename mfma32_traits<T>::frag F;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int r0 = k0 + 8 * (g >> 1) + q;
+  const int c = c0 + 16 * (g & 1) + 4 * p;
+  shortx4 lo = ld_tr4<T, COLS, SWZ>(base, r0, c);
+  shortx4 hi = ld_tr4<T, COLS, SWZ>(base, r0 + 4, c);
+  shortx8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(F, v);
+}
+
+template <typename T, int ROWS, int COLS, uint32_t SWZ, bool MN_CONTIG>
+TL_DEVICE typename mfma32_traits<T>::frag ld_operand32(const T* base, int mn0, int k0, int lane) {
+  if constexpr (!MN_CONTIG) {
+    return *reinterpret_cast<const typename mfma32_traits<T>::frag*>(
+        base + swz_offset<T, COLS, SWZ>(mn0 + (lane & 31), k0 + 8 * (lane >> 5)));
+  } else {
+    return ld_tr8_32<T, COLS, SWZ>(base, k0, mn0, lane);
+  }
+}
+
+template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TA, bool TB, int A_COLS, uint32_t SWZ_A,
+          int B_COLS, uint32_t SWZ_B>
+TL_DEVICE void gemm_ss_32(const T* __restrict__ A, const T* __restrict__ B, float* __restrict__ C) {
+  typedef mfma32_traits<T> MT;
+  typedef typename MT::frag F;
+  constexpr int WM = M / WARP_M, WN = N / WARP_N;
+  constexpr int M_REP = WM / 32, N_REP = WN / 32, KSTEPS = K / 16;
+  static_assert(WM % 32 == 0 && WN % 32 == 0 && K % 16 == 0, "MFMA 32x32x16 tiling");
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wm = wave / WARP_N, wn = wave % WARP_N;
+  floatx16* acc = reinterpret_cast<floatx16*>(C);
+#pragma unroll
+  for (int kk = 0; kk < KSTEPS; ++kk) {
+    F a[M_REP], b[N_REP];
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi)
+      a[mi] = ld_operand32<T, (TA ? K : M), A_COLS, SWZ_A, TA>(A, wm * WM + mi * 32, kk * 16, lane);
+#pragma unroll
+    for (int ni = 0; ni < N_REP; ++ni)
+      b[ni] = ld_operand32<T, (TB ? N : K), B_COLS, SWZ_B, !TB>(B, wn * WN + ni * 32, kk * 16, lane);
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < N_REP; ++ni)
+        acc[mi * N_REP + ni] = MT::mma(b[ni], a[mi], acc[mi * N_REP + ni]);
+  }
+}
+
+// int8 x int8 -> int32, both operands K-contiguous ([M][K] and [N][K] bytes in LDS).
+// MS = 16: v_mfma_i32_16x16x64_i8 (lane: row l & 15, 16 bytes at k = 16 (l >> 4));
+// MS = 32: v_mfma_i32_32x32x32_i8 (lane: row l & 31, 16 bytes at k = 16 (l >> 5)).
+template <int MS, int M, int N, int K, int WARP_M, int WARP_N, int A_COLS, uint32_t SWZ_A, int B_COLS,
+          uint32_t SWZ_B>
+TL_DEVICE void gemm_ss_i8(const int8_t* __restrict__ A_, const int8_t* __restrict__ B_, int* __restrict__ C) {
+  constexpr int WM = M / WARP_M, WN = N / WARP_N;
+  constexpr int M_REP = WM / MS, N_REP = WN / MS, KS = MS == 16 ? 64 : 32;
+  static_assert(WM % MS == 0 && WN % MS == 0 && K % KS == 0, "int8 MFMA tiling");
+  const uint8_t* A = reinterpret_cast<const uint8_t*>(A_);
+  const uint8_t* B = reinterpret_cast<const uint8_t*>(B_);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wm = wave / WARP_N, wn = wave % WARP_N;
+  const int r = lane & (MS - 1), g = MS == 16 ? (lane >> 4) : (lane >> 5);
+#pragma unroll
+  for (int kk = 0; kk < K / KS; ++kk) {
+    intx4 a[M_REP], b[N_REP];
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi)
+      a[mi] = *reinterpret_cast<const intx4*>(A + swz_offset<uint8_t, A_COLS, SWZ_A>(wm * WM + mi * MS + r,
+                                                                                       kk * KS + 16 * g));
+#pragma unroll
+    for (int ni = 0; ni < N_REP; ++ni)
+      b[ni] = *reinterpret_cast<const intx4*>(B + swz_offset<uint8_t, B_COLS, SWZ_B>(wn * WN + ni * MS + r,
+                                                                                       kk * KS + 16 * g));
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < N_REP; ++ni) {
+        if constexpr (MS == 16) {
+          intx4* acc = reinterpret_cast<intx4*>(C);
+          acc[mi * N_REP + ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni], a[mi], acc[mi * N_REP + ni], 0, 0, 0);
+        } else {
+          intx16* acc = reinterpret_cast<intx16*>(C);
+          acc[mi * N_REP + ni] = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[ni], a[mi], acc[mi * N_REP + ni], 0, 0, 0);
+        }
+      }
+  }
+}
+
+// fp32 x fp32 -> fp32 (exact f32 fmaf chain, the f32 VALU rate): v_mfma_f32_16x16x4_f32,
+// lane l holds A[m = l & 15][k = l >> 4] and B[k = l >> 4][n = l & 15]; any operand layout.
+template <int M, int N, int K, int WARP_M, int WARP_N, bool TA, bool TB, int A_COLS, int B_COLS>
+TL_DEVICE void gemm_ss_f32(const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C) {
+  constexpr int WM = M / WARP_M, WN = N / WARP_N;
+  constexpr int M_REP = WM / 16, N_REP = WN / 16;
+  static_assert(WM % 16 == 0 && WN % 16 == 0 && K % 4 == 0, "MFMA 16x16x4 f32 tiling");
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wm = wave / WARP_N, wn = wave % WARP_N;
+  const int r = lane & 15, g = lane >> 4;
+  floatx4* acc = reinterpret_cast<floatx4*>(C);
+#pragma unroll 4
+  for (int kk = 0; kk < K / 4; ++kk) {
+    float a[M_REP], b[N_REP];
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi) {
+      const int m = wm * WM + mi * 16 + r, k = kk * 4 + g;
+      a[mi] = TA ? A[k * A_COLS + m] : A[m * A_COLS + k];
+    }
+#pragma unroll
+    for (int ni = 0; ni < N_REP; ++ni) {
+      const int n = wn * WN + ni * 16 + r, k = kk * 4 + g;
+      b[ni] = TB ? B[n * B_COLS + k] : B[k * B_COLS + n];
+    }
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < N_REP; ++ni)
+        acc[mi * N_REP + ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[ni], a[mi], acc[mi * N_REP + ni], 0, 0, 0);
+  }
+}
+
+}  // namespace tl

@@ -190,6 +190,12 @@ class Printer:
                 extra += f", clear_accum={self.e(op.clear_accum)}"
             if op.k_pack != 1:
                 extra += f", k_pack={op.k_pack}"
+            if getattr(op, "mfma_shape", None):
+                extra += f", mfma_shape={op.mfma_shape!r}"
+            if getattr(op, "is_mx", False):
+                return (f"T.gemm_scaled({self.region(op.A)}, {self.region(op.B)}, {self.region(op.C)}, "
+                        f"{self.region(op.scale_A)}, {self.region(op.scale_B)}{extra}, a_format={op.a_fmt!r}, "
+                        f"b_format={op.b_fmt!r})")
             return f"T.gemm({self.region(op.A)}, {self.region(op.B)}, {self.region(op.C)}{extra})"
         if isinstance(op, O.FillOp):
             return f"T.fill({self.region(op.dst)}, {self.e(op.value)})"
@@ -222,9 +228,28 @@ class Printer:
         if isinstance(op, O.GatherRowsOp):
             return (f"T.gather_rows({self.region(op.src)}, {self.region(op.idx)}, {self.region(op.dst)}, "
                     f"row_dim={op.row_dim})")
-        if isinstance(op, O.Im2ColOp):
-            return f"T.c2d_im2col({self.region(op.img)}, {self.region(op.col)})"
-        return f"T.{k}(...)"
+        return f"T.{k}({self._generic_args(op)})"
+
+    def _generic_args(self, op) -> str:
+        """Every attribute of a tile op (regions, expressions, constants): the printed IR is the
+        kernel-cache key, so nothing that changes the generated code may be left out."""
+        parts = []
+        for name in sorted(vars(op)):
+            if name.startswith("_") or name == "plan":
+                continue
+            v = getattr(op, name)
+            if isinstance(v, BufferRegion):
+                parts.append(f"{name}={self.region(v)}")
+            elif hasattr(v, "dtype") and not isinstance(v, (int, float, str)):
+                try:
+                    parts.append(f"{name}={self.e(v)}")
+                except Exception:  # noqa: BLE001
+                    parts.append(f"{name}={v!r}")
+            elif isinstance(v, (int, float, str, bool, tuple, list, type(None))):
+                parts.append(f"{name}={v!r}")
+            else:
+                parts.append(f"{name}={type(v).__name__}")
+        return ", ".join(parts)
 
     def func(self, f: S.PrimFunc) -> str:
         params = []

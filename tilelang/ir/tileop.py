@@ -105,6 +105,7 @@ class GemmOp(TileOp):
         self.scale_A = scale_A  # block-scaled MX gemm (e8m0 scales), gfx950 only
         self.scale_B = scale_B
         self.a_fmt = self.b_fmt = None  # MX element formats ("e4m3", "e5m2", "e2m1")
+        self.mfma_shape = None  # "16x16" / "32x32" (T.gemm(mfma_shape=...))
 
     @property
     def is_mx(self) -> bool:

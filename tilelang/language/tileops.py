@@ -82,9 +82,17 @@ class GemmWarpPolicy(IntEnum):
 
 
 def gemm(A, B, C, transpose_A: bool = False, transpose_B: bool = False, policy=GemmWarpPolicy.Square,
-         clear_accum=False, k_pack: int = 1, wg_wait: int = 0, mbar=None):
+         clear_accum=False, k_pack: int = 1, wg_wait: int = 0, mbar=None, mfma_shape: Optional[str] = None):
+    """Tile GEMM ``C (+)= op(A) @ op(B)`` on the gfx950 matrix cores.  Inputs f16/bf16 (MFMA
+    16x16x32, or 32x32x16 with ``mfma_shape="32x32"`` / pass config ``tl.mfma_shape``), fp8
+    (16x16x32 / scaled 16x16x128), int8 (int32 accumulator; 16x16x64 or 32x32x32) and fp32
+    (16x16x4, exact f32).  ``wg_wait`` / ``mbar`` are NVIDIA-only and must stay at their defaults."""
+    if wg_wait not in (0, None) or mbar is not None:
+        raise NotImplementedError("T.gemm: wg_wait / mbar are WGMMA / mbarrier (NVIDIA) features")
     A, B, C = to_region(A), to_region(B), to_region(C)
-    return _emit(O.GemmOp(A, B, C, transpose_A, transpose_B, int(policy), clear_accum, k_pack, wg_wait))
+    op = O.GemmOp(A, B, C, transpose_A, transpose_B, int(policy), clear_accum, k_pack, wg_wait)
+    op.mfma_shape = mfma_shape
+    return _emit(op)
 
 
 gemm_v1 = gemm

@@ -134,6 +134,26 @@ def _read_patterns(kind: str, rows: int, cols: int, elem_bytes: int, row_base_st
             for k0 in range(0, cols, 64):
                 pats.append([(r0 + (l & 15), k0 + (l >> 4) * 16) for l in range(64)])
         return pats
+    if kind in ("k_rows_32", "k_rows_i8_32"):
+        # 32x32 MFMA K-contiguous operand: lane l reads row l & 31, 16 bytes at k-chunk (l >> 5)
+        epl = 16 // max(1, elem_bytes)
+        for r0 in range(0, min(rows, 64), 32):
+            for k0 in range(0, cols, 2 * epl):
+                pats.append([(r0 + (l & 31), k0 + (l >> 5) * epl) for l in range(64)])
+        return pats
+    if kind == "tr32":
+        # 32x32x16 MN-contiguous operand via ds_read_b64_tr_b16: lane (g, i) supplies row
+        # k0 + 8 (g >> 1) + 4 h + q, cols c0 + 16 (g & 1) + 4 p
+        for c0 in range(0, min(cols, 64), 32):
+            for k0 in range(0, rows, 16):
+                for h in range(2):
+                    p = []
+                    for l in range(64):
+                        g, i = l >> 4, l & 15
+                        q, pp = i >> 2, i & 3
+                        p.append((k0 + 8 * (g >> 1) + 4 * h + q, c0 + 16 * (g & 1) + 4 * pp))
+                    pats.append(p)
+        return pats
     if kind == "k_rows32mx":
         # fp8 operand of the block-scaled 16x16x128 MFMA in hardware K order: two b128 reads per
         # lane at byte 16g and 64 + 16g of the 128-byte K step (see tl/gemm.h gemm_ss_mx)
@@ -176,8 +196,10 @@ def _read_patterns(kind: str, rows: int, cols: int, elem_bytes: int, row_base_st
 
 
 def _instr_for(kind: str, elem_bytes: int) -> str:
-    if kind in ("k_rows32", "k_rows16", "k_rows32mx"):
+    if kind in ("k_rows32", "k_rows16", "k_rows32mx", "k_rows_32", "k_rows_i8_32"):
         return "ds_read_b128"
+    if kind == "tr32":
+        return "ds_read_b64_tr_b16"
     if kind == "k_rows":
         return "ds_read_b128" if elem_bytes == 2 else "ds_read_b64"
     return "ds_read_b64_tr_b16"

@@ -90,6 +90,73 @@ def _mx_plan(op: O.GemmOp, plan: Dict, num_threads: int, a_ext, b_ext, is_cpu: b
     return plan
 
 
+def _mfma_shape(op, target) -> str:
+    """'16x16' (default) or '32x32': ``T.gemm(..., mfma_shape=)`` > ``tl.mfma_shape`` pass config."""
+    sh = getattr(op, "mfma_shape", None) or getattr(target, "mfma_shape", None) or "16x16"
+    if sh not in ("16x16", "32x32"):
+        raise ValueError(f"mfma_shape must be '16x16' or '32x32', got {sh!r}")
+    return sh
+
+
+def _try_32x32(op: O.GemmOp, plan: Dict, nw: int):
+    """v_mfma_f32_32x32x16_{f16,bf16} plan (shared operands), or None when the tile does not fit."""
+    M, N, K = plan["M"], plan["N"], plan["K"]
+    A, B = op.A.buffer, op.B.buffer
+    if K % 16:
+        return None
+    try:
+        warp_m, warp_n = MF.compute_warp_partition(M, N, nw, op.policy, 32, 32)
+    except ValueError:
+        return None
+    plan.update(warp_m=warp_m, warp_n=warp_n, mfma=(32, 32, 16))
+    plan["c_layout"] = MF.mfma_c_fragment(M, N, warp_m, warp_n, (32, 32))
+    plan["a_kind"] = "tr32" if op.trans_A else "k_rows_32"
+    plan["b_kind"] = "k_rows_32" if op.trans_B else "tr32"
+    plan["a_smem_layout"] = MF.operand_swizzle(plan["a_kind"], A.static_shape(), 2)
+    plan["b_smem_layout"] = MF.operand_swizzle(plan["b_kind"], B.static_shape(), 2)
+    return plan
+
+
+def _int8_plan(op: O.GemmOp, plan: Dict, nw: int, target) -> Dict:
+    """int8 x int8 -> int32: v_mfma_i32_16x16x64_i8 / v_mfma_i32_32x32x32_i8, K-contiguous operands."""
+    M, N, K = plan["M"], plan["N"], plan["K"]
+    A, B, C = op.A.buffer, op.B.buffer, op.C.buffer
+    if op.trans_A or not op.trans_B or A.scope != "shared" or B.scope != "shared":
+        raise ValueError("int8 T.gemm on gfx950 needs K-contiguous shared operands: A [M,K] and B [N,K] "
+                         "(transpose_B=True)")
+    if C.dtype.name != "int32":
+        raise ValueError(f"int8 T.gemm accumulates in int32, got a {C.dtype} accumulator")
+    ms = 32 if _mfma_shape(op, target) == "32x32" else 16
+    ks = 64 if ms == 16 else 32
+    if K % ks:
+        raise ValueError(f"int8 T.gemm: K={K} must be a multiple of {ks} (MFMA {ms}x{ms}x{ks})")
+    warp_m, warp_n = MF.compute_warp_partition(M, N, nw, op.policy, ms, ms)
+    plan.update(warp_m=warp_m, warp_n=warp_n, mfma=(ms, ms, ks), int8=True)
+    plan["c_layout"] = MF.mfma_c_fragment(M, N, warp_m, warp_n, (ms, ms))
+    kind = "k_rows16" if ms == 16 else "k_rows_i8_32"
+    plan["a_kind"] = plan["b_kind"] = kind
+    plan["a_smem_layout"] = MF.operand_swizzle(kind, A.static_shape(), 1)
+    plan["b_smem_layout"] = MF.operand_swizzle(kind, B.static_shape(), 1)
+    return plan
+
+
+def _f32_plan(op: O.GemmOp, plan: Dict, nw: int) -> Dict:
+    """fp32 x fp32 -> fp32 on v_mfma_f32_16x16x4_f32 (exact f32 products, the f32 VALU rate)."""
+    M, N, K = plan["M"], plan["N"], plan["K"]
+    A, B = op.A.buffer, op.B.buffer
+    if A.scope != "shared" or B.scope != "shared":
+        raise ValueError("fp32 T.gemm on gfx950 needs shared-memory operands")
+    if K % 4:
+        raise ValueError(f"fp32 T.gemm: K={K} must be a multiple of 4 (MFMA 16x16x4)")
+    warp_m, warp_n = MF.compute_warp_partition(M, N, nw, op.policy)
+    plan.update(warp_m=warp_m, warp_n=warp_n, mfma=(16, 16, 4), f32=True)
+    plan["c_layout"] = MF.mfma_c_fragment(M, N, warp_m, warp_n)
+    plan["a_kind"] = plan["b_kind"] = "f32"
+    plan["a_smem_layout"] = LinearLayout(A.static_shape())
+    plan["b_smem_layout"] = LinearLayout(B.static_shape())
+    return plan
+
+
 def gemm_plan(op: O.GemmOp, num_threads: int, target=None, a_layout: Optional[Fragment] = None) -> Dict:
     a_ext, b_ext, c_ext = _trailing2(op.A), _trailing2(op.B), _trailing2(op.C)
     M, N = c_ext
@@ -115,11 +182,23 @@ def gemm_plan(op: O.GemmOp, num_threads: int, target=None, a_layout: Optional[Fr
     eb = A.dtype.bits
     if A.dtype != B.dtype:
         raise ValueError(f"T.gemm needs matching A/B dtypes, got {A.dtype} and {B.dtype}")
-    if eb not in (16, 8):
-        raise ValueError(f"T.gemm on gfx950 supports 16-bit (f16/bf16) and 8-bit (fp8) inputs, got {A.dtype}")
     if num_threads % 64:
         raise ValueError(f"block size {num_threads} is not a multiple of the 64-lane wavefront")
     nw = num_threads // 64
+    if A.dtype.name == "int8":
+        return _int8_plan(op, plan, nw, target)
+    if A.dtype.name == "float32":
+        return _f32_plan(op, plan, nw)
+    if eb not in (16, 8):
+        raise ValueError(f"T.gemm on gfx950 supports f16/bf16, fp8, int8 and fp32 inputs, got {A.dtype}")
+    shape = _mfma_shape(op, target)
+    if eb == 16 and shape == "32x32" and A.scope == "shared" and B.scope == "shared":
+        r = _try_32x32(op, plan, nw)
+        if r is not None:
+            return r
+        if getattr(op, "mfma_shape", None) == "32x32":
+            raise ValueError(f"T.gemm(mfma_shape='32x32'): a {M}x{N} tile over {nw} waves needs per-wave tiles "
+                             f"that are multiples of 32 and K % 16 == 0")
     warp_m, warp_n = MF.compute_warp_partition(M, N, nw, op.policy)
     plan.update(warp_m=warp_m, warp_n=warp_n, mfma=(16, 16, 32))
     plan["c_layout"] = MF.mfma_c_fragment(M, N, warp_m, warp_n)

@@ -993,6 +993,26 @@ class TileOpLowerer(Mutator):
         if B.scope != "shared":
             raise LoweringError("T.gemm: B operand must be in shared memory on gfx950")
         pb = self._operand_ptr(op.B)
+        if plan.get("int8"):
+            pa = self._operand_ptr(op.A)
+            out.append(L.CallStmt("tl::gemm_ss_i8", [pa, pb, L.BufferPtr(cl, 0)], [
+                plan["mfma"][0], plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"],
+                A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
+                B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u"]))
+            return S.SeqStmt(out)
+        if plan.get("f32"):
+            pa = self._operand_ptr(op.A)
+            out.append(L.CallStmt("tl::gemm_ss_f32", [pa, pb, L.BufferPtr(cl, 0)], [
+                plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_A), _b(op.trans_B),
+                A.static_shape()[-1], B.static_shape()[-1]]))
+            return S.SeqStmt(out)
+        if plan.get("mfma") == (32, 32, 16):
+            pa = self._operand_ptr(op.A)
+            out.append(L.CallStmt("tl::gemm_ss_32", [pa, pb, L.BufferPtr(cl, 0)], [
+                ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_A),
+                _b(op.trans_B), A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
+                B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u"]))
+            return S.SeqStmt(out)
         if A.dtype.bits == 8:
             pa = self._operand_ptr(op.A)
             out.append(L.CallStmt("tl::gemm_ss_f8", [pa, pb, L.BufferPtr(cl, 0)], [

@@ -39,6 +39,7 @@ class PassConfigKey(str, Enum):
     TL_DISABLE_GLDS = "tl.disable_glds"            # stage through registers instead of LDS-DMA
     TL_MIN_WAVES_PER_EU = "tl.min_waves_per_eu"    # second __launch_bounds__ argument
     TL_LDS_REUSE = "tl.lds_reuse"                  # liveness-based LDS arena sharing (default on)
+    TL_MFMA_SHAPE = "tl.mfma_shape"                # "16x16" (default) or "32x32" MFMA tiles
 
     def __str__(self):
         return self.value
@@ -63,6 +64,7 @@ EFFECT = {
     "tir.use_async_copy": "False: stage tiles through registers instead of LDS-DMA (= tl.disable_glds)",
     "tl.disable_glds": "stage tiles through registers instead of LDS-DMA",
     "tl.min_waves_per_eu": "second __launch_bounds__ argument (register budget for N waves per SIMD)",
+    "tl.mfma_shape": "'16x16' (default) or '32x32': matrix-core tile of T.gemm (f16/bf16, int8)",
 }
 
 # NVIDIA-only features / TVM passes that do not exist here: the value meaning "off" is what
@@ -103,6 +105,8 @@ def validate_pass_configs(cfg: dict) -> dict:
             raise NotImplementedError(f"pass config {k!r}: {UNSUPPORTED[k]}")
         if k in SATISFIED and v is not None and bool(v) != SATISFIED[k] and bool(v) != DEFAULTS.get(k, False):
             raise NotImplementedError(f"pass config {k}={v!r} asks for an NVIDIA-only feature that gfx950 does not have")
+        if k == "tl.mfma_shape" and v not in (None, "16x16", "32x32"):
+            raise ValueError(f"tl.mfma_shape must be '16x16' or '32x32', got {v!r}")
         if k == "tl.config_index_bitwidth" and v not in (None, 0, 32, 64):
             raise ValueError(f"tl.config_index_bitwidth must be 32 or 64, got {v!r}")
         if k == "tl.layout_visualization_formats" and v is not None:
