@@ -1,0 +1,56 @@
+"""K-half phased GEMM main loop (transform/gemm_ksplit.py + pipeline.py ``_phased_schedule``)."""
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "examples", "gemm"))
+
+import tilelang  # noqa: E402
+from example_gemm import matmul  # noqa: E402
+
+
+def _src(M, N, K, phased=None, bk=64, stages=2):
+    f = matmul.get_tir(M, N, K, 256, 256, bk, 512, stages, "float16")
+    cfg = {} if phased is None else {"tl.gemm_phased": phased}
+    return tilelang.lower(f, target="hip", pass_configs=cfg).kernel_source
+
+
+def test_phased_structure():
+    src = _src(4096, 4096, 4096)
+    body = src[src.index("for (int k"):]
+    # two K-half GEMMs (K = 32 each) per iteration, counted waits, vmcnt(0) only on the last iteration
+    assert body.count("tl::gemm_ss<half_t, 256, 256, 32,") == 2
+    assert "wait_vmcnt<8>" in body and body.count("tl::barrier_raw") >= 2
+    assert "A_shared_k0" in src and "B_shared_k1" in src
+
+
+def test_phased_opt_out_and_shape_gate():
+    src = _src(4096, 4096, 4096, phased=False)
+    assert "A_shared_k0" not in src and "gemm_ss<half_t, 256, 256, 64," in src
+    # BK != 64 or 3-stage rings keep the plain schedule
+    assert "A_shared_k0" not in _src(4096, 4096, 4096, bk=32, stages=4)
+
+
+def test_phased_config_validation():
+    f = matmul.get_tir(256, 256, 256, 256, 256, 64, 512, 2, "float16")
+    with pytest.raises(ValueError):
+        tilelang.lower(f, target="hip", pass_configs={"tl.gemm_phased": "fast"})
+    assert "setprio" in tilelang.lower(f, target="hip", pass_configs={"tl.gemm_phased": "prio"}).kernel_source
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [64, 128, 192, 1024])
+@pytest.mark.parametrize("phased", [True, "prio"])
+def test_phased_numerics(K, phased):
+    """1, 2, 3 and 16 K-tiles: the prologue / last-iteration waits of the phased ring."""
+    M, N = 512, 768
+    f = matmul.get_tir(M, N, K, 256, 256, 64, 512, 2, "float16")
+    k = tilelang.compile(f, out_idx=[-1], target="hip", pass_configs={"tl.gemm_phased": phased})
+    assert "A_shared_k0" in k.get_kernel_source()
+    a = torch.randn(M, K, device="cuda", dtype=torch.float16)
+    b = torch.randn(K, N, device="cuda", dtype=torch.float16)
+    c = k(a, b)
+    torch.testing.assert_close(c.float(), a.float() @ b.float(), rtol=1e-2, atol=1e-2 * K ** 0.5)

@@ -39,8 +39,8 @@ def gemm_kernel(M, N, K, bm, bn, bk, threads, dtype, accum, out_dtype, trans_A=F
 def _ref(a, b, ta, tb):
     a = a.t() if ta else a
     b = b.t() if tb else b
-    if a.dtype == torch.int8:
-        return (a.long() @ b.long())
+    if a.dtype == torch.int8:  # exact in float64 (|sum| < 2^53); integer matmul has no GPU kernel
+        return (a.double() @ b.double()).long()
     return a.float() @ b.float()
 
 
@@ -99,7 +99,7 @@ def test_mfma_form_gpu(case):
     k(a, b, c)
     ref = _ref(a, b, ta, tb)
     if dt == "int8":
-        assert torch.equal(c.long(), ref)
+        assert torch.equal(c.long().cpu(), ref.cpu())
     elif dt == "float32":
         torch.testing.assert_close(c, ref, rtol=1e-4, atol=1e-3)
     else:

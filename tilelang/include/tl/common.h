@@ -135,6 +135,10 @@ TL_DEVICE void sync_grid() {
   __syncthreads();
 }
 
+// wave issue priority (0..3): raised around MFMA clusters so the co-resident wave's loads
+// interleave with them (guide T5)
+template <int N> TL_DEVICE void setprio() { __builtin_amdgcn_s_setprio(N); }
+
 template <int N> TL_DEVICE void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

@@ -1,0 +1,157 @@
+"""K-half split of pipelined GEMM main loops (gfx950 "phased" GEMM schedule, part 1).
+
+A canonical tile-GEMM main loop
+
+    for k in T.Pipelined(K / BK, num_stages=2):
+        T.copy(A[.., k*BK : +BK], A_s)        # A_s [BM][BK]  (or [BK][BM])
+        T.copy(B[k*BK : +BK, ..], B_s)        # B_s [BK][BN]  (or [BN][BK])
+        T.gemm(A_s, B_s, C)
+
+is rewritten into two K halves with their own LDS tiles
+
+        T.copy(A[.., k*BK : +BK/2], A_s0);  T.copy(A[.., k*BK+BK/2 : +BK/2], A_s1)
+        T.copy(B[k*BK : +BK/2, ..], B_s0);  T.copy(B[k*BK+BK/2 : +BK/2, ..], B_s1)
+        T.gemm(A_s0, B_s0, C);  T.gemm(A_s1, B_s1, C)
+
+which computes the same thing, but makes each K half a contiguous LDS region that the
+LDS-DMA engine can refill on its own (``global_load_lds`` writes 1 KiB lane-linear pieces).
+The software pipeline (``pipeline.py``, ``phased`` schedule) then refills the K-half that the
+matrix cores have just finished with, so two half-tiles stay in flight across every barrier and
+no ``s_waitcnt vmcnt(0)`` sits in the main loop (guide §5 "The 256^2 8-phase template",
+"Pipelining across barriers").
+
+Applied when the loop matches that shape, both operands are 16-bit, BK = 64 (two 32-deep MFMA
+K steps), num_stages = 2, and ``tl.gemm_phased`` is not disabled.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+from ..ir import stmt as S
+from ..ir import tileop as O
+from ..ir.buffer import Buffer, BufferRegion
+from ..ir.expr import IntImm, as_int, binop
+from .utils import Mutator, flatten_seq
+
+
+def _k_dims(op: O.GemmOp):
+    """(dim of A_s holding K, dim of B_s holding K) for 2-D shared operands."""
+    return (0 if op.trans_A else 1), (1 if op.trans_B else 0)
+
+
+def _split_copy(cp: O.CopyOp, kdim_dst: int, half: int, new_dst: Buffer, which: int) -> Optional[O.CopyOp]:
+    """Copy of K-half ``which`` into ``new_dst``; the source dim that lands on ``kdim_dst``."""
+    src, dst = cp.src, cp.dst
+    dshape = dst.buffer.static_shape()
+    if dshape is None or len(dshape) != 2 or dst.static_extents() != dshape:
+        return None
+    sext = src.static_extents()
+    if sext is None:
+        return None
+    nonunit = [d for d, e in enumerate(sext) if e != 1]
+    if len(nonunit) != 2 or [sext[d] for d in nonunit] != dshape:
+        return None
+    sd = nonunit[kdim_dst]
+    region = list(src.region)
+    m, e = region[sd]
+    region[sd] = (binop("+", m, IntImm(which * half)), half)
+    new_src = BufferRegion(src.buffer, region)
+    dreg = [(IntImm(0), n) for n in new_dst.static_shape()]
+    return O.CopyOp(new_src, BufferRegion(new_dst, dreg), cp.coalesced_width, cp.disable_tma, cp.eviction_policy)
+
+
+class _KSplit(Mutator):
+
+    def __init__(self, mode=True):
+        self.mode = mode
+        self.new_allocs = {}  # old buffer -> (half0, half1)
+        self.applied = 0
+
+    def visit_ForStmt(self, s: S.ForStmt):
+        body = self.stmt(s.body)
+        loop = S.ForStmt(s.var, s.min, s.extent, s.kind, body, s.annotations)
+        if s.kind != "pipelined" or int(s.annotations.get("num_stages", 0)) != 2:
+            return loop
+        if s.annotations.get("order") or s.annotations.get("stage"):
+            return loop
+        stmts = flatten_seq(body)
+        gemms = [x for x in stmts if isinstance(x, S.TileOpStmt) and isinstance(x.op, O.GemmOp)]
+        copies = [x for x in stmts if isinstance(x, S.TileOpStmt) and isinstance(x.op, O.CopyOp)]
+        if len(gemms) != 1 or len(copies) != 2 or len(stmts) != 3:
+            return loop
+        g = gemms[0].op
+        if g.is_mx:
+            return loop
+        A, B = g.A.buffer, g.B.buffer
+        if A.scope != "shared" or B.scope != "shared" or A.dtype.bits != 16 or B.dtype != A.dtype:
+            return loop
+        if g.C.buffer.scope != "fragment":
+            return loop
+        cps = {c.op.dst.buffer: c.op for c in copies}
+        if set(cps) != {A, B} or any(c.op.src.buffer.scope != "global" for c in copies):
+            return loop
+        ka, kb = _k_dims(g)
+        sa, sb = A.static_shape(), B.static_shape()
+        if sa is None or sb is None or len(sa) != 2 or len(sb) != 2 or sa[ka] != 64 or sb[kb] != 64:
+            return loop
+        if g.A.static_extents() != sa or g.B.static_extents() != sb:
+            return loop
+        half = 32
+        parts = {}
+        for buf, kd in ((A, ka), (B, kb)):
+            shp = list(buf.static_shape())
+            shp[kd] = half
+            h0 = Buffer(buf.name + "_k0", shp, buf.dtype, "shared")
+            h1 = Buffer(buf.name + "_k1", shp, buf.dtype, "shared")
+            c0 = _split_copy(cps[buf], kd, half, h0, 0)
+            c1 = _split_copy(cps[buf], kd, half, h1, 1)
+            if c0 is None or c1 is None:
+                return loop
+            c0.khalf, c1.khalf = 0, 1
+            parts[buf] = (h0, h1, c0, c1)
+        new = []
+        for buf in (A, B):
+            h0, h1, c0, c1 = parts[buf]
+            new += [S.TileOpStmt(c0), S.TileOpStmt(c1)]
+        for i in range(2):
+            gi = O.GemmOp(BufferRegion(parts[A][i], [(IntImm(0), n) for n in parts[A][i].static_shape()]),
+                          BufferRegion(parts[B][i], [(IntImm(0), n) for n in parts[B][i].static_shape()]),
+                          g.C, g.trans_A, g.trans_B, g.policy, g.clear_accum if i == 0 else False, g.k_pack,
+                          g.wg_wait)
+            gi.mfma_shape = g.mfma_shape
+            gi.khalf = i
+            new.append(S.TileOpStmt(gi))
+        for buf in (A, B):
+            self.new_allocs[buf] = parts[buf][:2]
+        self.applied += 1
+        ann = dict(s.annotations)
+        ann["phased"] = self.mode
+        return S.ForStmt(s.var, s.min, s.extent, s.kind, S.SeqStmt(new), ann)
+
+    def visit_AllocStmt(self, s):
+        return s
+
+
+class _AllocSplit(Mutator):
+
+    def __init__(self, new_allocs, used):
+        self.new_allocs = new_allocs
+        self.used = used
+
+    def visit_AllocStmt(self, s):
+        if s.buffer in self.new_allocs:
+            h0, h1 = self.new_allocs[s.buffer]
+            keep = [s] if s.buffer in self.used else []
+            return S.seq(*(keep + [S.AllocStmt(h0), S.AllocStmt(h1)]))
+        return s
+
+
+def split_gemm_k_halves(kernel: S.KernelStmt, mode=True) -> S.KernelStmt:
+    """``mode``: True, or "prio" to also raise the wave priority around each MFMA cluster."""
+    ks = _KSplit(mode)
+    k = ks.stmt(kernel)
+    if not ks.applied:
+        return kernel
+    from .pipeline import _referenced_buffers
+    used = _referenced_buffers(k)
+    return _AllocSplit(ks.new_allocs, used).stmt(k)

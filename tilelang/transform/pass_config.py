@@ -40,6 +40,7 @@ class PassConfigKey(str, Enum):
     TL_MIN_WAVES_PER_EU = "tl.min_waves_per_eu"    # second __launch_bounds__ argument
     TL_LDS_REUSE = "tl.lds_reuse"                  # liveness-based LDS arena sharing (default on)
     TL_MFMA_SHAPE = "tl.mfma_shape"                # "16x16" (default) or "32x32" MFMA tiles
+    TL_GEMM_PHASED = "tl.gemm_phased"              # K-half phased GEMM main loop (gemm_ksplit)
 
     def __str__(self):
         return self.value
@@ -65,6 +66,9 @@ EFFECT = {
     "tl.disable_glds": "stage tiles through registers instead of LDS-DMA",
     "tl.min_waves_per_eu": "second __launch_bounds__ argument (register budget for N waves per SIMD)",
     "tl.mfma_shape": "'16x16' (default) or '32x32': matrix-core tile of T.gemm (f16/bf16, int8)",
+    "tl.gemm_phased": "default on; False keeps BK=64 16-bit GEMM main loops whole instead of splitting them "
+                      "into K halves refilled one phase apart (transform/gemm_ksplit.py + the phased "
+                      "pipeline schedule); 'prio' also raises wave priority around the MFMA clusters",
 }
 
 # NVIDIA-only features / TVM passes that do not exist here: the value meaning "off" is what
@@ -107,6 +111,8 @@ def validate_pass_configs(cfg: dict) -> dict:
             raise NotImplementedError(f"pass config {k}={v!r} asks for an NVIDIA-only feature that gfx950 does not have")
         if k == "tl.mfma_shape" and v not in (None, "16x16", "32x32"):
             raise ValueError(f"tl.mfma_shape must be '16x16' or '32x32', got {v!r}")
+        if k == "tl.gemm_phased" and v not in (None, True, False, "prio"):
+            raise ValueError(f"tl.gemm_phased must be a bool or 'prio', got {v!r}")
         if k == "tl.config_index_bitwidth" and v not in (None, 0, 32, 64):
             raise ValueError(f"tl.config_index_bitwidth must be 32 or 64, got {v!r}")
         if k == "tl.layout_visualization_formats" and v is not None:

@@ -435,6 +435,11 @@ class PipelineInjector(Mutator):
             prologue.append(S.seq(*st) if nv is not None and nv > 0 else S.IfStmt(binop("<", 0, n), S.seq(*st)))
 
         consumer_stmts = [st for st in stmts if not any(st is p for p, _ in prods)]
+        if loop.annotations.get("phased") and nstages == 2 and not staged and not gkeys and len(asyncs) == 4 and \
+                all(getattr(p.op, "khalf", None) is not None for p, _, _ in asyncs):
+            ph = _phased_schedule(self, loop, asyncs, issue_async, consumer_stmts, mapping, newbufs, kk, n)
+            if ph is not None:
+                return ph
         consumers = BufferReplacer(mapping).stmt(S.SeqStmt(consumer_stmts))
         body = []
         if asyncs:
@@ -468,6 +473,69 @@ class PipelineInjector(Mutator):
                 lst.append(NB)
         tail = [L.CallStmt("tl::barrier_raw", [])]
         return S.SeqStmt(prologue + [new_loop] + tail)
+
+
+def _phased_schedule(self, loop, asyncs, issue_async, consumer_stmts, mapping, newbufs, kk, n):
+    """K-half phased GEMM schedule (after ``gemm_ksplit``): two 2-deep LDS rings, one per K half.
+    Iteration t reads stage s = t % 2:
+
+        wait(k0(t)) barrier | issue k1(t+1) | gemm(k0 half of s)
+        wait(k1(t)) barrier | issue k0(t+2) | gemm(k1 half of s)
+
+    A K half is refilled as soon as every wave has passed the barrier behind its last read, and
+    each wait is counted (two half-tiles stay in flight), never vmcnt(0) in steady state."""
+    k = loop.var
+    halves = {0: [], 1: []}
+    for p, src, plan in asyncs:
+        halves[p.op.khalf].append((p, src, plan))
+    h = sum(pl["instrs"] for _, _, pl in halves[0])
+    if h != sum(pl["instrs"] for _, _, pl in halves[1]):
+        return None
+
+    def issue(half, j, stg):
+        out = []
+        for p, src, plan in halves[half]:
+            srcj = _subst_region(src, {k: binop("+", loop.min, j)})
+            NB = newbufs[p.op.dst.buffer]
+            dst = BufferRegion(NB, [(stg, 1)] + list(p.op.dst.region))
+            out.append(S.TileOpStmt(AsyncCopyOp(srcj, dst, plan, None, None)))
+        return S.seq(*out)
+
+    nv = as_int(n)
+    gemms = [st for st in consumer_stmts if isinstance(st, S.TileOpStmt) and isinstance(st.op, O.GemmOp)]
+    others = [st for st in consumer_stmts if st not in gemms]
+    if len(gemms) != 2 or others:
+        return None
+    g0 = BufferReplacer(mapping).stmt(gemms[0])
+    g1 = BufferReplacer(mapping).stmt(gemms[1])
+    if getattr(gemms[0].op, "khalf", 0) == 1:
+        g0, g1 = g1, g0
+
+    if loop.annotations.get("phased") == "prio":
+        g0 = S.seq(L.CallStmt("tl::setprio", [], [1]), g0, L.CallStmt("tl::setprio", [], [0]))
+        g1 = S.seq(L.CallStmt("tl::setprio", [], [1]), g1, L.CallStmt("tl::setprio", [], [0]))
+
+    def wait(more, n_more, n_last):
+        return S.IfStmt(more, L.CallStmt("tl::wait_vmcnt", [], [n_more]), L.CallStmt("tl::wait_vmcnt", [], [n_last]))
+
+    prologue = [issue(0, IntImm(0), IntImm(0)), issue(1, IntImm(0), IntImm(0))]
+    if nv is None or nv > 1:
+        prologue.append(S.IfStmt(binop("<", IntImm(1), n), issue(0, IntImm(1), IntImm(1))) if nv is None
+                        else issue(0, IntImm(1), IntImm(1)))
+    t1 = binop("+", kk, 1)
+    t2 = binop("+", kk, 2)
+    more = binop("<", t1, n)
+    body = [wait(more, 2 * h, h), L.CallStmt("tl::barrier_raw", []),
+            S.IfStmt(more, issue(1, t1, binop("%", t1, 2))), g0,
+            wait(more, 2 * h, 0), L.CallStmt("tl::barrier_raw", []),
+            S.IfStmt(binop("<", t2, n), issue(0, t2, binop("%", kk, 2))), g1]
+    new_loop = S.ForStmt(k, loop.min, loop.extent, "serial", S.SeqStmt(body), {"pipelined": 2, "phased": True})
+    self.replaced = getattr(self, "replaced", {})
+    for B, NB in newbufs.items():
+        lst = self.replaced.setdefault(B, [])
+        if NB not in lst:
+            lst.append(NB)
+    return S.SeqStmt(prologue + [new_loop, L.CallStmt("tl::barrier_raw", [])])
 
 
 def free_vars_stmt_outer(kernel):
