@@ -3,7 +3,8 @@
 Two levels:
   * compiled code objects keyed by sha256(kernel source, flags, arch, toolchain) under
     ``$TILELANG_CACHE_DIR/obj/<key>.hsaco`` (or ``.so`` for CPU);
-  * whole JIT kernels keyed by the printed IR + target + pass configs + out_idx, kept in-process.
+  * whole JIT kernels keyed by the printed IR + target + pass configs + out_idx + compiler
+    fingerprint, in-process and on disk (``kernel_cache.py``: a new process skips lowering).
 Writes are atomic (temp file + rename), so concurrent compiles (autotuner pools, several ranks)
 never observe partial files.
 """
@@ -90,6 +91,8 @@ def compile_cpu_cached(source: str, flags=None, verbose=False) -> str:
 def clear_cache():
     with _lock:
         _mem.clear()
+    from ..jit import _GLOBAL_JIT_CACHE
+    _GLOBAL_JIT_CACHE.clear()
     p = Path(env.TILELANG_CACHE_DIR)
     if p.exists():
         shutil.rmtree(p, ignore_errors=True)

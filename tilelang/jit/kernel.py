@@ -73,8 +73,22 @@ class JITKernel:
         self.config = None
         self.latency = None
         self.ref_latency = None
+        self._launch = None       # launcher specs restored from the disk cache
+        self.from_disk_cache = False
+        key = None
         if artifact is None:
-            artifact = lower(func, self.target, pass_configs=self.pass_configs)
+            from ..cache import kernel_cache
+            key = kernel_cache.kernel_key(func, self.target, out_idx, self.pass_configs, self.compile_flags)
+            hit = kernel_cache.load(key)
+            if hit is not None:
+                is_cpu, kernels, code, self._launch = hit
+                tgt = Target("cpu", "host", getattr(self.target, "mesh", None)) if is_cpu and \
+                    self.target.kind != "cpu" else self.target
+                artifact = CompiledArtifact(func, tgt, kernels, is_cpu)
+                self.from_disk_cache = True
+                key = None
+            else:
+                artifact = lower(func, self.target, pass_configs=self.pass_configs)
         self.artifact = artifact
         self.target = artifact.target
         nparams = len(func.params)
@@ -87,6 +101,9 @@ class JITKernel:
             if not isinstance(func.params[i], Buffer):
                 raise ValueError(f"out_idx {i} refers to a scalar parameter")
         self.code = code if code is not None else self._compile()
+        if key is not None:
+            from ..cache import kernel_cache
+            kernel_cache.save(key, self)
 
     # -- compilation -------------------------------------------------------------------
     def _compile(self):
@@ -157,7 +174,8 @@ class JITKernel:
                     a = self.artifact
                     rts = []
                     for i, (dk, code) in enumerate(zip(a.kernels, self.code)):
-                        specs, nsyms, grid = self._param_specs(dk, with_outputs=(i == 0))
+                        specs, nsyms, grid = self._launch[i] if self._launch is not None else \
+                            self._param_specs(dk, with_outputs=(i == 0))
                         blob = code.encode() if isinstance(code, str) else code
                         k = rt.Kernel(blob, dk.name, a.is_cpu, specs, nsyms, grid, [int(b) for b in dk.block],
                                       int(dk.lds_bytes), dk.name)
@@ -210,6 +228,18 @@ class JITKernel:
         for r, dk in zip(rts[1:], kernels[1:]):
             r(*full, *_margs(dk))
         return out
+
+    @classmethod
+    def from_database(cls, func: S.PrimFunc, out_idx=None, target="auto", pass_configs=None, compile_flags=None,
+                      **_):
+        """The cached kernel for this program/options, or None when the disk cache has no entry
+        (reference ``JITKernel.from_database``, ``tilelang/jit/kernel.py:142-183``)."""
+        from ..cache import kernel_cache
+        tgt = determine_target(target)
+        key = kernel_cache.kernel_key(func, tgt, out_idx, dict(pass_configs or {}), list(compile_flags or []))
+        if kernel_cache.load(key) is None:
+            return None
+        return cls(func, out_idx=out_idx, target=tgt, pass_configs=pass_configs, compile_flags=compile_flags)
 
     def set_validation(self, enabled: bool):
         for r in self.runtimes:
