@@ -75,6 +75,10 @@ class DType:
             return Var("v", self)
         return const(value, self)
 
+    def torch(self):
+        """The matching ``torch.dtype``."""
+        return to_torch(self)
+
     # ``T.float32.max()`` helpers used by some programs
     def max(self):
         from .expr import const
@@ -118,6 +122,9 @@ uint64 = _reg("uint64", "uint", 64)
 boolean = _reg("bool", "bool", 8)
 handle = _reg("handle", "handle", 64)
 void = _reg("void", "handle", 0)
+
+
+NAMES = _TABLE
 
 
 def as_dtype(x) -> DType:

@@ -130,62 +130,6 @@ def jit(func: Callable = None, *, out_idx=None, target="auto", target_host=None,
     return deco
 
 
-class LazyJITImpl:
-    """Kernel body with tensor annotations; specialised per call from the argument tensors."""
+from .lazy import LazyJITImpl, lazy_jit  # noqa: E402
 
-    def __init__(self, fn, out_idx=None, target="auto", pass_configs=None, compile_flags=None, verbose=False):
-        self.fn = fn
-        self.out_idx = out_idx
-        self.target = target
-        self.pass_configs = pass_configs
-        self.compile_flags = compile_flags
-        self.verbose = verbose
-        self._cache = {}
-        functools.update_wrapper(self, fn)
-
-    def _spec(self, args):
-        key = []
-        for a in args:
-            if hasattr(a, "shape") and hasattr(a, "dtype"):
-                key.append(("T", tuple(a.shape), str(a.dtype)))
-            else:
-                key.append(("S", _freeze(a)))
-        return tuple(key)
-
-    def get_kernel(self, *args) -> JITKernel:
-        key = self._spec(args)
-        k = self._cache.get(key)
-        if k is None:
-            from ..language.parser import trace_prim_func
-            func = trace_prim_func(self.fn, _lazy_overrides(self.fn, args))
-            out_idx = self.out_idx
-            if out_idx is None:
-                out_idx = [i for i, p in enumerate(func.params) if getattr(p, "is_empty_output", False)] or None
-            k = compile(func, out_idx, "auto", self.target, None, self.verbose, self.pass_configs,
-                        self.compile_flags)
-            self._cache[key] = k
-        return k
-
-    def __call__(self, *args):
-        k = self.get_kernel(*args)
-        inputs = [a for i, a in enumerate(args) if i not in (k.out_idx or [])]
-        return k(*inputs)
-
-
-def _lazy_overrides(fn, args):
-    """Bind dynamic (``T.dyn``) dims of annotations to the concrete call-site values when static."""
-    return None
-
-
-def lazy_jit(func: Callable = None, *, out_idx=None, target="auto", pass_configs=None, compile_flags=None,
-             verbose=False):
-
-    def deco(fn):
-        return LazyJITImpl(fn, out_idx, target, pass_configs, compile_flags, verbose)
-
-    if func is not None and callable(func):
-        return deco(func)
-    return deco
-
-
-__all__ = ["jit", "lazy_jit", "compile", "par_compile", "JITKernel", "JITImpl"]
+__all__ = ["jit", "lazy_jit", "compile", "par_compile", "JITKernel", "JITImpl", "LazyJITImpl"]

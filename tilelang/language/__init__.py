@@ -11,7 +11,9 @@ from ..ir.buffer import BufferRegion
 from ..ir.expr import BufferLoad
 from .parser import prim_func, macro, TensorAnnot
 from .annot import (Tensor, StridedTensor, FragmentBuffer, SharedBuffer, LocalBuffer, dyn, MeshTensor,
-                    MeshShardingPolicy, MeshReplicationType, TensorWithMeta, MeshTensorAnnot)
+                    MeshShardingPolicy, MeshReplicationType, TensorWithMeta, MeshTensorAnnot, TensorTemplate, ptr,
+                    dtype, make_tensor)
+from ..ir.dtypes import float8_e4m3fn as float8_e4m3  # noqa: F401
 from .annot import Buffer_ as Buffer
 from .kernel import (Kernel, KernelLaunchFrame, get_thread_binding, get_thread_bindings, get_block_binding,
                      get_block_bindings, get_thread_extent, get_block_extent, get_thread_extents,
@@ -35,13 +37,10 @@ from .builtin import (sync_threads, sync_warp, sync_global, sync_grid, fence_pro
                       address_of, dynamic, symbolic)
 from .builder import _IfFrame as If, _ElseFrame as Else, _WhileFrame as While
 from . import comm
+from .logical import any_of, all_of
 from ..layout import Layout, Fragment
 
 ceildiv = ceildiv  # noqa: F405 (from math)
-
-
-def ptr(dtype="handle"):
-    return Var("ptr", "handle")
 
 
 def int_(x):

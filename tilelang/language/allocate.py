@@ -9,7 +9,7 @@ from __future__ import annotations
 
 from ..ir import stmt as S
 from ..ir.buffer import Buffer
-from ..ir.expr import IntImm, convert
+from ..ir.expr import IntImm, PrimExpr, convert
 from ..ir import dtypes as _dt
 from .builder import current_builder, has_builder
 
@@ -99,7 +99,18 @@ class EmptyTensor:
         self.dtype = _dt.as_dtype(dtype)
 
 
-def empty(shape, dtype="float32"):
-    if isinstance(shape, int):
-        shape = [shape]
+def empty(*shape, dtype="float32"):
+    """``T.empty(M, N, dtype=...)`` / ``T.empty((M, N), dtype)``: inside a ``@tilelang.lazy_jit``
+    body, an output tensor the launcher allocates and the call returns."""
+    if len(shape) == 2 and isinstance(shape[0], (list, tuple)) and not isinstance(shape[1], (int, PrimExpr)):
+        shape, dtype = shape[0], shape[1]
+    elif len(shape) == 1 and isinstance(shape[0], (list, tuple)):
+        shape = shape[0]
+    shape = list(shape)
+    from .annot import LAZY_STACK
+    if LAZY_STACK:
+        b = Buffer("out", shape, dtype, "global")
+        b._auto_name = True
+        LAZY_STACK[-1].outputs.append(b)
+        return b
     return EmptyTensor(shape, dtype)

@@ -57,7 +57,98 @@ class _TensorFactory:
         if not isinstance(key, tuple) or len(key) != 2:
             raise TypeError("T.Tensor[shape, dtype]")
         shape, dtype = key
+        if _is_template(shape, None, dtype):
+            return TensorTemplate(shape, dtype)
         return TensorAnnot(shape, dtype, scope=self.scope)
+
+
+def _is_concrete_dim(d):
+    return isinstance(d, (int, PrimExpr)) and not isinstance(d, bool)
+
+
+def _is_template(shape, strides, dtype):
+    if isinstance(shape, (int, PrimExpr)):
+        shape = [shape]
+    dims = list(shape) + list(strides or [])
+    return any(not _is_concrete_dim(d) for d in dims) or dtype is Any or dtype is None
+
+
+class TensorTemplate:
+    """A ``@tilelang.lazy_jit`` parameter annotation specialised from the call-site tensor
+    (reference ``tilelang/language/v2/annot.py``): each dim / stride is
+
+      * ``int``            -> static, taken from the argument (one compiled kernel per value);
+      * a Python int       -> static, must match;
+      * ``T.dyn`` / ``T.dyn['name']`` -> a runtime symbol (one kernel for every value; named
+        symbols are shared between parameters);
+
+    and the dtype is fixed or ``Any`` (taken from the argument)."""
+
+    def __init__(self, shape, dtype=Any, strides=None):
+        if isinstance(shape, (int, PrimExpr)) or shape is int:
+            shape = [shape]
+        self.shape = list(shape)
+        self.strides = list(strides) if strides is not None else None
+        self.dtype = None if dtype is Any or dtype is None else _dt.as_dtype(dtype)
+
+    def __repr__(self):
+        return f"TensorTemplate({self.shape}, {self.dtype}, strides={self.strides})"
+
+
+class _StridedTensorFactory:
+    """``T.StridedTensor(shape, strides, dtype)`` and ``T.StridedTensor[shape, strides, dtype]``."""
+
+    def __call__(self, shape, strides, dtype="float32"):
+        if _is_template(shape, strides, dtype):
+            return TensorTemplate(shape, dtype, strides)
+        return TensorAnnot(shape, dtype, strides=list(strides))
+
+    def __getitem__(self, key):
+        if not isinstance(key, tuple) or len(key) != 3:
+            raise TypeError("T.StridedTensor[shape, strides, dtype]")
+        return self(*key)
+
+
+StridedTensor = _StridedTensorFactory()
+
+
+class DynAnnot:
+    """``T.dyn[int, 'X']``: a runtime integer (scalar parameter or shape symbol) named X."""
+
+    def __init__(self, dtype="int32", name=None):
+        self.dtype = _dt.as_dtype("int32" if dtype is int else dtype)
+        self.name = name
+
+
+class _PtrFactory:
+    """``T.ptr`` (lazy_jit annotation of a raw tensor pointer, bound with ``T.make_tensor``) and
+    ``T.ptr()`` (the matching placeholder in ``par_compile`` signatures)."""
+
+    def __call__(self, dtype="handle"):
+        return PtrSpec()
+
+    def __repr__(self):
+        return "T.ptr"
+
+
+class PtrSpec:
+    pass
+
+
+ptr = _PtrFactory()
+
+
+class _DTypeAnnot:
+    """``T.dtype``: annotation of a compile-time dtype parameter; ``T.dtype(x)`` converts."""
+
+    def __call__(self, x):
+        return _dt.as_dtype(x)
+
+    def __instancecheck__(self, obj):
+        return isinstance(obj, _dt.DType)
+
+
+dtype = _DTypeAnnot()
 
 
 Tensor = _TensorFactory("global")
@@ -67,15 +158,18 @@ SharedBuffer = _TensorFactory("shared")
 LocalBuffer = _TensorFactory("local")
 
 
-def StridedTensor(shape, strides, dtype="float32"):  # noqa: N802
-    return TensorAnnot(shape, dtype, strides=list(strides))
-
-
 class _Dyn:
-    """``T.dyn[int32]`` / ``T.dyn('m')``: dynamic scalar/shape symbol."""
+    """``T.dyn[int32]`` / ``T.dyn['name']`` / ``T.dyn[int, 'name']`` / ``T.dyn('m')``: dynamic
+    scalar/shape symbol."""
 
-    def __getitem__(self, dtype):
-        return ScalarAnnot(dtype)
+    def __getitem__(self, key):
+        if isinstance(key, tuple):
+            return DynAnnot(*key)
+        if isinstance(key, str) and key not in _dt.NAMES:
+            return DynAnnot("int32", key)
+        if key is int:
+            return DynAnnot("int32")
+        return ScalarAnnot(key)
 
     def __call__(self, name="n", dtype="int32"):
         return Var(name, _dt.as_dtype(dtype), nonneg=True)
@@ -220,3 +314,39 @@ class MeshTensorAnnot:
 
 
 MeshTensor = MeshTensorAnnot()
+
+
+# ---------------------------------------------------------------------------
+# lazy_jit tracing context (tilelang/jit/lazy.py)
+# ---------------------------------------------------------------------------
+
+
+class PtrParam:
+    """A ``T.ptr`` parameter while a lazy_jit kernel is traced; ``T.make_tensor`` binds it."""
+
+    def __init__(self, name):
+        self.name = name
+
+
+class LazyTrace:
+
+    def __init__(self):
+        self.outputs = []     # buffers created by T.empty, in creation order
+        self.ptr_buffers = {}  # PtrParam -> Buffer
+
+
+LAZY_STACK = []
+
+
+def make_tensor(ptr, shape, dtype="float32", strides=None):
+    """``T.make_tensor(ptr, shape, dtype)``: view a ``T.ptr`` parameter as a global tensor."""
+    if not isinstance(ptr, PtrParam) or not LAZY_STACK:
+        raise TypeError("T.make_tensor needs a T.ptr parameter of a @tilelang.lazy_jit kernel")
+    ctx = LAZY_STACK[-1]
+    if ptr in ctx.ptr_buffers:
+        raise ValueError(f"T.ptr parameter {ptr.name!r} is bound by T.make_tensor twice")
+    if isinstance(shape, (int, PrimExpr)):
+        shape = (shape, )
+    b = Buffer(ptr.name, list(shape), dtype, "global", strides=strides)
+    ctx.ptr_buffers[ptr] = b
+    return b
