@@ -155,5 +155,3 @@ def test_lazy_jit_gpu():
         a = torch.randn(256, 128, dtype=dt, device="cuda")
         b = torch.randn(128, 192, dtype=dt, device="cuda")
         torch.testing.assert_close(gemm_gpu(a, b), a.float() @ b.float(), rtol=1e-2, atol=1e-2)
-    x = torch.randn(96, 64, device="cuda")
-    assert torch.equal(copy_ret.compile(x) and copy_ret(x.cpu()), x.cpu())
