@@ -41,8 +41,9 @@ REF_ATTN_TF = 497.13
 PEAK_BF16_TF = 2500.0  # MI355X dense fp16/bf16 MFMA (AMD spec, no sparsity)
 
 GEMM_CFG = dict(M=4096, N=4096, K=4096, block_M=256, block_N=256, block_K=64, threads=512, num_stages=2)
-# FA tile (scripts/sweep_fa.py, profiles/r2/fa_sweep.log): 256x64, 8 waves, Q in registers, 3-stage K/V ring
-ATTN_CFG = dict(batch=1, heads=64, seq_len=4096, dim=128, block_M=256, block_N=64, threads=512, num_stages=3,
+# FA (scripts/sweep_fa.py, profiles/r2/fa_staged.log): 256x64 tile, 8 waves, Q in registers, 2-stage K/V
+# ring, T.Pipelined(order, stage) schedule: QK^T(t) | rescale+PV(t-1) | softmax(t)
+ATTN_CFG = dict(batch=1, heads=64, seq_len=4096, dim=128, block_M=256, block_N=64, threads=512, num_stages=2,
                 q_in_regs=True)
 MOE_CFG = dict(tokens=2048, hidden=4096, ffn=2048, experts=8, topk=2)
 # --device cpu (CI plumbing run on the CPU target under gloo): same program, tiny shapes
@@ -87,7 +88,7 @@ def build_gemm(device="cuda", g=None):
 def build_attn(device="cuda", a=None):
     import torch
     import tilelang
-    from example_mha_fwd import flashattn
+    from example_mha_fwd_pipelined import flashattn_pipelined as flashattn
     a = a or ATTN_CFG
     f = flashattn.get_tir(a["batch"], a["heads"], a["seq_len"], a["dim"], False, 1, a["block_M"], a["block_N"],
                           a["threads"], a["num_stages"], "bfloat16", True, a.get("q_in_regs", False))

@@ -1,0 +1,138 @@
+"""FlashAttention forward with a user-specified software-pipeline schedule
+(reference: examples/flash_attention/example_mha_fwd_bshd_wgmma_pipelined.py).
+
+``T.Pipelined(order=, stage=, group=)`` (transform/stage_schedule.py) runs the QK^T GEMM of tile t
+next to the rescale + PV GEMM of tile t-1, and the softmax of tile t last:
+
+    iteration t:   S(t) = Q K(t)^T          stage 0, order 0   (MFMA)
+                   O   *= scale(t-1)        stage 1, order 1   (VALU)
+                   O   += P(t-1) V(t-1)     stage 1, order 2   (MFMA)
+                   P(t) = softmax(S(t))     stage 0, order 3   (VALU + v_exp_f32)
+
+Neither neighbouring pair depends on the other, so inside one wave the compiler can interleave
+the MFMA stream of one tile with the exp/VALU stream of the other.  K/V tiles are LDS-DMA
+producers (order = stage = -1) staged ``num_stages`` deep.
+"""
+import argparse
+
+import tilelang
+import tilelang.language as T
+
+from example_mha_fwd import FAST_MATH, ref_program
+
+
+@tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
+def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=256, block_N=64,
+                        threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True):
+    scale = (1.0 / dim)**0.5 * 1.44269504
+    head_kv = heads // groups
+    q_shape = [batch, seq_len, heads, dim]
+    kv_shape = [batch, seq_len, head_kv, dim]
+    accum_dtype = "float"
+    n_softmax = 8 if lazy_rescale else 7  # statements of the softmax group below
+    group = [[0], [1, 2], list(range(3, 3 + n_softmax))]
+    group += [[3 + n_softmax], [4 + n_softmax], [5 + n_softmax]]
+
+    @T.prim_func
+    def main(
+            Q: T.Tensor(q_shape, dtype),
+            K: T.Tensor(kv_shape, dtype),
+            V: T.Tensor(kv_shape, dtype),
+            Output: T.Tensor(q_shape, dtype),
+    ):
+        with T.Kernel(T.ceildiv(seq_len, block_M), heads, batch, threads=threads) as (bx, by, bz):
+            if q_in_regs:
+                Q_s = T.alloc_fragment([block_M, dim], dtype)
+            else:
+                Q_s = T.alloc_shared([block_M, dim], dtype)
+            K_shared = T.alloc_shared([block_N, dim], dtype)
+            V_shared = T.alloc_shared([block_N, dim], dtype)
+            acc_s = T.alloc_fragment([block_M, block_N], accum_dtype)
+            acc_s_cast = T.alloc_fragment([block_M, block_N], dtype)
+            acc_o = T.alloc_fragment([block_M, dim], accum_dtype)
+            scores_max = T.alloc_fragment([block_M], accum_dtype)
+            scores_max_prev = T.alloc_fragment([block_M], accum_dtype)
+            scores_scale = T.alloc_fragment([block_M], accum_dtype)
+            scores_sum = T.alloc_fragment([block_M], accum_dtype)
+            logsum = T.alloc_fragment([block_M], accum_dtype)
+            rescale = T.alloc_var("int32")
+
+            T.copy(Q[bz, bx * block_M:(bx + 1) * block_M, by, :], Q_s)
+            T.fill(acc_o, 0)
+            T.fill(logsum, 0)
+            T.fill(scores_max, -(2.0**30) if lazy_rescale else -T.infinity(accum_dtype))
+            rescale = 1
+
+            loop_range = (T.ceildiv((bx + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N))
+
+            for k in T.Pipelined(loop_range, num_stages=num_stages, order=[-1, 0, 3, 1, -1, 2],
+                                 stage=[-1, 0, 0, 1, -1, 1], group=group):
+                # 0: K tile (producer)
+                T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
+                # 1-2: S = Q K^T
+                if is_causal:
+                    for i, j in T.Parallel(block_M, block_N):
+                        acc_s[i, j] = T.if_then_else(bx * block_M + i >= k * block_N + j, 0,
+                                                     -T.infinity(acc_s.dtype))
+                else:
+                    T.clear(acc_s)
+                T.gemm(Q_s, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                # softmax group
+                T.copy(scores_max, scores_max_prev)
+                if lazy_rescale:
+                    T.reduce_max(acc_s, scores_max_prev, dim=1, clear=False)
+                    rescale = 0
+                    for i in T.Parallel(block_M):
+                        if (scores_max_prev[i] - scores_max[i]) * scale > 8.0:
+                            scores_scale[i] = T.exp2((scores_max[i] - scores_max_prev[i]) * scale)
+                            scores_max[i] = scores_max_prev[i]
+                            rescale = 1
+                        else:
+                            scores_scale[i] = 1.0
+                else:
+                    T.reduce_max(acc_s, scores_max, dim=1, clear=False)
+                    for i in T.Parallel(block_M):
+                        scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
+                for i, j in T.Parallel(block_M, block_N):
+                    acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
+                T.reduce_sum(acc_s, scores_sum, dim=1)
+                for i in T.Parallel(block_M):
+                    logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
+                T.copy(acc_s, acc_s_cast)
+                # rescale group (one tile behind)
+                if rescale != 0:
+                    for i, j in T.Parallel(block_M, dim):
+                        acc_o[i, j] *= scores_scale[i]
+                # V tile (producer) and O += P V (one tile behind)
+                T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
+                T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
+            for i, j in T.Parallel(block_M, dim):
+                acc_o[i, j] /= logsum[i]
+            T.copy(acc_o, Output[bz, bx * block_M:(bx + 1) * block_M, by, :])
+
+    return main
+
+
+def main(batch=1, heads=64, seq_len=4096, dim=128, is_causal=False, groups=1):
+    import torch
+    flops = 4.0 * batch * heads * seq_len * seq_len * dim * (0.5 if is_causal else 1.0)
+    kernel = flashattn_pipelined(batch, heads, seq_len, dim, is_causal, groups)
+    q = torch.randn(batch, seq_len, heads, dim, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(batch, seq_len, heads // groups, dim, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(batch, seq_len, heads // groups, dim, device="cuda", dtype=torch.bfloat16)
+    o = kernel(q, k, v)
+    torch.testing.assert_close(o.float(), ref_program(q, k, v, is_causal, groups).float(), rtol=2e-2, atol=2e-2)
+    lat = kernel.get_profiler().do_bench(lambda: kernel(q, k, v))
+    print(f"flash attention fwd (order/stage pipelined): {lat:.3f} ms, {flops / lat * 1e-9:.1f} TFLOPS")
+
+
+if __name__ == "__main__":
+    p = argparse.ArgumentParser()
+    p.add_argument("--batch", type=int, default=1)
+    p.add_argument("--heads", type=int, default=64)
+    p.add_argument("--seq_len", type=int, default=4096)
+    p.add_argument("--dim", type=int, default=128)
+    p.add_argument("--is_causal", action="store_true")
+    p.add_argument("--groups", type=int, default=1)
+    a = p.parse_args()
+    main(a.batch, a.heads, a.seq_len, a.dim, a.is_causal, a.groups)

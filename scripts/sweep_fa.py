@@ -12,6 +12,7 @@ import torch  # noqa: E402
 
 import tilelang  # noqa: E402
 from example_mha_fwd import flashattn, ref_program  # noqa: E402
+from example_mha_fwd_pipelined import flashattn_pipelined  # noqa: E402
 from tilelang.profiler import do_bench  # noqa: E402
 
 B, H, S, D = 1, 64, 4096, 128
@@ -21,23 +22,21 @@ k = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
 v = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
 ref = None
 CFGS = [
-    # block_M, block_N, threads, stages, q_in_regs, fast_math
-    (256, 64, 512, 2, False, False),
-    (256, 64, 512, 2, False, True),
-    (256, 64, 512, 2, True, True),
-    (256, 64, 512, 3, True, True),
-    (256, 128, 512, 2, True, True),
-    (128, 64, 256, 2, True, True),
-    (128, 64, 256, 3, True, True),
-    (256, 64, 256, 2, True, True),
-    (128, 128, 256, 2, True, True),
+    # kind, block_M, block_N, threads, stages, q_in_regs, fast_math
+    ("plain", 256, 64, 512, 3, True, True),
+    ("staged", 256, 64, 512, 3, True, True),
+    ("staged", 256, 64, 512, 2, True, True),
+    ("plain", 128, 64, 256, 3, True, True),
+    ("staged", 128, 64, 256, 3, True, True),
+    ("staged", 256, 128, 512, 2, True, True),
 ]
 if "--quick" in sys.argv:
     CFGS = CFGS[:4]
-for bm, bn, th, st, qr, fm in CFGS:
-    tag = f"bm{bm} bn{bn} t{th} st{st} qregs{int(qr)} fast{int(fm)}"
+for kind, bm, bn, th, st, qr, fm in CFGS:
+    tag = f"{kind} bm{bm} bn{bn} t{th} st{st} qregs{int(qr)} fast{int(fm)}"
     try:
-        f = flashattn.get_tir(B, H, S, D, False, 1, bm, bn, th, st, "bfloat16", True, qr)
+        fac = flashattn if kind == "plain" else flashattn_pipelined
+        f = fac.get_tir(B, H, S, D, False, 1, bm, bn, th, st, "bfloat16", True, qr)
         kern = tilelang.compile(f, out_idx=[3], target="hip",
                                 pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: fm})
         o = kern(q, k, v)

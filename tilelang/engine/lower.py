@@ -119,6 +119,8 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
     if cfg.get("tl.force_let_inline"):
         from ..transform.let_inline import inline_lets
         kernel = inline_lets(kernel)
+    from ..transform.stage_schedule import apply_stage_schedules
+    kernel = apply_stage_schedules(kernel)  # T.Pipelined(order=, stage=, group=)
     phased = cfg.get("tl.gemm_phased")
     if target.kind == "hip" and phased is not False:  # default on: +15 % at 4096^3 (profiles/r2/gemm_phased.log)
         from ..transform.gemm_ksplit import split_gemm_k_halves
