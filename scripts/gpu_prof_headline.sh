@@ -23,6 +23,6 @@ for k in gemm fa; do
 done
 cd $ROOT
 for k in gemm fa; do
-  python scripts/pmc_summary.py "gemm_kernel|flashattn_kernel" $(find $OUT/pmc_${k}_p1 $OUT/pmc_${k}_p2 -name "*counter_collection.csv") > $OUT/pmc_${k}_summary.md
+  python scripts/pmc_summary.py "gemm_kernel|flashattn_kernel|flashattn_pipelined_kernel" $(find $OUT/pmc_${k}_p1 $OUT/pmc_${k}_p2 -name "*counter_collection.csv") > $OUT/pmc_${k}_summary.md
   cat $OUT/pmc_${k}_summary.md
 done
