@@ -65,3 +65,43 @@ def test_linear_attn_autograd_gpu():
     _close("o", o, ref_program(q, k, v))
     for n, a, r in (("dq", qa, qr), ("dk", ka, kr), ("dv", va, vr)):
         _close(n, a.grad, r.grad)
+
+
+# --------------------------------------------------------------------------- gated delta rule
+
+
+def _gdn_check(device, S, H, D, block_DV):
+    from example_gdn import make_inputs
+    from example_gdn_bwd import chunk_gated_delta_rule_bwd, reference_grads
+    q, k, v, g, beta = make_inputs(1, S, H, D, D, device)
+    do = torch.randn(1, S, H, D, generator=torch.Generator().manual_seed(1)).to(torch.bfloat16).to(device)
+    got = chunk_gated_delta_rule_bwd(q, k, v, g, beta, do, block_DV=block_DV)[:5]
+    ref = reference_grads(q, k, v, g, beta, do)
+    for n, a, r in zip(("dq", "dk", "dv", "dg", "dbeta"), got, ref):
+        _close(n, a.cpu(), r)
+
+
+def test_gdn_bwd_cpu():
+    _gdn_check("cpu", 128, 2, 32, 32)
+
+
+@pytest.mark.gpu
+def test_gdn_bwd_gpu():
+    _gdn_check("cuda", 256, 2, 128, 32)
+
+
+@pytest.mark.gpu
+def test_gdn_autograd_gpu():
+    from example_gdn import make_inputs, naive_recurrent
+    from example_gdn_bwd import ChunkGatedDeltaRule
+    q, k, v, g, beta = make_inputs(1, 192, 2, 64, 64, "cuda")
+    xs = [x.clone().requires_grad_(True) for x in (q, k, v, g, beta)]
+    o = ChunkGatedDeltaRule.apply(*xs)
+    do = torch.randn_like(o)
+    o.backward(do)
+    rs = [x.detach().float().cpu().requires_grad_(True) for x in (q, k, v, g, beta)]
+    o_ref, _ = naive_recurrent(*rs)
+    o_ref.backward(do.float().cpu())
+    _close("o", o.cpu(), o_ref, 5e-2)
+    for n, a, r in zip(("dq", "dk", "dv", "dg", "dbeta"), xs, rs):
+        _close(n, a.grad.cpu(), r.grad, 5e-2)
