@@ -1,0 +1,380 @@
+"""Native Sparse Attention selected-block attention, backward
+(reference: examples/deepseek_nsa/example_tilelang_nsa_bwd.py).  Forward: example_nsa_fwd.py.
+
+Per (token t, kv head h) the G query heads attend to the selected key blocks; with the forward's
+log-sum-exp L (log2 domain) and delta = rowsum(O * dO):
+
+    P  = exp2(s * scale - L),   dP = dO V^T,   dS = P * (dP - delta)
+    dQ = sm_scale dS K,   dK = sm_scale dS^T Q,   dV = P^T dO
+
+Kernels (MI355X):
+  nsa_fwd_lse     the forward, also writing L [B, SQ, HQ] (fp32)
+  nsa_bwd_prep    delta
+  nsa_block_mask  Mask[b, h, j, t] = 1 when token t selected key block j (inverse of BlockIndices)
+  nsa_bwd_dq      one workgroup per (token, kv head) walks its selected blocks (like the forward):
+                  dQ is produced whole, no atomics
+  nsa_bwd_dkv     one workgroup per (key block, kv head, batch) keeps K_j, V_j and the dK/dV
+                  accumulators resident and walks the tokens that can see the block in tiles of
+                  ``32 / G`` tokens (G * tokens = 32 MFMA rows, so dV += P^T dO and
+                  dK += dS^T Q are 32-deep bf16 MFMAs); tiles nobody in which selected j are skipped,
+                  rows of tokens that did not select it are zeroed.  dK/dV are produced whole.
+"""
+import argparse
+
+import tilelang
+import tilelang.language as T
+
+from example_nsa_fwd import FAST_MATH, LOG2E, make_block_indices
+
+
+@tilelang.jit(out_idx=[-2, -1], pass_configs=FAST_MATH)
+def nsa_fwd_lse(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=None, block_size=64, groups=16,
+                selected_blocks=16, num_stages=2, block_T=32, dtype="bfloat16"):
+    sm = (1.0 / dim)**0.5 if scale is None else scale
+    scale = sm * LOG2E
+    head_kv = heads // groups
+    G, BS, S, D = groups, block_size, selected_blocks, dim
+    BT = min(block_T, BS)
+    NT = BS // BT
+    assert G % 16 == 0
+    threads = 64 * (G // 16)
+    past = seq_len_kv - seq_len
+    accum_dtype = "float"
+
+    @T.prim_func
+    def main(Q: T.Tensor([batch, seq_len, heads, D], dtype), K: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
+             V: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
+             BlockIndices: T.Tensor([batch, seq_len, head_kv, S], "int32"),
+             Output: T.Tensor([batch, seq_len, heads, D], dtype), LSE: T.Tensor([batch, seq_len, heads], "float32")):
+        with T.Kernel(seq_len, batch * head_kv, threads=threads) as (bx, bz):
+            Q_shared = T.alloc_shared([G, D], dtype)
+            K_shared = T.alloc_shared([BT, D], dtype)
+            V_shared = T.alloc_shared([BT, D], dtype)
+            acc_s = T.alloc_fragment([G, BT], accum_dtype)
+            acc_s_cast = T.alloc_fragment([G, BT], dtype)
+            acc_o = T.alloc_fragment([G, D], accum_dtype)
+            o_cast = T.alloc_fragment([G, D], dtype)
+            m = T.alloc_fragment([G], accum_dtype)
+            m_prev = T.alloc_fragment([G], accum_dtype)
+            alpha = T.alloc_fragment([G], accum_dtype)
+            l_sum = T.alloc_fragment([G], accum_dtype)
+            r_sum = T.alloc_fragment([G], accum_dtype)
+            b = bz // head_kv
+            h = bz % head_kv
+            pos = bx + past
+            T.copy(Q[b, bx, h * G:(h + 1) * G, :], Q_shared)
+            T.fill(acc_o, 0)
+            T.fill(l_sum, 0)
+            T.fill(m, -(2.0**30))
+            for i in T.Pipelined(S * NT, num_stages=num_stages):
+                blk = BlockIndices[b, bx, h, i // NT]
+                i_s = T.min(T.max(blk, 0), seq_len_kv // BS - 1) * BS + (i % NT) * BT
+                T.copy(K[b, i_s:i_s + BT, h, :], K_shared)
+                T.copy(V[b, i_s:i_s + BT, h, :], V_shared)
+                for g, j in T.Parallel(G, BT):
+                    ok = (blk >= 0) & (blk * BS <= pos)
+                    if is_causal:
+                        ok = ok & (i_s + j <= pos)
+                    acc_s[g, j] = T.if_then_else(ok, 0, -T.infinity(accum_dtype))
+                T.gemm(Q_shared, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.copy(m, m_prev)
+                T.reduce_max(acc_s, m, dim=1, clear=False)
+                for g in T.Parallel(G):
+                    alpha[g] = T.exp2((m_prev[g] - m[g]) * scale)
+                for g, j in T.Parallel(G, BT):
+                    acc_s[g, j] = T.exp2(acc_s[g, j] * scale - m[g] * scale)
+                T.reduce_sum(acc_s, r_sum, dim=1)
+                for g in T.Parallel(G):
+                    l_sum[g] = l_sum[g] * alpha[g] + r_sum[g]
+                for g, d in T.Parallel(G, D):
+                    acc_o[g, d] *= alpha[g]
+                T.copy(acc_s, acc_s_cast)
+                T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
+            for g, d in T.Parallel(G, D):
+                o_cast[g, d] = acc_o[g, d] / T.max(l_sum[g], 1e-30)
+            T.copy(o_cast, Output[b, bx, h * G:(h + 1) * G, :])
+            for g in T.Parallel(G):
+                # rows with no visible key: +inf, so the backward's P is exactly 0 there
+                LSE[b, bx, h * G + g] = T.if_then_else(l_sum[g] > 0, m[g] * scale + T.log2(l_sum[g]),
+                                                       T.infinity("float32"))
+
+    return main
+
+
+@tilelang.jit(out_idx=[2])
+def nsa_bwd_prep(batch, seq_len, heads, dim, dtype="bfloat16", block_T=32):
+
+    @T.prim_func
+    def main(O: T.Tensor([batch, seq_len, heads, dim], dtype), dO: T.Tensor([batch, seq_len, heads, dim], dtype),
+             Delta: T.Tensor([batch, seq_len, heads], "float32")):
+        with T.Kernel(T.ceildiv(seq_len, block_T), batch, threads=256) as (bx, b):
+            acc = T.alloc_fragment([block_T * heads, dim], "float32")
+            dsum = T.alloc_fragment([block_T * heads], "float32")
+            for r, d in T.Parallel(block_T * heads, dim):
+                t = bx * block_T + r // heads
+                acc[r, d] = T.if_then_else(t < seq_len, T.cast(O[b, t, r % heads, d], "float32") *
+                                           T.cast(dO[b, t, r % heads, d], "float32"), 0.0)
+            T.reduce_sum(acc, dsum, dim=1)
+            for r in T.Parallel(block_T * heads):
+                t = bx * block_T + r // heads
+                if t < seq_len:
+                    Delta[b, t, r % heads] = dsum[r]
+
+    return main
+
+
+@tilelang.jit(out_idx=[1])
+def nsa_block_mask(batch, seq_len, head_kv, selected_blocks, num_blocks):
+
+    @T.prim_func
+    def main(BlockIndices: T.Tensor([batch, seq_len, head_kv, selected_blocks], "int32"),
+             Mask: T.Tensor([batch, head_kv, num_blocks, seq_len], "int8")):
+        with T.Kernel(T.ceildiv(seq_len, 64), batch * head_kv, threads=64) as (bx, bz):
+            b, h = bz // head_kv, bz % head_kv
+            for t in T.Parallel(64):
+                tt = bx * 64 + t
+                if tt < seq_len:
+                    for j in T.serial(num_blocks):
+                        Mask[b, h, j, tt] = 0
+                    for i in T.serial(selected_blocks):
+                        blk = BlockIndices[b, tt, h, i]
+                        if blk >= 0 and blk < num_blocks:
+                            Mask[b, h, blk, tt] = 1
+
+    return main
+
+
+@tilelang.jit(out_idx=[-1], pass_configs=FAST_MATH)
+def nsa_bwd_dq(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=None, block_size=64, groups=16,
+               selected_blocks=16, block_T=32, dtype="bfloat16"):
+    sm = (1.0 / dim)**0.5 if scale is None else scale
+    scale = sm * LOG2E
+    head_kv = heads // groups
+    G, BS, S, D = groups, block_size, selected_blocks, dim
+    BT = min(block_T, BS)
+    NT = BS // BT
+    threads = 64 * (G // 16)
+    past = seq_len_kv - seq_len
+    accum_dtype = "float"
+
+    @T.prim_func
+    def main(Q: T.Tensor([batch, seq_len, heads, D], dtype), K: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
+             V: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
+             BlockIndices: T.Tensor([batch, seq_len, head_kv, S], "int32"),
+             dO: T.Tensor([batch, seq_len, heads, D], dtype), LSE: T.Tensor([batch, seq_len, heads], "float32"),
+             Delta: T.Tensor([batch, seq_len, heads], "float32"), dQ: T.Tensor([batch, seq_len, heads, D], dtype)):
+        with T.Kernel(seq_len, batch * head_kv, threads=threads) as (bx, bz):
+            q_s = T.alloc_shared([G, D], dtype)
+            do_s = T.alloc_shared([G, D], dtype)
+            k_s = T.alloc_shared([BT, D], dtype)
+            v_s = T.alloc_shared([BT, D], dtype)
+            ds_s = T.alloc_shared([G, BT], dtype)
+            lse_s = T.alloc_shared([G], "float32")
+            dl_s = T.alloc_shared([G], "float32")
+            s = T.alloc_fragment([G, BT], accum_dtype)
+            dp = T.alloc_fragment([G, BT], accum_dtype)
+            dq = T.alloc_fragment([G, D], accum_dtype)
+            b = bz // head_kv
+            h = bz % head_kv
+            pos = bx + past
+            T.copy(Q[b, bx, h * G:(h + 1) * G, :], q_s)
+            T.copy(dO[b, bx, h * G:(h + 1) * G, :], do_s)
+            T.copy(LSE[b, bx, h * G:(h + 1) * G], lse_s)
+            T.copy(Delta[b, bx, h * G:(h + 1) * G], dl_s)
+            T.clear(dq)
+            for i in T.Pipelined(S * NT, num_stages=2):
+                blk = BlockIndices[b, bx, h, i // NT]
+                i_s = T.min(T.max(blk, 0), seq_len_kv // BS - 1) * BS + (i % NT) * BT
+                T.copy(K[b, i_s:i_s + BT, h, :], k_s)
+                T.copy(V[b, i_s:i_s + BT, h, :], v_s)
+                T.clear(s)
+                T.gemm(q_s, k_s, s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.clear(dp)
+                T.gemm(do_s, v_s, dp, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                for g, j in T.Parallel(G, BT):
+                    ok = (blk >= 0) & (blk * BS <= pos)
+                    if is_causal:
+                        ok = ok & (i_s + j <= pos)
+                    p = T.if_then_else(ok, T.exp2(s[g, j] * scale - lse_s[g]), 0.0)
+                    ds_s[g, j] = p * (dp[g, j] - dl_s[g]) * sm
+                T.gemm(ds_s, k_s, dq, policy=T.GemmWarpPolicy.FullRow)
+            T.copy(dq, dQ[b, bx, h * G:(h + 1) * G, :])
+
+    return main
+
+
+@tilelang.jit(out_idx=[-2, -1], pass_configs=FAST_MATH)
+def nsa_bwd_dkv(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=None, block_size=64, groups=16,
+                threads=256, dtype="bfloat16"):
+    sm = (1.0 / dim)**0.5 if scale is None else scale
+    scale = sm * LOG2E
+    head_kv = heads // groups
+    G, BS, D = groups, block_size, dim
+    TT = max(1, 32 // G)          # tokens per tile
+    R = TT * G                    # MFMA rows per tile
+    NB = seq_len_kv // BS
+    past = seq_len_kv - seq_len
+    accum_dtype = "float"
+
+    @T.prim_func
+    def main(Q: T.Tensor([batch, seq_len, heads, D], dtype), K: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
+             V: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
+             Mask: T.Tensor([batch, head_kv, NB, seq_len], "int8"), dO: T.Tensor([batch, seq_len, heads, D], dtype),
+             LSE: T.Tensor([batch, seq_len, heads], "float32"), Delta: T.Tensor([batch, seq_len, heads], "float32"),
+             dK: T.Tensor([batch, seq_len_kv, head_kv, D], dtype), dV: T.Tensor([batch, seq_len_kv, head_kv, D], dtype)):
+        with T.Kernel(NB, batch * head_kv, threads=threads) as (j, bz):
+            b = bz // head_kv
+            h = bz % head_kv
+            k_s = T.alloc_shared([BS, D], dtype)
+            v_s = T.alloc_shared([BS, D], dtype)
+            q_s = T.alloc_shared([R, D], dtype)
+            do_s = T.alloc_shared([R, D], dtype)
+            p_s = T.alloc_shared([R, BS], dtype)
+            ds_s = T.alloc_shared([R, BS], dtype)
+            lse_s = T.alloc_shared([R], "float32")
+            dl_s = T.alloc_shared([R], "float32")
+            sel_s = T.alloc_shared([TT], "int32")
+            s = T.alloc_fragment([R, BS], accum_dtype)
+            dp = T.alloc_fragment([R, BS], accum_dtype)
+            dk = T.alloc_fragment([BS, D], accum_dtype)
+            dv = T.alloc_fragment([BS, D], accum_dtype)
+            T.copy(K[b, j * BS:(j + 1) * BS, h, :], k_s)
+            T.copy(V[b, j * BS:(j + 1) * BS, h, :], v_s)
+            T.clear(dk)
+            T.clear(dv)
+            # tokens that can see block j: position >= j * BS
+            t0 = T.max(j * BS - past, 0) // TT
+            for ti in T.serial(T.ceildiv(seq_len, TT) - t0):
+                tb = (t0 + ti) * TT
+                for u in T.Parallel(TT):
+                    sel_s[u] = T.if_then_else(tb + u < seq_len, T.cast(Mask[b, h, j, T.min(tb + u, seq_len - 1)],
+                                                                        "int32"), 0)
+                if T.any_of(sel_s):
+                    for r, d in T.Parallel(R, D):
+                        t = T.min(tb + r // G, seq_len - 1)
+                        q_s[r, d] = Q[b, t, h * G + r % G, d]
+                        do_s[r, d] = dO[b, t, h * G + r % G, d]
+                    for r in T.Parallel(R):
+                        t = T.min(tb + r // G, seq_len - 1)
+                        lse_s[r] = LSE[b, t, h * G + r % G]
+                        dl_s[r] = Delta[b, t, h * G + r % G]
+                    T.clear(s)
+                    T.gemm(q_s, k_s, s, transpose_B=True)
+                    T.clear(dp)
+                    T.gemm(do_s, v_s, dp, transpose_B=True)
+                    for r, c in T.Parallel(R, BS):
+                        ok = sel_s[r // G] != 0
+                        if is_causal:
+                            ok = ok & (j * BS + c <= tb + r // G + past)
+                        p = T.if_then_else(ok, T.exp2(s[r, c] * scale - lse_s[r]), 0.0)
+                        p_s[r, c] = p
+                        ds_s[r, c] = p * (dp[r, c] - dl_s[r]) * sm
+                    T.gemm(p_s, do_s, dv, transpose_A=True)
+                    T.gemm(ds_s, q_s, dk, transpose_A=True)
+            T.copy(dk, dK[b, j * BS:(j + 1) * BS, h, :])
+            T.copy(dv, dV[b, j * BS:(j + 1) * BS, h, :])
+
+    return main
+
+
+def nsa_backward(q, k, v, block_indices, o, lse, do, block_size=64, is_causal=True):
+    """(dq, dk, dv) of the NSA selected-block attention."""
+    B, SQ, HQ, D = q.shape
+    SKV, H = k.shape[1], k.shape[2]
+    S = block_indices.shape[-1]
+    G = HQ // H
+    delta = nsa_bwd_prep(B, SQ, HQ, D, _dt(q))(o, do)
+    dq = nsa_bwd_dq(B, HQ, SQ, SKV, D, is_causal, None, block_size, G, S, dtype=_dt(q))(q, k, v, block_indices, do,
+                                                                                         lse, delta)
+    mask = nsa_block_mask(B, SQ, H, S, SKV // block_size)(block_indices)
+    dk, dv = nsa_bwd_dkv(B, HQ, SQ, SKV, D, is_causal, None, block_size, G, dtype=_dt(q))(q, k, v, mask, do, lse,
+                                                                                          delta)
+    return dq, dk, dv
+
+
+def _dt(t):
+    return str(t.dtype).replace("torch.", "")
+
+
+class NativeSparseAttention:
+    """``NativeSparseAttention.apply(q, k, v, block_indices, block_size)`` -> o, differentiable."""
+
+    @staticmethod
+    def apply(q, k, v, block_indices, block_size=64, is_causal=True):
+        import torch
+
+        class _Fn(torch.autograd.Function):
+
+            @staticmethod
+            def forward(ctx, q, k, v):
+                B, SQ, HQ, D = q.shape
+                fwd = nsa_fwd_lse(B, HQ, SQ, k.shape[1], D, is_causal, None, block_size, HQ // k.shape[2],
+                                  block_indices.shape[-1], dtype=_dt(q))
+                o, lse = fwd(q, k, v, block_indices)
+                ctx.save_for_backward(q, k, v, o, lse)
+                return o
+
+            @staticmethod
+            def backward(ctx, do):
+                q, k, v, o, lse = ctx.saved_tensors
+                return nsa_backward(q, k, v, block_indices, o, lse, do.contiguous().to(q.dtype), block_size,
+                                    is_causal)
+
+        return _Fn.apply(q, k, v)
+
+
+def ref_attention(q, k, v, block_indices, block_size, scale=None, is_causal=True):
+    """Differentiable fp32 reference (dense masked softmax over the selected tokens)."""
+    import torch
+    B, SQ, HQ, D = q.shape
+    SKV, H = k.shape[1], k.shape[2]
+    G = HQ // H
+    scale = D**-0.5 if scale is None else scale
+    past = SKV - SQ
+    bi = block_indices.long().cpu()
+    allowed = torch.zeros(B, SQ, H, SKV, dtype=torch.bool)
+    tok = torch.arange(SKV)
+    for s in range(bi.shape[-1]):
+        blk = bi[..., s]
+        inblk = (tok // block_size)[None, None, None, :] == blk[..., None]
+        allowed |= inblk & (blk[..., None] >= 0)
+    pos = (torch.arange(SQ) + past)[None, :, None, None]
+    allowed &= (tok[None, None, None, :] // block_size) * block_size <= pos
+    if is_causal:
+        allowed &= tok[None, None, None, :] <= pos
+    qf = q.float().cpu().view(B, SQ, H, G, D)
+    kf, vf = k.float().cpu(), v.float().cpu()
+    s = torch.einsum("bthgd,bshd->bthgs", qf, kf) * scale
+    s = s.masked_fill(~allowed[:, :, :, None, :], float("-inf"))
+    p = torch.softmax(s, -1).nan_to_num(0.0)
+    o = torch.einsum("bthgs,bshd->bthgd", p, vf)
+    return o.reshape(B, SQ, HQ, D)
+
+
+def main(B=2, SQ=4096, SKV=4096, HQ=64, H=4, D=128, S=16, block_size=64):
+    import torch
+    q = torch.randn(B, SQ, HQ, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, SKV, H, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, SKV, H, D, device="cuda", dtype=torch.bfloat16)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    nb = SKV // block_size
+    vis = (torch.arange(SQ, device="cuda")[:, None] + SKV - SQ) // block_size >= torch.arange(nb, device="cuda")
+    r = torch.where(vis[None, :, None, :], torch.rand(B, SQ, H, nb, device="cuda", generator=g), -1.0)
+    top = r.topk(min(S, nb), -1)
+    bi = torch.where(top.values >= 0, top.indices, -1).int().sort(-1)[0].contiguous()
+    fwd = nsa_fwd_lse(B, HQ, SQ, SKV, D, True, None, block_size, HQ // H, S)
+    o, lse = fwd(q, k, v, bi)
+    do = torch.randn_like(o)
+    from tilelang.profiler import do_bench
+    nsa_backward(q, k, v, bi, o, lse, do, block_size)
+    lat = do_bench(lambda: nsa_backward(q, k, v, bi, o, lse, do, block_size))
+    flops = 2.5 * 4 * B * SQ * HQ * D * S * block_size
+    print(f"NSA bwd B{B} SQ{SQ} HQ{HQ} H{H} D{D} S{S}x{block_size}: {lat:.3f} ms, {flops / lat * 1e-9:.1f} TFLOPS")
+
+
+if __name__ == "__main__":
+    p = argparse.ArgumentParser()
+    p.add_argument("--batch", type=int, default=2)
+    p.add_argument("--seq", type=int, default=4096)
+    a = p.parse_args()
+    main(B=a.batch, SQ=a.seq, SKV=a.seq)

@@ -105,3 +105,70 @@ def test_gdn_autograd_gpu():
     _close("o", o.cpu(), o_ref, 5e-2)
     for n, a, r in zip(("dq", "dk", "dv", "dg", "dbeta"), xs, rs):
         _close(n, a.grad.cpu(), r.grad, 5e-2)
+
+
+# --------------------------------------------------------------------------- NSA
+
+
+def _nsa_check(device, B, SQ, HQ, H, D, S, BS):
+    from example_nsa_fwd import make_block_indices
+    from example_nsa_bwd import nsa_fwd_lse, nsa_backward, ref_attention
+    g = torch.Generator().manual_seed(0)
+    q = torch.randn(B, SQ, HQ, D, generator=g).bfloat16().to(device)
+    k = torch.randn(B, SQ, H, D, generator=g).bfloat16().to(device)
+    v = torch.randn(B, SQ, H, D, generator=g).bfloat16().to(device)
+    bi = make_block_indices(B, SQ, SQ, H, S, BS, device)
+    o, lse = nsa_fwd_lse(B, HQ, SQ, SQ, D, True, None, BS, HQ // H, S)(q, k, v, bi)
+    do = torch.randn(o.shape, generator=g).bfloat16().to(device)
+    dq, dk, dv = nsa_backward(q, k, v, bi, o, lse, do, BS)
+    qr, kr, vr = (x.float().cpu().requires_grad_(True) for x in (q, k, v))
+    orf = ref_attention(qr, kr, vr, bi, BS)
+    _close("o", o.cpu(), orf)
+    orf.backward(do.float().cpu())
+    _close("dq", dq.cpu(), qr.grad)
+    _close("dk", dk.cpu(), kr.grad)
+    _close("dv", dv.cpu(), vr.grad)
+
+
+def test_nsa_bwd_cpu():
+    _nsa_check("cpu", 1, 96, 16, 1, 64, 2, 32)
+
+
+@pytest.mark.gpu
+def test_nsa_bwd_gpu():
+    _nsa_check("cuda", 2, 512, 32, 2, 128, 4, 64)
+
+
+# --------------------------------------------------------------------------- varlen FlashAttention
+
+
+def _varlen_check(device, lens_q, lens_k, H, G, D, causal, small):
+    from example_mha_fwd_varlen import make_varlen
+    from example_mha_bwd_varlen import (flashattn_varlen_fwd_lse, reference_grads, varlen_bwd_dkv, varlen_bwd_dq,
+                                        varlen_bwd_preprocess)
+    torch.manual_seed(0)
+    q, k, v, cu_q, cu_k = make_varlen(lens_q, lens_k, H, H // G, D, device)
+    B, TQ, TK = len(lens_q), q.shape[0], k.shape[0]
+    cfg = (64, 32, 128) if small else (128, 64, 256)
+    o, lse = flashattn_varlen_fwd_lse(B, H, TQ, TK, max(lens_q), D, causal, G, *cfg)(q, k, v, cu_q, cu_k)
+    do = torch.randn_like(o)
+    delta = varlen_bwd_preprocess(H, TQ, D)(o, do)
+    kv_cfg = (64, 32, 128) if small else (128, 64, 512)
+    dk, dv = varlen_bwd_dkv(B, H, TQ, TK, max(lens_k), D, causal, G, *kv_cfg)(q, k, v, do, lse, delta, cu_q, cu_k)
+    dq = varlen_bwd_dq(B, H, TQ, TK, max(lens_q), D, causal, G, *cfg)(q, k, v, do, lse, delta, cu_q, cu_k)
+    orf, gq, gk, gv = reference_grads(q, k, v, cu_q, cu_k, do, causal)
+    _close("o", o.cpu(), orf)
+    _close("dq", dq.cpu(), gq)
+    _close("dk", dk.cpu(), gk)
+    _close("dv", dv.cpu(), gv)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_varlen_attn_bwd_cpu(causal):
+    _varlen_check("cpu", [40, 100, 64], [72, 100, 64], 4, 2, 64, causal, True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [True, False])
+def test_varlen_attn_bwd_gpu(causal):
+    _varlen_check("cuda", [300, 1000, 64, 513], [300, 1200, 64, 700], 8, 4, 128, causal, False)
