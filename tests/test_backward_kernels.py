@@ -172,3 +172,44 @@ def test_varlen_attn_bwd_cpu(causal):
 @pytest.mark.parametrize("causal", [True, False])
 def test_varlen_attn_bwd_gpu(causal):
     _varlen_check("cuda", [300, 1000, 64, 513], [300, 1200, 64, 700], 8, 4, 128, causal, False)
+
+
+# --------------------------------------------------------------------------- DSA sparse fine-tuning
+
+
+def _dsa_check(device, S, H, HI, topk, lens):
+    from dsa import deepseek_sparse_attention, ref_sparse_attention, ref_attn_score, ref_indexer_loss
+    from indexer_topk_reducesum import indexer_topk_reducesum_interface, ref_index_score
+    g = torch.Generator().manual_seed(0)
+    DQK, DV, DI = 576, 512, 64
+    mk = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).bfloat16().to(device)  # noqa: E731
+    q, kv, iq, ik, w = mk(S, H, DQK, sc=0.5), mk(S, DQK, sc=0.5), mk(S, HI, DI), mk(S, DI), mk(S, HI)
+    offsets = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=device)
+    xs = [x.clone().requires_grad_(True) for x in (q, kv, iq, ik, w)]
+    o, idx = deepseek_sparse_attention(*xs, offsets, topk, DV)
+    do = torch.randn(o.shape, generator=g).to(device)
+    o.backward(do)
+    # the selection matches torch.topk as sets with the same softmax scores
+    idx_rel, score, idx_abs = indexer_topk_reducesum_interface(iq, w, ik, topk, offsets, return_abs=True)
+    ridx, rscore, _ = ref_index_score(iq.cpu(), w.cpu(), ik.cpu(), topk, offsets.cpu())
+    for t in range(0, S, 7):
+        a = sorted(float(s) for i, s in zip(idx_rel[t].cpu(), score[t].cpu()) if i >= 0)
+        b = sorted(float(s) for s in rscore[t] if s > 0)
+        assert len(a) == len(b) and max((abs(x - y) for x, y in zip(a, b)), default=0) < 2e-3, t
+    rs = [x.float().cpu().clone().requires_grad_(True) for x in (q, kv, iq, ik, w)]
+    idx_c = idx_abs.cpu()
+    orf, p = ref_sparse_attention(rs[0], rs[1], idx_c, DV)
+    _close("o", o.cpu(), orf)
+    orf.backward(do.float().cpu())
+    ref_indexer_loss(rs[2], rs[4], rs[3], idx_c, ref_attn_score(p.detach(), idx_c)).backward()
+    for n, a, r in zip(("dq", "dkv", "d_index_q", "d_index_k", "d_weights"), xs, rs):
+        _close(n, a.grad.cpu(), r.grad)
+
+
+def test_dsa_finetune_cpu():
+    _dsa_check("cpu", 128, 16, 16, 64, [50, 78])
+
+
+@pytest.mark.gpu
+def test_dsa_finetune_gpu():
+    _dsa_check("cuda", 512, 64, 32, 128, [200, 312])

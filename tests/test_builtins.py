@@ -84,3 +84,26 @@ def test_print_gpu(capfd):
     assert torch.equal(a, b)
     out = capfd.readouterr().out
     assert "S[3]" in out
+
+
+def test_no_barrier_inside_thread_guard():
+    """Regression: the lowering's partial-thread guard (if tid < n) must never contain a block
+    barrier (found in the DSA indexer backward: per-thread vector accesses to an LDS array were
+    taken for cross-thread hazards and synchronised inside the guard)."""
+    import os
+    import sys
+    import re
+    import tilelang
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "examples", "dsa_sparse_finetune"))
+    from indexer_bwd import indexer_bwd
+    src = tilelang.lower(indexer_bwd.get_tir(128, 32, 64, 64), target="hip").kernel_source
+    depth, guard_depths = 0, []
+    for line in src.splitlines():
+        if re.search(r"if \(\(tid_ < \d+\)\)", line):
+            guard_depths.append(depth)
+        if "sync_threads" in line or "barrier" in line:
+            assert not guard_depths, "block barrier inside a thread-dependent guard"
+        depth += line.count("{") - line.count("}")
+        while guard_depths and depth <= guard_depths[-1]:
+            guard_depths.pop()

@@ -112,6 +112,8 @@ class ThreadSync:
 
     def __init__(self):
         self.managed: Set = set()
+        self.tvars = ()
+        self.uniform = set()
 
     def needs(self, st: _State, r, w) -> bool:
         # RAW and WAR hazards; WAW between different threads writing the same location is
@@ -195,14 +197,22 @@ class ThreadSync:
             if self.needs(st, r0, w0):
                 out.append(_sync())
                 st = _State()
-            # scan branches for internal hazards (barriers inside are allowed only if the
-            # condition is block-uniform; we keep them, matching the reference behaviour)
+            if _thread_dependent(c.cond, self.tvars, self.uniform):
+                # divergent branch: a barrier inside would deadlock the workgroup.  Accesses in
+                # it are ordered against the surroundings by the barrier in front (above) and
+                # by the next conflicting access after it; inside, a thread only reorders its
+                # own accesses, which needs no barrier.
+                out.append(c)
+                return c, _State(st.reads | r0, st.writes | w0)
+            # block-uniform condition: scan the branches for internal hazards
             tb, st_t = self.scan(c.then_body, st.copy())
             eb, st_e = (self.scan(c.else_body, st.copy()) if c.else_body is not None else (None, st.copy()))
             nc = S.IfStmt(c.cond, tb, eb)
             out.append(nc)
             return nc, st_t.merge(st_e)
         if isinstance(c, S.KernelStmt):
+            self.tvars = tuple(c.thread_vars or ())
+            self.uniform = _uniform_registers(c, self.tvars)
             nb, st2 = self.scan(c.body, _State())
             k = S.KernelStmt(c.grid, c.threads, c.block_vars, c.thread_vars, nb, c.is_cpu, c.prelude)
             k.attrs = dict(c.attrs)
@@ -245,7 +255,9 @@ def _leaves(s):
         yield s
 
 
-_THREAD_NAMES = {"tid_", "tx", "ty", "tz", "lane_", "wave_"}
+# thread-index variables: the user's T.Kernel thread vars plus the lowering's own
+# (lower_tile_op.LowerCtx: tid / lane / wave, printed with a trailing underscore)
+_THREAD_NAMES = {"tid", "lane", "wave", "tid_", "tx", "ty", "tz", "lane_", "wave_"}
 
 
 def _thread_dependent(e, tvars, uniform=()) -> bool:
