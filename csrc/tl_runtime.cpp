@@ -157,7 +157,7 @@ class Kernel {
     int per_cu = 0;
     int64_t threads = 1;
     for (auto b : block_) threads *= b;
-    TL_HIP_CHECK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func_, (int)threads, 0));
+    TL_HIP_CHECK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func_, (int)threads, (size_t)lds_));
     int dev = 0;
     TL_HIP_CHECK(hipGetDevice(&dev));
     hipDeviceProp_t prop;

@@ -330,3 +330,60 @@ def test_all_reduce_tile_cpu(direction, clear):
     for r in range(4):
         exp = sum(As[m] for m in _dirs(nrow, ncol, r, direction)) + (0 if clear else 2.0)
         torch.testing.assert_close(Os[r], exp)
+
+
+@pytest.mark.parametrize("nrow,ncol,direction,kind", [(2, 2, "all", "sum"), (1, 4, "h", "max"), (4, 1, "v", "sum"),
+                                                      (2, 4, "all", "sum")])
+def test_all_reduce_tile_two_shot_cpu(nrow, ncol, direction, kind):
+    """Large tiles reduce-scatter + all-gather: each member reduces one chunk (in member order)
+    and broadcasts it, so every rank holds bitwise identical sums; the workspace holds chunks."""
+    from tilelang.parallel import comm_lower
+    M, N, blocks = 64, 64, 2
+    n = nrow * ncol
+    with device_mesh_config(nrow, ncol):
+
+        @T.prim_func
+        def main(A: T.Tensor((blocks * M, N), "float32"), O_: T.Tensor((blocks * M, N), "float32")):
+            with T.Kernel(blocks, threads=128) as bx:
+                a = T.alloc_fragment((M, N), "float32")
+                o = T.alloc_fragment((M, N), "float32")
+                for it in T.serial(2):  # two instances per launch
+                    T.copy(A[bx * M, 0], a)
+                    for i, j in T.Parallel(M, N):
+                        a[i, j] = a[i, j] * (it + 1)
+                    T.comm.all_reduce_tile(a, o, kind, direction)
+                T.copy(o, O_[bx * M, 0])
+
+        k = tilelang.compile(main, target="cpu")
+    meta = k.artifact.kernels[0].mesh
+    G = {"h": ncol, "v": nrow, "all": n}[direction]
+    assert meta["slot_bytes"] == M * N * 4 // G          # chunk-sized slots
+    one_shot = blocks * 1 * n * M * N * 4                 # nblocks * nops * nranks * tile
+    assert meta["ws_bytes"] < one_shot * 2 // G + 8192
+    vm = VirtualMesh(nrow, ncol, "cpu", workspace_bytes=4 << 20)
+    As = [torch.randn(blocks * M, N) for _ in range(n)]
+    Os = [torch.zeros(blocks * M, N) for _ in range(n)]
+    for _ in range(2):
+        _run(vm, k, [(a,) for a in As], [(o,) for o in Os])
+    for r in range(n):
+        parts = torch.stack([As[m] * 2 for m in _dirs(nrow, ncol, r, direction)])
+        exp = parts.sum(0) if kind == "sum" else parts.amax(0)
+        torch.testing.assert_close(Os[r], exp, rtol=1e-5, atol=1e-5)
+        for m in _dirs(nrow, ncol, r, direction):
+            assert torch.equal(Os[r], Os[m])
+
+
+def test_two_shot_hip_source():
+    with device_mesh_config(2, 4):
+
+        @T.prim_func
+        def main(A: T.Tensor((64, 64), "float32"), O_: T.Tensor((64, 64), "float32")):
+            with T.Kernel(1, threads=256) as bx:
+                a = T.alloc_fragment((64, 64), "float32")
+                o = T.alloc_fragment((64, 64), "float32")
+                T.copy(A, a)
+                T.comm.all_reduce_tile(a, o, "sum", "all")
+                T.copy(o, O_)
+
+        src = tilelang.lower(main, target="hip").kernel_source
+    assert "all-gather phase" in src and src.count("tl::mesh::publish") >= 2

@@ -83,3 +83,19 @@ def test_moe_layer_gpu():
     g, w1, w2 = (t.to("cuda") for t in init_moe_weights(cfg))
     ref = moe_reference(x, g, w1, w2, cfg.topk)
     torch.testing.assert_close(out, ref, rtol=3e-2, atol=3e-2 * ref.abs().max().item())
+
+
+def test_tp_expert_gemm_workspace_and_grid():
+    """The tensor-parallel expert GEMM (all-reduce inside the kernel) runs a persistent grid and
+    two-shot all-reduces: its mesh workspace is >= 10x smaller than one slot per (tile block, rank)
+    of whole fp32 tiles."""
+    from tilelang.ops.moe import expert_gemm_kernel
+    from tilelang.parallel import device_mesh_config
+    max_rows, K, N, E, bm, bn = 4352, 256, 4096, 8, 128, 128
+    with device_mesh_config(1, 8):
+        k = expert_gemm_kernel(max_rows, K, N, E, "bfloat16", "cpu", bm, bn, reduce_mesh="all", mesh_shape=(1, 8))
+    meta = k.artifact.kernels[0].mesh
+    tiles = (max_rows // bm) * (N // bn)
+    one_shot_per_tile = tiles * 8 * bm * bn * 4
+    assert meta["nblocks"] == 256 and meta["slot_bytes"] == bm * bn * 4 // 8
+    assert meta["ws_bytes"] * 10 <= one_shot_per_tile, (meta, one_shot_per_tile)

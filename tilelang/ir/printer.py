@@ -209,6 +209,18 @@ class Printer:
             return f"T.atomic_{op.op}({self.region(op.dst)}, {src})"
         if isinstance(op, O.FinalizeReducerOp):
             return f"T.finalize_reducer({self.region(op.buf)})"
+        if isinstance(op, O.CommOp):
+            # the mesh shape an op was traced for changes its lowering (group sizes, two-shot
+            # chunking): part of the printed IR, i.e. of the kernel-cache key
+            txt = self._comm(op)
+            return txt[:-1] + f", mesh={op.mesh!r})"
+        if isinstance(op, O.GatherRowsOp):
+            return (f"T.gather_rows({self.region(op.src)}, {self.region(op.idx)}, {self.region(op.dst)}, "
+                    f"row_dim={op.row_dim})")
+        return f"T.{k}({self._generic_args(op)})"
+
+    def _comm(self, op) -> str:
+        from . import tileop as O
         if isinstance(op, O.CommBroadcastOp):
             return (f"T.comm.broadcast({self.region(op.src)}, {self.region(op.dst)}, {self.e(op.src_core)}, "
                     f"direction={op.direction!r}, size={op.size})")
@@ -225,10 +237,7 @@ class Printer:
             return f"T.comm.barrier({op.group!r})"
         if isinstance(op, O.CommFenceOp):
             return "T.comm.fence()"
-        if isinstance(op, O.GatherRowsOp):
-            return (f"T.gather_rows({self.region(op.src)}, {self.region(op.idx)}, {self.region(op.dst)}, "
-                    f"row_dim={op.row_dim})")
-        return f"T.{k}({self._generic_args(op)})"
+        return f"T.comm.{op.kind}({self._generic_args(op)})"
 
     def _generic_args(self, op) -> str:
         """Every attribute of a tile op (regions, expressions, constants): the printed IR is the

@@ -74,6 +74,7 @@ class JITKernel:
         self.latency = None
         self.ref_latency = None
         self._launch = None       # launcher specs restored from the disk cache
+        self._residency_ok = set()
         self.from_disk_cache = False
         key = None
         if artifact is None:
@@ -211,6 +212,14 @@ class JITKernel:
 
         def _margs(dk):
             return mesh_ctx.launch_args(dk.mesh) if dk.mesh is not None else []
+
+        if mesh_ctx is not None and not self.artifact.is_cpu:
+            key = (id(mesh_ctx), mesh_ctx.ranks_on_device)
+            if key not in self._residency_ok:
+                for r, dk in zip(rts, kernels):
+                    if dk.mesh is not None:
+                        mesh_ctx.check_residency(dk.name, int(dk.mesh["nblocks"]), int(r.max_resident_blocks()))
+                self._residency_ok.add(key)
 
         out = rts[0](*args, *_margs(kernels[0]))
         if len(rts) == 1:

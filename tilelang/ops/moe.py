@@ -181,33 +181,38 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
 def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target: str, block_M: int = 128,
                        block_N: int = 128, block_K: int = 64, num_stages: int = 2, threads: int = 256,
                        reduce_mesh: Optional[str] = None, mesh_shape: Optional[Tuple[int, int]] = None,
-                       n_src: Optional[int] = None, swiglu: bool = False):
+                       n_src: Optional[int] = None, swiglu: bool = False, persistent_blocks: int = 256):
     """``C[r, :] = A[src(r), :] @ W[tile_expert[r // block_M]].T`` for every non-empty row tile.
 
     ``n_src`` given: A is the ``[n_src, K]`` source-row matrix and row ``r`` of the padded row
     space reads ``A[row_src[r]]`` (``-1`` = padding = zeros), gathered straight into LDS.
     ``reduce_mesh`` ("all"/"h"/"v"): tensor-parallel partial products are summed across the
-    mesh inside the kernel (``T.comm.all_reduce_tile`` on the fp32 accumulator tile).
+    mesh inside the kernel (``T.comm.all_reduce_tile`` on the fp32 accumulator tile) by a persistent
+    grid of ``persistent_blocks`` workgroups (one per CU) walking the tiles.
     ``swiglu``: W's rows are interleaved in groups of 4 (gate 2p, gate 2p+1, up 2p, up 2p+1, see
     ``swiglu_interleave``) and the epilogue writes ``C[r, p] = silu(gate) * up`` ([max_rows, N/2]):
     the 4 columns of such a group sit in the registers of ONE lane (MFMA C layout), so the
     activation needs no data movement and no separate kernel."""
     n_tiles = max_rows // block_M
+    n_by = (N + block_N - 1) // block_N
+    n_work = n_tiles * n_by
+    n_prog = min(n_work, persistent_blocks)
     accum = "float32"
     a_rows = n_src if n_src is not None else max_rows
     n_out = N // 2 if swiglu else N
     assert not (swiglu and reduce_mesh), "the SwiGLU epilogue belongs to the first expert GEMM"
 
-    @T.prim_func
-    def moe_expert_gemm(A: T.Tensor((a_rows, K), dtype), W: T.Tensor((E, N, K), dtype),
-             tile_expert: T.Tensor((n_tiles,), "int32"), row_src: T.Tensor((max_rows,), "int32"),
-             C: T.Tensor((max_rows, n_out), dtype)):
-        with T.Kernel(n_tiles, T.ceildiv(N, block_N), threads=threads) as (bx, by):
-            A_s = T.alloc_shared((block_M, block_K), dtype)
-            W_s = T.alloc_shared((block_N, block_K), dtype)
-            C_l = T.alloc_fragment((block_M, block_N), accum)
-            e = tile_expert[bx]
-            if reduce_mesh is None:
+    if reduce_mesh is None:
+
+        @T.prim_func
+        def moe_expert_gemm(A: T.Tensor((a_rows, K), dtype), W: T.Tensor((E, N, K), dtype),
+                            tile_expert: T.Tensor((n_tiles,), "int32"), row_src: T.Tensor((max_rows,), "int32"),
+                            C: T.Tensor((max_rows, n_out), dtype)):
+            with T.Kernel(n_tiles, T.ceildiv(N, block_N), threads=threads) as (bx, by):
+                A_s = T.alloc_shared((block_M, block_K), dtype)
+                W_s = T.alloc_shared((block_N, block_K), dtype)
+                C_l = T.alloc_fragment((block_M, block_N), accum)
+                e = tile_expert[bx]
                 if e >= 0:
                     T.clear(C_l)
                     for k in T.Pipelined(T.ceildiv(K, block_K), num_stages=num_stages):
@@ -225,25 +230,43 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
                                     dtype, C_l[i, j] / (1.0 + T.exp(-C_l[i, j])) * C_l[i, j + 2])
                     else:
                         T.copy(C_l, C[bx * block_M, by * block_N])
-            else:
-                # every rank holds the same tile table (replicated tokens), so all ranks take
-                # the same branch and meet at the same mesh op
-                C_r = T.alloc_fragment((block_M, block_N), accum)
-                if e >= 0:
-                    T.clear(C_l)
-                    for k in T.Pipelined(T.ceildiv(K, block_K), num_stages=num_stages):
-                        if n_src is not None:
-                            T.gather_rows(A[:, k * block_K:(k + 1) * block_K],
-                                          row_src[bx * block_M:(bx + 1) * block_M], A_s, row_dim=0)
-                        else:
-                            T.copy(A[bx * block_M, k * block_K], A_s)
-                        T.copy(W[e, by * block_N, k * block_K], W_s)
-                        T.gemm(A_s, W_s, C_l, transpose_B=True)
-                    T.comm.all_reduce_tile(C_l, C_r, "sum", reduce_mesh)
-                    T.copy(C_r, C[bx * block_M, by * block_N])
 
-    return tilelang.compile(moe_expert_gemm, out_idx=None, target=target,
-                            pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True} if swiglu else None)
+        return tilelang.compile(moe_expert_gemm, out_idx=None, target=target,
+                                pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True} if swiglu else None)
+
+    @T.prim_func
+    def moe_expert_gemm_tp(A: T.Tensor((a_rows, K), dtype), W: T.Tensor((E, N, K), dtype),
+                           tile_expert: T.Tensor((n_tiles,), "int32"), row_src: T.Tensor((max_rows,), "int32"),
+                           C: T.Tensor((max_rows, n_out), dtype)):
+        # persistent grid: the cross-GPU all-reduce needs every block of every rank resident at
+        # once (tl_runtime refuses larger grids), and the mesh workspace scales with the grid
+        with T.Kernel(n_prog, threads=threads) as pid:
+            A_s = T.alloc_shared((block_M, block_K), dtype)
+            W_s = T.alloc_shared((block_N, block_K), dtype)
+            C_l = T.alloc_fragment((block_M, block_N), accum)
+            C_r = T.alloc_fragment((block_M, block_N), accum)
+            for it in T.serial(T.ceildiv(n_work, n_prog)):
+                t = pid + it * n_prog
+                # every rank holds the same tile table (replicated tokens), so all ranks take
+                # the same branches and meet at the same mesh op instances
+                if t < n_work:
+                    bx = t // n_by
+                    by = t % n_by
+                    e = tile_expert[bx]
+                    if e >= 0:
+                        T.clear(C_l)
+                        for k in T.Pipelined(T.ceildiv(K, block_K), num_stages=num_stages):
+                            if n_src is not None:
+                                T.gather_rows(A[:, k * block_K:(k + 1) * block_K],
+                                              row_src[bx * block_M:(bx + 1) * block_M], A_s, row_dim=0)
+                            else:
+                                T.copy(A[bx * block_M, k * block_K], A_s)
+                            T.copy(W[e, by * block_N, k * block_K], W_s)
+                            T.gemm(A_s, W_s, C_l, transpose_B=True)
+                        T.comm.all_reduce_tile(C_l, C_r, "sum", reduce_mesh)
+                        T.copy(C_r, C[bx * block_M, by * block_N])
+
+    return tilelang.compile(moe_expert_gemm_tp, out_idx=None, target=target)
 
 
 def swiglu_interleave(w1: torch.Tensor) -> torch.Tensor:

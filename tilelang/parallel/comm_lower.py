@@ -54,12 +54,32 @@ def op_slot_bytes(op) -> int:
     if isinstance(op, O.CommAllGatherOp):
         return op.size * op.send.buffer.dtype.bytes
     if isinstance(op, O.CommAllReduceOp):
-        ext = op.dst.static_extents()  # (whole tile when dim is None)
+        part = op.src if op.dim is None else op.tmp
+        ext = (part or op.dst).static_extents()
         n = 1
         for e in ext:
             n *= e
-        return n * op.dst.buffer.dtype.bytes
+        G = _op_group_size(op)
+        if _two_shot(op, n, G):
+            return (n // G) * (part or op.dst).buffer.dtype.bytes
+        return n * (part or op.dst).buffer.dtype.bytes
     return 0
+
+
+# all_reduce partials of at least this many bytes go reduce-scatter + all-gather ("two-shot"):
+# every rank moves 2 (G-1)/G of a tile instead of (G-1) tiles and the workspace shrinks G-fold
+TWO_SHOT_MIN_BYTES = 4096
+
+
+def _op_group_size(op) -> int:
+    nrow, ncol = op.mesh if op.mesh is not None else (1, 1)
+    return {"h": ncol, "v": nrow, "all": nrow * ncol}[op.direction]
+
+
+def _two_shot(op, n: int, G: int) -> bool:
+    part = op.src if op.dim is None else op.tmp
+    nbytes = n * (part or op.dst).buffer.dtype.bytes
+    return G > 2 and n % G == 0 and nbytes >= TWO_SHOT_MIN_BYTES
 
 
 class MeshState:
@@ -320,6 +340,92 @@ def lower_put(lw, op: O.CommPutOp):
     return _scoped(out)
 
 
+def _write_chunk_nest(lw, src: BufferRegion, slot: Buffer, lo, c: int):
+    """slot[q - lo] = src[q] for the flat tile elements q in [lo, lo + c)."""
+
+    def mk(idx, q, _):
+        st = S.StoreStmt(slot, [binop("-", q, lo)], cast(BufferLoad(src.buffer, idx), slot.dtype))
+        return S.IfStmt(binop("&&", binop(">=", q, lo), binop("<", q, binop("+", lo, c))), st)
+
+    return _nest(lw, src, mk)
+
+
+def _send_chunks_loop(lw, st, oi, tag, src: BufferRegion, c: int, dirn: int, count: int, slot_dt):
+    """Reduce-scatter sends: member d (rotated from me) gets chunk group_index(d) of the tile."""
+    k = Var("cmk")
+    d = Var("cmdst", _dt.int32)
+    ci = Var("cmci", _dt.int32)
+    view = _slot_view("cm_out", slot_dt, st.slot_bytes // slot_dt.bytes)
+    body = [S.LetStmt(d, _ext("tl::mesh::group_member_rot", [st.mctx, dirn, st.rank, k])),
+            S.LetStmt(ci, _ext("tl::mesh::group_index", [st.mctx, dirn, d])),
+            L.CallStmt("tl::mesh::wait_ready", [st.mctx, st.blk, oi, d, tag]),
+            L.PtrDeclStmt(lw.ctx.flat_of(view), _ext("tl::mesh::slot", [st.mctx, d, st.blk, oi, st.rank], _dt.handle)),
+            _write_chunk_nest(lw, src, view, binop("*", ci, c), c),
+            L.CallStmt("tl::mesh::publish", [st.mctx, st.blk, oi, d, tag])]
+    return S.ForStmt(k, 0, count, "serial", _scoped(body))
+
+
+def _lower_all_reduce_two_shot(lw, st, op, part: BufferRegion, n: int, dirn: int, kind: str, out: List):
+    """Reduce-scatter + all-gather.  Phase 1: member k receives chunk k of every partial and
+    combines them in member order; phase 2: every member sends its reduced chunk to all.  Each
+    chunk is reduced once, so every rank ends with bitwise identical values."""
+    from ..ir.expr import Var as _V
+    G = _group_size(st, dirn)
+    c = n // G
+    pdt = part.buffer.dtype
+    oi1 = st.nops - 1
+    tag1 = [x for x in out if isinstance(x, S.LetStmt)][-1].var
+    out.append(_post_ready_loop(st, oi1, tag1, dirn, G))
+    out.append(_send_chunks_loop(lw, st, oi1, tag1, part, c, dirn, G, pdt))
+    out.append(_wait_data_loop(st, oi1, tag1, dirn, G))
+    oi2, tag2, pre2 = _begin(st, "all_reduce (all-gather phase)")
+    out += pre2
+    out.append(_post_ready_loop(st, oi2, tag2, dirn, G))
+    k = _V("cmk")
+    out.append(S.ForStmt(k, 0, G, "serial", L.CallStmt("tl::mesh::wait_ready", [
+        st.mctx, st.blk, oi2, _ext("tl::mesh::group_member", [st.mctx, dirn, st.rank, k]), tag2])))
+    # my chunk: combine the G received partial chunks, store it into every member's slot
+    mine, decl1, stride1 = _gathered_view(lw, st, oi1, dirn, pdt)
+    decls = [decl1]
+    outs = []
+    for m in range(G):
+        v = _slot_view(f"cm_ag{m}", pdt, st.slot_bytes // pdt.bytes)
+        decls.append(L.PtrDeclStmt(lw.ctx.flat_of(v), _ext("tl::mesh::slot", [
+            st.mctx, _ext("tl::mesh::group_member", [st.mctx, dirn, st.rank, m]), st.blk, oi2, st.rank], _dt.handle)))
+        outs.append(v)
+    j = _V("cmj")
+    acc = BufferLoad(mine, [j])
+    for m in range(1, G):
+        from ..transform.lower_tile_op import _combine
+        acc = _combine(kind, acc, BufferLoad(mine, [binop("+", j, m * stride1)]))
+    rv = _V("cmv", pdt)
+    body = S.seq(S.LetStmt(rv, acc), *[S.StoreStmt(v, [j], rv) for v in outs])
+    decls.append(lw.lower_nest(S.ForStmt(j, 0, c, "parallel", body), None))
+    out.append(_scoped(decls))
+    kk = _V("cmk")
+    out.append(S.ForStmt(kk, 0, G, "serial", L.CallStmt("tl::mesh::publish", [
+        st.mctx, st.blk, oi2, _ext("tl::mesh::group_member", [st.mctx, dirn, st.rank, kk]), tag2])))
+    out.append(_wait_data_loop(st, oi2, tag2, dirn, G))
+    # every chunk, reduced by its owner, gathered into dst
+    allv, decl2, stride2 = _gathered_view(lw, st, oi2, dirn, pdt)
+    dst = op.dst
+    ddt = dst.buffer.dtype
+
+    def mk(idx, q, _):
+        val = BufferLoad(allv, [binop("+", binop("*", binop("//", q, c), stride2), binop("%", q, c))])
+        if not op.clear:
+            val = _combine2(kind, BufferLoad(dst.buffer, idx), val)
+        return S.StoreStmt(dst.buffer, idx, cast(val, ddt))
+
+    out.append(_scoped([decl2, _nest(lw, dst, mk)]))
+    return _scoped(out)
+
+
+def _combine2(kind, a, b):
+    from ..transform.lower_tile_op import _combine
+    return _combine(kind, a, b)
+
+
 def _gather_phases(lw, st, oi, tag, src: BufferRegion, size: int, dirn: int):
     G = _group_size(st, dirn)
     return [_post_ready_loop(st, oi, tag, dirn, G),
@@ -371,10 +477,13 @@ def lower_all_reduce(lw, op: O.CommAllReduceOp):
     if not tile:
         # 1) local reduce along dim into the partial
         out.append(lw.lower_ReduceOp(O.ReduceOp(op.src, op.tmp, op.reduce_type, op.dim, True)))
-    # 2) all-gather the partials into the workspace
     n = 1
     for e in part.static_extents():
         n *= e
+    G = _group_size(st, dirn)
+    if _two_shot(op, n, G):
+        return _lower_all_reduce_two_shot(lw, st, op, part, n, dirn, _COMBINE[op.reduce_type], out)
+    # 2) all-gather the partials into the workspace
     out += _gather_phases(lw, st, oi, tag, part, n, dirn)
     # 3) combine in member (core-id) order — identical on every rank
     view, decl, stride = _gathered_view(lw, st, oi, dirn, op.dst.buffer.dtype)

@@ -121,6 +121,8 @@ class MeshContext:
         self.ws_bytes = 0
         self.ws_table = None      # int64 tensor [nranks] of workspace pointers (on self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # mesh ranks whose kernels share this GPU (co-residency budget, see check_residency)
+        self.ranks_on_device = 1
 
     # -- geometry ---------------------------------------------------------------------
     @property
@@ -175,6 +177,16 @@ class MeshContext:
             self.ensure_workspace(mesh_meta["ws_bytes"])
         ws = self.ws_table.data_ptr() if self.ws_table is not None else 0
         return [self.rank, ws, self.next_epoch(), self.err.data_ptr()]
+
+    def check_residency(self, label: str, nblocks: int, resident: int):
+        """Cross-GPU waits inside a T.comm kernel assume every block of every rank is running: a
+        block waiting on a peer block that was never scheduled (because the grid exceeds what the
+        GPU holds at once) would wait forever.  Refuse such launches up front."""
+        need = nblocks * self.ranks_on_device
+        if need > resident:
+            raise MeshError(f"{label}: T.comm kernel with {nblocks} blocks x {self.ranks_on_device} rank(s) on this GPU "
+                            f"needs {need} co-resident workgroups but the GPU holds {resident}; use a persistent grid "
+                            f"(T.Persistent / a loop over tiles inside fewer blocks)")
 
     def check(self):
         """Raise if any bounded wait of a mesh kernel on this rank timed out."""
@@ -262,6 +274,11 @@ class ProcessMesh(MeshContext):
             else:
                 device = torch.device("cpu")
         super().__init__(nrow, ncol, rank, device)
+        if self.device.type == "cuda":
+            # ranks that picked the same GPU share its workgroup slots
+            devs = [None] * world
+            dist.all_gather_object(devs, (os.uname().nodename, self.device.index))
+            self.ranks_on_device = sum(1 for d in devs if d == devs[rank])
         self.ws_flags = ws_flags
         self.world_group = dist.group.WORLD
         # every rank creates every row and column group in the same order (new_group is collective)
@@ -398,6 +415,8 @@ class VirtualMesh:
                         for _ in range(self.nrow * self.ncol)]
         self.ws_table = torch.tensor([b.data_ptr() for b in self.buffers], dtype=torch.int64, device=self.device)
         self.ranks = [VirtualRank(self, r) for r in range(self.nrow * self.ncol)]
+        for r in self.ranks:
+            r.ranks_on_device = len(self.ranks)  # all virtual ranks run on the one device
         self._coll = _VirtualCollectives(self.nrow * self.ncol)
         for r in self.ranks:
             r.collectives = self._coll
