@@ -55,8 +55,11 @@ def _check(rank, world, As, B, G, R, S_, src):
     torch.testing.assert_close(S_, sum(a.float() for a in As), rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("ncol", [2, 4])
+@pytest.mark.parametrize("ncol", [2])
 def test_virtual_mesh_gpu(ncol):
+    """All ranks on one device, one HIP stream each: the kernels must run concurrently, so the
+    mesh is limited by the process's hardware queues (GPU_MAX_HW_QUEUES = 4 on the test boxes,
+    one of them the default stream): larger meshes run as processes (test_process_mesh_ipc_gpu)."""
     k = _program(1, ncol)
     vm = VirtualMesh(1, ncol, "cuda", workspace_bytes=16 << 20)
     torch.manual_seed(0)
