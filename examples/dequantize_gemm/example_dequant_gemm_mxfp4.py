@@ -6,8 +6,13 @@ C[M, N] = A[M, K] (bf16) @ dequant(Bq, S)^T with Bq [N, K/2] uint8 = two OCP e2m
 packed tile (1/4 of a bf16 tile) and its scales stream through the LDS-DMA ring; the waves
 expand them into a bf16 LDS tile (the e2m1 decode is a 16-entry select, the e8m0 scale an
 exponent) and run bf16 MFMAs -- weight HBM traffic is 4.25 bits/element, which is what bounds
-the small-M (decode) shapes.  (gfx950 also has native fp4 MFMAs with e8m0 scales,
-v_mfma_scale_f32_16x16x128_f8f6f4; this example keeps the activations in bf16.)
+the small-M (decode) shapes.
+
+``mode="native"`` (the MI355X path for compute-bound, prefill-sized M): the activations are
+quantised on the fly to MXFP8 (e4m3 + e8m0 per 32, ``quant_act_mxfp8``) and the GEMM runs on the
+scaled matrix cores, ``v_mfma_scale_f32_16x16x128_f8f6f4`` with A in fp8 and the weights in their
+stored fp4 (``T.gemm_scaled``, examples/gemm_fp8/example_tilelang_gemm_mx.py): no dequantised
+tile ever exists, and the MFMA runs at the fp8 rate (2x bf16).
 """
 import argparse
 
@@ -20,13 +25,12 @@ from tilelang.quantize import dequantize_mxfp4, e2m1_to_float, quantize_mxfp4
 def dequant_gemm_mxfp4(M, N, K, block_M=None, block_N=None, block_K=128, threads=None, num_stages=2,
                        dtype="bfloat16", accum_dtype="float"):
     # decode (small M): thin tiles so N/block_N workgroups fill the CUs; prefill: 128x128
-    # (prefill: a 256-row tile amortises the per-element decode over twice the MFMA work)
-    if block_M is None:
-        block_M = 16 if M <= 16 else (64 if M <= 256 else 256)
+    if block_M is None:  # (a 256-row tile + the 2-stage ring + the bf16 B tile exceed 160 KiB of LDS)
+        block_M = 16 if M <= 16 else (64 if M <= 256 else 128)
     if block_N is None:
         block_N = 32 if M <= 16 else 128
     if threads is None:
-        threads = 64 if M <= 16 else (256 if M <= 256 else 512)
+        threads = 64 if M <= 16 else 256
     assert K % block_K == 0 and block_K % 32 == 0
 
     @T.prim_func
@@ -66,12 +70,64 @@ def dequant_gemm_mxfp4(M, N, K, block_M=None, block_N=None, block_K=128, threads
     return main
 
 
+@tilelang.jit(out_idx=[1, 2])
+def quant_act_mxfp8(M, K, block_M=64, threads=256, dtype="bfloat16"):
+    """A [M, K] -> (e4m3 [M, K], e8m0 [M, K/32]) with power-of-two block scales: every lane owns
+    one 32-element block (64 B read as 16-byte vectors)."""
+    G = K // 32
+
+    @T.prim_func
+    def main(A: T.Tensor((M, K), dtype), Q: T.Tensor((M, K), "float8_e4m3fn"), SA: T.Tensor((M, G), "uint8")):
+        with T.Kernel(T.ceildiv(M, block_M), threads=threads) as bx:
+            for r, g in T.Parallel(block_M, G):
+                row = bx * block_M + r
+                if row < M:
+                    v = T.alloc_local((32, ), "float32")
+                    amax = T.alloc_var("float32")
+                    amax = 1e-30
+                    for j in T.unroll(32):
+                        v[j] = T.Cast("float32", A[row, g * 32 + j])
+                        amax = T.max(amax, T.abs(v[j]))
+                    e = T.min(T.max(T.ceil(T.log2(amax / 448.0)), -127.0), 127.0)
+                    inv = T.exp2(-e)
+                    SA[row, g] = T.Cast("uint8", e + 127.0)
+                    for j in T.unroll(32):
+                        Q[row, g * 32 + j] = T.Cast("float8_e4m3fn", v[j] * inv)
+
+    return main
+
+
+def mxfp4_gemm_native(A, Bq, S):
+    """bf16 A x MXFP4 weights on the scaled matrix cores (A quantised to MXFP8 on the fly)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gemm_fp8"))
+    from example_tilelang_gemm_mx import mx_matmul
+    M, K = A.shape
+    N = Bq.shape[0]
+    q, sa = quant_act_mxfp8(M, K)(A)
+    return mx_matmul(M, N, K, a_fmt="e4m3", b_fmt="e2m1")(q, Bq, sa, S)
+
+
 def ref_program(A, Bq, S):
     return (A.float() @ dequantize_mxfp4(Bq, S).t()).to(A.dtype)
 
 
-def main(M=16, N=8192, K=8192):
+def main(M=16, N=8192, K=8192, mode="dequant"):
     import torch
+    if mode == "native":
+        A = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        Bq, S = quantize_mxfp4(torch.randn(N, K, device="cuda"))
+        c = mxfp4_gemm_native(A, Bq, S)
+        ref = ref_program(A, Bq, S).float()
+        rel = ((c.float() - ref).norm() / ref.norm()).item()
+        assert rel < 0.05, rel  # MXFP8 activations: ~2^-4 relative rounding per element
+        print(f"native MX path: relative error {rel:.3e} vs bf16 x dequant(fp4)")
+        from tilelang.profiler import do_bench
+        lat = do_bench(lambda: mxfp4_gemm_native(A, Bq, S))
+        print(f"bf16(->mxfp8) x mxfp4 GEMM {M}x{N}x{K} (quant + scaled MFMA): {lat:.4f} ms, "
+              f"{2 * M * N * K / lat * 1e-9:.1f} TFLOPS")
+        return
     kernel = dequant_gemm_mxfp4(M, N, K)
     A = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     Bq, S = quantize_mxfp4(torch.randn(N, K, device="cuda"))
@@ -88,5 +144,6 @@ if __name__ == "__main__":
     p.add_argument("--m", type=int, default=16)
     p.add_argument("--n", type=int, default=8192)
     p.add_argument("--k", type=int, default=8192)
+    p.add_argument("--mode", choices=["dequant", "native"], default="dequant")
     a = p.parse_args()
-    main(a.m, a.n, a.k)
+    main(a.m, a.n, a.k, a.mode)

@@ -20,10 +20,21 @@ _DT = {"e4m3": "float8_e4m3fn", "e5m2": "float8_e5m2", "e2m1": "uint8"}
 
 
 @tilelang.jit(out_idx=[-1])
-def mx_matmul(M, N, K, block_M=256, block_N=256, block_K=None, threads=512, num_stages=2, a_fmt="e4m3",
-              b_fmt="e4m3", out_dtype="bfloat16", accum_dtype="float", panel=8):
-    if block_K is None:  # 64 KiB of operand bytes per pipeline stage
+def mx_matmul(M, N, K, block_M=256, block_N=None, block_K=None, threads=512, num_stages=None, a_fmt="e4m3",
+              b_fmt="e4m3", out_dtype="bfloat16", accum_dtype="float", panel=8, scales_in_lds=True):
+    """``scales_in_lds``: the e8m0 scale tiles ([block, block_K/32] bytes) ride the pipeline into
+    LDS with the operands, so the MFMA loop reads them with ds_read instead of waiting on a
+    global load per K step."""
+    # tiles per format pair, measured at 8192^3 (scripts/sweep_mx.py, profiles/r2/mx_sweep.log):
+    # fp4 x fp4 256x128x256 3-stage 2.3-2.4 PF, fp8 x fp8 256x128x128 3-stage 1.4 PF,
+    # fp8 x fp4 256x256x128 2-stage 1.7 PF
+    same = a_fmt == b_fmt
+    if block_K is None:
         block_K = 256 if a_fmt == b_fmt == "e2m1" else 128
+    if block_N is None:
+        block_N = 128 if same else 256
+    if num_stages is None:
+        num_stages = 3 if same else 2
     ac = K // 2 if a_fmt == "e2m1" else K
     bc = K // 2 if b_fmt == "e2m1" else K
     bka = block_K // 2 if a_fmt == "e2m1" else block_K
@@ -42,14 +53,21 @@ def mx_matmul(M, N, K, block_M=256, block_N=256, block_K=None, threads=512, num_
             A_s = T.alloc_shared((block_M, bka), _DT[a_fmt])
             B_s = T.alloc_shared((block_N, bkb), _DT[b_fmt])
             C_l = T.alloc_fragment((block_M, block_N), accum_dtype)
+            SA_s = T.alloc_shared((block_M, sk), "uint8")
+            SB_s = T.alloc_shared((block_N, sk), "uint8")
             T.use_swizzle(panel_size=panel)
             T.clear(C_l)
             for k in T.Pipelined(T.ceildiv(K, block_K), num_stages=num_stages):
                 T.copy(A[by * block_M, k * bka], A_s)
                 T.copy(B[bx * block_N, k * bkb], B_s)
-                T.gemm_scaled(A_s, B_s, C_l, SA[by * block_M:(by + 1) * block_M, k * sk:(k + 1) * sk],
-                              SB[bx * block_N:(bx + 1) * block_N, k * sk:(k + 1) * sk], transpose_B=True,
-                              a_format=a_fmt, b_format=b_fmt)
+                if scales_in_lds:
+                    T.copy(SA[by * block_M, k * sk], SA_s)
+                    T.copy(SB[bx * block_N, k * sk], SB_s)
+                    T.gemm_scaled(A_s, B_s, C_l, SA_s, SB_s, transpose_B=True, a_format=a_fmt, b_format=b_fmt)
+                else:
+                    T.gemm_scaled(A_s, B_s, C_l, SA[by * block_M:(by + 1) * block_M, k * sk:(k + 1) * sk],
+                                  SB[bx * block_N:(bx + 1) * block_N, k * sk:(k + 1) * sk], transpose_B=True,
+                                  a_format=a_fmt, b_format=b_fmt)
             T.copy(C_l, C[by * block_M, bx * block_N])
 
     return main

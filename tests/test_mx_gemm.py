@@ -62,3 +62,20 @@ def test_mx_gemm_gpu(af, bf):
     b, sb = m.quantize(torch.randn(N, K, device="cuda") * 0.2, bf)
     assert len(set(sa.flatten().tolist())) > 1
     _check(k(a, b, sa, sb), a, b, sa, sb, af, bf)
+
+
+@pytest.mark.gpu
+def test_mxfp4_native_weight_gemm_gpu():
+    """bf16 activations quantised to MXFP8 on the fly x stored MXFP4 weights on the scaled MFMA."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples",
+                                    "dequantize_gemm"))
+    from example_dequant_gemm_mxfp4 import mxfp4_gemm_native, ref_program
+    from tilelang.quantize import quantize_mxfp4
+    torch.manual_seed(0)
+    A = torch.randn(512, 1024, device="cuda", dtype=torch.bfloat16)
+    Bq, S = quantize_mxfp4(torch.randn(768, 1024, device="cuda"))
+    c = mxfp4_gemm_native(A, Bq, S)
+    ref = ref_program(A, Bq, S).float()
+    assert ((c.float() - ref).norm() / ref.norm()).item() < 0.05
