@@ -474,3 +474,33 @@ TL_DEVICE void gemm_ss_f32(const float* __restrict__ A, const float* __restrict_
 }
 
 }  // namespace tl
+
+namespace tl {
+
+// ---------------------------------------------------------------------------
+// Single MFMA on per-thread register arrays, for the user-level intrinsic emitter
+// (tilelang/intrinsics/mfma_macro_generator.py).  Standard (unswapped) operand maps:
+//   a: lane l holds A[row = l & 15][k = K_PER * (l >> 4) + 0 .. K_PER-1]
+//   b: lane l holds B[k = K_PER * (l >> 4) + 0 .. K_PER-1][col = l & 15]
+//   c: lane l holds C[row = 4 * (l >> 4) + v][col = l & 15], v = 0..3
+// K_PER = 8 (f16 / bf16, 16x16x32) or 16 (int8, 16x16x64, int32 accumulator).
+// ---------------------------------------------------------------------------
+template <typename T> TL_DEVICE void mfma_16x16(float* c, const T* a, const T* b) {
+  typedef typename mfma_traits<T>::frag F;
+  F av = *reinterpret_cast<const F*>(a);
+  F bv = *reinterpret_cast<const F*>(b);
+  floatx4 cv = *reinterpret_cast<floatx4*>(c);
+  cv = mfma_traits<T>::mma16(av, bv, cv);
+  *reinterpret_cast<floatx4*>(c) = cv;
+}
+
+TL_DEVICE void mfma_16x16(int* c, const int8_t* a, const int8_t* b) {
+  intx4 av = *reinterpret_cast<const intx4*>(a);
+  intx4 bv = *reinterpret_cast<const intx4*>(b);
+  intx4 cv = *reinterpret_cast<intx4*>(c);
+  cv = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, cv, 0, 0, 0);
+  *reinterpret_cast<intx4*>(c) = cv;
+}
+
+}  // namespace tl
+
