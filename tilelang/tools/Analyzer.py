@@ -57,7 +57,7 @@ class Analyzer:
 
     def __init__(self, func: S.PrimFunc, arch: str = "MI355X"):
         self.func = func
-        self.arch = ARCH_CONFIGS[arch]
+        self.arch = ARCH_CONFIGS[arch if isinstance(arch, str) else "MI355X"]  # or a carver TileDevice
         self.flops = 0.0
         self.bytes = 0.0
         self.dtype_bits = 16
