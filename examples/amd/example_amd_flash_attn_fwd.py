@@ -1,0 +1,124 @@
+"""Persistent FlashAttention forward (reference: examples/amd/example_amd_flash_attn_fwd.py).
+
+``num_split_q`` workgroups per (batch, head) walk the query tiles with a ``T.While`` loop
+(tile = b_split, b_split + num_split_q, ...) instead of one workgroup per tile: the grid stays
+resident, and each workgroup's K/V stream (LDS-DMA ring) moves on to its next query tile without
+a relaunch.  Causal runs hand the heaviest (last) query tiles out first, so the per-workgroup work
+evens out.  The tile body is the MI355X FA kernel (examples/flash_attention/example_mha_fwd.py):
+Q in registers, P kept in registers as the PV operand, lazy rescale, fast exp2.
+"""
+import argparse
+
+import tilelang
+import tilelang.language as T
+
+FAST_MATH = {tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True}
+
+
+@tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
+def fast_flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=128, block_N=64, num_split_q=None,
+                   threads=256, num_stages=2, dtype="float16"):
+    scale = (1.0 / dim)**0.5 * 1.44269504
+    head_kv = heads // groups
+    q_shape = [batch, seq_len, heads, dim]
+    kv_shape = [batch, seq_len, head_kv, dim]
+    accum_dtype = "float"
+    num_q_blocks = (seq_len + block_M - 1) // block_M
+    if num_split_q is None:  # ~2 resident workgroups per CU over the whole grid
+        num_split_q = max(1, min(num_q_blocks, (256 * 2) // max(1, batch * heads)))
+
+    @T.prim_func
+    def main(Q: T.Tensor(q_shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
+             Output: T.Tensor(q_shape, dtype)):
+        with T.Kernel(num_split_q, batch * heads, threads=threads) as (b_split, byz):
+            bz = byz // heads
+            by = byz % heads
+            Q_r = T.alloc_fragment([block_M, dim], dtype)
+            K_shared = T.alloc_shared([block_N, dim], dtype)
+            V_shared = T.alloc_shared([block_N, dim], dtype)
+            acc_s = T.alloc_fragment([block_M, block_N], accum_dtype)
+            acc_s_cast = T.alloc_fragment([block_M, block_N], dtype)
+            acc_o = T.alloc_fragment([block_M, dim], accum_dtype)
+            m_i = T.alloc_fragment([block_M], accum_dtype)
+            m_prev = T.alloc_fragment([block_M], accum_dtype)
+            alpha = T.alloc_fragment([block_M], accum_dtype)
+            l_i = T.alloc_fragment([block_M], accum_dtype)
+            r_sum = T.alloc_fragment([block_M], accum_dtype)
+            it = T.alloc_var("int32")
+            it = b_split
+            while it < num_q_blocks:
+                # causal: the longest rows (last query tiles) first
+                bx = (num_q_blocks - 1 - it) if is_causal else it
+                T.copy(Q[bz, bx * block_M:(bx + 1) * block_M, by, :], Q_r)
+                T.fill(acc_o, 0)
+                T.fill(l_i, 0)
+                T.fill(m_i, -(2.0**30))
+                loop_end = T.ceildiv((bx + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N)
+                for k in T.Pipelined(loop_end, num_stages=num_stages):
+                    T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
+                    T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
+                    for i, j in T.Parallel(block_M, block_N):
+                        ok = k * block_N + j < seq_len
+                        if is_causal:
+                            ok = ok & (bx * block_M + i >= k * block_N + j)
+                        acc_s[i, j] = T.if_then_else(ok, 0, -T.infinity(accum_dtype))
+                    T.gemm(Q_r, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                    T.copy(m_i, m_prev)
+                    T.reduce_max(acc_s, m_i, dim=1, clear=False)
+                    for i in T.Parallel(block_M):
+                        alpha[i] = T.exp2((m_prev[i] - m_i[i]) * scale)
+                    for i, j in T.Parallel(block_M, dim):
+                        acc_o[i, j] *= alpha[i]
+                    for i, j in T.Parallel(block_M, block_N):
+                        acc_s[i, j] = T.exp2(acc_s[i, j] * scale - m_i[i] * scale)
+                    T.reduce_sum(acc_s, r_sum, dim=1)
+                    for i in T.Parallel(block_M):
+                        l_i[i] = l_i[i] * alpha[i] + r_sum[i]
+                    T.copy(acc_s, acc_s_cast)
+                    T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
+                for i, j in T.Parallel(block_M, dim):
+                    acc_o[i, j] /= T.max(l_i[i], 1e-30)
+                T.copy(acc_o, Output[bz, bx * block_M:(bx + 1) * block_M, by, :])
+                it = it + num_split_q
+
+    return main
+
+
+def ref_program(Q, K, V, is_causal, groups=1):
+    import math
+    import torch
+    import torch.nn.functional as F
+    dim = Q.size(-1)
+    K = K.repeat_interleave(groups, dim=2)
+    V = V.repeat_interleave(groups, dim=2)
+    scores = torch.einsum("bqhd,bkhd->bhqk", Q.float(), K.float()) / math.sqrt(dim)
+    if is_causal:
+        s = Q.size(1)
+        scores = scores.masked_fill(torch.tril(torch.ones(s, s, device=Q.device)) == 0, float("-inf"))
+    return torch.einsum("bhqk,bkhd->bqhd", F.softmax(scores, -1), V.float()).to(Q.dtype)
+
+
+def main(batch=1, heads=8, seq_len=4096, dim=128, is_causal=False, groups=1):
+    import torch
+    flops = 4.0 * batch * heads * seq_len * seq_len * dim * (0.5 if is_causal else 1.0)
+    kernel = fast_flashattn(batch, heads, seq_len, dim, is_causal, groups)
+    q = torch.randn(batch, seq_len, heads, dim, device="cuda", dtype=torch.float16)
+    k = torch.randn(batch, seq_len, heads // groups, dim, device="cuda", dtype=torch.float16)
+    v = torch.randn(batch, seq_len, heads // groups, dim, device="cuda", dtype=torch.float16)
+    o = kernel(q, k, v)
+    torch.testing.assert_close(o.float(), ref_program(q, k, v, is_causal, groups).float(), rtol=2e-2, atol=2e-2)
+    print("All checks pass.")
+    lat = kernel.get_profiler().do_bench(lambda: kernel(q, k, v))
+    print(f"persistent flash attention fwd: {lat:.3f} ms, {flops / lat * 1e-9:.1f} TFLOPS")
+
+
+if __name__ == "__main__":
+    p = argparse.ArgumentParser()
+    p.add_argument("--batch", type=int, default=1)
+    p.add_argument("--heads", type=int, default=8)
+    p.add_argument("--seq_len", type=int, default=4096)
+    p.add_argument("--dim", type=int, default=128)
+    p.add_argument("--is_causal", action="store_true")
+    p.add_argument("--groups", type=int, default=1)
+    a = p.parse_args()
+    main(a.batch, a.heads, a.seq_len, a.dim, a.is_causal, a.groups)
