@@ -1,0 +1,39 @@
+"""Sparse attention families: MInference vertical-slash, sparse GQA decode."""
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for d in ("minference", "blocksparse_attention"):
+    sys.path.insert(0, os.path.join(ROOT, "examples", d))
+
+import tilelang  # noqa: E402
+
+
+def _vs_inputs(B, H, S, device, nv, slashes):
+    g = torch.Generator().manual_seed(0)
+    q, k, v = (torch.randn(B, H, S, 64, generator=g).half().to(device) for _ in range(3))
+    v_idx = torch.stack([torch.randperm(S, generator=g)[:nv] for _ in range(B * H)]).view(B, H, -1).to(device)
+    s_idx = torch.tensor(slashes).view(1, H, -1).expand(B, H, -1).contiguous().to(device)
+    return q, k, v, v_idx, s_idx
+
+
+def test_vertical_slash_cpu():
+    from example_vertical_slash_sparse_attn import ref_program, vs_sparse_flashattn, convert_vertical_slash_indexes
+    q, k, v, v_idx, s_idx = _vs_inputs(1, 2, 512, "cpu", 40, [[0, 300], [0, 100]])
+    bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, 512, 64, 32)
+    assert int(cc.sum()) > 0 and int(bc.sum()) > 0  # both phases exercised
+    f = vs_sparse_flashattn.get_tir(1, 2, 512, 64, bo.shape[-1], ci.shape[-1], 64, 32, 128)
+    kern = tilelang.compile(f, out_idx=[7], target="cpu", pass_configs={"tl.enable_fast_math": True})
+    o = kern(q, k, v, bc, bo, cc, ci)
+    torch.testing.assert_close(o.float(), ref_program(q, k, v, v_idx, s_idx, 64, 32), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+def test_vertical_slash_gpu():
+    from example_vertical_slash_sparse_attn import ref_program, vertical_slash_sparse_attention
+    q, k, v, v_idx, s_idx = _vs_inputs(2, 2, 1024, "cuda", 100, [[0, 7, 300], [0, 64, 513]])
+    o = vertical_slash_sparse_attention(q, k, v, v_idx, s_idx)
+    torch.testing.assert_close(o.float(), ref_program(q, k, v, v_idx, s_idx), rtol=2e-2, atol=2e-2)
