@@ -37,3 +37,20 @@ def test_vertical_slash_gpu():
     q, k, v, v_idx, s_idx = _vs_inputs(2, 2, 1024, "cuda", 100, [[0, 7, 300], [0, 64, 513]])
     o = vertical_slash_sparse_attention(q, k, v, v_idx, s_idx)
     torch.testing.assert_close(o.float(), ref_program(q, k, v, v_idx, s_idx), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("variant", ["varlen_indice", "varlen_mask", "paged"])
+def test_sparse_gqa_decode_cpu(variant):
+    import importlib
+    m = importlib.import_module(f"example_tilelang_sparse_gqa_decode_{variant}")
+    m.run(batch=2, heads=32, heads_kv=2, max_cache_seqlen=256, dim=64, block_size=32, sparse_ratio=0.5, device="cpu",
+          num_split=2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["varlen_indice", "varlen_mask", "paged"])
+def test_sparse_gqa_decode_gpu(variant):
+    import importlib
+    m = importlib.import_module(f"example_tilelang_sparse_gqa_decode_{variant}")
+    m.run(batch=4, heads=32, heads_kv=4, max_cache_seqlen=2048, dim=128, block_size=32, sparse_ratio=0.7,
+          device="cuda", num_split=4)
