@@ -16,16 +16,16 @@ FAST_MATH = {tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True}
 
 
 @tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
-def fast_flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=128, block_N=64, num_split_q=None,
-                   threads=256, num_stages=2, dtype="float16"):
+def fast_flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=256, block_N=64, num_split_q=None,
+                   threads=512, num_stages=2, dtype="float16"):
     scale = (1.0 / dim)**0.5 * 1.44269504
     head_kv = heads // groups
     q_shape = [batch, seq_len, heads, dim]
     kv_shape = [batch, seq_len, head_kv, dim]
     accum_dtype = "float"
     num_q_blocks = (seq_len + block_M - 1) // block_M
-    if num_split_q is None:  # ~2 resident workgroups per CU over the whole grid
-        num_split_q = max(1, min(num_q_blocks, (256 * 2) // max(1, batch * heads)))
+    if num_split_q is None:  # one resident 8-wave workgroup per CU over the whole grid
+        num_split_q = max(1, min(num_q_blocks, 256 // max(1, batch * heads)))
 
     @T.prim_func
     def main(Q: T.Tensor(q_shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
