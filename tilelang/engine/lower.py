@@ -137,7 +137,7 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
     if target.kind == "hip" and not cfg.get("tl.disable_thread_storage_sync", False):
         lk = insert_thread_sync(lk)
     lk, offsets, total = plan_lds(lk, reuse=bool(cfg.get("tl.lds_reuse", True)),
-                                  aggressive=bool(cfg.get("tl.enable_aggressive_shared_memory_merge", False)))
+                                  aggressive=bool(cfg.get("tl.enable_aggressive_shared_memory_merge", True)))
     if cfg.get("tl.layout_visualization_enable"):
         from ..analysis.layout_visual import dump_layouts
         dump_layouts(name, li, cfg.get("tl.layout_visualization_formats") or "txt")

@@ -218,5 +218,22 @@ inline void cpu_gemm_mx(const void* A_, const void* B_, const void* SA_, const v
     }
 }
 
+// 2:4 sparse A (T.gemm_sp): A holds the kept values [M][K/2] ([K/2][M] when TA), E the 2-bit
+// positions, 16-bit word c of row i covering original K [16c, 16c+16) (value v at bits 2v).
+template <typename T, int M, int N, int K, bool TA, bool TB, int A_COLS, int E_COLS, int B_COLS>
+inline void cpu_gemm_sp(const T* A, const int16_t* E, const T* B, float* C) {
+  for (int i = 0; i < M; ++i)
+    for (int kc = 0; kc < K / 2; ++kc) {
+      const float a = TA ? (float)A[kc * A_COLS + i] : (float)A[i * A_COLS + kc];
+      const unsigned word = (unsigned)(uint16_t)E[i * E_COLS + kc / 8];
+      const int pos = (int)((word >> (2 * (kc % 8))) & 3u);
+      const int k = 4 * (kc / 2) + pos;
+      for (int j = 0; j < N; ++j) {
+        const float b = TB ? (float)B[j * B_COLS + k] : (float)B[k * B_COLS + j];
+        C[i * N + j] += a * b;
+      }
+    }
+}
+
 }  // namespace tl
 #include "mesh_cpu.h"

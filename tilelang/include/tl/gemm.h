@@ -504,3 +504,72 @@ TL_DEVICE void mfma_16x16(int* c, const int8_t* a, const int8_t* b) {
 
 }  // namespace tl
 
+
+namespace tl {
+
+// ---------------------------------------------------------------------------------------------
+// 2:4 structured-sparse A: v_smfmac_f32_16x16x64_{f16,bf16} (T.gemm_sp; reference
+// src/op/gemm_sp.cc:147 + src/tl_templates/cuda/gemm_sp*.h, which use NVIDIA mma.sp).
+// Operand map measured on gfx950 (scripts/probes/smfmac_map.hip): per 64-wide K step, lane
+// (i = l&15, g = l>>4) supplies the 8 kept A values of original K [16g, 16g+16) of row i (8
+// consecutive compressed elements = one ds_read_b128), their 2-bit in-group positions in the low
+// 16 bits of the index VGPR (value v at bits 2v), and 16 B values whose elements 0..7 / 8..15
+// are the dense 16x16x32 B fragments of K steps k0 and k0+32.  Issued as smfmac(A, B): C is in
+// the direct MFMA layout C[4g + v][i].
+template <typename T> struct smfmac_traits;
+template <> struct smfmac_traits<half_t> {
+  typedef half_t bfrag __attribute__((ext_vector_type(16)));
+  TL_DEVICE static floatx4 mma(halfx8 a, bfrag b, floatx4 c, int idx) {
+    return __builtin_amdgcn_smfmac_f32_16x16x64_f16(a, b, c, idx, 0, 0);
+  }
+};
+template <> struct smfmac_traits<bfloat16_t> {
+  typedef bfloat16_t bfrag __attribute__((ext_vector_type(16)));
+  TL_DEVICE static floatx4 mma(bf16x8 a, bfrag b, floatx4 c, int idx) {
+    return __builtin_amdgcn_smfmac_f32_16x16x64_bf16(a, b, c, idx, 0, 0);
+  }
+};
+
+// A_sp: LDS [M][K/2] (TA=false) or [K/2][M] (TA=true); E: [M][E_COLS] int16 (LDS or global);
+// B: [K][N] (TB=false) or [N][K] (TB=true).  C: floatx4 [M_REP][N_REP] per wave, direct layout.
+template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TA, bool TB, int A_COLS, uint32_t SWZ_A,
+          int E_COLS, int B_COLS, uint32_t SWZ_B>
+TL_DEVICE void gemm_sp_ss(const T* __restrict__ A, const int16_t* __restrict__ E, const T* __restrict__ B,
+                          float* __restrict__ C) {
+  typedef smfmac_traits<T> ST;
+  typedef typename mfma_traits<T>::frag F;
+  typedef typename ST::bfrag BF;
+  constexpr int WM = M / WARP_M, WN = N / WARP_N;
+  constexpr int M_REP = WM / 16, N_REP = WN / 16, KSTEPS = K / 64;
+  static_assert(WM % 16 == 0 && WN % 16 == 0 && K % 64 == 0, "smfmac 16x16x64 tiling");
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wm = wave / WARP_N, wn = wave % WARP_N;
+  floatx4* acc = reinterpret_cast<floatx4*>(C);
+#pragma unroll
+  for (int kk = 0; kk < KSTEPS; ++kk) {
+    F a[M_REP];
+    int idx[M_REP];
+    BF b[N_REP];
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi) {
+      const int m0 = wm * WM + mi * 16;
+      a[mi] = ld_operand<T, (TA ? K / 2 : M), A_COLS, SWZ_A, TA, 0>(A, m0, kk * 32, lane);
+      idx[mi] = (int)(uint16_t)E[(m0 + (lane & 15)) * E_COLS + kk * 4 + (lane >> 4)];
+    }
+#pragma unroll
+    for (int ni = 0; ni < N_REP; ++ni) {
+      const int n0 = wn * WN + ni * 16;
+      F lo = ld_operand<T, (TB ? N : K), B_COLS, SWZ_B, !TB, 0>(B, n0, kk * 64, lane);
+      F hi = ld_operand<T, (TB ? N : K), B_COLS, SWZ_B, !TB, 0>(B, n0, kk * 64 + 32, lane);
+      b[ni] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+    }
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < N_REP; ++ni)
+        acc[mi * N_REP + ni] = ST::mma(a[mi], b[ni], acc[mi * N_REP + ni], idx[mi]);
+  }
+}
+
+}  // namespace tl

@@ -196,6 +196,9 @@ class Printer:
                 return (f"T.gemm_scaled({self.region(op.A)}, {self.region(op.B)}, {self.region(op.C)}, "
                         f"{self.region(op.scale_A)}, {self.region(op.scale_B)}{extra}, a_format={op.a_fmt!r}, "
                         f"b_format={op.b_fmt!r})")
+            if getattr(op, "is_sp", False):
+                return (f"T.gemm_sp({self.region(op.A)}, {self.region(op.E)}, {self.region(op.B)}, "
+                        f"{self.region(op.C)}{extra})")
             return f"T.gemm({self.region(op.A)}, {self.region(op.B)}, {self.region(op.C)}{extra})"
         if isinstance(op, O.FillOp):
             return f"T.fill({self.region(op.dst)}, {self.e(op.value)})"

@@ -106,16 +106,24 @@ class GemmOp(TileOp):
         self.scale_B = scale_B
         self.a_fmt = self.b_fmt = None  # MX element formats ("e4m3", "e5m2", "e2m1")
         self.mfma_shape = None  # "16x16" / "32x32" (T.gemm(mfma_shape=...))
+        self.E = None  # 2:4 sparse metadata of A (T.gemm_sp): A is then the compressed [M, K/2] tile
 
     @property
     def is_mx(self) -> bool:
         return self.scale_A is not None
 
+    @property
+    def is_sp(self) -> bool:
+        return self.E is not None
+
+    def _extra(self):
+        return ([self.scale_A, self.scale_B] if self.is_mx else []) + ([self.E] if self.is_sp else [])
+
     def regions(self):
-        return [self.A, self.B, self.C] + ([self.scale_A, self.scale_B] if self.is_mx else [])
+        return [self.A, self.B, self.C] + self._extra()
 
     def reads(self):
-        return [self.A, self.B, self.C] + ([self.scale_A, self.scale_B] if self.is_mx else [])
+        return [self.A, self.B, self.C] + self._extra()
 
     def writes(self):
         return [self.C]

@@ -126,6 +126,8 @@ def use_swizzle(panel_size: int = 8, order: str = "row", enable: bool = True):
 
 def annotate_layout(layout_map: dict):
     for buf, layout in layout_map.items():
+        if layout is None:  # e.g. make_metadata_layout of a global tensor: nothing to annotate
+            continue
         buf.layout = layout
         buf.layout_annotated = True
 

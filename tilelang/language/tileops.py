@@ -99,6 +99,29 @@ gemm_v1 = gemm
 gemm_v2 = gemm
 
 
+def gemm_sp(A_sparse, E, B, C, transpose_A: bool = False, transpose_B: bool = False,
+            policy=GemmWarpPolicy.Square, clear_accum=False, k_pack: int = 1, wg_wait: int = 0):
+    """2:4 structured-sparse tile GEMM ``C (+)= decompress(A_sparse, E) @ op(B)`` on gfx950
+    ``v_smfmac_f32_16x16x64_{f16,bf16}`` (reference ``tilelang/language/experimental/gemm_sp.py:17``,
+    ``src/op/gemm_sp.cc:147``).
+
+    ``A_sparse``: ``[M, K/2]`` (or ``[K/2, M]`` with ``transpose_A``) f16/bf16 — the two kept
+    values of every group of 4 along K, in order.  ``E``: ``[M, K/16]`` int16 metadata — bits
+    ``[2v+1:2v]`` of word ``c`` give the position (0..3) inside its group of value ``v`` of the
+    16-wide K slice ``c`` (the smfmac index format, see ``tilelang.utils.sparse.compress``).
+    ``B``: ``[K, N]`` or ``[N, K]`` (``transpose_B``).  K must be a multiple of 64; the
+    accumulator is fp32."""
+    if wg_wait not in (0, None):
+        raise NotImplementedError("T.gemm_sp: wg_wait is a WGMMA (NVIDIA) feature")
+    A, Er, B, C = to_region(A_sparse), to_region(E), to_region(B), to_region(C)
+    op = O.GemmOp(A, B, C, transpose_A, transpose_B, int(policy), clear_accum, k_pack, wg_wait)
+    op.E = Er
+    return _emit(op)
+
+
+gemm_sp_v2 = gemm_sp
+
+
 _MX_FORMATS = {"e4m3": 0, "e5m2": 1, "e2m3": 2, "e3m2": 3, "e2m1": 4}
 
 

@@ -37,3 +37,18 @@ __all__ = [
     "operand_swizzle", "swizzle_report", "HierarchicalLayout", "make_hierarchical_layout",
     "make_blockwise_zz_layout", "make_linear_layout", "make_swizzled_layout", "physical_size"
 ]
+
+
+def make_metadata_layout(buffer, mma_dtype: str = "float16", block_k: int = None, arch=None, backend=None, **kwargs):
+    """Layout of 2:4 sparse metadata ``E`` for ``T.gemm_sp`` (reference
+    ``tilelang/layout/gemm_sp.py`` ``make_cutlass_metadata_layout``).  The NVIDIA ``mma.sp``
+    metadata needs an interleaved CUTLASS layout; the gfx950 smfmac index of a lane is one
+    16-bit word of the row, so ``E`` stays row-major: a linear layout for a shared tile and
+    nothing to annotate (None) for a global tensor."""
+    shape = buffer.static_shape() if hasattr(buffer, "static_shape") else None
+    if getattr(buffer, "scope", "global") == "global" or shape is None:
+        return None
+    return LinearLayout(shape)
+
+
+make_cutlass_metadata_layout = make_metadata_layout

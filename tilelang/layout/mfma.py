@@ -87,6 +87,17 @@ def mfma_c_fragment(M: int, N: int, warp_m: int, warp_n: int, mn: Tuple[int, int
     return Fragment([M, N], _drop_unit(thread), _drop_unit(local), f"mfma_c{mn[0]}")
 
 
+def mfma_c_fragment_direct(M: int, N: int, warp_m: int, warp_n: int) -> Fragment:
+    """Accumulator of a 16x16 MFMA issued with operands in natural order (``mfma(A, B)``): lane
+    ``l`` holds ``C[4(l>>4) + v][l & 15]``.  Used by the 2:4 sparse GEMM, whose sparse operand
+    must be the instruction's A source, so the swap trick of the dense path is unavailable."""
+    WM, WN = M // warp_m, N // warp_n
+    m_rep, n_rep = WM // 16, WN // 16
+    thread = [Digit(0, WM, warp_m), Digit(1, WN, warp_n), Digit(0, 4, 4), Digit(1, 1, 16)]
+    local = [Digit(0, 16, m_rep), Digit(1, 16, n_rep), Digit(0, 1, 4)]
+    return Fragment([M, N], _drop_unit(thread), _drop_unit(local), "mfma_c16_direct")
+
+
 def mfma_a_fragment(M: int, K: int, warp_m: int, warp_n: int, kperm: int = 0, mn=(16, 16)) -> Fragment:
     """A operand held in registers (gemm_rs).  Replicated over the ``warp_n`` waves.
 

@@ -80,7 +80,7 @@ class _KSplit(Mutator):
         if len(gemms) != 1 or len(copies) != 2 or len(stmts) != 3:
             return loop
         g = gemms[0].op
-        if g.is_mx:
+        if g.is_mx or g.is_sp:
             return loop
         A, B = g.A.buffer, g.B.buffer
         if A.scope != "shared" or B.scope != "shared" or A.dtype.bits != 16 or B.dtype != A.dtype:

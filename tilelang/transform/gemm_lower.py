@@ -157,10 +157,52 @@ def _f32_plan(op: O.GemmOp, plan: Dict, nw: int) -> Dict:
     return plan
 
 
+def _sp_plan(op: O.GemmOp, plan: Dict, num_threads: int, is_cpu: bool) -> Dict:
+    """2:4 sparse A (``v_smfmac_f32_16x16x64_{f16,bf16}``).  Per 64-wide K step the lane
+    (row/col ``l&15``, slice ``g=l>>4``) holds 8 kept A values of original K ``[16g, 16g+16)``
+    (one 16-byte read of the compressed row at ``8g``), the 16-bit index field ``E[row][g]``, and
+    the B values of K ``8g+j`` and ``32+8g+j`` — i.e. exactly two dense 16x16x32 B fragments
+    (measured on gfx950: scripts/probes/smfmac_map.hip).  Issued as ``smfmac(A, B)``, so C is
+    held in the direct (unswapped) MFMA layout."""
+    A, B, C, E = op.A.buffer, op.B.buffer, op.C.buffer, op.E.buffer
+    M, N, K = plan["M"], plan["N"], plan["K"]
+    if A.dtype.name not in ("float16", "bfloat16") or B.dtype != A.dtype:
+        raise ValueError(f"T.gemm_sp on gfx950 supports f16/bf16 operands (v_smfmac_f32_16x16x64), got "
+                         f"{A.dtype} x {B.dtype}")
+    if C.dtype.name != "float32":
+        raise ValueError(f"T.gemm_sp accumulates in float32, got a {C.dtype} accumulator")
+    if K % 64:
+        raise ValueError(f"T.gemm_sp: K={K} must be a multiple of 64 (one v_smfmac_f32_16x16x64 step)")
+    e_ext = _trailing2(op.E)
+    if tuple(e_ext) != (M, K // 16) or E.dtype.bits != 16:
+        raise ValueError(f"T.gemm_sp: metadata E must be a [M, K/16]=[{M}, {K // 16}] int16 tile, got "
+                         f"{list(e_ext)} {E.dtype}")
+    if A.scope != "shared" or B.scope != "shared" or E.scope not in ("shared", "global"):
+        raise ValueError("T.gemm_sp: A_sparse and B must be shared-memory tiles, E shared or global")
+    plan["sp"] = True
+    if is_cpu:
+        plan.update(warp_m=1, warp_n=1, mfma=None,
+                    c_layout=make_linear_fragment([M, N], num_threads, 1, "cpu_c"),
+                    a_smem_layout=LinearLayout(A.static_shape()), b_smem_layout=LinearLayout(B.static_shape()))
+        return plan
+    if num_threads % 64:
+        raise ValueError(f"block size {num_threads} is not a multiple of the 64-lane wavefront")
+    warp_m, warp_n = MF.compute_warp_partition(M, N, num_threads // 64, op.policy)
+    plan.update(warp_m=warp_m, warp_n=warp_n, mfma=(16, 16, 64))
+    plan["c_layout"] = MF.mfma_c_fragment_direct(M, N, warp_m, warp_n)
+    plan["a_kind"] = "tr" if op.trans_A else "k_rows"
+    plan["b_kind"] = "k_rows" if op.trans_B else "tr"
+    plan["a_smem_layout"] = MF.operand_swizzle(plan["a_kind"], A.static_shape(), 2)
+    plan["b_smem_layout"] = MF.operand_swizzle(plan["b_kind"], B.static_shape(), 2)
+    return plan
+
+
 def gemm_plan(op: O.GemmOp, num_threads: int, target=None, a_layout: Optional[Fragment] = None) -> Dict:
     a_ext, b_ext, c_ext = _trailing2(op.A), _trailing2(op.B), _trailing2(op.C)
     M, N = c_ext
     K = a_ext[0] if op.trans_A else a_ext[1]
+    if op.is_sp:
+        K *= 2  # A_sparse keeps 2 of every 4 K values
     kb = b_ext[1] if op.trans_B else b_ext[0]
     am = a_ext[1] if op.trans_A else a_ext[0]
     bn = b_ext[0] if op.trans_B else b_ext[1]
@@ -172,6 +214,8 @@ def gemm_plan(op: O.GemmOp, num_threads: int, target=None, a_layout: Optional[Fr
     is_cpu = target is not None and getattr(target, "kind", "hip") == "cpu"
     A, B, C = op.A.buffer, op.B.buffer, op.C.buffer
     plan = dict(M=M, N=N, K=K, a_kperm=0)
+    if op.is_sp:
+        return _sp_plan(op, plan, num_threads, is_cpu)
     if is_cpu and not op.is_mx:
         plan.update(warp_m=1, warp_n=1, mfma=None, c_layout=make_linear_fragment([M, N], num_threads, 1, "cpu_c"),
                     a_smem_layout=LinearLayout(A.static_shape() or a_ext),

@@ -91,8 +91,11 @@ def plan_lds(kernel: S.KernelStmt, reuse: bool = True, aggressive: bool = False)
     touches them) do not overlap share bytes; a ``__syncthreads()`` is inserted in front of the
     first statement that touches a buffer re-using bytes of a buffer that died earlier, so every
     access of the old tenant (any thread) is ordered before the new tenant's first access.
-    LDS-DMA (pipeline stage) buffers keep their bytes for the whole kernel unless ``aggressive``
-    (``tl.enable_aggressive_shared_memory_merge``).
+    ``aggressive`` (``tl.enable_aggressive_shared_memory_merge``, default on): LDS-DMA (pipeline
+    stage) buffers die at their last top-level use too, and the switch into their bytes is
+    preceded by ``s_waitcnt vmcnt(0)`` so no DMA still in flight can land in the new tenant (e.g.
+    the LDS ring of a GEMM main loop re-used by its C staging tile).  Off: DMA targets keep their
+    bytes for the whole kernel.
 
     Returns ``(kernel, offsets, total_bytes)``."""
     shared = []
@@ -108,7 +111,8 @@ def plan_lds(kernel: S.KernelStmt, reuse: bool = True, aggressive: bool = False)
         for b in t:
             first.setdefault(b, i)
             last[b] = i
-    pinned = set() if aggressive else _dma_targets(kernel)
+    dma = _dma_targets(kernel)
+    pinned = set() if aggressive else dma
     n_top = len(top)
     f = [0 if (b in pinned or b not in first) else first[b] for b in shared]
     l_ = [n_top if (b in pinned or b not in last) else last[b] for b in shared]
@@ -122,7 +126,7 @@ def plan_lds(kernel: S.KernelStmt, reuse: bool = True, aggressive: bool = False)
     if not reuse or kernel.is_cpu:
         return kernel, offsets, total
     # region switches: statement index -> needs a barrier in front
-    switch = set()
+    switch, drain = set(), set()
     for i, b in enumerate(shared):
         for j, a in enumerate(shared):
             if a is b or l_[j] >= f[i]:
@@ -130,11 +134,15 @@ def plan_lds(kernel: S.KernelStmt, reuse: bool = True, aggressive: bool = False)
             oa, ob = offsets[a], offsets[b]
             if oa < ob + sizes[b] and ob < oa + sizes[a]:
                 switch.add(f[i])
+                if a in dma:
+                    drain.add(f[i])
     if not switch:
         return kernel, offsets, total
     from .thread_sync import _sync
     new_top = []
     for i, st in enumerate(top):
+        if i in drain:
+            new_top.append(L.CallStmt("tl::wait_vmcnt", [], [0]))
         if i in switch:
             new_top.append(_sync())
         new_top.append(st)

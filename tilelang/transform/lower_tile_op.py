@@ -981,6 +981,8 @@ class TileOpLowerer(Mutator):
         ctype = _dt.hip_type(A.dtype)
         if op.is_mx:
             return self._lower_mx_gemm(op, plan, cl, out)
+        if op.is_sp:
+            return self._lower_sp_gemm(op, plan, cl, out)
         if ctx.is_cpu:
             pa = self._operand_ptr(op.A)
             pb = self._operand_ptr(op.B)
@@ -1059,6 +1061,25 @@ class TileOpLowerer(Mutator):
         targs += [plan["warp_m"], plan["warp_n"], A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
                   B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u", sa_shape[-1], sb_shape[-1]]
         out.append(L.CallStmt("tl::gemm_ss_mx", [pa, pb, psa, psb, L.BufferPtr(cl, 0)], targs))
+        return S.SeqStmt(out)
+
+    def _lower_sp_gemm(self, op: O.GemmOp, plan, cl, out):
+        """``tl::gemm_sp_ss`` (v_smfmac_f32_16x16x64) / ``tl::cpu_gemm_sp``: 2:4 sparse A."""
+        A, B, E = op.A.buffer, op.B.buffer, op.E.buffer
+        pa, pb, pe = self._operand_ptr(op.A), self._operand_ptr(op.B), self._operand_ptr(op.E)
+        e_shape = E.static_shape()
+        if e_shape is None:
+            raise LoweringError("T.gemm_sp: the metadata buffer needs a static shape (row stride)")
+        ctype = (_dt.cpu_type if self.ctx.is_cpu else _dt.hip_type)(A.dtype)
+        if self.ctx.is_cpu:
+            out.append(L.CallStmt("tl::cpu_gemm_sp", [pa, pe, pb, L.BufferPtr(cl, 0)], [
+                ctype, plan["M"], plan["N"], plan["K"], int(op.trans_A), int(op.trans_B), A.static_shape()[-1],
+                e_shape[-1], B.static_shape()[-1]]))
+            return S.SeqStmt(out)
+        out.append(L.CallStmt("tl::gemm_sp_ss", [pa, pe, pb, L.BufferPtr(cl, 0)], [
+            ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_A), _b(op.trans_B),
+            A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u", e_shape[-1],
+            B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u"]))
         return S.SeqStmt(out)
 
     def _operand_ptr(self, r: BufferRegion):

@@ -53,8 +53,9 @@ EFFECT = {
     "tl.config_index_bitwidth": "32 or 64: width of global-memory offsets (default: 64 only for tensors of "
                                 ">= 2^31 elements; the launcher refuses tensors too large for a 32-bit kernel)",
     "tl.disable_safe_memory_legalize": "no bounds guards on global accesses",
-    "tl.enable_aggressive_shared_memory_merge": "LDS buffers of disjoint live ranges share the arena even "
-                                                "across pipelined loops' stage buffers",
+    "tl.enable_aggressive_shared_memory_merge": "default True: LDS-DMA stage buffers of pipelined loops share "
+                                                "the arena with later buffers (vmcnt(0) drain + barrier at "
+                                                "the switch); False pins them for the whole kernel",
     "tl.lds_reuse": "liveness-based LDS arena sharing (False: every shared buffer gets its own bytes)",
     "tl.disable_thread_storage_sync": "no automatic __syncthreads insertion",
     "tl.force_let_inline": "every let binding inside a kernel is substituted into its uses",
