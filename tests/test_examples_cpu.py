@@ -464,3 +464,15 @@ def test_flash_attention_varlen_cpu(causal):
     tilelang.compile(f, out_idx=[5], target="hip")
     o = tilelang.compile(f, out_idx=[5], target="cpu")(q, k, v, cq, ck)
     torch.testing.assert_close(o.float(), ref_program(q, k, v, cq, ck, causal).float(), rtol=2e-2, atol=2e-2)
+
+
+def test_mla_decode_persistent_cpu():
+    """One persistent kernel: split-KV tiles, T.sync_grid (host threads on the CPU target), combine."""
+    from example_mla_decode_persistent import mla_decode_persistent
+    from example_mla_decode import ref_program
+    B, H, S, D, P, NS = 2, 64, 256, 128, 32, 2
+    k = _both(mla_decode_persistent, B, H, 1, S, D, P, block_N=32, block_H=32, num_split=NS, num_cu=3, threads=256)
+    q, qp = torch.randn(B, H, D, dtype=torch.float16), torch.randn(B, H, P, dtype=torch.float16)
+    kv, kp = torch.randn(B, S, 1, D, dtype=torch.float16), torch.randn(B, S, 1, P, dtype=torch.float16)
+    o = k(q, qp, kv, kp, torch.empty(B, H, NS), torch.empty(B, H, NS, D))
+    torch.testing.assert_close(o.float(), ref_program(q, qp, kv, kp).float(), rtol=2e-2, atol=2e-2)

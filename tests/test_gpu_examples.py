@@ -33,3 +33,18 @@ def test_mla_decode(batch, heads, kv_ctx, num_split):
     part = torch.empty(batch, heads, num_split, 512, device="cuda")
     out = k(q, q_pe, kv, k_pe, glse, part)
     torch.testing.assert_close(out.float(), ref_program(q, q_pe, kv, k_pe).float(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("batch,heads,kv_ctx,num_split", [(4, 128, 1024, 4), (3, 64, 512, 2)])
+def test_mla_decode_persistent(batch, heads, kv_ctx, num_split):
+    from example_mla_decode_persistent import mla_decode_persistent
+    from example_mla_decode import ref_program
+    k = mla_decode_persistent(batch, heads, 1, kv_ctx, 512, 64, num_split=num_split)
+    q = torch.randn(batch, heads, 512, device="cuda", dtype=torch.float16)
+    q_pe = torch.randn(batch, heads, 64, device="cuda", dtype=torch.float16)
+    kv = torch.randn(batch, kv_ctx, 1, 512, device="cuda", dtype=torch.float16)
+    k_pe = torch.randn(batch, kv_ctx, 1, 64, device="cuda", dtype=torch.float16)
+    glse = torch.empty(batch, heads, num_split, device="cuda")
+    part = torch.empty(batch, heads, num_split, 512, device="cuda")
+    out = k(q, q_pe, kv, k_pe, glse, part)
+    torch.testing.assert_close(out.float(), ref_program(q, q_pe, kv, k_pe).float(), rtol=2e-2, atol=2e-2)

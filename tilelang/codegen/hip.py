@@ -436,7 +436,34 @@ class CodeGen:
             hdr.append(k.prelude)
         nthreads = k.num_threads
         out = hdr + [""]
-        if self.is_cpu:
+        if self.is_cpu and any("tl::sync_grid()" in ln for ln in body):
+            # grid-wide barrier on the CPU target: every block is a host thread (their shared
+            # tiles are thread_local) meeting at tl::sync_grid(); block ids unpacked x-fastest
+            out.append(f'extern "C" void {kname}({", ".join(sig)}) {{')
+            gs = [self.e(g) for g in k.grid]
+            total = " * ".join(f"({g})" for g in gs) or "1"
+            out.append(f"  const int tl_nblocks = {total};")
+            out.append("  tl::GridBarrier tl_gbar(tl_nblocks);")
+            out.append("  std::vector<std::thread> tl_threads;")
+            out.append("  for (int tl_b = 0; tl_b < tl_nblocks; ++tl_b) {")
+            out.append("    tl_threads.emplace_back([&, tl_b]() {")
+            out.append("      tl::cur_grid_barrier() = &tl_gbar;")
+            stride = "1"
+            for v, g in zip(k.block_vars, gs):
+                vn = self.name_of(v, v.name)
+                out.append(f"      const int {vn} = (tl_b / ({stride})) % ({g});")
+                stride = f"({stride}) * ({g})"
+            out += ["    " + ln for ln in body]
+            out.append("    });")
+            out.append("  }")
+            out.append("  for (auto& t : tl_threads) t.join();")
+            out.append("}")
+            unpack = []
+            for i, p in enumerate(params):
+                ty = sig[i].rsplit(" ", 1)[0].replace("__restrict__", "").strip()
+                unpack.append(f"*reinterpret_cast<{ty}*>(args[{i}])")
+            out.append(f'extern "C" void tl_entry(void** args) {{ {kname}({", ".join(unpack)}); }}')
+        elif self.is_cpu:
             out.append(f'extern "C" void {kname}({", ".join(sig)}) {{')
             # grid loops
             depth = 0

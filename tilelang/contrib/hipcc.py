@@ -80,7 +80,7 @@ def compile_cpu(source: str, out_path: str, options: Optional[List[str]] = None,
     with tempfile.TemporaryDirectory(prefix="tl_cpu_") as d:
         src = Path(d) / "kernel.cpp"
         src.write_text(source)
-        cmd = [clang_path(), "-O2", "-std=c++17", "-shared", "-fPIC", "-I", str(INCLUDE_DIR), "-w"] + \
+        cmd = [clang_path(), "-O2", "-std=c++17", "-shared", "-fPIC", "-pthread", "-I", str(INCLUDE_DIR), "-w"] + \
             list(options or []) + ["-o", out_path, str(src)]
         if verbose:
             print(" ".join(cmd))

@@ -9,6 +9,10 @@
 #include <string.h>
 #include <cmath>
 #include <type_traits>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 typedef _Float16 half_t;
 typedef __bf16 bfloat16_t;
@@ -132,7 +136,33 @@ template <int B> inline void copy_bytes(void* dst, const void* src) { memcpy(dst
 
 inline void sync_threads() {}
 inline void sync_warp() {}
-inline void sync_grid() {}  // CPU target: blocks run one after another (no co-residency)
+// T.sync_grid on the CPU target: kernels that use it run every block as a host thread
+// (codegen/hip.py) meeting at this generation-counting barrier.
+struct GridBarrier {
+  explicit GridBarrier(int n) : n_(n) {}
+  void wait() {
+    std::unique_lock<std::mutex> lk(m_);
+    const long gen = gen_;
+    if (++count_ == n_) {
+      count_ = 0;
+      ++gen_;
+      cv_.notify_all();
+    } else {
+      cv_.wait(lk, [&] { return gen_ != gen; });
+    }
+  }
+  int n_, count_ = 0;
+  long gen_ = 0;
+  std::mutex m_;
+  std::condition_variable cv_;
+};
+inline GridBarrier*& cur_grid_barrier() {
+  static thread_local GridBarrier* b = nullptr;
+  return b;
+}
+inline void sync_grid() {
+  if (cur_grid_barrier()) cur_grid_barrier()->wait();
+}
 inline void print_val(const char* msg, double v) { printf("%s: %g\n", msg, v); fflush(stdout); }
 inline void print_val(const char* msg, float v) { print_val(msg, (double)v); }
 inline void print_val(const char* msg, half_t v) { print_val(msg, (double)(float)v); }
