@@ -476,3 +476,28 @@ def test_mla_decode_persistent_cpu():
     kv, kp = torch.randn(B, S, 1, D, dtype=torch.float16), torch.randn(B, S, 1, P, dtype=torch.float16)
     o = k(q, qp, kv, kp, torch.empty(B, H, NS), torch.empty(B, H, NS, D))
     torch.testing.assert_close(o.float(), ref_program(q, qp, kv, kp).float(), rtol=2e-2, atol=2e-2)
+
+
+def test_gqa_decode_varlen_logits_contiguous_and_paged():
+    import example_gqa_decode_varlen_logits as m
+    lens, b, h, kh, d, bn, ns = [150, 256, 37], 3, 8, 2, 64, 32, 3
+    q, k, v, cu, s_aux, kp, vp, table = m.make_inputs(lens, h, kh, d, "cpu", torch.float16, True, page_size=64)
+    ro, rs = m.ref_program(q, k, v, cu, s_aux, bn)
+    kern = _both(m.flashattn, b, h, kh, max(lens), k.shape[0], d, True, block_N=bn, num_split=ns)
+    o, s = m.AttnPoolDecode(kern, b, h, d, ns, max(lens), bn, "cpu")(q, k, v, cu, s_aux)
+    torch.testing.assert_close(o.float(), ro, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(s.float(), rs, rtol=1e-2, atol=1e-2)
+    kern = _both(m.flashattn_paged, b, h, kh, max(lens), kp.shape[0], d, True, 64, block_N=bn, num_split=ns)
+    o, s = m.AttnPoolDecode(kern, b, h, d, ns, max(lens), bn, "cpu")(q, kp, vp, cu, s_aux, table)
+    torch.testing.assert_close(o.float(), ro, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(s.float(), rs, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_mha_inference_split_kv(causal):
+    import example_mha_inference as m
+    b, h, sq, sk, d, ns = 1, 2, 80, 300, 64, 3
+    k = _both(m.flashattn, b, h, sq, sk, d, causal, 64, 32, ns, 256)
+    q, kk, v = torch.randn(b, sq, h, d).half(), torch.randn(b, sk, h, d).half(), torch.randn(b, sk, h, d).half()
+    o = k(q, kk, v, torch.empty(b, h, ns, sq), torch.empty(b, sq, h, ns, d))
+    torch.testing.assert_close(o.float(), m.ref_program(q, kk, v, causal).float(), rtol=1e-2, atol=1e-2)

@@ -362,3 +362,31 @@ def test_flash_attention_varlen_gpu():
     q, k, v, cq, ck = make_varlen([300, 1024, 77, 513], [300, 1100, 200, 513], 8, 2, 128, "cuda")
     o = flashattn_varlen(4, 8, q.shape[0], k.shape[0], 1024, 128, True, 4)(q, k, v, cq, ck)
     torch.testing.assert_close(o.float(), ref_program(q, k, v, cq, ck).float(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("paged", [False, True])
+def test_gqa_decode_varlen_logits(paged):
+    import example_gqa_decode_varlen_logits as m
+    lens, b, h, kh, d = [1500, 4096, 377, 2900], 4, 32, 8, 128
+    q, k, v, cu, s_aux, kp, vp, table = m.make_inputs(lens, h, kh, d, "cuda", torch.float16, True, page_size=128)
+    ro, rs = m.ref_program(q, k, v, cu, s_aux, 64)
+    if paged:
+        kern = m.flashattn_paged(b, h, kh, max(lens), kp.shape[0], d, True, 128)
+        o, s = m.AttnPoolDecode(kern, b, h, d, 8, max(lens), 64, "cuda")(q, kp, vp, cu, s_aux, table)
+    else:
+        kern = m.flashattn(b, h, kh, max(lens), k.shape[0], d, True)
+        o, s = m.AttnPoolDecode(kern, b, h, d, 8, max(lens), 64, "cuda")(q, k, v, cu, s_aux)
+    torch.testing.assert_close(o.float(), ro, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(s.float(), rs, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_mha_inference_split_kv(causal):
+    import example_mha_inference as m
+    b, h, sq, sk, d, ns = 2, 8, 128, 2048, 128, 8
+    k = m.flashattn(b, h, sq, sk, d, causal, num_split=ns)
+    q = torch.randn(b, sq, h, d, device="cuda", dtype=torch.float16)
+    kk, v = torch.randn(b, sk, h, d, device="cuda", dtype=torch.float16), torch.randn(b, sk, h, d, device="cuda",
+                                                                                       dtype=torch.float16)
+    o = k(q, kk, v, torch.empty(b, h, ns, sq, device="cuda"), torch.empty(b, sq, h, ns, d, device="cuda"))
+    torch.testing.assert_close(o.float(), m.ref_program(q, kk, v, causal).float(), rtol=1e-2, atol=1e-2)
