@@ -97,6 +97,33 @@ def flashattn_varlen(batch, heads, total_q, total_k, max_seqlen_q, dim, is_causa
     return main
 
 
+class flashattn:  # noqa: N801  (reference-named entry)
+    """Reference-compatible entry (reference examples/flash_attention/example_mha_fwd_varlen.py:71-101):
+    ``flashattn(batch_size, UQ, UKV, heads, dim, is_causal)`` returns a kernel called as
+    ``kernel(Q_unpad, K_unpad, V_unpad, cu_seqlens_q, cu_seqlens_k, max_seqlen_q) -> Output_unpad``.
+
+    ``max_seqlen_q`` is a runtime value there; here it sizes the grid, so it is rounded up to a
+    power-of-two number of ``block_M`` tiles and one kernel is compiled per bucket (a handful
+    at most).  The reference defaults to non-causal, and so does this entry.  Causal masking is
+    bottom-right aligned (FlashAttention-2 semantics); for q_len == k_len — the only case the
+    reference's driver checks — that is the same as its top-left mask."""
+
+    def __init__(self, batch_size, UQ, UKV, heads, dim, is_causal=False, groups=1, dtype="float16", **kw):
+        self.args = (batch_size, heads, UQ, UKV, dim, is_causal, groups)
+        self.dtype, self.kw, self.kernels = dtype, kw, {}
+
+    def __call__(self, q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q):
+        bm = self.kw.get("block_M", 256)
+        tiles = 1
+        while tiles * bm < int(max_seqlen_q):
+            tiles *= 2
+        key = tiles * bm
+        if key not in self.kernels:
+            b, h, uq, ukv, d, causal, g = self.args
+            self.kernels[key] = flashattn_varlen(b, h, uq, ukv, key, d, causal, g, dtype=self.dtype, **self.kw)
+        return self.kernels[key](q, k, v, cu_seqlens_q, cu_seqlens_k)
+
+
 def ref_program(q, k, v, cu_q, cu_k, is_causal=True):
     import torch
     H = q.shape[1]

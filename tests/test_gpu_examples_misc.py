@@ -390,3 +390,14 @@ def test_mha_inference_split_kv(causal):
                                                                                        dtype=torch.float16)
     o = k(q, kk, v, torch.empty(b, h, ns, sq, device="cuda"), torch.empty(b, sq, h, ns, d, device="cuda"))
     torch.testing.assert_close(o.float(), m.ref_program(q, kk, v, causal).float(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_flash_attention_varlen_reference_entry_gpu(causal):
+    """The reference-named flashattn(batch, UQ, UKV, heads, dim, causal) entry; non-causal is its default."""
+    from example_mha_fwd_varlen import flashattn, make_varlen, ref_program
+    lens = [300, 1024, 77, 513]
+    q, k, v, cq, ck = make_varlen(lens, lens, 8, 8, 128, "cuda", torch.float16)
+    kern = flashattn(4, q.shape[0], k.shape[0], 8, 128, causal)
+    o = kern(q, k, v, cq, ck, max(lens))
+    torch.testing.assert_close(o.float(), ref_program(q, k, v, cq, ck, causal).float(), rtol=2e-2, atol=2e-2)

@@ -55,6 +55,10 @@ def _key(source: str, flags, kind: str) -> str:
 
 
 def compile_hip_cached(source: str, flags=None, verbose=False) -> bytes:
+    from ..engine.callback import hip_compile_override
+    data = hip_compile_override(source, "hip")  # register_hip_compile hook: never cached
+    if data is not None:
+        return data
     key = _key(source, flags, "hip-gfx950")
     with _lock:
         if key in _mem:

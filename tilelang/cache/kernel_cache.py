@@ -64,7 +64,8 @@ def _freeze(x):
 
 
 def kernel_key(func, target, out_idx, pass_configs, compile_flags) -> str:
-    blob = json.dumps({"ir": func.script(), "target": str(target), "out_idx": _freeze(out_idx),
+    from ..engine.callback import hook_fingerprint
+    blob = json.dumps({"hooks": hook_fingerprint(), "ir": func.script(), "target": str(target), "out_idx": _freeze(out_idx),
                        "pass_configs": _freeze(pass_configs or {}), "flags": _freeze(compile_flags or []),
                        "compiler": compiler_fingerprint()}, sort_keys=True)
     return hashlib.sha256(blob.encode()).hexdigest()

@@ -145,7 +145,11 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
     ks: KernelSource = generate(func, lk, target, offsets, total, name, cfg)
     timings["codegen"] = timings.get("codegen", 0) + time.perf_counter() - t
     layout_info = {b.name: repr(lay) for b, lay in li.frag.items()}
-    return DeviceKernel(ks.source, ks.kernel_name, ks.grid, ks.block, ks.lds_bytes, ks.params, lk, layout_info,
+    src = ks.source
+    if target.kind == "hip":
+        from .callback import apply_hip_postproc
+        src = apply_hip_postproc(src, target)  # register_hip_postproc hook (engine/callback.py)
+    return DeviceKernel(src, ks.kernel_name, ks.grid, ks.block, ks.lds_bytes, ks.params, lk, layout_info,
                         lk.attrs.get("mesh"), set(lk.attrs.get("narrow_index", ())),
                         bool(lk.attrs.get("cooperative", False)))
 

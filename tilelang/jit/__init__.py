@@ -36,7 +36,9 @@ def compile(func: S.PrimFunc = None, out_idx=None, execution_backend: str = "aut
             target_host=None, verbose: bool = False, pass_configs: Optional[dict] = None,
             compile_flags: Optional[List[str]] = None) -> JITKernel:  # noqa: A001
     """Compile a PrimFunc into a callable kernel (memoised on the printed IR + options)."""
-    key = (func.script(), _freeze(out_idx), str(target), _freeze(pass_configs), _freeze(compile_flags))
+    from ..engine.callback import hook_fingerprint
+    key = (func.script(), _freeze(out_idx), str(target), _freeze(pass_configs), _freeze(compile_flags),
+           hook_fingerprint())
     k = _GLOBAL_JIT_CACHE.get(key)
     if k is None:
         k = JITKernel(func, out_idx=out_idx, target=target, target_host=target_host,
