@@ -67,6 +67,8 @@ PYBIND11_MODULE(_tl_core, m) {
            "register of `buf` holding buf[A @ idx + b] for register r of this loop layout on every thread "
            "(-1 not owned, -2 non-uniform)");
 
+  m.def("reduce_owners", &reduce_owners, py::arg("src"), py::arg("dst"), py::arg("dim"), py::arg("squeeze"),
+        py::arg("T"), "dst register of every src register for a tile reduction over `dim` (empty = incompatible)");
   m.def("lds_instruction_cycles", [](const std::string& instr, const std::vector<int64_t>& addrs) {
     if (addrs.size() != 64) throw std::invalid_argument("need 64 lane addresses");
     return instruction_cycles(lds_instr(instr), addrs.data());

@@ -124,4 +124,35 @@ int64_t Fragment::resolve_affine(const Fragment& buf, const std::vector<int64_t>
   return result;
 }
 
+std::vector<int64_t> reduce_owners(const Fragment& src, const Fragment& dst, int dim, bool squeeze, int64_t T) {
+  const int sn = src.ndim(), dn = dst.ndim();
+  const int64_t SL = src.local_size(), DL = dst.local_size();
+  std::vector<int64_t> owner((size_t)SL, -1);
+  std::vector<int64_t> idx((size_t)sn), didx((size_t)std::max(dn, 1)), dtab((size_t)(DL * std::max(dn, 1)));
+  for (int64_t t = 0; t < T; ++t) {
+    for (int64_t q = 0; q < DL; ++q) dst.inverse(t, q, &dtab[(size_t)(q * dn)]);
+    for (int64_t r = 0; r < SL; ++r) {
+      src.inverse(t, r, idx.data());
+      int k = 0;
+      for (int i = 0; i < sn; ++i) {
+        if (i == dim) {
+          if (squeeze) didx[(size_t)k++] = 0;
+        } else {
+          didx[(size_t)k++] = idx[(size_t)i];
+        }
+      }
+      int64_t li = -1;
+      for (int64_t q = 0; q < DL && li < 0; ++q) {
+        bool eq = true;
+        for (int i = 0; i < dn && eq; ++i) eq = dtab[(size_t)(q * dn + i)] == didx[(size_t)i];
+        if (eq) li = q;
+      }
+      if (li < 0) return {};
+      if (owner[(size_t)r] < 0) owner[(size_t)r] = li;
+      else if (owner[(size_t)r] != li) return {};
+    }
+  }
+  return owner;
+}
+
 }  // namespace tlcore

@@ -58,4 +58,10 @@ class Fragment {
   void validate() const;
 };
 
+// Reduction grouping of tile_op lowering (lower_tile_op._reduce_groups): for every register r of
+// `src`, the register of `dst` that every thread 0..T-1 holding src element idx (idx with `dim`
+// set to 0 when `squeeze`, else removed) owns; empty when some thread does not own that element
+// or two threads disagree (the layouts are not reduce-compatible).
+std::vector<int64_t> reduce_owners(const Fragment& src, const Fragment& dst, int dim, bool squeeze, int64_t T);
+
 }  // namespace tlcore

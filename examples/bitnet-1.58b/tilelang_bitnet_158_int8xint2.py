@@ -10,12 +10,14 @@ C [M, N] int32 = A int8 [M, K] @ B^T with B the unsigned 2-bit codes packed four
 import argparse
 
 import tilelang
-from tilelang.ops.bitnet import int2_gemm_kernel, pack_int2
+from tilelang.ops.bitnet import int2_gemm_kernel, int2_gemv_kernel, pack_int2
 
 
-def bitnet_158_int8xint2_decode(M, N, K, in_dtype="int8", out_dtype="int32", accum_dtype="int32"):
-    assert (in_dtype, out_dtype, accum_dtype) == ("int8", "int32", "int32")
-    return int2_gemm_kernel(M, N, K, 0, "int32")
+def bitnet_158_int8xint2_decode(M, N, K, in_dtype="int8", out_dtype="float32", accum_dtype="int32"):
+    """Decode (M <= 8): the weight-streaming GEMV kernel; with unit scales its fp32 output is the
+    exact int32 product.  Call as kernel(A, qw, ones(M), ones(N))."""
+    assert (in_dtype, accum_dtype) == ("int8", "int32") and M <= 8
+    return int2_gemv_kernel(M, N, K, -(-K // 256) * 256, 0, out_dtype)
 
 
 def bitnet_158_int8xint2_prefill(M, N, K, in_dtype="int8", out_dtype="int32", accum_dtype="int32"):
@@ -25,13 +27,21 @@ def bitnet_158_int8xint2_prefill(M, N, K, in_dtype="int8", out_dtype="int32", ac
 
 def check(M, N, K):
     import torch
-    kern = bitnet_158_int8xint2_decode(M, N, K) if M <= 16 else bitnet_158_int8xint2_prefill(M, N, K)
     A = torch.randint(0, 4, (M, K), device="cuda", dtype=torch.int8)
     B = torch.randint(0, 2, (N, K), device="cuda")
-    qw = pack_int2(B)
-    C = kern(A, qw)
-    torch.testing.assert_close(C, (A.double() @ B.double().t()).int(), rtol=0, atol=0)
-    lat = tilelang.profiler.do_bench(lambda: kern(A, qw))
+    ref = (A.double() @ B.double().t())
+    if M <= 8:
+        kern = bitnet_158_int8xint2_decode(M, N, K)
+        Kp = -(-K // 256) * 256
+        qw = pack_int2(torch.nn.functional.pad(B, (0, Kp - K)))
+        args = (A, qw, torch.ones(M, device="cuda"), torch.ones(N, device="cuda"))
+        torch.testing.assert_close(kern(*args).double(), ref, rtol=0, atol=0)
+    else:
+        kern = bitnet_158_int8xint2_prefill(M, N, K)
+        args = (A, pack_int2(B))
+        torch.testing.assert_close(kern(*args), ref.int(), rtol=0, atol=0)
+    qw = args[1]
+    lat = tilelang.profiler.do_bench(lambda: kern(*args))
     print(f"int8 x int2 M{M} N{N} K{K}: {lat * 1e3:.1f} us, {2 * M * N * K / lat * 1e-9:.1f} TOPS, "
           f"{N * K / 4 / lat * 1e-6:.0f} GB/s weights")
 

@@ -23,7 +23,10 @@ from example_mha_fwd import FAST_MATH, ref_program
 
 @tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
 def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=256, block_N=64,
-                        threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True):
+                        threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
+                        young_prio=False):
+    """``young_prio``: the second-dispatched half of the waves runs at issue priority 1 (one
+    ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4)."""
     scale = (1.0 / dim)**0.5 * 1.44269504
     head_kv = heads // groups
     q_shape = [batch, seq_len, heads, dim]
@@ -62,6 +65,9 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
             T.fill(logsum, 0)
             T.fill(scores_max, -(2.0**30) if lazy_rescale else -T.infinity(accum_dtype))
             rescale = 1
+            if young_prio:
+                if T.get_thread_binding() >= threads // 2:
+                    T.set_priority(1)
 
             loop_range = (T.ceildiv((bx + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N))
 

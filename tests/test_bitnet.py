@@ -71,3 +71,30 @@ def test_rms_norm_quant_gpu():
 @pytest.mark.gpu
 def test_bitnet_layer_gpu():
     _layer("cuda", 128)
+
+
+def _gemv(device, M, N, Kd):
+    Kp = -(-Kd // 256) * 256
+    x = torch.randint(-128, 128, (M, Kd), dtype=torch.int8, device=device)
+    codes = torch.randint(0, 3, (N, Kd), device=device)
+    wq = K.pack_int2(torch.nn.functional.pad(codes, (0, Kp - Kd), value=1))
+    sx, sw = torch.rand(M, device=device) + 0.5, torch.rand(N, device=device) + 0.5
+    out = K.int2_gemm(x, wq, sx, sw, out_dtype=torch.float32, zero=1)
+    ref = (x.double() @ (codes.double() - 1).t()) / (sx.double()[:, None] * sw.double()[None])
+    torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-3)
+
+
+def test_int2_gemv_decode_cpu():
+    _gemv("cpu", 1, 48, 320)
+    _gemv("cpu", 3, 64, 512)
+
+
+@pytest.mark.gpu
+def test_int2_gemv_decode_gpu():
+    _gemv("cuda", 1, 3200, 3200)
+    _gemv("cuda", 4, 3200, 8640)
+
+
+@pytest.mark.gpu
+def test_bitnet_layer_decode_gpu():
+    _layer("cuda", 1)

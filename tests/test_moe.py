@@ -60,13 +60,17 @@ def test_router_and_align_match_reference():
     torch.testing.assert_close(w, rw)
     for stable in (True, False):
         mr = K.max_padded_rows(600, 8, 16)
-        dest, row_src, te, counts = K.dispatch_plan(ids, 8, 16, mr, div=2, stable=stable)
+        dest, row_src, te, counts, trows = K.dispatch_plan(ids, 8, 16, mr, div=2, stable=stable)
         flat = ids.reshape(-1).long()
         assert counts.tolist() == torch.bincount(flat, minlength=8).tolist()
         d = dest.long()
         assert len(set(d.tolist())) == flat.numel()
         assert (te[d // 16].long() == flat).all()
         assert (row_src[d].long() == torch.arange(600) // 2).all()
+        ends = torch.zeros(mr // 16, dtype=torch.long)  # valid rows of every tile: a prefix
+        for r in d.tolist():
+            ends[r // 16] = max(int(ends[r // 16]), r % 16 + 1)
+        assert trows.long().tolist() == ends.tolist()
         if stable:  # assignment order kept inside every expert
             for e in range(8):
                 de = d[flat == e]

@@ -249,6 +249,8 @@ class CodeGen:
             return "tl::sync_warp()"
         if op == "tl.sync_grid":
             return "tl::sync_grid()"
+        if op == "tl.setprio":
+            return "(void)0" if self.is_cpu else f"__builtin_amdgcn_s_setprio({int(args[0].value)})"
         raise CodeGenError(f"unknown intrinsic {op}")
 
     def buf_ref(self, b: Buffer) -> str:

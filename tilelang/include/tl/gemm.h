@@ -109,7 +109,8 @@ TL_DEVICE typename mfma_traits<T>::frag ld_operand(const T* base, int mn0, int k
 // A: LDS tile [M][K] (TA=false) or [K][M] (TA=true); B: [K][N] (TB=false) or [N][K] (TB=true).
 template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TA, bool TB, int A_COLS, uint32_t SWZ_A,
           int B_COLS, uint32_t SWZ_B>
-TL_DEVICE void gemm_ss(const T* __restrict__ A, const T* __restrict__ B, float* __restrict__ C) {
+TL_DEVICE void gemm_ss(const T* __restrict__ A, const T* __restrict__ B, float* __restrict__ C,
+                       int m_limit = 0x3fffffff) {
   typedef mfma_traits<T> MT;
   typedef typename MT::frag F;
   constexpr int WM = M / WARP_M, WN = N / WARP_N;
@@ -118,6 +119,9 @@ TL_DEVICE void gemm_ss(const T* __restrict__ A, const T* __restrict__ B, float* 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int wm = wave / WARP_N, wn = wave % WARP_N;
+  // T.gemm(valid_m=): a wave whose rows all lie at or past the tile's valid-row count issues
+  // nothing (its accumulator rows are don't-care padding); uniform branch, folded when unused
+  if (wm * WM >= m_limit) return;
   floatx4* acc = reinterpret_cast<floatx4*>(C);
 #pragma unroll
   for (int kk = 0; kk < KSTEPS; ++kk) {
@@ -372,7 +376,8 @@ TL_DEVICE typename mfma32_traits<T>::frag ld_operand32(const T* base, int mn0, i
 
 template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TA, bool TB, int A_COLS, uint32_t SWZ_A,
           int B_COLS, uint32_t SWZ_B>
-TL_DEVICE void gemm_ss_32(const T* __restrict__ A, const T* __restrict__ B, float* __restrict__ C) {
+TL_DEVICE void gemm_ss_32(const T* __restrict__ A, const T* __restrict__ B, float* __restrict__ C,
+                          int m_limit = 0x3fffffff) {
   typedef mfma32_traits<T> MT;
   typedef typename MT::frag F;
   constexpr int WM = M / WARP_M, WN = N / WARP_N;
@@ -381,6 +386,7 @@ TL_DEVICE void gemm_ss_32(const T* __restrict__ A, const T* __restrict__ B, floa
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int wm = wave / WARP_N, wn = wave % WARP_N;
+  if (wm * WM >= m_limit) return;  // T.gemm(valid_m=), as gemm_ss
   floatx16* acc = reinterpret_cast<floatx16*>(C);
 #pragma unroll
   for (int kk = 0; kk < KSTEPS; ++kk) {

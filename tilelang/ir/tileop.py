@@ -107,6 +107,7 @@ class GemmOp(TileOp):
         self.a_fmt = self.b_fmt = None  # MX element formats ("e4m3", "e5m2", "e2m1")
         self.mfma_shape = None  # "16x16" / "32x32" (T.gemm(mfma_shape=...))
         self.E = None  # 2:4 sparse metadata of A (T.gemm_sp): A is then the compressed [M, K/2] tile
+        self.valid_m = None  # T.gemm(valid_m=): block-uniform count of rows that need results
 
     @property
     def is_mx(self) -> bool:

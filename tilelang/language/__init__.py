@@ -29,7 +29,7 @@ from .tileops import (copy, gather_rows, c2d_im2col, gemm, gemm_v1, gemm_v2, gem
                       atomic_addx4, atomic_load, atomic_store, reshape, view)
 from .math import *  # noqa: F401,F403
 from .math import (max, min, abs, round, pow)  # noqa: A004,F401
-from .builtin import (sync_threads, sync_warp, sync_global, sync_grid, fence_proxy_async, memory_fence,
+from .builtin import (sync_threads, sync_warp, sync_global, sync_grid, fence_proxy_async, memory_fence, set_priority,
                       get_lane_idx, get_warp_idx, get_warp_idx_sync, get_warp_group_idx, shfl_xor, shfl_down, shfl_up,
                       shfl_sync, ballot, clock, call_extern, call_intrin, evaluate, loop_break, device_assert, print,
                       use_swizzle, annotate_layout, annotate_safe_value, annotate_l2_hit_ratio, annotate_padding, attr,

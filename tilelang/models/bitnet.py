@@ -12,7 +12,8 @@ MI355X execution (``tilelang.ops.bitnet``):
 * every BitLinear input is produced by an RMSNorm, so norm + int8 quantisation are ONE kernel
   (``rms_norm_quant``) that writes the int8 row and its scale;
 * q|k|v and gate|up are each one fused int8 x int2 GEMM on ``v_mfma_i32_16x16x64_i8`` (weights
-  2 bits each in HBM, per-column weight scales in the dequantising epilogue);
+  2 bits each in HBM, per-column weight scales in the dequantising epilogue); decode-sized inputs
+  (<= 8 rows) take the weight-streaming GEMV kernel instead (no matrix cores, K padded to 256);
 * attention uses PyTorch SDPA (the BitNet-specific work is the ternary projections; the flash
   kernels live in examples/flash_attention).
 
@@ -63,23 +64,31 @@ class BitLinearGroup(nn.Module):
         self.weights = nn.ParameterList(
             [nn.Parameter(torch.randn(n, in_features, dtype=dtype) * in_features**-0.5) for n in self.splits])
         self.packed: Optional[torch.Tensor] = None
+        self.packed_dec: Optional[torch.Tensor] = None
         self.col_scale: Optional[torch.Tensor] = None
 
     @torch.no_grad()
     def freeze(self):
-        """Ternarise + pack the weights (per projection scale, expanded per output column)."""
+        """Ternarise + pack the weights (per projection scale, expanded per output column).  Two
+        packings: exact K for the prefill MFMA GEMM, K padded to 256 codes (padding = code 1 =
+        weight 0) for the decode GEMV."""
         packs, scales = [], []
         for w in self.weights:
             p, s = K.weight_quant_ternary(w)
             packs.append(p)
             scales.append(s.expand(w.shape[0]))
         self.packed = torch.cat(packs, 0).contiguous()
+        kp = -(-self.packed.shape[1] // 64) * 64
+        self.packed_dec = torch.nn.functional.pad(self.packed, (0, kp - self.packed.shape[1]),
+                                                  value=0b01010101).contiguous()
         self.col_scale = torch.cat(scales).float().contiguous()
 
     def forward(self, xq, sx, dtype):
         if self.packed is None or self.packed.device != xq.device:
             self.freeze()
-        y = K.int2_gemm(xq, self.packed, sx, self.col_scale, out_dtype=dtype, zero=1)
+        rows = xq.numel() // xq.shape[-1]
+        wq = self.packed_dec if rows <= 8 else self.packed
+        y = K.int2_gemm(xq, wq, sx, self.col_scale, out_dtype=dtype, zero=1)
         return torch.split(y, self.splits, -1) if len(self.splits) > 1 else y
 
 

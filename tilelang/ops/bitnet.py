@@ -83,40 +83,77 @@ def int2_gemm_kernel(M, N, K, zero=1, out_dtype="int32", target="hip", tiles=Non
 
 
 @functools.lru_cache(maxsize=None)
-def rms_norm_quant_kernel(M, N, dtype, eps, target="hip"):
-    """kernel(X [M,N], W [N]) -> (Xq int8 [M,N], s [M] fp32 = 127 / absmax(rmsnorm(x) * w))."""
-    blk_m = 4 if N <= 8192 else 1
-    threads = 256
+def int2_gemv_kernel(M, N, K, Kp, zero=1, out_dtype="float16", target="hip", block_N=16, num_stages=3):
+    """Decode-sized (M <= 8) int8 x int2 product without matrix cores: the packed weight rows
+    ([N, Kp/4] bytes, Kp = K rounded up to 256 codes, padding codes = ``zero``) stream through a
+    3-deep LDS-DMA ring, 64 bytes (256 codes) of each of ``block_N`` rows per step (16 B per lane,
+    one wave per workgroup, N / block_N workgroups), the activation rows sit in LDS for the
+    whole kernel, and every lane decodes its 64 codes with shifts and masks into int32 MACs.
+    kernel(xq [M, K] int8, wq [N, Kp/4] uint8, s_x [M], s_w [N]) -> C [M, N] (dequantised)."""
+    assert Kp % 256 == 0 and Kp >= K
+    KB = 64  # bytes per row per step
+
+    @T.prim_func
+    def main(A: T.Tensor((M, K), "int8"), B: T.Tensor((N, Kp // 4), "uint8"), sx: T.Tensor((M, ), "float32"),
+             sw: T.Tensor((N, ), "float32"), C: T.Tensor((M, N), out_dtype)):
+        with T.Kernel(T.ceildiv(N, block_N), threads=64) as bx:
+            x_s = T.alloc_shared((M, Kp), "int8")
+            b_s = T.alloc_shared((block_N, KB), "uint8")
+            b = T.alloc_fragment((block_N, KB), "uint8")
+            acc = T.alloc_fragment((M, block_N, KB), "int32")
+            row = T.alloc_fragment((M, block_N), "int32")
+            for m, k in T.Parallel(M, Kp):
+                x_s[m, k] = T.if_then_else(k < K, A[m, T.min(k, K - 1)], T.Cast("int8", 0))
+            T.clear(acc)
+            for ko in T.Pipelined(Kp // 256, num_stages=num_stages):
+                T.copy(B[bx * block_N, ko * KB], b_s)
+                T.copy(b_s, b)
+                for m, n, j in T.Parallel(M, block_N, KB):
+                    w = T.Cast("int32", b[n, j])
+                    base = ko * 256 + 4 * j
+                    acc[m, n, j] += ((w & 3) - zero) * T.Cast("int32", x_s[m, base]) + \
+                        (((w >> 2) & 3) - zero) * T.Cast("int32", x_s[m, base + 1]) + \
+                        (((w >> 4) & 3) - zero) * T.Cast("int32", x_s[m, base + 2]) + \
+                        (((w >> 6) & 3) - zero) * T.Cast("int32", x_s[m, base + 3])
+            T.reduce_sum(acc, row, dim=2)
+            for m, n in T.Parallel(M, block_N):
+                if bx * block_N + n < N:
+                    C[m, bx * block_N + n] = T.Cast(out_dtype, T.Cast("float32", row[m, n]) /
+                                                    (sx[m] * sw[bx * block_N + n]))
+
+    return tilelang.compile(main, out_idx=[-1], target=target)
+
+
+@functools.lru_cache(maxsize=None)
+def rms_norm_quant_kernel(M, N, dtype, eps, target="hip", threads=128):
+    """kernel(X [M,N], W [N]) -> (Xq int8 [M,N], s [M] fp32 = 127 / absmax(rmsnorm(x) * w)).
+    One row per workgroup, the row in registers padded to a multiple of 4 * threads (any N: the
+    BitNet-3B widths 3200 / 8640 are not powers of two), masked loads and stores."""
+    Np = -(-N // (4 * threads)) * (4 * threads)
 
     @T.prim_func
     def main(X: T.Tensor((M, N), dtype), Wt: T.Tensor((N, ), dtype), Q: T.Tensor((M, N), "int8"),
              S: T.Tensor((M, ), "float32")):
-        with T.Kernel(T.ceildiv(M, blk_m), threads=threads) as bx:
-            x = T.alloc_fragment((blk_m, N), "float32")
-            sq = T.alloc_fragment((blk_m, N), "float32")
-            ss = T.alloc_fragment((blk_m, ), "float32")
-            mx = T.alloc_fragment((blk_m, ), "float32")
-            q = T.alloc_fragment((blk_m, N), "int8")
-            T.copy(X[bx * blk_m, 0], x)
-            for i, j in T.Parallel(blk_m, N):
-                sq[i, j] = x[i, j] * x[i, j]
-            T.reduce_sum(sq, ss, dim=1)
-            for i in T.Parallel(blk_m):
-                ss[i] = T.rsqrt(ss[i] / N + eps)
-            for i, j in T.Parallel(blk_m, N):
-                # the model rounds the normalised activations to its dtype before quantising
-                x[i, j] = T.Cast("float32", T.Cast(dtype, T.Cast("float32", T.Cast(dtype, x[i, j] * ss[i])) *
-                                                   T.Cast("float32", Wt[j])))
-                sq[i, j] = T.abs(x[i, j])
-            T.reduce_max(sq, mx, dim=1)
-            for i in T.Parallel(blk_m):
-                mx[i] = 127.0 / T.max(mx[i], 1e-5)
-            for i, j in T.Parallel(blk_m, N):
-                q[i, j] = T.Cast("int8", T.max(T.min(T.nearbyint(x[i, j] * mx[i]), 127.0), -128.0))
-            T.copy(q, Q[bx * blk_m, 0])
-            for i in T.Parallel(blk_m):
-                if bx * blk_m + i < M:
-                    S[bx * blk_m + i] = mx[i]
+        with T.Kernel(M, threads=threads) as bx:
+            x = T.alloc_fragment((Np, ), "float32")
+            sq = T.alloc_fragment((Np, ), "float32")
+            ss = T.alloc_fragment((1, ), "float32")
+            mx = T.alloc_fragment((1, ), "float32")
+            for j in T.Parallel(Np):
+                x[j] = T.if_then_else(j < N, T.Cast("float32", X[bx, T.min(j, N - 1)]), 0.0)
+                sq[j] = x[j] * x[j]
+            T.reduce_sum(sq, ss, dim=0)
+            for j in T.Parallel(Np):
+                # the model rounds the normalised activations to its dtype before the weight multiply
+                x[j] = T.Cast("float32", T.Cast(dtype, T.Cast("float32", T.Cast(dtype, x[j] * T.rsqrt(
+                    ss[0] / N + eps))) * T.Cast("float32", Wt[T.min(j, N - 1)])))
+                sq[j] = T.if_then_else(j < N, T.abs(x[j]), 0.0)
+            T.reduce_max(sq, mx, dim=0)
+            for j in T.Parallel(Np):
+                if j < N:
+                    Q[bx, j] = T.Cast("int8", T.max(T.min(T.nearbyint(x[j] * (127.0 / T.max(mx[0], 1e-5))), 127.0),
+                                                    -128.0))
+            S[bx] = 127.0 / T.max(mx[0], 1e-5)
 
     return tilelang.compile(main, out_idx=[-2, -1], target=target)
 
@@ -142,8 +179,13 @@ def int2_gemm(xq: torch.Tensor, wq: torch.Tensor, s_x: torch.Tensor = None, s_w:
     N = wq.shape[0]
     if s_x is None:
         return int2_gemm_kernel(M, N, K, zero, "int32", _target(x2))(x2, wq).reshape(*shp[:-1], N)
-    k = int2_gemm_kernel(M, N, K, zero, _TDT[out_dtype], _target(x2))
     sw = s_w.reshape(-1).float().expand(N).contiguous()
+    Kp = wq.shape[1] * 4
+    if M <= 8 and Kp % 256 == 0:  # decode: weight streaming GEMV (packed K may be padded)
+        k = int2_gemv_kernel(M, N, K, Kp, zero, _TDT[out_dtype], _target(x2))
+    else:
+        assert Kp == K, "padded packed weights need the GEMV path (M <= 8)"
+        k = int2_gemm_kernel(M, N, K, zero, _TDT[out_dtype], _target(x2))
     return k(x2, wq, s_x.reshape(-1).float().contiguous(), sw).reshape(*shp[:-1], N)
 
 

@@ -100,7 +100,8 @@ def max_padded_rows(n_assign: int, E: int, block_M: int) -> int:
 def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: str, stable: bool = False,
                  threads: int = 1024):
     """Dispatch plan of ``n`` assignments (``expert_ids[n]``; assignment ``j`` reads source row
-    ``j // div``): ``dest[j]`` (its padded row), ``row_src[max_rows]``, ``tile_expert``, ``counts[E]``.
+    ``j // div``): ``dest[j]`` (its padded row), ``row_src[max_rows]``, ``tile_expert``, ``counts[E]``,
+    ``tile_rows`` (valid rows of every row tile: they are a prefix of the tile).
 
     One workgroup.  ``stable=False``: rows of one expert are placed in LDS-atomic order (each
     row's result is independent of its position, so the layer output does not depend on it).
@@ -115,7 +116,7 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
     @T.prim_func
     def moe_align(expert_ids: T.Tensor((n,), "int32"), dest: T.Tensor((n,), "int32"),
              row_src: T.Tensor((max_rows,), "int32"), tile_expert: T.Tensor((n_tiles,), "int32"),
-             counts: T.Tensor((E,), "int32")):
+             counts: T.Tensor((E,), "int32"), tile_rows: T.Tensor((n_tiles,), "int32")):
         # written with T.Parallel (one iteration per thread on the GPU, a serial loop on the
         # CPU target), never with raw thread ids, so the same program runs on both
         with T.Kernel(1, threads=threads):
@@ -153,11 +154,15 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                 counts[e] = cnt[e]
             for tt in T.Parallel(n_tiles):
                 te = T.alloc_var("int32")
+                tr = T.alloc_var("int32")
                 te = -1
+                tr = 0
                 for e in T.serial(E):
                     if tt * block_M >= start[e] and tt * block_M < start[e] + cnt[e]:
                         te = e
+                        tr = T.min(start[e] + cnt[e] - tt * block_M, block_M)
                 tile_expert[tt] = te
+                tile_rows[tt] = tr
             if stable:
                 for t in T.Parallel(threads):
                     for e in T.serial(E):
@@ -181,7 +186,8 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
 def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target: str, block_M: int = 128,
                        block_N: int = 128, block_K: int = 64, num_stages: int = 2, threads: int = 256,
                        reduce_mesh: Optional[str] = None, mesh_shape: Optional[Tuple[int, int]] = None,
-                       n_src: Optional[int] = None, swiglu: bool = False, persistent_blocks: int = 256):
+                       n_src: Optional[int] = None, swiglu: bool = False, persistent_blocks: int = 256,
+                       skip_padding: bool = True):
     """``C[r, :] = A[src(r), :] @ W[tile_expert[r // block_M]].T`` for every non-empty row tile.
 
     ``n_src`` given: A is the ``[n_src, K]`` source-row matrix and row ``r`` of the padded row
@@ -192,7 +198,9 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
     ``swiglu``: W's rows are interleaved in groups of 4 (gate 2p, gate 2p+1, up 2p, up 2p+1, see
     ``swiglu_interleave``) and the epilogue writes ``C[r, p] = silu(gate) * up`` ([max_rows, N/2]):
     the 4 columns of such a group sit in the registers of ONE lane (MFMA C layout), so the
-    activation needs no data movement and no separate kernel."""
+    activation needs no data movement and no separate kernel.
+    ``skip_padding``: waves whose rows of a row tile are all padding skip their MFMAs
+    (``T.gemm(valid_m=tile_rows[tile])``) — an expert's last tile is usually mostly padding."""
     n_tiles = max_rows // block_M
     n_by = (N + block_N - 1) // block_N
     n_work = n_tiles * n_by
@@ -207,7 +215,7 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
         @T.prim_func
         def moe_expert_gemm(A: T.Tensor((a_rows, K), dtype), W: T.Tensor((E, N, K), dtype),
                             tile_expert: T.Tensor((n_tiles,), "int32"), row_src: T.Tensor((max_rows,), "int32"),
-                            C: T.Tensor((max_rows, n_out), dtype)):
+                            tile_rows: T.Tensor((n_tiles,), "int32"), C: T.Tensor((max_rows, n_out), dtype)):
             with T.Kernel(n_tiles, T.ceildiv(N, block_N), threads=threads) as (bx, by):
                 A_s = T.alloc_shared((block_M, block_K), dtype)
                 W_s = T.alloc_shared((block_N, block_K), dtype)
@@ -222,7 +230,8 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
                         else:
                             T.copy(A[bx * block_M, k * block_K], A_s)
                         T.copy(W[e, by * block_N, k * block_K], W_s)
-                        T.gemm(A_s, W_s, C_l, transpose_B=True)
+                        # an expert's last row tile is partly padding: its empty waves skip the MFMAs
+                        T.gemm(A_s, W_s, C_l, transpose_B=True, valid_m=tile_rows[bx] if skip_padding else None)
                     if swiglu:
                         for i, j in T.Parallel(block_M, block_N):
                             if j % 4 < 2:
@@ -237,7 +246,7 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
     @T.prim_func
     def moe_expert_gemm_tp(A: T.Tensor((a_rows, K), dtype), W: T.Tensor((E, N, K), dtype),
                            tile_expert: T.Tensor((n_tiles,), "int32"), row_src: T.Tensor((max_rows,), "int32"),
-                           C: T.Tensor((max_rows, n_out), dtype)):
+                           tile_rows: T.Tensor((n_tiles,), "int32"), C: T.Tensor((max_rows, n_out), dtype)):
         # persistent grid: the cross-GPU all-reduce needs every block of every rank resident at
         # once (tl_runtime refuses larger grids), and the mesh workspace scales with the grid
         with T.Kernel(n_prog, threads=threads) as pid:
@@ -262,7 +271,7 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
                             else:
                                 T.copy(A[bx * block_M, k * block_K], A_s)
                             T.copy(W[e, by * block_N, k * block_K], W_s)
-                            T.gemm(A_s, W_s, C_l, transpose_B=True)
+                            T.gemm(A_s, W_s, C_l, transpose_B=True, valid_m=tile_rows[bx] if skip_padding else None)
                         T.comm.all_reduce_tile(C_l, C_r, "sum", reduce_mesh)
                         T.copy(C_r, C[bx * block_M, by * block_N])
 
@@ -338,7 +347,7 @@ def route(x: torch.Tensor, gate_w: torch.Tensor, topk: int):
 
 def dispatch_plan(expert_ids: torch.Tensor, E: int, block_M: int, max_rows: int, div: int = 1,
                   stable: bool = False):
-    """Device-side padded placement: ``(dest[n], row_src[max_rows], tile_expert, counts[E])``."""
+    """Device-side padded placement: ``(dest[n], row_src[max_rows], tile_expert, counts[E], tile_rows)``."""
     dev = expert_ids.device
     n = expert_ids.numel()
     ids = expert_ids.reshape(-1).to(torch.int32).contiguous()
@@ -346,13 +355,14 @@ def dispatch_plan(expert_ids: torch.Tensor, E: int, block_M: int, max_rows: int,
     row_src = torch.empty(max_rows, dtype=torch.int32, device=dev)
     te = torch.empty(max_rows // block_M, dtype=torch.int32, device=dev)
     counts = torch.empty(E, dtype=torch.int32, device=dev)
-    align_kernel(n, E, block_M, max_rows, div, _target(dev), stable)(ids, dest, row_src, te, counts)
-    return dest, row_src, te, counts
+    tile_rows = torch.empty(max_rows // block_M, dtype=torch.int32, device=dev)
+    align_kernel(n, E, block_M, max_rows, div, _target(dev), stable)(ids, dest, row_src, te, counts, tile_rows)
+    return dest, row_src, te, counts, tile_rows
 
 
 def pack_by_expert(expert_ids: torch.Tensor, E: int, block_M: int, max_rows: int):
     """``(dest[n], tile_expert[max_rows // block_M], counts[E])`` (see ``dispatch_plan``)."""
-    dest, _, te, counts = dispatch_plan(expert_ids, E, block_M, max_rows, stable=True)
+    dest, _, te, counts, _ = dispatch_plan(expert_ids, E, block_M, max_rows, stable=True)
     return dest.long(), te, counts.long()
 
 
@@ -373,21 +383,21 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
     n_src = _bucket(src_rows.shape[0])
     if src_rows.shape[0] != n_src:
         src_rows = torch.cat([src_rows, src_rows.new_zeros(n_src - src_rows.shape[0], src_rows.shape[1])])
-    dest, row_src, te, _ = dispatch_plan(expert_ids, E, block_M, max_rows, div, stable=reduce_mesh is not None)
+    dest, row_src, te, _, trows = dispatch_plan(expert_ids, E, block_M, max_rows, div, stable=reduce_mesh is not None)
     act = torch.empty(max_rows, F, dtype=src_rows.dtype, device=dev)
     if w1_interleaved:
         # gate/up rows interleaved: the activation is the first GEMM's epilogue
         k1 = expert_gemm_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, swiglu=True, **cfg)
-        k1(src_rows.contiguous(), w1, te, row_src, act)
+        k1(src_rows.contiguous(), w1, te, row_src, trows, act)
     else:
         k1 = expert_gemm_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, **cfg)
         h = torch.empty(max_rows, F2, dtype=src_rows.dtype, device=dev)
-        k1(src_rows.contiguous(), w1, te, row_src, h)
+        k1(src_rows.contiguous(), w1, te, row_src, trows, h)
         silu_mul_kernel(max_rows, F, tgt, target)(h, act)
     k2 = expert_gemm_kernel(max_rows, F, H, E, tgt, target, block_M, reduce_mesh=reduce_mesh,
                             mesh_shape=_mesh_shape() if reduce_mesh else None, **cfg)
     y = torch.empty(max_rows, H, dtype=src_rows.dtype, device=dev)
-    k2(act, w2, te, row_src, y)
+    k2(act, w2, te, row_src, trows, y)
     return y, dest
 
 

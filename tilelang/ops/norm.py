@@ -10,7 +10,32 @@ import tilelang.language as T
 
 
 @functools.lru_cache(maxsize=None)
+def _rms_kernel_padded(M, N, dtype, eps, target, threads=128):
+    """Widths that do not tile over the block (e.g. 3200): one row per workgroup, the row padded
+    to a multiple of 4 * threads in registers, masked loads and stores."""
+    Np = -(-N // (4 * threads)) * (4 * threads)
+
+    @T.prim_func
+    def main(X: T.Tensor((M, N), dtype), Wt: T.Tensor((N, ), dtype), Y: T.Tensor((M, N), dtype)):
+        with T.Kernel(M, threads=threads) as bx:
+            x = T.alloc_fragment((Np, ), "float32")
+            sq = T.alloc_fragment((Np, ), "float32")
+            ss = T.alloc_fragment((1, ), "float32")
+            for j in T.Parallel(Np):
+                x[j] = T.if_then_else(j < N, T.Cast("float32", X[bx, T.min(j, N - 1)]), 0.0)
+                sq[j] = x[j] * x[j]
+            T.reduce_sum(sq, ss, dim=0)
+            for j in T.Parallel(Np):
+                if j < N:
+                    Y[bx, j] = T.Cast(dtype, x[j] * T.rsqrt(ss[0] / N + eps) * T.Cast("float32", Wt[j]))
+
+    return tilelang.compile(main, out_idx=[-1], target=target)
+
+
+@functools.lru_cache(maxsize=None)
 def _rms_kernel(M, N, dtype, eps, target):
+    if N % 1024:
+        return _rms_kernel_padded(M, N, dtype, eps, target)
     blk_m = 4 if N <= 8192 else 1
     threads = 256
 

@@ -119,6 +119,7 @@ class _KSplit(Mutator):
                           g.C, g.trans_A, g.trans_B, g.policy, g.clear_accum if i == 0 else False, g.k_pack,
                           g.wg_wait)
             gi.mfma_shape = g.mfma_shape
+            gi.valid_m = getattr(g, "valid_m", None)
             gi.khalf = i
             new.append(S.TileOpStmt(gi))
         for buf in (A, B):

@@ -1008,9 +1008,13 @@ class TileOpLowerer(Mutator):
                 plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_A), _b(op.trans_B),
                 A.static_shape()[-1], B.static_shape()[-1]]))
             return S.SeqStmt(out)
+        vm = [self.expr(op.valid_m)] if getattr(op, "valid_m", None) is not None else []
+        if vm and (plan.get("int8") or plan.get("f32") or A.dtype.bits == 8 or A.scope != "shared"):
+            raise LoweringError("T.gemm(valid_m=) is supported for f16/bf16 GEMMs with both operands in shared "
+                                "memory")
         if plan.get("mfma") == (32, 32, 16):
             pa = self._operand_ptr(op.A)
-            out.append(L.CallStmt("tl::gemm_ss_32", [pa, pb, L.BufferPtr(cl, 0)], [
+            out.append(L.CallStmt("tl::gemm_ss_32", [pa, pb, L.BufferPtr(cl, 0)] + vm, [
                 ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_A),
                 _b(op.trans_B), A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
                 B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u"]))
@@ -1029,7 +1033,7 @@ class TileOpLowerer(Mutator):
             pa = self._operand_ptr(op.A)
             a_cols = A.static_shape()[-1]
             swz_a = gemm_lower.encode_swizzle(A.layout)
-            out.append(L.CallStmt("tl::gemm_ss", [pa, pb, L.BufferPtr(cl, 0)], [
+            out.append(L.CallStmt("tl::gemm_ss", [pa, pb, L.BufferPtr(cl, 0)] + vm, [
                 ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_A),
                 _b(op.trans_B), a_cols, f"{swz_a}u", b_cols, f"{swz_b}u"
             ]))
@@ -1192,28 +1196,16 @@ class TileOpLowerer(Mutator):
 
     def _reduce_groups(self, S_lay: Fragment, D_lay: Fragment, dim: int, squeeze_dim: bool):
         """src register -> dst register grouping, or None when some thread does not own the
-        destination of an element it holds (the layouts are not reduce-compatible)."""
+        destination of an element it holds (the layouts are not reduce-compatible).  The proof
+        runs over every thread of the block in the native core (csrc/core/fragment.cc
+        ``reduce_owners``)."""
+        from .._native import core
+        own = core().reduce_owners(S_lay.native, D_lay.native, dim, bool(squeeze_dim), self.ctx.T)
+        if len(own) == 0:
+            return None
         groups: Dict[int, List[int]] = {}
-        dmaps = {}
-        for r in range(S_lay.local_size):
-            owners = set()
-            for t in _sample_threads(self.ctx.T):
-                idx = S_lay.inverse(t, r)
-                didx = list(idx)
-                if squeeze_dim:
-                    didx[dim] = 0
-                else:
-                    didx.pop(dim)
-                m = dmaps.get(t)
-                if m is None:
-                    m = dmaps[t] = D_lay.thread_local_map(t)
-                li = m.get(tuple(didx))
-                if li is None:
-                    return None
-                owners.add(li)
-            if len(owners) != 1:
-                return None
-            groups.setdefault(owners.pop(), []).append(r)
+        for r, li in enumerate(own):
+            groups.setdefault(li, []).append(r)
         return groups
 
     def lower_reduce_simt(self, op: O.ReduceOp):

@@ -25,7 +25,8 @@ class Mutator:
     def tileop(self, op):
         import copy
         op = copy.copy(op)
-        for name in ("src", "dst", "A", "B", "C", "buf", "send", "recv", "tmp", "img", "col", "scale_A", "scale_B", "E"):
+        for name in ("src", "dst", "A", "B", "C", "buf", "send", "recv", "tmp", "img", "col", "scale_A", "scale_B", "E",
+                     "valid_m"):
             v = getattr(op, name, None)
             if isinstance(v, BufferRegion):
                 setattr(op, name, self.region(v))
