@@ -184,9 +184,10 @@ def main(lens=(1000, 3000, 2500, 4096), HQ=64, H=4, D=128, S=16, block_size=64):
     print("All checks pass.")
     from tilelang.profiler import do_bench
     lat = do_bench(lambda: kern(q, k, v, o, idx, cnt, off, ti))
-    flops = 4.0 * HQ * D * float(cnt.float().sum()) * block_size / H * H
+    # every selected (token, kv head, block) is G = HQ/H query rows x block_size keys x D, QK^T + PV
+    flops = 4.0 * (HQ // H) * D * block_size * float(cnt.float().sum())
     print(f"NSA varlen fwd C{C} HQ{HQ} H{H} D{D} S{S}x{block_size}: {lat:.3f} ms, {flops / lat * 1e-9:.1f} TFLOPS "
-          f"(selected blocks, upper bound)")
+          f"(selected blocks incl. their masked tails)")
 
 
 if __name__ == "__main__":
