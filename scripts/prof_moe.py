@@ -49,6 +49,16 @@ if "--skip-ab" in sys.argv:  # T.gemm(valid_m=) on the padded tail tiles vs full
     g, w1, w2 = (t.to("cuda") for t in init_moe_weights(layer.cfg))
     ref = moe_reference(x, g, w1, w2, layer.cfg.topk)
     print("max abs err", (out - ref).abs().max().item(), "ref max", ref.abs().max().item(), flush=True)
+if "--sk-ab" in sys.argv:  # stream-K hybrid expert GEMMs vs the plain tile grid
+    base = dict(layer.cfg.gemm_cfg or {})
+    for sk in (False, True, False, True):
+        layer.cfg.gemm_cfg = dict(base, stream_k=sk)
+        run(layer, x, f"stream_k={sk}")
+    layer.cfg.gemm_cfg = base
+    out = layer(x).float()
+    g, w1, w2 = (t.to("cuda") for t in init_moe_weights(layer.cfg))
+    ref = moe_reference(x, g, w1, w2, layer.cfg.topk)
+    print("max abs err", (out - ref).abs().max().item(), "ref max", ref.abs().max().item(), flush=True)
 if "--sweep" in sys.argv:
     for bm in (128, 256):
         for cfg in (dict(block_N=128, block_K=64, num_stages=2, threads=256),

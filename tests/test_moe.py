@@ -3,7 +3,7 @@
 import pytest
 import torch
 
-from tilelang.models.moe import MoEConfig, MoELayer, init_moe_weights, moe_reference
+from tilelang.models.moe import MoEConfig, MoELayer, init_moe_weights, moe_reference, routing_equivalent
 from tilelang.ops.moe import pack_by_expert, max_padded_rows
 from tilelang.parallel import VirtualMesh
 
@@ -85,7 +85,11 @@ def test_moe_layer_gpu():
     layer = MoELayer(cfg, "local", device="cuda")
     out = layer(x).float()
     g, w1, w2 = (t.to("cuda") for t in init_moe_weights(cfg))
-    ref = moe_reference(x, g, w1, w2, cfg.topk)
+    from tilelang.ops import moe as K
+    from tilelang.models.moe import routing_equivalent
+    ids, w = K.route(x, g, cfg.topk)  # fused MFMA router + top-k
+    assert routing_equivalent(x, g, cfg.topk, ids, w)
+    ref = moe_reference(x, g, w1, w2, cfg.topk, routing=(ids, w))
     torch.testing.assert_close(out, ref, rtol=3e-2, atol=3e-2 * ref.abs().max().item())
 
 
@@ -103,3 +107,47 @@ def test_tp_expert_gemm_workspace_and_grid():
     one_shot_per_tile = tiles * 8 * bm * bn * 4
     assert meta["nblocks"] == 256 and meta["slot_bytes"] == bm * bn * 4 // 8
     assert meta["ws_bytes"] * 10 <= one_shot_per_tile, (meta, one_shot_per_tile)
+
+
+@pytest.mark.parametrize("n_cu", [3, 5, 8])
+def test_moe_tail_balanced_cpu(n_cu):
+    """Tail-balanced expert GEMMs: whole leading units, the trailing partial round as narrow tiles
+    (n_cu chosen so the tail has 1-2 rounds of narrow tiles, or is empty)."""
+    cfg = MoEConfig(hidden=64, ffn=64, n_experts=4, topk=2, dtype=torch.float32, block_M=16,
+                    gemm_cfg=dict(block_N=64, block_K=32, num_stages=2, threads=128, stream_k=True, n_cu=n_cu,
+                                  tail_split=2))
+    layer = MoELayer(cfg, "local", device="cpu")
+    x = torch.randn(50, 64)
+    out = layer(x).float()
+    g, w1, w2 = init_moe_weights(cfg)
+    ref = moe_reference(x, g, w1, w2, cfg.topk)
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_moe_tail_balanced_gpu():
+    """The bench's MoE layer shape with the tail-balanced grid on vs off."""
+    cfg = MoEConfig(hidden=1024, ffn=512, n_experts=8, topk=2, dtype=torch.bfloat16, block_M=256,
+                    gemm_cfg=dict(block_N=256, block_K=64, num_stages=2, threads=512))
+    torch.manual_seed(0)
+    x = torch.randn(2048, cfg.hidden, device="cuda").to(cfg.dtype)
+    layer = MoELayer(cfg, "local", device="cuda")
+    g, w1, w2 = (t.to("cuda") for t in init_moe_weights(cfg))
+    from tilelang.ops import moe as K
+    ref = moe_reference(x, g, w1, w2, cfg.topk, routing=K.route(x, g, cfg.topk))
+    for sk in (True, False):
+        layer.cfg.gemm_cfg = dict(block_N=256, block_K=64, num_stages=2, threads=512, stream_k=sk)
+        out = layer(x).float()
+        torch.testing.assert_close(out, ref, rtol=3e-2, atol=3e-2 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_fused_router_cpu(dt):
+    """MFMA router GEMM + top-k in one kernel (16-bit activations): a valid top-k of the
+    reference probabilities (exact 16-bit logit ties may break the other way)."""
+    from tilelang.ops import moe as K
+    torch.manual_seed(0)
+    x = torch.randn(100, 512).to(dt)
+    g = (torch.randn(8, 512) * 0.05).to(dt)
+    ids, w = K.route(x, g, 2)
+    assert routing_equivalent(x, g, 2, ids, w)

@@ -51,9 +51,11 @@ def route(x: torch.Tensor, gate_w: torch.Tensor, topk: int):
     return ids, w
 
 
-def moe_reference(x, gate_w, w1, w2, topk):
-    """fp32 PyTorch definition (w1: [E, 2F, H] = [gate | up], w2: [E, H, F])."""
-    ids, wts = route(x, gate_w, topk)
+def moe_reference(x, gate_w, w1, w2, topk, routing=None):
+    """fp32 PyTorch definition (w1: [E, 2F, H] = [gate | up], w2: [E, H, F]).  ``routing``:
+    (ids, weights) to use instead of ``route`` -- a kernel's own choice between experts whose
+    16-bit logits tie exactly (see ``routing_equivalent``)."""
+    ids, wts = route(x, gate_w, topk) if routing is None else (routing[0].long(), routing[1].float())
     xf = x.float()
     out = torch.zeros_like(xf)
     F = w1.shape[1] // 2
@@ -65,6 +67,22 @@ def moe_reference(x, gate_w, w1, w2, topk):
         a = torch.nn.functional.silu(h[:, :F]) * h[:, F:]
         out.index_add_(0, tok, (a @ w2[e].float().t()) * wts[tok, slot, None])
     return out
+
+
+def routing_equivalent(x, gate_w, topk, ids, w, atol=1e-6) -> bool:
+    """True when (ids, w) is a valid top-k of ``route``'s probabilities: same weights, and every
+    expert that differs from the reference choice has exactly the probability of the expert it
+    replaces (an exact tie of the 16-bit logits, broken the other way)."""
+    rid, rw = route(x, gate_w, topk)
+    if not torch.allclose(w.float(), rw.float(), atol=atol, rtol=1e-5):
+        return False
+    probs = torch.softmax(torch.nn.functional.linear(x, gate_w).float(), -1)
+    diff = ids.long() != rid
+    if not diff.any():
+        return True
+    got = probs.gather(1, ids.long())
+    want = probs.gather(1, rid)
+    return bool(torch.allclose(got[diff], want[diff], atol=atol, rtol=1e-5))
 
 
 def init_moe_weights(cfg: MoEConfig, seed: int = 0):

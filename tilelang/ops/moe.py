@@ -90,6 +90,83 @@ def router_topk_kernel(n_tok: int, E: int, topk: int, target: str, threads: int 
     return tilelang.compile(moe_router_topk, out_idx=None, target=target)
 
 
+@functools.lru_cache(maxsize=None)
+def router_fused_kernel(n_tok: int, H: int, E: int, topk: int, dtype: str, target: str, block_T: int = 16,
+                        block_K: int = 256, num_stages: int = 3):
+    """Router in one kernel: logits = x Wg^T on the matrix cores (experts padded to the 16-wide MFMA
+    N dimension, padded rows of Wg are zero and masked), rounded to the activation dtype like a
+    library GEMM's output, then the top-k of each row and its renormalised softmax weights
+    (``router_topk_kernel``'s rule) from LDS.  Replaces vendor GEMM + fp32 cast + top-k kernel
+    (three launches, ~25 us at 2048 x 4096 x 8 on MI355X) with one pass over x.
+    kernel(x [n_tok, H], Wg [Ep, H] (Ep = E rounded up to 16), ids, w)."""
+    Ep = max(16, -(-E // 16) * 16)
+    assert H % block_K == 0
+
+    @T.prim_func
+    def moe_router_fused(X: T.Tensor((n_tok, H), dtype), Wg: T.Tensor((Ep, H), dtype),
+                         ids: T.Tensor((n_tok, topk), "int32"), w: T.Tensor((n_tok, topk), "float32")):
+        with T.Kernel(T.ceildiv(n_tok, block_T), threads=64) as bx:
+            X_s = T.alloc_shared((block_T, block_K), dtype)
+            W_s = T.alloc_shared((Ep, block_K), dtype)
+            L = T.alloc_fragment((block_T, Ep), "float32")
+            L_s = T.alloc_shared((block_T, Ep), "float32")
+            T.clear(L)
+            for k in T.Pipelined(H // block_K, num_stages=num_stages):
+                T.copy(X[bx * block_T, k * block_K], X_s)
+                T.copy(Wg[0, k * block_K], W_s)
+                T.gemm(X_s, W_s, L, transpose_B=True)
+            for i, e in T.Parallel(block_T, Ep):
+                L_s[i, e] = T.Cast("float32", T.Cast(dtype, L[i, e]))
+            for i in T.Parallel(64):
+                v = T.alloc_local((Ep,), "float32")
+                sel = T.alloc_local((topk,), "int32")
+                p = T.alloc_local((topk,), "float32")
+                best = T.alloc_var("float32")
+                bi = T.alloc_var("int32")
+                tot = T.alloc_var("float32")
+                if (i < block_T) & (bx * block_T + i < n_tok):
+                    for e in T.serial(E):
+                        v[e] = L_s[i, e]
+                    for kk in T.serial(topk):
+                        best = -T.infinity("float32")
+                        bi = 0
+                        for e in T.serial(E):
+                            if v[e] > best:
+                                best = v[e]
+                                bi = e
+                        sel[kk] = bi
+                        p[kk] = best
+                        v[bi] = -T.infinity("float32")
+                    tot = 0.0
+                    best = p[0]
+                    for kk in T.serial(topk):
+                        p[kk] = T.exp(p[kk] - best)
+                        tot = tot + p[kk]
+                    for kk in T.serial(topk):
+                        ids[bx * block_T + i, kk] = sel[kk]
+                        w[bx * block_T + i, kk] = p[kk] / tot
+
+    return tilelang.compile(moe_router_fused, out_idx=None, target=target)
+
+
+_GATE_PAD = {}
+
+
+def _padded_gate(gate_w: torch.Tensor) -> torch.Tensor:
+    """Wg padded with zero rows to a multiple of 16 experts (cached per weight tensor)."""
+    key = (gate_w.data_ptr(), tuple(gate_w.shape), gate_w.dtype, gate_w._version)
+    g = _GATE_PAD.get(key)
+    if g is None:
+        E, H = gate_w.shape
+        Ep = max(16, -(-E // 16) * 16)
+        g = torch.zeros(Ep, H, dtype=gate_w.dtype, device=gate_w.device)
+        g[:E] = gate_w
+        if len(_GATE_PAD) > 64:
+            _GATE_PAD.clear()
+        _GATE_PAD[key] = g
+    return g
+
+
 def max_padded_rows(n_assign: int, E: int, block_M: int) -> int:
     """Worst-case rows of the padded layout for ``n_assign`` (row, expert) pairs."""
     rows = n_assign + E * (block_M - 1)
@@ -278,6 +355,81 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
     return tilelang.compile(moe_expert_gemm_tp, out_idx=None, target=target)
 
 
+@functools.lru_cache(maxsize=None)
+def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target: str, block_M: int = 256,
+                          block_N: int = 256, block_K: int = 64, num_stages: int = 2, threads: int = 512,
+                          n_src: Optional[int] = None, swiglu: bool = False, n_cu: int = 256, tail_split: int = 4):
+    """Tail-balanced variant of ``expert_gemm_kernel`` (same arguments and output).
+
+    The (row tile x N tile) units are a data-dependent count U (the routing decides how many
+    row tiles are real), and a plain grid runs ceil(U / n_cu) rounds of whole tiles: U = 320 on
+    256 CUs -- the bench's 8-expert layer -- is two rounds for 1.25 rounds of work.  Here a
+    persistent grid of ``n_cu`` workgroups runs the floor(U / n_cu) * n_cu leading units as whole
+    ``block_M x block_N`` tiles, and the R = U mod n_cu trailing units as ``tail_split`` times
+    narrower ``block_M x block_N / tail_split`` tiles over the full K (R * tail_split workgroups:
+    one short round instead of a long one).  No K split, so no partial sums, workspace or second
+    kernel; the SwiGLU epilogue's 4-column groups stay inside a narrow tile.  Every workgroup
+    derives U and R from ``tile_expert`` (the real tiles are a prefix): nothing waits on the host."""
+    n_tiles = max_rows // block_M
+    n_by = (N + block_N - 1) // block_N
+    nk = (K + block_K - 1) // block_K
+    bn_t = block_N // tail_split
+    assert bn_t % 64 == 0 or bn_t == 32, "tail tiles must stay MFMA / SwiGLU-group aligned"
+    accum = "float32"
+    a_rows = n_src if n_src is not None else max_rows
+    n_out = N // 2 if swiglu else N
+
+    @T.macro
+    def tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, bx, e, col0, bn):
+        T.clear(C_l)
+        for k in T.Pipelined(nk, num_stages=num_stages):
+            if n_src is not None:
+                T.gather_rows(A[:, k * block_K:(k + 1) * block_K], row_src[bx * block_M:(bx + 1) * block_M], A_s,
+                              row_dim=0)
+            else:
+                T.copy(A[bx * block_M, k * block_K], A_s)
+            T.copy(W[e, col0, k * block_K], W_s)
+            T.gemm(A_s, W_s, C_l, transpose_B=True, valid_m=tile_rows[bx])
+        if swiglu:
+            for i, j in T.Parallel(block_M, bn):
+                if j % 4 < 2:
+                    C[bx * block_M + i, col0 // 2 + (j // 4) * 2 + j % 4] = T.Cast(
+                        dtype, C_l[i, j] / (1.0 + T.exp(-C_l[i, j])) * C_l[i, j + 2])
+        else:
+            T.copy(C_l, C[bx * block_M, col0])
+
+    @T.prim_func
+    def moe_expert_gemm_tb(A: T.Tensor((a_rows, K), dtype), W: T.Tensor((E, N, K), dtype),
+                           tile_expert: T.Tensor((n_tiles,), "int32"), row_src: T.Tensor((max_rows,), "int32"),
+                           tile_rows: T.Tensor((n_tiles,), "int32"), C: T.Tensor((max_rows, n_out), dtype)):
+        with T.Kernel(n_cu, threads=threads) as pid:
+            A_s = T.alloc_shared((block_M, block_K), dtype)
+            W_s = T.alloc_shared((block_N, block_K), dtype)
+            C_l = T.alloc_fragment((block_M, block_N), accum)
+            Wt_s = T.alloc_shared((bn_t, block_K), dtype)
+            Ct_l = T.alloc_fragment((block_M, bn_t), accum)
+            nt = T.alloc_var("int32")
+            nt = 0
+            for t in T.serial(n_tiles):
+                if tile_expert[t] >= 0:
+                    nt = t + 1
+            units = nt * n_by
+            full = units - units % n_cu
+            for it in T.serial(full // n_cu):  # whole tiles
+                u = pid + it * n_cu
+                tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, u // n_by, tile_expert[u // n_by],
+                     (u % n_by) * block_N, block_N)
+            for it in T.serial(T.ceildiv((units - full) * tail_split, n_cu)):  # narrow tail tiles
+                q = pid + it * n_cu
+                if q < (units - full) * tail_split:
+                    u = full + q // tail_split
+                    tile(A, W, row_src, tile_rows, C, A_s, Wt_s, Ct_l, u // n_by, tile_expert[u // n_by],
+                         (u % n_by) * block_N + (q % tail_split) * bn_t, bn_t)
+
+    return tilelang.compile(moe_expert_gemm_tb, out_idx=None, target=target,
+                            pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True} if swiglu else None)
+
+
 def swiglu_interleave(w1: torch.Tensor) -> torch.Tensor:
     """``[E, 2F, H]`` (gate rows then up rows) -> the row order of the fused SwiGLU GEMM:
     groups of 4 rows (gate 2p, gate 2p+1, up 2p, up 2p+1)."""
@@ -336,7 +488,17 @@ def combine_kernel(n_tok: int, H: int, topk: int, max_rows: int, dtype: str, tar
 
 
 def route(x: torch.Tensor, gate_w: torch.Tensor, topk: int):
-    """Router: logits (vendor GEMM, fp32 out) -> top-k ids [T, k] int32 + renormalised weights [T, k]."""
+    """Router -> top-k ids [T, k] int32 + renormalised weights [T, k].  16-bit activations with
+    H % 256 == 0 take the fused MFMA GEMM + top-k kernel; otherwise logits come from
+    ``torch.nn.functional.linear`` (fp32 routers, odd widths) and ``router_topk_kernel``."""
+    n_tok, H = x.shape
+    E = gate_w.shape[0]
+    if x.dtype in (torch.float16, torch.bfloat16) and H % 256 == 0 and gate_w.dtype == x.dtype and E <= 64:
+        ids = torch.empty(n_tok, topk, dtype=torch.int32, device=x.device)
+        w = torch.empty(n_tok, topk, dtype=torch.float32, device=x.device)
+        router_fused_kernel(n_tok, H, E, topk, _tdt(x.dtype), _target(x.device))(x.contiguous(), _padded_gate(gate_w),
+                                                                                  ids, w)
+        return ids, w
     logits = torch.nn.functional.linear(x, gate_w).float()
     n_tok, E = logits.shape
     ids = torch.empty(n_tok, topk, dtype=torch.int32, device=x.device)
@@ -385,6 +547,20 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
         src_rows = torch.cat([src_rows, src_rows.new_zeros(n_src - src_rows.shape[0], src_rows.shape[1])])
     dest, row_src, te, _, trows = dispatch_plan(expert_ids, E, block_M, max_rows, div, stable=reduce_mesh is not None)
     act = torch.empty(max_rows, F, dtype=src_rows.dtype, device=dev)
+    sk = cfg.pop("stream_k", None)
+    n_cu = cfg.pop("n_cu", 256)
+    if sk is None:
+        sk = target == "hip"
+    if sk and reduce_mesh is None and w1_interleaved:
+        # tail-balanced grid: whole tiles for the leading rounds, narrow tiles for the trailing partial round
+        skc = {k: v for k, v in cfg.items() if k in ("block_N", "block_K", "num_stages", "threads", "tail_split")}
+        k1 = expert_gemm_sk_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, swiglu=True, n_cu=n_cu,
+                                   **skc)
+        k1(src_rows.contiguous(), w1, te, row_src, trows, act)
+        k2 = expert_gemm_sk_kernel(max_rows, F, H, E, tgt, target, block_M, n_cu=n_cu, **skc)
+        y = torch.empty(max_rows, H, dtype=src_rows.dtype, device=dev)
+        k2(act, w2, te, row_src, trows, y)
+        return y, dest
     if w1_interleaved:
         # gate/up rows interleaved: the activation is the first GEMM's epilogue
         k1 = expert_gemm_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, swiglu=True, **cfg)

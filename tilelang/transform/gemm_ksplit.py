@@ -101,8 +101,11 @@ class _KSplit(Mutator):
         for buf, kd in ((A, ka), (B, kb)):
             shp = list(buf.static_shape())
             shp[kd] = half
-            h0 = Buffer(buf.name + "_k0", shp, buf.dtype, "shared")
-            h1 = Buffer(buf.name + "_k1", shp, buf.dtype, "shared")
+            if buf in self.new_allocs:  # a second phased loop over the same operand tile reuses its halves
+                h0, h1 = self.new_allocs[buf]
+            else:
+                h0 = Buffer(buf.name + "_k0", shp, buf.dtype, "shared")
+                h1 = Buffer(buf.name + "_k1", shp, buf.dtype, "shared")
             c0 = _split_copy(cps[buf], kd, half, h0, 0)
             c1 = _split_copy(cps[buf], kd, half, h1, 1)
             if c0 is None or c1 is None:
