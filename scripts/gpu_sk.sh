@@ -11,3 +11,6 @@ cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format cs
 cd $GRAFT_REPO_ROOT
 grep -v "PASSED\|^$\|amdgpu.ids" gpurun_out/sk.log | tail -30
 find gpurun_out/prof_sk -name "*kernel_stats.csv" | head -3
+cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_mhainf -o run -- python3 $GRAFT_REPO_ROOT/examples/flash_decoding/example_mha_inference.py >> $GRAFT_REPO_ROOT/gpurun_out/sk.log 2>&1 || { echo FAILED rocprof2; exit 1; }
+cd $GRAFT_REPO_ROOT
+find gpurun_out/prof_mhainf -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-150 | head -8
