@@ -184,6 +184,21 @@ def main(BATCH=1, H=32, Q_CTX=128, KV_CTX=8192, D_HEAD=128, causal=False, num_sp
           f"{flops / lat * 1e-9:.1f} TFLOPS")
 
 
+def sweep(BATCH=1, H=32, Q_CTX=128, KV_CTX=8192, D_HEAD=128):
+    import torch
+    from tilelang.profiler import do_bench
+    flops = 4.0 * BATCH * H * Q_CTX * KV_CTX * D_HEAD
+    q = torch.randn(BATCH, Q_CTX, H, D_HEAD, device="cuda", dtype=torch.float16)
+    k = torch.randn(BATCH, KV_CTX, H, D_HEAD, device="cuda", dtype=torch.float16)
+    v = torch.randn_like(k)
+    for bm, th, ns in ((128, 256, 8), (128, 256, 16), (64, 128, 8), (64, 128, 16), (128, 512, 8), (256, 512, 8)):
+        kern = flashattn(BATCH, H, Q_CTX, KV_CTX, D_HEAD, False, bm, 64, ns, th)
+        glse = torch.empty(BATCH, H, ns, Q_CTX, device="cuda")
+        part = torch.empty(BATCH, Q_CTX, H, ns, D_HEAD, device="cuda")
+        lat = do_bench(lambda: kern(q, k, v, glse, part))
+        print(f"block_M {bm} threads {th} split {ns}: {lat * 1e3:.1f} us, {flops / lat * 1e-9:.1f} TF", flush=True)
+
+
 if __name__ == "__main__":
     p = argparse.ArgumentParser()
     p.add_argument("--batch", type=int, default=1)
@@ -193,5 +208,9 @@ if __name__ == "__main__":
     p.add_argument("--dim", type=int, default=128)
     p.add_argument("--causal", action="store_true")
     p.add_argument("--num_split", type=int, default=8)
+    p.add_argument("--sweep", action="store_true")
     a = p.parse_args()
-    main(a.batch, a.heads, a.q_ctx, a.kv_ctx, a.dim, a.causal, a.num_split)
+    if a.sweep:
+        sweep(a.batch, a.heads, a.q_ctx, a.kv_ctx, a.dim)
+    else:
+        main(a.batch, a.heads, a.q_ctx, a.kv_ctx, a.dim, a.causal, a.num_split)

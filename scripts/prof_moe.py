@@ -59,6 +59,12 @@ if "--sk-ab" in sys.argv:  # stream-K hybrid expert GEMMs vs the plain tile grid
     g, w1, w2 = (t.to("cuda") for t in init_moe_weights(layer.cfg))
     ref = moe_reference(x, g, w1, w2, layer.cfg.topk)
     print("max abs err", (out - ref).abs().max().item(), "ref max", ref.abs().max().item(), flush=True)
+if "--tail-sweep" in sys.argv:  # narrow-tail width of the tail-balanced expert GEMMs
+    base = dict(layer.cfg.gemm_cfg or {})
+    for ts in (4, 2, 4, 2):
+        layer.cfg.gemm_cfg = dict(base, stream_k=True, tail_split=ts)
+        run(layer, x, f"tail_split={ts}")
+    layer.cfg.gemm_cfg = base
 if "--sweep" in sys.argv:
     for bm in (128, 256):
         for cfg in (dict(block_N=128, block_K=64, num_stages=2, threads=256),
