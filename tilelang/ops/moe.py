@@ -358,7 +358,8 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
 @functools.lru_cache(maxsize=None)
 def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target: str, block_M: int = 256,
                           block_N: int = 256, block_K: int = 64, num_stages: int = 2, threads: int = 512,
-                          n_src: Optional[int] = None, swiglu: bool = False, n_cu: int = 256, tail_split: int = 4):
+                          n_src: Optional[int] = None, swiglu: bool = False, n_cu: int = 256, tail_split: int = 4,
+                          phased: bool = True):
     """Tail-balanced variant of ``expert_gemm_kernel`` (same arguments and output).
 
     The (row tile x N tile) units are a data-dependent count U (the routing decides how many
@@ -426,8 +427,10 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
                     tile(A, W, row_src, tile_rows, C, A_s, Wt_s, Ct_l, u // n_by, tile_expert[u // n_by],
                          (u % n_by) * block_N + (q % tail_split) * bn_t, bn_t)
 
-    return tilelang.compile(moe_expert_gemm_tb, out_idx=None, target=target,
-                            pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True} if swiglu else None)
+    cfg = {"tl.gemm_phased": bool(phased)}  # K-half phased main loop, row gathers included
+    if swiglu:
+        cfg[tilelang.PassConfigKey.TL_ENABLE_FAST_MATH] = True
+    return tilelang.compile(moe_expert_gemm_tb, out_idx=None, target=target, pass_configs=cfg)
 
 
 def swiglu_interleave(w1: torch.Tensor) -> torch.Tensor:
@@ -553,7 +556,8 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
         sk = target == "hip"
     if sk and reduce_mesh is None and w1_interleaved:
         # tail-balanced grid: whole tiles for the leading rounds, narrow tiles for the trailing partial round
-        skc = {k: v for k, v in cfg.items() if k in ("block_N", "block_K", "num_stages", "threads", "tail_split")}
+        skc = {k: v for k, v in cfg.items() if k in ("block_N", "block_K", "num_stages", "threads", "tail_split",
+                                                      "phased")}
         k1 = expert_gemm_sk_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, swiglu=True, n_cu=n_cu,
                                    **skc)
         k1(src_rows.contiguous(), w1, te, row_src, trows, act)

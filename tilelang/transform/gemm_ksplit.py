@@ -60,6 +60,25 @@ def _split_copy(cp: O.CopyOp, kdim_dst: int, half: int, new_dst: Buffer, which: 
     return O.CopyOp(new_src, BufferRegion(new_dst, dreg), cp.coalesced_width, cp.disable_tma, cp.eviction_policy)
 
 
+def _split_gather(gp: O.GatherRowsOp, kdim_dst: int, half: int, new_dst: Buffer, which: int):
+    """K-half ``which`` of a row gather into ``new_dst``: the gathered rows are the tile's M dim,
+    the source's column dim (its last non-row, non-unit dim) is K."""
+    dshape = gp.dst.buffer.static_shape()
+    if dshape is None or len(dshape) != 2 or kdim_dst != 1 or gp.dst.static_extents() != dshape:
+        return None
+    sext = gp.src.static_extents()
+    if sext is None:
+        return None
+    cols = [d for d, e in enumerate(sext) if d != gp.row_dim and e != 1]
+    if len(cols) != 1 or sext[cols[0]] != dshape[1]:
+        return None
+    region = list(gp.src.region)
+    m, e = region[cols[0]]
+    region[cols[0]] = (binop("+", m, IntImm(which * half)), half)
+    dreg = [(IntImm(0), n) for n in new_dst.static_shape()]
+    return O.GatherRowsOp(BufferRegion(gp.src.buffer, region), gp.idx, BufferRegion(new_dst, dreg), gp.row_dim)
+
+
 class _KSplit(Mutator):
 
     def __init__(self, mode=True):
@@ -76,7 +95,7 @@ class _KSplit(Mutator):
             return loop
         stmts = flatten_seq(body)
         gemms = [x for x in stmts if isinstance(x, S.TileOpStmt) and isinstance(x.op, O.GemmOp)]
-        copies = [x for x in stmts if isinstance(x, S.TileOpStmt) and isinstance(x.op, O.CopyOp)]
+        copies = [x for x in stmts if isinstance(x, S.TileOpStmt) and isinstance(x.op, (O.CopyOp, O.GatherRowsOp))]
         if len(gemms) != 1 or len(copies) != 2 or len(stmts) != 3:
             return loop
         g = gemms[0].op
@@ -106,8 +125,9 @@ class _KSplit(Mutator):
             else:
                 h0 = Buffer(buf.name + "_k0", shp, buf.dtype, "shared")
                 h1 = Buffer(buf.name + "_k1", shp, buf.dtype, "shared")
-            c0 = _split_copy(cps[buf], kd, half, h0, 0)
-            c1 = _split_copy(cps[buf], kd, half, h1, 1)
+            split = _split_gather if isinstance(cps[buf], O.GatherRowsOp) else _split_copy
+            c0 = split(cps[buf], kd, half, h0, 0)
+            c1 = split(cps[buf], kd, half, h1, 1)
             if c0 is None or c1 is None:
                 return loop
             c0.khalf, c1.khalf = 0, 1

@@ -435,9 +435,9 @@ class PipelineInjector(Mutator):
             prologue.append(S.seq(*st) if nv is not None and nv > 0 else S.IfStmt(binop("<", 0, n), S.seq(*st)))
 
         consumer_stmts = [st for st in stmts if not any(st is p for p, _ in prods)]
-        if loop.annotations.get("phased") and nstages == 2 and not staged and not gkeys and len(asyncs) == 4 and \
+        if loop.annotations.get("phased") and nstages == 2 and not staged and len(asyncs) == 4 and \
                 all(getattr(p.op, "khalf", None) is not None for p, _, _ in asyncs):
-            ph = _phased_schedule(self, loop, asyncs, issue_async, consumer_stmts, mapping, newbufs, kk, n)
+            ph = _phased_schedule(self, loop, asyncs, issue_async, consumer_stmts, mapping, newbufs, kk, n, lets)
             if ph is not None:
                 return ph
         consumers = BufferReplacer(mapping).stmt(S.SeqStmt(consumer_stmts))
@@ -475,7 +475,7 @@ class PipelineInjector(Mutator):
         return S.SeqStmt(prologue + [new_loop] + tail)
 
 
-def _phased_schedule(self, loop, asyncs, issue_async, consumer_stmts, mapping, newbufs, kk, n):
+def _phased_schedule(self, loop, asyncs, issue_async, consumer_stmts, mapping, newbufs, kk, n, lets=None):
     """K-half phased GEMM schedule (after ``gemm_ksplit``): two 2-deep LDS rings, one per K half.
     Iteration t reads stage s = t % 2:
 
@@ -492,13 +492,26 @@ def _phased_schedule(self, loop, asyncs, issue_async, consumer_stmts, mapping, n
     if h != sum(pl["instrs"] for _, _, pl in halves[1]):
         return None
 
+    # row gathers (MoE token rows): their indices must not depend on the K step; they are loaded
+    # into registers once before the loop, so the counted vmcnt waits see only the DMAs
+    idx_pre, idx_key = [], {}
+    for p, src, plan in asyncs:
+        if isinstance(p.op, O.GatherRowsOp):
+            idx = _subst_region(p.op.idx, lets or {})
+            if any(v is k for m, e in idx.region for v in free_vars(m)):
+                return None
+            self.key += 1
+            idx_key[id(p)] = (self.key, idx)
+            idx_pre.append(S.TileOpStmt(GatherIndexOp(idx, plan, self.key)))
+
     def issue(half, j, stg):
         out = []
         for p, src, plan in halves[half]:
             srcj = _subst_region(src, {k: binop("+", loop.min, j)})
             NB = newbufs[p.op.dst.buffer]
             dst = BufferRegion(NB, [(stg, 1)] + list(p.op.dst.region))
-            out.append(S.TileOpStmt(AsyncCopyOp(srcj, dst, plan, None, None)))
+            key, idxj = idx_key.get(id(p), (None, None))
+            out.append(S.TileOpStmt(AsyncCopyOp(srcj, dst, plan, idxj, key)))
         return S.seq(*out)
 
     nv = as_int(n)
@@ -518,7 +531,7 @@ def _phased_schedule(self, loop, asyncs, issue_async, consumer_stmts, mapping, n
     def wait(more, n_more, n_last):
         return S.IfStmt(more, L.CallStmt("tl::wait_vmcnt", [], [n_more]), L.CallStmt("tl::wait_vmcnt", [], [n_last]))
 
-    prologue = [issue(0, IntImm(0), IntImm(0)), issue(1, IntImm(0), IntImm(0))]
+    prologue = idx_pre + [issue(0, IntImm(0), IntImm(0)), issue(1, IntImm(0), IntImm(0))]
     if nv is None or nv > 1:
         prologue.append(S.IfStmt(binop("<", IntImm(1), n), issue(0, IntImm(1), IntImm(1))) if nv is None
                         else issue(0, IntImm(1), IntImm(1)))
