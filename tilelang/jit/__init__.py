@@ -39,7 +39,8 @@ def compile(func: S.PrimFunc = None, out_idx=None, execution_backend: str = "aut
     from ..engine.callback import hook_fingerprint
     key = (func.script(), _freeze(out_idx), str(target), _freeze(pass_configs), _freeze(compile_flags),
            hook_fingerprint())
-    k = _GLOBAL_JIT_CACHE.get(key)
+    visual = bool(dict(pass_configs or {}).get("tl.layout_visualization_enable"))
+    k = None if visual else _GLOBAL_JIT_CACHE.get(key)
     if k is None:
         k = JITKernel(func, out_idx=out_idx, target=target, target_host=target_host,
                       execution_backend=execution_backend, verbose=verbose, pass_configs=pass_configs,

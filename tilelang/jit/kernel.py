@@ -80,7 +80,9 @@ class JITKernel:
         if artifact is None:
             from ..cache import kernel_cache
             key = kernel_cache.kernel_key(func, self.target, out_idx, self.pass_configs, self.compile_flags)
-            hit = kernel_cache.load(key)
+            # the layout dump is a side effect of lowering: never serve such a compile from the cache
+            visual = bool(dict(self.pass_configs or {}).get("tl.layout_visualization_enable"))
+            hit = None if visual else kernel_cache.load(key)
             if hit is not None:
                 is_cpu, kernels, code, self._launch = hit
                 tgt = Target("cpu", "host", getattr(self.target, "mesh", None)) if is_cpu and \

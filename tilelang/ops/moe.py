@@ -359,7 +359,7 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
 def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target: str, block_M: int = 256,
                           block_N: int = 256, block_K: int = 64, num_stages: int = 2, threads: int = 512,
                           n_src: Optional[int] = None, swiglu: bool = False, n_cu: int = 256, tail_split: int = 4,
-                          phased: bool = True):
+                          phased: bool = False):
     """Tail-balanced variant of ``expert_gemm_kernel`` (same arguments and output).
 
     The (row tile x N tile) units are a data-dependent count U (the routing decides how many
@@ -427,7 +427,9 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
                     tile(A, W, row_src, tile_rows, C, A_s, Wt_s, Ct_l, u // n_by, tile_expert[u // n_by],
                          (u % n_by) * block_N + (q % tail_split) * bn_t, bn_t)
 
-    cfg = {"tl.gemm_phased": bool(phased)}  # K-half phased main loop, row gathers included
+    # K-half phased main loop (row gathers included) measured slower here: 382-403 vs 300-356 us per
+    # layer (profiles/r2/session2/moe_phased_tail_sweep.log), so off by default
+    cfg = {"tl.gemm_phased": bool(phased)}
     if swiglu:
         cfg[tilelang.PassConfigKey.TL_ENABLE_FAST_MATH] = True
     return tilelang.compile(moe_expert_gemm_tb, out_idx=None, target=target, pass_configs=cfg)
