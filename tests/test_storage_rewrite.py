@@ -1,0 +1,49 @@
+"""StorageRewrite for per-thread local arrays (transform/storage_rewrite.py)."""
+import torch
+
+import tilelang
+import tilelang.language as T
+from tilelang.transform.storage_rewrite import rewrite_local_storage
+
+
+def _prog(n=256):
+
+    @T.prim_func
+    def main(A: T.Tensor((n, 8), "float32"), I: T.Tensor((n, ), "int32"), B: T.Tensor((n, ), "float32"),
+             C: T.Tensor((n, ), "float32")):
+        with T.Kernel(n, threads=64) as bx:  # one row per block (every lane computes it)
+            u = T.alloc_local((8, ), "float32")  # dynamically indexed: a private array
+            v = T.alloc_local((8, ), "float32")  # same dtype/shape, live only after u dies
+            w = T.alloc_local((4, ), "float32")  # different shape: kept
+            for j in T.serial(8):
+                u[j] = A[bx, j]
+            B[bx] = u[I[bx] % 8]
+            for j in T.serial(8):
+                v[j] = A[bx, j] * 2.0
+            w[0] = v[(I[bx] + 1) % 8]
+            C[bx] = w[0]
+
+    return main
+
+
+def test_disjoint_local_arrays_share_storage():
+    f = _prog()
+    k2, merged = rewrite_local_storage([s for s in __import__("tilelang.ir.stmt", fromlist=["walk"]).walk(f.body)
+                                        if type(s).__name__ == "KernelStmt"][0])
+    assert merged == {"v": "u"}
+    src = tilelang.compile(f, out_idx=[2, 3], target="hip").get_kernel_source()
+    assert " v[" not in src and "u[" in src
+    src_off = tilelang.compile(f, out_idx=[2, 3], target="hip",
+                               pass_configs={"tir.disable_storage_rewrite": True}).get_kernel_source()
+    assert " v[" in src_off or "v[8]" in src_off
+
+
+def test_merged_program_computes_the_same():
+    f = _prog()
+    k = tilelang.compile(f, out_idx=[2, 3], target="cpu")
+    A = torch.randn(256, 8)
+    I = torch.randint(0, 100, (256, ), dtype=torch.int32)
+    b, c = k(A, I)
+    rows = torch.arange(256)
+    torch.testing.assert_close(b, A[rows, (I % 8).long()])
+    torch.testing.assert_close(c, 2 * A[rows, ((I + 1) % 8).long()])

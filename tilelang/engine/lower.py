@@ -121,6 +121,9 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
         kernel = inline_lets(kernel)
     from ..transform.stage_schedule import apply_stage_schedules
     kernel = apply_stage_schedules(kernel)  # T.Pipelined(order=, stage=, group=)
+    if not cfg.get("tir.disable_storage_rewrite"):
+        from ..transform.storage_rewrite import rewrite_local_storage
+        kernel, _ = rewrite_local_storage(kernel)  # local arrays with disjoint lifetimes share storage
     phased = cfg.get("tl.gemm_phased")
     if target.kind == "hip" and phased is not False:  # default on: +15 % at 4096^3 (profiles/r2/gemm_phased.log)
         from ..transform.gemm_ksplit import split_gemm_k_halves

@@ -35,6 +35,7 @@ class PassConfigKey(str, Enum):
     TIR_USE_ASYNC_COPY = "tir.use_async_copy"
     TIR_MERGE_STATIC_SMEM = "tir.merge_static_smem"
     TIR_DISABLE_CSE_TIR = "tir.disable_cse_tir"
+    TIR_DISABLE_STORAGE_REWRITE = "tir.disable_storage_rewrite"
     # gfx950 additions
     TL_DISABLE_GLDS = "tl.disable_glds"            # stage through registers instead of LDS-DMA
     TL_MIN_WAVES_PER_EU = "tl.min_waves_per_eu"    # second __launch_bounds__ argument
@@ -67,6 +68,8 @@ EFFECT = {
     "tl.disable_glds": "stage tiles through registers instead of LDS-DMA",
     "tl.min_waves_per_eu": "second __launch_bounds__ argument (register budget for N waves per SIMD)",
     "tl.mfma_shape": "'16x16' (default) or '32x32': matrix-core tile of T.gemm (f16/bf16, int8)",
+    "tir.disable_storage_rewrite": "True: per-thread local arrays with disjoint lifetimes keep separate "
+                                   "storage (transform/storage_rewrite.py merges them by default)",
     "tl.gemm_phased": "default on; False keeps BK=64 16-bit GEMM main loops whole instead of splitting them "
                       "into K halves refilled one phase apart (transform/gemm_ksplit.py + the phased "
                       "pipeline schedule); 'prio' also raises wave priority around the MFMA clusters",
