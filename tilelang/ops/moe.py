@@ -381,7 +381,13 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
     n_out = N // 2 if swiglu else N
 
     @T.macro
-    def tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, bx, e, col0, bn):
+    def tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, bx_raw, e_raw, col0, bn):
+        # tile / expert ids come from device tables: clamp them so the operand copies are provably
+        # in bounds (LDS-DMA instead of guarded register staging) and read them once per tile
+        bx = T.min(bx_raw, n_tiles - 1)  # expressions, so the bounds prover sees the clamps
+        e = T.min(T.max(e_raw, 0), E - 1)
+        nrows = T.alloc_var("int32")
+        nrows = tile_rows[bx]
         T.clear(C_l)
         for k in T.Pipelined(nk, num_stages=num_stages):
             if n_src is not None:
@@ -390,7 +396,7 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
             else:
                 T.copy(A[bx * block_M, k * block_K], A_s)
             T.copy(W[e, col0, k * block_K], W_s)
-            T.gemm(A_s, W_s, C_l, transpose_B=True, valid_m=tile_rows[bx])
+            T.gemm(A_s, W_s, C_l, transpose_B=True, valid_m=nrows)
         if swiglu:
             for i, j in T.Parallel(block_M, bn):
                 if j % 4 < 2:

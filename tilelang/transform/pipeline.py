@@ -276,6 +276,9 @@ class PipelineInjector(Mutator):
         return self.pipeline(S.ForStmt(s.var, s.min, s.extent, s.kind, body, s.annotations))
 
     def visit_LetStmt(self, s):
+        b = bound(s.value, self.ranges)  # clamped table lookups stay provably in bounds
+        if b is not None:
+            self.ranges[s.var] = b
         return s
 
     def pipeline(self, loop: S.ForStmt):

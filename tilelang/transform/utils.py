@@ -200,6 +200,9 @@ def _bound(e, ranges):
             if e.op == "min":
                 return (min(a[0], b[0]), min(a[1], b[1]))
             return (max(a[0], b[0]), max(a[1], b[1]))
+        if e.op == "%" and b is not None and b[0] == b[1] and b[0] > 0 and \
+                (a is None or _INF in (abs(a[0]), abs(a[1])) or a[0] < 0):
+            return (0, b[0] - 1)  # floor modulo: in [0, b) whatever the dividend
         if a is None or b is None or _INF in (abs(a[0]), abs(a[1]), abs(b[0]), abs(b[1])):
             return None
         if e.op == "+":
