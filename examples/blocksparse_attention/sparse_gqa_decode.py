@@ -62,7 +62,8 @@ def _program(mode, batch, heads, heads_kv, dim, block_size, max_sel, num_split, 
                 kv0 = T.max(blk, 0) * BN
                 if mode == "paged":
                     page = block_table[bx, kv0 // page_size]
-                    off = kv0 % page_size
+                    # == kv0 % page_size (kv0 is block aligned); provably off + BN <= page_size (LDS-DMA)
+                    off = T.max(blk, 0) % (page_size // BN) * BN
                     T.copy(K[page, off:off + BN, g, :], K_s)
                     T.copy(V[page, off:off + BN, g, :], V_s)
                 else:

@@ -69,7 +69,7 @@ def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe
             for t in T.Pipelined(t_begin, t_end, num_stages=num_stages):
                 tok = t * block_N
                 page = BlockTable[bx, tok // page_size]
-                off = tok % page_size
+                off = t % (page_size // block_N) * block_N  # == tok % page_size; provably + block_N <= page_size
                 T.copy(KV[page, off:off + block_N, :], KV_shared)
                 T.copy(K_pe[page, off:off + block_N, :], K_pe_shared)
                 for i, j in T.Parallel(block_H, block_N):

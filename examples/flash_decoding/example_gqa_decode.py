@@ -36,6 +36,8 @@ def _decode_program(batch, heads, groups, dim, block_N, block_H, num_split, thre
     if paged:
         assert page_size % block_N == 0
         max_len = max_pages * page_size
+        # every split starts on a block boundary, so a block never straddles two pages
+        assert (-(-max_len // num_split)) % block_N == 0, "paged: max_pages * page_size / num_split % block_N"
         k_shape = [num_pages, page_size, groups, dim]
     else:
         max_len = seqlen_kv
@@ -69,7 +71,8 @@ def _decode_program(batch, heads, groups, dim, block_N, block_H, num_split, thre
                 kv_start = bz * split_len + k * block_N
                 if paged:
                     page = block_table[bx, kv_start // page_size]
-                    off = kv_start % page_size
+                    # block-granular in-page offset: provably off + block_N <= page_size (LDS-DMA)
+                    off = (kv_start // block_N) % (page_size // block_N) * block_N
                     T.copy(K[page, off:off + block_N, g, :], K_shared)
                     T.copy(V[page, off:off + block_N, g, :], V_shared)
                 else:
