@@ -306,7 +306,8 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
                                           row_src[bx * block_M:(bx + 1) * block_M], A_s, row_dim=0)
                         else:
                             T.copy(A[bx * block_M, k * block_K], A_s)
-                        T.copy(W[e, by * block_N, k * block_K], W_s)
+                        # clamped expert id: provably in bounds, so the W tile is an LDS-DMA producer
+                        T.copy(W[T.min(T.max(e, 0), E - 1), by * block_N, k * block_K], W_s)
                         # an expert's last row tile is partly padding: its empty waves skip the MFMAs
                         T.gemm(A_s, W_s, C_l, transpose_B=True, valid_m=tile_rows[bx] if skip_padding else None)
                     if swiglu:
@@ -347,7 +348,7 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
                                               row_src[bx * block_M:(bx + 1) * block_M], A_s, row_dim=0)
                             else:
                                 T.copy(A[bx * block_M, k * block_K], A_s)
-                            T.copy(W[e, by * block_N, k * block_K], W_s)
+                            T.copy(W[T.min(T.max(e, 0), E - 1), by * block_N, k * block_K], W_s)
                             T.gemm(A_s, W_s, C_l, transpose_B=True, valid_m=tile_rows[bx] if skip_padding else None)
                         T.comm.all_reduce_tile(C_l, C_r, "sum", reduce_mesh)
                         T.copy(C_r, C[bx * block_M, by * block_N])
