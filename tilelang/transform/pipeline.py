@@ -32,6 +32,10 @@ from ..layout.layout import Layout, LinearLayout, SwizzleLayout
 from .utils import BufferReplacer, Mutator, Substituter, bound, flatten_seq
 
 
+import logging as _logging
+
+_log = _logging.getLogger("tilelang.pipeline")
+
 class AsyncCopyOp(O.TileOp):
     """Global->LDS DMA copy (lowered to ``tl::glds16``)."""
     kind = "async_copy"
@@ -371,6 +375,8 @@ class PipelineInjector(Mutator):
                 asyncs.append((p, src, plan))
             else:
                 staged.append((p, src))
+                _log.debug("register-staged pipeline copy %s -> %s (not provably in bounds / not DMA-shaped)",
+                           src.buffer.name, p.op.dst.buffer.name)
         L_instr = sum(pl["instrs"] for _, _, pl in asyncs)
 
         gkeys = {}
