@@ -202,8 +202,10 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
             loop_ed = T.ceildiv(seq_len, block_N)
             n_q = loop_ed - loop_st
             for it in T.Pipelined(n_q * groups, num_stages=num_stages):
-                hq = bx * groups + it // n_q
-                k = loop_st + it % n_q
+                # clamped into range: provably in bounds, so the Q / dO / lse / Delta tiles are LDS-DMA
+                # producers (division / modulo by a runtime count hides the range from the prover)
+                hq = T.max(T.min(bx * groups + it // n_q, heads - 1), 0)
+                k = T.max(T.min(loop_st + it % n_q, loop_ed - 1), 0)
                 T.copy(Q[bz, k * block_N:(k + 1) * block_N, hq, :], q)
                 T.clear(qkT)
                 T.gemm(K_shared, q, qkT, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)

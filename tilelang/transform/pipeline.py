@@ -356,15 +356,19 @@ class PipelineInjector(Mutator):
         else:
             # data-dependent trip counts (causal / windowed attention): interval of the loop
             # var from the bounds of its start and end, so LDS-DMA stays provably in bounds
-            lo = bound(loop.min, self.ranges)
+            # (only the start's lower bound and the end's upper bound matter: half-open intervals
+            # such as max(0, data-dependent) starts still give a finite loop-var range)
+            from .utils import _bound
+            lo = _bound(loop.min, self.ranges)
             ext = loop.extent
             from ..ir.expr import BinOp, structural_equal
             if isinstance(ext, BinOp) and ext.op == "-" and structural_equal(ext.b, loop.min):
-                hi = bound(ext.a, self.ranges)  # T.Pipelined(start, end): extent = end - start
+                hi = _bound(ext.a, self.ranges)  # T.Pipelined(start, end): extent = end - start
             else:
-                hi = bound(binop("+", loop.min, ext), self.ranges)
-            if lo is not None and hi is not None:
-                rng[k] = (lo[0], max(lo[0], hi[1] - 1))
+                hi = _bound(binop("+", loop.min, ext), self.ranges)
+            inf = float("inf")
+            if lo is not None and hi is not None and abs(lo[0]) != inf and abs(hi[1]) != inf:
+                rng[k] = (int(lo[0]), int(max(lo[0], hi[1] - 1)))
         asyncs, staged = [], []
         for p, src in prods:
             if isinstance(p.op, O.GatherRowsOp):
@@ -375,8 +379,9 @@ class PipelineInjector(Mutator):
                 asyncs.append((p, src, plan))
             else:
                 staged.append((p, src))
-                _log.debug("register-staged pipeline copy %s -> %s (not provably in bounds / not DMA-shaped)",
-                           src.buffer.name, p.op.dst.buffer.name)
+                _log.debug("register-staged pipeline copy %s -> %s (not provably in bounds / not DMA-shaped): %s",
+                           src.buffer.name, p.op.dst.buffer.name,
+                           [(str(m), bound(m, rng)) for m, _ in src.region])
         L_instr = sum(pl["instrs"] for _, _, pl in asyncs)
 
         gkeys = {}
