@@ -164,6 +164,22 @@ def main():
     ref = A[:64].float() @ B.float()
     if not torch.allclose(C[:64].float(), ref, rtol=2e-2, atol=2e-1):
         raise SystemExit("GEMM result check failed")
+    # attention: one head against the fp32 definition (bshd layout)
+    O = attn(Q, K, V)
+    q1, k1, v1 = (t[:, :, :1].float().transpose(1, 2) for t in (Q, K, V))
+    o_ref = torch.softmax(q1 @ k1.transpose(-1, -2) / q1.shape[-1]**0.5, -1) @ v1
+    if not torch.allclose(O[:, :, :1].float().transpose(1, 2), o_ref, rtol=3e-2, atol=3e-2):
+        raise SystemExit("attention result check failed")
+    if moe is not None and mesh is None:
+        # MoE layer on a token subset vs the fp32 definition with the kernel's own routing
+        # (exact 16-bit logit ties may pick either expert: models.moe.routing_equivalent)
+        from tilelang.models.moe import moe_reference, init_moe_weights
+        from tilelang.ops.moe import route
+        xs = X[:256]
+        g_w, w1, w2 = (t.to(xs.device) for t in init_moe_weights(moe.cfg))
+        y_ref = moe_reference(xs, g_w, w1, w2, moe.cfg.topk, routing=route(xs, moe.gate_w, moe.cfg.topk))
+        if not torch.allclose(moe(xs).float(), y_ref, rtol=3e-2, atol=3e-2 * float(y_ref.abs().max())):
+            raise SystemExit("MoE result check failed")
 
     gemm_flops = 2.0 * g["M"] * g["N"] * g["K"]
     attn_flops = 4.0 * a_["batch"] * a_["heads"] * a_["seq_len"]**2 * a_["dim"]
