@@ -120,3 +120,15 @@ def test_dynamic_shape_gemm():
         a = torch.randn(M, 256, device="cuda", dtype=torch.float16)
         b = torch.randn(256, 256, device="cuda", dtype=torch.float16)
         torch.testing.assert_close(k(a, b).float(), a.float() @ b.float(), rtol=2e-2, atol=2e-1)
+
+
+def test_runtime_facade():
+    """tilelang.runtime: device properties and runtime-owned (uncached) workspace memory."""
+    from tilelang import runtime as R
+    info = R.device_info(0)
+    assert info["gcnArchName"].startswith("gfx950") and info["multiProcessorCount"] >= 1
+    ws = R.Workspace(4096, 0, uncached=True)
+    assert ws.ptr != 0
+    ws.zero()
+    ws.close()
+    assert ws.ptr == 0

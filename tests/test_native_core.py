@@ -102,3 +102,10 @@ def test_hierarchical_native_offsets():
     with pytest.raises(ValueError, match="partition"):
         make_hierarchical_layout([2, 4], [4, 1], [(0, 1), (0, 1)])
     assert core.shard_hier([8, 32, 4, 32], [(0, 2), (2, 4)], 0, 4) == [2, 32, 4, 32]
+
+
+def test_runtime_package_surface():
+    import tilelang.runtime as R
+    assert R.available() in (True, False)
+    for name in ("device_info", "Workspace", "can_access_peer", "NativeRuntimeMissing"):
+        assert hasattr(R, name)
