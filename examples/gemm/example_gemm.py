@@ -8,11 +8,12 @@ import argparse
 
 import tilelang
 import tilelang.language as T
+from tilelang.layout import PaddedLayout
 
 
 @tilelang.jit(out_idx=[-1])
 def matmul(M, N, K, block_M=128, block_N=128, block_K=32, threads=256, num_stages=3, dtype="float16",
-           accum_dtype="float", trans_B=False, swizzle=True, panel=8):
+           accum_dtype="float", trans_B=False, swizzle=True, panel=8, staged_epilogue=False):
 
     B_shape = (N, K) if trans_B else (K, N)
 
@@ -36,7 +37,16 @@ def matmul(M, N, K, block_M=128, block_N=128, block_K=32, threads=256, num_stage
                 else:
                     T.copy(B[k * block_K, bx * block_N], B_shared)
                 T.gemm(A_shared, B_shared, C_local, transpose_B=trans_B)
-            T.copy(C_local, C[by * block_M, bx * block_N])
+            if staged_epilogue:
+                # row-contiguous 16-byte stores: MFMA fragment -> LDS (reuses the A/B ring's
+                # space, dead after the loop) -> global
+                C_shared = T.alloc_shared((block_M, block_N), dtype)
+                # 16-byte row pad: the 16 rows one MFMA store instruction touches land on distinct banks
+                T.annotate_layout({C_shared: PaddedLayout((block_M, block_N), 8)})
+                T.copy(C_local, C_shared)
+                T.copy(C_shared, C[by * block_M, bx * block_N])
+            else:
+                T.copy(C_local, C[by * block_M, bx * block_N])
 
     return gemm
 

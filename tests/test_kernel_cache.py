@@ -50,3 +50,16 @@ def test_disk_cache_across_processes(tmp_path):
     outs = [subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
             for _ in range(2)]
     assert [o.stdout.strip().splitlines()[-1] for o in outs] == ["MISS", "HIT"], [o.stderr[-2000:] for o in outs]
+
+
+def test_annotated_layout_changes_cache_key():
+    """A user layout (T.annotate_layout) changes the generated code, so it must change the key."""
+    f0 = matmul.get_tir(256, 256, 256, 256, 256, 64, 512, 2, "float16", staged_epilogue=True)
+    import tilelang.language as T  # noqa: F401
+    from tilelang.layout import PaddedLayout
+    k0 = kernel_cache.kernel_key(f0, "hip", [-1], {}, [])
+    f1 = matmul.get_tir(256, 256, 256, 256, 256, 64, 512, 2, "float16", staged_epilogue=True)
+    bufs = [s.buffer for s in __import__("tilelang.ir.stmt", fromlist=["walk"]).walk(f1.body)
+            if type(s).__name__ == "AllocStmt" and s.buffer.name == "C_shared"]
+    bufs[0].layout = PaddedLayout((256, 256), 16)
+    assert kernel_cache.kernel_key(f1, "hip", [-1], {}, []) != k0

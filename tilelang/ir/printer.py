@@ -155,6 +155,10 @@ class Printer:
                 self.w(f"{self.names(b, b.name)} = T.alloc_var({b.dtype.name!r})")
             else:
                 self.w(f"{self.names(b, b.name)} = T.{fn}({shape}, {b.dtype.name!r})")
+            if getattr(b, "layout_annotated", False) and b.layout is not None:
+                # user layouts change the generated code: they belong in the printed program
+                # (and therefore in the kernel-cache key)
+                self.w(f"T.annotate_layout({{{self.names(b, b.name)}: {_layout_key(b.layout)}}})")
         elif isinstance(s, S.TileOpStmt):
             self.w(self.tileop(s.op))
         elif isinstance(s, S.BreakStmt):
@@ -291,3 +295,23 @@ def stmt_str(s) -> str:
 
 def func_str(f) -> str:
     return Printer().func(f)
+
+
+def _layout_key(layout) -> str:
+    """Printable identity of a layout.  Subclasses carry a complete ``signature()``; a generic
+    callable-defined ``Layout`` is identified by its index map sampled over (a prefix of) its
+    domain, since two lambdas of the same shape would otherwise print alike."""
+    from ..layout.layout import Layout
+    sig = layout.signature() if hasattr(layout, "signature") else repr(layout)
+    if type(layout) is not Layout:
+        return repr(sig)
+    import hashlib
+    import itertools
+    shape = [int(x) for x in layout.shape]
+    h = hashlib.sha1()
+    for idx in itertools.islice(itertools.product(*(range(n) for n in shape)), 8192):
+        try:
+            h.update(repr(layout.forward(*idx)).encode())
+        except Exception:
+            h.update(b"?")
+    return repr(sig + (h.hexdigest()[:16],))
