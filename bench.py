@@ -40,7 +40,9 @@ REF_GEMM_TF = 736.0
 REF_ATTN_TF = 497.13
 PEAK_BF16_TF = 2500.0  # MI355X dense fp16/bf16 MFMA (AMD spec, no sparsity)
 
-GEMM_CFG = dict(M=4096, N=4096, K=4096, block_M=256, block_N=256, block_K=64, threads=512, num_stages=2)
+# staged_epilogue: C tile through LDS, row-contiguous 16-byte stores (+3-4 % cold, profiles/r2/session2/gemm_epi_ab.log)
+GEMM_CFG = dict(M=4096, N=4096, K=4096, block_M=256, block_N=256, block_K=64, threads=512, num_stages=2,
+                staged_epilogue=True)
 # FA (scripts/sweep_fa.py, profiles/r2/fa_staged.log): 256x64 tile, 8 waves, Q in registers, 2-stage K/V
 # ring, T.Pipelined(order, stage) schedule: QK^T(t) | rescale+PV(t-1) | softmax(t)
 ATTN_CFG = dict(batch=1, heads=64, seq_len=4096, dim=128, block_M=256, block_N=64, threads=512, num_stages=2,
@@ -78,7 +80,7 @@ def build_gemm(device="cuda", g=None):
     from example_gemm import matmul
     g = g or GEMM_CFG
     f = matmul.get_tir(g["M"], g["N"], g["K"], g["block_M"], g["block_N"], g["block_K"], g["threads"],
-                       g["num_stages"], "float16")
+                       g["num_stages"], "float16", staged_epilogue=g.get("staged_epilogue", False))
     k = tilelang.compile(f, out_idx=[-1], target=_target(device))
     A = torch.randn(g["M"], g["K"], device=device).to(torch.float16)
     B = torch.randn(g["K"], g["N"], device=device).to(torch.float16)

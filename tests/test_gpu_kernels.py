@@ -20,11 +20,14 @@ def _native_loaded():
     (1024, 1024, 1024, 256, 256, 64, 512, 2, False, "float16"),
     (512, 512, 512, 128, 128, 32, 256, 2, False, "bfloat16"),
     (512, 512, 512, 128, 128, 64, 256, 1, True, "bfloat16"),
+    (1024, 768, 512, 256, 256, 64, 512, 2, "staged", "float16"),
 ])
 def test_gemm(M, N, K, bm, bn, bk, threads, stages, trans_b, dtype):
     _native_loaded()
     from example_gemm import matmul
-    k = matmul(M, N, K, bm, bn, bk, threads, stages, dtype, trans_B=trans_b)
+    staged = trans_b == "staged"  # LDS-staged epilogue (padded C tile, 16-byte row stores)
+    trans_b = False if staged else trans_b
+    k = matmul(M, N, K, bm, bn, bk, threads, stages, dtype, trans_B=trans_b, staged_epilogue=staged)
     tdt = getattr(torch, dtype)
     a = torch.randn(M, K, device="cuda", dtype=tdt)
     b = torch.randn((N, K) if trans_b else (K, N), device="cuda", dtype=tdt)
