@@ -17,6 +17,7 @@ import argparse
 
 import tilelang
 import tilelang.language as T
+from tilelang.layout import PaddedLayout
 
 from example_mha_fwd import FAST_MATH, ref_program
 
@@ -24,7 +25,7 @@ from example_mha_fwd import FAST_MATH, ref_program
 @tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
 def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=256, block_N=64,
                         threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
-                        young_prio=False):
+                        young_prio=False, staged_epilogue=False):
     """``young_prio``: the second-dispatched half of the waves runs at issue priority 1 (one
     ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4)."""
     scale = (1.0 / dim)**0.5 * 1.44269504
@@ -114,7 +115,13 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                 T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
             for i, j in T.Parallel(block_M, dim):
                 acc_o[i, j] /= logsum[i]
-            T.copy(acc_o, Output[bz, bx * block_M:(bx + 1) * block_M, by, :])
+            if staged_epilogue:  # O tile through row-padded LDS: 16-byte row-contiguous stores
+                O_s = T.alloc_shared([block_M, dim], dtype)
+                T.annotate_layout({O_s: PaddedLayout((block_M, dim), 8)})
+                T.copy(acc_o, O_s)
+                T.copy(O_s, Output[bz, bx * block_M:(bx + 1) * block_M, by, :])
+            else:
+                T.copy(acc_o, Output[bz, bx * block_M:(bx + 1) * block_M, by, :])
 
     return main
 
