@@ -25,13 +25,22 @@ from example_mha_fwd import FAST_MATH, ref_program
 @tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
 def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=256, block_N=64,
                         threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
-                        young_prio=False, staged_epilogue=False):
+                        young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd"):
     """``young_prio``: the second-dispatched half of the waves runs at issue priority 1 (one
-    ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4)."""
+    ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4).
+    ``seq_kv`` (default ``seq_len``): key/value length; with ``is_causal`` the mask is aligned
+    bottom-right (query i sees keys up to i + seq_kv - seq_len).  ``layout``: "bshd" or "bhsd"
+    for Q/K/V/O (reference example_mha_fwd_bhsd.py)."""
     scale = (1.0 / dim)**0.5 * 1.44269504
     head_kv = heads // groups
-    q_shape = [batch, seq_len, heads, dim]
-    kv_shape = [batch, seq_len, head_kv, dim]
+    seq_kv = seq_len if seq_kv is None else seq_kv
+    past = seq_kv - seq_len
+    assert past >= 0, "seq_kv must be >= seq_len"
+    assert seq_kv % block_N == 0, "no key-padding mask: seq_kv must be a multiple of block_N"
+    bhsd = layout == "bhsd"
+    assert layout in ("bshd", "bhsd")
+    q_shape = [batch, heads, seq_len, dim] if bhsd else [batch, seq_len, heads, dim]
+    kv_shape = [batch, head_kv, seq_kv, dim] if bhsd else [batch, seq_kv, head_kv, dim]
     accum_dtype = "float"
     n_softmax = 8 if lazy_rescale else 7  # statements of the softmax group below
     group = [[0], [1, 2], list(range(3, 3 + n_softmax))]
@@ -61,7 +70,10 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
             logsum = T.alloc_fragment([block_M], accum_dtype)
             rescale = T.alloc_var("int32")
 
-            T.copy(Q[bz, bx * block_M:(bx + 1) * block_M, by, :], Q_s)
+            if bhsd:
+                T.copy(Q[bz, by, bx * block_M:(bx + 1) * block_M, :], Q_s)
+            else:
+                T.copy(Q[bz, bx * block_M:(bx + 1) * block_M, by, :], Q_s)
             T.fill(acc_o, 0)
             T.fill(logsum, 0)
             T.fill(scores_max, -(2.0**30) if lazy_rescale else -T.infinity(accum_dtype))
@@ -70,16 +82,23 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                 if T.get_thread_binding() >= threads // 2:
                     T.set_priority(1)
 
-            loop_range = (T.ceildiv((bx + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N))
+            if is_causal:
+                loop_range = T.ceildiv((bx + 1) * block_M, block_N) if past == 0 else T.min(
+                    T.ceildiv((bx + 1) * block_M + past, block_N), T.ceildiv(seq_kv, block_N))
+            else:
+                loop_range = T.ceildiv(seq_kv, block_N)
 
             for k in T.Pipelined(loop_range, num_stages=num_stages, order=[-1, 0, 3, 1, -1, 2],
                                  stage=[-1, 0, 0, 1, -1, 1], group=group):
                 # 0: K tile (producer)
-                T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
+                if bhsd:
+                    T.copy(K[bz, by // groups, k * block_N:(k + 1) * block_N, :], K_shared)
+                else:
+                    T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
                 # 1-2: S = Q K^T
                 if is_causal:
                     for i, j in T.Parallel(block_M, block_N):
-                        acc_s[i, j] = T.if_then_else(bx * block_M + i >= k * block_N + j, 0,
+                        acc_s[i, j] = T.if_then_else(bx * block_M + i + past >= k * block_N + j, 0,
                                                      -T.infinity(acc_s.dtype))
                 else:
                     T.clear(acc_s)
@@ -111,7 +130,10 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                     for i, j in T.Parallel(block_M, dim):
                         acc_o[i, j] *= scores_scale[i]
                 # V tile (producer) and O += P V (one tile behind)
-                T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
+                if bhsd:
+                    T.copy(V[bz, by // groups, k * block_N:(k + 1) * block_N, :], V_shared)
+                else:
+                    T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
                 T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
             for i, j in T.Parallel(block_M, dim):
                 acc_o[i, j] /= logsum[i]
@@ -119,7 +141,12 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                 O_s = T.alloc_shared([block_M, dim], dtype)
                 T.annotate_layout({O_s: PaddedLayout((block_M, dim), 8)})
                 T.copy(acc_o, O_s)
-                T.copy(O_s, Output[bz, bx * block_M:(bx + 1) * block_M, by, :])
+                if bhsd:
+                    T.copy(O_s, Output[bz, by, bx * block_M:(bx + 1) * block_M, :])
+                else:
+                    T.copy(O_s, Output[bz, bx * block_M:(bx + 1) * block_M, by, :])
+            elif bhsd:
+                T.copy(acc_o, Output[bz, by, bx * block_M:(bx + 1) * block_M, :])
             else:
                 T.copy(acc_o, Output[bz, bx * block_M:(bx + 1) * block_M, by, :])
 

@@ -501,3 +501,26 @@ def test_mha_inference_split_kv(causal):
     q, kk, v = torch.randn(b, sq, h, d).half(), torch.randn(b, sk, h, d).half(), torch.randn(b, sk, h, d).half()
     o = k(q, kk, v, torch.empty(b, h, ns, sq), torch.empty(b, sq, h, ns, d))
     torch.testing.assert_close(o.float(), m.ref_program(q, kk, v, causal).float(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_mha_fwd_bhsd_seq_q_ne_kv_cpu(causal):
+    """bhsd layout, seq_q < seq_kv, bottom-right causal alignment (example_mha_fwd_bhsd.py)."""
+    from example_mha_fwd_pipelined import flashattn_pipelined as fa
+    from example_mha_fwd_bhsd import ref_program
+    f = fa.get_tir(1, 2, 64, 64, causal, 1, 64, 32, 128, 2, "bfloat16", seq_kv=128, layout="bhsd")
+    tilelang.compile(f, out_idx=[3], target="hip", pass_configs=fa.pass_configs)
+    k = tilelang.compile(f, out_idx=[3], target="cpu", pass_configs=fa.pass_configs)
+    q = torch.randn(1, 2, 64, 64).bfloat16()
+    kk, v = (torch.randn(1, 2, 128, 64).bfloat16() for _ in range(2))
+    torch.testing.assert_close(k(q, kk, v).float(), ref_program(q, kk, v, causal).float(), rtol=2e-2, atol=2e-2)
+
+
+def test_gqa_fwd_bshd_cpu():
+    from example_mha_fwd_pipelined import flashattn_pipelined as fa
+    from example_mha_fwd import ref_program
+    f = fa.get_tir(1, 4, 128, 64, True, 2, 64, 32, 128, 2, "bfloat16")
+    k = tilelang.compile(f, out_idx=[3], target="cpu", pass_configs=fa.pass_configs)
+    q = torch.randn(1, 128, 4, 64).bfloat16()
+    kk, v = (torch.randn(1, 128, 2, 64).bfloat16() for _ in range(2))
+    torch.testing.assert_close(k(q, kk, v).float(), ref_program(q, kk, v, True, 2).float(), rtol=2e-2, atol=2e-2)

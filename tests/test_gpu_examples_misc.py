@@ -401,3 +401,14 @@ def test_flash_attention_varlen_reference_entry_gpu(causal):
     kern = flashattn(4, q.shape[0], k.shape[0], 8, 128, causal)
     o = kern(q, k, v, cq, ck, max(lens))
     torch.testing.assert_close(o.float(), ref_program(q, k, v, cq, ck, causal).float(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_mha_fwd_bhsd(causal):
+    import example_mha_fwd_bhsd as m
+    m.main(2, 8, 256, 1024, 128, causal)
+
+
+def test_gqa_fwd_bshd():
+    import example_gqa_fwd_bshd as m
+    m.main(1, 32, 1024, 128, True, 8)
