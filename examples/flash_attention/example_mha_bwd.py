@@ -31,7 +31,7 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[3, 4], pass_configs=FAST_MATH)
 def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=256, block_N=64, threads=None, dtype="float16",
-                  groups=1, num_stages=2):
+                  groups=1, num_stages=2, dim_v=None):
     """Forward that also writes the base-2 LSE (the training forward).  Schedule as the sink
     kernel (examples/attention_sink): heads on the fastest grid axis and the heaviest causal
     query tiles first, KV tiles below the diagonal in an unmasked loop and the diagonal ones
@@ -39,8 +39,11 @@ def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=256, block_N=64
     if threads is None:
         threads = min(512, 64 * (block_M // 16))  # FullRow: >= 16 query rows per wave
     scale = (1.0 / dim)**0.5 * LOG2E
+    dv_ = dim if dim_v is None else dim_v  # V / O head dim (e.g. 192 / 128 in DeepSeek-style heads)
     shape = [batch, seq_len, heads, dim]
     kv_shape = [batch, seq_len, heads // groups, dim]
+    v_shape = [batch, seq_len, heads // groups, dv_]
+    o_shape = [batch, seq_len, heads, dv_]
     accum_dtype = "float"
     n_qt = (seq_len + block_M - 1) // block_M
 
@@ -68,7 +71,7 @@ def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=256, block_N=64
             else:
                 alpha[i] = 1.0
         if rescale != 0:
-            for i, j in T.Parallel(block_M, dim):
+            for i, j in T.Parallel(block_M, dv_):
                 acc_o[i, j] *= alpha[i]
         for i, j in T.Parallel(block_M, block_N):
             acc_s[i, j] = T.exp2(acc_s[i, j] * scale - m[i] * scale)
@@ -79,16 +82,16 @@ def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=256, block_N=64
         T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
 
     @T.prim_func
-    def flash_fwd(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
-                  Output: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype)):
+    def flash_fwd(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(v_shape, dtype),
+                  Output: T.Tensor(o_shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype)):
         with T.Kernel(heads, n_qt, batch, threads=threads) as (by, bx, bz):
             Q_shared = T.alloc_shared([block_M, dim], dtype)
             K_shared = T.alloc_shared([block_N, dim], dtype)
-            V_shared = T.alloc_shared([block_N, dim], dtype)
+            V_shared = T.alloc_shared([block_N, dv_], dtype)
             acc_s = T.alloc_fragment([block_M, block_N], accum_dtype)
             acc_s_cast = T.alloc_fragment([block_M, block_N], dtype)
-            acc_o = T.alloc_fragment([block_M, dim], accum_dtype)
-            o_cast = T.alloc_fragment([block_M, dim], dtype)
+            acc_o = T.alloc_fragment([block_M, dv_], accum_dtype)
+            o_cast = T.alloc_fragment([block_M, dv_], dtype)
             m = T.alloc_fragment([block_M], accum_dtype)
             m_prev = T.alloc_fragment([block_M], accum_dtype)
             alpha = T.alloc_fragment([block_M], accum_dtype)
@@ -111,7 +114,7 @@ def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=256, block_N=64
             for k in T.Pipelined(full_end, end, num_stages=num_stages):
                 step(K, V, Q_shared, K_shared, V_shared, acc_s, acc_s_cast, acc_o, m, m_prev, alpha, r_sum, l_sum, k,
                      qt, by, bz, True)
-            for i, j in T.Parallel(block_M, dim):
+            for i, j in T.Parallel(block_M, dv_):
                 o_cast[i, j] = acc_o[i, j] / l_sum[i]
             T.copy(o_cast, Output[bz, qt * block_M:(qt + 1) * block_M, by, :])
             for i in T.Parallel(block_M):
@@ -161,26 +164,42 @@ def flashattn_bwd_postprocess(batch, heads, seq_len, dim, blk=64, threads=256, d
 
 @tilelang.jit(pass_configs=FAST_MATH)
 def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=512, num_stages=2,
-                  dtype="float16", dq_mode="atomic", groups=1):
+                  dtype="float16", dq_mode="atomic", groups=1, dim_v=None, kv_split=1):
     """``dq_mode``: "atomic" (fp32 atomics into dQ, one kernel) or "none" (dK/dV only; dQ comes from
     ``flashattn_bwd_dq``) -- the dQ atomics were 85% of the single-kernel time on MI355X.
     GQA (``groups`` query heads per KV head): one block per KV head walks the Q/dO tiles of all
     its query heads in ONE pipelined loop (head = it // n_q, tile = it % n_q), so dK/dV of the
-    group accumulate in registers -- no atomics, no per-query-head dK/dV buffers."""
+    group accumulate in registers -- no atomics, no per-query-head dK/dV buffers.
+    ``kv_split`` > 1 (few KV heads, e.g. 2 KV heads x 8 key tiles x batch 8 = 128 workgroups on
+    256 CUs): each KV head's query heads are split over ``kv_split`` workgroups that write fp32
+    partial dK/dV [kv_split, batch, seq, head_kv, d] (summed by the caller), so the grid fills
+    the chip instead of serialising all ``groups`` heads in one workgroup."""
     sm_scale = (1.0 / dim)**0.5
     scale = sm_scale * LOG2E
     shape = [batch, seq_len, heads, dim]
     head_kv = heads // groups
     kv_shape = [batch, seq_len, head_kv, dim]
+    dv_ = dim if dim_v is None else dim_v
+    v_shape = [batch, seq_len, head_kv, dv_]
+    o_shape = [batch, seq_len, heads, dv_]
     accum_dtype = "float"
+    assert groups % kv_split == 0 and (kv_split == 1 or dq_mode == "none")
+    gps = groups // kv_split  # query heads per workgroup
+    if kv_split > 1:
+        kv_shape_o = [kv_split, batch, seq_len, head_kv, dim]
+        v_shape_o = [kv_split, batch, seq_len, head_kv, dv_]
+        out_dtype = accum_dtype
+    else:
+        kv_shape_o, v_shape_o, out_dtype = kv_shape, v_shape, dtype
 
     @T.macro
     def body(Q, K, V, dO, lse, Delta, dQ, dK, dV):
-        with T.Kernel(head_kv, T.ceildiv(seq_len, block_M), batch, threads=threads) as (bx, by, bz):
+        with T.Kernel(head_kv * kv_split, T.ceildiv(seq_len, block_M), batch, threads=threads) as (bxs, by, bz):
+            bx, sp = (bxs // kv_split, bxs % kv_split) if kv_split > 1 else (bxs, 0)  # KV head, query-head slice
             K_shared = T.alloc_shared([block_M, dim], dtype)
-            V_shared = T.alloc_shared([block_M, dim], dtype)
+            V_shared = T.alloc_shared([block_M, dv_], dtype)
             q = T.alloc_shared([block_N, dim], dtype)
-            do = T.alloc_shared([block_N, dim], dtype)
+            do = T.alloc_shared([block_N, dv_], dtype)
             dsT_shared = T.alloc_shared([block_M, block_N], dtype)
             lse_shared = T.alloc_shared([block_N], accum_dtype)
             delta = T.alloc_shared([block_N], accum_dtype)
@@ -188,10 +207,10 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
             dsT = T.alloc_fragment([block_M, block_N], accum_dtype)
             qkT_cast = T.alloc_fragment([block_M, block_N], dtype)
             dsT_cast = T.alloc_fragment([block_M, block_N], dtype)
-            dv = T.alloc_fragment([block_M, dim], accum_dtype)
+            dv = T.alloc_fragment([block_M, dv_], accum_dtype)
             dk = T.alloc_fragment([block_M, dim], accum_dtype)
             dq = T.alloc_fragment([block_N, dim], accum_dtype)
-            dv_cast = T.alloc_fragment([block_M, dim], dtype)
+            dv_cast = T.alloc_fragment([block_M, dv_], dtype)
             dk_cast = T.alloc_fragment([block_M, dim], dtype)
 
             T.copy(K[bz, by * block_M:(by + 1) * block_M, bx, :], K_shared)
@@ -201,10 +220,11 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
             loop_st = T.floordiv(by * block_M, block_N) if is_causal else 0
             loop_ed = T.ceildiv(seq_len, block_N)
             n_q = loop_ed - loop_st
-            for it in T.Pipelined(n_q * groups, num_stages=num_stages):
+            for it in T.Pipelined(n_q * gps, num_stages=num_stages):
                 # clamped into range: provably in bounds, so the Q / dO / lse / Delta tiles are LDS-DMA
                 # producers (division / modulo by a runtime count hides the range from the prover)
-                hq = T.max(T.min(bx * groups + it // n_q, heads - 1), 0)
+                hq0 = bx * groups + sp * gps if kv_split > 1 else bx * groups
+                hq = T.max(T.min(hq0 + it // n_q, heads - 1), 0)
                 k = T.max(T.min(loop_st + it % n_q, loop_ed - 1), 0)
                 T.copy(Q[bz, k * block_N:(k + 1) * block_N, hq, :], q)
                 T.clear(qkT)
@@ -229,26 +249,30 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
                     T.clear(dq)
                     T.gemm(dsT_shared, K_shared, dq, transpose_A=True)
                     T.atomic_add(dQ[bz, k * block_N:(k + 1) * block_N, hq, :], dq)
-            T.copy(dv, dv_cast)
-            T.copy(dk, dk_cast)
-            T.copy(dv_cast, dV[bz, by * block_M:(by + 1) * block_M, bx, :])
-            T.copy(dk_cast, dK[bz, by * block_M:(by + 1) * block_M, bx, :])
+            if kv_split > 1:
+                T.copy(dv, dV[sp, bz, by * block_M:(by + 1) * block_M, bx, :])
+                T.copy(dk, dK[sp, bz, by * block_M:(by + 1) * block_M, bx, :])
+            else:
+                T.copy(dv, dv_cast)
+                T.copy(dk, dk_cast)
+                T.copy(dv_cast, dV[bz, by * block_M:(by + 1) * block_M, bx, :])
+                T.copy(dk_cast, dK[bz, by * block_M:(by + 1) * block_M, bx, :])
 
     if dq_mode == "atomic":
 
         @T.prim_func
-        def flash_bwd(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
-                      dO: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
+        def flash_bwd(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(v_shape, dtype),
+                      dO: T.Tensor(o_shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
                       Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dQ: T.Tensor(shape, accum_dtype),
-                      dK: T.Tensor(kv_shape, dtype), dV: T.Tensor(kv_shape, dtype)):
+                      dK: T.Tensor(kv_shape, dtype), dV: T.Tensor(v_shape, dtype)):
             body(Q, K, V, dO, lse, Delta, dQ, dK, dV)
     else:
 
         @T.prim_func
-        def flash_bwd(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
-                      dO: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
-                      Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dK: T.Tensor(kv_shape, dtype),
-                      dV: T.Tensor(kv_shape, dtype)):
+        def flash_bwd(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(v_shape, dtype),
+                      dO: T.Tensor(o_shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
+                      Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dK: T.Tensor(kv_shape_o, out_dtype),
+                      dV: T.Tensor(v_shape_o, out_dtype)):
             body(Q, K, V, dO, lse, Delta, None, dK, dV)
 
     return flash_bwd
@@ -256,7 +280,7 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
 
 @tilelang.jit(out_idx=[6], pass_configs=FAST_MATH)
 def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=256, num_stages=2,
-                     dtype="float16", groups=1):
+                     dtype="float16", groups=1, dim_v=None):
     """dQ without atomics: one block per (query tile, head, batch) walks the KV tiles, recomputing
     P and dP (2 extra GEMMs) and accumulating dQ = dS K in registers -- on MI355X this is ~4x
     faster than fp32 atomics from every KV block (measured: docs/RESULTS.md)."""
@@ -264,17 +288,20 @@ def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N
     scale = sm_scale * LOG2E
     shape = [batch, seq_len, heads, dim]
     kv_shape = [batch, seq_len, heads // groups, dim]
+    dv_ = dim if dim_v is None else dim_v
+    v_shape = [batch, seq_len, heads // groups, dv_]
+    o_shape = [batch, seq_len, heads, dv_]
     accum_dtype = "float"
 
     @T.prim_func
-    def flash_bwd_dq(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
-                     dO: T.Tensor(shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
+    def flash_bwd_dq(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(v_shape, dtype),
+                     dO: T.Tensor(o_shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
                      Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dQ: T.Tensor(shape, dtype)):
         with T.Kernel(heads, T.ceildiv(seq_len, block_M), batch, threads=threads) as (bx, by, bz):
             q = T.alloc_shared([block_M, dim], dtype)
-            do = T.alloc_shared([block_M, dim], dtype)
+            do = T.alloc_shared([block_M, dv_], dtype)
             K_shared = T.alloc_shared([block_N, dim], dtype)
-            V_shared = T.alloc_shared([block_N, dim], dtype)
+            V_shared = T.alloc_shared([block_N, dv_], dtype)
             lse_f = T.alloc_fragment([block_M], accum_dtype)
             delta_f = T.alloc_fragment([block_M], accum_dtype)
             s = T.alloc_fragment([block_M, block_N], accum_dtype)
@@ -309,6 +336,23 @@ def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N
 BWD_DQ_MODE = "separate"  # or "atomic" (single kernel, fp32 atomics into dQ)
 
 
+def _tiles(D, Dv, kind):
+    """Tile sizes that keep each kernel's LDS (operand tiles + 2-stage rings) under 160 KiB: the
+    defaults are sized for D = Dv <= 128; wider heads (e.g. D=192 / Dv=128) halve the streamed tile."""
+    if D + Dv <= 256:
+        return {}
+    return {"fwd": dict(block_M=128), "bwd": dict(block_N=32), "dq": dict(block_N=32)}[kind]
+
+
+def _kv_split(B, S, HKV, G, block_M, target_wgs=512):
+    """Query-head split of the GQA dK/dV kernel so the grid reaches ~``target_wgs`` workgroups."""
+    wgs = B * HKV * -(-S // block_M)
+    split = 1
+    while split < G and wgs * split < target_wgs and G % (split * 2) == 0:
+        split *= 2
+    return split
+
+
 class _attention:
     """torch.autograd.Function built lazily (keeps this module importable without a GPU)."""
     fn = None
@@ -325,7 +369,8 @@ class _attention:
                     B, S, H, D = q.shape
                     G = H // k.shape[2]
                     dt = "bfloat16" if q.dtype == torch.bfloat16 else "float16"
-                    o, lse = flashattn_fwd(B, H, S, D, causal, dtype=dt, groups=G)(q, k, v)
+                    Dv = v.shape[-1]
+                    o, lse = flashattn_fwd(B, H, S, D, causal, dtype=dt, groups=G, dim_v=Dv, **_tiles(D, Dv, "fwd"))(q, k, v)
                     ctx.save_for_backward(q, k, v, o, lse)
                     ctx.causal = causal
                     return o
@@ -336,19 +381,31 @@ class _attention:
                     B, S, H, D = q.shape
                     G = H // k.shape[2]
                     dt = "bfloat16" if q.dtype == torch.bfloat16 else "float16"
+                    Dv = v.shape[-1]
                     do = do.contiguous()
-                    delta = flashattn_bwd_preprocess(B, H, S, D, dtype=dt)(o, do)
+                    delta = flashattn_bwd_preprocess(B, H, S, Dv, dtype=dt)(o, do)
                     dk = torch.empty_like(k)
                     dv = torch.empty_like(v)
+                    bw = _tiles(D, Dv, "bwd")
+                    split = _kv_split(B, S, k.shape[2], G, bw.get("block_M", 128))
                     if BWD_DQ_MODE == "atomic":
                         dq = torch.zeros(B, S, H, D, dtype=torch.float32, device=q.device)
-                        flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, groups=G)(q, k, v, do, lse, delta, dq, dk, dv)
+                        flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv, **_tiles(D, Dv, "bwd"))(q, k, v, do, lse, delta, dq, dk,
+                                                                                           dv)
                         return flashattn_bwd_postprocess(B, H, S, D, dtype=dt)(dq), dk, dv, None
                     # dK/dV kernel without dQ + an atomic-free dQ kernel (the two could run on
                     # separate streams; they only share read-only inputs)
-                    flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, dq_mode="none", groups=G)(q, k, v, do, lse, delta,
-                                                                                              dk, dv)
-                    dq = flashattn_bwd_dq(B, H, S, D, ctx.causal, dtype=dt, groups=G)(q, k, v, do, lse, delta)
+                    if split > 1:
+                        dkp = torch.empty((split, ) + tuple(k.shape), dtype=torch.float32, device=k.device)
+                        dvp = torch.empty((split, ) + tuple(v.shape), dtype=torch.float32, device=v.device)
+                        flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, dq_mode="none", groups=G, dim_v=Dv,
+                                      kv_split=split, **bw)(q, k, v, do, lse, delta, dkp, dvp)
+                        dk, dv = dkp.sum(0).to(k.dtype), dvp.sum(0).to(v.dtype)
+                    else:
+                        flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, dq_mode="none", groups=G, dim_v=Dv,
+                                      **bw)(q, k, v, do, lse, delta, dk, dv)
+                    dq = flashattn_bwd_dq(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv, **_tiles(D, Dv, "dq"))(q, k, v, do, lse,
+                                                                                          delta)
                     return dq, dk, dv, None
 
             cls.fn = Attn

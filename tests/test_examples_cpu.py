@@ -320,22 +320,23 @@ def test_gdn_chunked_matches_recurrence_cpu():
     torch.testing.assert_close(hf, h_ref, rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("causal", [False, True])
-def test_gqa_attention_fwd_bwd_cpu(causal):
+@pytest.mark.parametrize("causal,Dv", [(False, 64), (True, 64), (True, 32)])
+def test_gqa_attention_fwd_bwd_cpu(causal, Dv):
+    """GQA forward + backward; Dv != D is the example_gqa_bwd.py case (QK head dim != V head dim)."""
     import example_mha_bwd as m
     B, S, H, HKV, D = 1, 128, 4, 2, 64
     G = H // HKV
-    q, do = torch.randn(B, S, H, D).half(), torch.randn(B, S, H, D).half()
-    k, v = torch.randn(B, S, HKV, D).half(), torch.randn(B, S, HKV, D).half()
-    o, lse = _both(m.flashattn_fwd, B, H, S, D, causal, 64, 64, groups=G)(q, k, v)
+    q, do = torch.randn(B, S, H, D).half(), torch.randn(B, S, H, Dv).half()
+    k, v = torch.randn(B, S, HKV, D).half(), torch.randn(B, S, HKV, Dv).half()
+    o, lse = _both(m.flashattn_fwd, B, H, S, D, causal, 64, 64, groups=G, dim_v=Dv)(q, k, v)
     qf, kf, vf = [t.float().requires_grad_() for t in (q, k, v)]
     ro = m.ref_program(qf, kf, vf, causal)
     ro.backward(do.float())
     torch.testing.assert_close(o.float(), ro.detach(), rtol=1e-2, atol=1e-2)
-    delta = _both(m.flashattn_bwd_preprocess, B, H, S, D)(o, do)
-    dq = _both(m.flashattn_bwd_dq, B, H, S, D, causal, 64, 64, 256, groups=G)(q, k, v, do, lse, delta)
+    delta = _both(m.flashattn_bwd_preprocess, B, H, S, Dv)(o, do)
+    dq = _both(m.flashattn_bwd_dq, B, H, S, D, causal, 64, 64, 256, groups=G, dim_v=Dv)(q, k, v, do, lse, delta)
     dk, dv = torch.empty_like(k), torch.empty_like(v)
-    f = m.flashattn_bwd.get_tir(B, H, S, D, causal, 64, 64, 256, dq_mode="none", groups=G)
+    f = m.flashattn_bwd.get_tir(B, H, S, D, causal, 64, 64, 256, dq_mode="none", groups=G, dim_v=Dv)
     tilelang.compile(f, target="hip")
     tilelang.compile(f, target="cpu")(q, k, v, do, lse, delta, dk, dv)
     for a, r in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
@@ -524,3 +525,23 @@ def test_gqa_fwd_bshd_cpu():
     q = torch.randn(1, 128, 4, 64).bfloat16()
     kk, v = (torch.randn(1, 128, 2, 64).bfloat16() for _ in range(2))
     torch.testing.assert_close(k(q, kk, v).float(), ref_program(q, kk, v, True, 2).float(), rtol=2e-2, atol=2e-2)
+
+
+def test_gqa_bwd_kv_split_cpu():
+    """GQA dK/dV with the query heads of each KV head split over 2 workgroups (fp32 partials)."""
+    import example_mha_bwd as m
+    B, S, H, HKV, D = 1, 128, 4, 1, 64
+    G = H // HKV
+    q, do = torch.randn(B, S, H, D).half(), torch.randn(B, S, H, D).half()
+    k, v = torch.randn(B, S, HKV, D).half(), torch.randn(B, S, HKV, D).half()
+    o, lse = _both(m.flashattn_fwd, B, H, S, D, True, 64, 64, groups=G)(q, k, v)
+    qf, kf, vf = [t.float().requires_grad_() for t in (q, k, v)]
+    m.ref_program(qf, kf, vf, True).backward(do.float())
+    delta = _both(m.flashattn_bwd_preprocess, B, H, S, D)(o, do)
+    dkp = torch.empty(2, B, S, HKV, D)
+    dvp = torch.empty(2, B, S, HKV, D)
+    f = m.flashattn_bwd.get_tir(B, H, S, D, True, 64, 64, 256, dq_mode="none", groups=G, kv_split=2)
+    tilelang.compile(f, target="hip")
+    tilelang.compile(f, target="cpu")(q, k, v, do, lse, delta, dkp, dvp)
+    torch.testing.assert_close(dkp.sum(0), kf.grad, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(dvp.sum(0), vf.grad, rtol=1e-2, atol=1e-2)

@@ -412,3 +412,9 @@ def test_mha_fwd_bhsd(causal):
 def test_gqa_fwd_bshd():
     import example_gqa_fwd_bshd as m
     m.main(1, 32, 1024, 128, True, 8)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_gqa_bwd_qk192_v128(causal):
+    import example_gqa_bwd as m
+    m.main(1, 16, 512, 192, 128, 8, causal)
