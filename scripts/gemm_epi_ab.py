@@ -7,7 +7,7 @@ import torch
 import tilelang
 from tilelang.profiler import do_bench
 
-sys.path.insert(0, "examples/gemm")
+sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), "..", "examples", "gemm"))
 from example_gemm import matmul  # noqa: E402
 
 for (M, N, K) in [(4096, 4096, 4096), (8192, 8192, 4096), (8192, 8192, 8192)]:

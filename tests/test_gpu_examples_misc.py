@@ -418,3 +418,9 @@ def test_gqa_fwd_bshd():
 def test_gqa_bwd_qk192_v128(causal):
     import example_gqa_bwd as m
     m.main(1, 16, 512, 192, 128, 8, causal)
+
+
+def test_mha_sink_fwd_bhsd():
+    import example_mha_sink_fwd_bhsd as m
+    m.main(1, 8, 512, 512, 128, None)
+    m.main(1, 8, 512, 512, 128, 128)
