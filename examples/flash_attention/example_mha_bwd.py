@@ -297,7 +297,10 @@ def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N
     def flash_bwd_dq(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(v_shape, dtype),
                      dO: T.Tensor(o_shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
                      Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dQ: T.Tensor(shape, dtype)):
-        with T.Kernel(heads, T.ceildiv(seq_len, block_M), batch, threads=threads) as (bx, by, bz):
+        n_t = (seq_len + block_M - 1) // block_M
+        with T.Kernel(heads, n_t, batch, threads=threads) as (bx, by_raw, bz):
+            # causal: the longest rows of dQ (last query tiles) are dispatched first
+            by = (n_t - 1 - by_raw) if is_causal else by_raw
             q = T.alloc_shared([block_M, dim], dtype)
             do = T.alloc_shared([block_M, dv_], dtype)
             K_shared = T.alloc_shared([block_N, dim], dtype)
