@@ -7,6 +7,14 @@ import tilelang.language as T
 from tilelang.engine import callback
 
 
+@pytest.fixture(autouse=True)
+def _fresh_cache(tmp_path, monkeypatch):
+    """Hooks run at compile time: a kernel found in the on-disk cache (same program and hook
+    fingerprint from an earlier run) would skip them, so every test compiles into an empty cache."""
+    from tilelang import env
+    monkeypatch.setattr(env, "TILELANG_CACHE_DIR", str(tmp_path))
+
+
 def _prog(n=256):
 
     @T.prim_func

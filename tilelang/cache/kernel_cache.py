@@ -121,7 +121,9 @@ def save(key: str, kernel) -> bool:
                 "grid_exprs": [str(g) for g in dk.grid], "cooperative": bool(getattr(dk, "cooperative", False)),
                 "params": [{"kind": p["kind"], "name": p["name"], "dtype": str(p.get("dtype", ""))}
                            for p in dk.params],
-                "specs": _json_specs(specs), "nsyms": nsyms, "grid": grid})
+                "specs": _json_specs(specs), "nsyms": nsyms, "grid": grid,
+                "narrow_index": sorted(getattr(dk, "narrow_index", ()) or ()),
+                "layout_info": dict(getattr(dk, "layout_info", {}) or {})})
         (tmp / "meta.json").write_text(json.dumps(meta))
         try:
             os.replace(tmp, dest)
@@ -151,6 +153,8 @@ def load(key: str):
         src = (d / f"kernel_{i}.hip").read_text()
         dk = DeviceKernel(src, k["name"], k["grid_exprs"], k["block"], k["lds_bytes"], k["params"])
         dk.cooperative = k["cooperative"]
+        dk.narrow_index = set(k.get("narrow_index", ()))  # int32-addressed params (launcher overflow check)
+        dk.layout_info = dict(k.get("layout_info", {}))
         kernels.append(dk)
         path = d / f"code_{i}.{'so' if meta['is_cpu'] else 'hsaco'}"
         code.append(str(path) if meta["is_cpu"] else path.read_bytes())
