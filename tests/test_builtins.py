@@ -107,3 +107,63 @@ def test_no_barrier_inside_thread_guard():
         depth += line.count("{") - line.count("}")
         while guard_depths and depth <= guard_depths[-1]:
             guard_depths.pop()
+
+
+def test_cross_wave_hazard_in_divergent_branch_is_refused():
+    """A thread-dependent branch in which one wave writes LDS that another wave then reads
+    cannot be synchronised (a barrier inside would deadlock): lowering must refuse it instead
+    of emitting a silent race."""
+    import pytest
+    import tilelang
+    import tilelang.language as T
+
+    @T.prim_func
+    def bad(A: T.Tensor((256, ), "float32"), B: T.Tensor((256, ), "float32")):
+        with T.Kernel(1, threads=256) as bx:
+            S = T.alloc_shared((256, ), "float32")
+            tx = T.get_thread_binding()
+            if tx < 128:
+                S[tx] = A[tx]
+                B[tx] = S[tx + 64]  # written by another wave of the same branch
+    with pytest.raises(RuntimeError, match="thread-dependent branch"):
+        tilelang.lower(bad, target="hip")
+
+
+def test_own_element_reuse_in_divergent_branch_is_allowed():
+    import tilelang
+    import tilelang.language as T
+
+    @T.prim_func
+    def ok(A: T.Tensor((256, ), "float32"), B: T.Tensor((256, ), "float32")):
+        with T.Kernel(1, threads=256) as bx:
+            S = T.alloc_shared((256, ), "float32")
+            tx = T.get_thread_binding()
+            if tx < 128:
+                S[tx] = A[tx] * 2.0
+                B[tx] = S[tx] + 1.0  # the thread's own element
+    src = tilelang.lower(ok, target="hip").kernel_source
+    assert "sync_threads" not in src.split("if")[-1]
+
+
+def test_register_set_under_thread_guard_is_not_uniform():
+    """``if tid == 0: flag = 1`` makes ``flag`` per-thread: a barrier under ``if flag`` must be
+    refused as divergent (it would deadlock), not taken as block-uniform."""
+    import pytest
+    import tilelang
+    import tilelang.language as T
+
+    @T.prim_func
+    def bad(A: T.Tensor((256, ), "float32"), B: T.Tensor((256, ), "float32")):
+        with T.Kernel(1, threads=256) as bx:
+            S = T.alloc_shared((256, ), "float32")
+            flag = T.alloc_var("int32")
+            tx = T.get_thread_binding()
+            flag = 0
+            if tx == 0:
+                flag = 1
+            if flag == 1:
+                S[tx] = A[tx]
+                T.sync_threads()
+                B[tx] = S[255 - tx]
+    with pytest.raises(RuntimeError):
+        tilelang.lower(bad, target="hip")

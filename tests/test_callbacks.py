@@ -78,3 +78,27 @@ def test_cpu_target_unaffected():
         torch.testing.assert_close(k(a), a * 2)
     finally:
         callback.unregister()
+
+
+def test_hooks_with_same_body_different_closures_get_different_keys():
+    """A hook built in a loop (same bytecode, different captured values) must not be served
+    the kernel compiled under its sibling (hook_fingerprint hashed only co_code)."""
+    srcs = []
+    for tag in ("// variant-a", "// variant-b"):
+        callback.register_hip_postproc(lambda code, target: tag + "\n" + code)
+        try:
+            srcs.append(tilelang.compile(_prog(2048), out_idx=[1], target="hip").get_kernel_source())
+        finally:
+            callback.unregister()
+    assert srcs[0].startswith("// variant-a") and srcs[1].startswith("// variant-b")
+
+
+def test_compiler_fingerprint_covers_native_core():
+    from tilelang.cache import kernel_cache
+    import hashlib
+    from pathlib import Path
+    import tilelang as tl
+    sos = sorted(Path(tl.__file__).parent.glob("_tl_*.so"))
+    assert sos, "native extensions must be built in-tree"
+    fp = kernel_cache.compiler_fingerprint()
+    assert isinstance(fp, str) and len(fp) == 64

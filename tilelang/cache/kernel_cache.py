@@ -9,7 +9,9 @@ size and LDS bytes.  Key = sha256 of
     that lower differently never share a key — ``ir/printer.py``),
   * target, pass configs, ``out_idx``, compile flags,
   * a fingerprint of the compiler itself (every ``tilelang/**/*.py`` that lowers/generates code, the
-    ``tl/*.h`` device headers and the hipcc version), so editing the compiler invalidates entries.
+    ``tl/*.h`` device headers, the built native core/runtime extensions and the hipcc version), so
+    editing or rebuilding the compiler invalidates entries,
+  * the registered compile hooks, closures and referenced globals included (``hook_fingerprint``).
 
 Layout: ``$TILELANG_CACHE_DIR/kernels/<key>/{meta.json, kernel_<i>.hip, code_<i>.{hsaco,so}}``,
 written into a temp directory and renamed into place (concurrent writers — autotuner threads,
@@ -48,7 +50,13 @@ def compiler_fingerprint() -> str:
                 for d in _COMPILER_DIRS:
                     files += sorted((root / d).rglob("*.py"))
                 files += sorted((INCLUDE_DIR / "tl").rglob("*.h"))
+                files += [root / "_native.py", root / "__init__.py"]
+                # the native compiler core (reduce_owners, plan_arena, fragment inverses) and the
+                # runtime: a rebuilt extension must not be served entries lowered by the old one
+                files += sorted(root.glob("_tl_*.so"))
                 for f in files:
+                    if not f.exists():
+                        continue
                     h.update(str(f.relative_to(root.parent) if root.parent in f.parents else f.name).encode())
                     h.update(f.read_bytes())
                 _FP = h.hexdigest()

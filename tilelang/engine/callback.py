@@ -80,14 +80,52 @@ def hook_fingerprint() -> str:
         return ""
     h = hashlib.sha256()
     for name in sorted(_HOOKS):
-        f = _HOOKS[name]
-        code = getattr(f, "__code__", None)
         h.update(name.encode())
-        h.update(getattr(f, "__qualname__", repr(f)).encode())
-        if code is not None:
-            h.update(code.co_code)
-            h.update(repr(code.co_consts).encode())
+        _hash_callable(h, _HOOKS[name], depth=0)
     return h.hexdigest()
+
+
+def _hash_value(h, v, depth):
+    """Hash what a hook can read besides its bytecode: closure cells, defaults and the module
+    globals it names.  Two hooks with one body but different captured values (a lambda built in
+    a loop over variants) must not share a cache key."""
+    if isinstance(v, (str, bytes, int, float, bool, type(None))):
+        h.update(repr(v).encode())
+    elif isinstance(v, (list, tuple, set, frozenset)):
+        h.update(type(v).__name__.encode())
+        for x in (sorted(v, key=repr) if isinstance(v, (set, frozenset)) else v):
+            _hash_value(h, x, depth)
+    elif isinstance(v, dict):
+        for k in sorted(v, key=repr):
+            _hash_value(h, k, depth)
+            _hash_value(h, v[k], depth)
+    elif callable(v) and hasattr(v, "__code__") and depth < 3:
+        _hash_callable(h, v, depth + 1)
+    else:
+        # objects without a stable value: their type only (a mutable object is the user's business)
+        h.update(type(v).__qualname__.encode())
+
+
+def _hash_callable(h, f, depth):
+    code = getattr(f, "__code__", None)
+    h.update(getattr(f, "__qualname__", repr(f)).encode())
+    if code is None:
+        h.update(repr(f).encode())
+        return
+    h.update(code.co_code)
+    h.update(repr(code.co_consts).encode())
+    for cell in (getattr(f, "__closure__", None) or ()):
+        try:
+            _hash_value(h, cell.cell_contents, depth)
+        except ValueError:  # empty cell
+            h.update(b"<empty>")
+    _hash_value(h, getattr(f, "__defaults__", None), depth)
+    _hash_value(h, getattr(f, "__kwdefaults__", None), depth)
+    g = getattr(f, "__globals__", {})
+    for n in code.co_names:
+        if n in g and not isinstance(g[n], type(hashlib)):
+            h.update(n.encode())
+            _hash_value(h, g[n], depth)
 
 
 def apply_hip_postproc(code: str, target) -> str:

@@ -15,6 +15,8 @@ Sharding rules (kept identical so programs are portable):
 """
 from __future__ import annotations
 
+import threading
+
 import math
 from enum import Enum
 from typing import Any, Optional, Sequence, Tuple
@@ -335,7 +337,36 @@ class LazyTrace:
         self.ptr_buffers = {}  # PtrParam -> Buffer
 
 
-LAZY_STACK = []
+class _ThreadLocalStack:
+    """A per-thread list: ``lazy_jit.par_compile`` traces kernels in a thread pool, and one
+    thread's ``T.empty`` outputs / ``T.make_tensor`` bindings must never land on another's trace."""
+
+    def __init__(self):
+        self._tls = threading.local()
+
+    def _list(self):
+        lst = getattr(self._tls, "stack", None)
+        if lst is None:
+            lst = self._tls.stack = []
+        return lst
+
+    def append(self, x):
+        self._list().append(x)
+
+    def pop(self):
+        return self._list().pop()
+
+    def __getitem__(self, i):
+        return self._list()[i]
+
+    def __len__(self):
+        return len(self._list())
+
+    def __bool__(self):
+        return bool(self._list())
+
+
+LAZY_STACK = _ThreadLocalStack()
 
 
 def make_tensor(ptr, shape, dtype="float32", strides=None):

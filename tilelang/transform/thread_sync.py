@@ -113,6 +113,8 @@ class ThreadSync:
     def __init__(self):
         self.managed: Set = set()
         self.tvars = ()
+        self.nthreads = 0
+        self.loop_ranges = {}  # enclosing constant-bounded loops (for the divergent-branch proof)
         self.uniform = set()
 
     def needs(self, st: _State, r, w) -> bool:
@@ -166,6 +168,12 @@ class ThreadSync:
                             managed_here.add(b)
             saved = set(self.managed)
             self.managed |= managed_here
+            saved_ranges = self.loop_ranges
+            if isinstance(c, S.ForStmt):
+                from ..ir.expr import as_int
+                lo, ext = as_int(c.min), as_int(c.extent)
+                if lo is not None and ext is not None:
+                    self.loop_ranges = {**self.loop_ranges, c.var: range(lo, lo + ext)}
             # hazard with what precedes the loop: barrier in front
             r0, w0 = self.first_access(body)
             if self.needs(st, r0, w0):
@@ -178,6 +186,7 @@ class ThreadSync:
                 nb = S.SeqStmt([_sync(), nb])
                 nb, st_end = self.scan(nb, _State())
             self.managed = saved
+            self.loop_ranges = saved_ranges
             if isinstance(c, S.ForStmt):
                 nc = S.ForStmt(c.var, c.min, c.extent, c.kind, nb, c.annotations)
             else:
@@ -200,8 +209,11 @@ class ThreadSync:
             if _thread_dependent(c.cond, self.tvars, self.uniform):
                 # divergent branch: a barrier inside would deadlock the workgroup.  Accesses in
                 # it are ordered against the surroundings by the barrier in front (above) and
-                # by the next conflicting access after it; inside, a thread only reorders its
-                # own accesses, which needs no barrier.
+                # by the next conflicting access after it.  Inside, a hazard needs no barrier
+                # only when a thread reads back exactly the elements it wrote itself (same
+                # index expression); anything else crosses threads (possibly waves) and is
+                # refused rather than emitted as a silent race.
+                _check_divergent_hazards(c, self.managed, self.nthreads, self.tvars, self.loop_ranges)
                 out.append(c)
                 return c, _State(st.reads | r0, st.writes | w0)
             # block-uniform condition: scan the branches for internal hazards
@@ -212,6 +224,9 @@ class ThreadSync:
             return nc, st_t.merge(st_e)
         if isinstance(c, S.KernelStmt):
             self.tvars = tuple(c.thread_vars or ())
+            self.nthreads = 1
+            for n in (c.threads or [1]):
+                self.nthreads *= int(n)
             self.uniform = _uniform_registers(c, self.tvars)
             nb, st2 = self.scan(c.body, _State())
             k = S.KernelStmt(c.grid, c.threads, c.block_vars, c.thread_vars, nb, c.is_cpu, c.prelude)
@@ -228,6 +243,208 @@ class ThreadSync:
         out.append(c)
         st = _State(st.reads | r, st.writes | w)
         return c, st
+
+
+def _indexed_access(s, managed):
+    """[(buffer, 'r'|'w', [index exprs] | None, width)] of the LDS accesses of one leaf; None =
+    an access whose extent is unknown (a pointer handed to a device call)."""
+    out = []
+
+    def reads_of(e):
+        if not isinstance(e, PrimExpr):
+            return
+        for n in post_order(e):
+            if isinstance(n, BufferLoad) and _shared(n.buffer):
+                out.append((n.buffer, "r", list(n.indices), 1))
+            elif isinstance(n, L.BufferPtr) and _shared(n.buffer):
+                out.append((n.buffer, "r", None, 0))
+
+    if isinstance(s, L.CallStmt):
+        if s.name in ("tl::glds16", "tl::glds4", "tl::buffer_lds16", "tl::glds16_nt"):
+            return []
+        writes = s.name.startswith("tl::mesh") or s.name.startswith("tl::comm")  # as _stmt_access
+        for a in s.args:
+            if isinstance(a, L.BufferPtr) and _shared(a.buffer):
+                out.append((a.buffer, "r", None, 0))
+                if writes:
+                    out.append((a.buffer, "w", None, 0))
+            else:
+                reads_of(a)
+    elif isinstance(s, S.StoreStmt):
+        for i in s.indices:
+            reads_of(i)
+        reads_of(s.value)
+        if _shared(s.buffer):
+            out.append((s.buffer, "w", list(s.indices), 1))
+    elif isinstance(s, L.VecStoreStmt):
+        reads_of(s.index)
+        for v in s.values:
+            reads_of(v)
+        if _shared(s.buffer):
+            out.append((s.buffer, "w", [s.index], len(s.values)))
+    elif isinstance(s, L.VecLoadStmt):
+        if _shared(s.src):
+            out.append((s.src, "r", [s.src_index], s.n))
+    elif isinstance(s, L.CopyBytesStmt):
+        if _shared(s.src):
+            out.append((s.src, "r", [s.src_index], max(1, s.nbytes // s.src.dtype.bytes)))
+        if _shared(s.dst):
+            out.append((s.dst, "w", [s.dst_index], max(1, s.nbytes // s.dst.dtype.bytes)))
+    elif isinstance(s, S.EvaluateStmt):
+        reads_of(s.expr)
+        from ..ir.expr import Call
+        if isinstance(s.expr, Call) and s.expr.op.startswith("tl.atomic"):
+            a0 = s.expr.args[0]
+            if isinstance(a0, BufferLoad) and _shared(a0.buffer):
+                out.append((a0.buffer, "w", list(a0.indices), 1))
+    elif isinstance(s, (S.LetStmt, S.AssertStmt)):
+        reads_of(s.value if isinstance(s, S.LetStmt) else s.cond)
+    return [a for a in out if a[0] not in managed]
+
+
+_MAX_ENUM = 1 << 16  # threads x loop-iteration points enumerated by the ownership proof
+
+
+def _loop_ranges(body):
+    """var -> range of the constant-bounded loops inside ``body``."""
+    from ..ir.expr import as_int
+    out = {}
+    for x in S.walk(body) if body is not None else ():
+        if isinstance(x, S.ForStmt):
+            lo, ext = as_int(x.min), as_int(x.extent)
+            if lo is not None and ext is not None:
+                out[x.var] = range(lo, lo + ext)
+    return out
+
+
+def _thread_env(t, tvars):
+    """Values of the thread-index variables for flat thread id ``t`` (None if the expression
+    would need a variable this model does not know)."""
+    env = {}
+    for v in tvars:
+        env[v] = t
+    return env
+
+
+def _elements_by_thread(accs, cond, nthreads, tvars, ranges):
+    """{(kind, element): {threads}} over every guard-satisfying thread and loop point, or None
+    when an index cannot be evaluated (unknown variable, register load, pointer access)."""
+    import itertools
+    from ..ir.expr import EvalError, Var, evaluate, free_vars
+    names = {"tid": lambda t: t, "tid_": lambda t: t, "tx": lambda t: t, "lane": lambda t: t % 64,
+             "lane_": lambda t: t % 64, "wave": lambda t: t // 64, "wave_": lambda t: t // 64}
+    out = {}
+    for kind, idx, width in accs:
+        if idx is None or any(not isinstance(i, PrimExpr) for i in idx):
+            return None
+        fv = set()
+        for i in idx:
+            fv |= set(free_vars(i))
+        if any(isinstance(n, BufferLoad) for i in idx for n in post_order(i)):
+            return None
+        loops = [v for v in fv if v in ranges]
+        thread_like = [v for v in fv if v in tvars or v.name in names]
+        if len(loops) + len(thread_like) != len(fv):
+            return None  # a variable of unknown range (outer loop, block index): not provable here
+        pts = 1
+        for v in loops:
+            pts *= len(ranges[v])
+        if pts * nthreads > _MAX_ENUM:
+            return None
+        for t in range(nthreads):
+            env = {v: (t if v in tvars else names[v.name](t)) for v in thread_like}
+            try:
+                cenv = {v: (t if v in tvars else names[v.name](t)) for v in free_vars(cond)
+                        if v in tvars or v.name in names} if cond is not None else {}
+                if cond is not None and not evaluate(cond, cenv):
+                    continue
+            except EvalError:
+                pass  # a condition on other values: every thread may take the branch
+            for combo in itertools.product(*[ranges[v] for v in loops]):
+                e2 = dict(env)
+                e2.update(zip(loops, combo))
+                try:
+                    el = tuple(evaluate(i, e2) for i in idx)
+                except EvalError:
+                    return None
+                for w in range(width):
+                    key = (kind, el[:-1] + (el[-1] + w, ))
+                    out.setdefault(key, set()).add(t)
+    return out
+
+
+def _owned_per_instance(b, accs, cond, nthreads, tvars, inner, outer):
+    """True if, for every instance of the enclosing loops (barriers separate instances: the
+    scan puts one in front of a loop-carried hazard), no element of ``b`` is written by one
+    thread and read by another inside the branch; raises on a proven cross-thread pair;
+    False if not provable (unknown index variables / too many points)."""
+    import itertools
+    from ..ir.expr import free_vars
+    used = set()
+    for _, idx, _ in accs:
+        for i in (idx or ()):
+            used |= set(free_vars(i))
+    outer_vars = [v for v in used if v in outer and v not in inner]
+    n_inst = 1
+    for v in outer_vars:
+        n_inst *= len(outer[v])
+    if n_inst > 64:
+        return False
+    for combo in itertools.product(*[outer[v] for v in outer_vars]):
+        fixed = dict(zip(outer_vars, combo))
+        from ..ir.expr import substitute
+        accs_i = [(k, [substitute(i, fixed) for i in idx] if idx is not None else None, w) for k, idx, w in accs]
+        owners = _elements_by_thread(accs_i, cond, nthreads, tvars, inner)
+        if owners is None:
+            return False
+        for (kind, el), ts in owners.items():
+            if kind != "w":
+                continue
+            readers = owners.get(("r", el), set())
+            if readers and len(ts | readers) > 1:
+                raise RuntimeError(
+                    f"LDS hazard inside a thread-dependent branch (if {cond}): element {list(el)} of "
+                    f"'{b.name}' is written by thread(s) {sorted(ts)[:4]} and read by thread(s) "
+                    f"{sorted(readers)[:4]}; a barrier cannot be placed inside the branch. Move the "
+                    f"shared-memory exchange out of the branch.")
+    return True
+
+
+def _check_divergent_hazards(c: "S.IfStmt", managed, nthreads=0, tvars=(), outer_ranges=None):
+    """Raise on an LDS hazard between accesses INSIDE a thread-dependent branch that crosses
+    threads: a barrier cannot be placed there (it would deadlock), and leaving it out would be a
+    race.  A write and a read (either order) of one element by two different threads is such a
+    hazard; a thread re-reading elements it wrote itself is ordered by program order.  Proof by
+    enumeration of the threads that take the branch and of the branch's constant-bounded loops;
+    anything not provable that way must at least use the same index expression for the write
+    and the read."""
+    for body in (c.then_body, c.else_body):
+        if body is None:
+            continue
+        from ..ir.expr import substitute
+        by_buf, lets = {}, {}
+        for x in _leaves(body):
+            if isinstance(x, S.LetStmt):
+                lets[x.var] = substitute(x.value, lets) if lets else x.value
+            for b, kind, idx, width in _indexed_access(x, managed):
+                if idx is not None and lets:
+                    idx = [substitute(i, lets) for i in idx]
+                by_buf.setdefault(b, []).append((kind, idx, width))
+        inner = _loop_ranges(body)
+        for b, accs in by_buf.items():
+            kinds = {k for k, _, _ in accs}
+            if kinds != {"r", "w"}:
+                continue
+            if nthreads and _owned_per_instance(b, accs, c.cond, nthreads, tvars, inner, outer_ranges or {}):
+                continue
+            keys_w = {repr(i) for k, i, _ in accs if k == "w"}
+            keys_r = {repr(i) for k, i, _ in accs if k == "r"}
+            if any(i is None for _, i, _ in accs) or keys_w != keys_r or len(keys_w) != 1:
+                raise RuntimeError(
+                    f"LDS hazard inside a thread-dependent branch (if {c.cond}): buffer '{b.name}' is "
+                    f"written and read at elements that cannot be shown to belong to one thread; a "
+                    f"barrier cannot be placed inside the branch. Move the shared-memory exchange out "
+                    f"of the branch.")
 
 
 def _leaves(s):
@@ -276,20 +493,43 @@ def _thread_dependent(e, tvars, uniform=()) -> bool:
     return False
 
 
+def _register_stores(s, guards, out):
+    """(store, enclosing if-conditions / loop bounds) of every register store under ``s``."""
+    if s is None:
+        return
+    if isinstance(s, S.StoreStmt):
+        if getattr(s.buffer, "scope", "") not in ("global", "shared"):
+            out.setdefault(s.buffer, []).append((s, guards))
+    elif isinstance(s, S.SeqStmt):
+        for c in s.stmts:
+            _register_stores(c, guards, out)
+    elif isinstance(s, S.IfStmt):
+        g = guards + (s.cond,)
+        _register_stores(s.then_body, g, out)
+        _register_stores(s.else_body, g, out)
+    elif isinstance(s, S.ForStmt):
+        _register_stores(s.body, guards + (s.min, s.extent), out)
+    elif isinstance(s, S.WhileStmt):
+        _register_stores(s.body, guards + (s.cond,), out)
+    elif isinstance(s, (S.KernelStmt, S.AttrStmt)) or hasattr(s, "body"):
+        _register_stores(getattr(s, "body", None), guards, out)
+
+
 def _uniform_registers(k: S.KernelStmt, tvars) -> set:
-    """Register buffers (``T.alloc_var`` / locals) whose every store is block-uniform (fixpoint)."""
+    """Register buffers (``T.alloc_var`` / locals) whose every store is block-uniform (fixpoint).
+    A store counts as uniform only if its value, its indices AND every condition / loop bound
+    it sits under are: ``if tid == 0: flag = 1`` leaves ``flag`` thread-dependent."""
     stores = {}
-    for x in S.walk(k):
-        if isinstance(x, S.StoreStmt) and getattr(x.buffer, "scope", "") not in ("global", "shared"):
-            stores.setdefault(x.buffer, []).append(x)
+    _register_stores(k.body, (), stores)
     uniform = set(stores)
     changed = True
     while changed:
         changed = False
         for b in list(uniform):
-            for st in stores[b]:
+            for st, guards in stores[b]:
                 if _thread_dependent(st.value, tvars, uniform) or \
-                        any(_thread_dependent(i, tvars, uniform) for i in st.indices):
+                        any(_thread_dependent(i, tvars, uniform) for i in st.indices) or \
+                        any(_thread_dependent(g, tvars, uniform) for g in guards):
                     uniform.discard(b)
                     changed = True
                     break
