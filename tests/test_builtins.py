@@ -57,8 +57,74 @@ def grid_sync_kernel(nb, threads=256):
 
 def test_grid_sync_codegen():
     k = tilelang.compile(grid_sync_kernel(64), target="hip")
-    assert "tl::sync_grid()" in k.get_kernel_source()
+    src = k.get_kernel_source()
+    # per-launch barrier workspace + device error word, no module-global barrier state
+    assert "tl::sync_grid(tl_gsync_ws" in src and "tl_dev_err" in src
     assert k.artifact.kernels[0].cooperative
+    names = [p["name"] for p in k.artifact.kernels[0].params]
+    assert names[-2:] == ["tl_gsync_ws", "tl_dev_err"]
+
+
+def grid_sync_skip_kernel(nb, threads=256):
+    """Block 0 never reaches the barrier: every other block must time out, not hang."""
+
+    @T.prim_func
+    def main(X: T.Tensor((nb, ), "int32")):
+        with T.Kernel(nb, threads=threads) as bx:
+            if bx > 0:
+                T.sync_grid()
+            for z in T.Parallel(1):
+                X[bx + z] = bx + 1
+
+    return main
+
+
+def test_grid_sync_skip_compiles():
+    k = tilelang.compile(grid_sync_skip_kernel(64), target="hip",
+                         compile_flags=["-DTL_GRID_SYNC_TIMEOUT_TICKS=2000000"])
+    assert len(k.code[0]) > 0
+
+
+@pytest.mark.gpu
+def test_grid_sync_timeout_raises():
+    """A forced grid-barrier timeout finishes the kernel and raises GridSyncTimeout at the next
+    check point (and only once); a healthy launch afterwards works."""
+    from tilelang.runtime import errors
+    nb = 64
+    k = tilelang.compile(grid_sync_skip_kernel(nb), target="hip",
+                         compile_flags=["-DTL_GRID_SYNC_TIMEOUT_TICKS=2000000"])  # 20 ms
+    x = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    k(x)
+    with pytest.raises(errors.GridSyncTimeout):
+        errors.check()
+    errors.check()  # raised once
+    good = tilelang.compile(grid_sync_kernel(nb), target="hip")
+    y = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    good(x, y)
+    errors.check()
+    assert torch.equal(y, ((torch.arange(nb, device="cuda") + 1) % nb + 1).to(torch.int32))
+
+
+@pytest.mark.gpu
+def test_grid_sync_concurrent_streams():
+    """Two launches of one grid-barrier kernel on two streams: per-launch barrier state."""
+    nb = 64
+    k = tilelang.compile(grid_sync_kernel(nb), target="hip")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for _ in range(5):
+        for s in (s1, s2):
+            with torch.cuda.stream(s):
+                x = torch.zeros(nb, dtype=torch.int32, device="cuda")
+                y = torch.zeros(nb, dtype=torch.int32, device="cuda")
+                k(x, y)
+                outs.append(y)
+    torch.cuda.synchronize()
+    from tilelang.runtime import errors
+    errors.check()
+    exp = ((torch.arange(nb, device="cuda") + 1) % nb + 1).to(torch.int32)
+    for y in outs:
+        assert torch.equal(y, exp)
 
 
 @pytest.mark.gpu

@@ -248,7 +248,14 @@ class CodeGen:
         if op == "tl.sync_warp":
             return "tl::sync_warp()"
         if op == "tl.sync_grid":
-            return "tl::sync_grid()"
+            if self.is_cpu:
+                return "tl::sync_grid()"
+            ex = {x["name"]: x for x in self.kernel.attrs.get("extra_params", [])}
+            if "tl_gsync_ws" not in ex:
+                raise CodeGenError("T.sync_grid in a kernel without its grid-barrier workspace parameters")
+            ws = self.name_of(ex["tl_gsync_ws"]["var"], "tl_gsync_ws")
+            err = self.name_of(ex["tl_dev_err"]["var"], "tl_dev_err")
+            return f"tl::sync_grid({ws}, {err})"
         if op == "tl.setprio":
             return "(void)0" if self.is_cpu else f"__builtin_amdgcn_s_setprio({int(args[0].value)})"
         raise CodeGenError(f"unknown intrinsic {op}")

@@ -102,30 +102,43 @@ TL_DEVICE void sync_warp() {
 
 // Grid-wide barrier (reference T.sync_grid / sync_global).  Needs every workgroup of the grid
 // resident at once: the launcher uses hipModuleLaunchCooperativeKernel for kernels that call it,
-// which refuses grids larger than the device can hold.  Sense-reversing counter barrier with
-// agent-scope release/acquire (MI355X guide, Guideline 16: per-XCD L2s are not coherent):
-// lane 0 of every workgroup publishes with a release fence, arrives, and the last arriver resets
-// the count and bumps the generation the others poll (relaxed loads + s_sleep, bounded).
-__device__ unsigned int tl_grid_bar_count = 0;
-__device__ unsigned int tl_grid_bar_gen = 0;
-TL_DEVICE void sync_grid() {
+// which refuses grids larger than the device can hold.  Counter barrier with agent-scope
+// release/acquire (MI355X guide, Guideline 16: per-XCD L2s are not coherent): lane 0 of every
+// workgroup publishes with a release fence, arrives, and the last arriver resets the count and
+// bumps the generation the others poll (relaxed loads + s_sleep).
+// State is PER LAUNCH: `ws` = {count, generation, poisoned} in a zeroed workspace the launcher
+// allocates for each launch on its stream (two concurrent launches of one kernel never share a
+// barrier).  The wait is bounded by wall clock (s_memrealtime, 100 MHz): on timeout the block
+// records GRID_SYNC (8) in the device error word `err` — raised by the host at its next check
+// (tilelang/runtime/errors.py) — and poisons the barrier so every later barrier of this launch
+// falls through at once (the kernel finishes instead of hanging the GPU).
+#ifndef TL_GRID_SYNC_TIMEOUT_TICKS
+#define TL_GRID_SYNC_TIMEOUT_TICKS 200000000ull  // 2 s
+#endif
+TL_DEVICE void sync_grid(long long ws_, long long err_) {
+  unsigned* ws = reinterpret_cast<unsigned*>(ws_);
+  int* err = reinterpret_cast<int*>(err_);
   __syncthreads();
   if (threadIdx.x == 0 && threadIdx.y == 0 && threadIdx.z == 0) {
     const unsigned nblocks = gridDim.x * gridDim.y * gridDim.z;
-    const unsigned gen = __hip_atomic_load(&tl_grid_bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned gen = __hip_atomic_load(&ws[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned arrived =
-        __hip_atomic_fetch_add(&tl_grid_bar_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const unsigned arrived = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     if (arrived == nblocks) {
-      __hip_atomic_store(&tl_grid_bar_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ws[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&tl_grid_bar_gen, gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      // bounded spin (~seconds): a grid that is not fully resident must not hang the device
-      for (long it = 0; it < (1l << 26); ++it) {
-        if (__hip_atomic_load(&tl_grid_bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen) break;
+      __hip_atomic_store(&ws[1], gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (__hip_atomic_load(&ws[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(&ws[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        if (__hip_atomic_load(&ws[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > TL_GRID_SYNC_TIMEOUT_TICKS) {
+          __hip_atomic_fetch_or(err, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&ws[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
         __builtin_amdgcn_s_sleep(2);
       }
     }

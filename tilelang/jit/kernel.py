@@ -201,8 +201,11 @@ class JITKernel:
                 if n in kwargs:
                     full.append(kwargs[n])
             args = tuple(full)
+        from ..runtime import errors as _errors
+        _errors.poll()  # a bounded device wait of an earlier launch timed out: raise it here
         rts = self.runtimes
         kernels = self.artifact.kernels
+        is_cpu = self.artifact.is_cpu
         mesh_ctx = None
         if any(dk.mesh is not None for dk in kernels):
             from ..parallel.mesh import current_mesh, MeshError
@@ -212,8 +215,24 @@ class JITKernel:
                                 f"tilelang.parallel.init_mesh() (one process per GPU) or run it inside "
                                 f"VirtualMesh.run()")
 
+        keep = []  # per-launch workspaces stay referenced until every launch is issued
+        watch = []  # (error word, label, decoder) read back behind the launches
+
         def _margs(dk):
-            return mesh_ctx.launch_args(dk.mesh) if dk.mesh is not None else []
+            out = mesh_ctx.launch_args(dk.mesh) if dk.mesh is not None else []
+            if dk.mesh is not None and not is_cpu:
+                watch.append((mesh_ctx.err, f"{dk.name} (mesh rank {mesh_ctx.rank})", mesh_ctx.error_decoder))
+            if getattr(dk, "cooperative", False) and not is_cpu:
+                import torch
+                dev = next((a.device for a in args if isinstance(a, torch.Tensor) and a.is_cuda), None)
+                dev = dev if dev is not None else torch.device("cuda", torch.cuda.current_device())
+                # barrier state of THIS launch (tl/common.h sync_grid): zeroed on the launch stream
+                ws = torch.zeros(4, dtype=torch.int32, device=dev)
+                err = _errors.device_word(dev)
+                keep.append(ws)
+                watch.append((err, dk.name, None))
+                out = out + [ws.data_ptr(), err.data_ptr()]
+            return out
 
         if mesh_ctx is not None and not self.artifact.is_cpu:
             key = (id(mesh_ctx), mesh_ctx.ranks_on_device)
@@ -225,6 +244,8 @@ class JITKernel:
 
         out = rts[0](*args, *_margs(kernels[0]))
         if len(rts) == 1:
+            for w, label, dec in watch:
+                _errors.record(w, label, dec)
             return out
         # later kernels of the program see the outputs of the first as ordinary arguments
         outs = list(out) if isinstance(out, tuple) else ([out] if out is not None else [])
@@ -238,6 +259,8 @@ class JITKernel:
                 ai += 1
         for r, dk in zip(rts[1:], kernels[1:]):
             r(*full, *_margs(dk))
+        for w, label, dec in watch:
+            _errors.record(w, label, dec)
         return out
 
     @classmethod

@@ -1,4 +1,4 @@
-"""``linear(x, w)`` = x @ w^T on MFMA (reference counterpart: examples/deepseek_v32/inference/kernel.py
+"""``linear(x, w)`` = x @ w^T on MFMA (f16 / bf16: 16x16x32; fp32: the exact-f32 16x16x4 form) (reference counterpart: examples/deepseek_v32/inference/kernel.py
 ``fp8_gemm`` / the model's ``linear``).  One compiled kernel per (M, N, K, dtype, target); the
 tile is chosen by M so decode-sized (skinny) and prefill-sized GEMMs both fill the CUs."""
 from __future__ import annotations
@@ -15,7 +15,13 @@ def _tdt(dtype: torch.dtype) -> str:
     return {torch.float16: "float16", torch.bfloat16: "bfloat16", torch.float32: "float32"}[dtype]
 
 
-def _tiles(M: int, N: int, K: int):
+def _tiles(M: int, N: int, K: int, dtype: str = "float16"):
+    if dtype == "float32":
+        # exact-f32 MFMA (v_mfma_f32_16x16x4_f32, tl::gemm_ss_f32): fp32 tiles are twice the
+        # bytes, so keep the 128x128 tile at BK=32 (2 x 16 KiB per stage)
+        bm = 64 if M <= 64 else 128
+        bn = 64 if N <= 256 else 128
+        return bm, bn, 32, 256
     bm = 64 if M <= 64 else (128 if M <= 2048 else 256)
     bn = 64 if N <= 256 else 128 if M <= 2048 else 256
     bk = 64 if K % 64 == 0 else 32
@@ -25,7 +31,7 @@ def _tiles(M: int, N: int, K: int):
 
 @functools.lru_cache(maxsize=None)
 def _linear_kernel(M, N, K, dtype, target):
-    bm, bn, bk, threads = _tiles(M, N, K)
+    bm, bn, bk, threads = _tiles(M, N, K, dtype)
 
     @T.prim_func
     def main(A: T.Tensor((M, K), dtype), W: T.Tensor((N, K), dtype), C: T.Tensor((M, N), dtype)):
@@ -52,7 +58,15 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     x2 = x.reshape(-1, shp[-1]).contiguous()
     M, K = x2.shape
     N = w.shape[0]
-    if K % 32 or x2.dtype == torch.float32:
-        return torch.nn.functional.linear(x, w)  # fp32 / odd K: not an MFMA shape (router logits etc.)
+    w2 = w.contiguous()
+    if w2.dtype != x2.dtype:
+        raise TypeError(f"linear: x is {x2.dtype} but w is {w2.dtype}")
+    if K % 32:
+        # the MFMA K step is 32 (f16/bf16) / 4 (f32) and tiles are staged 16 bytes at a time:
+        # zero-pad K (exact: the padded products are 0) instead of leaving the MFMA path
+        pad = (-K) % 32
+        x2 = torch.nn.functional.pad(x2, (0, pad))
+        w2 = torch.nn.functional.pad(w2, (0, pad))
+        K += pad
     k = _linear_kernel(M, N, K, _tdt(x2.dtype), "cpu" if x2.device.type == "cpu" else "hip")
-    return k(x2, w.contiguous()).reshape(*shp[:-1], N)
+    return k(x2, w2).reshape(*shp[:-1], N)

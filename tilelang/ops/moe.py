@@ -502,7 +502,8 @@ def combine_kernel(n_tok: int, H: int, topk: int, max_rows: int, dtype: str, tar
 def route(x: torch.Tensor, gate_w: torch.Tensor, topk: int):
     """Router -> top-k ids [T, k] int32 + renormalised weights [T, k].  16-bit activations with
     H % 256 == 0 take the fused MFMA GEMM + top-k kernel; otherwise logits come from
-    ``torch.nn.functional.linear`` (fp32 routers, odd widths) and ``router_topk_kernel``."""
+    ``ops.gemm.linear`` (the exact-f32 MFMA GEMM for fp32 routers, K zero-padded for odd widths)
+    and ``router_topk_kernel``."""
     n_tok, H = x.shape
     E = gate_w.shape[0]
     if x.dtype in (torch.float16, torch.bfloat16) and H % 256 == 0 and gate_w.dtype == x.dtype and E <= 64:
@@ -511,7 +512,8 @@ def route(x: torch.Tensor, gate_w: torch.Tensor, topk: int):
         router_fused_kernel(n_tok, H, E, topk, _tdt(x.dtype), _target(x.device))(x.contiguous(), _padded_gate(gate_w),
                                                                                   ids, w)
         return ids, w
-    logits = torch.nn.functional.linear(x, gate_w).float()
+    from .gemm import linear
+    logits = linear(x, gate_w.to(x.dtype)).float()  # MFMA (exact-f32 form for fp32 routers)
     n_tok, E = logits.shape
     ids = torch.empty(n_tok, topk, dtype=torch.int32, device=x.device)
     w = torch.empty(n_tok, topk, dtype=torch.float32, device=x.device)

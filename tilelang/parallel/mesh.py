@@ -188,22 +188,28 @@ class MeshContext:
                             f"needs {need} co-resident workgroups but the GPU holds {resident}; use a persistent grid "
                             f"(T.Persistent / a loop over tiles inside fewer blocks)")
 
+    def error_decoder(self, label, e):
+        """MeshError for the bits of the device error word (tl/mesh.h spin codes)."""
+        what = []
+        if e & 1:
+            what.append("waiting for a receiver to free its slot")
+        if e & 2:
+            what.append("waiting for data from a sender")
+        if e & 4:
+            what.append("waiting at a mesh barrier")
+        return MeshError(f"{label}: timed out " + ", ".join(what) + " (a peer did not run the same kernel sequence)")
+
     def check(self):
         """Raise if any bounded wait of a mesh kernel on this rank timed out."""
         import torch
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
+            from ..runtime import errors
+            errors.poll()  # launches recorded by JITKernel raise through the monitor first
         e = int(self.err.item())
         if e:
-            what = []
-            if e & 1:
-                what.append("waiting for a receiver to free its slot")
-            if e & 2:
-                what.append("waiting for data from a sender")
-            if e & 4:
-                what.append("waiting at a mesh barrier")
-            raise MeshError(f"mesh rank {self.rank}: timed out " + ", ".join(what) +
-                            " (a peer did not run the same kernel sequence)")
+            self.err.zero_()
+            raise self.error_decoder(f"mesh rank {self.rank}", e)
 
     @contextlib.contextmanager
     def activate(self):

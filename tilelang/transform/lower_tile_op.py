@@ -1916,6 +1916,14 @@ def lower_tile_ops(kernel: S.KernelStmt, target, pass_cfg=None):
     k.attrs = dict(kernel.attrs)
     k.attrs["narrow_index"] = {b.name for b in ctx.narrow_index}
     k.attrs["cooperative"] = ctx.uses_grid_sync
+    if ctx.uses_grid_sync and not kernel.is_cpu:
+        # per-launch barrier state + the device error word (tl/common.h sync_grid, runtime/errors.py)
+        from ..ir.expr import Var as _Var
+        k.attrs["extra_params"] = list(k.attrs.get("extra_params", [])) + [
+            dict(kind="extra", name="tl_gsync_ws", var=_Var("tl_gsync_ws", "int64"), ctype="long long", nbytes=8,
+                 runtime="gsync"),
+            dict(kind="extra", name="tl_dev_err", var=_Var("tl_dev_err", "int64"), ctype="long long", nbytes=8,
+                 runtime="err")]
     if ctx.mesh is not None:
         k.attrs["extra_params"] = list(k.attrs.get("extra_params", [])) + ctx.mesh.extra_params()
         k.attrs["mesh"] = ctx.mesh.meta()
