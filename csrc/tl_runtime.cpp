@@ -97,7 +97,26 @@ int64_t run_prog(const std::vector<int64_t>& prog, const std::vector<int64_t>& s
   return st.back();
 }
 
-const char* type_name(int st) { return c10::toString(static_cast<c10::ScalarType>(st)); }
+// torch spelling of a dtype (float16, bfloat16, float8_e4m3fn, ...) for error messages
+std::string type_name(int st) {
+  switch (static_cast<c10::ScalarType>(st)) {
+    case c10::ScalarType::Half: return "float16";
+    case c10::ScalarType::Float: return "float32";
+    case c10::ScalarType::Double: return "float64";
+    case c10::ScalarType::BFloat16: return "bfloat16";
+    case c10::ScalarType::Int: return "int32";
+    case c10::ScalarType::Long: return "int64";
+    case c10::ScalarType::Short: return "int16";
+    case c10::ScalarType::Char: return "int8";
+    case c10::ScalarType::Byte: return "uint8";
+    case c10::ScalarType::Bool: return "bool";
+    case c10::ScalarType::Float8_e4m3fn: return "float8_e4m3fn";
+    case c10::ScalarType::Float8_e5m2: return "float8_e5m2";
+    case c10::ScalarType::Float8_e4m3fnuz: return "float8_e4m3fnuz";
+    case c10::ScalarType::Float8_e5m2fnuz: return "float8_e5m2fnuz";
+    default: return c10::toString(static_cast<c10::ScalarType>(st));
+  }
+}
 
 class Kernel {
  public:
@@ -183,12 +202,14 @@ class Kernel {
       if (p.kind == kDyn || p.is_output) continue;
       py::handle a = args[ai++];
       if (p.kind == kBuffer) {
-        if (!THPVariable_Check(a.ptr())) throw py::type_error(label_ + ": argument '" + p.name + "' must be a torch.Tensor");
+        if (!THPVariable_Check(a.ptr()))
+          throw py::type_error(label_ + ": argument '" + p.name + "' expects a pointer (torch.Tensor), got " +
+                               py::str(a.get_type().attr("__name__")).cast<std::string>());
         at::Tensor t = THPVariable_Unpack(a.ptr());
         check_tensor(p, t, syms, device);
         tensors[i] = t;
       } else if (p.kind == kScalar && p.sym >= 0 && !p.is_float) {
-        syms.at(p.sym) = py::isinstance<py::bool_>(a) ? (a.cast<bool>() ? 1 : 0) : a.cast<int64_t>();
+        syms.at(p.sym) = scalar_int(p, a);
       }
     }
     // pass 2: outputs
@@ -338,8 +359,35 @@ class Kernel {
     }
   }
 
+  // Python value of a scalar parameter, checked against its declared type (reference
+  // maint/host_checks/10_scalar_type_mismatch.py): floats take int/float, integers reject
+  // float (no silent truncation), bool takes only bool or 0/1.
+  int64_t scalar_int(const Param& p, py::handle a) {
+    const bool is_bool = p.scalar_type == (int)c10::ScalarType::Bool;
+    if (py::isinstance<py::bool_>(a)) return a.cast<bool>() ? 1 : 0;
+    if (PyFloat_Check(a.ptr()) || !PyLong_Check(a.ptr())) {
+      std::ostringstream os;
+      os << label_ << ": argument '" << p.name << "' expects " << (is_bool ? "a bool" : "an integer") << ", got "
+         << py::str(a.get_type().attr("__name__")).cast<std::string>();
+      throw py::type_error(os.str());
+    }
+    const int64_t v = a.cast<int64_t>();
+    if (is_bool && v != 0 && v != 1) {
+      std::ostringstream os;
+      os << label_ << ": argument '" << p.name << "' expects a bool, got the integer " << v;
+      throw py::type_error(os.str());
+    }
+    return v;
+  }
+
   void pack_scalar(const Param& p, py::handle a, uint64_t* out) {
     if (p.is_float) {
+      if (!PyFloat_Check(a.ptr()) && !PyLong_Check(a.ptr())) {
+        std::ostringstream os;
+        os << label_ << ": argument '" << p.name << "' expects a float, got "
+           << py::str(a.get_type().attr("__name__")).cast<std::string>();
+        throw py::type_error(os.str());
+      }
       double v = a.cast<double>();
       if (p.nbytes == 8) std::memcpy(out, &v, 8);
       else {
@@ -347,9 +395,7 @@ class Kernel {
         std::memcpy(out, &f, 4);
       }
     } else {
-      int64_t v;
-      if (py::isinstance<py::bool_>(a)) v = a.cast<bool>() ? 1 : 0;
-      else v = a.cast<int64_t>();
+      int64_t v = scalar_int(p, a);
       if (p.nbytes == 8) std::memcpy(out, &v, 8);
       else if (p.nbytes == 4) {
         int32_t v32 = (int32_t)v;
@@ -474,6 +520,15 @@ void ipc_close_handle(int64_t ptr, int device) {
   TL_HIP_CHECK(hipIpcCloseMemHandle(reinterpret_cast<void*>(ptr)));
 }
 
+// A non-owning uint8 tensor over device memory the runtime allocated (a symmetric workspace):
+// lets PyTorch ops and tilelang kernels read a peer-written buffer in place.  The caller keeps
+// the allocation alive for as long as the tensor is used.
+py::object tensor_from_ptr(int64_t ptr, int64_t nbytes, int device) {
+  auto opts = at::TensorOptions().dtype(at::kByte).device(at::Device(at::kCUDA, device));
+  at::Tensor t = at::from_blob(reinterpret_cast<void*>(ptr), {nbytes}, [](void*) {}, opts);
+  return py::reinterpret_steal<py::object>(THPVariable_Wrap(t));
+}
+
 bool can_access_peer(int dev, int peer) {
   int ok = 0;
   TL_HIP_CHECK(hipDeviceCanAccessPeer(&ok, dev, peer));
@@ -490,6 +545,7 @@ PYBIND11_MODULE(_tl_runtime, m) {
   m.def("ipc_open_handle", &ipc_open_handle);
   m.def("ipc_close_handle", &ipc_close_handle);
   m.def("can_access_peer", &can_access_peer);
+  m.def("tensor_from_ptr", &tensor_from_ptr);
   m.doc() = "tilelang native kernel runtime for MI355X (gfx950)";
   py::class_<Kernel, std::shared_ptr<Kernel>>(m, "Kernel")
       .def(py::init<py::bytes, std::string, bool, py::list, int, std::vector<std::vector<int64_t>>,

@@ -20,6 +20,9 @@
 #ifndef PRIO
 #define PRIO 0
 #endif
+#ifndef YOUNG_PRIO
+#define YOUNG_PRIO 0
+#endif
 #ifndef GM
 #define GM 4096
 #endif
@@ -46,7 +49,7 @@ struct Frags {
   F b[N_REP];
 };
 
-TL_DEVICE void load_frags(const half_t* As, const half_t* Bs, Frags& f, int wm, int wn, int lane) {
+TL_DEVICE void load_frags(const half_t* __restrict__ As, const half_t* __restrict__ Bs, Frags& __restrict__ f, int wm, int wn, int lane) {
 #pragma unroll
   for (int mi = 0; mi < M_REP; ++mi) f.a[mi] = ld_operand<half_t, BM, KH, SWZ_A, false, 0>(As, wm * WM + mi * 16, 0, lane);
 #pragma unroll
@@ -126,57 +129,76 @@ extern "C" __global__ void __launch_bounds__(512) gemm_kernel(half_t* __restrict
   for (int i = 0; i < M_REP * N_REP; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
   const Dma d(by, bx, tid);
   constexpr int NH = GK / KH;  // half-tiles
+#if YOUNG_PRIO
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);  // guide T5 static form
+#endif
 #if PREFETCH
-  // 4-slot ring of half-tiles; half h lives in slot h%4.  At half h: fragments of h are in
-  // registers, slot h+1 is waited for and read, slot h%4 (read during h-1) is refilled with h+4.
-#pragma unroll
-  for (int h = 0; h < 4; ++h) issue(A, B, d, h, smem + h * SLOT, wave, lane);
+  // Two K-half banks (even halves in bank 0, odd halves in bank 1), each double-buffered by
+  // tile parity: a step refills the slot of ITS OWN bank that the previous step read, and reads
+  // the other bank, so every ds_read provably misses the LDS-DMA just issued (the compiler can
+  // then keep its counted waits instead of a vmcnt(0) before the first read of each step).
+  // At half h the fragments of h are already in registers (read during h-1).
+  half_t* bank0 = smem;             // [2][SLOT]: half 0 of tiles k%2
+  half_t* bank1 = smem + 2 * SLOT;  // [2][SLOT]: half 1 of tiles k%2
+  constexpr int NT = GK / (2 * KH);
+  issue(A, B, d, 0, bank0, wave, lane);
+  issue(A, B, d, 1, bank1, wave, lane);
+  issue(A, B, d, 2, bank0 + SLOT, wave, lane);
+  issue(A, B, d, 3, bank1 + SLOT, wave, lane);
   Frags f0, f1;
   tl::wait_vmcnt<12>();
   tl::barrier_raw();
-  load_frags(smem, smem + BM * KH, f0, wm, wn, lane);
-  for (int h = 0; h < NH; h += 2) {
-    // ---- even half h: compute f0, read slot h+1 into f1
-    if (h + 3 < NH) tl::wait_vmcnt<8>(); else tl::wait_vmcnt<0>();  // slot h+1 landed
+  load_frags(bank0, bank0 + BM * KH, f0, wm, wn, lane);
+  for (int k = 0; k < NT; ++k) {
+    half_t* s0 = bank0 + (k & 1) * SLOT;
+    half_t* s1 = bank1 + (k & 1) * SLOT;
+    half_t* s0n = bank0 + ((k + 1) & 1) * SLOT;
+    // even half 2k: f0 = half 0 of tile k; read half 1 (bank 1), refill bank 0 slot with tile k+2
+    if (k + 1 < NT) tl::wait_vmcnt<8>(); else tl::wait_vmcnt<0>();
     tl::barrier_raw();
     __builtin_amdgcn_sched_barrier(0);
-    if (h + 4 < NH) issue(A, B, d, h + 4, smem + (h % 4) * SLOT, wave, lane);
-    {
-      half_t* s = smem + ((h + 1) % 4) * SLOT;
-      load_frags(s, s + BM * KH, f1, wm, wn, lane);
-    }
+    if (k + 2 < NT) issue(A, B, d, 2 * (k + 2), s0, wave, lane);
+    load_frags(s1, s1 + BM * KH, f1, wm, wn, lane);
     prio_on();
     mma(f0, acc);
     prio_off();
     interleave();
-    // ---- odd half h+1: compute f1, read slot h+2 into f0
-    if (h + 4 < NH) tl::wait_vmcnt<8>(); else if (h + 3 < NH) tl::wait_vmcnt<4>(); else tl::wait_vmcnt<0>();
+    // odd half 2k+1: f1 = half 1 of tile k; read half 0 of tile k+1 (bank 0), refill bank 1 slot
+    if (k + 2 < NT) tl::wait_vmcnt<8>(); else if (k + 1 < NT) tl::wait_vmcnt<4>(); else tl::wait_vmcnt<0>();
     tl::barrier_raw();
     __builtin_amdgcn_sched_barrier(0);
-    if (h + 5 < NH) issue(A, B, d, h + 5, smem + ((h + 1) % 4) * SLOT, wave, lane);
-    if (h + 2 < NH) {
-      half_t* s = smem + ((h + 2) % 4) * SLOT;
-      load_frags(s, s + BM * KH, f0, wm, wn, lane);
-    }
+    if (k + 2 < NT) issue(A, B, d, 2 * (k + 2) + 1, s1, wave, lane);
+    if (k + 1 < NT) load_frags(s0n, s0n + BM * KH, f0, wm, wn, lane);
     prio_on();
     mma(f1, acc);
     prio_off();
     interleave();
   }
 #else
-  // current DSL schedule: wait for the slot, barrier, refill the slot read two halves ago, read+MMA
+  // current DSL schedule: wait for the slot, barrier, refill the slot read the step before,
+  // read + MMA (unrolled 4x: compile-time slots, see above)
 #pragma unroll
   for (int h = 0; h < 3; ++h) issue(A, B, d, h, smem + h * SLOT, wave, lane);
-  for (int h = 0; h < NH; ++h) {
-    if (h + 2 < NH) tl::wait_vmcnt<8>(); else if (h + 1 < NH) tl::wait_vmcnt<4>(); else tl::wait_vmcnt<0>();
-    tl::barrier_raw();
-    if (h + 3 < NH) issue(A, B, d, h + 3, smem + ((h + 3) % 4) * SLOT, wave, lane);
-    Frags f;
-    half_t* s = smem + (h % 4) * SLOT;
-    load_frags(s, s + BM * KH, f, wm, wn, lane);
-    prio_on();
-    mma(f, acc);
-    prio_off();
+  for (int h0 = 0; h0 < NH; h0 += 4) {
+#define NP_STEP(S)                                                                         \
+  {                                                                                        \
+    const int h = h0 + S;                                                                  \
+    if (h + 2 < NH) tl::wait_vmcnt<8>();                                                   \
+    else if (h + 1 < NH) tl::wait_vmcnt<4>();                                              \
+    else tl::wait_vmcnt<0>();                                                              \
+    tl::barrier_raw();                                                                     \
+    if (h + 3 < NH) issue(A, B, d, h + 3, smem + ((S + 3) % 4) * SLOT, wave, lane);        \
+    Frags f;                                                                               \
+    load_frags(smem + S * SLOT, smem + S * SLOT + BM * KH, f, wm, wn, lane);               \
+    prio_on();                                                                             \
+    mma(f, acc);                                                                           \
+    prio_off();                                                                            \
+  }
+    NP_STEP(0)
+    NP_STEP(1)
+    NP_STEP(2)
+    NP_STEP(3)
+#undef NP_STEP
   }
 #endif
   // epilogue: fragments -> row-padded LDS tile -> 16-byte row stores

@@ -23,11 +23,12 @@ from example_gemm import matmul  # noqa: E402
 
 DEFAULT = [
     "dsl:",
-    "noprefetch:-DWAVES_M=4 -DPREFETCH=0",
     "rp4x2:-DWAVES_M=4 -DPREFETCH=1 -DILV=0",
-    "rp4x2_ilv:-DWAVES_M=4 -DPREFETCH=1 -DILV=1",
+    "rp2x4:-DWAVES_M=2 -DPREFETCH=1 -DILV=0",
     "rp2x4_ilv:-DWAVES_M=2 -DPREFETCH=1 -DILV=1",
-    "rp4x2_ilv_prio:-DWAVES_M=4 -DPREFETCH=1 -DILV=1 -DPRIO=1",
+    "rp2x4_prio:-DWAVES_M=2 -DPREFETCH=1 -DILV=0 -DPRIO=1",
+    "rp2x4_young:-DWAVES_M=2 -DPREFETCH=1 -DILV=0 -DYOUNG_PRIO=1",
+    "rp4x2_young:-DWAVES_M=4 -DPREFETCH=1 -DILV=0 -DYOUNG_PRIO=1",
 ]
 
 

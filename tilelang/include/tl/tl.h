@@ -8,3 +8,4 @@
 #include "swizzle.h"
 #include "debug.h"
 #include "mesh.h"
+#include "ep.h"

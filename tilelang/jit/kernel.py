@@ -154,6 +154,7 @@ class JITKernel:
                 v = p["var"]
                 d["nbytes"] = max(1, v.dtype.bits // 8)
                 d["is_float"] = v.dtype.is_float
+                d["scalar_type"] = _scalar_type_code(v.dtype)  # host check of the Python value's type
                 d["sym"] = symtab.get(v, -1)
             elif p["kind"] == "dyn":
                 v = p["var"]

@@ -23,6 +23,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Optional
 
+import os
+
 import torch
 
 from ..ops.moe import expert_ffn
@@ -137,12 +139,41 @@ class MoELayer(torch.nn.Module):
                                           reduce_mesh="all" if self.parallel == "tp" else None, cfg=cfg.gemm_cfg,
                                           w1_interleaved=True)
             return K.combine(y, dest, wts)
+        if self._device_ep():
+            return self._ep_device(x, ids, wts)
         y = self._ep(x, ids)
         return K.combine(y, torch.arange(y.shape[0], device=x.device, dtype=torch.int32), wts)
 
+    def _device_ep(self) -> bool:
+        """GPU process meshes exchange tokens with device kernels over IPC (ops/ep.py); CPU and
+        virtual meshes use the host collectives."""
+        from ..parallel.mesh import ProcessMesh
+        return isinstance(self.mesh, ProcessMesh) and self.mesh.device.type == "cuda" and self.ep_mode == "device"
+
+    # "device" (ops/ep.py, no host sync) or "host" (RCCL all_to_all_v); TL_EP_MODE overrides
+    ep_mode = os.environ.get("TL_EP_MODE", "device")
+
+    def _ep_device(self, x, ids, wts):
+        """Expert parallel without host synchronisation: rows go straight into the owners'
+        symmetric buffers (tl/ep.h), the local experts run on the received row table (empty
+        slots carry expert id -1), and results come back the same way."""
+        from ..ops import moe as K
+        from ..ops.ep import EPExchange
+        key = (x.shape[0], x.shape[1], x.dtype)
+        ex = self.__dict__.get("_exchange")
+        if ex is None or ex[0] != key:
+            ex = (key, EPExchange(self.mesh, x.shape[0], x.shape[1], self.cfg.topk, self.cfg.n_experts, x.dtype))
+            self._exchange = ex
+        xc = ex[1]
+        rows, rids, rcnt, ret_index = xc.dispatch(x, ids)
+        y_pad, ydest = K.expert_ffn_padded(rows, rids, 1, self.w1, self.w2, self.cfg.block_M, cfg=self.cfg.gemm_cfg,
+                                           w1_interleaved=True)
+        back = xc.combine_rows(y_pad, ydest, rcnt)
+        return K.combine(back, ret_index, wts)
+
     def _ep(self, x, ids):
-        """Expert parallel: (token, expert) pairs travel to the expert's rank and back (two
-        variable-size all-to-alls; one host sync for the split sizes)."""
+        """Expert parallel over host collectives: (token, expert) pairs travel to the expert's
+        rank and back (two variable-size all-to-alls; one host sync for the split sizes)."""
         from ..ops import moe as K
         from ..parallel import collectives as C
         m = self.mesh

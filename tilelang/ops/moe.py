@@ -177,7 +177,7 @@ def max_padded_rows(n_assign: int, E: int, block_M: int) -> int:
 def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: str, stable: bool = False,
                  threads: int = 1024):
     """Dispatch plan of ``n`` assignments (``expert_ids[n]``; assignment ``j`` reads source row
-    ``j // div``): ``dest[j]`` (its padded row), ``row_src[max_rows]``, ``tile_expert``, ``counts[E]``,
+    ``j // div``; a negative id is an empty slot: not placed, ``dest[j] = -1``): ``dest[j]`` (its padded row), ``row_src[max_rows]``, ``tile_expert``, ``counts[E]``,
     ``tile_rows`` (valid rows of every row tile: they are a prefix of the tile).
 
     One workgroup.  ``stable=False``: rows of one expert are placed in LDS-atomic order (each
@@ -208,7 +208,7 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                     for e in T.serial(E):
                         tc[t, e] = 0
                     for i in T.serial(c):
-                        if t * c + i < n:
+                        if t * c + i < n and expert_ids[t * c + i] >= 0:
                             tc[t, expert_ids[t * c + i]] = tc[t, expert_ids[t * c + i]] + 1
                 T.cumsum(tc, run, dim=0)
                 for e in T.Parallel(E):
@@ -218,7 +218,8 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                     cnt[e] = 0
                     fill[e] = 0
                 for j in T.Parallel(n):
-                    T.atomic_add(cnt[expert_ids[j]], 1)
+                    if expert_ids[j] >= 0:
+                        T.atomic_add(cnt[expert_ids[j]], 1)
             for r in T.Parallel(max_rows):
                 row_src[r] = -1
             for z in T.Parallel(1):
@@ -245,16 +246,21 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                     for e in T.serial(E):
                         run[t, e] = start[e] + run[t, e] - tc[t, e]
                     for i in T.serial(c):
-                        if t * c + i < n:
+                        if t * c + i < n and expert_ids[t * c + i] >= 0:
                             d = run[t, expert_ids[t * c + i]]
                             run[t, expert_ids[t * c + i]] = d + 1
                             dest[t * c + i] = d
                             row_src[d] = (t * c + i) // div
+                        if t * c + i < n and expert_ids[t * c + i] < 0:
+                            dest[t * c + i] = -1
             else:
                 for j in T.Parallel(n):
-                    slot = T.atomic_add(fill[expert_ids[j]], 1, return_prev=True)
-                    dest[j] = start[expert_ids[j]] + slot
-                    row_src[start[expert_ids[j]] + slot] = j // div
+                    if expert_ids[j] >= 0:
+                        slot = T.atomic_add(fill[expert_ids[j]], 1, return_prev=True)
+                        dest[j] = start[expert_ids[j]] + slot
+                        row_src[start[expert_ids[j]] + slot] = j // div
+                    if expert_ids[j] < 0:
+                        dest[j] = -1
 
     return tilelang.compile(moe_align, out_idx=None, target=target)
 

@@ -375,13 +375,87 @@ class ProcessMesh(MeshContext):
         dist.barrier()
         self.ensure_workspace(n)
 
+    # -- named symmetric buffers (device-driven exchanges outside T.comm, e.g. ops/ep.py) -----
+    def symmetric_buffer(self, key: str, nbytes: int) -> "SymmetricBuffer":
+        """Collective: a zeroed device buffer of ``nbytes`` on every rank, IPC-opened by every
+        peer (the ``T.comm`` workspace stays separate).  Cached by ``key``; a larger request
+        re-allocates it (all ranks must request the same size at the same point)."""
+        import torch
+        import torch.distributed as dist
+        if self.device.type != "cuda":
+            raise MeshError("symmetric buffers are device memory: use a GPU mesh")
+        bufs = self.__dict__.setdefault("_sym", {})
+        b = bufs.get(key)
+        if b is not None and b.nbytes >= nbytes:
+            return b
+        torch.cuda.synchronize(self.device)
+        dist.barrier()
+        if b is not None:
+            b.release()
+        from .. import _native
+        rt = _native.runtime()
+        dev = self.device.index
+        own = rt.ws_alloc(int(nbytes), dev, self.ws_flags)
+        handles = [None] * self.world
+        dist.all_gather_object(handles, rt.ipc_get_handle(own, dev))
+        ptrs, peers = [], []
+        for r, h in enumerate(handles):
+            if r == self.rank:
+                ptrs.append(own)
+            else:
+                q = rt.ipc_open_handle(h, dev)
+                peers.append(q)
+                ptrs.append(q)
+        b = SymmetricBuffer(self, own, peers, ptrs, int(nbytes))
+        bufs[key] = b
+        dist.barrier()
+        return b
+
     def close(self):
         import torch
         import torch.distributed as dist
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         dist.barrier()
+        for b in self.__dict__.pop("_sym", {}).values():
+            b.release()
         self._release()
+
+
+class SymmetricBuffer:
+    """One rank's view of a symmetric IPC buffer: ``local`` (uint8 tensor over this rank's
+    allocation) and ``table`` (int64 device tensor of every rank's base address as mapped in
+    this process, indexed by rank)."""
+
+    def __init__(self, mesh, own: int, peers, ptrs, nbytes: int):
+        import torch
+        from .. import _native
+        self.mesh, self.own, self.peers, self.nbytes = mesh, own, list(peers), nbytes
+        self.ptrs = list(ptrs)
+        dev = mesh.device.index
+        self.local = _native.runtime().tensor_from_ptr(own, nbytes, dev)
+        self.table = torch.tensor(self.ptrs, dtype=torch.int64, device=mesh.device)
+
+    def view(self, offset: int, shape, dtype):
+        """A typed tensor over [offset, offset + prod(shape) * itemsize) of the local buffer."""
+        import math
+        import torch
+        n = math.prod(shape) * torch.empty((), dtype=dtype).element_size()
+        if offset % 16 or offset + n > self.nbytes:
+            raise ValueError(f"view [{offset}, {offset + n}) outside the {self.nbytes}-byte buffer or misaligned")
+        return self.local[offset:offset + n].view(dtype).view(*shape)
+
+    def release(self):
+        if self.own is None:
+            return
+        from .. import _native
+        rt = _native.runtime()
+        dev = self.mesh.device.index
+        self.local = None
+        for q in self.peers:
+            rt.ipc_close_handle(q, dev)
+        rt.ws_free(self.own, dev)
+        self.own, self.peers = None, []
 
 
 class VirtualRank(MeshContext):
