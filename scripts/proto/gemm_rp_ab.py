@@ -23,20 +23,19 @@ from example_gemm import matmul  # noqa: E402
 
 DEFAULT = [
     "dsl:",
-    "rp4x2:-DWAVES_M=4 -DPREFETCH=1 -DILV=0",
-    "rp2x4:-DWAVES_M=2 -DPREFETCH=1 -DILV=0",
+    "dsl_noilv:cfg tl.gemm_interleave=0",
+    "dsl_noprefetch:cfg tl.gemm_prefetch=0",
     "rp2x4_ilv:-DWAVES_M=2 -DPREFETCH=1 -DILV=1",
-    "rp2x4_prio:-DWAVES_M=2 -DPREFETCH=1 -DILV=0 -DPRIO=1",
-    "rp2x4_young:-DWAVES_M=2 -DPREFETCH=1 -DILV=0 -DYOUNG_PRIO=1",
-    "rp4x2_young:-DWAVES_M=4 -DPREFETCH=1 -DILV=0 -DYOUNG_PRIO=1",
 ]
 
 
 def build(M, N, K, defines):
     f = matmul.get_tir(M, N, K, 256, 256, 64, 512, 2, "float16", staged_epilogue=True)
-    if not defines:
+    if not defines or defines.startswith("cfg "):
+        # the DSL kernel; "cfg key=0 key2=1" sets boolean pass configs
+        cfg = {kv.split("=")[0]: bool(int(kv.split("=")[1])) for kv in defines.split()[1:]} if defines else {}
         callback.unregister()
-        return tilelang.compile(f, out_idx=[-1], target="hip")
+        return tilelang.compile(f, out_idx=[-1], target="hip", pass_configs=cfg)
     src = open(os.path.join(HERE, "gemm_rp.hip")).read()
     head = "".join(f"#define {d[2:].replace('=', ' ', 1)}\n" for d in defines.split())
     head += f"#define GM {M}\n#define GN {N}\n#define GK {K}\n"

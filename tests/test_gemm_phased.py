@@ -12,19 +12,35 @@ import tilelang  # noqa: E402
 from example_gemm import matmul  # noqa: E402
 
 
-def _src(M, N, K, phased=None, bk=64, stages=2):
+def _src(M, N, K, phased=None, bk=64, stages=2, prefetch=None):
     f = matmul.get_tir(M, N, K, 256, 256, bk, 512, stages, "float16")
     cfg = {} if phased is None else {"tl.gemm_phased": phased}
+    if prefetch is not None:
+        cfg["tl.gemm_prefetch"] = prefetch
     return tilelang.lower(f, target="hip", pass_configs=cfg).kernel_source
 
 
 def test_phased_structure():
-    src = _src(4096, 4096, 4096)
+    src = _src(4096, 4096, 4096, prefetch=False)
     body = src[src.index("for (int k"):]
     # two K-half GEMMs (K = 32 each) per iteration, counted waits, vmcnt(0) only on the last iteration
     assert body.count("tl::gemm_ss<half_t, 256, 256, 32,") == 2
     assert "wait_vmcnt<8>" in body and body.count("tl::barrier_raw") >= 2
     assert "A_shared_k0" in src and "B_shared_k1" in src
+
+
+def test_prefetch_structure():
+    """Default: fragments of the next K half are read one phase ahead of their MFMAs, from the
+    bank the phase does not refill; the 256x256 tile runs 2x4 waves (fewer LDS reads)."""
+    src = _src(4096, 4096, 4096)
+    pre, body = src[:src.index("for (int k")], src[src.index("for (int k"):]
+    assert pre.count("tl::ss_frags<half_t, 256, 256, 32, 2, 4>") == 2
+    assert "tl::gemm_ss_load" in pre and "wait_vmcnt<12>" in pre
+    assert body.count("tl::gemm_ss_load<") == 2 and body.count("tl::gemm_ss_mma<half_t, 256, 256, 32, 2, 4, 16>") == 2
+    # the even phase refills bank 0 and reads bank 1; the odd phase the other way round
+    even, odd = body.split("tl::gemm_ss_mma", 1)
+    assert "&A_shared_k0" in even.split("gemm_ss_load")[0] and "A_shared_k1" in even.split("gemm_ss_load")[1]
+    assert "tl::gemm_ss<" not in body
 
 
 def test_phased_opt_out_and_shape_gate():
@@ -43,12 +59,15 @@ def test_phased_config_validation():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("K", [64, 128, 192, 1024])
-@pytest.mark.parametrize("phased", [True, "prio"])
+@pytest.mark.parametrize("phased", [True, "prio", "noprefetch", "noilv"])
 def test_phased_numerics(K, phased):
-    """1, 2, 3 and 16 K-tiles: the prologue / last-iteration waits of the phased ring."""
+    """1, 2, 3 and 16 K-tiles: the prologue / last-iteration waits of the phased ring (with and
+    without the register-prefetched fragments)."""
     M, N = 512, 768
     f = matmul.get_tir(M, N, K, 256, 256, 64, 512, 2, "float16")
-    k = tilelang.compile(f, out_idx=[-1], target="hip", pass_configs={"tl.gemm_phased": phased})
+    cfg = {"tl.gemm_phased": phased} if phased in (True, "prio") else {
+        "tl.gemm_prefetch": False} if phased == "noprefetch" else {"tl.gemm_interleave": False}
+    k = tilelang.compile(f, out_idx=[-1], target="hip", pass_configs=cfg)
     assert "A_shared_k0" in k.get_kernel_source()
     a = torch.randn(M, K, device="cuda", dtype=torch.float16)
     b = torch.randn(K, N, device="cuda", dtype=torch.float16)

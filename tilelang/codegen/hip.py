@@ -354,6 +354,8 @@ class CodeGen:
         elif isinstance(st, L.PtrDeclStmt):
             ct = self.ctype(st.buffer.dtype)
             self.w(f"{ct}* {self.buf_name(st.buffer)} = reinterpret_cast<{ct}*>({self.e(st.ptr)});")
+        elif isinstance(st, L.ObjDeclStmt):
+            self.w(f"{st.ctype} {self.e(st.var)};")
         elif isinstance(st, L.AutoLetStmt):
             self.w(f"const auto {self.e(st.var)} = {self.e(st.value)};")
         elif isinstance(st, S.KernelStmt):

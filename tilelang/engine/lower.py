@@ -137,6 +137,9 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
     t = time.perf_counter()
     lk, ctx = lower_tile_ops(kernel, target, cfg)
     timings["lower_tile_op"] = timings.get("lower_tile_op", 0) + time.perf_counter() - t
+    if target.kind == "hip" and not cfg.get("tl.disable_address_hoist"):
+        from ..transform.hoist_addresses import hoist_dma_sources
+        lk = hoist_dma_sources(lk)  # per-thread LDS-DMA source addresses out of pipelined loops
     if target.kind == "hip" and not cfg.get("tl.disable_thread_storage_sync", False):
         lk = insert_thread_sync(lk)
     lk, offsets, total = plan_lds(lk, reuse=bool(cfg.get("tl.lds_reuse", True)),
@@ -169,6 +172,8 @@ def lower(func: S.PrimFunc, target="auto", target_host=None, pass_configs: Optio
     if cfg.get("tl.disable_glds"):
         target.disable_glds = True
     target.mfma_shape = cfg.get("tl.mfma_shape")
+    target.gemm_prefetch = cfg.get("tl.gemm_prefetch")      # register-prefetched K-half GEMM schedule
+    target.gemm_interleave = cfg.get("tl.gemm_interleave")  # its 1 MFMA : 1 ds_read sched_group_barrier
     timings: Dict[str, float] = {}
     dks = []
     for i, k in enumerate(kernels):

@@ -14,6 +14,13 @@
 
 namespace tl {
 
+// the wave index: callers in loops pass the kernel's own (computed once before the loop); a
+// readfirstlane inside the loop is convergent, so LLVM cannot hoist it or the swizzled LDS
+// addresses derived from it (+35 VALU per GEMM main-loop iteration, see pipeline.py)
+TL_DEVICE int wave_or(int wave_in) {
+  return wave_in >= 0 ? wave_in : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
+
 template <uint32_t SWZ> TL_DEVICE int swz_term(int row) {
   int t = 0;
 #pragma unroll
@@ -110,14 +117,14 @@ TL_DEVICE typename mfma_traits<T>::frag ld_operand(const T* base, int mn0, int k
 template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TA, bool TB, int A_COLS, uint32_t SWZ_A,
           int B_COLS, uint32_t SWZ_B>
 TL_DEVICE void gemm_ss(const T* __restrict__ A, const T* __restrict__ B, float* __restrict__ C,
-                       int m_limit = 0x3fffffff) {
+                       int m_limit = 0x3fffffff, int wave_in = -1) {
   typedef mfma_traits<T> MT;
   typedef typename MT::frag F;
   constexpr int WM = M / WARP_M, WN = N / WARP_N;
   constexpr int M_REP = WM / 16, N_REP = WN / 16, KSTEPS = K / 32;
   static_assert(WM % 16 == 0 && WN % 16 == 0 && K % 32 == 0, "MFMA 16x16x32 tiling");
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wave = wave_or(wave_in);
   const int wm = wave / WARP_N, wn = wave % WARP_N;
   // T.gemm(valid_m=): a wave whose rows all lie at or past the tile's valid-row count issues
   // nothing (its accumulator rows are don't-care padding); uniform branch, folded when unused
@@ -140,17 +147,85 @@ TL_DEVICE void gemm_ss(const T* __restrict__ A, const T* __restrict__ B, float* 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Register-prefetched gemm_ss (the pipelined K-half schedule, transform/pipeline.py): the
+// operand fragments of the NEXT K half are read from LDS while the MFMAs of the current half
+// run on fragments read one phase earlier, so no MFMA waits on a ds_read issued after the
+// phase's barrier.  gemm_ss == gemm_ss_load + gemm_ss_mma on one fragment set.
+// ---------------------------------------------------------------------------
+template <typename T, int M, int N, int K, int WARP_M, int WARP_N> struct ss_frags {
+  static constexpr int M_REP = M / WARP_M / 16, N_REP = N / WARP_N / 16, KSTEPS = K / 32;
+  typename mfma_traits<T>::frag a[KSTEPS][M_REP];
+  typename mfma_traits<T>::frag b[KSTEPS][N_REP];
+};
+
+template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TA, bool TB, int A_COLS, uint32_t SWZ_A,
+          int B_COLS, uint32_t SWZ_B>
+TL_DEVICE void gemm_ss_load(const T* __restrict__ A, const T* __restrict__ B,
+                            ss_frags<T, M, N, K, WARP_M, WARP_N>& __restrict__ f, int wave) {
+  // `wave` is the kernel's wave index (computed once, outside the loop): a readfirstlane here
+  // is convergent, so LLVM keeps it -- and the swizzled addresses derived from it -- in the loop
+  typedef ss_frags<T, M, N, K, WARP_M, WARP_N> Fr;
+  constexpr int WM = M / WARP_M, WN = N / WARP_N;
+  static_assert(WM % 16 == 0 && WN % 16 == 0 && K % 32 == 0, "MFMA 16x16x32 tiling");
+  const int lane = threadIdx.x & 63;
+  const int wm = wave / WARP_N, wn = wave % WARP_N;
+#pragma unroll
+  for (int kk = 0; kk < Fr::KSTEPS; ++kk) {
+#pragma unroll
+    for (int mi = 0; mi < Fr::M_REP; ++mi)
+      f.a[kk][mi] = ld_operand<T, (TA ? K : M), A_COLS, SWZ_A, TA, 0>(A, wm * WM + mi * 16, kk * 32, lane);
+#pragma unroll
+    for (int ni = 0; ni < Fr::N_REP; ++ni)
+      f.b[kk][ni] = ld_operand<T, (TB ? N : K), B_COLS, SWZ_B, !TB, 0>(B, wn * WN + ni * 16, kk * 32, lane);
+  }
+}
+
+// ds_read instructions gemm_ss_load issues (MN-contiguous operands use two ds_read_b64_tr_b16)
+template <int M, int N, int K, int WARP_M, int WARP_N, bool TA, bool TB> struct ss_load_count {
+  static constexpr int value = (K / 32) * ((M / WARP_M / 16) * (TA ? 2 : 1) + (N / WARP_N / 16) * (TB ? 1 : 2));
+};
+
+// MFMAs on a fragment set.  NLOAD > 0: the caller issued NLOAD ds_reads (the next half's
+// gemm_ss_load) just before, in the same basic block: pin a 1 MFMA : 1 ds_read interleave so the
+// reads drain under the matrix pipe instead of queueing in front of it (guide T19).
+template <typename T, int M, int N, int K, int WARP_M, int WARP_N, int NLOAD>
+TL_DEVICE void gemm_ss_mma(const ss_frags<T, M, N, K, WARP_M, WARP_N>& __restrict__ f, float* __restrict__ C) {
+  typedef ss_frags<T, M, N, K, WARP_M, WARP_N> Fr;
+  typedef mfma_traits<T> MT;
+  floatx4* acc = reinterpret_cast<floatx4*>(C);
+#pragma unroll
+  for (int kk = 0; kk < Fr::KSTEPS; ++kk)
+#pragma unroll
+    for (int ni = 0; ni < Fr::N_REP; ++ni)
+#pragma unroll
+      for (int mi = 0; mi < Fr::M_REP; ++mi)
+        acc[mi * Fr::N_REP + ni] = MT::mma16(f.b[kk][ni], f.a[kk][mi], acc[mi * Fr::N_REP + ni]);
+  if constexpr (NLOAD > 0) {
+    constexpr int NMFMA = Fr::KSTEPS * Fr::M_REP * Fr::N_REP;
+    constexpr int PAIRS = NLOAD < NMFMA ? NLOAD : NMFMA;
+#pragma unroll
+    for (int i = 0; i < PAIRS; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 ds_read
+    }
+    if constexpr (NMFMA > PAIRS) __builtin_amdgcn_sched_group_barrier(0x008, NMFMA - PAIRS, 0);
+    if constexpr (NLOAD > PAIRS) __builtin_amdgcn_sched_group_barrier(0x100, NLOAD - PAIRS, 0);
+  }
+}
+
 // A operand in registers (gemm_rs): a_regs holds the A fragment, 8 elements per (mi, kk) at
 // a_regs + (mi*KSTEPS + kk)*8.  KPERM=1 when the fragment came from an accumulator layout.
 template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TB, int B_COLS, uint32_t SWZ_B, int KPERM>
-TL_DEVICE void gemm_rs(const T* __restrict__ a_regs, const T* __restrict__ B, float* __restrict__ C) {
+TL_DEVICE void gemm_rs(const T* __restrict__ a_regs, const T* __restrict__ B, float* __restrict__ C,
+                       int wave_in = -1) {
   typedef mfma_traits<T> MT;
   typedef typename MT::frag F;
   constexpr int WM = M / WARP_M, WN = N / WARP_N;
   constexpr int M_REP = WM / 16, N_REP = WN / 16, KSTEPS = K / 32;
   static_assert(WM % 16 == 0 && WN % 16 == 0 && K % 32 == 0, "MFMA 16x16x32 tiling");
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wave = wave_or(wave_in);
   const int wn = wave % WARP_N;
   floatx4* acc = reinterpret_cast<floatx4*>(C);
 #pragma unroll
@@ -208,13 +283,14 @@ TL_DEVICE long ld_rows8_b8(const uint8_t* base, int row, int col) {
 // A: [M][K] (K contiguous), B: [N][K] (K contiguous)
 template <typename TA, typename TB, int M, int N, int K, int WARP_M, int WARP_N, int A_COLS, uint32_t SWZ_A,
           int B_COLS, uint32_t SWZ_B>
-TL_DEVICE void gemm_ss_f8(const TA* __restrict__ A_, const TB* __restrict__ B_, float* __restrict__ C) {
+TL_DEVICE void gemm_ss_f8(const TA* __restrict__ A_, const TB* __restrict__ B_, float* __restrict__ C,
+                          int wave_in = -1) {
   constexpr int WM = M / WARP_M, WN = N / WARP_N;
   constexpr int M_REP = WM / 16, N_REP = WN / 16;
   const uint8_t* A = reinterpret_cast<const uint8_t*>(A_);
   const uint8_t* B = reinterpret_cast<const uint8_t*>(B_);
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wave = wave_or(wave_in);
   const int wm = wave / WARP_N, wn = wave % WARP_N;
   const int r = lane & 15, g = lane >> 4;
   floatx4* acc = reinterpret_cast<floatx4*>(C);
@@ -287,7 +363,7 @@ TL_DEVICE intx8 ld_mx_operand(const uint8_t* base, int row, int bcol0, int g) {
 template <int FA, int FB, int M, int N, int K, int WARP_M, int WARP_N, int A_COLS, uint32_t SWZ_A, int B_COLS,
           uint32_t SWZ_B, int SA_STRIDE, int SB_STRIDE>
 TL_DEVICE void gemm_ss_mx(const void* __restrict__ A_, const void* __restrict__ B_, const void* __restrict__ SA_,
-                          const void* __restrict__ SB_, float* __restrict__ C) {
+                          const void* __restrict__ SB_, float* __restrict__ C, int wave_in = -1) {
   constexpr int WM = M / WARP_M, WN = N / WARP_N;
   constexpr int M_REP = WM / 16, N_REP = WN / 16;
   constexpr int BA = mx_fmt<FA>::lane_bytes, BB = mx_fmt<FB>::lane_bytes;  // bytes per lane per step
@@ -297,7 +373,7 @@ TL_DEVICE void gemm_ss_mx(const void* __restrict__ A_, const void* __restrict__ 
   const uint8_t* SA = reinterpret_cast<const uint8_t*>(SA_);
   const uint8_t* SB = reinterpret_cast<const uint8_t*>(SB_);
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wave = wave_or(wave_in);
   const int wm = wave / WARP_N, wn = wave % WARP_N;
   const int r = lane & 15, g = lane >> 4;
   floatx4* acc = reinterpret_cast<floatx4*>(C);
@@ -377,14 +453,14 @@ TL_DEVICE typename mfma32_traits<T>::frag ld_operand32(const T* base, int mn0, i
 template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TA, bool TB, int A_COLS, uint32_t SWZ_A,
           int B_COLS, uint32_t SWZ_B>
 TL_DEVICE void gemm_ss_32(const T* __restrict__ A, const T* __restrict__ B, float* __restrict__ C,
-                          int m_limit = 0x3fffffff) {
+                          int m_limit = 0x3fffffff, int wave_in = -1) {
   typedef mfma32_traits<T> MT;
   typedef typename MT::frag F;
   constexpr int WM = M / WARP_M, WN = N / WARP_N;
   constexpr int M_REP = WM / 32, N_REP = WN / 32, KSTEPS = K / 16;
   static_assert(WM % 32 == 0 && WN % 32 == 0 && K % 16 == 0, "MFMA 32x32x16 tiling");
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wave = wave_or(wave_in);
   const int wm = wave / WARP_N, wn = wave % WARP_N;
   if (wm * WM >= m_limit) return;  // T.gemm(valid_m=), as gemm_ss
   floatx16* acc = reinterpret_cast<floatx16*>(C);
@@ -410,14 +486,15 @@ TL_DEVICE void gemm_ss_32(const T* __restrict__ A, const T* __restrict__ B, floa
 // MS = 32: v_mfma_i32_32x32x32_i8 (lane: row l & 31, 16 bytes at k = 16 (l >> 5)).
 template <int MS, int M, int N, int K, int WARP_M, int WARP_N, int A_COLS, uint32_t SWZ_A, int B_COLS,
           uint32_t SWZ_B>
-TL_DEVICE void gemm_ss_i8(const int8_t* __restrict__ A_, const int8_t* __restrict__ B_, int* __restrict__ C) {
+TL_DEVICE void gemm_ss_i8(const int8_t* __restrict__ A_, const int8_t* __restrict__ B_, int* __restrict__ C,
+                          int wave_in = -1) {
   constexpr int WM = M / WARP_M, WN = N / WARP_N;
   constexpr int M_REP = WM / MS, N_REP = WN / MS, KS = MS == 16 ? 64 : 32;
   static_assert(WM % MS == 0 && WN % MS == 0 && K % KS == 0, "int8 MFMA tiling");
   const uint8_t* A = reinterpret_cast<const uint8_t*>(A_);
   const uint8_t* B = reinterpret_cast<const uint8_t*>(B_);
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wave = wave_or(wave_in);
   const int wm = wave / WARP_N, wn = wave % WARP_N;
   const int r = lane & (MS - 1), g = MS == 16 ? (lane >> 4) : (lane >> 5);
 #pragma unroll
@@ -449,12 +526,13 @@ TL_DEVICE void gemm_ss_i8(const int8_t* __restrict__ A_, const int8_t* __restric
 // fp32 x fp32 -> fp32 (exact f32 fmaf chain, the f32 VALU rate): v_mfma_f32_16x16x4_f32,
 // lane l holds A[m = l & 15][k = l >> 4] and B[k = l >> 4][n = l & 15]; any operand layout.
 template <int M, int N, int K, int WARP_M, int WARP_N, bool TA, bool TB, int A_COLS, int B_COLS>
-TL_DEVICE void gemm_ss_f32(const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C) {
+TL_DEVICE void gemm_ss_f32(const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C,
+                           int wave_in = -1) {
   constexpr int WM = M / WARP_M, WN = N / WARP_N;
   constexpr int M_REP = WM / 16, N_REP = WN / 16;
   static_assert(WM % 16 == 0 && WN % 16 == 0 && K % 4 == 0, "MFMA 16x16x4 f32 tiling");
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wave = wave_or(wave_in);
   const int wm = wave / WARP_N, wn = wave % WARP_N;
   const int r = lane & 15, g = lane >> 4;
   floatx4* acc = reinterpret_cast<floatx4*>(C);
@@ -541,7 +619,7 @@ template <> struct smfmac_traits<bfloat16_t> {
 template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TA, bool TB, int A_COLS, uint32_t SWZ_A,
           int E_COLS, int B_COLS, uint32_t SWZ_B>
 TL_DEVICE void gemm_sp_ss(const T* __restrict__ A, const int16_t* __restrict__ E, const T* __restrict__ B,
-                          float* __restrict__ C) {
+                          float* __restrict__ C, int wave_in = -1) {
   typedef smfmac_traits<T> ST;
   typedef typename mfma_traits<T>::frag F;
   typedef typename ST::bfrag BF;
@@ -549,7 +627,7 @@ TL_DEVICE void gemm_sp_ss(const T* __restrict__ A, const int16_t* __restrict__ E
   constexpr int M_REP = WM / 16, N_REP = WN / 16, KSTEPS = K / 64;
   static_assert(WM % 16 == 0 && WN % 16 == 0 && K % 64 == 0, "smfmac 16x16x64 tiling");
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wave = wave_or(wave_in);
   const int wm = wave / WARP_N, wn = wave % WARP_N;
   floatx4* acc = reinterpret_cast<floatx4*>(C);
 #pragma unroll

@@ -79,6 +79,15 @@ class PtrDeclStmt(Stmt):
         self.ptr = ptr
 
 
+class ObjDeclStmt(Stmt):
+    """``ctype name;`` — a value of a device-library struct type (e.g. ``tl::ss_frags<...>``, the
+    register fragments a prefetched GEMM keeps across pipeline phases)."""
+
+    def __init__(self, ctype: str, var):
+        self.ctype = ctype
+        self.var = var
+
+
 class AutoLetStmt(Stmt):
     """``const auto name = value;`` for values of device-library struct type."""
 

@@ -41,10 +41,15 @@ def mfma_shape(dtype_bits: int, prefer_32: bool = False) -> Tuple[int, int, int]
 
 
 def compute_warp_partition(M: int, N: int, num_warps: int, policy: int = 0, mtile: int = 16,
-                           ntile: int = 16) -> Tuple[int, int]:
+                           ntile: int = 16, read_cost: Optional[Tuple[int, int]] = None) -> Tuple[int, int]:
     """Split ``num_warps`` waves into ``warp_m x warp_n`` (reference gemm.cc:144-354).
 
     policy: 0 = Square (balance per-wave tile), 1 = FullRow (waves along M), 2 = FullCol (along N).
+    ``read_cost`` = (ds_read instructions per 16 rows of A, per 16 columns of B) per 32-deep K
+    step (1 for a K-contiguous LDS operand read with ds_read_b128, 2 for an MN-contiguous one
+    read with two ds_read_b64_tr_b16): among equally square tilings, the one issuing fewer LDS
+    read instructions wins (256x256 over 8 waves with B [K][N]: 2x4 issues 16 reads per step,
+    4x2 issues 20 -- +1-2 % on the fp16 GEMM, profiles/r3/gemm_prefetch_ab.log).
     """
     cands = []
     for wm in range(1, num_warps + 1):
@@ -65,8 +70,9 @@ def compute_warp_partition(M: int, N: int, num_warps: int, policy: int = 0, mtil
     def score(c):
         wm, wn = c
         tm, tn = M // wm, N // wn
-        # prefer square per-wave tiles, then more waves along M (A-operand reuse)
-        return (abs(tm - tn) / max(tm, tn), -wm)
+        reads = 0 if read_cost is None else (tm // 16) * read_cost[0] + (tn // 16) * read_cost[1]
+        # prefer square per-wave tiles, then fewer LDS read instructions, then more waves along M
+        return (abs(tm - tn) / max(tm, tn), reads, -wm)
 
     return min(cands, key=score)
 

@@ -84,6 +84,7 @@ class _KSplit(Mutator):
     def __init__(self, mode=True):
         self.mode = mode
         self.new_allocs = {}  # old buffer -> (half0, half1)
+        self.pairs = {}       # A tile <-> B tile of one split GEMM
         self.applied = 0
 
     def visit_ForStmt(self, s: S.ForStmt):
@@ -147,6 +148,7 @@ class _KSplit(Mutator):
             new.append(S.TileOpStmt(gi))
         for buf in (A, B):
             self.new_allocs[buf] = parts[buf][:2]
+        self.pairs[A], self.pairs[B] = B, A
         self.applied += 1
         ann = dict(s.annotations)
         ann["phased"] = self.mode
@@ -157,16 +159,27 @@ class _KSplit(Mutator):
 
 
 class _AllocSplit(Mutator):
+    """Allocates the halves as A_k0, B_k0, A_k1, B_k1 at the first of the two tiles' allocations:
+    the LDS arena follows allocation order, so the A and B tiles one phase reads sit within
+    64 KiB of each other and every ds_read of the phase addresses them from one base register
+    with the 16-bit immediate offset (A_k1 and B_k1 64 KiB apart cost 2 VALU per read pair)."""
 
-    def __init__(self, new_allocs, used):
+    def __init__(self, new_allocs, used, pairs):
         self.new_allocs = new_allocs
         self.used = used
+        self.pairs = pairs
+        self.done = set()
 
     def visit_AllocStmt(self, s):
         if s.buffer in self.new_allocs:
-            h0, h1 = self.new_allocs[s.buffer]
             keep = [s] if s.buffer in self.used else []
-            return S.seq(*(keep + [S.AllocStmt(h0), S.AllocStmt(h1)]))
+            if s.buffer in self.done:
+                return S.seq(*keep) if keep else S.SeqStmt([])
+            other = self.pairs.get(s.buffer)
+            first = [s.buffer] + ([other] if other is not None and other in self.new_allocs else [])
+            order = [self.new_allocs[b][0] for b in first] + [self.new_allocs[b][1] for b in first]
+            self.done.update(first)
+            return S.seq(*(keep + [S.AllocStmt(h) for h in order]))
         return s
 
 
@@ -178,4 +191,4 @@ def split_gemm_k_halves(kernel: S.KernelStmt, mode=True) -> S.KernelStmt:
         return kernel
     from .pipeline import _referenced_buffers
     used = _referenced_buffers(k)
-    return _AllocSplit(ks.new_allocs, used).stmt(k)
+    return _AllocSplit(ks.new_allocs, used, ks.pairs).stmt(k)

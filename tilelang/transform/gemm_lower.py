@@ -243,7 +243,12 @@ def gemm_plan(op: O.GemmOp, num_threads: int, target=None, a_layout: Optional[Fr
         if getattr(op, "mfma_shape", None) == "32x32":
             raise ValueError(f"T.gemm(mfma_shape='32x32'): a {M}x{N} tile over {nw} waves needs per-wave tiles "
                              f"that are multiples of 32 and K % 16 == 0")
-    warp_m, warp_n = MF.compute_warp_partition(M, N, nw, op.policy)
+    rc = None
+    if eb == 16 and A.scope == "shared" and B.scope == "shared" and getattr(op, "khalf", None) is not None:
+        # only for the K-split GEMM main loop (transform/gemm_ksplit.py): other GEMMs that share
+        # an accumulator fragment must keep one partition whatever their operand orientation
+        rc = (2 if op.trans_A else 1, 1 if op.trans_B else 2)
+    warp_m, warp_n = MF.compute_warp_partition(M, N, nw, op.policy, read_cost=rc)
     plan.update(warp_m=warp_m, warp_n=warp_n, mfma=(16, 16, 32))
     plan["c_layout"] = MF.mfma_c_fragment(M, N, warp_m, warp_n)
     if K % 32:

@@ -997,14 +997,14 @@ class TileOpLowerer(Mutator):
         pb = self._operand_ptr(op.B)
         if plan.get("int8"):
             pa = self._operand_ptr(op.A)
-            out.append(L.CallStmt("tl::gemm_ss_i8", [pa, pb, L.BufferPtr(cl, 0)], [
+            out.append(L.CallStmt("tl::gemm_ss_i8", [pa, pb, L.BufferPtr(cl, 0), ctx.wave_expr()], [
                 plan["mfma"][0], plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"],
                 A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
                 B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u"]))
             return S.SeqStmt(out)
         if plan.get("f32"):
             pa = self._operand_ptr(op.A)
-            out.append(L.CallStmt("tl::gemm_ss_f32", [pa, pb, L.BufferPtr(cl, 0)], [
+            out.append(L.CallStmt("tl::gemm_ss_f32", [pa, pb, L.BufferPtr(cl, 0), ctx.wave_expr()], [
                 plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_A), _b(op.trans_B),
                 A.static_shape()[-1], B.static_shape()[-1]]))
             return S.SeqStmt(out)
@@ -1014,14 +1014,15 @@ class TileOpLowerer(Mutator):
                                 "memory")
         if plan.get("mfma") == (32, 32, 16):
             pa = self._operand_ptr(op.A)
-            out.append(L.CallStmt("tl::gemm_ss_32", [pa, pb, L.BufferPtr(cl, 0)] + vm, [
+            out.append(L.CallStmt("tl::gemm_ss_32", [pa, pb, L.BufferPtr(cl, 0)] + (vm or [IntImm(0x3fffffff)]) +
+                                  [ctx.wave_expr()], [
                 ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_A),
                 _b(op.trans_B), A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
                 B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u"]))
             return S.SeqStmt(out)
         if A.dtype.bits == 8:
             pa = self._operand_ptr(op.A)
-            out.append(L.CallStmt("tl::gemm_ss_f8", [pa, pb, L.BufferPtr(cl, 0)], [
+            out.append(L.CallStmt("tl::gemm_ss_f8", [pa, pb, L.BufferPtr(cl, 0), ctx.wave_expr()], [
                 _dt.hip_type(A.dtype), _dt.hip_type(B.dtype), plan["M"], plan["N"], plan["K"], plan["warp_m"],
                 plan["warp_n"], A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
                 B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u"
@@ -1029,11 +1030,35 @@ class TileOpLowerer(Mutator):
             return S.SeqStmt(out)
         b_cols = B.static_shape()[-1]
         swz_b = gemm_lower.encode_swizzle(B.layout)
+        frag = getattr(op, "frag", None)
+        if frag is not None:
+            # register-prefetched K-half schedule (transform/pipeline.py _prefetch_schedule)
+            if A.scope != "shared" or vm:
+                raise LoweringError("prefetched T.gemm needs both operands in shared memory")
+            mode, var = frag
+            shape = [ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"]]
+            if mode == "decl":
+                return L.ObjDeclStmt(f"tl::ss_frags<{', '.join(str(x) for x in shape)}>", var)
+            if mode == "load":
+                out.append(L.CallStmt("tl::gemm_ss_load", [self._operand_ptr(op.A), pb, var, ctx.wave_expr()], shape + [
+                    _b(op.trans_A), _b(op.trans_B), A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
+                    b_cols, f"{swz_b}u"]))
+                return S.SeqStmt(out)
+            # mma: interleaved with the load the schedule issued just before it (same phase)
+            ksteps = plan["K"] // 32
+            m_rep = plan["M"] // plan["warp_m"] // 16
+            n_rep = plan["N"] // plan["warp_n"] // 16
+            nload = ksteps * (m_rep * (2 if op.trans_A else 1) + n_rep * (1 if op.trans_B else 2))
+            if getattr(ctx.target, "gemm_interleave", None) is False:
+                nload = 0
+            out.append(L.CallStmt("tl::gemm_ss_mma", [var, L.BufferPtr(cl, 0)], shape + [nload]))
+            return S.SeqStmt(out)
         if A.scope == "shared":
             pa = self._operand_ptr(op.A)
             a_cols = A.static_shape()[-1]
             swz_a = gemm_lower.encode_swizzle(A.layout)
-            out.append(L.CallStmt("tl::gemm_ss", [pa, pb, L.BufferPtr(cl, 0)] + vm, [
+            out.append(L.CallStmt("tl::gemm_ss", [pa, pb, L.BufferPtr(cl, 0)] + (vm or [IntImm(0x3fffffff)]) +
+                                  [ctx.wave_expr()], [
                 ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_A),
                 _b(op.trans_B), a_cols, f"{swz_a}u", b_cols, f"{swz_b}u"
             ]))
@@ -1041,7 +1066,7 @@ class TileOpLowerer(Mutator):
             al = ctx.local_of(A)
             if op.trans_A:
                 raise LoweringError("register A operand cannot be transposed")
-            out.append(L.CallStmt("tl::gemm_rs", [L.BufferPtr(al, 0), pb, L.BufferPtr(cl, 0)], [
+            out.append(L.CallStmt("tl::gemm_rs", [L.BufferPtr(al, 0), pb, L.BufferPtr(cl, 0), ctx.wave_expr()], [
                 ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_B), b_cols,
                 f"{swz_b}u", plan.get("a_kperm", 0)
             ]))
@@ -1064,7 +1089,7 @@ class TileOpLowerer(Mutator):
             return S.SeqStmt(out)
         targs += [plan["warp_m"], plan["warp_n"], A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
                   B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u", sa_shape[-1], sb_shape[-1]]
-        out.append(L.CallStmt("tl::gemm_ss_mx", [pa, pb, psa, psb, L.BufferPtr(cl, 0)], targs))
+        out.append(L.CallStmt("tl::gemm_ss_mx", [pa, pb, psa, psb, L.BufferPtr(cl, 0), self.ctx.wave_expr()], targs))
         return S.SeqStmt(out)
 
     def _lower_sp_gemm(self, op: O.GemmOp, plan, cl, out):
@@ -1080,7 +1105,7 @@ class TileOpLowerer(Mutator):
                 ctype, plan["M"], plan["N"], plan["K"], int(op.trans_A), int(op.trans_B), A.static_shape()[-1],
                 e_shape[-1], B.static_shape()[-1]]))
             return S.SeqStmt(out)
-        out.append(L.CallStmt("tl::gemm_sp_ss", [pa, pe, pb, L.BufferPtr(cl, 0)], [
+        out.append(L.CallStmt("tl::gemm_sp_ss", [pa, pe, pb, L.BufferPtr(cl, 0), self.ctx.wave_expr()], [
             ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_A), _b(op.trans_B),
             A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u", e_shape[-1],
             B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u"]))

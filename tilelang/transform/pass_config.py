@@ -42,6 +42,9 @@ class PassConfigKey(str, Enum):
     TL_LDS_REUSE = "tl.lds_reuse"                  # liveness-based LDS arena sharing (default on)
     TL_MFMA_SHAPE = "tl.mfma_shape"                # "16x16" (default) or "32x32" MFMA tiles
     TL_GEMM_PHASED = "tl.gemm_phased"              # K-half phased GEMM main loop (gemm_ksplit)
+    TL_GEMM_PREFETCH = "tl.gemm_prefetch"          # fragments read one phase ahead of their MFMAs
+    TL_GEMM_INTERLEAVE = "tl.gemm_interleave"      # 1 MFMA : 1 ds_read sched_group_barrier pattern
+    TL_DISABLE_ADDRESS_HOIST = "tl.disable_address_hoist"  # keep LDS-DMA source addresses in the loop
 
     def __str__(self):
         return self.value
@@ -73,6 +76,13 @@ EFFECT = {
     "tl.gemm_phased": "default on; False keeps BK=64 16-bit GEMM main loops whole instead of splitting them "
                       "into K halves refilled one phase apart (transform/gemm_ksplit.py + the phased "
                       "pipeline schedule); 'prio' also raises wave priority around the MFMA clusters",
+    "tl.gemm_prefetch": "default on; False: in the phased K-half schedule, read each half's MFMA fragments "
+                        "after its own barrier instead of one phase ahead (transform/pipeline.py "
+                        "_prefetch_schedule, tl::gemm_ss_load / gemm_ss_mma)",
+    "tl.disable_address_hoist": "True keeps the per-thread LDS-DMA source address arithmetic inside pipelined "
+                                "loops (transform/hoist_addresses.py hoists it by default)",
+    "tl.gemm_interleave": "default on; False drops the 1 MFMA : 1 ds_read sched_group_barrier pattern of the "
+                          "prefetched GEMM (the compiler schedules the two streams itself)",
 }
 
 # NVIDIA-only features / TVM passes that do not exist here: the value meaning "off" is what

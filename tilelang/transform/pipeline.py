@@ -545,6 +545,10 @@ def _phased_schedule(self, loop, asyncs, issue_async, consumer_stmts, mapping, n
     def wait(more, n_more, n_last):
         return S.IfStmt(more, L.CallStmt("tl::wait_vmcnt", [], [n_more]), L.CallStmt("tl::wait_vmcnt", [], [n_last]))
 
+    if loop.annotations.get("phased") is True and getattr(self.target, "gemm_prefetch", None) is not False and \
+            all(_prefetchable(g.op, self.target) for g in gemms):
+        return _prefetch_schedule(self, loop, gemms, newbufs, issue, wait, idx_pre, h, kk, n, nv)
+
     prologue = idx_pre + [issue(0, IntImm(0), IntImm(0)), issue(1, IntImm(0), IntImm(0))]
     if nv is None or nv > 1:
         prologue.append(S.IfStmt(binop("<", IntImm(1), n), issue(0, IntImm(1), IntImm(1))) if nv is None
@@ -556,6 +560,76 @@ def _phased_schedule(self, loop, asyncs, issue_async, consumer_stmts, mapping, n
             S.IfStmt(more, issue(1, t1, binop("%", t1, 2))), g0,
             wait(more, 2 * h, 0), L.CallStmt("tl::barrier_raw", []),
             S.IfStmt(binop("<", t2, n), issue(0, t2, binop("%", kk, 2))), g1]
+    new_loop = S.ForStmt(k, loop.min, loop.extent, "serial", S.SeqStmt(body), {"pipelined": 2, "phased": True})
+    self.replaced = getattr(self, "replaced", {})
+    for B, NB in newbufs.items():
+        lst = self.replaced.setdefault(B, [])
+        if NB not in lst:
+            lst.append(NB)
+    return S.SeqStmt(prologue + [new_loop, L.CallStmt("tl::barrier_raw", [])])
+
+
+def _prefetchable(op, target) -> bool:
+    """A K-half GEMM whose fragments can be read one phase ahead (``tl::gemm_ss_load`` /
+    ``gemm_ss_mma``): 16-bit operands, both in LDS, the 16x16x32 MFMA, nothing else fused."""
+    from ..ir import dtypes as _dt
+    if not isinstance(op, O.GemmOp) or op.is_mx or op.is_sp or getattr(op, "valid_m", None) is not None:
+        return False
+    if op.clear_accum not in (False, None, 0):
+        return False
+    if (getattr(op, "mfma_shape", None) or getattr(target, "mfma_shape", None)) == "32x32":
+        return False
+    A, B = op.A.buffer, op.B.buffer
+    return A.scope == "shared" and B.scope == "shared" and A.dtype == B.dtype and \
+        A.dtype in (_dt.float16, _dt.bfloat16)
+
+
+def _prefetch_schedule(self, loop, gemms, newbufs, issue, wait, idx_pre, h, kk, n, nv):
+    """Register-prefetched K-half schedule.  Half-tiles go to two LDS banks (even K halves in
+    bank 0, odd in bank 1), each two stages deep; the fragments of a half are read from LDS in
+    the phase BEFORE its MFMAs, while the previous half's MFMAs run:
+
+        prologue: issue tiles 0, 1;  wait(0a) barrier;  F0 <- frags(bank0[0])
+        iteration t (s = t % 2):
+          wait(t.b)   barrier | issue (t+2).a -> bank0[s] | F1 <- frags(bank1[s])   | mma(F0)
+          wait(t+1.a) barrier | issue (t+2).b -> bank1[s] | F0 <- frags(bank0[s^1]) | mma(F1)
+
+    A phase refills the slot of its own bank that the previous phase read and reads the other
+    bank, so the ds_reads provably miss the LDS-DMA just issued (no compiler vmcnt(0)); every
+    wait is counted (two half-tiles in flight across each barrier).  Measured on gfx950:
+    fp16 4096^3 1057 -> 1225 TF (profiles/r3/gemm_prefetch_ab.log)."""
+    from ..ir.expr import Var
+    from ..ir import dtypes as _dt
+    import copy
+    k = loop.var
+    self.key += 1
+    f0, f1 = Var(f"tl_frag{self.key}_0", _dt.handle), Var(f"tl_frag{self.key}_1", _dt.handle)
+
+    def at(g, stage, mode, var):
+        st = BufferReplacer({B: (NB, [stage]) for B, NB in newbufs.items()}).stmt(g)
+        op = copy.copy(st.op)
+        op.frag = (mode, var)
+        return S.TileOpStmt(op)
+
+    g0, g1 = gemms
+    if getattr(g0.op, "khalf", 0) == 1:
+        g0, g1 = g1, g0
+    zero, one = IntImm(0), IntImm(1)
+    prologue = idx_pre + [issue(0, zero, zero), issue(1, zero, zero)]
+    if nv is None or nv > 1:
+        two = S.seq(issue(0, one, one), issue(1, one, one))
+        prologue.append(S.IfStmt(binop("<", one, n), two) if nv is None else two)
+    prologue += [at(g0, zero, "decl", f0), at(g0, zero, "decl", f1)]
+    prologue.append(wait(binop("<", one, n), 3 * h, h))
+    prologue += [L.CallStmt("tl::barrier_raw", []), at(g0, zero, "load", f0)]
+    t1, t2 = binop("+", kk, 1), binop("+", kk, 2)
+    more, more2 = binop("<", t1, n), binop("<", t2, n)
+    s_, s1 = binop("%", kk, 2), binop("%", t1, 2)
+    odd_wait = S.IfStmt(more2, L.CallStmt("tl::wait_vmcnt", [], [2 * h]), wait(more, h, 0))
+    body = [wait(more, 2 * h, 0), L.CallStmt("tl::barrier_raw", []),
+            S.IfStmt(more2, issue(0, t2, s_)), at(g1, s_, "load", f1), at(g0, s_, "mma", f0),
+            odd_wait, L.CallStmt("tl::barrier_raw", []),
+            S.IfStmt(more2, issue(1, t2, s_)), at(g0, s1, "load", f0), at(g1, s_, "mma", f1)]
     new_loop = S.ForStmt(k, loop.min, loop.extent, "serial", S.SeqStmt(body), {"pipelined": 2, "phased": True})
     self.replaced = getattr(self, "replaced", {})
     for B, NB in newbufs.items():

@@ -48,7 +48,10 @@ class Mutator:
 
     def default(self, s):
         if isinstance(s, S.SeqStmt):
-            return S.SeqStmt([self.stmt(c) for c in s.stmts])
+            out = S.SeqStmt([self.stmt(c) for c in s.stmts])
+            if getattr(s, "scoped", False):
+                out.scoped = True  # a C++ block: its let bindings must not leak into siblings
+            return out
         if isinstance(s, S.ForStmt):
             return S.ForStmt(s.var, self.expr(s.min), self.expr(s.extent), s.kind, self.stmt(s.body), s.annotations)
         if isinstance(s, S.WhileStmt):
