@@ -53,3 +53,21 @@ def test_tensor_and_expert_parallel_match_single_rank(tmp_path):
     port = 29500 + (os.getpid() % 2000)
     mp.spawn(_tp_worker, args=(2, port, toks, out), nprocs=2, join=True)
     torch.testing.assert_close(torch.load(out, weights_only=True), ref, rtol=3e-2, atol=3e-2)
+
+
+def test_fp8_checkpoint_format_model():
+    """gemm_impl='fp8': every projection is fp8 e4m3 + 128x128 block scales, run as act_quant +
+    block-scaled fp8 GEMM (reference model.py ``linear``); logits stay close to the bf16 model
+    built from the same weights (fp8 weight/activation rounding only)."""
+    from tilelang.models import deepseek_v32 as D
+    toks = torch.randint(0, 512, (2, 8), generator=torch.Generator().manual_seed(5))
+    ref = Transformer(ModelArgs.tiny(), seed=0, device="cpu")(toks, 0)
+    m = Transformer(ModelArgs.tiny(gemm_impl="fp8"), seed=0, device="cpu")
+    fp8_layers = [x for x in m.modules() if isinstance(x, D.Linear) and x.scale is not None]
+    assert len(fp8_layers) > 10 and all(x.weight.dtype == torch.float8_e4m3fn for x in fp8_layers)
+    assert m.head.scale is None  # the output head stays bf16, as the reference's
+    out = m(toks, 0)
+    rel = (out.float() - ref.float()).norm() / ref.float().norm()
+    assert rel < 0.15, rel
+    m2 = Transformer(ModelArgs.tiny(gemm_impl="fp8", scale_fmt="ue8m0"), seed=0, device="cpu")
+    assert torch.isfinite(m2(toks, 0)).all()

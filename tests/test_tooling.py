@@ -130,3 +130,27 @@ def test_math_testing_utils_libinfo():
             assert [int(x) for x in retrieve_shape(A[0:16, :])] == [16, 64]
             T.copy(A[0:16, :], s)
             T.copy(s, r)
+
+
+def test_precision_probe_cpu():
+    """maint/precision counterpart: the probe runs every op and reports float64-referenced errors."""
+    from tilelang.tools import precision as P
+    res = P.run("cpu", n=1 << 12, ops=["exp", "div", "log", "rsqrt"])
+    for op, rows in res.items():
+        assert set(rows) == {"TileLang (precise)", "TileLang (fast math)", "PyTorch"}
+        assert rows["TileLang (precise)"]["max_ulp"] <= 4.0, (op, rows)
+    md = P.to_markdown(res, "cpu")
+    assert "### exp" in md and "Max ULP" in md
+
+
+@pytest.mark.gpu
+def test_precision_probe_gpu():
+    """gfx950: precise OCML paths within a few ULP; the hardware fast-math transcendentals the
+    attention kernels use stay within float32-softmax tolerance."""
+    from tilelang.tools import precision as P
+    res = P.run("cuda", n=1 << 16)
+    for op, rows in res.items():
+        assert rows["TileLang (precise)"]["max_ulp"] <= 4.0, (op, rows["TileLang (precise)"])
+        assert rows["TileLang (precise)"]["nonfinite"] == 0
+    assert res["exp"]["TileLang (fast math)"]["max_rel"] < 1e-5
+    assert res["exp2"]["TileLang (fast math)"]["max_rel"] < 1e-5

@@ -17,9 +17,15 @@ reference's only torch.distributed workload).  Same architecture and parallel de
 
 MI355X-first choices: one process per GPU (torchrun / ``torch.distributed``, backend ``nccl`` =
 RCCL over xGMI); every projection is a tilelang MFMA GEMM; fp8 is OCP e4m3 (gfx950), not fnuz.
+``ModelArgs.gemm_impl = "fp8"`` (the reference's ``dtype = "fp8"``) stores every projection weight
+in the checkpoint's fp8 format -- OCP e4m3 with one fp32 scale per 128x128 block -- and runs it
+as ``act_quant`` (per-token, 128-wide groups; ``scale_fmt="ue8m0"`` for power-of-two scales) +
+the block-scaled fp8 GEMM (``tilelang.ops.fp8_gemm``, 2xAcc promotion), as the reference's
+``linear`` does (model.py:140-168).  The absorbed MLA up-projection dequantises ``wkv_b``
+(``weight_dequant``, model.py:514); routed experts stay on the bf16 grouped-GEMM kernels.
+
 Simplifications (documented, weights are random -- no checkpoint is available): plain RoPE
-(no YaRN rescaling), no Hadamard rotation before the indexer's fp8 cast, bf16 weights instead
-of the fp8 block-scaled checkpoint format.
+(no YaRN rescaling), no Hadamard rotation before the indexer's fp8 cast.
 """
 from __future__ import annotations
 
@@ -68,6 +74,8 @@ class ModelArgs:
     rope_theta: float = 10000.0
     norm_eps: float = 1e-6
     block_M: int = 128  # MoE row tile
+    gemm_impl: str = "bf16"  # "fp8": block-scaled fp8 projection weights (the checkpoint format)
+    scale_fmt: Optional[str] = None  # "ue8m0": power-of-two activation scales
 
     @staticmethod
     def from_json(path: str, **over) -> "ModelArgs":
@@ -119,6 +127,9 @@ class _Init:
 
 
 class Linear(nn.Module):
+    # set by Transformer from ModelArgs.gemm_impl / scale_fmt (the reference's Linear.dtype)
+    fp8 = False
+    scale_fmt: Optional[str] = None
 
     def __init__(self, init: _Init, in_features: int, out_features: int, dtype, part_out=1, part_in=1, rank=0):
         super().__init__()
@@ -129,10 +140,32 @@ class Linear(nn.Module):
         if part_in > 1:
             n = in_features // part_in
             w = w[:, rank * n:(rank + 1) * n]
-        self.weight = nn.Parameter(w.contiguous(), requires_grad=False)
+        self.scale = None
+        if Linear.fp8 and dtype != torch.float32 and w.shape[1] % 128 == 0:
+            # the checkpoint format: fp8 e4m3 + one fp32 scale per 128x128 block of this rank's slice
+            from ..ops.fp8_gemm import weight_quant
+            wq, ws = weight_quant(w.contiguous())
+            self.weight = nn.Parameter(wq, requires_grad=False)
+            self.scale = nn.Parameter(ws, requires_grad=False)
+            self.out_dtype = dtype
+        else:
+            self.weight = nn.Parameter(w.contiguous(), requires_grad=False)
+
+    def _mm(self, x):
+        if self.scale is None:
+            return linear(x, self.weight)
+        from ..ops.fp8_gemm import fp8_linear
+        return fp8_linear(x.to(self.out_dtype), self.weight, self.scale, Linear.scale_fmt == "ue8m0")
+
+    def dequant_weight(self) -> torch.Tensor:
+        """The weight in its compute dtype (fp8 blocks rescaled: reference ``weight_dequant``)."""
+        if self.scale is None:
+            return self.weight
+        from ..ops.fp8_gemm import weight_dequant
+        return weight_dequant(self.weight, self.scale).to(self.out_dtype)
 
     def forward(self, x):
-        return linear(x, self.weight)
+        return self._mm(x)
 
 
 def ColumnParallelLinear(init, in_features, out_features, dtype):
@@ -150,7 +183,7 @@ class RowParallelLinear(Linear):
         self.reduce_output = reduce_output
 
     def forward(self, x):
-        y = linear(x, self.weight)
+        y = self._mm(x)
         if self.reduce_output and _world()[0] > 1:
             y = _all_reduce(y.float()).to(x.dtype)
         return y
@@ -289,7 +322,7 @@ class MLA(nn.Module):
         self.kv_cache[:b, start_pos:end] = self.kv_norm(latent.contiguous())
         self.pe_cache[:b, start_pos:end] = apply_rotary_emb(k_pe.contiguous().unsqueeze(2), freqs).squeeze(2)
         # absorb W_uk into the query: q_lat = q_nope @ W_uk  (per head)
-        wkv_b = self.wkv_b.weight.view(self.n_local_heads, self.nope + self.vdim, self.kv_lora)
+        wkv_b = self.wkv_b.dequant_weight().view(self.n_local_heads, self.nope + self.vdim, self.kv_lora)
         q_lat = torch.einsum("bshd,hdc->bshc", q_nope.float(), wkv_b[:, :self.nope].float()).to(x.dtype)
         qf = torch.cat([q_lat, q_pe], -1).contiguous()                          # [b, s, h, 576]
         kvf = torch.cat([self.kv_cache[:b, :end], self.pe_cache[:b, :end]], -1).unsqueeze(2).contiguous()
@@ -405,9 +438,14 @@ class Transformer(nn.Module):
         super().__init__()
         init = _Init(seed)
         self.args = args
+        if args.gemm_impl not in ("bf16", "fp8"):
+            raise ValueError(f"gemm_impl must be 'bf16' or 'fp8', got {args.gemm_impl!r}")
+        Linear.fp8 = args.gemm_impl == "fp8"
+        Linear.scale_fmt = args.scale_fmt
         self.embed = ParallelEmbedding(init, args.vocab_size, args.dim, args.dtype)
         self.layers = nn.ModuleList([Block(init, i, args) for i in range(args.n_layers)])
         self.norm = RMSNorm(args.dim, args.norm_eps, args.dtype)
+        Linear.fp8 = False  # the output head stays in the compute dtype (as the reference)
         self.head = ColumnParallelLinear(init, args.dim, args.vocab_size, args.dtype)
         self.register_buffer("freqs_cis", precompute_freqs_cis(args.qk_rope_head_dim, args.max_seq_len,
                                                                 args.rope_theta), persistent=False)
