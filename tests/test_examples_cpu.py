@@ -545,3 +545,32 @@ def test_gqa_bwd_kv_split_cpu():
     tilelang.compile(f, target="cpu")(q, k, v, do, lse, delta, dkp, dvp)
     torch.testing.assert_close(dkp.sum(0), kf.grad, rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(dvp.sum(0), vf.grad, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("block_N,stages,qk_fp8", [(64, 1, True), (32, 2, True), (32, 2, False)])
+def test_mla_decode_kv_fp8_cpu(block_N, stages, qk_fp8):
+    """fp8 latent cache: fp8 (or bf16) score GEMM + widened V tile, against fp32 over the dequantised
+    cache (with the kernel's fp8 Q when ``qk_fp8``)."""
+    from example_mla_decode_kv_fp8 import mla_decode_kv_fp8, quantize_kv, ref_program
+    b, h, S, D, P, ns = 2, 64, 128, 128, 32, 2
+    k = _both(mla_decode_kv_fp8, b, h, S, D, P, block_N, 64, ns, num_stages=stages, qk_fp8=qk_fp8)
+    q, qpe = torch.randn(b, h, D).bfloat16(), torch.randn(b, h, P).bfloat16()
+    kv8, s = quantize_kv(torch.randn(b, S, 1, D) * 2)
+    kpe = torch.randn(b, S, 1, P).bfloat16()
+    o = k(q, qpe, kv8, kpe, s, torch.empty(b, h, ns), torch.empty(b, h, ns, D))
+    torch.testing.assert_close(o.float(), ref_program(q, qpe, kv8, s, kpe, qk_fp8), rtol=2e-2, atol=2e-2)
+    r = ref_program(q, qpe, kv8, s, kpe)
+    assert (o.float() - r).norm() / r.norm() < 5e-2
+
+
+def test_group_per_split_token_cast_cpu():
+    from example_group_per_split_token_cast_to_fp8 import group_per_split_token_cast_to_fp8, ref_program
+    sizes = [10, 0, 25, 6]
+    M, N, M_max = sum(sizes), 256, 32
+    x = torch.randn(M, N).bfloat16()
+    bs = torch.tensor(sizes, dtype=torch.int32)
+    q, s = _both(group_per_split_token_cast_to_fp8, M, M_max, N, 4, 8)(x, bs)
+    rq, rs = ref_program(x, bs, M_max)
+    torch.testing.assert_close(s, rs, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(q.float(), rq.float(), rtol=0.13, atol=0.01)
+    assert q[1].float().abs().max() == 0 and q[0, 10:].float().abs().max() == 0

@@ -48,3 +48,39 @@ def test_mla_decode_persistent(batch, heads, kv_ctx, num_split):
     part = torch.empty(batch, heads, num_split, 512, device="cuda")
     out = k(q, q_pe, kv, k_pe, glse, part)
     torch.testing.assert_close(out.float(), ref_program(q, q_pe, kv, k_pe).float(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("batch,heads,kv_ctx,num_split,block_N,stages,qk_fp8",
+                         [(4, 128, 1024, 2, 64, 1, True), (3, 64, 512, 1, 32, 2, True), (2, 128, 2048, 4, 32, 2, True),
+                          (2, 128, 1024, 2, 32, 2, False)])
+def test_mla_decode_kv_fp8(batch, heads, kv_ctx, num_split, block_N, stages, qk_fp8):
+    """fp8 (OCP e4m3) latent cache: scaled-MFMA scores vs an fp32 reference over the dequantised cache."""
+    from example_mla_decode_kv_fp8 import mla_decode_kv_fp8, quantize_kv, ref_program
+    k = mla_decode_kv_fp8(batch, heads, kv_ctx, 512, 64, block_N=block_N, num_split=num_split, num_stages=stages,
+                          qk_fp8=qk_fp8)
+    src = k.get_kernel_source()
+    assert ("gemm_ss_f8" in src) == qk_fp8
+    q = torch.randn(batch, heads, 512, device="cuda", dtype=torch.bfloat16)
+    q_pe = torch.randn(batch, heads, 64, device="cuda", dtype=torch.bfloat16)
+    kv8, s = quantize_kv(torch.randn(batch, kv_ctx, 1, 512, device="cuda") * 3.0)
+    k_pe = torch.randn(batch, kv_ctx, 1, 64, device="cuda", dtype=torch.bfloat16)
+    glse = torch.empty(batch, heads, num_split, device="cuda")
+    part = torch.empty(batch, heads, num_split, 512, device="cuda")
+    out = k(q, q_pe, kv8, k_pe, s, glse, part)
+    torch.testing.assert_close(out.float(), ref_program(q, q_pe, kv8, s, k_pe, qk_fp8), rtol=2e-2, atol=2e-2)
+    ref = ref_program(q, q_pe, kv8, s, k_pe)
+    assert (out.float() - ref).norm() / ref.norm() < 5e-2
+
+
+def test_group_per_split_token_cast_gpu():
+    from example_group_per_split_token_cast_to_fp8 import group_per_split_token_cast_to_fp8, ref_program
+    sizes = [100, 0, 257, 64]
+    M, N, M_max = sum(sizes), 1024, 320
+    x = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    bs = torch.tensor(sizes, dtype=torch.int32, device="cuda")
+    k = group_per_split_token_cast_to_fp8(M, M_max, N, len(sizes), 8)
+    q, s = k(x, bs)
+    rq, rs = ref_program(x, bs, M_max)
+    torch.testing.assert_close(s, rs, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(q.float(), rq.float(), rtol=0.13, atol=0.01)  # one e4m3 ulp (rounding ties)
+    assert q[1].float().abs().max() == 0 and q[0, 100:].float().abs().max() == 0  # padding rows are zero
