@@ -1,80 +1,108 @@
-"""GEMM written with the user-level MFMA emitter (reference: examples/gemm/example_gemm_intrinsics.py).
+"""GEMM written with the user-level MFMA emitter (reference: examples/gemm/example_gemm_intrinsics.py,
+testing/python/amd/test_tilelang_gemm_mfma_intrinsic.py / _preshuffle.py).
 
-The tile loop stages A/B into LDS with ``T.Parallel`` copies, then for every 32-deep (64 for
-int8) K step each wave loads its register fragments with ``ldmatrix_a/b`` and issues one
-``v_mfma_*_16x16x*`` per warp-tile pair through ``mma``; ``stmatrix`` writes the accumulators
-to an LDS tile in the reference's [M/16, N/16, 16, 16] layout, copied out by a ``T.Parallel``
-store.  ``T.gemm`` does all of this (plus swizzles, LDS-DMA and the phased schedule) by itself;
-this form is for programs that need to own the instruction stream.
+The tile loop stages A/B into XOR-swizzled LDS tiles with ``T.copy`` (LDS-DMA, pipelined), then
+for every K step each wave loads its register fragments with ``ldmatrix_a/b`` (16-byte runs)
+and issues its MFMAs through ``mfma``; ``stmatrix`` writes the accumulators straight to C.
+``T.gemm`` does all of this (plus the phased K-half schedule) by itself; this form is for programs
+that need to own the instruction stream.
+
+``b_preshuffle``: B is stored tile-major (``shuffle_weight``) and each wave loads its fragments
+directly from global memory (coalesced 1 KiB per wave and tile), so only A goes through LDS.
 """
 import argparse
 
 import tilelang
 import tilelang.language as T
-from tilelang.intrinsics import MatrixCoreIntrinEmitter
+from tilelang.intrinsics import MatrixCoreIntrinEmitter, make_mfma_swizzle_layout
 
 
 @tilelang.jit(out_idx=[2])
 def tl_matmul(M, N, K, in_dtype="float16", out_dtype="float16", accum_dtype="float32", block_row_warps=2,
-              block_col_warps=2, warp_row_tiles=64, warp_col_tiles=64, chunk=None, stage=2):
-    if chunk is None:
-        chunk = 64 if in_dtype == "int8" else 32
-    emitter = MatrixCoreIntrinEmitter(in_dtype, in_dtype, accum_dtype, a_transposed=False, b_transposed=True,
+              block_col_warps=4, warp_row_tiles=128, warp_col_tiles=64, chunk=None, stage=2, micro_size=32,
+              k_pack=1, b_preshuffle=False, b_transposed=True, fp8_k_dim=None):
+    emitter = MatrixCoreIntrinEmitter(in_dtype, in_dtype, accum_dtype, a_transposed=False, b_transposed=b_transposed,
                                       block_row_warps=block_row_warps, block_col_warps=block_col_warps,
-                                      warp_row_tiles=warp_row_tiles, warp_col_tiles=warp_col_tiles, chunk=chunk)
+                                      warp_row_tiles=warp_row_tiles, warp_col_tiles=warp_col_tiles,
+                                      chunk=chunk or 1 << 30, micro_size=micro_size, k_pack=k_pack,
+                                      b_preshuffle=b_preshuffle, fp8_k_dim=fp8_k_dim)
+    pk = emitter.micro_size_k * k_pack
+    if chunk is None:
+        chunk = max(pk, 128 // (1 if in_dtype.startswith(("float8", "int8")) else 2))
+    emitter.chunk = chunk
+    assert chunk % pk == 0
     block_M = block_row_warps * warp_row_tiles
     block_N = block_col_warps * warp_col_tiles
     block_K = chunk
-    C_shared_shape = (block_M // 16, block_N // 16, 16, 16)
+    ms = micro_size
+    if b_preshuffle:
+        B_shape = (N // ms, K // pk, ms, pk) if b_transposed else (K // pk, N // ms, pk, ms)
+    else:
+        B_shape = (N, K) if b_transposed else (K, N)
+    B_sh = (block_N, block_K) if b_transposed else (block_K, block_N)
 
     @T.prim_func
-    def gemm_intrinsics(A: T.Tensor((M, K), in_dtype), B: T.Tensor((N, K), in_dtype),
+    def gemm_intrinsics(A: T.Tensor((M, K), in_dtype), B: T.Tensor(B_shape, in_dtype),
                         C: T.Tensor((M, N), out_dtype)):
         with T.Kernel(T.ceildiv(N, block_N), T.ceildiv(M, block_M), threads=emitter.threads) as (bx, by):
             A_shared = T.alloc_shared((block_M, block_K), in_dtype)
-            B_shared = T.alloc_shared((block_N, block_K), in_dtype)
-            C_shared = T.alloc_shared(C_shared_shape, out_dtype)
             A_local = T.alloc_local((emitter.warp_rows * emitter.local_size_a, ), in_dtype)
             B_local = T.alloc_local((emitter.warp_cols * emitter.local_size_b, ), in_dtype)
             C_local = T.alloc_local((emitter.warp_rows * emitter.warp_cols * emitter.local_size_out, ), accum_dtype)
+            if not b_preshuffle:
+                B_shared = T.alloc_shared(B_sh, in_dtype)
+                T.annotate_layout({A_shared: make_mfma_swizzle_layout(A_shared),
+                                   B_shared: make_mfma_swizzle_layout(B_shared)})
+            else:
+                T.annotate_layout({A_shared: make_mfma_swizzle_layout(A_shared)})
             T.use_swizzle(panel_size=8)
             T.clear(C_local)
             for ko in T.Pipelined(K // block_K, num_stages=stage):
-                for i, k in T.Parallel(block_M, block_K):
-                    A_shared[i, k] = A[by * block_M + i, ko * block_K + k]
-                for j, k in T.Parallel(block_N, block_K):
-                    B_shared[j, k] = B[bx * block_N + j, ko * block_K + k]
-                for ki in T.serial(block_K // emitter.micro_size_k):
+                T.copy(A[by * block_M, ko * block_K], A_shared)
+                if not b_preshuffle:
+                    if b_transposed:
+                        T.copy(B[bx * block_N, ko * block_K], B_shared)
+                    else:
+                        T.copy(B[ko * block_K, bx * block_N], B_shared)
+                for ki in T.unroll(block_K // pk):
                     emitter.ldmatrix_a(A_local, A_shared, ki)
-                    emitter.ldmatrix_b(B_local, B_shared, ki)
-                    emitter.mma(A_local, B_local, C_local)
-            emitter.stmatrix(C_local, C_shared)
-            for i, j in T.Parallel(block_M, block_N):
-                C[by * block_M + i, bx * block_N + j] = C_shared[i // 16, j // 16, i % 16, j % 16]
+                    if b_preshuffle:
+                        emitter.ldmatrix_b(B_local, B, ko * (block_K // pk) + ki, pid_m=by, pid_n=bx)
+                    else:
+                        emitter.ldmatrix_b(B_local, B_shared, ki)
+                    emitter.mfma(A_local, B_local, C_local)
+            emitter.stmatrix(C_local, C, pid_m=by, pid_n=bx)
 
     return gemm_intrinsics
 
 
-def ref_program(A, B):
-    return A.float() @ B.float().T
+def ref_program(A, B, b_transposed=True):
+    return A.float() @ (B.float().T if b_transposed else B.float())
 
 
-def main(M=4096, N=4096, K=4096, in_dtype="float16"):
+def main(M=4096, N=4096, K=4096, in_dtype="float16", micro_size=32, b_preshuffle=False):
     import torch
-    out_dtype = "int32" if in_dtype == "int8" else "float16"
+    from tilelang.intrinsics import shuffle_weight
+    out_dtype = "int32" if in_dtype == "int8" else "float16" if in_dtype == "float16" else "float32"
     accum = "int32" if in_dtype == "int8" else "float32"
-    kernel = tl_matmul(M, N, K, in_dtype, out_dtype, accum)
+    kernel = tl_matmul(M, N, K, in_dtype, out_dtype, accum, micro_size=micro_size, b_preshuffle=b_preshuffle)
     if in_dtype == "int8":
         a = torch.randint(-8, 8, (M, K), device="cuda", dtype=torch.int8)
         b = torch.randint(-8, 8, (N, K), device="cuda", dtype=torch.int8)
     else:
-        a = torch.randn(M, K, device="cuda", dtype=torch.float16)
-        b = torch.randn(N, K, device="cuda", dtype=torch.float16)
-    c = kernel(a, b)
+        tdt = getattr(torch, in_dtype)
+        a = torch.randn(M, K, device="cuda").to(tdt)
+        b = torch.randn(N, K, device="cuda").to(tdt)
+    bk = b
+    if b_preshuffle:
+        pk = MatrixCoreIntrinEmitter(in_dtype, in_dtype, accum, micro_size=micro_size, chunk=256).micro_size_k
+        bk = shuffle_weight(b, (micro_size, pk), is_transpose=True)
+    c = kernel(a, bk)
     torch.testing.assert_close(c.float(), ref_program(a, b), rtol=1e-2, atol=1e-2)
     print("All checks pass.")
-    lat = kernel.get_profiler().do_bench(lambda: kernel(a, b))
-    print(f"intrinsic-emitter GEMM {M}x{N}x{K} {in_dtype}: {lat:.3f} ms, {2 * M * N * K / lat * 1e-9:.1f} TFLOPS")
+    lat = kernel.get_profiler().do_bench(lambda: kernel(a, bk))
+    print(f"intrinsic-emitter GEMM {M}x{N}x{K} {in_dtype} mfma{micro_size} preshuffle={b_preshuffle}: {lat:.3f} ms, "
+          f"{2 * M * N * K / lat * 1e-9:.1f} TFLOPS")
 
 
 if __name__ == "__main__":
@@ -83,5 +111,7 @@ if __name__ == "__main__":
     p.add_argument("--n", type=int, default=4096)
     p.add_argument("--k", type=int, default=4096)
     p.add_argument("--dtype", default="float16")
+    p.add_argument("--micro", type=int, default=32)
+    p.add_argument("--preshuffle", action="store_true")
     a = p.parse_args()
-    main(a.m, a.n, a.k, a.dtype)
+    main(a.m, a.n, a.k, a.dtype, a.micro, a.preshuffle)

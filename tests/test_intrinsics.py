@@ -25,30 +25,70 @@ def test_lane_maps_cover_tiles():
 
 def test_emitter_validation():
     with pytest.raises(NotImplementedError):
-        MatrixCoreIntrinEmitter("float32", "float32")
+        MatrixCoreIntrinEmitter("float8_e4m3fnuz", "float8_e4m3fnuz")
     with pytest.raises(ValueError):
         MatrixCoreIntrinEmitter("float16", "float16", warp_row_tiles=24)
+    with pytest.raises(ValueError):
+        MatrixCoreIntrinEmitter("int8", "int8", "float32")
+    e = MatrixCoreIntrinEmitter("float8_e4m3fn", "float8_e5m2", chunk=128)
+    assert (e.k_dim, e.local_size_a) == (128, 32)  # the scaled f8f6f4 form
+    e = MatrixCoreIntrinEmitter("float8_e4m3fn", "float8_e4m3fn", micro_size=32, fp8_k_dim=16, chunk=64, k_pack=2)
+    assert (e.k_dim, e.local_size_a, e.local_size_out) == (16, 16, 16)
+    e = MatrixCoreIntrinEmitter("float32", "float32", chunk=4)
+    assert (e.k_dim, e.local_size_a) == (4, 1)
 
 
-@pytest.mark.parametrize("dt", ["float16", "int8"])
-def test_intrinsics_gemm_compiles(dt):
-    out, acc = ("int32", "int32") if dt == "int8" else ("float16", "float32")
-    src = tilelang.lower(tl_matmul.get_tir(256, 256, 256, dt, out, acc), target="hip").kernel_source
-    assert src.count("tl::mfma_16x16") == 16  # 4 x 4 warp tiles per K step
+def test_shuffle_weight_tile_major():
+    from tilelang.intrinsics import shuffle_weight
+    b = torch.arange(64 * 96).view(64, 96)
+    s = shuffle_weight(b, (16, 32), is_transpose=True)
+    assert s.shape == (4, 3, 16, 32)
+    assert s[2, 1, 5, 7] == b[2 * 16 + 5, 1 * 32 + 7]
+    s = shuffle_weight(b, (16, 32), is_transpose=False)  # [K=64, N=96]
+    assert s.shape == (2, 6, 32, 16) and s[1, 4, 3, 9] == b[32 + 3, 4 * 16 + 9]
+
+
+_CASES = [("float16", {}), ("float16", dict(micro_size=16, block_col_warps=2, warp_row_tiles=64)),
+          ("bfloat16", dict(k_pack=2)), ("float16", dict(b_transposed=False)), ("float16", dict(b_preshuffle=True)),
+          ("int8", {}), ("int8", dict(micro_size=16, block_col_warps=2, warp_row_tiles=64)),
+          ("float8_e4m3fn", {}), ("float8_e4m3fn", dict(micro_size=16, block_col_warps=2, warp_row_tiles=64)),
+          ("float8_e5m2", dict(fp8_k_dim=16)), ("float8_e4m3fn", dict(b_preshuffle=True))]
+
+
+def _types(dt):
+    return ("int32", "int32") if dt == "int8" else (("float16" if dt == "float16" else "float32"), "float32")
+
+
+@pytest.mark.parametrize("dt,kw", _CASES)
+def test_intrinsics_gemm_compiles(dt, kw):
+    out, acc = _types(dt)
+    src = tilelang.compile(tl_matmul.get_tir(512, 512, 512, dt, out, acc, **kw), out_idx=[2],
+                           target="hip").get_kernel_source()
+    assert "tl::mfma_emit<%d, " % kw.get("micro_size", 32) in src
+    assert "tl::ld_run<" in src
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dt", ["float16", "bfloat16", "int8"])
-def test_intrinsics_gemm_gpu(dt):
-    out, acc = ("int32", "int32") if dt == "int8" else (dt, "float32")
-    M, N, K = 512, 384, 256
-    k = tl_matmul(M, N, K, dt, out, acc)
+@pytest.mark.parametrize("dt,kw", _CASES)
+def test_intrinsics_gemm_gpu(dt, kw):
+    from tilelang.intrinsics import shuffle_weight
+    out, acc = _types(dt)
+    M, N, K = 512, 768, 1024
+    k = tl_matmul(M, N, K, dt, out, acc, **kw)
     if dt == "int8":
         a = torch.randint(-8, 8, (M, K), device="cuda", dtype=torch.int8)
         b = torch.randint(-8, 8, (N, K), device="cuda", dtype=torch.int8)
-        torch.testing.assert_close(k(a, b).cpu(), (a.cpu().long() @ b.cpu().long().T).int())
     else:
         tdt = getattr(torch, dt)
-        a = torch.randn(M, K, device="cuda", dtype=tdt)
-        b = torch.randn(N, K, device="cuda", dtype=tdt)
-        torch.testing.assert_close(k(a, b).float(), a.float() @ b.float().T, rtol=2e-2, atol=2e-2)
+        a = torch.randn(M, K, device="cuda").to(tdt)
+        b = torch.randn(N, K, device="cuda").to(tdt)
+    bt = b.t().contiguous() if kw.get("b_transposed", True) is False else b
+    if kw.get("b_preshuffle"):
+        e = MatrixCoreIntrinEmitter(dt, dt, acc, micro_size=kw.get("micro_size", 32), chunk=1 << 20)
+        bt = shuffle_weight(b, (kw.get("micro_size", 32), e.micro_size_k), is_transpose=True)
+    c = k(a, bt)
+    ref = a.cpu().float() @ b.cpu().float().T
+    if dt == "int8":
+        torch.testing.assert_close(c.cpu(), ref.int())
+    else:
+        torch.testing.assert_close(c.float().cpu(), ref, rtol=2e-2, atol=2e-2 * (K ** 0.5))

@@ -12,6 +12,8 @@
 //     encoded in a 32-bit SWZ (nibble cb = 1 + row bit XORed into chunk bit cb, 0 = none).
 #pragma once
 
+#include <type_traits>
+
 namespace tl {
 
 // the wave index: callers in loops pass the kernel's own (computed once before the loop); a
@@ -584,6 +586,112 @@ TL_DEVICE void mfma_16x16(int* c, const int8_t* a, const int8_t* b) {
   intx4 cv = *reinterpret_cast<intx4*>(c);
   cv = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, cv, 0, 0, 0);
   *reinterpret_cast<intx4*>(c) = cv;
+}
+
+// General form for the emitter: MS x MS tiles (16 or 32), KPER consecutive k per lane, standard
+// operand order mfma(A, B) (no swap):
+//   MS = 16: lane l holds A[l & 15][KPER (l >> 4) + j], B[KPER (l >> 4) + j][l & 15];
+//            C[4 (l >> 4) + v][l & 15], v < 4
+//   MS = 32: lane l holds A[l & 31][KPER (l >> 5) + j], B[KPER (l >> 5) + j][l & 31];
+//            C[8 (v >> 2) + 4 (l >> 5) + (v & 3)][l & 31], v < 16
+// Instructions: f16/bf16 KPER 8 (16x16x32, 32x32x16); int8 KPER 16 (16x16x64, 32x32x32); OCP fp8
+// (e4m3fn / e5m2, any mix) KPER 8 (16x16x32, 32x32x16) or KPER 32 (the f8f6f4 16x16x128 / 32x32x64
+// forms with unit e8m0 scales, 2x the rate; their in-lane k order is a fixed permutation applied
+// to A and B alike, so the contraction is unchanged); fp32 KPER 1 (16x16x4, 32x32x2).
+template <typename T> struct emit_kind { static constexpr int v = 0; };
+template <> struct emit_kind<half_t> { static constexpr int v = 1; };
+template <> struct emit_kind<bfloat16_t> { static constexpr int v = 1; };
+template <> struct emit_kind<int8_t> { static constexpr int v = 2; };
+template <> struct emit_kind<fp8_e4_t> { static constexpr int v = 3; };
+template <> struct emit_kind<fp8_e5_t> { static constexpr int v = 3; };
+template <> struct emit_kind<float> { static constexpr int v = 4; };
+
+template <typename TA, typename TB> TL_DEVICE floatx16 mma_f8_32x32(long a, long b, floatx16 c) {
+  if constexpr (fp8_fmt<TA>::code == 0 && fp8_fmt<TB>::code == 0)
+    return __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c, 0, 0, 0);
+  else if constexpr (fp8_fmt<TA>::code == 0)
+    return __builtin_amdgcn_mfma_f32_32x32x16_fp8_bf8(a, b, c, 0, 0, 0);
+  else if constexpr (fp8_fmt<TB>::code == 0)
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf8_fp8(a, b, c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf8_bf8(a, b, c, 0, 0, 0);
+}
+
+template <int MS, int KPER, typename TA, typename TB, typename TC>
+TL_DEVICE void mfma_emit(TC* c, const TA* a, const TB* b) {
+  constexpr int K = emit_kind<TA>::v;
+  static_assert(K != 0 && K == emit_kind<TB>::v, "mfma_emit: unsupported operand types");
+  static_assert(MS == 16 || MS == 32, "mfma_emit: 16x16 or 32x32 tiles");
+  typedef typename std::conditional<MS == 16, floatx4, floatx16>::type FAcc;
+  if constexpr (K == 1) {
+    static_assert(KPER == 8, "f16/bf16 MFMA: 8 k per lane");
+    static_assert(std::is_same<TA, TB>::value, "f16/bf16 MFMA: same operand type");
+    if constexpr (MS == 16) {
+      typedef typename mfma_traits<TA>::frag F;
+      floatx4 cv = *reinterpret_cast<floatx4*>(c);
+      cv = mfma_traits<TA>::mma16(*reinterpret_cast<const F*>(a), *reinterpret_cast<const F*>(b), cv);
+      *reinterpret_cast<floatx4*>(c) = cv;
+    } else {
+      typedef typename mfma32_traits<TA>::frag F;
+      floatx16 cv = *reinterpret_cast<floatx16*>(c);
+      cv = mfma32_traits<TA>::mma(*reinterpret_cast<const F*>(a), *reinterpret_cast<const F*>(b), cv);
+      *reinterpret_cast<floatx16*>(c) = cv;
+    }
+  } else if constexpr (K == 2) {
+    static_assert(KPER == 16, "int8 MFMA: 16 k per lane");
+    intx4 av = *reinterpret_cast<const intx4*>(a), bv = *reinterpret_cast<const intx4*>(b);
+    if constexpr (MS == 16) {
+      intx4 cv = *reinterpret_cast<intx4*>(c);
+      *reinterpret_cast<intx4*>(c) = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, cv, 0, 0, 0);
+    } else {
+      intx16 cv = *reinterpret_cast<intx16*>(c);
+      *reinterpret_cast<intx16*>(c) = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, cv, 0, 0, 0);
+    }
+  } else if constexpr (K == 3) {
+    FAcc cv = *reinterpret_cast<FAcc*>(c);
+    if constexpr (KPER == 8) {
+      const long av = *reinterpret_cast<const long*>(a), bv = *reinterpret_cast<const long*>(b);
+      if constexpr (MS == 16)
+        cv = mma_f8_32<TA, TB>(av, bv, cv);
+      else
+        cv = mma_f8_32x32<TA, TB>(av, bv, cv);
+    } else {
+      static_assert(KPER == 32, "fp8 MFMA: 8 or 32 k per lane");
+      const intx8 av = *reinterpret_cast<const intx8*>(a), bv = *reinterpret_cast<const intx8*>(b);
+      if constexpr (MS == 16)
+        cv = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, cv, fp8_fmt<TA>::code, fp8_fmt<TB>::code, 0,
+                                                              127, 0, 127);
+      else
+        cv = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, bv, cv, fp8_fmt<TA>::code, fp8_fmt<TB>::code, 0,
+                                                             127, 0, 127);
+    }
+    *reinterpret_cast<FAcc*>(c) = cv;
+  } else {
+    static_assert(KPER == 1, "fp32 MFMA: 1 k per lane");
+    FAcc cv = *reinterpret_cast<FAcc*>(c);
+    if constexpr (MS == 16)
+      cv = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], cv, 0, 0, 0);
+    else
+      cv = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0], b[0], cv, 0, 0, 0);
+    *reinterpret_cast<FAcc*>(c) = cv;
+  }
+}
+
+// contiguous register run <- LDS / global (16-byte aligned runs: ds_read_b128 / global_load_dwordx4)
+template <typename T, int N> TL_DEVICE void ld_run(T* dst, const T* src) {
+  constexpr int BYTES = N * (int)sizeof(T);
+  if constexpr (BYTES % 16 == 0) {
+#pragma unroll
+    for (int i = 0; i < BYTES / 16; ++i)
+      reinterpret_cast<intx4*>(dst)[i] = reinterpret_cast<const intx4*>(src)[i];
+  } else if constexpr (BYTES == 8) {
+    *reinterpret_cast<long*>(dst) = *reinterpret_cast<const long*>(src);
+  } else if constexpr (BYTES == 4) {
+    *reinterpret_cast<int*>(dst) = *reinterpret_cast<const int*>(src);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) dst[i] = src[i];
+  }
 }
 
 }  // namespace tl

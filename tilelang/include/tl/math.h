@@ -1,7 +1,8 @@
 // tl/math.h — scalar math used by lowered kernels.
 //
-// Precise variants go to OCML (__ocml_*) via clang builtins; the "fast" variants map to the
-// gfx950 transcendental unit (v_exp_f32 computes 2^x, v_log_f32 log2, v_rcp_f32, v_rsq_f32).
+// Precise variants call OCML (__ocml_*_f32) directly: clang's __builtin_tanhf & co. become LLVM
+// intrinsics that the AMDGPU backend cannot always lower ("no libcall available for ftanh").
+// The "fast" variants map to the gfx950 transcendental unit (v_exp_f32 computes 2^x, v_log_f32 log2, v_rcp_f32, v_rsq_f32).
 // Reference: src/target/intrin_rule_hip.cc:134-171 (HIPMath / HIPFastMath dispatch).
 #pragma once
 
@@ -9,27 +10,27 @@ namespace tl {
 
 #define TL_F32(x) static_cast<float>(x)
 
-template <typename T> TL_DEVICE T exp(T x) { return (T)__builtin_expf(TL_F32(x)); }
-template <typename T> TL_DEVICE T exp2(T x) { return (T)__builtin_exp2f(TL_F32(x)); }
-template <typename T> TL_DEVICE T exp10(T x) { return (T)__builtin_expf(TL_F32(x) * 2.302585092994046f); }
-template <typename T> TL_DEVICE T log(T x) { return (T)__builtin_logf(TL_F32(x)); }
-template <typename T> TL_DEVICE T log2(T x) { return (T)__builtin_log2f(TL_F32(x)); }
-template <typename T> TL_DEVICE T log10(T x) { return (T)__builtin_log10f(TL_F32(x)); }
-template <typename T> TL_DEVICE T log1p(T x) { return (T)__builtin_log1pf(TL_F32(x)); }
-template <typename T> TL_DEVICE T expm1(T x) { return (T)__builtin_expm1f(TL_F32(x)); }
+template <typename T> TL_DEVICE T exp(T x) { return (T)__ocml_exp_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T exp2(T x) { return (T)__ocml_exp2_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T exp10(T x) { return (T)__ocml_exp10_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T log(T x) { return (T)__ocml_log_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T log2(T x) { return (T)__ocml_log2_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T log10(T x) { return (T)__ocml_log10_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T log1p(T x) { return (T)__ocml_log1p_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T expm1(T x) { return (T)__ocml_expm1_f32(TL_F32(x)); }
 template <typename T> TL_DEVICE T sqrt(T x) { return (T)__builtin_sqrtf(TL_F32(x)); }
 template <typename T> TL_DEVICE T rsqrt(T x) { return (T)(1.0f / __builtin_sqrtf(TL_F32(x))); }
 template <typename T> TL_DEVICE T rcp(T x) { return (T)(1.0f / TL_F32(x)); }
-template <typename T> TL_DEVICE T sin(T x) { return (T)__builtin_sinf(TL_F32(x)); }
-template <typename T> TL_DEVICE T cos(T x) { return (T)__builtin_cosf(TL_F32(x)); }
-template <typename T> TL_DEVICE T tan(T x) { return (T)__builtin_tanf(TL_F32(x)); }
-template <typename T> TL_DEVICE T asin(T x) { return (T)__builtin_asinf(TL_F32(x)); }
-template <typename T> TL_DEVICE T acos(T x) { return (T)__builtin_acosf(TL_F32(x)); }
-template <typename T> TL_DEVICE T atan(T x) { return (T)__builtin_atanf(TL_F32(x)); }
-template <typename T> TL_DEVICE T sinh(T x) { return (T)__builtin_sinhf(TL_F32(x)); }
-template <typename T> TL_DEVICE T cosh(T x) { return (T)__builtin_coshf(TL_F32(x)); }
-template <typename T> TL_DEVICE T tanh(T x) { return (T)__builtin_tanhf(TL_F32(x)); }
-template <typename T> TL_DEVICE T erf(T x) { return (T)__builtin_erff(TL_F32(x)); }
+template <typename T> TL_DEVICE T sin(T x) { return (T)__ocml_sin_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T cos(T x) { return (T)__ocml_cos_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T tan(T x) { return (T)__ocml_tan_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T asin(T x) { return (T)__ocml_asin_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T acos(T x) { return (T)__ocml_acos_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T atan(T x) { return (T)__ocml_atan_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T sinh(T x) { return (T)__ocml_sinh_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T cosh(T x) { return (T)__ocml_cosh_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T tanh(T x) { return (T)__ocml_tanh_f32(TL_F32(x)); }
+template <typename T> TL_DEVICE T erf(T x) { return (T)__ocml_erf_f32(TL_F32(x)); }
 template <typename T> TL_DEVICE T floor(T x) { return (T)__builtin_floorf(TL_F32(x)); }
 template <typename T> TL_DEVICE T ceil(T x) { return (T)__builtin_ceilf(TL_F32(x)); }
 template <typename T> TL_DEVICE T trunc(T x) { return (T)__builtin_truncf(TL_F32(x)); }

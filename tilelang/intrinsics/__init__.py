@@ -1,5 +1,6 @@
 """Hand-scheduled matrix-core programming (reference: tilelang/intrinsics)."""
-from .mfma_macro_generator import MatrixCoreIntrinEmitter, TensorCoreIntrinEmitter  # noqa: F401
+from .mfma_macro_generator import (MatrixCoreIntrinEmitter, MatrixCorePreshuffleIntrinEmitter,  # noqa: F401
+                                   TensorCoreIntrinEmitter, shuffle_weight)
 from . import mfma_layout  # noqa: F401
 
 
@@ -13,3 +14,12 @@ def get_swizzle_layout(row, col, row_size, dtype):
         return row, col
     chunk = (col // per) ^ (row % chunks)
     return row, chunk * per + col % per
+
+
+def make_mfma_swizzle_layout(shared_buf, *args, **kwargs):
+    """XOR-swizzled LDS layout for an MFMA operand tile (reference
+    ``tilelang.intrinsics.make_mfma_swizzle_layout``): the same 16-byte-chunk swizzle ``T.gemm``
+    picks, so the emitter's 16-byte fragment runs are bank-conflict-free and the tile still
+    loads by LDS-DMA."""
+    from ..layout.layout import make_swizzled_layout
+    return make_swizzled_layout(shared_buf)
