@@ -31,8 +31,7 @@ def test_unknown_and_unsupported_keys_raise():
         validate_pass_configs({"tl.no_such_key": True})
     with pytest.raises(NotImplementedError):
         validate_pass_configs({"tl.ptxas_register_usage_level": 10})
-    with pytest.raises(NotImplementedError):
-        validate_pass_configs({"tl.storage_rewrite_detect_inplace": True})
+    assert validate_pass_configs({"tl.storage_rewrite_detect_inplace": True})
     with pytest.raises(ValueError):
         validate_pass_configs({"tl.config_index_bitwidth": 16})
     assert validate_pass_configs({"tl.disable_tma_lower": True, "tl.disable_warp_specialized": True})

@@ -47,3 +47,49 @@ def test_merged_program_computes_the_same():
     rows = torch.arange(256)
     torch.testing.assert_close(b, A[rows, (I % 8).long()])
     torch.testing.assert_close(c, 2 * A[rows, ((I + 1) % 8).long()])
+
+
+def _inplace_prog(n=64, shifted=False):
+
+    @T.prim_func
+    def main(A: T.Tensor((n, 8), "float32"), I: T.Tensor((n, ), "int32"), C: T.Tensor((n, ), "float32")):
+        with T.Kernel(n, threads=64) as bx:
+            u = T.alloc_local((8, ), "float32")
+            v = T.alloc_local((8, ), "float32")
+            for j in T.serial(8):
+                u[j] = A[bx, j]
+            if shifted:
+                for j in T.serial(8):
+                    v[j] = u[(j + 1) % 8] * 2.0  # reads an element another iteration overwrites
+            else:
+                for j in T.serial(8):
+                    v[j] = u[j] * 2.0 + 1.0  # element-wise: v may live in u's storage
+            C[bx] = v[I[bx] % 8]
+
+    return main
+
+
+def _kernel_of(f):
+    from tilelang.ir import stmt as S
+    return [s for s in S.walk(f.body) if isinstance(s, S.KernelStmt)][0]
+
+
+def test_inplace_detection():
+    _, merged = rewrite_local_storage(_kernel_of(_inplace_prog()))
+    assert merged == {}  # live ranges touch: not merged without in-place detection
+    _, merged = rewrite_local_storage(_kernel_of(_inplace_prog()), detect_inplace=True)
+    assert merged == {"v": "u"}
+    _, merged = rewrite_local_storage(_kernel_of(_inplace_prog(shifted=True)), detect_inplace=True)
+    assert merged == {}
+    for shifted in (False, True):
+        f = _inplace_prog(shifted=shifted)
+        k = tilelang.compile(f, out_idx=[2], target="cpu", pass_configs={"tl.storage_rewrite_detect_inplace": True})
+        A = torch.randn(64, 8)
+        I = torch.randint(0, 100, (64, ), dtype=torch.int32)
+        rows = torch.arange(64)
+        j = (I % 8).long()
+        ref = 2 * A[rows, (j + 1) % 8] if shifted else 2 * A[rows, j] + 1
+        torch.testing.assert_close(k(A, I), ref)
+        src = tilelang.compile(f, out_idx=[2], target="hip",
+                               pass_configs={"tl.storage_rewrite_detect_inplace": True}).get_kernel_source()
+        assert ("v[" in src) == shifted

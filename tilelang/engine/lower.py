@@ -123,7 +123,8 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
     kernel = apply_stage_schedules(kernel)  # T.Pipelined(order=, stage=, group=)
     if not cfg.get("tir.disable_storage_rewrite"):
         from ..transform.storage_rewrite import rewrite_local_storage
-        kernel, _ = rewrite_local_storage(kernel)  # local arrays with disjoint lifetimes share storage
+        # local arrays with disjoint lifetimes share storage (+ element-wise in-place reuse if asked)
+        kernel, _ = rewrite_local_storage(kernel, bool(cfg.get("tl.storage_rewrite_detect_inplace")))
     phased = cfg.get("tl.gemm_phased")
     if target.kind == "hip" and phased is not False:  # default on: +15 % at 4096^3 (profiles/r2/gemm_phased.log)
         from ..transform.gemm_ksplit import split_gemm_k_halves

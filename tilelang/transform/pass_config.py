@@ -7,8 +7,8 @@ Every key is either implemented on gfx950 or rejected (``validate_pass_configs``
 * satisfied by construction — the reference uses the key to switch OFF an NVIDIA-only feature
   (TMA, WGMMA, warp specialisation, 256-bit vectors) or a TVM pass this compiler does not have;
   the "off" value is what gfx950 always does and is accepted, asking for the feature raises;
-* unsupported — raises ``NotImplementedError`` (``tl.ptxas_register_usage_level``,
-  ``tl.storage_rewrite_detect_inplace``) with the gfx950 alternative in the message.
+* unsupported — raises ``NotImplementedError`` (``tl.ptxas_register_usage_level``) with the
+  gfx950 alternative in the message.
 """
 from enum import Enum
 
@@ -81,6 +81,9 @@ EFFECT = {
                         "_prefetch_schedule, tl::gemm_ss_load / gemm_ss_mma)",
     "tl.disable_address_hoist": "True keeps the per-thread LDS-DMA source address arithmetic inside pipelined "
                                 "loops (transform/hoist_addresses.py hoists it by default)",
+    "tl.storage_rewrite_detect_inplace": "a local array first written by the element-wise statement that last "
+                                         "reads another of the same dtype/shape takes over its storage "
+                                         "(transform/storage_rewrite.py _inplace_ok)",
     "tl.gemm_interleave": "default on; False drops the 1 MFMA : 1 ds_read sched_group_barrier pattern of the "
                           "prefetched GEMM (the compiler schedules the two streams itself)",
 }
@@ -100,8 +103,6 @@ SATISFIED = {
 UNSUPPORTED = {
     "tl.ptxas_register_usage_level": "ptxas is NVIDIA-only; bound gfx950 registers with "
                                      "pass_configs={'tl.min_waves_per_eu': N}",
-    "tl.storage_rewrite_detect_inplace": "in-place buffer reuse detection is not implemented; LDS reuse is "
-                                         "liveness based ('tl.lds_reuse')",
 }
 
 DEFAULTS = {"tl.disable_dynamic_tail_split": False, "tir.merge_static_smem": False,
