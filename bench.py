@@ -225,7 +225,8 @@ def main():
                 from tilelang.runtime import errors
                 errors.check()
             rows = slice(0, 256)
-            y_ref = moe_reference(xs[rows], g_w, w1, w2, moe.cfg.topk, routing=route(xs[rows], moe.gate_w, moe.cfg.topk))
+            y_ref = moe_reference(xs[rows], g_w, w1, w2, moe.cfg.topk,
+                                  routing=route(xs[rows], moe.gate_w, moe.cfg.topk))
             return bool(torch.allclose(ys[rows].float(), y_ref, rtol=3e-2, atol=3e-2 * float(y_ref.abs().max())))
 
         def all_ranks(flag):

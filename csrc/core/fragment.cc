@@ -27,7 +27,8 @@ void Fragment::validate() const {
     std::sort(ds.begin(), ds.end(), [](const Digit& a, const Digit& b) { return a.stride < b.stride; });
     int64_t acc = 1;
     for (auto& d : ds) {
-      if (d.stride != acc) throw std::invalid_argument("fragment digits of dim " + std::to_string(dim) + " do not tile it");
+      if (d.stride != acc)
+        throw std::invalid_argument("fragment digits of dim " + std::to_string(dim) + " do not tile it");
       acc *= d.size;
     }
     if (acc != shape_[dim])

@@ -86,7 +86,8 @@ std::vector<int64_t> swizzle_costs(const std::string& instr, const std::vector<i
                                    int64_t cols, int64_t elem_bytes,
                                    const std::vector<std::vector<std::pair<int, int>>>& candidates) {
   const LdsInstr& ins = lds_instr(instr);
-  if ((int64_t)rows_cols.size() != npat * 64 * 2) throw std::invalid_argument("swizzle_costs: patterns must be [P,64,2]");
+  if ((int64_t)rows_cols.size() != npat * 64 * 2)
+    throw std::invalid_argument("swizzle_costs: patterns must be [P,64,2]");
   std::vector<int64_t> costs(candidates.size(), 0);
   std::vector<int64_t> addrs(64);
   const int64_t row_bytes = cols * elem_bytes;

@@ -8,7 +8,9 @@
 typedef int intx8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-__device__ unsigned char f2e4(float f) { return (unsigned char)(__builtin_amdgcn_cvt_pk_fp8_f32(f, f, 0, false) & 0xff); }
+__device__ unsigned char f2e4(float f) {
+  return (unsigned char)(__builtin_amdgcn_cvt_pk_fp8_f32(f, f, 0, false) & 0xff);
+}
 
 // hypothesis H: lane l holds k = kmap(l, j) for j in [0,32)
 __device__ int kmap(int h, int l, int j) {

@@ -24,7 +24,7 @@ import argparse
 import tilelang
 import tilelang.language as T
 
-from example_nsa_fwd import FAST_MATH, LOG2E, make_block_indices
+from example_nsa_fwd import FAST_MATH, LOG2E
 
 
 @tilelang.jit(out_idx=[-2, -1], pass_configs=FAST_MATH)
@@ -221,7 +221,8 @@ def nsa_bwd_dkv(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=No
              V: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
              Mask: T.Tensor([batch, head_kv, NB, seq_len], "int8"), dO: T.Tensor([batch, seq_len, heads, D], dtype),
              LSE: T.Tensor([batch, seq_len, heads], "float32"), Delta: T.Tensor([batch, seq_len, heads], "float32"),
-             dK: T.Tensor([batch, seq_len_kv, head_kv, D], dtype), dV: T.Tensor([batch, seq_len_kv, head_kv, D], dtype)):
+             dK: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
+             dV: T.Tensor([batch, seq_len_kv, head_kv, D], dtype)):
         with T.Kernel(NB, batch * head_kv, threads=threads) as (j, bz):
             b = bz // head_kv
             h = bz % head_kv

@@ -11,8 +11,6 @@ the H heads of each token with a short serial reduction per (token, key) lane.
 """
 import argparse
 
-import tilelang
-import tilelang.language as T
 
 
 from tilelang.ops.dsa import mqa_attn_return_logits  # noqa: E402,F401  (kernel lives in the library)

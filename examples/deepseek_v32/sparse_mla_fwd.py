@@ -11,8 +11,6 @@ single query token already gives a full MFMA tile.
 """
 import argparse
 
-import tilelang
-import tilelang.language as T
 
 LOG2E = 1.44269504
 

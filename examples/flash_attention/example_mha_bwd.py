@@ -373,7 +373,8 @@ class _attention:
                     G = H // k.shape[2]
                     dt = "bfloat16" if q.dtype == torch.bfloat16 else "float16"
                     Dv = v.shape[-1]
-                    o, lse = flashattn_fwd(B, H, S, D, causal, dtype=dt, groups=G, dim_v=Dv, **_tiles(D, Dv, "fwd"))(q, k, v)
+                    fwd = flashattn_fwd(B, H, S, D, causal, dtype=dt, groups=G, dim_v=Dv, **_tiles(D, Dv, "fwd"))
+                    o, lse = fwd(q, k, v)
                     ctx.save_for_backward(q, k, v, o, lse)
                     ctx.causal = causal
                     return o
@@ -393,8 +394,9 @@ class _attention:
                     split = _kv_split(B, S, k.shape[2], G, bw.get("block_M", 128))
                     if BWD_DQ_MODE == "atomic":
                         dq = torch.zeros(B, S, H, D, dtype=torch.float32, device=q.device)
-                        flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv, **_tiles(D, Dv, "bwd"))(q, k, v, do, lse, delta, dq, dk,
-                                                                                           dv)
+                        bwd = flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv,
+                                            **_tiles(D, Dv, "bwd"))
+                        bwd(q, k, v, do, lse, delta, dq, dk, dv)
                         return flashattn_bwd_postprocess(B, H, S, D, dtype=dt)(dq), dk, dv, None
                     # dK/dV kernel without dQ + an atomic-free dQ kernel (the two could run on
                     # separate streams; they only share read-only inputs)
@@ -407,8 +409,9 @@ class _attention:
                     else:
                         flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, dq_mode="none", groups=G, dim_v=Dv,
                                       **bw)(q, k, v, do, lse, delta, dk, dv)
-                    dq = flashattn_bwd_dq(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv, **_tiles(D, Dv, "dq"))(q, k, v, do, lse,
-                                                                                          delta)
+                    bdq = flashattn_bwd_dq(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv,
+                                           **_tiles(D, Dv, "dq"))
+                    dq = bdq(q, k, v, do, lse, delta)
                     return dq, dk, dv, None
 
             cls.fn = Attn

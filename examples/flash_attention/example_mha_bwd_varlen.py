@@ -18,7 +18,7 @@ import argparse
 import tilelang
 import tilelang.language as T
 
-from example_mha_fwd_varlen import FAST_MATH, LOG2E, make_varlen, ref_program
+from example_mha_fwd_varlen import FAST_MATH, LOG2E, make_varlen
 
 
 @tilelang.jit(out_idx=[5, 6], pass_configs=FAST_MATH)
@@ -104,8 +104,8 @@ def varlen_bwd_preprocess(heads, total_q, dim, blk=32, dtype="bfloat16"):
             dsum = T.alloc_fragment([blk], "float32")
             for i, d in T.Parallel(blk, dim):
                 r = by * blk + i
-                acc[i, d] = T.if_then_else(r < total_q, T.cast(O[r, bx, d], "float32") * T.cast(dO[r, bx, d], "float32"),
-                                           0.0)
+                acc[i, d] = T.if_then_else(r < total_q,
+                                           T.cast(O[r, bx, d], "float32") * T.cast(dO[r, bx, d], "float32"), 0.0)
             T.reduce_sum(acc, dsum, dim=1)
             for i in T.Parallel(blk):
                 if by * blk + i < total_q:

@@ -148,7 +148,8 @@ def flashattn(batch, heads, seqlen_q, seqlen_kv, dim, is_causal=False, block_M=1
 
     @T.prim_func
     def flashattn_mha_inference(Q: T.Tensor(shape_q, dtype), K: T.Tensor(shape_kv, dtype),
-                                V: T.Tensor(shape_kv, dtype), glse: T.Tensor([batch, heads, num_split, seqlen_q], accum),
+                                V: T.Tensor(shape_kv, dtype),
+                                glse: T.Tensor([batch, heads, num_split, seqlen_q], accum),
                                 Output_partial: T.Tensor(part_shape, accum), Output: T.Tensor(shape_q, dtype)):
         split_kernel(Q, K, V, glse, Output_partial)
         combine(glse, Output_partial, Output)

@@ -362,7 +362,8 @@ def _bwd_kernels(B, S, H, DK, DV, C, block_DV, tgt):
     def k_(impl, *args, out_idx):
         return tilelang.compile(impl.get_tir(*args), out_idx=out_idx, target=tgt)
 
-    return dict(cum=k_(chunk_cumsum, B, S, H, C, out_idx=[1]), kkt=k_(chunk_scaled_dot_kkt, B, S, H, DK, C, out_idx=[3]),
+    return dict(cum=k_(chunk_cumsum, B, S, H, C, out_idx=[1]),
+                kkt=k_(chunk_scaled_dot_kkt, B, S, H, DK, C, out_idx=[3]),
                 tril=k_(solve_tril, B, S, H, C, out_idx=[1]), wy=k_(wy_fast, B, S, H, DK, DV, C, out_idx=[5, 6]),
                 h=k_(chunk_delta_h, B, S, H, DK, DV, C, min(block_DV, DV), out_idx=[4, 5, 6]),
                 dvl=k_(chunk_bwd_dv_local, B, S, H, DK, DV, C, out_idx=[4]),

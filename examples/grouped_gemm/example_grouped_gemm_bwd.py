@@ -95,7 +95,8 @@ def main(batch_sizes=(64, 300, 1024, 17), K=1024, N=2048):
     from tilelang.profiler import do_bench
     kd = grouped_gemm_dw(tuple(batch_sizes), K, N)
     ms = do_bench(lambda: kd(a, dc, bs, bo))
-    print(f"grouped dW {list(batch_sizes)} K={K} N={N}: {ms:.4f} ms, {2 * sum(batch_sizes) * K * N / ms * 1e-9:.1f} TFLOPS")
+    tf = 2 * sum(batch_sizes) * K * N / ms * 1e-9
+    print(f"grouped dW {list(batch_sizes)} K={K} N={N}: {ms:.4f} ms, {tf:.1f} TFLOPS")
 
 
 if __name__ == "__main__":

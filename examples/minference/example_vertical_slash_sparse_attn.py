@@ -34,7 +34,8 @@ def convert_vertical_slash_indexes(v_idx, s_idx, seq_len, block_M=64, block_N=64
     m0 = torch.arange(NQ, device=dev) * block_M                      # query block starts
     s = s_idx.long()[:, :, None, :]                                   # [B,H,1,NS]
     lo = (m0[None, None, :, None] - s).clamp(min=0)                   # first key of the slash segment
-    hi = torch.minimum(m0[None, None, :, None] + block_M - 1 - s, (m0 + block_M - 1).clamp(max=seq_len - 1)[None, None, :, None])
+    hi = torch.minimum(m0[None, None, :, None] + block_M - 1 - s,
+                       (m0 + block_M - 1).clamp(max=seq_len - 1)[None, None, :, None])
     valid = hi >= lo
     kb = torch.arange(NK, device=dev)
     blk_lo, blk_hi = lo // block_N, hi // block_N
@@ -168,7 +169,8 @@ def main(B=1, H=8, S=8192, D=128, n_vertical=1000, n_slash=200):
     import torch
     q, k, v = (torch.randn(B, H, S, D, device="cuda", dtype=torch.float16) for _ in range(3))
     g = torch.Generator(device="cuda").manual_seed(0)
-    v_idx = torch.stack([torch.randperm(S, device="cuda", generator=g)[:n_vertical] for _ in range(B * H)]).view(B, H, -1)
+    v_idx = torch.stack([torch.randperm(S, device="cuda", generator=g)[:n_vertical]
+                         for _ in range(B * H)]).view(B, H, -1)
     s_idx = torch.stack([torch.randperm(S, device="cuda", generator=g)[:n_slash] for _ in range(B * H)]).view(B, H, -1)
     s_idx[..., 0] = 0  # the main diagonal
     o = vertical_slash_sparse_attention(q, k, v, v_idx, s_idx)

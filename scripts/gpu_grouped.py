@@ -1,10 +1,10 @@
 """Grouped GEMM: correctness sweep + MoE-shaped perf vs a per-expert hipBLASLt loop."""
-import sys, os, time
+import sys, os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "examples", "grouped_gemm"))
 import torch
-from example_grouped_gemm_fwd import run, grouped_gemm, construct_inputs, torch_gmm
+from example_grouped_gemm_fwd import grouped_gemm, construct_inputs, torch_gmm
 from tilelang.profiler import do_bench
 
 

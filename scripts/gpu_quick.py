@@ -1,9 +1,8 @@
 """Quick on-GPU sanity + timing for the GEMM path (used during development)."""
-import sys, time, os
+import sys, os
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "examples", "gemm"))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
 import torch
-import tilelang
 from example_gemm import matmul
 
 

@@ -103,15 +103,15 @@ def main():
           lambda fn: torch.testing.assert_close(fn().float(), (A.float() @ xv.float()), rtol=2e-2, atol=2e-1))
 
     from example_per_token_cast_to_fp8 import per_token_cast_to_fp8
-    xh = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    xh = torch.randn(M, N, device="cuda")
     cfgs = [(8, 128), (8, 256), (16, 256), (4, 128), (32, 512), (16, 512)]
 
     def cast_k(bm, t):
         k = per_token_cast_to_fp8(M, N, bm, 128, t)
         return lambda: k(xh)
 
-    print("per-token(group 128) fp8 cast bf16 8192^2 (256 MiB in, 64 MiB + scales out)", flush=True)
-    sweep("cast", xh.numel() * 3 + M * (N // 128) * 4, [(f"{c}", (lambda c=c: cast_k(*c))) for c in cfgs])
+    print("per-token(group 128) fp8 cast fp32 8192^2 (256 MiB in, 64 MiB + scales out)", flush=True)
+    sweep("cast", xh.numel() * 5 + M * (N // 128) * 4, [(f"{c}", (lambda c=c: cast_k(*c))) for c in cfgs])
 
 
 if __name__ == "__main__":

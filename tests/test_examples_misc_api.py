@@ -3,7 +3,6 @@ import os
 import sys
 
 import pytest
-import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for d in ("", "compile_flags", "visual_layout_inference", "plot_layout", "lazy_jit"):

@@ -1,7 +1,6 @@
 import pytest
 import tilelang.language as T
 from tilelang.ir import stmt as S
-from tilelang.ir import tileop as O
 
 
 def _gemm_func(M=256, N=256, K=128, bm=128, bn=128, bk=32):

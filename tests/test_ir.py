@@ -1,6 +1,5 @@
-import tilelang.language as T
 from tilelang.ir import expr as E
-from tilelang.ir.dtypes import float16, int32, float32
+from tilelang.ir.dtypes import float16, float32
 
 
 def test_constant_folding_and_identities():

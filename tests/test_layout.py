@@ -5,8 +5,7 @@ import pytest
 from tilelang.layout import (mfma_c_fragment, mfma_a_fragment, make_linear_fragment, SwizzleLayout,
                              choose_swizzle, swizzle_report, compute_warp_partition, make_hierarchical_layout,
                              make_blockwise_zz_layout, Fragment)
-from tilelang.layout.fragment import Digit
-from tilelang.transform.layout_inference import reduce_dst_layout, project_layout
+from tilelang.transform.layout_inference import reduce_dst_layout
 
 
 def _check_bijective(f):

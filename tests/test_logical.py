@@ -48,7 +48,8 @@ def _ref(a, b, mask, bm, bn, bk, op):
             for k in range(K // bk):
                 if sel[i, j, k]:
                     c[i * bm:(i + 1) * bm, j * bn:(j + 1) * bn] += \
-                        a[i * bm:(i + 1) * bm, k * bk:(k + 1) * bk].float() @ b[k * bk:(k + 1) * bk, j * bn:(j + 1) * bn].float()
+                        a[i * bm:(i + 1) * bm, k * bk:(k + 1) * bk].float() @ \
+                        b[k * bk:(k + 1) * bk, j * bn:(j + 1) * bn].float()
     return c
 
 

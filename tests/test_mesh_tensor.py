@@ -36,7 +36,8 @@ def test_replicate_row(shape, y, nrows, ncols):
 
 
 @pytest.mark.parametrize("policy, msg", [
-    (MeshShardingPolicy(x=1, y=0, replicate=MeshReplicationType.ROW), "Cannot shard on x-axis when replicating on rows"),
+    (MeshShardingPolicy(x=1, y=0, replicate=MeshReplicationType.ROW),
+     "Cannot shard on x-axis when replicating on rows"),
     (MeshShardingPolicy(y=3, replicate=MeshReplicationType.ROW), "Invalid y-split dimension"),
     (MeshShardingPolicy(x=1, y=0, replicate=MeshReplicationType.COLUMN), "Cannot shard on y-axis"),
 ])

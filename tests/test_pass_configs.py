@@ -104,7 +104,8 @@ def test_use_async_copy_false_disables_lds_dma():
     import example_gemm
     f = example_gemm.matmul.get_tir(256, 256, 256, 128, 128, 32, 256, 2)
     on = tilelang.compile(f, out_idx=[-1], target="hip").get_kernel_source()
-    off = tilelang.compile(f, out_idx=[-1], target="hip", pass_configs={"tir.use_async_copy": False}).get_kernel_source()
+    off = tilelang.compile(f, out_idx=[-1], target="hip",
+                           pass_configs={"tir.use_async_copy": False}).get_kernel_source()
     assert "glds16" in on and "glds16" not in off
 
 

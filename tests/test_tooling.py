@@ -77,7 +77,8 @@ def test_int4_and_mxfp4_roundtrip():
     rel = (deq - W).abs() / W.abs().clamp(min=1e-3)
     assert rel.median() < 0.15
     codes = torch.arange(16, dtype=torch.uint8)
-    assert torch.equal(Q.float_to_e2m1(Q.e2m1_to_float_torch(codes)) & 0xF, torch.where(codes == 8, 0, codes).to(torch.uint8))
+    assert torch.equal(Q.float_to_e2m1(Q.e2m1_to_float_torch(codes)) & 0xF,
+                       torch.where(codes == 8, 0, codes).to(torch.uint8))
 
 
 @tilelang.jit(out_idx=[-1], target="cpu")

@@ -27,7 +27,6 @@ import shutil
 import tempfile
 import threading
 from pathlib import Path
-from typing import Optional
 
 from ..env import env, INCLUDE_DIR
 
@@ -73,7 +72,8 @@ def _freeze(x):
 
 def kernel_key(func, target, out_idx, pass_configs, compile_flags) -> str:
     from ..engine.callback import hook_fingerprint
-    blob = json.dumps({"hooks": hook_fingerprint(), "ir": func.script(), "target": str(target), "out_idx": _freeze(out_idx),
+    blob = json.dumps({"hooks": hook_fingerprint(), "ir": func.script(), "target": str(target),
+                       "out_idx": _freeze(out_idx),
                        "pass_configs": _freeze(pass_configs or {}), "flags": _freeze(compile_flags or []),
                        "compiler": compiler_fingerprint()}, sort_keys=True)
     return hashlib.sha256(blob.encode()).hexdigest()

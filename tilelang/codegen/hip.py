@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import math
 import re
-from typing import Dict, List, Optional
+from typing import Dict, List
 
 from ..ir import stmt as S
 from ..ir import lowered as L
@@ -341,11 +341,12 @@ class CodeGen:
             n = len(st.values)
             ct = self.ctype(b.dtype)
             vals = ", ".join(self.e(v) for v in st.values)
-            self.w(f"{{ {ct} _v[{n}] = {{{vals}}}; tl::store_vec<{ct}, {n}>(&{self.buf_ref(b)}[{self.e(st.index)}], _v); }}")
+            dst = f"&{self.buf_ref(b)}[{self.e(st.index)}]"
+            self.w(f"{{ {ct} _v[{n}] = {{{vals}}}; tl::store_vec<{ct}, {n}>({dst}, _v); }}")
         elif isinstance(st, L.VecLoadStmt):
             ct = self.ctype(st.src.dtype)
-            self.w(f"tl::load_vec<{ct}, {st.n}>(*reinterpret_cast<{ct}(*)[{st.n}]>(&{self.buf_ref(st.dst)}[{st.dst_index}]), "
-                   f"&{self.buf_ref(st.src)}[{self.e(st.src_index)}]);")
+            dst = f"*reinterpret_cast<{ct}(*)[{st.n}]>(&{self.buf_ref(st.dst)}[{st.dst_index}])"
+            self.w(f"tl::load_vec<{ct}, {st.n}>({dst}, &{self.buf_ref(st.src)}[{self.e(st.src_index)}]);")
         elif isinstance(st, L.CopyBytesStmt):
             self.w(f"tl::copy_bytes<{st.nbytes}>(&{self.buf_ref(st.dst)}[{self.e(st.dst_index)}], "
                    f"&{self.buf_ref(st.src)}[{self.e(st.src_index)}]);")

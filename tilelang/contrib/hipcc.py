@@ -46,7 +46,8 @@ def toolchain_version() -> str:
         return "unknown"
 
 
-DEFAULT_HIP_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=fast", "-Wno-unused-variable", "-Wno-unused-value",
+DEFAULT_HIP_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=fast-honor-pragmas", "-Wno-unused-variable",
+                     "-Wno-unused-value",
                      "-Wno-unused-but-set-variable", "-Wno-pass-failed"]
 
 

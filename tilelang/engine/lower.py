@@ -23,8 +23,6 @@ from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
 from ..ir import stmt as S
-from ..ir.buffer import Buffer
-from ..ir.expr import PrimExpr, Var
 from ..utils.target import Target, determine_target
 from ..analysis.checks import semantic_check, SemanticError
 from ..transform.layout_inference import infer_layouts

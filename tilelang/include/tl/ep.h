@@ -48,7 +48,9 @@ struct Layout {
 };
 
 TL_DEVICE unsigned* ctrl(char* base) { return reinterpret_cast<unsigned*>(base); }
-TL_DEVICE void st_sys(unsigned* p, unsigned v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
+TL_DEVICE void st_sys(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 TL_DEVICE unsigned ld_sys(unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 
 // one lane: wait until *p == v (exact) or (int)(*p - v) >= 0; bounded; error code on timeout

@@ -301,9 +301,11 @@ TL_DEVICE void gemm_ss_f8(const TA* __restrict__ A_, const TB* __restrict__ B_, 
     for (int kk = 0; kk < K / 128; ++kk) {
       intx8 a[M_REP], b[N_REP];
 #pragma unroll
-      for (int mi = 0; mi < M_REP; ++mi) a[mi] = ld_rows32_b8<A_COLS, SWZ_A>(A, wm * WM + mi * 16 + r, kk * 128 + 32 * g);
+      for (int mi = 0; mi < M_REP; ++mi)
+        a[mi] = ld_rows32_b8<A_COLS, SWZ_A>(A, wm * WM + mi * 16 + r, kk * 128 + 32 * g);
 #pragma unroll
-      for (int ni = 0; ni < N_REP; ++ni) b[ni] = ld_rows32_b8<B_COLS, SWZ_B>(B, wn * WN + ni * 16 + r, kk * 128 + 32 * g);
+      for (int ni = 0; ni < N_REP; ++ni)
+        b[ni] = ld_rows32_b8<B_COLS, SWZ_B>(B, wn * WN + ni * 16 + r, kk * 128 + 32 * g);
 #pragma unroll
       for (int mi = 0; mi < M_REP; ++mi)
 #pragma unroll

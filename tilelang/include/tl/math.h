@@ -2,7 +2,8 @@
 //
 // Precise variants call OCML (__ocml_*_f32) directly: clang's __builtin_tanhf & co. become LLVM
 // intrinsics that the AMDGPU backend cannot always lower ("no libcall available for ftanh").
-// The "fast" variants map to the gfx950 transcendental unit (v_exp_f32 computes 2^x, v_log_f32 log2, v_rcp_f32, v_rsq_f32).
+// The "fast" variants map to the gfx950 transcendental unit (v_exp_f32 computes 2^x, v_log_f32
+// log2, v_rcp_f32, v_rsq_f32).
 // Reference: src/target/intrin_rule_hip.cc:134-171 (HIPMath / HIPFastMath dispatch).
 #pragma once
 

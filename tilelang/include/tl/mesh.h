@@ -80,8 +80,8 @@ TL_DEVICE unsigned* flag_at(const Ctx& c, int owner, int blk, int op, int src) {
   return reinterpret_cast<unsigned*>(c.ws[owner]) + ((long long)blk * c.nops + op) * (c.nrow * c.ncol) + src;
 }
 TL_DEVICE unsigned* ready_at(const Ctx& c, int owner, int blk, int op, int dst) {
-  return reinterpret_cast<unsigned*>(c.ws[owner] + flags_bytes(c)) + ((long long)blk * c.nops + op) * (c.nrow * c.ncol) +
-         dst;
+  unsigned* base = reinterpret_cast<unsigned*>(c.ws[owner] + flags_bytes(c));
+  return base + ((long long)blk * c.nops + op) * (c.nrow * c.ncol) + dst;
 }
 TL_DEVICE char* slot(const Ctx& c, int owner, int blk, int op, int src) {
   return c.ws[owner] + 2 * flags_bytes(c) +

@@ -73,7 +73,8 @@ class MatrixCoreIntrinEmitter:
                  thread_var=None, micro_size=16, fp8_k_dim=None, a_preshuffle=False):
         for d in (a_dtype, b_dtype):
             if d == "float8_e4m3fnuz":
-                raise NotImplementedError("gfx950 MFMA consumes OCP fp8: use float8_e4m3fn (e4m3fnuz is CDNA3's format)")
+                raise NotImplementedError("gfx950 MFMA consumes OCP fp8: use float8_e4m3fn "
+                                          "(e4m3fnuz is CDNA3's format)")
             if d not in _CTYPE:
                 raise NotImplementedError(f"MFMA emitter: unsupported input dtype {d} "
                                           "(float16, bfloat16, int8, float8_e4m3fn, float8_e5m2, float32)")

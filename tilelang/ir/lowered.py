@@ -7,7 +7,7 @@ the per-thread register index of their ``local`` array.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
+from typing import List, Sequence
 
 from .expr import PrimExpr, convert
 from . import dtypes as _dt

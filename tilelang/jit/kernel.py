@@ -8,17 +8,15 @@ the current stream).
 """
 from __future__ import annotations
 
-import json
-import os
 import threading
 from pathlib import Path
-from typing import Any, List, Optional, Sequence, Union
+from typing import List, Optional, Union
 
 from ..engine.lower import lower, CompiledArtifact
 from ..ir import dtypes as _dt
 from ..ir import stmt as S
 from ..ir.buffer import Buffer
-from ..ir.expr import BinOp, IntImm, PrimExpr, Var, as_int
+from ..ir.expr import BinOp, IntImm, Var, as_int
 from ..utils.target import Target, determine_target
 from ..contrib import hipcc
 from .. import cache as _cache

@@ -22,7 +22,8 @@ from .loop import Parallel, Pipelined, Persistent, serial, Serial, unroll, Unrol
 from .allocate import (alloc_shared, alloc_fragment, alloc_local, alloc_var, alloc_buffer, alloc_reducer,
                        alloc_barrier, alloc_tmem, alloc_descriptor, alloc_wgmma_desc, alloc_tcgen05_smem_desc,
                        alloc_tcgen05_instr_desc, empty)
-from .tileops import (copy, gather_rows, c2d_im2col, gemm, gemm_v1, gemm_v2, gemm_scaled, gemm_sp, gemm_sp_v2, GemmWarpPolicy, fill, clear, reduce,
+from .tileops import (copy, gather_rows, c2d_im2col, gemm, gemm_v1, gemm_v2, gemm_scaled, gemm_sp, gemm_sp_v2,
+                      GemmWarpPolicy, fill, clear, reduce,
                       reduce_max, reduce_min, reduce_sum, reduce_abssum, reduce_absmax, reduce_bitand, reduce_bitor,
                       reduce_bitxor, cumsum, finalize_reducer, warp_reduce_sum, warp_reduce_max, warp_reduce_min,
                       warp_reduce_bitand, warp_reduce_bitor, atomic_add, atomic_max, atomic_min, atomic_addx2,

@@ -11,7 +11,7 @@ from ..ir import stmt as S
 from ..ir.buffer import Buffer
 from ..ir.expr import IntImm, PrimExpr, convert
 from ..ir import dtypes as _dt
-from .builder import current_builder, has_builder
+from .builder import current_builder
 
 
 def _alloc(shape, dtype, scope, name=None):

@@ -19,7 +19,7 @@ import threading
 
 import math
 from enum import Enum
-from typing import Any, Optional, Sequence, Tuple
+from typing import Any, Optional, Tuple
 
 from ..ir import dtypes as _dt
 from ..ir.buffer import Buffer

@@ -13,8 +13,7 @@ from typing import List, Optional
 
 from ..ir import stmt as S
 from ..ir.buffer import Buffer
-from ..ir.expr import PrimExpr, Var, cast, convert, const, as_int, IntImm
-from ..ir import dtypes as _dt
+from ..ir.expr import PrimExpr, Var, cast, convert, as_int, IntImm
 
 _tls = threading.local()
 

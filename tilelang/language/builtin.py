@@ -9,7 +9,7 @@ from __future__ import annotations
 
 from ..ir import stmt as S
 from ..ir.buffer import Buffer, BufferRegion
-from ..ir.expr import PrimExpr, Var, call, convert, const, StringImm, IntImm
+from ..ir.expr import Var, call, convert, StringImm, IntImm
 from ..ir import dtypes as _dt
 from .builder import current_builder
 

@@ -18,7 +18,7 @@ from typing import Tuple, Union
 
 from ..ir import stmt as S
 from ..ir import tileop as O
-from ..ir.buffer import Buffer, BufferRegion, to_region
+from ..ir.buffer import Buffer, to_region
 from ..ir.expr import IntImm, call, convert
 from ..ir import dtypes as _dt
 from .builder import current_builder

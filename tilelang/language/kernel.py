@@ -7,10 +7,10 @@ Reference: ``tilelang/language/kernel.py:228-358`` (``KernelLaunchFrame``,
 """
 from __future__ import annotations
 
-from typing import List, Optional
+from typing import Optional
 
 from ..ir import stmt as S
-from ..ir.expr import Var, convert, as_int
+from ..ir.expr import Var, convert
 from .builder import current_builder, BuilderError
 
 

@@ -10,7 +10,7 @@ from __future__ import annotations
 from typing import List, Optional
 
 from ..ir import stmt as S
-from ..ir.expr import Var, convert, const, as_int, PrimExpr
+from ..ir.expr import Var, convert, const
 from ..ir import dtypes as _dt
 from .builder import current_builder
 

@@ -6,8 +6,8 @@ transcendental instructions (``v_exp_f32`` = 2^x, ``v_log_f32``, ``v_rcp_f32``,
 """
 from __future__ import annotations
 
-from ..ir.expr import (PrimExpr, call, cast as _cast, convert, select, binop, const, FloatImm, IntImm,
-                       min_expr, max_expr, ceildiv as _ceildiv, as_int)
+from ..ir.expr import (call, cast as _cast, convert, select, binop, const, FloatImm, min_expr, max_expr,
+                       ceildiv as _ceildiv)
 from ..ir import dtypes as _dt
 
 

@@ -28,7 +28,7 @@ from ..ir import stmt as S
 from ..ir.buffer import Buffer
 from ..ir.expr import Var, PrimExpr
 from ..ir import dtypes as _dt
-from .builder import HELPERS, building, current_builder, has_builder
+from .builder import HELPERS, building
 
 _IR_LOOP_FUNCS = {"range", "serial", "Parallel", "Pipelined", "unroll", "Serial", "Unroll", "Persistent",
                   "vectorized", "grid", "Vectorized"}

@@ -10,8 +10,7 @@ from typing import Optional
 from ..ir import stmt as S
 from ..ir import tileop as O
 from ..ir.buffer import Buffer, BufferRegion, to_region
-from ..ir.expr import BufferLoad, PrimExpr, convert, call, const, as_int, cast, IntImm
-from ..ir import dtypes as _dt
+from ..ir.expr import BufferLoad, PrimExpr, convert, call, const, as_int
 from .builder import current_builder
 
 

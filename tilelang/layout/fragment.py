@@ -16,10 +16,9 @@ register index.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
-from ..ir.expr import PrimExpr, as_int, const, convert
 
 
 @dataclass(frozen=True)

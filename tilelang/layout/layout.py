@@ -17,9 +17,9 @@ global *source* address — guide rule 21).
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional, Sequence, Tuple
+from typing import Callable, Optional, Sequence, Tuple
 
-from ..ir.expr import PrimExpr, as_int, convert
+from ..ir.expr import as_int
 
 
 class Layout:

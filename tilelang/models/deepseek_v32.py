@@ -29,8 +29,7 @@ Simplifications (documented, weights are random -- no checkpoint is available): 
 """
 from __future__ import annotations
 
-import math
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Optional
 
 import torch

@@ -27,7 +27,6 @@ import os
 
 import torch
 
-from ..ops.moe import expert_ffn
 
 
 @dataclass

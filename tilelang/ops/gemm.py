@@ -1,5 +1,6 @@
-"""``linear(x, w)`` = x @ w^T on MFMA (f16 / bf16: 16x16x32; fp32: the exact-f32 16x16x4 form) (reference counterpart: examples/deepseek_v32/inference/kernel.py
-``fp8_gemm`` / the model's ``linear``).  One compiled kernel per (M, N, K, dtype, target); the
+"""``linear(x, w)`` = x @ w^T on MFMA (f16 / bf16: 16x16x32; fp32: the exact-f32 16x16x4 form)
+(reference counterpart: examples/deepseek_v32/inference/kernel.py ``fp8_gemm`` / the model's
+``linear``).  One compiled kernel per (M, N, K, dtype, target); the
 tile is chosen by M so decode-sized (skinny) and prefill-sized GEMMs both fill the CUs."""
 from __future__ import annotations
 

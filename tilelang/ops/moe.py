@@ -177,7 +177,8 @@ def max_padded_rows(n_assign: int, E: int, block_M: int) -> int:
 def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: str, stable: bool = False,
                  threads: int = 1024):
     """Dispatch plan of ``n`` assignments (``expert_ids[n]``; assignment ``j`` reads source row
-    ``j // div``; a negative id is an empty slot: not placed, ``dest[j] = -1``): ``dest[j]`` (its padded row), ``row_src[max_rows]``, ``tile_expert``, ``counts[E]``,
+    ``j // div``; a negative id is an empty slot: not placed, ``dest[j] = -1``): ``dest[j]`` (its
+    padded row), ``row_src[max_rows]``, ``tile_expert``, ``counts[E]``,
     ``tile_rows`` (valid rows of every row tile: they are a prefix of the tile).
 
     One workgroup.  ``stable=False``: rows of one expert are placed in LDS-atomic order (each

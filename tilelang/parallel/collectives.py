@@ -14,7 +14,6 @@ inference example uses raw ``dist.all_reduce`` / ``all_gather`` for TP/EP
 """
 from __future__ import annotations
 
-import itertools
 from typing import List, Optional, Union
 
 import torch

@@ -30,7 +30,7 @@ from ..ir import lowered as L
 from ..ir import stmt as S
 from ..ir import tileop as O
 from ..ir.buffer import Buffer, BufferRegion
-from ..ir.expr import BufferLoad, IntImm, PrimExpr, Var, as_int, binop, call, cast, const
+from ..ir.expr import BufferLoad, IntImm, Var, as_int, binop, call, cast, const
 
 DIR = {"h": 0, "v": 1, "all": 2}
 

@@ -17,7 +17,7 @@ Two views of the same op:
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import List, Optional, Tuple
+from typing import List, Tuple
 
 from ..ir import tileop as O
 

@@ -29,7 +29,7 @@ import mmap
 import os
 import threading
 import uuid
-from typing import List, Optional, Sequence, Tuple
+from typing import List, Optional, Tuple
 
 _override: Optional[Tuple[int, int]] = None
 _global_ctx: Optional["MeshContext"] = None
@@ -184,7 +184,8 @@ class MeshContext:
         GPU holds at once) would wait forever.  Refuse such launches up front."""
         need = nblocks * self.ranks_on_device
         if need > resident:
-            raise MeshError(f"{label}: T.comm kernel with {nblocks} blocks x {self.ranks_on_device} rank(s) on this GPU "
+            raise MeshError(f"{label}: T.comm kernel with {nblocks} blocks x {self.ranks_on_device} rank(s) "
+                            f"on this GPU "
                             f"needs {need} co-resident workgroups but the GPU holds {resident}; use a persistent grid "
                             f"(T.Persistent / a loop over tiles inside fewer blocks)")
 
@@ -276,7 +277,8 @@ class ProcessMesh(MeshContext):
         rank = dist.get_rank()
         if device is None:
             if dist.get_backend() == "nccl":
-                device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", rank % max(1, torch.cuda.device_count()))))
+                local = os.environ.get("LOCAL_RANK", rank % max(1, torch.cuda.device_count()))
+                device = torch.device("cuda", int(local))
             else:
                 device = torch.device("cpu")
         super().__init__(nrow, ncol, rank, device)

@@ -9,8 +9,7 @@ x split), COLUMN (no y split), ALL (full copy everywhere).
 """
 from __future__ import annotations
 
-import math
-from typing import List, Optional, Sequence, Tuple
+from typing import List, Sequence, Tuple
 
 import torch
 

@@ -1,8 +1,11 @@
 """Kernel timing (reference ``tilelang/profiler/bench.py:63-204``).
 
-MI355X specifics: the cache flush before every timed launch writes a 512 MiB buffer so
-that both the per-XCD L2s (8 x 4 MiB) and the 256 MiB Infinity Cache are evicted
-(the reference flushes 256 MB, sized for NVIDIA L2).  Timing uses HIP events on the
+MI355X specifics: the cache flush before every timed launch READS a 512 MiB buffer so that
+both the per-XCD L2s (8 x 4 MiB) and the 256 MiB Infinity Cache are evicted (the reference
+writes 256 MB, sized for NVIDIA L2).  Reading matters on MI355X: a zero-fill leaves up to
+256 MiB of dirty Infinity-Cache lines that the timed kernel then pays to write back -- a
+streaming copy measured 4.4 TB/s after a write flush (gpurun_out r3 membound sweep), i.e. the
+flush's write-back was being billed to the kernel.  Timing uses HIP events on the
 current stream; ``backend="profiler"`` uses torch.profiler device time (rocprofiler).
 """
 from __future__ import annotations
@@ -16,9 +19,16 @@ def _flush_buffer(device):
     import torch
     b = _FLUSH.get(device)
     if b is None:
-        b = torch.empty(512 * 1024 * 1024 // 4, dtype=torch.int32, device=device)
-        _FLUSH[device] = b
-    return b
+        b = torch.zeros(512 * 1024 * 1024 // 4, dtype=torch.int32, device=device)
+        _FLUSH[device] = (b, torch.empty(1, dtype=torch.int32, device=device))
+    return _FLUSH[device]
+
+
+def _flush(cache):
+    """Evict L2 + Infinity Cache without leaving dirty lines (a max-reduction over 512 MiB)."""
+    import torch
+    buf, out = cache
+    torch.amax(buf, dim=0, keepdim=True, out=out)
 
 
 def do_bench(fn: Callable, warmup: float = 25, rep: float = 100, _n_warmup: int = 0, _n_repeat: int = 0,
@@ -38,7 +48,7 @@ def do_bench(fn: Callable, warmup: float = 25, rep: float = 100, _n_warmup: int 
     s.record()
     for _ in range(5):
         if cache is not None:
-            cache.zero_()
+            _flush(cache)
         fn()
     e.record()
     torch.cuda.synchronize()
@@ -51,7 +61,7 @@ def do_bench(fn: Callable, warmup: float = 25, rep: float = 100, _n_warmup: int 
         fn()
     for i in range(n_repeat):
         if cache is not None:
-            cache.zero_()
+            _flush(cache)
         starts[i].record()
         fn()
         ends[i].record()

@@ -30,7 +30,7 @@ from typing import Optional
 from ..ir import stmt as S
 from ..ir import tileop as O
 from ..ir.buffer import Buffer, BufferRegion
-from ..ir.expr import IntImm, as_int, binop
+from ..ir.expr import IntImm, binop
 from .utils import Mutator, flatten_seq
 
 

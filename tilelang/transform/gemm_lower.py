@@ -16,8 +16,6 @@ from __future__ import annotations
 from typing import Dict, Optional
 
 from ..ir import tileop as O
-from ..ir.buffer import Buffer
-from ..ir.expr import as_int
 from ..layout import mfma as MF
 from ..layout.fragment import make_linear_fragment, Fragment
 from ..layout.layout import LinearLayout, SwizzleLayout

@@ -16,14 +16,14 @@ levels, BFS propagation, ``LayoutConflictException``) and each op's
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, List, Optional
 
 from ..ir import stmt as S
 from ..ir import tileop as O
 from ..ir.buffer import Buffer, BufferRegion
-from ..ir.expr import BufferLoad, PrimExpr, Var, as_int, post_order, loads_of
+from ..ir.expr import Var, as_int, loads_of
 from ..layout.fragment import Digit, Fragment, make_linear_fragment, make_replicated_fragment
-from ..layout.layout import Layout, SwizzleLayout, LinearLayout
+from ..layout.layout import LinearLayout
 from ..layout import mfma as MF
 
 

@@ -13,7 +13,7 @@ model used to choose swizzles holds for every buffer.  Buffers whose live ranges
 """
 from __future__ import annotations
 
-from typing import Dict, List, Tuple
+from typing import Dict, List
 
 from ..ir import stmt as S
 from ..ir import lowered as L

@@ -18,7 +18,7 @@ After this pass:
 from __future__ import annotations
 
 import math
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, List, Optional
 
 from ..ir import stmt as S
 from ..ir import tileop as O
@@ -26,13 +26,13 @@ from ..ir import lowered as L
 from ..ir import dtypes as _dt
 from ..ir.buffer import Buffer, BufferRegion
 from ..ir.expr import (BinOp, BufferLoad, Call, IntImm, PrimExpr, Var, as_int, binop, call, cast, compile_py, const,
-                       convert, divisible_by, evaluate, free_vars, logical_and, logical_not, select, substitute, transform,
-                       post_order, loads_of, modular)
-from ..layout.fragment import Digit, Fragment, make_linear_fragment
-from ..layout.layout import Layout, LinearLayout, SwizzleLayout
-from .layout_inference import ParallelNest, collect_nests, lift_layout, _index_map
+                       convert, divisible_by, free_vars, logical_and, logical_not, select, substitute, transform,
+                       post_order, modular)
+from ..layout.fragment import Digit, Fragment
+from ..layout.layout import LinearLayout, SwizzleLayout
+from .layout_inference import ParallelNest
 from .pipeline import AsyncCopyOp, GatherIndexOp, StagedCopyOp
-from .utils import Mutator, Substituter, bound, flatten_seq
+from .utils import Mutator, Substituter, bound
 from . import gemm_lower
 
 

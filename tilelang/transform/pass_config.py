@@ -123,7 +123,8 @@ def validate_pass_configs(cfg: dict) -> dict:
         if k in UNSUPPORTED and v not in (None, False, 0):
             raise NotImplementedError(f"pass config {k!r}: {UNSUPPORTED[k]}")
         if k in SATISFIED and v is not None and bool(v) != SATISFIED[k] and bool(v) != DEFAULTS.get(k, False):
-            raise NotImplementedError(f"pass config {k}={v!r} asks for an NVIDIA-only feature that gfx950 does not have")
+            raise NotImplementedError(f"pass config {k}={v!r} asks for an NVIDIA-only feature that gfx950 "
+                                      "does not have")
         if k == "tl.mfma_shape" and v not in (None, "16x16", "32x32"):
             raise ValueError(f"tl.mfma_shape must be '16x16' or '32x32', got {v!r}")
         if k == "tl.gemm_phased" and v not in (None, True, False, "prio"):

@@ -25,11 +25,10 @@ from ..ir import stmt as S
 from ..ir import tileop as O
 from ..ir import lowered as L
 from ..ir.buffer import Buffer, BufferRegion
-from ..ir.expr import (PrimExpr, Var, IntImm, as_int, binop, const, convert, divisible_by, free_vars, substitute,
-                       call)
+from ..ir.expr import PrimExpr, Var, IntImm, as_int, binop, convert, divisible_by, free_vars, substitute
 from ..ir import dtypes as _dt
 from ..layout.layout import Layout, LinearLayout, SwizzleLayout
-from .utils import BufferReplacer, Mutator, Substituter, bound, flatten_seq
+from .utils import BufferReplacer, Mutator, bound, flatten_seq
 
 
 import logging as _logging

@@ -17,7 +17,7 @@ from typing import List, Set, Tuple
 from ..ir import stmt as S
 from ..ir import lowered as L
 from ..ir.buffer import Buffer
-from ..ir.expr import BufferLoad, PrimExpr, post_order, loads_of
+from ..ir.expr import BufferLoad, PrimExpr, post_order
 
 _BARRIERS = {"tl::sync_threads", "tl::barrier_raw"}
 

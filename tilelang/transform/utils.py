@@ -1,14 +1,13 @@
 """IR rewriting utilities shared by the passes."""
 from __future__ import annotations
 
-from typing import Callable, Dict, List, Optional
+from typing import Dict, List
 
 from ..ir import stmt as S
 from ..ir import tileop as O
 from ..ir import lowered as L
 from ..ir.buffer import Buffer, BufferRegion
-from ..ir.expr import (BinOp, BufferLoad, Call, Cast, PrimExpr, Select, UnOp, Var, as_int, binop, cast, convert,
-                       logical_not, select, substitute, transform as expr_transform, IntImm)
+from ..ir.expr import BinOp, BufferLoad, Cast, PrimExpr, Var, substitute, transform as expr_transform, IntImm
 
 
 class Mutator:

@@ -9,7 +9,6 @@ reference's ``Sunmmio`` target string maps to a cpu target with its default 4x4 
 """
 from __future__ import annotations
 
-import os
 import re
 from dataclasses import dataclass, field
 from typing import Optional, Tuple
