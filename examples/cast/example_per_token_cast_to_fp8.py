@@ -14,26 +14,34 @@ FP8_MAX = 448.0
 
 
 @tilelang.jit(out_idx=[1, 2])
-def per_token_cast_to_fp8(M, N, blk_m=8, group_size=128, threads=128):
+def per_token_cast_to_fp8(M, N, blk_m=8, group_size=128, threads=128, groups=1, nt=True):
+    """``groups``: 128-column groups per block (one block reads ``blk_m x groups*128``); ``nt``: the
+    input is streamed once (non-temporal loads and stores)."""
     dtype = "float32"
+    gw = groups * group_size
+    assert N % gw == 0
 
     @T.prim_func
     def per_token_cast(X: T.Tensor((M, N), dtype), X_fp8: T.Tensor((M, N), "float8_e4m3fn"),
                        X_amax: T.Tensor((M, T.ceildiv(N, group_size)), dtype)):
-        with T.Kernel(T.ceildiv(M, blk_m), T.ceildiv(N, group_size), threads=threads) as (bx, by):
-            y = T.alloc_fragment((blk_m, group_size), dtype)
-            amax = T.alloc_fragment((blk_m, ), dtype)
-            scale = T.alloc_fragment((blk_m, ), dtype)
-            q = T.alloc_fragment((blk_m, group_size), "float8_e4m3fn")
-            T.copy(X[bx * blk_m:(bx + 1) * blk_m, by * group_size:(by + 1) * group_size], y)
-            T.reduce_absmax(y, amax, dim=1)
-            for i in T.Parallel(blk_m):
-                scale[i] = T.max(amax[i], 1e-4) / FP8_MAX
-            for i, j in T.Parallel(blk_m, group_size):
-                q[i, j] = T.clamp(y[i, j] / scale[i], -FP8_MAX, FP8_MAX)
-            for i in T.Parallel(blk_m):
-                X_amax[bx * blk_m + i, by] = scale[i]
-            T.copy(q, X_fp8[bx * blk_m:(bx + 1) * blk_m, by * group_size:(by + 1) * group_size])
+        with T.Kernel(T.ceildiv(M, blk_m), N // gw, threads=threads) as (bx, by):
+            y = T.alloc_fragment((blk_m, groups, group_size), dtype)
+            amax = T.alloc_fragment((blk_m, groups), dtype)
+            scale = T.alloc_fragment((blk_m, groups), dtype)
+            q = T.alloc_fragment((blk_m, groups, group_size), "float8_e4m3fn")
+            if nt:
+                T.annotate_nontemporal(X, X_fp8)
+            for i, g, j in T.Parallel(blk_m, groups, group_size):
+                y[i, g, j] = X[bx * blk_m + i, by * gw + g * group_size + j]
+            T.reduce_absmax(y, amax, dim=2)
+            for i, g in T.Parallel(blk_m, groups):
+                scale[i, g] = T.max(amax[i, g], 1e-4) / FP8_MAX
+            for i, g, j in T.Parallel(blk_m, groups, group_size):
+                q[i, g, j] = T.clamp(y[i, g, j] / scale[i, g], -FP8_MAX, FP8_MAX)
+            for i, g in T.Parallel(blk_m, groups):
+                X_amax[bx * blk_m + i, by * groups + g] = scale[i, g]
+            for i, g, j in T.Parallel(blk_m, groups, group_size):
+                X_fp8[bx * blk_m + i, by * gw + g * group_size + j] = q[i, g, j]
 
     return per_token_cast
 

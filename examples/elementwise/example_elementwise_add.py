@@ -11,7 +11,9 @@ import tilelang.language as T
 
 
 @tilelang.jit(out_idx=[-1])
-def elementwise_add(M, N, block_M=32, block_N=256, threads=256, in_dtype="float32", out_dtype="float32"):
+def elementwise_add(M, N, block_M=32, block_N=256, threads=256, in_dtype="float32", out_dtype="float32", nt=True):
+    """``nt``: A, B and C are streamed once -- non-temporal 16-byte accesses (evict_first)."""
+    pol = "evict_first" if nt else None
 
     @T.prim_func
     def main(A: T.Tensor((M, N), in_dtype), B: T.Tensor((M, N), in_dtype), C: T.Tensor((M, N), out_dtype)):
@@ -19,11 +21,11 @@ def elementwise_add(M, N, block_M=32, block_N=256, threads=256, in_dtype="float3
             A_local = T.alloc_fragment((block_M, block_N), in_dtype)
             B_local = T.alloc_fragment((block_M, block_N), in_dtype)
             C_local = T.alloc_fragment((block_M, block_N), out_dtype)
-            T.copy(A[by * block_M, bx * block_N], A_local)
-            T.copy(B[by * block_M, bx * block_N], B_local)
+            T.copy(A[by * block_M, bx * block_N], A_local, eviction_policy=pol)
+            T.copy(B[by * block_M, bx * block_N], B_local, eviction_policy=pol)
             for i, j in T.Parallel(block_M, block_N):
                 C_local[i, j] = A_local[i, j] + B_local[i, j]
-            T.copy(C_local, C[by * block_M, bx * block_N])
+            T.copy(C_local, C[by * block_M, bx * block_N], eviction_policy=pol)
 
     return main
 

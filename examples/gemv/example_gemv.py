@@ -13,7 +13,9 @@ import tilelang.language as T
 
 
 @tilelang.jit(out_idx=[-1])
-def gemv(N, K, block_N=8, block_K=512, threads=256, dtype="float16", accum_dtype="float"):
+def gemv(N, K, block_N=8, block_K=512, threads=256, dtype="float16", accum_dtype="float", nt=True):
+    """``nt``: the weight matrix is streamed once -- non-temporal 16-byte loads."""
+    pol = "evict_first" if nt else None
 
     @T.prim_func
     def main(A: T.Tensor((N, K), dtype), x: T.Tensor((K, ), dtype), y: T.Tensor((N, ), dtype)):
@@ -23,7 +25,7 @@ def gemv(N, K, block_N=8, block_K=512, threads=256, dtype="float16", accum_dtype
             row = T.alloc_fragment((block_N, ), accum_dtype)
             T.clear(acc)
             for ko in T.serial(T.ceildiv(K, block_K)):
-                T.copy(A[bn * block_N, ko * block_K], a_frag)
+                T.copy(A[bn * block_N, ko * block_K], a_frag, eviction_policy=pol)
                 for i, j in T.Parallel(block_N, block_K):
                     acc[i, j] += T.Cast(accum_dtype, a_frag[i, j]) * T.Cast(accum_dtype, x[ko * block_K + j])
             T.reduce_sum(acc, row, dim=1)

@@ -13,7 +13,9 @@ import tilelang.language as T
 
 
 @tilelang.jit(out_idx=[-1])
-def rms_norm(M, N, blk_m=4, threads=256, dtype="float32", eps=1e-12):
+def rms_norm(M, N, blk_m=4, threads=256, dtype="float32", eps=1e-12, nt=True):
+    """``nt``: input and output rows are streamed once -- non-temporal 16-byte accesses."""
+    pol = "evict_first" if nt else None
 
     @T.prim_func
     def main(A: T.Tensor((M, N), dtype), B: T.Tensor((M, N), dtype)):
@@ -22,7 +24,7 @@ def rms_norm(M, N, blk_m=4, threads=256, dtype="float32", eps=1e-12):
             A_pow = T.alloc_fragment((blk_m, N), "float32")
             A_powsum = T.alloc_fragment((blk_m, ), "float32")
             B_local = T.alloc_fragment((blk_m, N), dtype)
-            T.copy(A[bx * blk_m:(bx + 1) * blk_m, :], A_local)
+            T.copy(A[bx * blk_m:(bx + 1) * blk_m, :], A_local, eviction_policy=pol)
             for i, j in T.Parallel(blk_m, N):
                 A_pow[i, j] = A_local[i, j] * A_local[i, j]
             T.reduce_sum(A_pow, A_powsum, dim=1)
@@ -30,7 +32,7 @@ def rms_norm(M, N, blk_m=4, threads=256, dtype="float32", eps=1e-12):
                 A_powsum[i] = T.rsqrt(A_powsum[i] / N + eps)
             for i, j in T.Parallel(blk_m, N):
                 B_local[i, j] = A_local[i, j] * A_powsum[i]
-            T.copy(B_local, B[bx * blk_m:(bx + 1) * blk_m, :])
+            T.copy(B_local, B[bx * blk_m:(bx + 1) * blk_m, :], eviction_policy=pol)
 
     return main
 

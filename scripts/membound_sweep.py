@@ -62,29 +62,31 @@ def main():
     if a.quick:
         cfgs = cfgs[:3]
 
-    def add_k(bm, bn, t):
-        k = elementwise_add(M, N, bm, bn, t)
+    def add_k(bm, bn, t, nt=True):
+        k = elementwise_add(M, N, bm, bn, t, nt=nt)
         return lambda: k(x, y)
 
     def add_check(fn):
         torch.testing.assert_close(fn(), x + y)
 
     print("elementwise add fp32 8192^2 (3 x 256 MiB)", flush=True)
-    sweep("add", 3 * x.numel() * 4, [(f"{c}", (lambda c=c: add_k(*c))) for c in cfgs], lambda: torch.add(x, y),
+    sweep("add", 3 * x.numel() * 4, [(f"{c} nt={nt}", (lambda c=c, nt=nt: add_k(*c, nt=nt))) for c in cfgs
+                                     for nt in (True, False)], lambda: torch.add(x, y),
           add_check)
 
     from rms_norm import rms_norm
     cfgs = [(1, 256), (1, 512), (1, 1024), (2, 512), (2, 1024), (4, 1024), (4, 256), (8, 1024)]
 
-    def rms_k(bm, t):
-        k = rms_norm(M, N, bm, t)
+    def rms_k(bm, t, nt=True):
+        k = rms_norm(M, N, bm, t, nt=nt)
         return lambda: k(x)
 
     def rms_ref():
         return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + 1e-12)
 
     print("rms norm fp32 8192^2 (2 x 256 MiB)", flush=True)
-    sweep("rms", 2 * x.numel() * 4, [(f"{c}", (lambda c=c: rms_k(*c))) for c in cfgs], rms_ref,
+    sweep("rms", 2 * x.numel() * 4, [(f"{c} nt={nt}", (lambda c=c, nt=nt: rms_k(*c, nt=nt))) for c in cfgs
+                                     for nt in (True, False)], rms_ref,
           lambda fn: torch.testing.assert_close(fn(), rms_ref(), rtol=1e-4, atol=1e-4))
 
     from example_gemv import gemv
@@ -94,24 +96,27 @@ def main():
     cfgs = [(8, 512, 256), (8, 1024, 256), (8, 2048, 256), (4, 2048, 256), (16, 1024, 256), (4, 4096, 256),
             (2, 4096, 256), (8, 2048, 512), (16, 2048, 512)]
 
-    def gemv_k(bn, bk, t):
-        k = gemv(NG, KG, bn, bk, t)
+    def gemv_k(bn, bk, t, nt=True):
+        k = gemv(NG, KG, bn, bk, t, nt=nt)
         return lambda: k(A, xv)
 
     print("gemv fp16 16384^2 (512 MiB of weights)", flush=True)
-    sweep("gemv", A.numel() * 2, [(f"{c}", (lambda c=c: gemv_k(*c))) for c in cfgs], lambda: A @ xv,
+    sweep("gemv", A.numel() * 2, [(f"{c} nt={nt}", (lambda c=c, nt=nt: gemv_k(*c, nt=nt))) for c in cfgs
+                                  for nt in (True, False)], lambda: A @ xv,
           lambda fn: torch.testing.assert_close(fn().float(), (A.float() @ xv.float()), rtol=2e-2, atol=2e-1))
 
     from example_per_token_cast_to_fp8 import per_token_cast_to_fp8
     xh = torch.randn(M, N, device="cuda")
-    cfgs = [(8, 128), (8, 256), (16, 256), (4, 128), (32, 512), (16, 512)]
+    cfgs = [(8, 128, 1), (8, 128, 4), (8, 256, 4), (16, 256, 2), (4, 256, 8), (8, 256, 8), (16, 512, 4),
+            (32, 256, 1), (8, 512, 8)]
 
-    def cast_k(bm, t):
-        k = per_token_cast_to_fp8(M, N, bm, 128, t)
+    def cast_k(bm, t, g, nt=True):
+        k = per_token_cast_to_fp8(M, N, bm, 128, t, g, nt=nt)
         return lambda: k(xh)
 
     print("per-token(group 128) fp8 cast fp32 8192^2 (256 MiB in, 64 MiB + scales out)", flush=True)
-    sweep("cast", xh.numel() * 5 + M * (N // 128) * 4, [(f"{c}", (lambda c=c: cast_k(*c))) for c in cfgs])
+    sweep("cast", xh.numel() * 5 + M * (N // 128) * 4, [(f"{c} nt={nt}", (lambda c=c, nt=nt: cast_k(*c, nt=nt)))
+                                                         for c in cfgs for nt in (True, False)])
 
 
 if __name__ == "__main__":

@@ -195,6 +195,11 @@ class CodeGen:
             return f"({a} {op} {b})"
         return f"({a} {op} {b})"
 
+    def _nt(self, buf) -> bool:
+        """Streamed-once global buffer (``T.copy(..., eviction_policy="evict_first")``): non-temporal
+        vector accesses (``global_load/store ... nt``) on the GPU."""
+        return not self.is_cpu and buf.scope == "global" and getattr(buf, "nontemporal", False)
+
     def call(self, x: Call) -> str:
         op = x.op
         args = x.args
@@ -342,11 +347,13 @@ class CodeGen:
             ct = self.ctype(b.dtype)
             vals = ", ".join(self.e(v) for v in st.values)
             dst = f"&{self.buf_ref(b)}[{self.e(st.index)}]"
-            self.w(f"{{ {ct} _v[{n}] = {{{vals}}}; tl::store_vec<{ct}, {n}>({dst}, _v); }}")
+            fn = "store_vec_nt" if self._nt(b) else "store_vec"
+            self.w(f"{{ {ct} _v[{n}] = {{{vals}}}; tl::{fn}<{ct}, {n}>({dst}, _v); }}")
         elif isinstance(st, L.VecLoadStmt):
             ct = self.ctype(st.src.dtype)
             dst = f"*reinterpret_cast<{ct}(*)[{st.n}]>(&{self.buf_ref(st.dst)}[{st.dst_index}])"
-            self.w(f"tl::load_vec<{ct}, {st.n}>({dst}, &{self.buf_ref(st.src)}[{self.e(st.src_index)}]);")
+            fn = "load_vec_nt" if self._nt(st.src) else "load_vec"
+            self.w(f"tl::{fn}<{ct}, {st.n}>({dst}, &{self.buf_ref(st.src)}[{self.e(st.src_index)}]);")
         elif isinstance(st, L.CopyBytesStmt):
             self.w(f"tl::copy_bytes<{st.nbytes}>(&{self.buf_ref(st.dst)}[{self.e(st.dst_index)}], "
                    f"&{self.buf_ref(st.src)}[{self.e(st.src_index)}]);")

@@ -65,6 +65,23 @@ template <typename T, int N> TL_DEVICE void store_vec(T* dst, const T (&vals)[N]
   *reinterpret_cast<V*>(dst) = v;
 }
 
+// non-temporal variants (global_load / global_store ... nt): streamed-once data
+template <typename T, int N> TL_DEVICE void store_vec_nt(T* dst, const T (&vals)[N]) {
+  constexpr int B = N * (int)sizeof(T);
+  static_assert(B == 1 || B == 2 || B == 4 || B == 8 || B == 16, "vector store width");
+  typedef typename bytes_t<B>::type V;
+  V v;
+  __builtin_memcpy(&v, vals, B);
+  __builtin_nontemporal_store(v, reinterpret_cast<V*>(dst));
+}
+
+template <typename T, int N> TL_DEVICE void load_vec_nt(T (&vals)[N], const T* src) {
+  constexpr int B = N * (int)sizeof(T);
+  typedef typename bytes_t<B>::type V;
+  V v = __builtin_nontemporal_load(reinterpret_cast<const V*>(src));
+  __builtin_memcpy(vals, &v, B);
+}
+
 template <typename T, int N> TL_DEVICE void load_vec(T (&vals)[N], const T* src) {
   constexpr int B = N * (int)sizeof(T);
   typedef typename bytes_t<B>::type V;

@@ -33,7 +33,8 @@ from .math import (max, min, abs, round, pow)  # noqa: A004,F401
 from .builtin import (sync_threads, sync_warp, sync_global, sync_grid, fence_proxy_async, memory_fence, set_priority,
                       get_lane_idx, get_warp_idx, get_warp_idx_sync, get_warp_group_idx, shfl_xor, shfl_down, shfl_up,
                       shfl_sync, ballot, clock, call_extern, call_intrin, evaluate, loop_break, device_assert, print,
-                      use_swizzle, annotate_layout, annotate_safe_value, annotate_l2_hit_ratio, annotate_padding, attr,
+                      use_swizzle, annotate_layout, annotate_safe_value, annotate_l2_hit_ratio, annotate_padding,
+                      annotate_nontemporal, attr,
                       block_attr, import_source, no_set_max_nreg, set_max_nreg, disable_warp_group_reg_alloc, assume,
                       address_of, dynamic, symbolic)
 from .builder import _IfFrame as If, _ElseFrame as Else, _WhileFrame as While

@@ -158,6 +158,18 @@ def annotate_padding(*args, **kwargs):
     return None
 
 
+def annotate_nontemporal(*buffers):
+    """gfx950 addition: the global ``buffers`` are streamed once -- every vector access to them is
+    non-temporal (``global_load/store ... nt``), as ``T.copy(..., eviction_policy="evict_first")``
+    does for a copy's global side.  For element loops that read or write global memory directly."""
+    for b in buffers:
+        buf = b.buffer if hasattr(b, "buffer") else b
+        if buf.scope != "global":
+            raise ValueError(f"T.annotate_nontemporal: {buf.name} is not a global tensor")
+        buf.nontemporal = True
+        current_builder().emit(S.AttrStmt("tl.nontemporal", buf.name))
+
+
 def attr(node, key, value):
     current_builder().emit(S.AttrStmt(key, value))
 

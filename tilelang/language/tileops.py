@@ -44,6 +44,14 @@ def copy(src, dst, coalesced_width: Optional[int] = None, disable_tma: bool = Fa
         # T.copy(scalar, dst) == fill
         return fill(dst, src)
     s, d = _pair_regions(src, dst)
+    if eviction_policy not in (None, "evict_normal", "evict_first", "evict_last"):
+        raise ValueError(f"T.copy: eviction_policy must be evict_normal / evict_first / evict_last, "
+                         f"got {eviction_policy!r}")
+    if eviction_policy == "evict_first":
+        # streamed-once global operand: non-temporal vector accesses (codegen/hip.py _nt)
+        for r in (s, d):
+            if r.buffer.scope == "global":
+                r.buffer.nontemporal = True
     return _emit(O.CopyOp(s, d, coalesced_width, disable_tma, eviction_policy))
 
 

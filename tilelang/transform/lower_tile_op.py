@@ -155,6 +155,7 @@ class LowerCtx:
             fb = Buffer(b.name, [size] if size is not None else [b.numel()], b.dtype, b.scope)
             fb.orig = b
             fb.param_index = b.param_index
+            fb.nontemporal = getattr(b, "nontemporal", False)
             fb._auto_name = False
             self.flat[b] = fb
         return fb
