@@ -97,6 +97,27 @@ def quant_act_mxfp8(M, K, block_M=64, threads=256, dtype="bfloat16"):
     return main
 
 
+@tilelang.jit(out_idx=[-1])
+def mxfp4_gemv(M, N, K, block_N=None, threads=256, dtype="bfloat16"):
+    """Decode-sized (M <= 8) bf16 x MXFP4: a pure weight stream (include/tl/gemv.h): 16-byte
+    non-temporal weight loads, v_cvt_scalef32_pk_f32_fp4 (two codes per instruction, the e8m0
+    scale folded in), FMAs against x held in registers, one block reduction per BLOCK_N rows."""
+    assert M <= 8 and K % 32 == 0 and dtype == "bfloat16"
+    if block_N is None:
+        block_N = max(2, 16 // M)
+
+    @T.prim_func
+    def main(A: T.Tensor((M, K), dtype), Bq: T.Tensor((N, K // 2), "uint8"), S: T.Tensor((N, K // 32), "uint8"),
+             C: T.Tensor((M, N), dtype)):
+        with T.Kernel(T.ceildiv(N, block_N), threads=threads) as bx:
+            red = T.alloc_shared((threads // 64, block_N * M), "float32")
+            T.evaluate(T.call_extern("handle", f"tl::mxfp4_gemv<{M}, {block_N}, {threads}>", T.address_of(A[0, 0]),
+                                     T.address_of(Bq[0, 0]), T.address_of(S[0, 0]), T.address_of(C[0, 0]), N, K,
+                                     bx * block_N, T.address_of(red[0, 0])))
+
+    return main
+
+
 def mxfp4_gemm_native(A, Bq, S):
     """bf16 A x MXFP4 weights on the scaled matrix cores (A quantised to MXFP8 on the fly)."""
     import os
@@ -115,6 +136,16 @@ def ref_program(A, Bq, S):
 
 def main(M=16, N=8192, K=8192, mode="dequant"):
     import torch
+    if mode == "gemv":
+        kernel = mxfp4_gemv(M, N, K)
+        A = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        Bq, S = quantize_mxfp4(torch.randn(N, K, device="cuda"))
+        c = kernel(A, Bq, S)
+        torch.testing.assert_close(c.float(), ref_program(A, Bq, S).float(), rtol=2e-2, atol=1.0)
+        lat = kernel.get_profiler().do_bench(lambda: kernel(A, Bq, S))
+        wbytes = N * K // 2 + N * K // 32
+        print(f"bf16 x mxfp4 GEMV {M}x{N}x{K}: {lat * 1e3:.1f} us, {wbytes / lat * 1e-9:.2f} TB/s of weights")
+        return
     if mode == "native":
         A = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
         Bq, S = quantize_mxfp4(torch.randn(N, K, device="cuda"))
@@ -144,6 +175,6 @@ if __name__ == "__main__":
     p.add_argument("--m", type=int, default=16)
     p.add_argument("--n", type=int, default=8192)
     p.add_argument("--k", type=int, default=8192)
-    p.add_argument("--mode", choices=["dequant", "native"], default="dequant")
+    p.add_argument("--mode", choices=["dequant", "native", "gemv"], default="dequant")
     a = p.parse_args()
     main(a.m, a.n, a.k, a.mode)

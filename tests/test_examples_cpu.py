@@ -380,6 +380,17 @@ def test_dequant_gemm_mxfp4_cpu():
     torch.testing.assert_close(k(A, Bq, S).float(), ref_program(A, Bq, S).float(), rtol=2e-2, atol=0.5)
 
 
+@pytest.mark.parametrize("M", [1, 3])
+def test_mxfp4_gemv_cpu(M):
+    from example_dequant_gemm_mxfp4 import mxfp4_gemv, ref_program
+    from tilelang.quantize import quantize_mxfp4
+    N, K = 100, 512
+    k = _both(mxfp4_gemv, M, N, K)
+    A = torch.randn(M, K).bfloat16()
+    Bq, S = quantize_mxfp4(torch.randn(N, K))
+    torch.testing.assert_close(k(A, Bq, S).float(), ref_program(A, Bq, S).float(), rtol=2e-2, atol=0.5)
+
+
 def test_gemm_with_mesh_tensor_cpu():
     from example_gemm_with_mesh_tensor import matmul
     k = _both(matmul, 128, 128, 128, 64, 64, 32)

@@ -321,6 +321,18 @@ def test_dequant_gemm_mxfp4_gpu():
                                rtol=2e-2, atol=1.0)
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 8192, 8192), (4, 1000, 4096), (8, 512, 1024)])
+def test_mxfp4_gemv_gpu(M, N, K):
+    """Decode GEMV over MXFP4 weights (tl/gemv.h: hardware fp4 -> bf16 conversion + dot2)."""
+    from example_dequant_gemm_mxfp4 import mxfp4_gemv, ref_program
+    from tilelang.quantize import quantize_mxfp4
+    A = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    Bq, S = quantize_mxfp4(torch.randn(N, K, device="cuda"))
+    k = mxfp4_gemv(M, N, K)
+    assert "mxfp4_gemv<" in k.get_kernel_source()
+    torch.testing.assert_close(k(A, Bq, S).float(), ref_program(A, Bq, S).float(), rtol=2e-2, atol=1.0)
+
+
 def test_sparse_mla_bwd_gpu():
     import sparse_mla_bwd as m
     from tilelang.ops.dsa import sparse_mla_fwd

@@ -228,6 +228,23 @@ template <int FMT> inline float mx_elem(const uint8_t* row, int k) {
 
 inline float e8m0(uint8_t s) { return s == 255 ? NAN : std::ldexp(1.0f, (int)s - 127); }
 
+// tl/gemv.h mxfp4_gemv on the CPU target: the block's BLOCK_N rows, serially
+template <int M, int BLOCK_N, int THREADS>
+inline void mxfp4_gemv(const bfloat16_t* X, const uint8_t* Bq, const uint8_t* S, bfloat16_t* Y, int N, int K, int n0,
+                       float*) {
+  for (int n = n0; n < n0 + BLOCK_N && n < N; ++n)
+    for (int m = 0; m < M; ++m) {
+      float acc = 0.0f;
+      for (int kb = 0; kb < K / 32; ++kb) {
+        float part = 0.0f;
+        for (int k = kb * 32; k < kb * 32 + 32; ++k)
+          part += mx_elem<4>(Bq + (long long)n * (K / 2), k) * (float)X[(long long)m * K + k];
+        acc += part * e8m0(S[(long long)n * (K / 32) + kb]);
+      }
+      Y[(long long)m * N + n] = (bfloat16_t)acc;
+    }
+}
+
 // C[M][N] += sum_k (A[m][k] * 2^(SA[m][k/32]-127)) * (B[n][k] * 2^(SB[n][k/32]-127))
 template <int FA, int FB, int M, int N, int K, int A_COLS, int B_COLS, int SA_STRIDE, int SB_STRIDE>
 inline void cpu_gemm_mx(const void* A_, const void* B_, const void* SA_, const void* SB_, float* C) {

@@ -9,3 +9,4 @@
 #include "debug.h"
 #include "mesh.h"
 #include "ep.h"
+#include "gemv.h"
