@@ -11,8 +11,9 @@ __global__ void probe(unsigned char* out, int pass) {
   for (int j = threadIdx.x; j < 1024; j += 64)
     lds[j] = pass == 0 ? (unsigned char)(j & 255) : (unsigned char)(j >> 8);
   __syncthreads();
-  int2v r = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
-      (__attribute__((address_space(3))) int2v*)((__attribute__((address_space(3))) unsigned char*)lds + threadIdx.x * 8));
+  typedef __attribute__((address_space(3))) unsigned char lds_u8;
+  typedef __attribute__((address_space(3))) int2v lds_i2;
+  int2v r = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_i2*)((lds_u8*)lds + threadIdx.x * 8));
   unsigned char* p = reinterpret_cast<unsigned char*>(&r);
   for (int b = 0; b < 8; ++b) out[threadIdx.x * 8 + b] = p[b];
 }
