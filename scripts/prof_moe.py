@@ -65,6 +65,17 @@ if "--tail-sweep" in sys.argv:  # narrow-tail width of the tail-balanced expert 
         layer.cfg.gemm_cfg = dict(base, stream_k=True, tail_split=ts, phased=ph)
         run(layer, x, f"tail_split={ts} phased={ph}")
     layer.cfg.gemm_cfg = base
+if "--prefetch-ab" in sys.argv:  # phased K-half (+register prefetch when nothing is skipped) vs whole-K loop
+    base = dict(layer.cfg.gemm_cfg or {})
+    for ph, sk in ((False, True), (True, False), (True, True), (False, False), (False, True), (True, False)):
+        layer.cfg.gemm_cfg = dict(base, phased=ph, skip_padding=sk)
+        run(layer, x, f"phased={ph} skip_padding={sk}")
+    layer.cfg.gemm_cfg = dict(base, phased=True, skip_padding=False)
+    out = layer(x).float()
+    g, w1, w2 = (t.to("cuda") for t in init_moe_weights(layer.cfg))
+    ref = moe_reference(x, g, w1, w2, layer.cfg.topk)
+    print("phased/prefetch max abs err", (out - ref).abs().max().item(), "ref max", ref.abs().max().item(), flush=True)
+    layer.cfg.gemm_cfg = base
 if "--sweep" in sys.argv:
     for bm in (128, 256):
         for cfg in (dict(block_N=128, block_K=64, num_stages=2, threads=256),

@@ -43,6 +43,22 @@ def test_prefetch_structure():
     assert "tl::gemm_ss<" not in body
 
 
+def test_prefetch_valid_m_structure():
+    """T.gemm(valid_m=) in the prefetched schedule: one uniform branch per phase around the
+    fragment load AND the MFMAs (same basic block, so the 1:1 interleave still applies)."""
+    from tilelang.ops.moe import expert_gemm_sk_kernel, max_padded_rows
+    mr = max_padded_rows(4096, 8, 256)
+    k = expert_gemm_sk_kernel(mr, 2048, 4096, 8, "bfloat16", "hip", 256, phased=True, skip_padding=True,
+                              block_N=256, block_K=64, num_stages=2, threads=512)
+    src = k.get_kernel_source()
+    body = src[src.index("for (int k"):]
+    guard = "if ((((wave_ / 2) * 64) < nrows[0])) {"
+    assert body.count(guard) >= 2
+    for part in body.split(guard)[1:3]:
+        head = part[:part.index("}")]
+        assert "tl::gemm_ss_load<" in head and "tl::gemm_ss_mma<" in head
+
+
 def test_phased_opt_out_and_shape_gate():
     src = _src(4096, 4096, 4096, phased=False)
     assert "A_shared_k0" not in src and "gemm_ss<half_t, 256, 256, 64," in src

@@ -135,8 +135,11 @@ def test_moe_tail_balanced_gpu():
     g, w1, w2 = (t.to("cuda") for t in init_moe_weights(cfg))
     from tilelang.ops import moe as K
     ref = moe_reference(x, g, w1, w2, cfg.topk, routing=K.route(x, g, cfg.topk))
-    for sk in (True, False):
-        layer.cfg.gemm_cfg = dict(block_N=256, block_K=64, num_stages=2, threads=512, stream_k=sk)
+    for sk, ph, skip in ((True, False, True), (False, False, True), (True, True, True), (True, True, False)):
+        # phased: K-half ring with register-prefetched fragments; skip: padding waves skip
+        # their reads and MFMAs (T.gemm(valid_m=)) inside the prefetched schedule too
+        layer.cfg.gemm_cfg = dict(block_N=256, block_K=64, num_stages=2, threads=512, stream_k=sk, phased=ph,
+                                  skip_padding=skip)
         out = layer(x).float()
         torch.testing.assert_close(out, ref, rtol=3e-2, atol=3e-2 * ref.abs().max().item())
 

@@ -15,6 +15,7 @@
 namespace tl {
 
 typedef __bf16 tl_bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 tl_bf16x8 __attribute__((ext_vector_type(8)));
 
 template <int M, int BLOCK_N, int THREADS>
 TL_DEVICE void mxfp4_gemv(const bfloat16_t* __restrict__ X, const uint8_t* __restrict__ Bq,
@@ -31,11 +32,11 @@ TL_DEVICE void mxfp4_gemv(const bfloat16_t* __restrict__ X, const uint8_t* __res
     for (int m = 0; m < M; ++m) acc[n][m] = 0.f;
   for (int c = tid; c < chunks; c += THREADS) {
     // the thread's x chunk stays packed: 16 bf16 pairs per row
-    intx4 x[M][4];
+    tl_bf16x8 x[M][4];
 #pragma unroll
     for (int m = 0; m < M; ++m)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) x[m][q] = reinterpret_cast<const intx4*>(X + (long long)m * K + c * 32)[q];
+      for (int q = 0; q < 4; ++q) x[m][q] = reinterpret_cast<const tl_bf16x8*>(X + (long long)m * K + c * 32)[q];
     intx4 w[BLOCK_N];
     float sc[BLOCK_N];
 #pragma unroll
@@ -56,13 +57,15 @@ TL_DEVICE void mxfp4_gemv(const bfloat16_t* __restrict__ X, const uint8_t* __res
         const tl_bf16x2 w3 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(u, sc[n], 3);
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          // x pairs for k = 8d .. 8d + 7 are dwords 4d .. 4d + 3 of the chunk (x[m][d] = 16 bytes)
-          const intx4 xv = x[m][d];
+          // x pairs for k = 8d .. 8d + 7 are elements 2b, 2b + 1 of x[m][d].  Pairs are taken with
+          // shufflevector: bit-casting the dwords of an int vector to bf16x2 miscompiles on ROCm
+          // 7.2 (every pair became dword 0 -- csrc/probes/fp4_perm_probe.hip)
+          const tl_bf16x8 xv = x[m][d];
           float a = acc[n][m];
-          a = __builtin_amdgcn_fdot2_f32_bf16(w0, __builtin_bit_cast(tl_bf16x2, xv[0]), a, false);
-          a = __builtin_amdgcn_fdot2_f32_bf16(w1, __builtin_bit_cast(tl_bf16x2, xv[1]), a, false);
-          a = __builtin_amdgcn_fdot2_f32_bf16(w2, __builtin_bit_cast(tl_bf16x2, xv[2]), a, false);
-          a = __builtin_amdgcn_fdot2_f32_bf16(w3, __builtin_bit_cast(tl_bf16x2, xv[3]), a, false);
+          a = __builtin_amdgcn_fdot2_f32_bf16(w0, __builtin_shufflevector(xv, xv, 0, 1), a, false);
+          a = __builtin_amdgcn_fdot2_f32_bf16(w1, __builtin_shufflevector(xv, xv, 2, 3), a, false);
+          a = __builtin_amdgcn_fdot2_f32_bf16(w2, __builtin_shufflevector(xv, xv, 4, 5), a, false);
+          a = __builtin_amdgcn_fdot2_f32_bf16(w3, __builtin_shufflevector(xv, xv, 6, 7), a, false);
           acc[n][m] = a;
         }
       }

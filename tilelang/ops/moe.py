@@ -367,7 +367,7 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
 def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target: str, block_M: int = 256,
                           block_N: int = 256, block_K: int = 64, num_stages: int = 2, threads: int = 512,
                           n_src: Optional[int] = None, swiglu: bool = False, n_cu: int = 256, tail_split: int = 4,
-                          phased: bool = False):
+                          phased: bool = False, skip_padding: bool = True):
     """Tail-balanced variant of ``expert_gemm_kernel`` (same arguments and output).
 
     The (row tile x N tile) units are a data-dependent count U (the routing decides how many
@@ -404,7 +404,7 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
             else:
                 T.copy(A[bx * block_M, k * block_K], A_s)
             T.copy(W[e, col0, k * block_K], W_s)
-            T.gemm(A_s, W_s, C_l, transpose_B=True, valid_m=nrows)
+            T.gemm(A_s, W_s, C_l, transpose_B=True, valid_m=nrows if skip_padding else None)
         if swiglu:
             for i, j in T.Parallel(block_M, bn):
                 if j % 4 < 2:
@@ -575,7 +575,7 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
     if sk and reduce_mesh is None and w1_interleaved:
         # tail-balanced grid: whole tiles for the leading rounds, narrow tiles for the trailing partial round
         skc = {k: v for k, v in cfg.items() if k in ("block_N", "block_K", "num_stages", "threads", "tail_split",
-                                                      "phased")}
+                                                      "phased", "skip_padding")}
         k1 = expert_gemm_sk_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, swiglu=True, n_cu=n_cu,
                                    **skc)
         k1(src_rows.contiguous(), w1, te, row_src, trows, act)
@@ -583,6 +583,8 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
         y = torch.empty(max_rows, H, dtype=src_rows.dtype, device=dev)
         k2(act, w2, te, row_src, trows, y)
         return y, dest
+    for key in ("tail_split", "phased"):  # options of the tail-balanced grid only
+        cfg.pop(key, None)
     if w1_interleaved:
         # gate/up rows interleaved: the activation is the first GEMM's epilogue
         k1 = expert_gemm_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, swiglu=True, **cfg)

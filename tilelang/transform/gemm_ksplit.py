@@ -176,7 +176,8 @@ class _AllocSplit(Mutator):
             if s.buffer in self.done:
                 return S.seq(*keep) if keep else S.SeqStmt([])
             other = self.pairs.get(s.buffer)
-            first = [s.buffer] + ([other] if other is not None and other in self.new_allocs else [])
+            first = [s.buffer] + ([other] if other is not None and other in self.new_allocs and other not in self.done
+                                  else [])
             order = [self.new_allocs[b][0] for b in first] + [self.new_allocs[b][1] for b in first]
             self.done.update(first)
             return S.seq(*(keep + [S.AllocStmt(h) for h in order]))

@@ -1034,25 +1034,37 @@ class TileOpLowerer(Mutator):
         frag = getattr(op, "frag", None)
         if frag is not None:
             # register-prefetched K-half schedule (transform/pipeline.py _prefetch_schedule)
-            if A.scope != "shared" or vm:
+            if A.scope != "shared":
                 raise LoweringError("prefetched T.gemm needs both operands in shared memory")
-            mode, var = frag
+            mode, var = frag[0], frag[1]
             shape = [ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"]]
             if mode == "decl":
                 return L.ObjDeclStmt(f"tl::ss_frags<{', '.join(str(x) for x in shape)}>", var)
-            if mode == "load":
-                out.append(L.CallStmt("tl::gemm_ss_load", [self._operand_ptr(op.A), pb, var, ctx.wave_expr()], shape + [
-                    _b(op.trans_A), _b(op.trans_B), A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
-                    b_cols, f"{swz_b}u"]))
-                return S.SeqStmt(out)
-            # mma: interleaved with the load the schedule issued just before it (same phase)
             ksteps = plan["K"] // 32
             m_rep = plan["M"] // plan["warp_m"] // 16
             n_rep = plan["N"] // plan["warp_n"] // 16
             nload = ksteps * (m_rep * (2 if op.trans_A else 1) + n_rep * (1 if op.trans_B else 2))
             if getattr(ctx.target, "gemm_interleave", None) is False:
                 nload = 0
-            out.append(L.CallStmt("tl::gemm_ss_mma", [var, L.BufferPtr(cl, 0)], shape + [nload]))
+            calls = []
+            if mode in ("load", "load_mma"):
+                calls.append(L.CallStmt("tl::gemm_ss_load", [self._operand_ptr(op.A), pb, var, ctx.wave_expr()],
+                                        shape + [_b(op.trans_A), _b(op.trans_B), A.static_shape()[-1],
+                                                 f"{gemm_lower.encode_swizzle(A.layout)}u", b_cols, f"{swz_b}u"]))
+            if mode in ("mma", "load_mma"):
+                # interleaved with the load issued just before it (same phase, same basic block)
+                mvar = frag[2] if mode == "load_mma" else var
+                calls.append(L.CallStmt("tl::gemm_ss_mma", [mvar, L.BufferPtr(cl, 0)],
+                                        shape + [nload if mode == "load_mma" else 0]))
+            body = S.seq(*calls)
+            if vm:
+                # T.gemm(valid_m=): a wave whose rows are all padding skips its reads and MFMAs
+                # (the tile's valid-row count is fixed over the K loop, so the two fragment sets
+                # stay consistent); one uniform branch around the load+MMA pair keeps them in
+                # one basic block for the interleave
+                wm = binop("//", ctx.wave_expr(), IntImm(plan["warp_n"]))
+                body = S.IfStmt(binop("<", binop("*", wm, IntImm(plan["M"] // plan["warp_m"])), vm[0]), body)
+            out.append(body)
             return S.SeqStmt(out)
         if A.scope == "shared":
             pa = self._operand_ptr(op.A)

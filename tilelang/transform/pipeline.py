@@ -572,7 +572,7 @@ def _prefetchable(op, target) -> bool:
     """A K-half GEMM whose fragments can be read one phase ahead (``tl::gemm_ss_load`` /
     ``gemm_ss_mma``): 16-bit operands, both in LDS, the 16x16x32 MFMA, nothing else fused."""
     from ..ir import dtypes as _dt
-    if not isinstance(op, O.GemmOp) or op.is_mx or op.is_sp or getattr(op, "valid_m", None) is not None:
+    if not isinstance(op, O.GemmOp) or op.is_mx or op.is_sp:
         return False
     if op.clear_accum not in (False, None, 0):
         return False
@@ -604,10 +604,10 @@ def _prefetch_schedule(self, loop, gemms, newbufs, issue, wait, idx_pre, h, kk, 
     self.key += 1
     f0, f1 = Var(f"tl_frag{self.key}_0", _dt.handle), Var(f"tl_frag{self.key}_1", _dt.handle)
 
-    def at(g, stage, mode, var):
+    def at(g, stage, mode, var, mma_var=None):
         st = BufferReplacer({B: (NB, [stage]) for B, NB in newbufs.items()}).stmt(g)
         op = copy.copy(st.op)
-        op.frag = (mode, var)
+        op.frag = (mode, var) if mma_var is None else (mode, var, mma_var)
         return S.TileOpStmt(op)
 
     g0, g1 = gemms
@@ -626,9 +626,9 @@ def _prefetch_schedule(self, loop, gemms, newbufs, issue, wait, idx_pre, h, kk, 
     s_, s1 = binop("%", kk, 2), binop("%", t1, 2)
     odd_wait = S.IfStmt(more2, L.CallStmt("tl::wait_vmcnt", [], [2 * h]), wait(more, h, 0))
     body = [wait(more, 2 * h, 0), L.CallStmt("tl::barrier_raw", []),
-            S.IfStmt(more2, issue(0, t2, s_)), at(g1, s_, "load", f1), at(g0, s_, "mma", f0),
+            S.IfStmt(more2, issue(0, t2, s_)), at(g1, s_, "load_mma", f1, f0),
             odd_wait, L.CallStmt("tl::barrier_raw", []),
-            S.IfStmt(more2, issue(1, t2, s_)), at(g0, s1, "load", f0), at(g1, s_, "mma", f1)]
+            S.IfStmt(more2, issue(1, t2, s_)), at(g0, s1, "load_mma", f0, f1)]
     new_loop = S.ForStmt(k, loop.min, loop.extent, "serial", S.SeqStmt(body), {"pipelined": 2, "phased": True})
     self.replaced = getattr(self, "replaced", {})
     for B, NB in newbufs.items():
