@@ -134,7 +134,8 @@ int main() {
         double ref = 0;
         for (int k = 0; k < K; ++k) {
           const uint8_t byte = wq[n * K / 2 + k / 2];
-          ref += (double)e2m1[(k & 1) ? byte >> 4 : byte & 15] * ldexpf(1.f, sc[n * K / 32 + k / 32] - 127) * xf[m * K + k];
+          const float w = e2m1[(k & 1) ? byte >> 4 : byte & 15] * ldexpf(1.f, sc[n * K / 32 + k / 32] - 127);
+          ref += (double)w * xf[m * K + k];
         }
         if (fabs(yf[m * N + n] - ref) > 1e-3 * fabs(ref) + 1e-3) {
           if (bad2 < 3) printf("  mode %d y[%d][%d] got %g ref %g\n", mode, m, n, yf[m * N + n], ref);
