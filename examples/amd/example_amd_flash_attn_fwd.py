@@ -1,11 +1,11 @@
 """Persistent FlashAttention forward (reference: examples/amd/example_amd_flash_attn_fwd.py).
 
 ``num_split_q`` workgroups per (batch, head) walk the query tiles with a ``T.While`` loop
-(tile = b_split, b_split + num_split_q, ...) instead of one workgroup per tile: the grid stays
-resident, and each workgroup's K/V stream (LDS-DMA ring) moves on to its next query tile without
-a relaunch.  Causal runs hand the heaviest (last) query tiles out first, so the per-workgroup work
-evens out.  The tile body is the MI355X FA kernel (examples/flash_attention/example_mha_fwd.py):
-Q in registers, P kept in registers as the PV operand, lazy rescale, fast exp2.
+instead of one workgroup per tile: the grid stays resident (one 8-wave workgroup per CU), and each
+workgroup's K/V stream (LDS-DMA ring) moves on to its next query tile without a relaunch.  Tiles
+are dealt in cost order along a snake, so causal heads are balanced exactly (see fast_flashattn).  The tile body is the staged FA kernel of examples/flash_attention/example_mha_fwd_pipelined.py
+(T.Pipelined order/stage/group: QK^T(t) next to rescale + PV(t-1)): Q in registers, P kept in
+registers as the PV operand, lazy rescale, fast exp2.
 """
 import argparse
 
@@ -17,15 +17,22 @@ FAST_MATH = {tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True}
 
 @tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
 def fast_flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=256, block_N=64, num_split_q=None,
-                   threads=512, num_stages=2, dtype="float16"):
+                   threads=512, num_stages=2, dtype="float16", mfma="16x16"):
+    """``num_split_q`` resident workgroups per (batch, head) (default: enough to put one 8-wave
+    workgroup on each of the 256 CUs).  Work assignment in cost order: query tiles are ranked
+    longest-first (causal: the last tiles see the most keys) and dealt to the workgroups of a head
+    in a snake (``s, 2S-1-s, 2S+s, ...``), so every workgroup of a causal head gets the same number
+    of KV blocks (tile pairs (i, n-1-i)) and no CU idles at the end."""
     scale = (1.0 / dim)**0.5 * 1.44269504
     head_kv = heads // groups
     q_shape = [batch, seq_len, heads, dim]
     kv_shape = [batch, seq_len, head_kv, dim]
     accum_dtype = "float"
     num_q_blocks = (seq_len + block_M - 1) // block_M
+    assert seq_len % block_N == 0, "no key-padding mask: seq_len must be a multiple of block_N"
     if num_split_q is None:  # one resident 8-wave workgroup per CU over the whole grid
         num_split_q = max(1, min(num_q_blocks, 256 // max(1, batch * heads)))
+    group = [[0], [1, 2], list(range(3, 11)), [11], [12], [13]]  # as example_mha_fwd_pipelined
 
     @T.prim_func
     def main(Q: T.Tensor(q_shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
@@ -44,41 +51,60 @@ def fast_flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_
             alpha = T.alloc_fragment([block_M], accum_dtype)
             l_i = T.alloc_fragment([block_M], accum_dtype)
             r_sum = T.alloc_fragment([block_M], accum_dtype)
+            rescale = T.alloc_var("int32")
             it = T.alloc_var("int32")
-            it = b_split
+            it = 0
             while it < num_q_blocks:
-                # causal: the longest rows (last query tiles) first
-                bx = (num_q_blocks - 1 - it) if is_causal else it
-                T.copy(Q[bz, bx * block_M:(bx + 1) * block_M, by, :], Q_r)
-                T.fill(acc_o, 0)
-                T.fill(l_i, 0)
-                T.fill(m_i, -(2.0**30))
-                loop_end = T.ceildiv((bx + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N)
-                for k in T.Pipelined(loop_end, num_stages=num_stages):
-                    T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
-                    T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
-                    for i, j in T.Parallel(block_M, block_N):
-                        ok = k * block_N + j < seq_len
+                # snake over the cost-ranked tiles: rank r = it + (s | 2S-1-s), tile = n-1-r (causal)
+                r = T.if_then_else((it // num_split_q) % 2 == 0, it + b_split, it + num_split_q - 1 - b_split)
+                bx = (num_q_blocks - 1 - r) if is_causal else r
+                if r < num_q_blocks:
+                    T.copy(Q[bz, bx * block_M:(bx + 1) * block_M, by, :], Q_r)
+                    T.fill(acc_o, 0)
+                    T.fill(l_i, 0)
+                    T.fill(m_i, -(2.0**30))
+                    rescale = 1
+                    loop_end = T.ceildiv((bx + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N)
+                    for k in T.Pipelined(loop_end, num_stages=num_stages, order=[-1, 0, 3, 1, -1, 2],
+                                         stage=[-1, 0, 0, 1, -1, 1], group=group):
+                        T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
                         if is_causal:
-                            ok = ok & (bx * block_M + i >= k * block_N + j)
-                        acc_s[i, j] = T.if_then_else(ok, 0, -T.infinity(accum_dtype))
-                    T.gemm(Q_r, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                    T.copy(m_i, m_prev)
-                    T.reduce_max(acc_s, m_i, dim=1, clear=False)
-                    for i in T.Parallel(block_M):
-                        alpha[i] = T.exp2((m_prev[i] - m_i[i]) * scale)
+                            if (k + 1) * block_N <= bx * block_M + 1:  # block fully visible: no mask
+                                T.clear(acc_s)
+                            else:
+                                for i, j in T.Parallel(block_M, block_N):
+                                    acc_s[i, j] = T.if_then_else(bx * block_M + i >= k * block_N + j, 0,
+                                                                 -T.infinity(accum_dtype))
+                        else:
+                            T.clear(acc_s)
+                        T.gemm(Q_r, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow,
+                               mfma_shape=mfma)
+                        # softmax (lazy rescale: a row keeps its max until exceeded by 2^8)
+                        T.copy(m_i, m_prev)
+                        T.reduce_max(acc_s, m_prev, dim=1, clear=False)
+                        rescale = 0
+                        for i in T.Parallel(block_M):
+                            if (m_prev[i] - m_i[i]) * scale > 8.0:
+                                alpha[i] = T.exp2((m_i[i] - m_prev[i]) * scale)
+                                m_i[i] = m_prev[i]
+                                rescale = 1
+                            else:
+                                alpha[i] = 1.0
+                        for i, j in T.Parallel(block_M, block_N):
+                            acc_s[i, j] = T.exp2(acc_s[i, j] * scale - m_i[i] * scale)
+                        T.reduce_sum(acc_s, r_sum, dim=1)
+                        for i in T.Parallel(block_M):
+                            l_i[i] = l_i[i] * alpha[i] + r_sum[i]
+                        T.copy(acc_s, acc_s_cast)
+                        # one tile behind: rescale O, then O += P V
+                        if rescale != 0:
+                            for i, j in T.Parallel(block_M, dim):
+                                acc_o[i, j] *= alpha[i]
+                        T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
+                        T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
                     for i, j in T.Parallel(block_M, dim):
-                        acc_o[i, j] *= alpha[i]
-                    for i, j in T.Parallel(block_M, block_N):
-                        acc_s[i, j] = T.exp2(acc_s[i, j] * scale - m_i[i] * scale)
-                    T.reduce_sum(acc_s, r_sum, dim=1)
-                    for i in T.Parallel(block_M):
-                        l_i[i] = l_i[i] * alpha[i] + r_sum[i]
-                    T.copy(acc_s, acc_s_cast)
-                    T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
-                for i, j in T.Parallel(block_M, dim):
-                    acc_o[i, j] /= T.max(l_i[i], 1e-30)
-                T.copy(acc_o, Output[bz, bx * block_M:(bx + 1) * block_M, by, :])
+                        acc_o[i, j] /= T.max(l_i[i], 1e-30)
+                    T.copy(acc_o, Output[bz, bx * block_M:(bx + 1) * block_M, by, :])
                 it = it + num_split_q
 
     return main

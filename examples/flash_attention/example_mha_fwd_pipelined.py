@@ -25,12 +25,14 @@ from example_mha_fwd import FAST_MATH, ref_program
 @tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
 def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=256, block_N=64,
                         threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
-                        young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd"):
+                        young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd", mfma="16x16"):
     """``young_prio``: the second-dispatched half of the waves runs at issue priority 1 (one
     ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4).
     ``seq_kv`` (default ``seq_len``): key/value length; with ``is_causal`` the mask is aligned
     bottom-right (query i sees keys up to i + seq_kv - seq_len).  ``layout``: "bshd" or "bhsd"
-    for Q/K/V/O (reference example_mha_fwd_bhsd.py)."""
+    for Q/K/V/O (reference example_mha_fwd_bhsd.py).  ``mfma``: "16x16" (16x16x32) or "32x32"
+    (32x32x16 tiles for both GEMMs: one query row per lane, P fed to P V in the accumulator's
+    k order, and 24 of each MFMA's 32 cycles free for the softmax VALU stream)."""
     scale = (1.0 / dim)**0.5 * 1.44269504
     head_kv = heads // groups
     seq_kv = seq_len if seq_kv is None else seq_kv
@@ -42,6 +44,7 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     q_shape = [batch, heads, seq_len, dim] if bhsd else [batch, seq_len, heads, dim]
     kv_shape = [batch, head_kv, seq_kv, dim] if bhsd else [batch, seq_kv, head_kv, dim]
     accum_dtype = "float"
+    n_qt = (seq_len + block_M - 1) // block_M
     n_softmax = 8 if lazy_rescale else 7  # statements of the softmax group below
     group = [[0], [1, 2], list(range(3, 3 + n_softmax))]
     group += [[3 + n_softmax], [4 + n_softmax], [5 + n_softmax]]
@@ -53,7 +56,10 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
             V: T.Tensor(kv_shape, dtype),
             Output: T.Tensor(q_shape, dtype),
     ):
-        with T.Kernel(T.ceildiv(seq_len, block_M), heads, batch, threads=threads) as (bx, by, bz):
+        # causal: heads on the fastest grid axis and the longest (last) query tiles dispatched first
+        with T.Kernel(*((heads, n_qt, batch) if is_causal else (n_qt, heads, batch)), threads=threads) as (g0, g1, bz):
+            bx = (n_qt - 1 - g1) if is_causal else g0
+            by = g0 if is_causal else g1
             if q_in_regs:
                 Q_s = T.alloc_fragment([block_M, dim], dtype)
             else:
@@ -97,12 +103,16 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                     T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
                 # 1-2: S = Q K^T
                 if is_causal:
-                    for i, j in T.Parallel(block_M, block_N):
-                        acc_s[i, j] = T.if_then_else(bx * block_M + i + past >= k * block_N + j, 0,
-                                                     -T.infinity(acc_s.dtype))
+                    # only the diagonal blocks pay for the per-element mask (uniform branch)
+                    if (k + 1) * block_N <= bx * block_M + past + 1:
+                        T.clear(acc_s)
+                    else:
+                        for i, j in T.Parallel(block_M, block_N):
+                            acc_s[i, j] = T.if_then_else(bx * block_M + i + past >= k * block_N + j, 0,
+                                                         -T.infinity(acc_s.dtype))
                 else:
                     T.clear(acc_s)
-                T.gemm(Q_s, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.gemm(Q_s, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
                 # softmax group
                 T.copy(scores_max, scores_max_prev)
                 if lazy_rescale:
@@ -134,7 +144,7 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                     T.copy(V[bz, by // groups, k * block_N:(k + 1) * block_N, :], V_shared)
                 else:
                     T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
-                T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
+                T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
             for i, j in T.Parallel(block_M, dim):
                 acc_o[i, j] /= logsum[i]
             if staged_epilogue:  # O tile through row-padded LDS: 16-byte row-contiguous stores

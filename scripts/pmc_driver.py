@@ -1,0 +1,44 @@
+"""Run one bench kernel (the headline GEMM or FA) N times for a rocprofv3 --pmc pass.
+
+    rocprofv3 --pmc <counters> -- python3 scripts/pmc_driver.py gemm|fa|fa32 [iters]
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, ".."))
+sys.path.insert(0, os.path.join(HERE, "..", "examples", "gemm"))
+sys.path.insert(0, os.path.join(HERE, "..", "examples", "flash_attention"))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    which = sys.argv[1]
+    iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    torch.manual_seed(0)
+    if which == "gemm":
+        from example_gemm import matmul
+        g = bench.GEMM_CFG
+        k = matmul(**g)
+        a = torch.randn(g["M"], g["K"], device="cuda").half()
+        b = torch.randn(g["K"], g["N"], device="cuda").half()
+        fn = lambda: k(a, b)  # noqa: E731
+    else:
+        from example_mha_fwd_pipelined import flashattn_pipelined
+        c = dict(bench.ATTN_CFG)
+        k = flashattn_pipelined(c["batch"], c["heads"], c["seq_len"], c["dim"], False, 1, c["block_M"], c["block_N"],
+                                c["threads"], c["num_stages"], mfma="32x32" if which == "fa32" else "16x16")
+        q, kk, v = (torch.randn(c["batch"], c["seq_len"], c["heads"], c["dim"], device="cuda",
+                                dtype=torch.bfloat16) for _ in range(3))
+        fn = lambda: k(q, kk, v)  # noqa: E731
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    print("done", which)
+
+
+if __name__ == "__main__":
+    main()

@@ -77,10 +77,21 @@ def test_fa_staged_hip_source():
     assert "wait_vmcnt" in src
 
 
+def test_fa_mfma32_hip_source():
+    """32x32x16 tiles: Q (natural k order) and P (the accumulator's k order) as register A operands."""
+    f = flashattn_pipelined.get_tir(1, 64, 4096, 128, False, 1, 256, 64, 512, 2, mfma="32x32")
+    src = tilelang.lower(f, target="hip", pass_configs=flashattn_pipelined.pass_configs).kernel_source
+    assert src.count("tl::gemm_rs_32<") == 4
+    assert ", 0>((&Q_s[0])" in src and ", 1>((&acc_s_cast[0])" in src
+    # one query row per lane: the row max / sum need only the lane^32 exchange
+    assert "lane_allreduce<tl::MaxOp, 32>" in src
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("mfma", ["16x16", "32x32"])
 @pytest.mark.parametrize("causal", [False, True])
-def test_fa_staged_gpu(causal):
-    k = flashattn_pipelined(2, 4, 1024, 128, causal, 2, 256, 64, 512, 2)
+def test_fa_staged_gpu(causal, mfma):
+    k = flashattn_pipelined(2, 4, 1024, 128, causal, 2, 256, 64, 512, 2, mfma=mfma)
     q = torch.randn(2, 1024, 4, 128, device="cuda", dtype=torch.bfloat16)
     kk = torch.randn(2, 1024, 2, 128, device="cuda", dtype=torch.bfloat16)
     v = torch.randn_like(kk)

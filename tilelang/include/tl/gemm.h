@@ -431,26 +431,37 @@ template <> struct mfma32_traits<bfloat16_t> {
 };
 
 // MN-contiguous operand of the 32x32x16 MFMA: lane (g = l >> 4, i = l & 15) needs column
-// c0 + 16 (g & 1) + i, rows k0 + 8 (g >> 1) + 0..7: two ds_read_b64_tr_b16 of 4 rows each
-template <typename T, int COLS, uint32_t SWZ>
+// c0 + 16 (g & 1) + i, rows k0 + 8 (g >> 1) + 0..7: two ds_read_b64_tr_b16 of 4 rows each.
+// KPERM=1 (the A operand is a 32x32 accumulator, layout.mfma._mfma_a_fragment32): rows
+// k0 + 4 (g >> 1) + 0..3 and k0 + 8 + 4 (g >> 1) + 0..3 -- still two 4-row transposed reads.
+template <typename T, int COLS, uint32_t SWZ, int KPERM = 0>
 TL_DEVICE typename mfma32_traits<T>::frag ld_tr8_32(const T* base, int k0, int c0, int lane) {
   typedef typename mfma32_traits<T>::frag F;
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int r0 = k0 + 8 * (g >> 1) + q;
+  const int r0 = KPERM ? (k0 + 4 * (g >> 1) + q) : (k0 + 8 * (g >> 1) + q);
   const int c = c0 + 16 * (g & 1) + 4 * p;
   shortx4 lo = ld_tr4<T, COLS, SWZ>(base, r0, c);
-  shortx4 hi = ld_tr4<T, COLS, SWZ>(base, r0 + 4, c);
+  shortx4 hi = ld_tr4<T, COLS, SWZ>(base, r0 + (KPERM ? 8 : 4), c);
   shortx8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(F, v);
 }
 
-template <typename T, int ROWS, int COLS, uint32_t SWZ, bool MN_CONTIG>
+template <typename T, int ROWS, int COLS, uint32_t SWZ, bool MN_CONTIG, int KPERM = 0>
 TL_DEVICE typename mfma32_traits<T>::frag ld_operand32(const T* base, int mn0, int k0, int lane) {
   if constexpr (!MN_CONTIG) {
-    return *reinterpret_cast<const typename mfma32_traits<T>::frag*>(
-        base + swz_offset<T, COLS, SWZ>(mn0 + (lane & 31), k0 + 8 * (lane >> 5)));
+    if constexpr (KPERM == 0) {
+      return *reinterpret_cast<const typename mfma32_traits<T>::frag*>(
+          base + swz_offset<T, COLS, SWZ>(mn0 + (lane & 31), k0 + 8 * (lane >> 5)));
+    } else {  // k0 + 4h + 0..3 and k0 + 8 + 4h + 0..3
+      typedef typename mfma32_traits<T>::frag F;
+      const int row = mn0 + (lane & 31), c = k0 + 4 * (lane >> 5);
+      shortx4 lo = *reinterpret_cast<const shortx4*>(base + swz_offset<T, COLS, SWZ>(row, c));
+      shortx4 hi = *reinterpret_cast<const shortx4*>(base + swz_offset<T, COLS, SWZ>(row, c + 8));
+      shortx8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      return __builtin_bit_cast(F, v);
+    }
   } else {
-    return ld_tr8_32<T, COLS, SWZ>(base, k0, mn0, lane);
+    return ld_tr8_32<T, COLS, SWZ, KPERM>(base, k0, mn0, lane);
   }
 }
 
@@ -482,6 +493,41 @@ TL_DEVICE void gemm_ss_32(const T* __restrict__ A, const T* __restrict__ B, floa
 #pragma unroll
       for (int ni = 0; ni < N_REP; ++ni)
         acc[mi * N_REP + ni] = MT::mma(b[ni], a[mi], acc[mi * N_REP + ni]);
+  }
+}
+
+// A operand in registers, 32x32x16 MFMA: a_regs holds 8 elements per (mi, kk) at
+// a_regs + (mi*KSTEPS + kk)*8 (KSTEPS = K/16).  KPERM=1 when the fragment is a 32x32
+// accumulator (FlashAttention's P): its k order is matched by the B read (ld_tr8_32<KPERM>).
+// With one query row per lane, the softmax row reductions of such a kernel are in-register
+// except one lane^32 exchange, and a 32-cycle MFMA leaves 24 of its cycles to the VALU (8 of
+// 16 for 16x16x32): the exp/max/sum stream of the softmax fits in the matrix pipe's shadow.
+template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TB, int B_COLS, uint32_t SWZ_B, int KPERM>
+TL_DEVICE void gemm_rs_32(const T* __restrict__ a_regs, const T* __restrict__ B, float* __restrict__ C,
+                          int wave_in = -1) {
+  typedef mfma32_traits<T> MT;
+  typedef typename MT::frag F;
+  constexpr int WM = M / WARP_M, WN = N / WARP_N;
+  constexpr int M_REP = WM / 32, N_REP = WN / 32, KSTEPS = K / 16;
+  static_assert(WM % 32 == 0 && WN % 32 == 0 && K % 16 == 0, "MFMA 32x32x16 tiling");
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_or(wave_in);
+  const int wn = wave % WARP_N;
+  floatx16* acc = reinterpret_cast<floatx16*>(C);
+#pragma unroll
+  for (int kk = 0; kk < KSTEPS; ++kk) {
+    F b[N_REP];
+#pragma unroll
+    for (int ni = 0; ni < N_REP; ++ni)
+      b[ni] = ld_operand32<T, (TB ? N : K), B_COLS, SWZ_B, !TB, KPERM>(B, wn * WN + ni * 32, kk * 16, lane);
+#pragma unroll
+    for (int mi = 0; mi < M_REP; ++mi) {
+      F a;
+      __builtin_memcpy(&a, a_regs + (mi * KSTEPS + kk) * 8, sizeof(F));
+#pragma unroll
+      for (int ni = 0; ni < N_REP; ++ni)
+        acc[mi * N_REP + ni] = MT::mma(b[ni], a, acc[mi * N_REP + ni]);
+    }
   }
 }
 

@@ -111,8 +111,10 @@ def mfma_a_fragment(M: int, K: int, warp_m: int, warp_n: int, kperm: int = 0, mn
     kperm=1: C-layout compatible  k = 32*kk + 16*h + 4*g + v   (local order kk, h, v)
     """
     WM = M // warp_m
+    if mn == (32, 32):
+        return _mfma_a_fragment32(M, K, warp_m, warp_n, kperm)
     if mn != (16, 16):
-        raise NotImplementedError("register A operand is implemented for 16x16x32 MFMA")
+        raise NotImplementedError(f"register A operand for MFMA {mn}")
     m_rep = WM // 16
     kk = K // 32
     thread = [Digit(0, WM, warp_m), Digit(-1, 1, warp_n)]
@@ -123,6 +125,27 @@ def mfma_a_fragment(M: int, K: int, warp_m: int, warp_n: int, kperm: int = 0, mn
         thread += [Digit(1, 4, 4), Digit(0, 1, 16)]
         local = [Digit(0, 16, m_rep), Digit(1, 16, 2 * kk), Digit(1, 1, 4)]
     return Fragment([M, K], _drop_unit(thread), _drop_unit(local), f"mfma_a_kperm{kperm}")
+
+
+def _mfma_a_fragment32(M: int, K: int, warp_m: int, warp_n: int, kperm: int) -> Fragment:
+    """Register A operand of ``v_mfma_f32_32x32x16_{f16,bf16}`` (lane: row ``l&31``, k-half ``h=l>>5``).
+
+    kperm=0: natural  k = 16*kk + 8*h + j                       (local order kk, j)
+    kperm=1: the k order of a 32x32 accumulator used as the next GEMM's A operand:
+             k = 16*kk + 8*(j>>2) + 4*h + (j&3)                  (local order kk, j>>2, j&3)
+             -- C holds n = 32*ni + 8*(v>>2) + 4*h + (v&3), so registers v = 8s..8s+7 of tile ni
+             are exactly the 8 values of k step kk = 2*ni + s (no data movement).
+    """
+    WM = M // warp_m
+    m_rep, kk = WM // 32, K // 16
+    thread = [Digit(0, WM, warp_m), Digit(-1, 1, warp_n)]
+    if kperm == 0:
+        thread += [Digit(1, 8, 2), Digit(0, 1, 32)]
+        local = [Digit(0, 32, m_rep), Digit(1, 16, kk), Digit(1, 1, 8)]
+    else:
+        thread += [Digit(1, 4, 2), Digit(0, 1, 32)]
+        local = [Digit(0, 32, m_rep), Digit(1, 16, kk), Digit(1, 8, 2), Digit(1, 1, 4)]
+    return Fragment([M, K], _drop_unit(thread), _drop_unit(local), f"mfma32_a_kperm{kperm}")
 
 
 def _drop_unit(digs: List[Digit]) -> List[Digit]:
@@ -158,9 +181,9 @@ def _read_patterns(kind: str, rows: int, cols: int, elem_bytes: int, row_base_st
             for k0 in range(0, cols, 2 * epl):
                 pats.append([(r0 + (l & 31), k0 + (l >> 5) * epl) for l in range(64)])
         return pats
-    if kind == "tr32":
+    if kind in ("tr32", "tr32_kperm"):
         # 32x32x16 MN-contiguous operand via ds_read_b64_tr_b16: lane (g, i) supplies row
-        # k0 + 8 (g >> 1) + 4 h + q, cols c0 + 16 (g & 1) + 4 p
+        # k0 + 8 (g >> 1) + 4 h + q (kperm: k0 + 4 (g >> 1) + 8 h + q), cols c0 + 16 (g & 1) + 4 p
         for c0 in range(0, min(cols, 64), 32):
             for k0 in range(0, rows, 16):
                 for h in range(2):
@@ -168,7 +191,8 @@ def _read_patterns(kind: str, rows: int, cols: int, elem_bytes: int, row_base_st
                     for l in range(64):
                         g, i = l >> 4, l & 15
                         q, pp = i >> 2, i & 3
-                        p.append((k0 + 8 * (g >> 1) + 4 * h + q, c0 + 16 * (g & 1) + 4 * pp))
+                        r = k0 + 8 * (g >> 1) + 4 * h + q if kind == "tr32" else k0 + 4 * (g >> 1) + 8 * h + q
+                        p.append((r, c0 + 16 * (g & 1) + 4 * pp))
                     pats.append(p)
         return pats
     if kind == "k_rows32mx":
@@ -215,7 +239,7 @@ def _read_patterns(kind: str, rows: int, cols: int, elem_bytes: int, row_base_st
 def _instr_for(kind: str, elem_bytes: int) -> str:
     if kind in ("k_rows32", "k_rows16", "k_rows32mx", "k_rows_32", "k_rows_i8_32"):
         return "ds_read_b128"
-    if kind == "tr32":
+    if kind in ("tr32", "tr32_kperm"):
         return "ds_read_b64_tr_b16"
     if kind == "k_rows":
         return "ds_read_b128" if elem_bytes == 2 else "ds_read_b64"

@@ -96,8 +96,12 @@ def _mfma_shape(op, target) -> str:
     return sh
 
 
-def _try_32x32(op: O.GemmOp, plan: Dict, nw: int):
-    """v_mfma_f32_32x32x16_{f16,bf16} plan (shared operands), or None when the tile does not fit."""
+def _try_32x32(op: O.GemmOp, plan: Dict, nw: int, num_threads: int = 0, a_layout: Optional[Fragment] = None):
+    """v_mfma_f32_32x32x16_{f16,bf16} plan, or None when the tile does not fit.
+
+    A in LDS (``tl::gemm_ss_32``) or in registers (``tl::gemm_rs_32``): a register A operand that
+    came from a 32x32 accumulator keeps its k order (``kperm=1``, layout.mfma._mfma_a_fragment32)
+    and the B tile is then read in that order (``tr32_kperm``)."""
     M, N, K = plan["M"], plan["N"], plan["K"]
     A, B = op.A.buffer, op.B.buffer
     if K % 16:
@@ -108,9 +112,18 @@ def _try_32x32(op: O.GemmOp, plan: Dict, nw: int):
         return None
     plan.update(warp_m=warp_m, warp_n=warp_n, mfma=(32, 32, 16))
     plan["c_layout"] = MF.mfma_c_fragment(M, N, warp_m, warp_n, (32, 32))
-    plan["a_kind"] = "tr32" if op.trans_A else "k_rows_32"
-    plan["b_kind"] = "k_rows_32" if op.trans_B else "tr32"
-    plan["a_smem_layout"] = MF.operand_swizzle(plan["a_kind"], A.static_shape(), 2)
+    if A.scope == "fragment":
+        if op.trans_A:
+            return None
+        if a_layout is not None:
+            k1 = MF.mfma_a_fragment(M, K, warp_m, warp_n, 1, (32, 32))
+            k1r = k1 if k1.num_threads == num_threads else k1.replicate(num_threads // k1.num_threads)
+            if a_layout.is_equal(k1r) or a_layout.is_equal(k1):
+                plan["a_kperm"] = 1
+    else:
+        plan["a_kind"] = "tr32" if op.trans_A else "k_rows_32"
+        plan["a_smem_layout"] = MF.operand_swizzle(plan["a_kind"], A.static_shape(), 2)
+    plan["b_kind"] = "k_rows_32" if op.trans_B else ("tr32_kperm" if plan["a_kperm"] else "tr32")
     plan["b_smem_layout"] = MF.operand_swizzle(plan["b_kind"], B.static_shape(), 2)
     return plan
 
@@ -234,8 +247,8 @@ def gemm_plan(op: O.GemmOp, num_threads: int, target=None, a_layout: Optional[Fr
     if eb not in (16, 8):
         raise ValueError(f"T.gemm on gfx950 supports f16/bf16, fp8, int8 and fp32 inputs, got {A.dtype}")
     shape = _mfma_shape(op, target)
-    if eb == 16 and shape == "32x32" and A.scope == "shared" and B.scope == "shared":
-        r = _try_32x32(op, plan, nw)
+    if eb == 16 and shape == "32x32" and A.scope in ("shared", "fragment") and B.scope == "shared":
+        r = _try_32x32(op, plan, nw, num_threads, a_layout if A.scope == "fragment" else None)
         if r is not None:
             return r
         if getattr(op, "mfma_shape", None) == "32x32":

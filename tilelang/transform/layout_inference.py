@@ -373,8 +373,9 @@ class LayoutInference:
                 changed |= self.set_frag(A, self.default_fragment(A), "cpu gemm A")
         elif _is_frag(A):
             lay_cur = self.frag.get(A)
-            k0 = MF.mfma_a_fragment(plan["M"], plan["K"], plan["warp_m"], plan["warp_n"], 0)
-            k1 = MF.mfma_a_fragment(plan["M"], plan["K"], plan["warp_m"], plan["warp_n"], 1)
+            mn = tuple(plan["mfma"][:2]) if plan["mfma"][:2] == (32, 32) else (16, 16)
+            k0 = MF.mfma_a_fragment(plan["M"], plan["K"], plan["warp_m"], plan["warp_n"], 0, mn)
+            k1 = MF.mfma_a_fragment(plan["M"], plan["K"], plan["warp_m"], plan["warp_n"], 1, mn)
             if lay_cur is not None:
                 if lay_cur.is_equal(k1) or _equal_rep(lay_cur, k1, self.T):
                     plan["a_kperm"] = 1

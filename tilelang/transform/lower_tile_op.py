@@ -1013,6 +1013,14 @@ class TileOpLowerer(Mutator):
         if vm and (plan.get("int8") or plan.get("f32") or A.dtype.bits == 8 or A.scope != "shared"):
             raise LoweringError("T.gemm(valid_m=) is supported for f16/bf16 GEMMs with both operands in shared "
                                 "memory")
+        if plan.get("mfma") == (32, 32, 16) and A.scope == "fragment":
+            if vm:
+                raise LoweringError("T.gemm(valid_m=) needs both operands in shared memory")
+            out.append(L.CallStmt("tl::gemm_rs_32", [L.BufferPtr(ctx.local_of(A), 0), pb, L.BufferPtr(cl, 0),
+                                                     ctx.wave_expr()], [
+                ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_B),
+                B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u", plan.get("a_kperm", 0)]))
+            return S.SeqStmt(out)
         if plan.get("mfma") == (32, 32, 16):
             pa = self._operand_ptr(op.A)
             out.append(L.CallStmt("tl::gemm_ss_32", [pa, pb, L.BufferPtr(cl, 0)] + (vm or [IntImm(0x3fffffff)]) +
