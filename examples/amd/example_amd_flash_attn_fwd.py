@@ -57,7 +57,8 @@ def fast_flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_
             while it < num_q_blocks:
                 # snake over the cost-ranked tiles: rank r = it + (s | 2S-1-s), tile = n-1-r (causal)
                 r = T.if_then_else((it // num_split_q) % 2 == 0, it + b_split, it + num_split_q - 1 - b_split)
-                bx = (num_q_blocks - 1 - r) if is_causal else r
+                # clamped so the bounds prover sees the K/V tiles in range (LDS-DMA, not register staging)
+                bx = T.max(T.min((num_q_blocks - 1 - r) if is_causal else r, num_q_blocks - 1), 0)
                 if r < num_q_blocks:
                     T.copy(Q[bz, bx * block_M:(bx + 1) * block_M, by, :], Q_r)
                     T.fill(acc_o, 0)

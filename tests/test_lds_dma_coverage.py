@@ -8,7 +8,7 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for d in ("gemm", "flash_attention", "flash_decoding", "deepseek_mla", "blocksparse_attention"):
+for d in ("gemm", "flash_attention", "flash_decoding", "deepseek_mla", "blocksparse_attention", "amd"):
     sys.path.insert(0, os.path.join(ROOT, "examples", d))
 
 import tilelang  # noqa: E402
@@ -23,7 +23,8 @@ def _hip(jf, *a, **kw):
     return tilelang.compile(f, out_idx=jf.out_idx, target="hip", pass_configs=jf.pass_configs).get_kernel_source()
 
 
-@pytest.mark.parametrize("name", ["gemm", "fa", "gqa_paged", "mla_paged", "sparse_gqa_paged"])
+@pytest.mark.parametrize("name", ["gemm", "fa", "fa_causal", "fa_persistent", "gqa_paged", "mla_paged",
+                                  "sparse_gqa_paged"])
 def test_examples_use_lds_dma(name):
     if name == "gemm":
         from example_gemm import matmul
@@ -31,6 +32,12 @@ def test_examples_use_lds_dma(name):
     elif name == "fa":
         from example_mha_fwd_pipelined import flashattn_pipelined as fa
         src = _hip(fa, 1, 64, 4096, 128, False, 1, 256, 64, 512, 2, "bfloat16", True, True)
+    elif name == "fa_causal":
+        from example_mha_fwd_pipelined import flashattn_pipelined as fa
+        src = _hip(fa, 1, 64, 4096, 128, True, 1, 256, 64, 512, 2, "bfloat16", True, True, mfma="32x32")
+    elif name == "fa_persistent":  # the tile index comes from a while loop: clamped for the prover
+        from example_amd_flash_attn_fwd import fast_flashattn
+        src = _hip(fast_flashattn, 1, 64, 4096, 128, True, 1)
     elif name == "gqa_paged":
         import example_gqa_decode as d
         src = _hip(d.gqa_decode_paged, 4, 32, 8, 64, 64, 32, 128)

@@ -155,3 +155,52 @@ def test_precision_probe_gpu():
         assert rows["TileLang (precise)"]["nonfinite"] == 0
     assert res["exp"]["TileLang (fast math)"]["max_rel"] < 1e-5
     assert res["exp2"]["TileLang (fast math)"]["max_rel"] < 1e-5
+
+
+def test_carver_bestfit_packing():
+    from tilelang.carver.roller.bestfit import BestFit, pack, gemm_lds_bytes
+    a = BestFit(16)
+    x, y = a.malloc(100), a.malloc(50)
+    assert (x.start, y.start) == (0, 112)
+    a.free(x)
+    z = a.malloc(40)  # best fit reuses the freed hole
+    assert z.start == 0 and a.limit == 112 + 64
+    # disjoint lifetimes share bytes; overlapping ones do not
+    size, off = pack([("ring", 1024, 0, 2), ("epi", 512, 2, 3)])
+    assert size == 1024 and off["epi"] == 0
+    size, _ = pack([("a", 1024, 0, 2), ("b", 512, 1, 3)])
+    assert size == 1536
+    # the staged GEMM epilogue (256 x 264 fp16) reuses the 2-stage 256x256x64 ring: max, not sum
+    assert gemm_lds_bytes(256, 256, 64, 2, 2) == 131072
+    assert gemm_lds_bytes(256, 256, 64, 2, 2, staged_epilogue=True) == 256 * 264 * 2
+
+
+def test_carver_conv_and_reduction_hints_drive_kernels():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "examples", "convolution"))
+    sys.path.insert(0, os.path.join(root, "examples", "norm"))
+    from tilelang.carver.template import ConvTemplate, GeneralReductionTemplate
+    from example_convolution import convolution
+    from rms_norm import rms_norm, ref_program as rms_ref
+    arch = CDNA()
+    # implicit-GEMM conv: N*OH*OW x F x KH*KW*C
+    hints = ConvTemplate(N=2, C=64, H=16, W=16, F=64, K=3, S=1, D=1, P=1).with_arch(arch).recommend_hints(4)
+    assert hints
+    c = hints[0].to_config()
+    f = convolution.get_tir(2, 64, 16, 16, 64, 3, 1, 1, 1, c["block_M"], c["block_N"], c["block_K"],
+                            c["num_stages"], c["threads"])
+    k = tilelang.compile(f, out_idx=[-1], target="cpu")
+    x = torch.randn(2, 16, 16, 64).half()
+    w = torch.randn(3, 3, 64, 64).half()
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(3, 2, 0, 1).float(), padding=1)
+    torch.testing.assert_close(k(x, w).float(), ref.permute(0, 2, 3, 1), rtol=2e-2, atol=5e-1)
+    # row reduction (RMS norm): whole rows in registers, blk_m rows per block
+    r = GeneralReductionTemplate(shape=[8192, 8192], dtype="float32").with_arch(arch).recommend_hints(4)
+    assert r and all(h.score["per_lane"] <= 64 for h in r)
+    small = GeneralReductionTemplate(shape=[64, 256], dtype="float32").with_arch(arch).recommend_hints(1)[0]
+    cfg = small.to_config()
+    assert set(cfg) == {"blk_m", "threads"}
+    kr = tilelang.compile(rms_norm.get_tir(64, 256, cfg["blk_m"], cfg["threads"]), out_idx=[-1], target="cpu")
+    a = torch.randn(64, 256)
+    torch.testing.assert_close(kr(a), rms_ref(a), rtol=1e-4, atol=1e-4)

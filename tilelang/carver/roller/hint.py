@@ -26,7 +26,8 @@ class Hint:
 
     def to_config(self) -> Dict[str, int]:
         """The keyword arguments the examples' kernel factories take."""
-        if len(self.block) == 1 and self.extra:  # 1-D families (GEMV) name their own tile keys
+        if (len(self.block) == 1 or "blk_m" in self.extra) and self.extra:
+            # families that name their own tile keys (GEMV: block_N/block_K, row reductions: blk_m)
             return dict(self.extra, threads=self.threads)
         cfg = {"block_M": self.block[0], "threads": self.threads, "num_stages": self.pipeline_stage}
         if len(self.block) > 1:

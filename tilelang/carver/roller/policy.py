@@ -18,6 +18,7 @@ import itertools
 import math
 from typing import List, Optional, Sequence
 
+from .bestfit import gemm_lds_bytes
 from .hint import Hint
 from .rasterization import NoRasterization, Rasterization2DRow
 
@@ -36,7 +37,7 @@ def gemm_cost(arch, M, N, K, bm, bn, bk, threads, stages, in_dtype="float16", wa
         return None
     if bk * eb < 32 or (bk * eb) % 64 and eb == 1:
         return None
-    lds = stages * (bm + bn) * bk * eb
+    lds = gemm_lds_bytes(bm, bn, bk, stages, eb)  # best-fit arena (roller/bestfit.py)
     if lds > arch.smem_cap:
         return None
     acc_regs = bm * bn // threads  # fp32 accumulators per lane

@@ -93,13 +93,38 @@ class ElementwiseTemplate(BaseTemplate):
 
 @dataclass
 class GeneralReductionTemplate(BaseTemplate):
+    """Row reductions (``structure="SR"``: spatial rows x reduced columns) with whole rows held in
+    registers -- the shape of RMS norm / softmax / row sums (``examples/norm/rms_norm.py``:
+    ``to_config()`` gives its ``blk_m`` and ``threads``).  Model: one HBM read + one write of the
+    rows at the HBM rate, derated when the grid under-fills the 256 CUs (fewer than ~4 blocks per
+    CU) and when a lane carries long serial chains; tiles whose rows do not fit the register
+    budget (64 fp32 per lane) are rejected."""
     structure: str = "SR"  # spatial x reduce
     shape: List[int] = field(default_factory=lambda: [1024, 1024])
     dtype: str = "float16"
 
     def _hints(self, topk):
-        hs = DefaultPolicy(self.arch, self.shape, self.dtype, reduce_len=1).emit_config(topk * 4)
-        return [h for h in hs if h.block[-1] >= min(self.shape[-1], 256)][:topk] or hs[:topk]
+        import math
+        from .roller.policy import _eb
+        rows, cols = self.shape[0], self.shape[-1]
+        eb = _eb(self.dtype)
+        hints = []
+        for th in (128, 256, 512):
+            for bm in (1, 2, 4, 8, 16, 32):
+                if bm > rows or th % bm:
+                    continue
+                per_lane = bm * cols / th
+                if per_lane > 64 or per_lane < 1 or (th // bm) * max(1, 16 // eb) > cols * 4:
+                    continue
+                blocks = math.ceil(rows / bm)
+                cover = blocks / (self.arch.compute_max_core * 4)
+                t = 2 * rows * cols * eb / (self.arch.bandwidth[0] * 1e9) * 1e6
+                t /= min(1.0, 0.3 + 0.7 * min(1.0, cover)) * (1.0 if per_lane <= 32 else 0.85)
+                hints.append(Hint(block=[bm, cols], warp=[bm, cols], rstep=[cols], pipeline_stage=1, threads=th,
+                                  estimated_us=t, score=dict(blocks=blocks, per_lane=per_lane),
+                                  extra={"blk_m": bm}))
+        hints.sort(key=lambda h: (h.estimated_us, -h.threads))
+        return hints[:topk]
 
     def reference(self, x):
         return x.sum(-1)
