@@ -11,13 +11,13 @@ Kernels (MI355X):
   nsa_fwd_lse     the forward, also writing L [B, SQ, HQ] (fp32)
   nsa_bwd_prep    delta
   nsa_block_mask  Mask[b, h, j, t] = 1 when token t selected key block j (inverse of BlockIndices)
+  token_lists     the same inverse as compacted, padded token lists per (batch, kv head, block)
   nsa_bwd_dq      one workgroup per (token, kv head) walks its selected blocks (like the forward):
                   dQ is produced whole, no atomics
   nsa_bwd_dkv     one workgroup per (key block, kv head, batch) keeps K_j, V_j and the dK/dV
-                  accumulators resident and walks the tokens that can see the block in tiles of
-                  ``32 / G`` tokens (G * tokens = 32 MFMA rows, so dV += P^T dO and
-                  dK += dS^T Q are 32-deep bf16 MFMAs); tiles nobody in which selected j are skipped,
-                  rows of tokens that did not select it are zeroed.  dK/dV are produced whole.
+                  accumulators resident and walks ONLY the tokens that selected the block (its
+                  token list), ``64 / G`` tokens per tile (G * tokens = 64 MFMA rows): Q / dO rows
+                  arrive by LDS-DMA row gathers in a pipelined loop.  dK/dV are produced whole.
 """
 import argparse
 
@@ -102,23 +102,24 @@ def nsa_fwd_lse(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=No
 
 
 @tilelang.jit(out_idx=[2])
-def nsa_bwd_prep(batch, seq_len, heads, dim, dtype="bfloat16", block_T=32):
+def nsa_bwd_prep(batch, seq_len, heads, dim, dtype="bfloat16", block_R=64, threads=256):
+    """Delta = rowsum(O * dO) over the B*SQ*HQ rows of the flattened [rows, dim] views (one HBM
+    pass; ``block_R`` rows per workgroup keep the fp32 products at 32 registers per lane)."""
+    rows = batch * seq_len * heads
 
     @T.prim_func
-    def main(O: T.Tensor([batch, seq_len, heads, dim], dtype), dO: T.Tensor([batch, seq_len, heads, dim], dtype),
-             Delta: T.Tensor([batch, seq_len, heads], "float32")):
-        with T.Kernel(T.ceildiv(seq_len, block_T), batch, threads=256) as (bx, b):
-            acc = T.alloc_fragment([block_T * heads, dim], "float32")
-            dsum = T.alloc_fragment([block_T * heads], "float32")
-            for r, d in T.Parallel(block_T * heads, dim):
-                t = bx * block_T + r // heads
-                acc[r, d] = T.if_then_else(t < seq_len, T.cast(O[b, t, r % heads, d], "float32") *
-                                           T.cast(dO[b, t, r % heads, d], "float32"), 0.0)
+    def main(O: T.Tensor([rows, dim], dtype), dO: T.Tensor([rows, dim], dtype), Delta: T.Tensor([rows], "float32")):
+        with T.Kernel(T.ceildiv(rows, block_R), threads=threads) as bx:
+            o = T.alloc_fragment([block_R, dim], dtype)
+            do = T.alloc_fragment([block_R, dim], dtype)
+            acc = T.alloc_fragment([block_R, dim], "float32")
+            dsum = T.alloc_fragment([block_R], "float32")
+            T.copy(O[bx * block_R:(bx + 1) * block_R, :], o)
+            T.copy(dO[bx * block_R:(bx + 1) * block_R, :], do)
+            for r, d in T.Parallel(block_R, dim):
+                acc[r, d] = T.cast(o[r, d], "float32") * T.cast(do[r, d], "float32")
             T.reduce_sum(acc, dsum, dim=1)
-            for r in T.Parallel(block_T * heads):
-                t = bx * block_T + r // heads
-                if t < seq_len:
-                    Delta[b, t, r % heads] = dsum[r]
+            T.copy(dsum, Delta[bx * block_R:(bx + 1) * block_R])
 
     return main
 
@@ -204,23 +205,32 @@ def nsa_bwd_dq(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=Non
 
 
 @tilelang.jit(out_idx=[-2, -1], pass_configs=FAST_MATH)
-def nsa_bwd_dkv(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=None, block_size=64, groups=16,
-                threads=256, dtype="bfloat16"):
+def nsa_bwd_dkv(batch, heads, seq_len, seq_len_kv, dim, n_pairs, is_causal=True, scale=None, block_size=64,
+                groups=16, tokens_per_tile=4, threads=256, num_stages=2, dtype="bfloat16"):
+    """dK/dV over the compacted (block -> selecting tokens) lists built by ``token_lists``.
+
+    One workgroup per (key block j, kv head, batch) keeps K_j / V_j and the dK / dV accumulators
+    resident and walks ONLY the tokens that selected j, ``tokens_per_tile`` at a time
+    (R = tokens * G query-head rows): the Q / dO rows are gathered by LDS-DMA (``T.gather_rows``
+    over the flattened [B*SQ*HQ, D] views, row ids from the list; pad entries are -1 -> zero
+    rows) and the per-row LSE / Delta come pre-gathered, so every K step is a pipelined
+    producer and no tile is spent on tokens that did not select the block."""
     sm = (1.0 / dim)**0.5 if scale is None else scale
     scale = sm * LOG2E
     head_kv = heads // groups
-    G, BS, D = groups, block_size, dim
-    TT = max(1, 32 // G)          # tokens per tile
-    R = TT * G                    # MFMA rows per tile
+    G, BS, D, TT = groups, block_size, dim, tokens_per_tile
+    R = TT * G
     NB = seq_len_kv // BS
     past = seq_len_kv - seq_len
+    rows = batch * seq_len * heads
     accum_dtype = "float"
 
     @T.prim_func
-    def main(Q: T.Tensor([batch, seq_len, heads, D], dtype), K: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
-             V: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
-             Mask: T.Tensor([batch, head_kv, NB, seq_len], "int8"), dO: T.Tensor([batch, seq_len, heads, D], dtype),
-             LSE: T.Tensor([batch, seq_len, heads], "float32"), Delta: T.Tensor([batch, seq_len, heads], "float32"),
+    def main(Q: T.Tensor([rows, D], dtype), K: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
+             V: T.Tensor([batch, seq_len_kv, head_kv, D], dtype), dO: T.Tensor([rows, D], dtype),
+             RowIdx: T.Tensor([n_pairs * G], "int32"), TokP: T.Tensor([n_pairs], "int32"),
+             LseP: T.Tensor([n_pairs * G], "float32"), DeltaP: T.Tensor([n_pairs * G], "float32"),
+             Off: T.Tensor([batch * head_kv * NB + 1], "int32"),
              dK: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
              dV: T.Tensor([batch, seq_len_kv, head_kv, D], dtype)):
         with T.Kernel(NB, batch * head_kv, threads=threads) as (j, bz):
@@ -234,7 +244,7 @@ def nsa_bwd_dkv(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=No
             ds_s = T.alloc_shared([R, BS], dtype)
             lse_s = T.alloc_shared([R], "float32")
             dl_s = T.alloc_shared([R], "float32")
-            sel_s = T.alloc_shared([TT], "int32")
+            tok_s = T.alloc_shared([TT], "int32")
             s = T.alloc_fragment([R, BS], accum_dtype)
             dp = T.alloc_fragment([R, BS], accum_dtype)
             dk = T.alloc_fragment([BS, D], accum_dtype)
@@ -243,39 +253,76 @@ def nsa_bwd_dkv(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=No
             T.copy(V[b, j * BS:(j + 1) * BS, h, :], v_s)
             T.clear(dk)
             T.clear(dv)
-            # tokens that can see block j: position >= j * BS
-            t0 = T.max(j * BS - past, 0) // TT
-            for ti in T.serial(T.ceildiv(seq_len, TT) - t0):
-                tb = (t0 + ti) * TT
-                for u in T.Parallel(TT):
-                    sel_s[u] = T.if_then_else(tb + u < seq_len, T.cast(Mask[b, h, j, T.min(tb + u, seq_len - 1)],
-                                                                        "int32"), 0)
-                if T.any_of(sel_s):
-                    for r, d in T.Parallel(R, D):
-                        t = T.min(tb + r // G, seq_len - 1)
-                        q_s[r, d] = Q[b, t, h * G + r % G, d]
-                        do_s[r, d] = dO[b, t, h * G + r % G, d]
-                    for r in T.Parallel(R):
-                        t = T.min(tb + r // G, seq_len - 1)
-                        lse_s[r] = LSE[b, t, h * G + r % G]
-                        dl_s[r] = Delta[b, t, h * G + r % G]
-                    T.clear(s)
-                    T.gemm(q_s, k_s, s, transpose_B=True)
-                    T.clear(dp)
-                    T.gemm(do_s, v_s, dp, transpose_B=True)
-                    for r, c in T.Parallel(R, BS):
-                        ok = sel_s[r // G] != 0
-                        if is_causal:
-                            ok = ok & (j * BS + c <= tb + r // G + past)
-                        p = T.if_then_else(ok, T.exp2(s[r, c] * scale - lse_s[r]), 0.0)
-                        p_s[r, c] = p
-                        ds_s[r, c] = p * (dp[r, c] - dl_s[r]) * sm
-                    T.gemm(p_s, do_s, dv, transpose_A=True)
-                    T.gemm(ds_s, q_s, dk, transpose_A=True)
+            p0 = Off[bz * NB + j]
+            n_t = (Off[bz * NB + j + 1] - p0) // TT
+            for it in T.Pipelined(n_t, num_stages=num_stages):
+                base = p0 + it * TT
+                T.gather_rows(Q[:, :], RowIdx[base * G:base * G + R], q_s, row_dim=0)
+                T.gather_rows(dO[:, :], RowIdx[base * G:base * G + R], do_s, row_dim=0)
+                T.copy(LseP[base * G:base * G + R], lse_s)
+                T.copy(DeltaP[base * G:base * G + R], dl_s)
+                T.copy(TokP[base:base + TT], tok_s)
+                T.clear(s)
+                T.gemm(q_s, k_s, s, transpose_B=True)
+                T.clear(dp)
+                T.gemm(do_s, v_s, dp, transpose_B=True)
+                for r, c in T.Parallel(R, BS):
+                    ok = tok_s[r // G] >= 0
+                    if is_causal:
+                        ok = ok & (j * BS + c <= tok_s[r // G] + past)
+                    p = T.if_then_else(ok, T.exp2(s[r, c] * scale - lse_s[r]), 0.0)
+                    p_s[r, c] = p
+                    ds_s[r, c] = p * (dp[r, c] - dl_s[r]) * sm
+                T.gemm(p_s, do_s, dv, transpose_A=True)
+                T.gemm(ds_s, q_s, dk, transpose_A=True)
             T.copy(dk, dK[b, j * BS:(j + 1) * BS, h, :])
             T.copy(dv, dV[b, j * BS:(j + 1) * BS, h, :])
 
     return main
+
+
+def token_lists(block_indices, lse, delta, num_blocks, heads, tokens_per_tile=4):
+    """Invert BlockIndices [B, SQ, H, S] into per-(batch, kv head, block) lists of the tokens that
+    selected the block (on the device, torch sort + scatters), each list padded to a multiple of
+    ``tokens_per_tile`` with -1 entries.  Returns (RowIdx, TokP, LseP, DeltaP, Off, n_pairs): the
+    flattened Q row of every (pair, query head in the group), the token of every pair, the LSE /
+    Delta of every row, and the list offsets."""
+    import torch
+    B, SQ, H, S = block_indices.shape
+    G = heads // H
+    TT = tokens_per_tile
+    dev = block_indices.device
+    blk = block_indices.long()
+    bb = torch.arange(B, device=dev).view(B, 1, 1, 1).expand_as(blk)
+    tt = torch.arange(SQ, device=dev).view(1, SQ, 1, 1).expand_as(blk)
+    hh = torch.arange(H, device=dev).view(1, 1, H, 1).expand_as(blk)
+    ok = (blk >= 0) & (blk < num_blocks)
+    key = ((bb * H + hh) * num_blocks + blk)[ok]
+    tok = tt[ok]
+    order = torch.argsort(key * SQ + tok)
+    key, tok = key[order], tok[order]
+    nl = B * H * num_blocks
+    cnt = torch.bincount(key, minlength=nl)
+    padded = (cnt + TT - 1) // TT * TT
+    off = torch.zeros(nl + 1, dtype=torch.long, device=dev)
+    off[1:] = torch.cumsum(padded, 0)
+    start = torch.zeros(nl, dtype=torch.long, device=dev)
+    start[1:] = torch.cumsum(cnt, 0)[:-1]
+    n_pairs = max(int(off[-1].item()), TT)  # one host sync: the buffer sizes
+    dest = off[key] + (torch.arange(key.numel(), device=dev) - start[key])
+    tokp = torch.full((n_pairs, ), -1, dtype=torch.int32, device=dev)
+    tokp[dest] = tok.int()
+    b_of = key // (H * num_blocks)
+    h_of = (key // num_blocks) % H
+    g = torch.arange(G, device=dev)
+    rows = ((b_of * SQ + tok) * (H * G) + h_of * G).view(-1, 1) + g.view(1, -1)  # [pairs, G]
+    rowidx = torch.full((n_pairs, G), -1, dtype=torch.int32, device=dev)
+    rowidx[dest] = rows.int()
+    lsep = torch.zeros((n_pairs, G), dtype=torch.float32, device=dev)
+    dlp = torch.zeros((n_pairs, G), dtype=torch.float32, device=dev)
+    lsep[dest] = lse.reshape(-1)[rows]
+    dlp[dest] = delta.reshape(-1)[rows]
+    return rowidx.view(-1), tokp, lsep.view(-1), dlp.view(-1), off.int(), n_pairs
 
 
 def nsa_backward(q, k, v, block_indices, o, lse, do, block_size=64, is_causal=True):
@@ -284,12 +331,13 @@ def nsa_backward(q, k, v, block_indices, o, lse, do, block_size=64, is_causal=Tr
     SKV, H = k.shape[1], k.shape[2]
     S = block_indices.shape[-1]
     G = HQ // H
-    delta = nsa_bwd_prep(B, SQ, HQ, D, _dt(q))(o, do)
+    delta = nsa_bwd_prep(B, SQ, HQ, D, _dt(q))(o.reshape(-1, D), do.reshape(-1, D)).view(B, SQ, HQ)
     dq = nsa_bwd_dq(B, HQ, SQ, SKV, D, is_causal, None, block_size, G, S, dtype=_dt(q))(q, k, v, block_indices, do,
                                                                                          lse, delta)
-    mask = nsa_block_mask(B, SQ, H, S, SKV // block_size)(block_indices)
-    dk, dv = nsa_bwd_dkv(B, HQ, SQ, SKV, D, is_causal, None, block_size, G, dtype=_dt(q))(q, k, v, mask, do, lse,
-                                                                                          delta)
+    TT = max(1, 64 // G)
+    rowidx, tokp, lsep, dlp, off, n_pairs = token_lists(block_indices, lse, delta, SKV // block_size, HQ, TT)
+    dk, dv = nsa_bwd_dkv(B, HQ, SQ, SKV, D, n_pairs, is_causal, None, block_size, G, TT, dtype=_dt(q))(
+        q.reshape(-1, D), k, v, do.reshape(-1, D), rowidx, tokp, lsep, dlp, off)
     return dq, dk, dv
 
 

@@ -337,11 +337,21 @@ def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N
 
 
 BWD_DQ_MODE = "separate"  # or "atomic" (single kernel, fp32 atomics into dQ)
+BWD_OVERLAP = True  # dQ kernel on a side stream, concurrent with the dK/dV kernel
 
 
-def _tiles(D, Dv, kind):
+def _tiles(D, Dv, kind, causal=False):
     """Tile sizes that keep each kernel's LDS (operand tiles + 2-stage rings) under 160 KiB: the
-    defaults are sized for D = Dv <= 128; wider heads (e.g. D=192 / Dv=128) halve the streamed tile."""
+    defaults are sized for D = Dv <= 128; wider heads (e.g. D=192 / Dv=128) halve the streamed tile.
+    d64 heads use the winners of scripts/sweep_fa_bwd.py (b8 h32 s1024, profiles/r3/s3/bwd/):
+    non-causal dK/dV 256x64 over 8 waves (209 -> 182 us), dQ 128x64 over 8 waves (150 -> 130 us);
+    causal 64x32 / 64x64 over 4 waves (more, shorter workgroups balance the triangle)."""
+    if D + Dv <= 128:
+        if causal:
+            return {"fwd": {}, "bwd": dict(block_M=64, block_N=32, threads=256),
+                    "dq": dict(block_M=64, block_N=64, threads=256)}[kind]
+        return {"fwd": {}, "bwd": dict(block_M=256, block_N=64, threads=512),
+                "dq": dict(block_M=128, block_N=64, threads=512)}[kind]
     if D + Dv <= 256:
         return {}
     return {"fwd": dict(block_M=128), "bwd": dict(block_N=32), "dq": dict(block_N=32)}[kind]
@@ -390,16 +400,26 @@ class _attention:
                     delta = flashattn_bwd_preprocess(B, H, S, Dv, dtype=dt)(o, do)
                     dk = torch.empty_like(k)
                     dv = torch.empty_like(v)
-                    bw = _tiles(D, Dv, "bwd")
+                    bw = _tiles(D, Dv, "bwd", ctx.causal)
                     split = _kv_split(B, S, k.shape[2], G, bw.get("block_M", 128))
                     if BWD_DQ_MODE == "atomic":
                         dq = torch.zeros(B, S, H, D, dtype=torch.float32, device=q.device)
                         bwd = flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv,
-                                            **_tiles(D, Dv, "bwd"))
+                                            **_tiles(D, Dv, "bwd", ctx.causal))
                         bwd(q, k, v, do, lse, delta, dq, dk, dv)
                         return flashattn_bwd_postprocess(B, H, S, D, dtype=dt)(dq), dk, dv, None
-                    # dK/dV kernel without dQ + an atomic-free dQ kernel (the two could run on
-                    # separate streams; they only share read-only inputs)
+                    # dK/dV kernel without dQ + an atomic-free dQ kernel; they only share read-only
+                    # inputs, so with BWD_OVERLAP the dQ kernel runs on a side stream and fills the
+                    # CUs the dK/dV grid's tail leaves idle
+                    bdq = flashattn_bwd_dq(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv,
+                                           **_tiles(D, Dv, "dq", ctx.causal))
+                    side = None
+                    if BWD_OVERLAP and q.is_cuda:
+                        main_s = torch.cuda.current_stream()
+                        side = torch.cuda.Stream()
+                        side.wait_stream(main_s)
+                        with torch.cuda.stream(side):
+                            dq = bdq(q, k, v, do, lse, delta)
                     if split > 1:
                         dkp = torch.empty((split, ) + tuple(k.shape), dtype=torch.float32, device=k.device)
                         dvp = torch.empty((split, ) + tuple(v.shape), dtype=torch.float32, device=v.device)
@@ -409,9 +429,11 @@ class _attention:
                     else:
                         flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, dq_mode="none", groups=G, dim_v=Dv,
                                       **bw)(q, k, v, do, lse, delta, dk, dv)
-                    bdq = flashattn_bwd_dq(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv,
-                                           **_tiles(D, Dv, "dq"))
-                    dq = bdq(q, k, v, do, lse, delta)
+                    if side is None:
+                        dq = bdq(q, k, v, do, lse, delta)
+                    else:
+                        main_s.wait_stream(side)
+                        dq.record_stream(main_s)
                     return dq, dk, dv, None
 
             cls.fn = Attn

@@ -156,21 +156,31 @@ def varlen_bwd_dkv(batch, heads, total_q, total_k, max_seqlen_k, dim, is_causal=
                 loop_st = T.max(by * block_M - off, 0) // block_N if is_causal else 0
                 n_q = T.max(T.ceildiv(q_len, block_N) - loop_st, 0)
                 for it in T.Pipelined(n_q * groups, num_stages=num_stages):
-                    hq = bx * groups + it // n_q
+                    # head clamped into range so the bounds prover keeps the Q / dO tiles LDS-DMA (the
+                    # row offset may run past the sequence: buffer-resource DMA zero-fills past the tensor)
+                    hq = T.max(T.min(bx * groups + it // n_q, heads - 1), 0)
                     kq = loop_st + it % n_q
                     T.copy(Q[q0 + kq * block_N:q0 + (kq + 1) * block_N, hq, :], q)
                     T.copy(dO[q0 + kq * block_N:q0 + (kq + 1) * block_N, hq, :], do)
-                    for j in T.Parallel(block_N):
-                        r = T.min(q0 + kq * block_N + j, total_q - 1)
-                        lse_s[j] = LSE[hq, r]
-                        delta_s[j] = Delta[hq, r]
+                    # pipelined copies (issued a stage ahead; rows past total_q are guarded to 0 and
+                    # masked below) instead of synchronous per-iteration loads
+                    T.copy(LSE[hq, q0 + kq * block_N:q0 + (kq + 1) * block_N], lse_s)
+                    T.copy(Delta[hq, q0 + kq * block_N:q0 + (kq + 1) * block_N], delta_s)
                     T.clear(qkT)
                     T.gemm(K_s, q, qkT, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                    for i, j in T.Parallel(block_M, block_N):
-                        ok = (kq * block_N + j < q_len) & (by * block_M + i < k_len)
-                        if is_causal:
-                            ok = ok & (kq * block_N + j + off >= by * block_M + i)
-                        qkT[i, j] = T.if_then_else(ok, T.exp2(qkT[i, j] * scale - lse_s[j]), 0.0)
+                    # interior tiles (every query valid and, causal, past the diagonal) skip the mask
+                    inner = ((kq + 1) * block_N <= q_len) & ((by + 1) * block_M <= k_len)
+                    if is_causal:
+                        inner = inner & (kq * block_N + off >= (by + 1) * block_M - 1)
+                    if inner:
+                        for i, j in T.Parallel(block_M, block_N):
+                            qkT[i, j] = T.exp2(qkT[i, j] * scale - lse_s[j])
+                    else:
+                        for i, j in T.Parallel(block_M, block_N):
+                            ok = (kq * block_N + j < q_len) & (by * block_M + i < k_len)
+                            if is_causal:
+                                ok = ok & (kq * block_N + j + off >= by * block_M + i)
+                            qkT[i, j] = T.if_then_else(ok, T.exp2(qkT[i, j] * scale - lse_s[j]), 0.0)
                     T.clear(dsT)
                     T.gemm(V_s, do, dsT, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                     T.copy(qkT, qkT_cast)
@@ -200,7 +210,9 @@ def varlen_bwd_dq(batch, heads, total_q, total_k, max_seqlen_q, dim, is_causal=T
              LSE: T.Tensor([heads, total_q], "float32"), Delta: T.Tensor([heads, total_q], "float32"),
              cu_q: T.Tensor([batch + 1], "int32"), cu_k: T.Tensor([batch + 1], "int32"),
              dQ: T.Tensor([total_q, heads, dim], dtype)):
-        with T.Kernel(T.ceildiv(max_seqlen_q, block_M), heads, batch, threads=threads) as (bx, by, bz):
+        n_qt = (max_seqlen_q + block_M - 1) // block_M
+        with T.Kernel(heads, n_qt, batch, threads=threads) as (by, bx_raw, bz):
+            bx = (n_qt - 1 - bx_raw) if is_causal else bx_raw  # causal: longest dQ rows first
             q = T.alloc_shared([block_M, dim], dtype)
             do = T.alloc_shared([block_M, dim], dtype)
             K_s = T.alloc_shared([block_N, dim], dtype)
@@ -233,12 +245,19 @@ def varlen_bwd_dq(batch, heads, total_q, total_k, max_seqlen_q, dim, is_causal=T
                     T.gemm(q, K_s, s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                     T.clear(dp)
                     T.gemm(do, V_s, dp, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                    for i, j in T.Parallel(block_M, block_N):
-                        ok = (k * block_N + j < k_len) & (bx * block_M + i < q_len)
-                        if is_causal:
-                            ok = ok & (bx * block_M + i + off >= k * block_N + j)
-                        ds_cast[i, j] = T.if_then_else(
-                            ok, T.exp2(s[i, j] * scale - lse_s[i]) * (dp[i, j] - delta_s[i]) * sm_scale, 0.0)
+                    inner = ((k + 1) * block_N <= k_len) & ((bx + 1) * block_M <= q_len)
+                    if is_causal:
+                        inner = inner & (bx * block_M + off >= (k + 1) * block_N - 1)
+                    if inner:
+                        for i, j in T.Parallel(block_M, block_N):
+                            ds_cast[i, j] = T.exp2(s[i, j] * scale - lse_s[i]) * (dp[i, j] - delta_s[i]) * sm_scale
+                    else:
+                        for i, j in T.Parallel(block_M, block_N):
+                            ok = (k * block_N + j < k_len) & (bx * block_M + i < q_len)
+                            if is_causal:
+                                ok = ok & (bx * block_M + i + off >= k * block_N + j)
+                            ds_cast[i, j] = T.if_then_else(
+                                ok, T.exp2(s[i, j] * scale - lse_s[i]) * (dp[i, j] - delta_s[i]) * sm_scale, 0.0)
                     T.gemm(ds_cast, K_s, dq, policy=T.GemmWarpPolicy.FullRow)
                 for i, d in T.Parallel(block_M, dim):
                     if bx * block_M + i < q_len:
