@@ -147,14 +147,19 @@ def nsa_block_mask(batch, seq_len, head_kv, selected_blocks, num_blocks):
 
 @tilelang.jit(out_idx=[-1], pass_configs=FAST_MATH)
 def nsa_bwd_dq(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=None, block_size=64, groups=16,
-               selected_blocks=16, block_T=32, dtype="bfloat16"):
+               selected_blocks=16, block_T=64, dtype="bfloat16", threads=None):
+    """One workgroup per (token, kv head).  The G x BT score tile and the G x D dQ tile are split
+    over ``threads // 64`` waves along their columns (default 4 waves for G=16), so a token's
+    16 x 1024 x 128 chain of small GEMMs runs on four SIMDs instead of one."""
     sm = (1.0 / dim)**0.5 if scale is None else scale
     scale = sm * LOG2E
     head_kv = heads // groups
     G, BS, S, D = groups, block_size, selected_blocks, dim
     BT = min(block_T, BS)
     NT = BS // BT
-    threads = 64 * (G // 16)
+    if threads is None:
+        threads = 64 * max(1, min(4, BT // 16))
+    pol = T.GemmWarpPolicy.FullRow if threads == 64 * (G // 16) else T.GemmWarpPolicy.FullCol
     past = seq_len_kv - seq_len
     accum_dtype = "float"
 
@@ -189,32 +194,45 @@ def nsa_bwd_dq(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=Non
                 T.copy(K[b, i_s:i_s + BT, h, :], k_s)
                 T.copy(V[b, i_s:i_s + BT, h, :], v_s)
                 T.clear(s)
-                T.gemm(q_s, k_s, s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.gemm(q_s, k_s, s, transpose_B=True, policy=pol)
                 T.clear(dp)
-                T.gemm(do_s, v_s, dp, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                T.gemm(do_s, v_s, dp, transpose_B=True, policy=pol)
                 for g, j in T.Parallel(G, BT):
                     ok = (blk >= 0) & (blk * BS <= pos)
                     if is_causal:
                         ok = ok & (i_s + j <= pos)
                     p = T.if_then_else(ok, T.exp2(s[g, j] * scale - lse_s[g]), 0.0)
                     ds_s[g, j] = p * (dp[g, j] - dl_s[g]) * sm
-                T.gemm(ds_s, k_s, dq, policy=T.GemmWarpPolicy.FullRow)
+                T.gemm(ds_s, k_s, dq, policy=pol)
             T.copy(dq, dQ[b, bx, h * G:(h + 1) * G, :])
 
     return main
 
 
-@tilelang.jit(out_idx=[-2, -1], pass_configs=FAST_MATH)
-def nsa_bwd_dkv(batch, heads, seq_len, seq_len_kv, dim, n_pairs, is_causal=True, scale=None, block_size=64,
-                groups=16, tokens_per_tile=4, threads=256, num_stages=2, dtype="bfloat16"):
+def _list_bounds(batch, seq_len, head_kv, selected_blocks, num_blocks, tokens_per_tile, chunk_tiles):
+    """Static upper bounds of the token-list buffers (so the kernels never recompile as the
+    selection changes): pairs incl. per-list padding, tiles, and work items (chunks)."""
+    n_lists = batch * head_kv * num_blocks
+    pairs = batch * seq_len * head_kv * selected_blocks
+    p_max = pairs + n_lists * (tokens_per_tile - 1)
+    t_max = p_max // tokens_per_tile
+    i_max = -(-t_max // chunk_tiles) + n_lists
+    return p_max, i_max
+
+
+@tilelang.jit(pass_configs=FAST_MATH)  # dK / dV: caller-zeroed fp32 accumulators (atomics)
+def nsa_bwd_dkv(batch, heads, seq_len, seq_len_kv, dim, selected_blocks, is_causal=True, scale=None, block_size=64,
+                groups=16, tokens_per_tile=4, chunk_tiles=32, threads=256, num_stages=2, dtype="bfloat16"):
     """dK/dV over the compacted (block -> selecting tokens) lists built by ``token_lists``.
 
-    One workgroup per (key block j, kv head, batch) keeps K_j / V_j and the dK / dV accumulators
-    resident and walks ONLY the tokens that selected j, ``tokens_per_tile`` at a time
-    (R = tokens * G query-head rows): the Q / dO rows are gathered by LDS-DMA (``T.gather_rows``
-    over the flattened [B*SQ*HQ, D] views, row ids from the list; pad entries are -1 -> zero
-    rows) and the per-row LSE / Delta come pre-gathered, so every K step is a pipelined
-    producer and no tile is spent on tokens that did not select the block."""
+    Work item = (key block j of one kv head and batch, a chunk of <= ``chunk_tiles`` tiles of its
+    token list): early key blocks are selected by far more tokens than late ones (causal
+    selection), so whole lists per workgroup left the grid waiting on block 0's list; chunks keep
+    every item about the same size.  An item keeps K_j / V_j in LDS, walks only tokens that
+    selected j, ``tokens_per_tile`` at a time (R = tokens * G query-head rows): Q / dO rows are
+    gathered by LDS-DMA (``T.gather_rows`` over the flattened [B*SQ*HQ, D] views; pad entries are
+    -1 -> zero rows), LSE / Delta come pre-gathered, and the partial dK / dV are added into fp32
+    accumulators with atomics (one 64 x 128 tile per item)."""
     sm = (1.0 / dim)**0.5 if scale is None else scale
     scale = sm * LOG2E
     head_kv = heads // groups
@@ -223,19 +241,19 @@ def nsa_bwd_dkv(batch, heads, seq_len, seq_len_kv, dim, n_pairs, is_causal=True,
     NB = seq_len_kv // BS
     past = seq_len_kv - seq_len
     rows = batch * seq_len * heads
+    p_max, i_max = _list_bounds(batch, seq_len, head_kv, selected_blocks, NB, TT, chunk_tiles)
     accum_dtype = "float"
 
     @T.prim_func
     def main(Q: T.Tensor([rows, D], dtype), K: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
              V: T.Tensor([batch, seq_len_kv, head_kv, D], dtype), dO: T.Tensor([rows, D], dtype),
-             RowIdx: T.Tensor([n_pairs * G], "int32"), TokP: T.Tensor([n_pairs], "int32"),
-             LseP: T.Tensor([n_pairs * G], "float32"), DeltaP: T.Tensor([n_pairs * G], "float32"),
-             Off: T.Tensor([batch * head_kv * NB + 1], "int32"),
-             dK: T.Tensor([batch, seq_len_kv, head_kv, D], dtype),
-             dV: T.Tensor([batch, seq_len_kv, head_kv, D], dtype)):
-        with T.Kernel(NB, batch * head_kv, threads=threads) as (j, bz):
-            b = bz // head_kv
-            h = bz % head_kv
+             RowIdx: T.Tensor([p_max * G], "int32"), TokP: T.Tensor([p_max], "int32"),
+             LseP: T.Tensor([p_max * G], "float32"), DeltaP: T.Tensor([p_max * G], "float32"),
+             ItemList: T.Tensor([i_max], "int32"), ItemPair0: T.Tensor([i_max], "int32"),
+             ItemTiles: T.Tensor([i_max], "int32"),
+             dK: T.Tensor([batch, seq_len_kv, head_kv, D], accum_dtype),
+             dV: T.Tensor([batch, seq_len_kv, head_kv, D], accum_dtype)):
+        with T.Kernel(i_max, threads=threads) as item:
             k_s = T.alloc_shared([BS, D], dtype)
             v_s = T.alloc_shared([BS, D], dtype)
             q_s = T.alloc_shared([R, D], dtype)
@@ -249,96 +267,127 @@ def nsa_bwd_dkv(batch, heads, seq_len, seq_len_kv, dim, n_pairs, is_causal=True,
             dp = T.alloc_fragment([R, BS], accum_dtype)
             dk = T.alloc_fragment([BS, D], accum_dtype)
             dv = T.alloc_fragment([BS, D], accum_dtype)
-            T.copy(K[b, j * BS:(j + 1) * BS, h, :], k_s)
-            T.copy(V[b, j * BS:(j + 1) * BS, h, :], v_s)
-            T.clear(dk)
-            T.clear(dv)
-            p0 = Off[bz * NB + j]
-            n_t = (Off[bz * NB + j + 1] - p0) // TT
-            for it in T.Pipelined(n_t, num_stages=num_stages):
-                base = p0 + it * TT
-                T.gather_rows(Q[:, :], RowIdx[base * G:base * G + R], q_s, row_dim=0)
-                T.gather_rows(dO[:, :], RowIdx[base * G:base * G + R], do_s, row_dim=0)
-                T.copy(LseP[base * G:base * G + R], lse_s)
-                T.copy(DeltaP[base * G:base * G + R], dl_s)
-                T.copy(TokP[base:base + TT], tok_s)
-                T.clear(s)
-                T.gemm(q_s, k_s, s, transpose_B=True)
-                T.clear(dp)
-                T.gemm(do_s, v_s, dp, transpose_B=True)
-                for r, c in T.Parallel(R, BS):
-                    ok = tok_s[r // G] >= 0
-                    if is_causal:
-                        ok = ok & (j * BS + c <= tok_s[r // G] + past)
-                    p = T.if_then_else(ok, T.exp2(s[r, c] * scale - lse_s[r]), 0.0)
-                    p_s[r, c] = p
-                    ds_s[r, c] = p * (dp[r, c] - dl_s[r]) * sm
-                T.gemm(p_s, do_s, dv, transpose_A=True)
-                T.gemm(ds_s, q_s, dk, transpose_A=True)
-            T.copy(dk, dK[b, j * BS:(j + 1) * BS, h, :])
-            T.copy(dv, dV[b, j * BS:(j + 1) * BS, h, :])
+            lst = ItemList[item]
+            if lst >= 0:
+                # list id -> (batch, kv head, block), clamped for the bounds prover
+                j = T.max(T.min(lst % NB, NB - 1), 0)
+                h = T.max(T.min((lst // NB) % head_kv, head_kv - 1), 0)
+                b = T.max(T.min(lst // (NB * head_kv), batch - 1), 0)
+                p0 = ItemPair0[item]
+                T.copy(K[b, j * BS:(j + 1) * BS, h, :], k_s)
+                T.copy(V[b, j * BS:(j + 1) * BS, h, :], v_s)
+                T.clear(dk)
+                T.clear(dv)
+                for it in T.Pipelined(ItemTiles[item], num_stages=num_stages):
+                    base = p0 + it * TT
+                    T.gather_rows(Q[:, :], RowIdx[base * G:base * G + R], q_s, row_dim=0)
+                    T.gather_rows(dO[:, :], RowIdx[base * G:base * G + R], do_s, row_dim=0)
+                    T.copy(LseP[base * G:base * G + R], lse_s)
+                    T.copy(DeltaP[base * G:base * G + R], dl_s)
+                    T.copy(TokP[base:base + TT], tok_s)
+                    T.clear(s)
+                    T.gemm(q_s, k_s, s, transpose_B=True)
+                    T.clear(dp)
+                    T.gemm(do_s, v_s, dp, transpose_B=True)
+                    for r, c in T.Parallel(R, BS):
+                        ok = tok_s[r // G] >= 0
+                        if is_causal:
+                            ok = ok & (j * BS + c <= tok_s[r // G] + past)
+                        p = T.if_then_else(ok, T.exp2(s[r, c] * scale - lse_s[r]), 0.0)
+                        p_s[r, c] = p
+                        ds_s[r, c] = p * (dp[r, c] - dl_s[r]) * sm
+                    T.gemm(p_s, do_s, dv, transpose_A=True)
+                    T.gemm(ds_s, q_s, dk, transpose_A=True)
+                T.atomic_add(dK[b, j * BS:(j + 1) * BS, h, :], dk)
+                T.atomic_add(dV[b, j * BS:(j + 1) * BS, h, :], dv)
 
     return main
 
 
-def token_lists(block_indices, lse, delta, num_blocks, heads, tokens_per_tile=4):
+def token_lists(block_indices, lse, delta, num_blocks, heads, tokens_per_tile=4, chunk_tiles=32):
     """Invert BlockIndices [B, SQ, H, S] into per-(batch, kv head, block) lists of the tokens that
-    selected the block (on the device, torch sort + scatters), each list padded to a multiple of
-    ``tokens_per_tile`` with -1 entries.  Returns (RowIdx, TokP, LseP, DeltaP, Off, n_pairs): the
-    flattened Q row of every (pair, query head in the group), the token of every pair, the LSE /
-    Delta of every row, and the list offsets."""
+    selected the block (on the device: torch sort + scatters, no host sync), each list padded to a
+    multiple of ``tokens_per_tile`` with -1 entries, and cut into work items of <= ``chunk_tiles``
+    tiles.  Buffers have the static sizes of ``_list_bounds``.  Returns (RowIdx, TokP, LseP, DeltaP,
+    ItemList, ItemPair0, ItemTiles): the flattened Q row of every (pair, query head in the group),
+    the token of every pair, the LSE / Delta of every row, and per work item its list id (-1:
+    unused), first pair and tile count."""
     import torch
     B, SQ, H, S = block_indices.shape
     G = heads // H
-    TT = tokens_per_tile
+    TT, CH = tokens_per_tile, chunk_tiles
     dev = block_indices.device
+    nl = B * H * num_blocks
+    p_max, i_max = _list_bounds(B, SQ, H, S, num_blocks, TT, CH)
     blk = block_indices.long()
     bb = torch.arange(B, device=dev).view(B, 1, 1, 1).expand_as(blk)
     tt = torch.arange(SQ, device=dev).view(1, SQ, 1, 1).expand_as(blk)
     hh = torch.arange(H, device=dev).view(1, 1, H, 1).expand_as(blk)
     ok = (blk >= 0) & (blk < num_blocks)
-    key = ((bb * H + hh) * num_blocks + blk)[ok]
-    tok = tt[ok]
+    # invalid pairs sort to the end under key nl (dropped by the bincount range below)
+    key = torch.where(ok, (bb * H + hh) * num_blocks + blk, torch.full_like(blk, nl)).reshape(-1)
+    tok = tt.reshape(-1)
     order = torch.argsort(key * SQ + tok)
     key, tok = key[order], tok[order]
-    nl = B * H * num_blocks
-    cnt = torch.bincount(key, minlength=nl)
-    padded = (cnt + TT - 1) // TT * TT
+    cnt = torch.bincount(key, minlength=nl + 1)[:nl]
+    tiles = (cnt + TT - 1) // TT
     off = torch.zeros(nl + 1, dtype=torch.long, device=dev)
-    off[1:] = torch.cumsum(padded, 0)
-    start = torch.zeros(nl, dtype=torch.long, device=dev)
-    start[1:] = torch.cumsum(cnt, 0)[:-1]
-    n_pairs = max(int(off[-1].item()), TT)  # one host sync: the buffer sizes
-    dest = off[key] + (torch.arange(key.numel(), device=dev) - start[key])
-    tokp = torch.full((n_pairs, ), -1, dtype=torch.int32, device=dev)
-    tokp[dest] = tok.int()
-    b_of = key // (H * num_blocks)
-    h_of = (key // num_blocks) % H
+    off[1:] = torch.cumsum(tiles * TT, 0)
+    start = torch.zeros(nl + 1, dtype=torch.long, device=dev)
+    start[1:] = torch.cumsum(cnt, 0)
+    valid = key < nl
+    kv_ = torch.where(valid, key, torch.zeros_like(key))
+    rank = torch.arange(key.numel(), device=dev) - start[kv_]
+    dest = torch.where(valid, off[kv_] + rank, torch.full_like(key, p_max))  # p_max: a dump slot
+    tokp = torch.full((p_max + 1, ), -1, dtype=torch.int32, device=dev)
+    tokp[dest] = torch.where(valid, tok, torch.full_like(tok, -1)).int()
+    b_of = kv_ // (H * num_blocks)
+    h_of = (kv_ // num_blocks) % H
     g = torch.arange(G, device=dev)
     rows = ((b_of * SQ + tok) * (H * G) + h_of * G).view(-1, 1) + g.view(1, -1)  # [pairs, G]
-    rowidx = torch.full((n_pairs, G), -1, dtype=torch.int32, device=dev)
-    rowidx[dest] = rows.int()
-    lsep = torch.zeros((n_pairs, G), dtype=torch.float32, device=dev)
-    dlp = torch.zeros((n_pairs, G), dtype=torch.float32, device=dev)
+    rowidx = torch.full((p_max + 1, G), -1, dtype=torch.int32, device=dev)
+    rowidx[dest] = torch.where(valid.view(-1, 1), rows, torch.full_like(rows, -1)).int()
+    lsep = torch.zeros((p_max + 1, G), dtype=torch.float32, device=dev)
+    dlp = torch.zeros((p_max + 1, G), dtype=torch.float32, device=dev)
     lsep[dest] = lse.reshape(-1)[rows]
     dlp[dest] = delta.reshape(-1)[rows]
-    return rowidx.view(-1), tokp, lsep.view(-1), dlp.view(-1), off.int(), n_pairs
+    # work items: list l contributes ceil(tiles_l / CH) chunks
+    nchunk = (tiles + CH - 1) // CH
+    ilist = torch.repeat_interleave(torch.arange(nl, device=dev), nchunk)
+    cstart = torch.zeros(nl + 1, dtype=torch.long, device=dev)
+    cstart[1:] = torch.cumsum(nchunk, 0)
+    ci = torch.arange(ilist.numel(), device=dev) - cstart[ilist]
+    item_list = torch.full((i_max, ), -1, dtype=torch.int32, device=dev)
+    item_p0 = torch.zeros((i_max, ), dtype=torch.int32, device=dev)
+    item_nt = torch.zeros((i_max, ), dtype=torch.int32, device=dev)
+    n_items = ilist.numel()  # <= i_max by construction
+    item_list[:n_items] = ilist.int()
+    item_p0[:n_items] = (off[ilist] + ci * CH * TT).int()
+    item_nt[:n_items] = torch.minimum(tiles[ilist] - ci * CH, torch.full_like(ci, CH)).int()
+    return (rowidx[:p_max].reshape(-1), tokp[:p_max], lsep[:p_max].reshape(-1), dlp[:p_max].reshape(-1), item_list,
+            item_p0, item_nt)
 
 
 def nsa_backward(q, k, v, block_indices, o, lse, do, block_size=64, is_causal=True):
     """(dq, dk, dv) of the NSA selected-block attention."""
+    import torch
     B, SQ, HQ, D = q.shape
     SKV, H = k.shape[1], k.shape[2]
     S = block_indices.shape[-1]
     G = HQ // H
     delta = nsa_bwd_prep(B, SQ, HQ, D, _dt(q))(o.reshape(-1, D), do.reshape(-1, D)).view(B, SQ, HQ)
-    dq = nsa_bwd_dq(B, HQ, SQ, SKV, D, is_causal, None, block_size, G, S, dtype=_dt(q))(q, k, v, block_indices, do,
-                                                                                         lse, delta)
-    TT = max(1, 64 // G)
-    rowidx, tokp, lsep, dlp, off, n_pairs = token_lists(block_indices, lse, delta, SKV // block_size, HQ, TT)
-    dk, dv = nsa_bwd_dkv(B, HQ, SQ, SKV, D, n_pairs, is_causal, None, block_size, G, TT, dtype=_dt(q))(
-        q.reshape(-1, D), k, v, do.reshape(-1, D), rowidx, tokp, lsep, dlp, off)
-    return dq, dk, dv
+    dq = nsa_bwd_dq(B, HQ, SQ, SKV, D, is_causal, None, block_size, G, S, dtype=_dt(q), **DQ_CFG)(
+        q, k, v, block_indices, do, lse, delta)
+    TT, CH = max(1, 64 // G), 32
+    lists = token_lists(block_indices, lse, delta, SKV // block_size, HQ, TT, CH)
+    dk32 = torch.zeros(k.shape, dtype=torch.float32, device=k.device)
+    dv32 = torch.zeros(v.shape, dtype=torch.float32, device=v.device)
+    nsa_bwd_dkv(B, HQ, SQ, SKV, D, S, is_causal, None, block_size, G, TT, CH, dtype=_dt(q))(
+        q.reshape(-1, D), k, v, do.reshape(-1, D), *lists, dk32, dv32)
+    return dq, dk32.to(k.dtype), dv32.to(v.dtype)
+
+
+DQ_CFG = {}  # nsa_bwd_dq tile overrides (block_T, threads) for A/B runs
 
 
 def _dt(t):

@@ -337,7 +337,7 @@ def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N
 
 
 BWD_DQ_MODE = "separate"  # or "atomic" (single kernel, fp32 atomics into dQ)
-BWD_OVERLAP = True  # dQ kernel on a side stream, concurrent with the dK/dV kernel
+BWD_OVERLAP = False  # dQ on a side stream: measured slower (0.374 -> 0.509 ms, profiles/r3/s3/bwd/)
 
 
 def _tiles(D, Dv, kind, causal=False):
