@@ -3,7 +3,8 @@
 ``num_split_q`` workgroups per (batch, head) walk the query tiles with a ``T.While`` loop
 instead of one workgroup per tile: the grid stays resident (one 8-wave workgroup per CU), and each
 workgroup's K/V stream (LDS-DMA ring) moves on to its next query tile without a relaunch.  Tiles
-are dealt in cost order along a snake, so causal heads are balanced exactly (see fast_flashattn).  The tile body is the staged FA kernel of examples/flash_attention/example_mha_fwd_pipelined.py
+are dealt in cost order along a snake, so causal heads are balanced exactly (see fast_flashattn).
+The tile body is the staged FA kernel of examples/flash_attention/example_mha_fwd_pipelined.py
 (T.Pipelined order/stage/group: QK^T(t) next to rescale + PV(t-1)): Q in registers, P kept in
 registers as the PV operand, lazy rescale, fast exp2.
 """

@@ -60,3 +60,34 @@ def test_moe_expert_gemms_use_lds_dma(gather):
         src = fn(mr, 2048, 4096, 8, "bfloat16", "hip", 256, 256, 64, 2, 512, **kw).get_kernel_source()
         dma, staged = _counts(src)
         assert dma > 0 and staged == 0, (fn.__name__, gather, dma, staged)
+
+
+def _small_tile_kernel(big_elems):
+    import tilelang.language as T
+
+    @T.prim_func
+    def main(L: T.Tensor((64, 4096), "float32"), X: T.Tensor((64, 64), "float32"), O: T.Tensor((64, 64), "float32")):
+        with T.Kernel(64, threads=256) as bx:
+            big = T.alloc_shared((big_elems, ), "float32")
+            l_s = T.alloc_shared((64, ), "float32")
+            acc = T.alloc_fragment((64, ), "float32")
+            T.clear(acc)
+            T.copy(X[bx, :], big[0:64])
+            for k in T.Pipelined(64, num_stages=3):
+                T.copy(L[bx, k * 64:(k + 1) * 64], l_s)
+                for i in T.Parallel(64):
+                    acc[i] += l_s[i] * big[i]
+            T.copy(acc, O[bx, :])
+
+    return main
+
+
+def test_small_tile_dma_and_lds_overflow_fallback():
+    """A 256-byte per-step tile (an LSE row, an MX scale tile) becomes ONE 4-byte buffer LDS-DMA per
+    wave (tl::buffer_lds4) instead of a register-staged copy; when the padded stage slots would push
+    the arena past 160 KiB the kernel is lowered again with register staging."""
+    src = tilelang.lower(_small_tile_kernel(1024), target="hip").kernel_source
+    assert "tl::buffer_lds4(" in src and not re.search(r"\bstage\d+\[", src)
+    # 158 KiB of other LDS: 3 padded 1 KiB slots (4 waves x 256 B) no longer fit
+    src = tilelang.lower(_small_tile_kernel(158 * 256), target="hip").kernel_source
+    assert "tl::buffer_lds4(" not in src and re.search(r"\bstage\d+\[", src)

@@ -35,5 +35,10 @@ TL_DEVICE __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t num_bytes)
 TL_DEVICE void buffer_lds16(__amdgpu_buffer_rsrc_t rsrc, uint32_t voffset, void* lds_dst) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(lds_dst), 16, voffset, 0, 0, 0);
 }
+// 4 bytes per lane (small tiles: one instruction per wave, see transform/pipeline.py
+// _small_dma_plan); lane l writes lds_dst + 4 l
+TL_DEVICE void buffer_lds4(__amdgpu_buffer_rsrc_t rsrc, uint32_t voffset, void* lds_dst) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)(lds_dst), 4, voffset, 0, 0, 0);
+}
 
 }  // namespace tl

@@ -1370,6 +1370,8 @@ class TileOpLowerer(Mutator):
         p = op.plan
         if p.get("gather"):
             return self.lower_async_gather(op)
+        if p.get("small"):
+            return self.lower_async_small(op)
         src, dst = op.src, op.dst
         NB = dst.buffer
         lay = NB.layout
@@ -1407,6 +1409,34 @@ class TileOpLowerer(Mutator):
             out.append(L.CallStmt("tl::glds16", [L.BufferPtr(ctx.flat_of(src.buffer), gidx),
                                                  L.BufferPtr(ctx.flat_of(NB), lds_off)]))
         return S.SeqStmt(out)
+
+    def lower_async_small(self, op: AsyncCopyOp):
+        """Small-tile DMA (pipeline._small_dma_plan): one 4-byte buffer LDS-DMA per wave; lane chunk
+        ``P = wave * 64 + lane`` of the row-major tile, lanes past the tile (or the tensor) get an
+        out-of-range offset and write a zero into the slot's padding."""
+        ctx = self.ctx
+        p = op.plan
+        src, dst = op.src, op.dst
+        NB = dst.buffer
+        eb, cpr = p["eb"], p["cpr"]
+        epc = max(1, 4 // eb)
+        wave, lane = ctx.wave_expr(), ctx.lane_expr()
+        stage = self.expr(dst.mins[0])
+        base_off = ctx.flat_index(NB, [stage] + [IntImm(0)] * (NB.ndim - 1))
+        P = binop("+", binop("*", wave, 64), lane)
+        row = binop("//", P, cpr)
+        col = binop("*", binop("%", P, cpr), epc)
+        idx = [self.expr(m) for m in src.mins]
+        if p["rdim"] is not None:
+            idx[p["rdim"]] = binop("+", idx[p["rdim"]], row)
+        idx[p["cdim"]] = binop("+", idx[p["cdim"]], col)
+        gidx = ctx.flat_index(src.buffer, idx)
+        rsrc = call("extern", ["tl::make_rsrc", L.BufferPtr(ctx.flat_of(src.buffer), 0),
+                               IntImm(p["oob_bytes"], _dt.uint32)], _dt.handle)
+        ok = binop("<", P, p["nchunks"])
+        voff = select(ok, cast(binop("*", gidx, eb), _dt.uint32), IntImm(0xFFFFFFF0, _dt.uint32))
+        lds_off = binop("+", base_off, binop("*", binop("*", wave, 64), epc if eb <= 4 else 1))
+        return S.SeqStmt([L.CallStmt("tl::buffer_lds4", [rsrc, voff, L.BufferPtr(ctx.flat_of(NB), lds_off)])])
 
     def lower_async_gather(self, op: AsyncCopyOp):
         """Row gather as buffer LDS-DMA: each lane fetches the 16-byte chunk that lands at its

@@ -126,10 +126,14 @@ def glds_plan(op: O.CopyOp, num_threads: int, ranges, target) -> Optional[dict]:
     eb = sb.dtype.bytes
     dext = dst.static_extents()
     dshape = db.static_shape()
-    if dext is None or dshape is None or dext != dshape or len(dshape) != 2:
+    if dext is None or dshape is None or dext != dshape or len(dshape) not in (1, 2):
         return None
+    if len(dshape) == 1 or (dshape[0] * dshape[1] * eb) % (1024 * (num_threads // 64)):
+        if getattr(target, "disable_small_dma", False):
+            return None
+        return _small_dma_plan(op, num_threads, ranges)
     R, C = dshape
-    if (C * eb) % 16 or (R * C * eb) % (1024 * (num_threads // 64)):
+    if (C * eb) % 16:
         return None
     lay = db.layout
     if lay is not None and not isinstance(lay, (SwizzleLayout, LinearLayout)):
@@ -188,6 +192,89 @@ def glds_plan(op: O.CopyOp, num_threads: int, ranges, target) -> Optional[dict]:
     nw = num_threads // 64
     return dict(R=R, C=C, eb=eb, rdim=rdim, cdim=cdim, instrs=n_chunks // 64 // nw, nwaves=nw, cpr=C * eb // 16,
                 oob_bytes=nbytes)
+
+
+def _small_dma_plan(op: O.CopyOp, num_threads: int, ranges) -> Optional[dict]:
+    """LDS-DMA for a tile smaller than one 16-byte DMA per lane of the workgroup (MX scale tiles,
+    per-row LSE / Delta vectors): every wave issues exactly ONE 4-byte buffer LDS-DMA
+    (``tl::buffer_lds4``), lane chunk ``P = wave * 64 + lane``; lanes past the tile get an
+    out-of-range offset (the hardware writes a zero and reads nothing) and land in padding of the
+    stage slot, which is sized ``waves * 256`` bytes.  One instruction per wave keeps the counted
+    ``vmcnt`` waits uniform; the alternative -- a register-staged copy -- needs its global load
+    retired before its ds_write, and the compiler's conservative LDS-DMA alias wait in front of that
+    ds_write is ``vmcnt(0)``, which drained the whole ring every iteration."""
+    src, dst = op.src, op.dst
+    sb, db = src.buffer, dst.buffer
+    eb = sb.dtype.bytes
+    dshape = db.static_shape()
+    nw = num_threads // 64
+    total = 1
+    for d in dshape:
+        total *= d
+    if (total * eb) % 4 or total * eb > 256 * nw or eb > 4:
+        return None
+    lay = db.layout
+    if lay is not None and not (isinstance(lay, LinearLayout) or (isinstance(lay, SwizzleLayout) and not lay.bits)):
+        return None
+    R, C = (1, dshape[0]) if len(dshape) == 1 else dshape
+    if (C * eb) % 4:
+        return None
+    sext = src.static_extents()
+    if sext is None:
+        return None
+    nonunit = [d for d, e in enumerate(sext) if e != 1]
+    if R == 1:
+        if len(nonunit) != 1 or sext[nonunit[0]] != C:
+            return None
+        rdim, cdim = None, nonunit[0]
+    else:
+        if len(nonunit) != 2 or sext[nonunit[0]] != R or sext[nonunit[1]] != C:
+            return None
+        rdim, cdim = nonunit
+    strides = sb.get_strides()
+    if as_int(strides[cdim]) != 1:
+        return None
+    epc = max(1, 4 // eb)  # elements per 4-byte chunk
+    if rdim is not None and not divisible_by(convert(strides[rdim]), epc):
+        return None
+    if not divisible_by(src.region[cdim][0], epc):
+        return None
+    shape = sb.shape
+    for d, (m, e) in enumerate(src.region):  # outer dim may leave the tensor (zero fill), others not
+        b = bound(m, ranges)
+        s_ = as_int(shape[d])
+        ev = as_int(e)
+        if b is None or s_ is None or ev is None or b[0] < 0 or b[1] + ev > s_:
+            if d == 0 and ev is not None:
+                continue
+            return None
+    numel = 1
+    for s_ in shape:
+        if as_int(s_) is None:
+            return None
+        numel *= as_int(s_)
+    if sb.strides is not None or numel * eb >= (1 << 31):
+        return None
+    return dict(small=True, R=R, C=C, eb=eb, rdim=rdim, cdim=cdim, cpr=C * eb // 4, instrs=1, nwaves=nw,
+                nchunks=total * eb // 4, oob_bytes=numel * eb, pad_elems=nw * 256 // eb)
+
+
+def _padded_stage_layout(shape: List[int], stages: int, pad_elems: int) -> Layout:
+    """Row-major stage slots of ``pad_elems`` elements each (small-tile DMA padding)."""
+    strides = []
+    acc = 1
+    for d in reversed(shape):
+        strides.append(acc)
+        acc *= d
+    strides = strides[::-1]
+
+    def fwd(s, *idx):
+        off = s * pad_elems
+        for i, st in zip(idx, strides):
+            off = off + i * st
+        return [off]
+
+    return Layout([stages] + list(shape), fwd, None, [stages * pad_elems], name="stage_padded")
 
 
 def gather_plan(op: O.GatherRowsOp, num_threads: int, target) -> Optional[dict]:
@@ -323,31 +410,6 @@ class PipelineInjector(Mutator):
                 fv |= {id(v) for v in free_vars(m)}
             loop_local = {id(v) for v in lets}  # unresolved lets would appear as themselves
             prods.append((p, src))
-        # multi-version the shared buffers
-        mapping = {}
-        newbufs = {}
-        versions = getattr(self, "versions", None)
-        if versions is None:
-            versions = self.versions = {}
-        for p, _ in prods:
-            B = p.op.dst.buffer
-            if B in newbufs:
-                continue
-            # several pipelined loops over the same tile (e.g. an unmasked main loop and a masked
-            # tail) share one multi-versioned LDS ring per stage count
-            NB = versions.get((B, nstages))
-            if NB is None:
-                shp = B.static_shape()
-                NB = Buffer(B.name, [nstages] + shp, B.dtype, "shared")
-                NB.layout = stage_layout(B.layout, shp, nstages)
-                NB._auto_name = False
-                NB.stages_of = B
-                versions[(B, nstages)] = NB
-            newbufs[B] = NB
-        kk = binop("-", k, loop.min)
-        stage = binop("%", kk, nstages)
-        for B, NB in newbufs.items():
-            mapping[B] = (NB, [stage])
         # classify producers
         rng = dict(self.ranges)
         if as_int(loop.min) is not None and as_int(loop.extent) is not None:
@@ -381,6 +443,38 @@ class PipelineInjector(Mutator):
                 _log.debug("register-staged pipeline copy %s -> %s (not provably in bounds / not DMA-shaped): %s",
                            src.buffer.name, p.op.dst.buffer.name,
                            [(str(m), bound(m, rng)) for m, _ in src.region])
+        small_pad = {}
+        for p, _, plan in asyncs:
+            if plan.get("small"):
+                small_pad[p.op.dst.buffer] = plan["pad_elems"]
+        # multi-version the shared buffers
+        mapping = {}
+        newbufs = {}
+        versions = getattr(self, "versions", None)
+        if versions is None:
+            versions = self.versions = {}
+        for p, _ in prods:
+            B = p.op.dst.buffer
+            if B in newbufs:
+                continue
+            # several pipelined loops over the same tile (e.g. an unmasked main loop and a masked
+            # tail) share one multi-versioned LDS ring per stage count
+            pad = small_pad.get(B)
+            NB = versions.get((B, nstages, pad))
+            if NB is None:
+                shp = B.static_shape()
+                NB = Buffer(B.name, [nstages] + shp, B.dtype, "shared")
+                # small-tile DMA: every wave writes a 256-byte window of the slot (padding)
+                NB.layout = stage_layout(B.layout, shp, nstages) if pad is None else \
+                    _padded_stage_layout(shp, nstages, pad)
+                NB._auto_name = False
+                NB.stages_of = B
+                versions[(B, nstages, pad)] = NB
+            newbufs[B] = NB
+        kk = binop("-", k, loop.min)
+        stage = binop("%", kk, nstages)
+        for B, NB in newbufs.items():
+            mapping[B] = (NB, [stage])
         L_instr = sum(pl["instrs"] for _, _, pl in asyncs)
 
         gkeys = {}
@@ -463,15 +557,19 @@ class PipelineInjector(Mutator):
             else:
                 body.append(L.CallStmt("tl::wait_vmcnt", [], [0]))
         body.append(L.CallStmt("tl::barrier_raw", []))
+        if staged:
+            # register-staged loads go out BEFORE this iteration's LDS-DMAs: vmcnt retires in issue
+            # order, so the wait the compiler puts in front of their LDS store can leave the DMAs
+            # in flight (vmcnt(#DMAs)); issued after them it had to be vmcnt(0), which drained the
+            # whole ring every iteration (the MX GEMM's scale tiles: 63 % of wave cycles waiting)
+            j1 = binop("+", kk, 1)
+            body.append(S.IfStmt(binop("<", j1, n), S.seq(*staged_phase(j1, binop("%", j1, nstages), "load"))))
         if asyncs:
             j = binop("+", kk, nstages - 1)
             body.append(S.IfStmt(binop("<", j, n), S.seq(*issue_async(j, binop("%", j, nstages)))))
             if gkeys:
                 j2 = binop("+", kk, nstages)
                 body.append(S.IfStmt(binop("<", j2, n), S.seq(*gather_idx(j2))))
-        if staged:
-            j1 = binop("+", kk, 1)
-            body.append(S.IfStmt(binop("<", j1, n), S.seq(*staged_phase(j1, binop("%", j1, nstages), "load"))))
         body.append(consumers)
         if staged:
             j1 = binop("+", kk, 1)

@@ -33,6 +33,7 @@ class Target:
     mesh: Optional[Tuple[int, int]] = None
     attrs: dict = field(default_factory=dict)
     disable_glds: bool = False
+    disable_small_dma: bool = False  # set when small-tile LDS-DMA padding would overflow the LDS
 
     def __str__(self):
         s = self.kind if self.kind == "cpu" else f"hip -mcpu={self.arch}"
