@@ -25,16 +25,16 @@ def mx_matmul(M, N, K, block_M=256, block_N=None, block_K=None, threads=512, num
     """``scales_in_lds``: the e8m0 scale tiles ([block, block_K/32] bytes) ride the pipeline into
     LDS with the operands, so the MFMA loop reads them with ds_read instead of waiting on a
     global load per K step."""
-    # tiles per format pair, measured at 8192^3 (scripts/sweep_mx.py, profiles/r2/mx_sweep.log):
-    # fp4 x fp4 256x128x256 3-stage 2.3-2.4 PF, fp8 x fp8 256x128x128 3-stage 1.4 PF,
-    # fp8 x fp4 256x256x128 2-stage 1.7 PF
-    same = a_fmt == b_fmt
+    # tiles per format pair, measured at 8192^3 (scripts/sweep_mx.py, profiles/r3/s3/lowp/): with the
+    # scale tiles on small-tile LDS-DMA the 256x256 2-stage tiles win for every pair:
+    # fp4 x fp4 256x256x256 3.33 PF (256x128x256 3-stage 2.49), fp8 x fp8 256x256x128 1.86 PF
+    # (256x128x128 3-stage 1.44), fp8 x fp4 256x256x128 2.26 PF
     if block_K is None:
         block_K = 256 if a_fmt == b_fmt == "e2m1" else 128
     if block_N is None:
-        block_N = 128 if same else 256
+        block_N = 256
     if num_stages is None:
-        num_stages = 3 if same else 2
+        num_stages = 2
     ac = K // 2 if a_fmt == "e2m1" else K
     bc = K // 2 if b_fmt == "e2m1" else K
     bka = block_K // 2 if a_fmt == "e2m1" else block_K

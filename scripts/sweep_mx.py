@@ -13,10 +13,10 @@ from example_tilelang_gemm_mx import mx_matmul, quantize, ref_program  # noqa: E
 
 M = N = K = 8192
 CFGS = [  # fmt, bm, bn, bk, threads, stages
-    ("e4m3", 256, 128, 128, 512, 3), ("e4m3", 128, 256, 128, 256, 3), ("e4m3", 256, 64, 128, 256, 4),
-    ("e4m3", 192, 128, 128, 512, 3),
-    ("e2m1", 256, 128, 256, 512, 3), ("e2m1", 256, 128, 128, 512, 4), ("e2m1", 256, 128, 128, 512, 6),
-    ("e2m1", 256, 256, 128, 512, 4), ("e2m1", 128, 256, 256, 512, 3),
+    ("e4m3", 256, 128, 128, 512, 3), ("e4m3", 256, 256, 128, 512, 2), ("e4m3", 128, 256, 128, 256, 3),
+    ("e4m3", 256, 128, 128, 512, 2), ("e4m3", 256, 128, 256, 512, 2), ("e4m3", 128, 128, 128, 256, 3),
+    ("e2m1", 256, 128, 256, 512, 3), ("e2m1", 256, 256, 256, 512, 2), ("e2m1", 256, 256, 128, 512, 3),
+    ("e2m1", 256, 128, 256, 512, 2), ("e2m1", 128, 256, 256, 256, 3),
 ]
 data = {}
 for f, bm, bn, bk, th, st in CFGS:
