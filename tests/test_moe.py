@@ -15,8 +15,9 @@ def test_pack_by_expert():
     mr = max_padded_rows(7, 4, 4)
     dest, te, counts = pack_by_expert(ids, 4, 4, mr)
     assert counts.tolist() == [2, 0, 4, 1]
-    assert dest.tolist() == [4, 0, 5, 8, 1, 6, 7]
-    assert te.tolist()[:3] == [0, 2, 3] and all(t == -1 for t in te.tolist()[3:])
+    # full tiles first (expert 2's four rows), then one partial tile per expert (0, then 3)
+    assert dest.tolist() == [0, 4, 1, 8, 5, 2, 3]
+    assert te.tolist()[:3] == [2, 0, 3] and all(t == -1 for t in te.tolist()[3:])
 
 
 def test_moe_local_cpu():

@@ -175,7 +175,7 @@ def max_padded_rows(n_assign: int, E: int, block_M: int) -> int:
 
 @functools.lru_cache(maxsize=None)
 def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: str, stable: bool = False,
-                 threads: int = 1024):
+                 threads: int = 1024, full_first: bool = True):
     """Dispatch plan of ``n`` assignments (``expert_ids[n]``; assignment ``j`` reads source row
     ``j // div``; a negative id is an empty slot: not placed, ``dest[j] = -1``): ``dest[j]`` (its
     padded row), ``row_src[max_rows]``, ``tile_expert``, ``counts[E]``,
@@ -185,7 +185,13 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
     row's result is independent of its position, so the layer output does not depend on it).
     ``stable=True``: assignment order is kept inside every expert (per-thread runs + a scan of
     the per-thread counts) — identical placement on every rank, which the tensor-parallel
-    in-kernel reduction needs."""
+    in-kernel reduction needs.
+
+    ``full_first``: every expert's FULL row tiles come first (expert order), then one partial tile
+    per expert with a remainder.  The tail-balanced expert GEMM runs the leading units as whole
+    tiles and splits only the trailing ones: with the partial tiles (usually a few valid rows)
+    last, the whole-tile rounds are all full tiles and the split tail is the nearly-empty work
+    (before, an expert's partial tile sat between full ones and full tiles landed in the tail)."""
     n_tiles = max_rows // block_M
     if stable:
         threads = 256
@@ -223,12 +229,24 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                         T.atomic_add(cnt[expert_ids[j]], 1)
             for r in T.Parallel(max_rows):
                 row_src[r] = -1
-            for z in T.Parallel(1):
-                acc = 0
-                for e in T.serial(E):
-                    start[e] = acc
-                    acc = acc + (cnt[e] + block_M - 1) // block_M * block_M
-                start[E] = acc + z
+            if full_first:
+                pstart = T.alloc_shared((E,), "int32")
+                for z in T.Parallel(1):
+                    acc = 0
+                    for e in T.serial(E):  # full tiles of every expert
+                        start[e] = acc
+                        acc = acc + cnt[e] // block_M * block_M
+                    for e in T.serial(E):  # then one partial tile per expert with a remainder
+                        pstart[e] = acc
+                        acc = acc + T.if_then_else(cnt[e] % block_M > 0, block_M, 0)
+                    start[E] = acc + z
+            else:
+                for z in T.Parallel(1):
+                    acc = 0
+                    for e in T.serial(E):
+                        start[e] = acc
+                        acc = acc + (cnt[e] + block_M - 1) // block_M * block_M
+                    start[E] = acc + z
             for e in T.Parallel(E):
                 counts[e] = cnt[e]
             for tt in T.Parallel(n_tiles):
@@ -237,9 +255,17 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                 te = -1
                 tr = 0
                 for e in T.serial(E):
-                    if tt * block_M >= start[e] and tt * block_M < start[e] + cnt[e]:
-                        te = e
-                        tr = T.min(start[e] + cnt[e] - tt * block_M, block_M)
+                    if full_first:
+                        if tt * block_M >= start[e] and tt * block_M < start[e] + cnt[e] // block_M * block_M:
+                            te = e
+                            tr = block_M
+                        if cnt[e] % block_M > 0 and tt * block_M == pstart[e]:
+                            te = e
+                            tr = cnt[e] % block_M
+                    else:
+                        if tt * block_M >= start[e] and tt * block_M < start[e] + cnt[e]:
+                            te = e
+                            tr = T.min(start[e] + cnt[e] - tt * block_M, block_M)
                 tile_expert[tt] = te
                 tile_rows[tt] = tr
             if stable:
@@ -248,8 +274,13 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                         run[t, e] = start[e] + run[t, e] - tc[t, e]
                     for i in T.serial(c):
                         if t * c + i < n and expert_ids[t * c + i] >= 0:
-                            d = run[t, expert_ids[t * c + i]]
-                            run[t, expert_ids[t * c + i]] = d + 1
+                            e_ = expert_ids[t * c + i]
+                            d = run[t, e_]
+                            run[t, e_] = d + 1
+                            if full_first:  # slot d - start[e] of expert e -> its full or partial tile
+                                sl = d - start[e_]
+                                d = T.if_then_else(sl < cnt[e_] // block_M * block_M, d,
+                                                   pstart[e_] + sl - cnt[e_] // block_M * block_M)
                             dest[t * c + i] = d
                             row_src[d] = (t * c + i) // div
                         if t * c + i < n and expert_ids[t * c + i] < 0:
@@ -257,9 +288,16 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
             else:
                 for j in T.Parallel(n):
                     if expert_ids[j] >= 0:
-                        slot = T.atomic_add(fill[expert_ids[j]], 1, return_prev=True)
-                        dest[j] = start[expert_ids[j]] + slot
-                        row_src[start[expert_ids[j]] + slot] = j // div
+                        e_ = expert_ids[j]
+                        slot = T.atomic_add(fill[e_], 1, return_prev=True)
+                        if full_first:
+                            d = T.if_then_else(slot < cnt[e_] // block_M * block_M, start[e_] + slot,
+                                               pstart[e_] + slot - cnt[e_] // block_M * block_M)
+                            dest[j] = d
+                            row_src[d] = j // div
+                        else:
+                            dest[j] = start[e_] + slot
+                            row_src[start[e_] + slot] = j // div
                     if expert_ids[j] < 0:
                         dest[j] = -1
 
