@@ -1,0 +1,54 @@
+"""Expert GEMMs of the bench MoE layer in isolation: balanced routing (every expert exactly
+tokens*topk/E rows: whole tiles only, no tail) vs random routing, against the plain GEMM with the
+same FLOPs.  Separates "the expert GEMM kernel is slow" from "the routing tail is slow".
+
+    python scripts/moe_gemm_probe.py
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "examples", "gemm")]
+import torch  # noqa: E402
+
+from tilelang.ops import moe as K  # noqa: E402
+from tilelang.profiler import do_bench  # noqa: E402
+
+T_, H, F, E, TOP = 2048, 4096, 2048, 8, 2
+BM = 256
+dev = "cuda"
+torch.manual_seed(0)
+x = torch.randn(T_, H, device=dev, dtype=torch.bfloat16)
+w1 = (torch.randn(E, 2 * F, H, device=dev) * 0.02).to(torch.bfloat16)
+w2 = (torch.randn(E, H, F, device=dev) * 0.02).to(torch.bfloat16)
+n = T_ * TOP
+
+
+def run(ids, tag, **kw):
+    max_rows = K.max_padded_rows(K._bucket(n), E, BM)
+    dest, row_src, te, counts, trows = K.dispatch_plan(ids, E, BM, max_rows, TOP)
+    act = torch.empty(max_rows, F, dtype=x.dtype, device=dev)
+    y = torch.empty(max_rows, H, dtype=x.dtype, device=dev)
+    k1 = K.expert_gemm_sk_kernel(max_rows, H, 2 * F, E, "bfloat16", "hip", BM, n_src=T_, swiglu=True, **kw)
+    k2 = K.expert_gemm_sk_kernel(max_rows, F, H, E, "bfloat16", "hip", BM, **kw)
+    t1 = do_bench(lambda: k1(x, w1, te, row_src, trows, act), warmup=10, rep=50)
+    t2 = do_bench(lambda: k2(act, w2, te, row_src, trows, y), warmup=10, rep=50)
+    f1, f2 = 2.0 * n * H * 2 * F, 2.0 * n * F * H
+    nt = int((te >= 0).sum())
+    print(f"{tag} {kw}: tiles {nt}  GEMM1 {t1 * 1e3:.1f} us {f1 / t1 * 1e-9:.0f} TF  GEMM2 {t2 * 1e3:.1f} us "
+          f"{f2 / t2 * 1e-9:.0f} TF", flush=True)
+
+
+bal = torch.arange(n, device=dev, dtype=torch.int32) % E  # exactly n/E rows per expert
+rnd = torch.randint(0, E, (n, ), device=dev, dtype=torch.int32)
+for kw in ({}, dict(tail_split=2), dict(block_K=128, num_stages=2), dict(phased=True)):
+    try:
+        run(bal, "balanced", **kw)
+        run(rnd, "random  ", **kw)
+    except Exception as e:  # noqa: BLE001
+        print(kw, "failed", str(e)[:200], flush=True)
+from example_gemm import matmul  # noqa: E402
+g = matmul(4096, 4096, 4096, 256, 256, 64, 512, 2, staged_epilogue=True)
+a, b = torch.randn(4096, 4096, device=dev).half(), torch.randn(4096, 4096, device=dev).half()
+t = do_bench(lambda: g(a, b), warmup=10, rep=50)
+print(f"plain GEMM 4096^3 (= GEMM1 FLOPs): {t * 1e3:.1f} us {2 * 4096**3 / t * 1e-9:.0f} TF")

@@ -405,8 +405,12 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
 def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target: str, block_M: int = 256,
                           block_N: int = 256, block_K: int = 64, num_stages: int = 2, threads: int = 512,
                           n_src: Optional[int] = None, swiglu: bool = False, n_cu: int = 256, tail_split: int = 4,
-                          phased: bool = False, skip_padding: bool = True):
+                          phased: bool = False, skip_padding: bool = True, partial_first: bool = False):
     """Tail-balanced variant of ``expert_gemm_kernel`` (same arguments and output).
+
+    ``partial_first``: with the full-tiles-first dispatch layout, rotate the unit order so the
+    (nearly-empty) partial tiles run in the whole-tile rounds and full tiles form the split tail:
+    the workgroups that drew a partial tile finish early and start on the tail at once.
 
     The (row tile x N tile) units are a data-dependent count U (the routing decides how many
     row tiles are real), and a plain grid runs ceil(U / n_cu) rounds of whole tiles: U = 320 on
@@ -462,20 +466,26 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
             Wt_s = T.alloc_shared((bn_t, block_K), dtype)
             Ct_l = T.alloc_fragment((block_M, bn_t), accum)
             nt = T.alloc_var("int32")
+            nfull = T.alloc_var("int32")
             nt = 0
+            nfull = 0
             for t in T.serial(n_tiles):
                 if tile_expert[t] >= 0:
                     nt = t + 1
+                    if tile_rows[t] == block_M:
+                        nfull = t + 1
             units = nt * n_by
             full = units - units % n_cu
+            # unit u -> tile (u + shift) % units: partial tiles first when asked
+            shift = (nt - nfull) * n_by if partial_first else 0
             for it in T.serial(full // n_cu):  # whole tiles
-                u = pid + it * n_cu
+                u = (pid + it * n_cu + shift) % units
                 tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, u // n_by, tile_expert[u // n_by],
                      (u % n_by) * block_N, block_N)
             for it in T.serial(T.ceildiv((units - full) * tail_split, n_cu)):  # narrow tail tiles
                 q = pid + it * n_cu
                 if q < (units - full) * tail_split:
-                    u = full + q // tail_split
+                    u = (full + q // tail_split + shift) % units
                     tile(A, W, row_src, tile_rows, C, A_s, Wt_s, Ct_l, u // n_by, tile_expert[u // n_by],
                          (u % n_by) * block_N + (q % tail_split) * bn_t, bn_t)
 
@@ -614,14 +624,16 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
         # tail-balanced grid: whole tiles for the leading rounds, narrow tiles for the trailing partial round
         skc = {k: v for k, v in cfg.items() if k in ("block_N", "block_K", "num_stages", "threads", "tail_split",
                                                       "phased", "skip_padding")}
+        # partial_first for the down projection: measured neutral (profiles/r3/s3/moe/), off
+        pf2 = cfg.get("partial_first2", False)
         k1 = expert_gemm_sk_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, swiglu=True, n_cu=n_cu,
                                    **skc)
         k1(src_rows.contiguous(), w1, te, row_src, trows, act)
-        k2 = expert_gemm_sk_kernel(max_rows, F, H, E, tgt, target, block_M, n_cu=n_cu, **skc)
+        k2 = expert_gemm_sk_kernel(max_rows, F, H, E, tgt, target, block_M, n_cu=n_cu, partial_first=pf2, **skc)
         y = torch.empty(max_rows, H, dtype=src_rows.dtype, device=dev)
         k2(act, w2, te, row_src, trows, y)
         return y, dest
-    for key in ("tail_split", "phased"):  # options of the tail-balanced grid only
+    for key in ("tail_split", "phased", "partial_first2"):  # options of the tail-balanced grid only
         cfg.pop(key, None)
     if w1_interleaved:
         # gate/up rows interleaved: the activation is the first GEMM's epilogue
