@@ -31,8 +31,9 @@ def run(ids, tag, **kw):
     y = torch.empty(max_rows, H, dtype=x.dtype, device=dev)
     k1 = K.expert_gemm_sk_kernel(max_rows, H, 2 * F, E, "bfloat16", "hip", BM, n_src=T_, swiglu=True, **kw)
     k2 = K.expert_gemm_sk_kernel(max_rows, F, H, E, "bfloat16", "hip", BM, **kw)
-    t1 = do_bench(lambda: k1(x, w1, te, row_src, trows, act), warmup=10, rep=50)
-    t2 = do_bench(lambda: k2(act, w2, te, row_src, trows, y), warmup=10, rep=50)
+    ws = K._tail_workspace(dev, 256, kw["tail_ksplit"], BM, 256) if kw.get("tail_ksplit") else ()
+    t1 = do_bench(lambda: k1(x, w1, te, row_src, trows, act, *ws), warmup=10, rep=50)
+    t2 = do_bench(lambda: k2(act, w2, te, row_src, trows, y, *ws), warmup=10, rep=50)
     f1, f2 = 2.0 * n * H * 2 * F, 2.0 * n * F * H
     nt = int((te >= 0).sum())
     print(f"{tag} {kw}: tiles {nt}  GEMM1 {t1 * 1e3:.1f} us {f1 / t1 * 1e-9:.0f} TF  GEMM2 {t2 * 1e3:.1f} us "
@@ -41,7 +42,7 @@ def run(ids, tag, **kw):
 
 bal = torch.arange(n, device=dev, dtype=torch.int32) % E  # exactly n/E rows per expert
 rnd = torch.randint(0, E, (n, ), device=dev, dtype=torch.int32)
-for kw in ({}, dict(tail_split=2), dict(block_K=128, num_stages=2), dict(phased=True)):
+for kw in ({}, dict(tail_ksplit=2), dict(tail_ksplit=4), dict(tail_ksplit=8), {}):
     try:
         run(bal, "balanced", **kw)
         run(rnd, "random  ", **kw)

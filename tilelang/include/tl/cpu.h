@@ -135,6 +135,10 @@ template <typename T, int N> inline void load_vec(T (&vals)[N], const T* src) { 
 template <int B> inline void copy_bytes(void* dst, const void* src) { memcpy(dst, src, B); }
 
 inline void sync_threads() {}
+// blocks run one after another on the CPU target: memory fences are compiler barriers only
+inline void fence_workgroup() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
+inline void fence_agent() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
+inline void fence_system() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
 inline void sync_warp() {}
 // T.sync_grid on the CPU target: kernels that use it run every block as a host thread
 // (codegen/hip.py) meeting at this generation-counting barrier.

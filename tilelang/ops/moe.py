@@ -405,8 +405,18 @@ def expert_gemm_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target
 def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, target: str, block_M: int = 256,
                           block_N: int = 256, block_K: int = 64, num_stages: int = 2, threads: int = 512,
                           n_src: Optional[int] = None, swiglu: bool = False, n_cu: int = 256, tail_split: int = 4,
-                          phased: bool = False, skip_padding: bool = True, partial_first: bool = False):
+                          phased: bool = False, skip_padding: bool = True, partial_first: bool = False,
+                          tail_ksplit: int = 0):
     """Tail-balanced variant of ``expert_gemm_kernel`` (same arguments and output).
+
+    ``tail_ksplit`` = S > 0: the trailing units run as S K-chunks each (full tile width) instead of
+    narrow tiles: with the full-tiles-first layout the tail is the partial row tiles, whose cost
+    is the latency chain of their K loop, not their FLOPs (balanced routing 120-137 us vs random
+    173 us for the bench layer's GEMM1, scripts/moe_gemm_probe.py).  Every chunk writes its fp32
+    partial (valid rows only) to a workspace slot, publishes it (release fence + counter); the
+    last of the S chunks to arrive adds the others' partials and runs the epilogue, then resets
+    the counter -- one kernel, no host sync, no separate reduction pass.  Extra arguments:
+    ``WS [n_cu, S, block_M, block_N] fp32`` and ``Cnt [n_cu] int32`` (zero before the first call).
 
     ``partial_first``: with the full-tiles-first dispatch layout, rotate the unit order so the
     (nearly-empty) partial tiles run in the whole-tile rounds and full tiles form the split tail:
@@ -425,7 +435,7 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
     n_by = (N + block_N - 1) // block_N
     nk = (K + block_K - 1) // block_K
     bn_t = block_N // tail_split
-    assert bn_t % 64 == 0 or bn_t == 32, "tail tiles must stay MFMA / SwiGLU-group aligned"
+    assert tail_ksplit or bn_t % 64 == 0 or bn_t == 32, "tail tiles must stay MFMA / SwiGLU-group aligned"
     accum = "float32"
     a_rows = n_src if n_src is not None else max_rows
     n_out = N // 2 if swiglu else N
@@ -454,6 +464,101 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
                         dtype, C_l[i, j] / (1.0 + T.exp(-C_l[i, j])) * C_l[i, j + 2])
         else:
             T.copy(C_l, C[bx * block_M, col0])
+
+    S_ = max(1, tail_ksplit)
+    nks = nk // S_
+    assert tail_ksplit == 0 or nk % S_ == 0, "tail_ksplit must divide the K steps"
+
+    @T.macro
+    def kchunk(A, W, row_src, A_s, W_s, C_l, bx, e, col0, nrows, kbase):
+        T.clear(C_l)
+        for k in T.Pipelined(nks, num_stages=num_stages):
+            if n_src is not None:
+                T.gather_rows(A[:, (kbase + k) * block_K:(kbase + k + 1) * block_K],
+                              row_src[bx * block_M:(bx + 1) * block_M], A_s, row_dim=0)
+            else:
+                T.copy(A[bx * block_M, (kbase + k) * block_K], A_s)
+            T.copy(W[e, col0, (kbase + k) * block_K], W_s)
+            T.gemm(A_s, W_s, C_l, transpose_B=True, valid_m=nrows if skip_padding else None)
+
+    @T.macro
+    def epilogue(C, C_l, bx, col0, bn):
+        if swiglu:
+            for i, j in T.Parallel(block_M, bn):
+                if j % 4 < 2:
+                    C[bx * block_M + i, col0 // 2 + (j // 4) * 2 + j % 4] = T.Cast(
+                        dtype, C_l[i, j] / (1.0 + T.exp(-C_l[i, j])) * C_l[i, j + 2])
+        else:
+            T.copy(C_l, C[bx * block_M, col0])
+
+    @T.macro
+    def body(A, W, tile_expert, row_src, tile_rows, C, WS, Cnt, pid):
+        A_s = T.alloc_shared((block_M, block_K), dtype)
+        W_s = T.alloc_shared((block_N, block_K), dtype)
+        C_l = T.alloc_fragment((block_M, block_N), accum)
+        nt = T.alloc_var("int32")
+        nfull = T.alloc_var("int32")
+        nt = 0
+        nfull = 0
+        for t in T.serial(n_tiles):
+            if tile_expert[t] >= 0:
+                nt = t + 1
+                if tile_rows[t] == block_M:
+                    nfull = t + 1
+        units = nt * n_by
+        full = units - units % n_cu
+        shift = (nt - nfull) * n_by if partial_first else 0
+        for it in T.serial(full // n_cu):  # whole tiles
+            u = (pid + it * n_cu + shift) % units
+            tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, u // n_by, tile_expert[u // n_by],
+                 (u % n_by) * block_N, block_N)
+        prev = T.alloc_shared((1, ), "int32")
+        for it in T.serial(T.ceildiv((units - full) * S_, n_cu)):  # K-chunks of the tail units
+            q = pid + it * n_cu
+            if q < (units - full) * S_:
+                slot = T.max(T.min(q // S_, n_cu - 1), 0)
+                kc = q % S_
+                u = (full + q // S_ + shift) % units
+                bx = T.min(u // n_by, n_tiles - 1)
+                e = T.min(T.max(tile_expert[bx], 0), E - 1)
+                col0 = (u % n_by) * block_N
+                nrows = T.alloc_var("int32")
+                nrows = tile_rows[bx]
+                kchunk(A, W, row_src, A_s, W_s, C_l, bx, e, col0, nrows, kc * nks)
+                for i, j in T.Parallel(block_M, block_N):  # publish the partial (valid rows)
+                    if i < nrows:
+                        WS[slot, kc, i, j] = C_l[i, j]
+                T.memory_fence()
+                T.sync_threads()
+                if T.get_thread_binding() == 0:
+                    prev[0] = T.atomic_add(Cnt[slot], 1, return_prev=True)
+                T.sync_threads()
+                if prev[0] == S_ - 1:  # last chunk: sum the others' partials, run the epilogue
+                    T.memory_fence()
+                    for kc2 in T.serial(S_):
+                        if kc2 != kc:
+                            for i, j in T.Parallel(block_M, block_N):
+                                if i < nrows:
+                                    C_l[i, j] += WS[slot, kc2, i, j]
+                    epilogue(C, C_l, bx, col0, block_N)
+                    if T.get_thread_binding() == 0:
+                        Cnt[slot] = 0
+                T.sync_threads()
+
+    if tail_ksplit:
+
+        @T.prim_func
+        def moe_expert_gemm_tbk(A: T.Tensor((a_rows, K), dtype), W: T.Tensor((E, N, K), dtype),
+                                tile_expert: T.Tensor((n_tiles,), "int32"), row_src: T.Tensor((max_rows,), "int32"),
+                                tile_rows: T.Tensor((n_tiles,), "int32"), C: T.Tensor((max_rows, n_out), dtype),
+                                WS: T.Tensor((n_cu, S_, block_M, block_N), accum), Cnt: T.Tensor((n_cu,), "int32")):
+            with T.Kernel(n_cu, threads=threads) as pid:
+                body(A, W, tile_expert, row_src, tile_rows, C, WS, Cnt, pid)
+
+        cfg = {"tl.gemm_phased": bool(phased)}
+        if swiglu:
+            cfg[tilelang.PassConfigKey.TL_ENABLE_FAST_MATH] = True
+        return tilelang.compile(moe_expert_gemm_tbk, out_idx=None, target=target, pass_configs=cfg)
 
     @T.prim_func
     def moe_expert_gemm_tb(A: T.Tensor((a_rows, K), dtype), W: T.Tensor((E, N, K), dtype),
@@ -597,6 +702,19 @@ def pack_by_expert(expert_ids: torch.Tensor, E: int, block_M: int, max_rows: int
     return dest.long(), te, counts.long()
 
 
+_TAIL_WS = {}
+
+
+def _tail_workspace(dev, n_cu, S, block_M, block_N):
+    """fp32 partial-sum slots + arrival counters of the K-split tail (expert_gemm_sk_kernel);
+    the counters are reset by the last arriver, so one zeroed allocation serves every call."""
+    key = (str(dev), n_cu, S, block_M, block_N)
+    if key not in _TAIL_WS:
+        _TAIL_WS[key] = (torch.empty(n_cu, S, block_M, block_N, dtype=torch.float32, device=dev),
+                         torch.zeros(n_cu, dtype=torch.int32, device=dev))
+    return _TAIL_WS[key]
+
+
 def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int, w1: torch.Tensor,
                       w2: torch.Tensor, block_M: int = 128, reduce_mesh: Optional[str] = None,
                       cfg: Optional[dict] = None, w1_interleaved: bool = False):
@@ -623,15 +741,18 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
     if sk and reduce_mesh is None and w1_interleaved:
         # tail-balanced grid: whole tiles for the leading rounds, narrow tiles for the trailing partial round
         skc = {k: v for k, v in cfg.items() if k in ("block_N", "block_K", "num_stages", "threads", "tail_split",
-                                                      "phased", "skip_padding")}
+                                                      "phased", "skip_padding", "tail_ksplit")}
         # partial_first for the down projection: measured neutral (profiles/r3/s3/moe/), off
         pf2 = cfg.get("partial_first2", False)
+        ws = ()
+        if skc.get("tail_ksplit"):
+            ws = _tail_workspace(dev, n_cu, skc["tail_ksplit"], block_M, skc.get("block_N", 256))
         k1 = expert_gemm_sk_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, swiglu=True, n_cu=n_cu,
                                    **skc)
-        k1(src_rows.contiguous(), w1, te, row_src, trows, act)
+        k1(src_rows.contiguous(), w1, te, row_src, trows, act, *ws)
         k2 = expert_gemm_sk_kernel(max_rows, F, H, E, tgt, target, block_M, n_cu=n_cu, partial_first=pf2, **skc)
         y = torch.empty(max_rows, H, dtype=src_rows.dtype, device=dev)
-        k2(act, w2, te, row_src, trows, y)
+        k2(act, w2, te, row_src, trows, y, *ws)
         return y, dest
     for key in ("tail_split", "phased", "partial_first2"):  # options of the tail-balanced grid only
         cfg.pop(key, None)
