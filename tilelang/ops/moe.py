@@ -410,9 +410,10 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
     """Tail-balanced variant of ``expert_gemm_kernel`` (same arguments and output).
 
     ``tail_ksplit`` = S > 0: the trailing units run as S K-chunks each (full tile width) instead of
-    narrow tiles: with the full-tiles-first layout the tail is the partial row tiles, whose cost
-    is the latency chain of their K loop, not their FLOPs (balanced routing 120-137 us vs random
-    173 us for the bench layer's GEMM1, scripts/moe_gemm_probe.py).  Every chunk writes its fp32
+    narrow tiles.  Measured SLOWER on the bench layer (GEMM1 173 -> 255 / 357 / 572 us for S = 2 /
+    4 / 8, profiles/r3/s3/moe/expert_gemm_probe.log): the partial tiles of the tail are often
+    nearly full (an expert with 500 rows has one full tile and a 244-row partial), so the fp32
+    partials are large and their traffic grows with S.  Kept as an option, off by default.  Every chunk writes its fp32
     partial (valid rows only) to a workspace slot, publishes it (release fence + counter); the
     last of the S chunks to arrive adds the others' partials and runs the epilogue, then resets
     the counter -- one kernel, no host sync, no separate reduction pass.  Extra arguments:
