@@ -98,20 +98,26 @@ def quant_act_mxfp8(M, K, block_M=64, threads=256, dtype="bfloat16"):
 
 
 @tilelang.jit(out_idx=[-1])
-def mxfp4_gemv(M, N, K, block_N=None, threads=256, dtype="bfloat16"):
+def mxfp4_gemv(M, N, K, block_N=None, threads=256, dtype="bfloat16", row_group=None):
     """Decode-sized (M <= 8) bf16 x MXFP4: a pure weight stream (include/tl/gemv.h): 16-byte
     non-temporal weight loads, v_cvt_scalef32_pk_f32_fp4 (two codes per instruction, the e8m0
-    scale folded in), FMAs against x held in registers, one block reduction per BLOCK_N rows."""
+    scale folded in), FMAs against x held in registers, one block reduction per ``row_group``
+    rows.  ``block_N`` rows per block (x is re-read once per row group from L1/L2: 32 rows per
+    block keep the x traffic a fraction of the weight bytes for every M)."""
     assert M <= 8 and K % 32 == 0 and dtype == "bfloat16"
+    if row_group is None:  # ~16 accumulators per thread, a power of two
+        row_group = max(2, 1 << ((16 // M).bit_length() - 1))
     if block_N is None:
-        block_N = max(2, 16 // M)
+        block_N = max(row_group, 32 if M > 1 else 16)
+    assert block_N % row_group == 0
 
     @T.prim_func
     def main(A: T.Tensor((M, K), dtype), Bq: T.Tensor((N, K // 2), "uint8"), S: T.Tensor((N, K // 32), "uint8"),
              C: T.Tensor((M, N), dtype)):
         with T.Kernel(T.ceildiv(N, block_N), threads=threads) as bx:
-            red = T.alloc_shared((threads // 64, block_N * M), "float32")
-            T.evaluate(T.call_extern("handle", f"tl::mxfp4_gemv<{M}, {block_N}, {threads}>", T.address_of(A[0, 0]),
+            red = T.alloc_shared((threads // 64, row_group * M), "float32")
+            T.evaluate(T.call_extern("handle", f"tl::mxfp4_gemv<{M}, {block_N}, {threads}, {row_group}>",
+                                     T.address_of(A[0, 0]),
                                      T.address_of(Bq[0, 0]), T.address_of(S[0, 0]), T.address_of(C[0, 0]), N, K,
                                      bx * block_N, T.address_of(red[0, 0])))
 

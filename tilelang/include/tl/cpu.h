@@ -233,7 +233,7 @@ template <int FMT> inline float mx_elem(const uint8_t* row, int k) {
 inline float e8m0(uint8_t s) { return s == 255 ? NAN : std::ldexp(1.0f, (int)s - 127); }
 
 // tl/gemv.h mxfp4_gemv on the CPU target: the block's BLOCK_N rows, serially
-template <int M, int BLOCK_N, int THREADS>
+template <int M, int BLOCK_N, int THREADS, int RG = BLOCK_N>
 inline void mxfp4_gemv(const bfloat16_t* X, const uint8_t* Bq, const uint8_t* S, bfloat16_t* Y, int N, int K, int n0,
                        float*) {
   for (int n = n0; n < n0 + BLOCK_N && n < N; ++n)
