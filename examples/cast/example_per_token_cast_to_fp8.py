@@ -34,12 +34,10 @@ def per_token_cast_to_fp8(M, N, blk_m=8, group_size=128, threads=128, groups=1, 
             for i, g, j in T.Parallel(blk_m, groups, group_size):
                 y[i, g, j] = X[bx * blk_m + i, by * gw + g * group_size + j]
             T.reduce_absmax(y, amax, dim=2)
-            inv = T.alloc_fragment((blk_m, groups), dtype)
             for i, g in T.Parallel(blk_m, groups):
                 scale[i, g] = T.max(amax[i, g], 1e-4) / FP8_MAX
-                inv[i, g] = FP8_MAX / T.max(amax[i, g], 1e-4)  # one divide per group, not per element
             for i, g, j in T.Parallel(blk_m, groups, group_size):
-                q[i, g, j] = T.clamp(y[i, g, j] * inv[i, g], -FP8_MAX, FP8_MAX)
+                q[i, g, j] = T.clamp(y[i, g, j] / scale[i, g], -FP8_MAX, FP8_MAX)
             for i, g in T.Parallel(blk_m, groups):
                 X_amax[bx * blk_m + i, by * groups + g] = scale[i, g]
             for i, g, j in T.Parallel(blk_m, groups, group_size):

@@ -105,10 +105,13 @@ def mxfp4_gemv(M, N, K, block_N=None, threads=256, dtype="bfloat16", row_group=N
     rows.  ``block_N`` rows per block (x is re-read once per row group from L1/L2: 32 rows per
     block keep the x traffic a fraction of the weight bytes for every M)."""
     assert M <= 8 and K % 32 == 0 and dtype == "bfloat16"
-    if row_group is None:  # ~16 accumulators per thread, a power of two
-        row_group = max(2, 1 << ((16 // M).bit_length() - 1))
     if block_N is None:
-        block_N = max(row_group, 32 if M > 1 else 16)
+        block_N = max(2, 16 // M)
+    if row_group is None:
+        # one group per block: more, smaller blocks keep more weight bytes in flight; 32-row blocks
+        # in row groups cut the x re-reads but halved the M = 4 / 8 rate (1436 -> 699 GB/s at M = 4,
+        # profiles/r3/s3/lowp/gemv_rowgroup_ab.log)
+        row_group = block_N
     assert block_N % row_group == 0
 
     @T.prim_func
