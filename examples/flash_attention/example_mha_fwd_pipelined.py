@@ -25,14 +25,19 @@ from example_mha_fwd import FAST_MATH, ref_program
 @tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
 def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=256, block_N=64,
                         threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
-                        young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd", mfma="16x16"):
+                        young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd", mfma="16x16",
+                        sum_mfma=False):
     """``young_prio``: the second-dispatched half of the waves runs at issue priority 1 (one
     ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4).
     ``seq_kv`` (default ``seq_len``): key/value length; with ``is_causal`` the mask is aligned
     bottom-right (query i sees keys up to i + seq_kv - seq_len).  ``layout``: "bshd" or "bhsd"
     for Q/K/V/O (reference example_mha_fwd_bhsd.py).  ``mfma``: "16x16" (16x16x32) or "32x32"
     (32x32x16 tiles for both GEMMs: one query row per lane, P fed to P V in the accumulator's
-    k order, and 24 of each MFMA's 32 cycles free for the softmax VALU stream)."""
+    k order, and 24 of each MFMA's 32 cycles free for the softmax VALU stream).
+    ``sum_mfma``: the softmax row sums come from the matrix cores: P times a ones tile (16 or 32
+    columns) accumulates next to O, rescaled with it, so the per-tile VALU adds, their cross-lane
+    reduction and the running-sum update leave the VALU stream (the loop is VALU-issue bound:
+    an MFMA holds the SIMD's vector issue for half its cycles)."""
     scale = (1.0 / dim)**0.5 * 1.44269504
     head_kv = heads // groups
     seq_kv = seq_len if seq_kv is None else seq_kv
@@ -45,9 +50,10 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     kv_shape = [batch, head_kv, seq_kv, dim] if bhsd else [batch, seq_kv, head_kv, dim]
     accum_dtype = "float"
     n_qt = (seq_len + block_M - 1) // block_M
-    n_softmax = 8 if lazy_rescale else 7  # statements of the softmax group below
+    n_softmax = (8 if lazy_rescale else 7) - (2 if sum_mfma else 0)  # statements of the softmax group
     group = [[0], [1, 2], list(range(3, 3 + n_softmax))]
-    group += [[3 + n_softmax], [4 + n_softmax], [5 + n_softmax]]
+    group += [[3 + n_softmax], [4 + n_softmax], [5 + n_softmax] + ([6 + n_softmax] if sum_mfma else [])]
+    n_ones = 16 if mfma == "16x16" else 32
 
     @T.prim_func
     def main(
@@ -75,6 +81,11 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
             scores_sum = T.alloc_fragment([block_M], accum_dtype)
             logsum = T.alloc_fragment([block_M], accum_dtype)
             rescale = T.alloc_var("int32")
+            if sum_mfma:
+                ones_s = T.alloc_shared([block_N, n_ones], dtype)
+                acc_l = T.alloc_fragment([block_M, n_ones], accum_dtype)
+                T.fill(ones_s, 1)
+                T.fill(acc_l, 0)
 
             if bhsd:
                 T.copy(Q[bz, by, bx * block_M:(bx + 1) * block_M, :], Q_s)
@@ -131,20 +142,28 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                         scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
                 for i, j in T.Parallel(block_M, block_N):
                     acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
-                T.reduce_sum(acc_s, scores_sum, dim=1)
-                for i in T.Parallel(block_M):
-                    logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
+                if not sum_mfma:
+                    T.reduce_sum(acc_s, scores_sum, dim=1)
+                    for i in T.Parallel(block_M):
+                        logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
                 T.copy(acc_s, acc_s_cast)
                 # rescale group (one tile behind)
                 if rescale != 0:
                     for i, j in T.Parallel(block_M, dim):
                         acc_o[i, j] *= scores_scale[i]
+                    if sum_mfma:
+                        for i, j in T.Parallel(block_M, n_ones):
+                            acc_l[i, j] *= scores_scale[i]
                 # V tile (producer) and O += P V (one tile behind)
                 if bhsd:
                     T.copy(V[bz, by // groups, k * block_N:(k + 1) * block_N, :], V_shared)
                 else:
                     T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
                 T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
+                if sum_mfma:
+                    T.gemm(acc_s_cast, ones_s, acc_l, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
+            if sum_mfma:  # every column of acc_l holds the row sum: spread it in the row layout
+                T.reduce_max(acc_l, logsum, dim=1)
             for i, j in T.Parallel(block_M, dim):
                 acc_o[i, j] /= logsum[i]
             if staged_epilogue:  # O tile through row-padded LDS: 16-byte row-contiguous stores

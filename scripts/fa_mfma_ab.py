@@ -22,6 +22,8 @@ VARIANTS = {
     "m32_n64_s2": dict(block_N=64, num_stages=2, mfma="32x32"),
     "m32_n64_s3": dict(block_N=64, num_stages=3, mfma="32x32"),
     "m32_n128_s2": dict(block_N=128, num_stages=2, mfma="32x32"),
+    "m16_sum": dict(block_N=64, num_stages=2, mfma="16x16", sum_mfma=True),
+    "m32_sum": dict(block_N=64, num_stages=2, mfma="32x32", sum_mfma=True),
 }
 
 
@@ -42,7 +44,7 @@ def main():
     for name in a.variants:
         cfg = VARIANTS[name]
         kk = fa(b, h, s, d, a.causal, 1, 256, cfg["block_N"], 512, cfg["num_stages"], "bfloat16", True, True,
-                mfma=cfg["mfma"])
+                mfma=cfg["mfma"], sum_mfma=cfg.get("sum_mfma", False))
         err = (kk(q, k, v).float() - ref).abs().max().item()
         print(f"{name}: max err {err:.4f}{'  WRONG' if err > 0.05 else ''}", flush=True)
         if err <= 0.05:

@@ -60,9 +60,10 @@ def test_bad_group_rejected():
 
 
 @pytest.mark.parametrize("causal", [False, True])
-@pytest.mark.parametrize("lazy", [False, True])
-def test_fa_staged_cpu(causal, lazy):
-    f = flashattn_pipelined.get_tir(1, 2, 192, 64, causal, 1, 64, 32, 128, 2, "bfloat16", lazy, False)
+@pytest.mark.parametrize("lazy,sum_mfma", [(False, False), (True, False), (True, True)])
+def test_fa_staged_cpu(causal, lazy, sum_mfma):
+    f = flashattn_pipelined.get_tir(1, 2, 192, 64, causal, 1, 64, 32, 128, 2, "bfloat16", lazy, False,
+                                    sum_mfma=sum_mfma)
     k = tilelang.compile(f, out_idx=[3], target="cpu")
     q = torch.randn(1, 192, 2, 64, dtype=torch.bfloat16)
     kk, v = torch.randn_like(q), torch.randn_like(q)
@@ -88,10 +89,10 @@ def test_fa_mfma32_hip_source():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mfma", ["16x16", "32x32"])
+@pytest.mark.parametrize("mfma,sum_mfma", [("16x16", False), ("32x32", False), ("16x16", True), ("32x32", True)])
 @pytest.mark.parametrize("causal", [False, True])
-def test_fa_staged_gpu(causal, mfma):
-    k = flashattn_pipelined(2, 4, 1024, 128, causal, 2, 256, 64, 512, 2, mfma=mfma)
+def test_fa_staged_gpu(causal, mfma, sum_mfma):
+    k = flashattn_pipelined(2, 4, 1024, 128, causal, 2, 256, 64, 512, 2, mfma=mfma, sum_mfma=sum_mfma)
     q = torch.randn(2, 1024, 4, 128, device="cuda", dtype=torch.bfloat16)
     kk = torch.randn(2, 1024, 2, 128, device="cuda", dtype=torch.bfloat16)
     v = torch.randn_like(kk)
