@@ -82,8 +82,23 @@ def _combine(kind, a, b):
 
 
 def _tree_combine(kind, xs):
-    """Balanced reduction tree: log-depth dependency chains (ILP) and shallow expressions."""
+    """Balanced reduction tree: log-depth dependency chains (ILP) and shallow expressions.
+    max / min trees are ternary, max(max(a, b), c) per node, which the backend emits as one
+    v_max3 / v_min3: (n-1)/2 instructions instead of n-1 on the VALU (FA's row max)."""
     xs = list(xs)
+    if kind in ("max", "absmax", "min"):
+        while len(xs) > 1:
+            nxt = []
+            i = 0
+            while i < len(xs):
+                grp = xs[i:i + 3]
+                acc = grp[0]
+                for g in grp[1:]:
+                    acc = _combine(kind, acc, g)
+                nxt.append(acc)
+                i += 3
+            xs = nxt
+        return xs[0]
     while len(xs) > 1:
         nxt = [_combine(kind, xs[i], xs[i + 1]) for i in range(0, len(xs) - 1, 2)]
         if len(xs) % 2:
