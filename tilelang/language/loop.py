@@ -123,6 +123,11 @@ def Pipelined(start, stop=None, num_stages: int = 0, order=None, stage=None, syn
 
     On gfx950 the global->LDS copies become ``global_load_lds_dwordx4`` DMA issued
     ``num_stages-1`` iterations ahead, with counted ``s_waitcnt vmcnt`` waits.
+
+    ``order`` / ``stage`` / ``group``: user schedule (transform/stage_schedule.py).  ``sync`` is
+    accepted and recorded but has no effect, exactly as in the reference (``src/ir.cc:105`` sets
+    ``tl_pipeline_sync`` and no pass reads it); LDS hazards between the scheduled statements get
+    their barriers from the thread-sync pass, which proves them per access.
     """
     ann = {"num_stages": int(num_stages)}
     if order is not None:
