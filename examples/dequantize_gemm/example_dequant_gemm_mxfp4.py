@@ -105,8 +105,8 @@ def mxfp4_gemv(M, N, K, block_N=None, threads=256, dtype="bfloat16", row_group=N
     rows.  ``block_N`` rows per block (x is re-read once per row group from L1/L2: 32 rows per
     block keep the x traffic a fraction of the weight bytes for every M)."""
     assert M <= 8 and K % 32 == 0 and dtype == "bfloat16"
-    if block_N is None:
-        block_N = max(2, 16 // M)
+    if block_N is None:  # scripts/sweep_gemv_fp4.py (profiles/r3/s3/lowp/sweep_gemv_fp4.log): 4-row blocks
+        block_N = 4 if M <= 4 else 2  # M=1 16384^2: 4.69 TB/s of weights (16-row blocks 4.10)
     if row_group is None:
         # one group per block: more, smaller blocks keep more weight bytes in flight; 32-row blocks
         # in row groups cut the x re-reads but halved the M = 4 / 8 rate (1436 -> 699 GB/s at M = 4,
