@@ -42,7 +42,7 @@ def run(ids, tag, **kw):
 
 bal = torch.arange(n, device=dev, dtype=torch.int32) % E  # exactly n/E rows per expert
 rnd = torch.randint(0, E, (n, ), device=dev, dtype=torch.int32)
-for kw in ({}, dict(tail_ksplit=2), dict(tail_ksplit=4), dict(tail_ksplit=8), {}):
+for kw in ({}, dict(tail_stages=2), {}):
     try:
         run(bal, "balanced", **kw)
         run(rnd, "random  ", **kw)

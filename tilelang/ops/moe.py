@@ -236,10 +236,21 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                     for e in T.serial(E):  # full tiles of every expert
                         start[e] = acc
                         acc = acc + cnt[e] // block_M * block_M
-                    for e in T.serial(E):  # then one partial tile per expert with a remainder
-                        pstart[e] = acc
-                        acc = acc + T.if_then_else(cnt[e] % block_M > 0, block_M, 0)
-                    start[E] = acc + z
+                    # then one partial tile per expert with a remainder, fullest first: the
+                    # tail-balanced GEMM splits the LAST units, which are then the lightest
+                    npart = T.alloc_var("int32")
+                    npart = 0
+                    for e in T.serial(E):
+                        rk = T.alloc_var("int32")
+                        rk = 0
+                        for e2 in T.serial(E):
+                            if cnt[e2] % block_M > cnt[e] % block_M or (
+                                    cnt[e2] % block_M == cnt[e] % block_M and e2 < e):
+                                rk = rk + 1
+                        pstart[e] = acc + rk * block_M
+                        if cnt[e] % block_M > 0:
+                            npart = npart + 1
+                    start[E] = acc + npart * block_M + z
             else:
                 for z in T.Parallel(1):
                     acc = 0
@@ -406,7 +417,7 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
                           block_N: int = 256, block_K: int = 64, num_stages: int = 2, threads: int = 512,
                           n_src: Optional[int] = None, swiglu: bool = False, n_cu: int = 256, tail_split: int = 4,
                           phased: bool = False, skip_padding: bool = True, partial_first: bool = False,
-                          tail_ksplit: int = 0):
+                          tail_ksplit: int = 0, tail_stages: Optional[int] = None):
     """Tail-balanced variant of ``expert_gemm_kernel`` (same arguments and output).
 
     ``tail_ksplit`` = S > 0: the trailing units run as S K-chunks each (full tile width) instead of
@@ -436,13 +447,21 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
     n_by = (N + block_N - 1) // block_N
     nk = (K + block_K - 1) // block_K
     bn_t = block_N // tail_split
+    # the narrow tail tiles are latency-bound (a partial tile's K loop carries little MFMA work):
+    # a deeper LDS ring there (the whole-tile ring is dead by then; the LDS planner shares bytes)
+    # (+3 stages: GEMM1 172 -> 156 us, GEMM2 100 -> 92 us on the bench layer, profiles/r3/s3/moe/)
+    narrow_stage_bytes = (block_M + bn_t) * block_K * (2 if dtype in ("bfloat16", "float16") else 4)
+    if tail_stages is None:
+        t_stages = max(num_stages, 3) if 3 * narrow_stage_bytes <= 144 * 1024 else num_stages
+    else:
+        t_stages = tail_stages
     assert tail_ksplit or bn_t % 64 == 0 or bn_t == 32, "tail tiles must stay MFMA / SwiGLU-group aligned"
     accum = "float32"
     a_rows = n_src if n_src is not None else max_rows
     n_out = N // 2 if swiglu else N
 
     @T.macro
-    def tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, bx_raw, e_raw, col0, bn):
+    def tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, bx_raw, e_raw, col0, bn, stages):
         # tile / expert ids come from device tables: clamp them so the operand copies are provably
         # in bounds (LDS-DMA instead of guarded register staging) and read them once per tile
         bx = T.min(bx_raw, n_tiles - 1)  # expressions, so the bounds prover sees the clamps
@@ -450,7 +469,7 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
         nrows = T.alloc_var("int32")
         nrows = tile_rows[bx]
         T.clear(C_l)
-        for k in T.Pipelined(nk, num_stages=num_stages):
+        for k in T.Pipelined(nk, num_stages=stages):
             if n_src is not None:
                 T.gather_rows(A[:, k * block_K:(k + 1) * block_K], row_src[bx * block_M:(bx + 1) * block_M], A_s,
                               row_dim=0)
@@ -512,7 +531,7 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
         for it in T.serial(full // n_cu):  # whole tiles
             u = (pid + it * n_cu + shift) % units
             tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, u // n_by, tile_expert[u // n_by],
-                 (u % n_by) * block_N, block_N)
+                 (u % n_by) * block_N, block_N, num_stages)
         prev = T.alloc_shared((1, ), "int32")
         for it in T.serial(T.ceildiv((units - full) * S_, n_cu)):  # K-chunks of the tail units
             q = pid + it * n_cu
@@ -587,13 +606,13 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
             for it in T.serial(full // n_cu):  # whole tiles
                 u = (pid + it * n_cu + shift) % units
                 tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, u // n_by, tile_expert[u // n_by],
-                     (u % n_by) * block_N, block_N)
+                     (u % n_by) * block_N, block_N, num_stages)
             for it in T.serial(T.ceildiv((units - full) * tail_split, n_cu)):  # narrow tail tiles
                 q = pid + it * n_cu
                 if q < (units - full) * tail_split:
                     u = (full + q // tail_split + shift) % units
                     tile(A, W, row_src, tile_rows, C, A_s, Wt_s, Ct_l, u // n_by, tile_expert[u // n_by],
-                         (u % n_by) * block_N + (q % tail_split) * bn_t, bn_t)
+                         (u % n_by) * block_N + (q % tail_split) * bn_t, bn_t, t_stages)
 
     # K-half phased main loop (row gathers included) measured slower here: 382-403 vs 300-356 us per
     # layer (profiles/r2/session2/moe_phased_tail_sweep.log), so off by default
@@ -742,7 +761,7 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
     if sk and reduce_mesh is None and w1_interleaved:
         # tail-balanced grid: whole tiles for the leading rounds, narrow tiles for the trailing partial round
         skc = {k: v for k, v in cfg.items() if k in ("block_N", "block_K", "num_stages", "threads", "tail_split",
-                                                      "phased", "skip_padding", "tail_ksplit")}
+                                                      "phased", "skip_padding", "tail_ksplit", "tail_stages")}
         # partial_first for the down projection: measured neutral (profiles/r3/s3/moe/), off
         pf2 = cfg.get("partial_first2", False)
         ws = ()
@@ -755,7 +774,7 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
         y = torch.empty(max_rows, H, dtype=src_rows.dtype, device=dev)
         k2(act, w2, te, row_src, trows, y, *ws)
         return y, dest
-    for key in ("tail_split", "phased", "partial_first2"):  # options of the tail-balanced grid only
+    for key in ("tail_split", "phased", "partial_first2", "tail_ksplit", "tail_stages"):  # tail-balanced grid only
         cfg.pop(key, None)
     if w1_interleaved:
         # gate/up rows interleaved: the activation is the first GEMM's epilogue
