@@ -26,7 +26,7 @@ from example_mha_fwd import FAST_MATH, ref_program
 def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=256, block_N=64,
                         threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
                         young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd", mfma="16x16",
-                        sum_mfma=False):
+                        sum_mfma=False, sink=False, sm_scale=None):
     """``young_prio``: the second-dispatched half of the waves runs at issue priority 1 (one
     ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4).
     ``seq_kv`` (default ``seq_len``): key/value length; with ``is_causal`` the mask is aligned
@@ -37,8 +37,10 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     ``sum_mfma``: the softmax row sums come from the matrix cores: P times a ones tile (16 or 32
     columns) accumulates next to O, rescaled with it, so the per-tile VALU adds, their cross-lane
     reduction and the running-sum update leave the VALU stream (the loop is VALU-issue bound:
-    an MFMA holds the SIMD's vector issue for half its cycles)."""
-    scale = (1.0 / dim)**0.5 * 1.44269504
+    an MFMA holds the SIMD's vector issue for half its cycles).
+    ``sink``: a learned per-head logit ``Sinks[heads]`` joins every row's softmax normaliser (the
+    gpt-oss attention of examples/attention_sink); it contributes nothing to the output."""
+    scale = ((1.0 / dim)**0.5 if sm_scale is None else sm_scale) * 1.44269504
     head_kv = heads // groups
     seq_kv = seq_len if seq_kv is None else seq_kv
     past = seq_kv - seq_len
@@ -55,13 +57,8 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     group += [[3 + n_softmax], [4 + n_softmax], [5 + n_softmax] + ([6 + n_softmax] if sum_mfma else [])]
     n_ones = 16 if mfma == "16x16" else 32
 
-    @T.prim_func
-    def main(
-            Q: T.Tensor(q_shape, dtype),
-            K: T.Tensor(kv_shape, dtype),
-            V: T.Tensor(kv_shape, dtype),
-            Output: T.Tensor(q_shape, dtype),
-    ):
+    @T.macro
+    def body(Q, K, V, Output, Sinks):
         # causal: heads on the fastest grid axis and the longest (last) query tiles dispatched first
         with T.Kernel(*((heads, n_qt, batch) if is_causal else (n_qt, heads, batch)), threads=threads) as (g0, g1, bz):
             bx = (n_qt - 1 - g1) if is_causal else g0
@@ -164,6 +161,9 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                     T.gemm(acc_s_cast, ones_s, acc_l, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
             if sum_mfma:  # every column of acc_l holds the row sum: spread it in the row layout
                 T.reduce_max(acc_l, logsum, dim=1)
+            if sink:
+                for i in T.Parallel(block_M):
+                    logsum[i] += T.exp2(T.Cast(accum_dtype, Sinks[by]) * 1.44269504 - scores_max[i] * scale)
             for i, j in T.Parallel(block_M, dim):
                 acc_o[i, j] /= logsum[i]
             if staged_epilogue:  # O tile through row-padded LDS: 16-byte row-contiguous stores
@@ -178,6 +178,19 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                 T.copy(acc_o, Output[bz, by, bx * block_M:(bx + 1) * block_M, :])
             else:
                 T.copy(acc_o, Output[bz, bx * block_M:(bx + 1) * block_M, by, :])
+
+    if sink:
+
+        @T.prim_func
+        def main(Q: T.Tensor(q_shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
+                 Output: T.Tensor(q_shape, dtype), Sinks: T.Tensor([heads], dtype)):
+            body(Q, K, V, Output, Sinks)
+    else:
+
+        @T.prim_func
+        def main(Q: T.Tensor(q_shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
+                 Output: T.Tensor(q_shape, dtype)):
+            body(Q, K, V, Output, None)
 
     return main
 

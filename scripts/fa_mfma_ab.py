@@ -24,6 +24,9 @@ VARIANTS = {
     "m32_n128_s2": dict(block_N=128, num_stages=2, mfma="32x32"),
     "m16_sum": dict(block_N=64, num_stages=2, mfma="16x16", sum_mfma=True),
     "m32_sum": dict(block_N=64, num_stages=2, mfma="32x32", sum_mfma=True),
+    "m16_sum_s3": dict(block_N=64, num_stages=3, mfma="16x16", sum_mfma=True),
+    "m16_sum_n128": dict(block_N=128, num_stages=2, mfma="16x16", sum_mfma=True),
+    "m16_sum_n32": dict(block_N=32, num_stages=3, mfma="16x16", sum_mfma=True),
 }
 
 
