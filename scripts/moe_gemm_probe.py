@@ -24,7 +24,7 @@ w2 = (torch.randn(E, H, F, device=dev) * 0.02).to(torch.bfloat16)
 n = T_ * TOP
 
 
-def run(ids, tag, **kw):
+def run(ids, tag, BM=256, **kw):
     max_rows = K.max_padded_rows(K._bucket(n), E, BM)
     dest, row_src, te, counts, trows = K.dispatch_plan(ids, E, BM, max_rows, TOP)
     act = torch.empty(max_rows, F, dtype=x.dtype, device=dev)
@@ -36,13 +36,13 @@ def run(ids, tag, **kw):
     t2 = do_bench(lambda: k2(act, w2, te, row_src, trows, y, *ws), warmup=10, rep=50)
     f1, f2 = 2.0 * n * H * 2 * F, 2.0 * n * F * H
     nt = int((te >= 0).sum())
-    print(f"{tag} {kw}: tiles {nt}  GEMM1 {t1 * 1e3:.1f} us {f1 / t1 * 1e-9:.0f} TF  GEMM2 {t2 * 1e3:.1f} us "
+    print(f"{tag} BM{BM} {kw}: tiles {nt}  GEMM1 {t1 * 1e3:.1f} us {f1 / t1 * 1e-9:.0f} TF  GEMM2 {t2 * 1e3:.1f} us "
           f"{f2 / t2 * 1e-9:.0f} TF", flush=True)
 
 
 bal = torch.arange(n, device=dev, dtype=torch.int32) % E  # exactly n/E rows per expert
 rnd = torch.randint(0, E, (n, ), device=dev, dtype=torch.int32)
-for kw in ({}, dict(tail_stages=2), {}):
+for kw in ({}, dict(BM=128), dict(BM=128, threads=256), {}):
     try:
         run(bal, "balanced", **kw)
         run(rnd, "random  ", **kw)
