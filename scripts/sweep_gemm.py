@@ -15,16 +15,14 @@ from example_gemm import matmul  # noqa: E402
 from tilelang.profiler import do_bench  # noqa: E402
 
 CFGS = [
-    # M, N, K, bm, bn, bk, threads, stages, mfma_shape, phased
-    (4096, 4096, 4096, 256, 256, 64, 512, 2, "16x16", False),
-    (4096, 4096, 4096, 256, 256, 64, 512, 2, "16x16", True),
-    (4096, 4096, 4096, 256, 256, 64, 256, 2, "16x16", False),
-    (4096, 4096, 4096, 256, 256, 64, 256, 2, "16x16", True),
-    (4096, 4096, 4096, 256, 256, 64, 256, 2, "32x32", False),
-    (4096, 4096, 4096, 256, 256, 64, 256, 2, "32x32", True),
-    (8192, 8192, 4096, 256, 256, 64, 512, 2, "16x16", False),
-    (8192, 8192, 4096, 256, 256, 64, 256, 2, "16x16", True),
-    (8192, 8192, 4096, 256, 256, 64, 256, 2, "32x32", True),
+    # M, N, K, bm, bn, bk, threads, stages, mfma_shape, phased (None = default: phased + prefetch)
+    (4096, 4096, 4096, 256, 256, 64, 512, 2, "16x16", None),
+    (4096, 4096, 4096, 256, 128, 64, 512, 2, "16x16", None),
+    (4096, 4096, 4096, 128, 256, 64, 512, 2, "16x16", None),
+    (4096, 4096, 4096, 256, 128, 64, 256, 2, "16x16", None),
+    (4096, 4096, 4096, 256, 128, 128, 512, 2, "16x16", None),
+    (8192, 8192, 4096, 256, 256, 64, 512, 2, "16x16", None),
+    (8192, 8192, 4096, 256, 128, 64, 512, 2, "16x16", None),
 ]
 if len(sys.argv) > 1 and sys.argv[1] == "--quick":
     CFGS = [c for c in CFGS if c[0] == 4096 and c[5] == 64 and c[8] == "16x16"]
@@ -33,7 +31,7 @@ for M, N, K, bm, bn, bk, th, st, sh, ph in CFGS:
     try:
         f = matmul.get_tir(M, N, K, bm, bn, bk, th, st, "float16")
         k = tilelang.compile(f, out_idx=[-1], target="hip",
-                             pass_configs={"tl.mfma_shape": sh, "tl.gemm_phased": ph})
+                             pass_configs={"tl.mfma_shape": sh, **({} if ph is None else {"tl.gemm_phased": ph})})
         a = torch.randn(M, K, device="cuda", dtype=torch.float16)
         b = torch.randn(K, N, device="cuda", dtype=torch.float16)
         c = k(a, b)
