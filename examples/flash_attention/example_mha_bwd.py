@@ -475,8 +475,13 @@ def main(batch=8, heads=32, seq_len=1024, dim=64, causal=False):
     print("All checks pass.")
     from tilelang.profiler import do_bench
     O = attention(Q, K, V, causal)  # the check above freed the first graph
+    # same measurement as the reference example (examples/flash_attention/example_mha_bwd_bshd.py:333):
+    # includes autograd's accumulation of dQ/dK/dV into the leaves' .grad (three elementwise adds)
     lat = do_bench(lambda: O.backward(dO, retain_graph=True))
     print(f"flash attention bwd: {lat:.3f} ms, {flops / lat * 1e-9:.1f} TFLOPS")
+    # the backward alone: torch.autograd.grad returns the gradients without accumulating them
+    lat = do_bench(lambda: torch.autograd.grad(O, (Q, K, V), dO, retain_graph=True))
+    print(f"flash attention bwd (no .grad accumulation): {lat:.3f} ms, {flops / lat * 1e-9:.1f} TFLOPS")
 
 
 if __name__ == "__main__":
