@@ -21,10 +21,13 @@ _DT = {"e4m3": "float8_e4m3fn", "e5m2": "float8_e5m2", "e2m1": "uint8"}
 
 @tilelang.jit(out_idx=[-1])
 def mx_matmul(M, N, K, block_M=256, block_N=None, block_K=None, threads=512, num_stages=None, a_fmt="e4m3",
-              b_fmt="e4m3", out_dtype="bfloat16", accum_dtype="float", panel=8, scales_in_lds=True):
+              b_fmt="e4m3", out_dtype="bfloat16", accum_dtype="float", panel=8, scales_in_lds=True,
+              preshuffle_scales=False):
     """``scales_in_lds``: the e8m0 scale tiles ([block, block_K/32] bytes) ride the pipeline into
     LDS with the operands, so the MFMA loop reads them with ds_read instead of waiting on a
-    global load per K step."""
+    global load per K step.  ``preshuffle_scales``: SA / SB are 1-D, in the tile order of
+    ``tilelang.quantize.preshuffle_mx_scales(s, block_M or block_N, block_K)``: one ds_read_b32 per
+    four 16-row fragments instead of a byte read per fragment."""
     # tiles per format pair, measured at 8192^3 (scripts/sweep_mx.py, profiles/r3/s3/lowp/): with the
     # scale tiles on small-tile LDS-DMA the 256x256 2-stage tiles win for every pair:
     # fp4 x fp4 256x256x256 3.33 PF (256x128x256 3-stage 2.49), fp8 x fp8 256x256x128 1.86 PF
@@ -40,6 +43,10 @@ def mx_matmul(M, N, K, block_M=256, block_N=None, block_K=None, threads=512, num
     bka = block_K // 2 if a_fmt == "e2m1" else block_K
     bkb = block_K // 2 if b_fmt == "e2m1" else block_K
     sk = block_K // 32
+    nk = K // block_K
+    if preshuffle_scales:
+        return _mx_matmul_ps(M, N, K, block_M, block_N, block_K, threads, num_stages, a_fmt, b_fmt, out_dtype,
+                             accum_dtype, panel, ac, bc, bka, bkb, sk, nk)
 
     @T.prim_func
     def main(
@@ -74,6 +81,38 @@ def mx_matmul(M, N, K, block_M=256, block_N=None, block_K=None, threads=512, num
 
 
 E2M1 = [0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0, -0.0, -0.5, -1.0, -1.5, -2.0, -3.0, -4.0, -6.0]
+
+
+def _mx_matmul_ps(M, N, K, block_M, block_N, block_K, threads, num_stages, a_fmt, b_fmt, out_dtype, accum_dtype,
+                  panel, ac, bc, bka, bkb, sk, nk):
+    ta, tb = block_M * sk, block_N * sk  # bytes per pre-shuffled scale tile (64-byte rows)
+
+    @T.prim_func
+    def main(
+            A: T.Tensor((M, ac), _DT[a_fmt]),
+            B: T.Tensor((N, bc), _DT[b_fmt]),
+            SA: T.Tensor((M * K // 2048, 64), "uint8"),
+            SB: T.Tensor((N * K // 2048, 64), "uint8"),
+            C: T.Tensor((M, N), out_dtype),
+    ):
+        with T.Kernel(T.ceildiv(N, block_N), T.ceildiv(M, block_M), threads=threads) as (bx, by):
+            A_s = T.alloc_shared((block_M, bka), _DT[a_fmt])
+            B_s = T.alloc_shared((block_N, bkb), _DT[b_fmt])
+            C_l = T.alloc_fragment((block_M, block_N), accum_dtype)
+            SA_s = T.alloc_shared((ta // 64, 64), "uint8")
+            SB_s = T.alloc_shared((tb // 64, 64), "uint8")
+            T.use_swizzle(panel_size=panel)
+            T.clear(C_l)
+            for k in T.Pipelined(nk, num_stages=num_stages):
+                T.copy(A[by * block_M, k * bka], A_s)
+                T.copy(B[bx * block_N, k * bkb], B_s)
+                T.copy(SA[(by * nk + k) * (ta // 64), 0], SA_s)
+                T.copy(SB[(bx * nk + k) * (tb // 64), 0], SB_s)
+                T.gemm_scaled(A_s, B_s, C_l, SA_s, SB_s, transpose_B=True, a_format=a_fmt, b_format=b_fmt,
+                              scale_layout="preshuffled")
+            T.copy(C_l, C[by * block_M, bx * block_N])
+
+    return main
 
 
 def quantize(x, fmt):

@@ -79,3 +79,51 @@ def test_mxfp4_native_weight_gemm_gpu():
     c = mxfp4_gemm_native(A, Bq, S)
     ref = ref_program(A, Bq, S).float()
     assert ((c.float() - ref).norm() / ref.norm()).item() < 0.05
+
+
+def test_preshuffle_mx_scales_order():
+    """Byte ((((kk * R/64 + q) * 4 + g) * 16 + r) * 4 + b) of a tile holds the scale of row
+    64 q + 16 b + r, column 4 kk + g (tl/gemm.h gemm_ss_mx SCALE_PS)."""
+    from tilelang.quantize import preshuffle_mx_scales
+    R, C, bk = 128, 16, 256  # one 128-row tile, two K tiles of 8 scale columns
+    s = torch.arange(R * C, dtype=torch.int32).reshape(R, C)
+    p = preshuffle_mx_scales(s, R, bk).reshape(-1)
+    tile = bk // 32
+    for row in (0, 17, 63, 64, 100, 127):
+        for col in (0, 3, 5, 7, 8, 15):
+            tk, kb = divmod(col, tile)
+            kk, g = divmod(kb, 4)
+            q, rem = divmod(row, 64)
+            b, r = divmod(rem, 16)
+            idx = tk * R * tile + ((((kk * (R // 64) + q) * 4 + g) * 16 + r) * 4 + b)
+            assert p[idx].item() == s[row, col].item()
+    with pytest.raises(ValueError):
+        preshuffle_mx_scales(s[:96], 96, bk)
+
+
+@pytest.mark.parametrize("af,bf", [("e4m3", "e4m3"), ("e2m1", "e2m1")])
+def test_mx_gemm_preshuffled_cpu(af, bf):
+    import example_tilelang_gemm_mx as m
+    from tilelang.quantize import preshuffle_mx_scales
+    M, N, K, bm, bn, bk = 128, 128, 512, 128, 128, 256
+    f = m.mx_matmul.get_tir(M, N, K, bm, bn, bk, 256, 2, af, bf, preshuffle_scales=True)
+    k = tilelang.compile(f, out_idx=[-1], target="cpu")
+    a, sa = m.quantize(torch.randn(M, K) * 3, af)
+    b, sb = m.quantize(torch.randn(N, K) * 0.2, bf)
+    c = k(a, b, preshuffle_mx_scales(sa, bm, bk), preshuffle_mx_scales(sb, bn, bk))
+    _check(c, a, b, sa, sb, af, bf)
+    kh = tilelang.compile(f, out_idx=[-1], target="hip")
+    assert "gemm_ss_mx" in kh.get_kernel_source() and len(kh.code[0]) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("af,bf", [("e4m3", "e4m3"), ("e2m1", "e2m1"), ("e4m3", "e2m1")])
+def test_mx_gemm_preshuffled_gpu(af, bf):
+    import example_tilelang_gemm_mx as m
+    from tilelang.quantize import preshuffle_mx_scales
+    M, N, K = 512, 512, 1024
+    bk = 256 if af == bf == "e2m1" else 128
+    k = m.mx_matmul(M, N, K, 256, 256, bk, 512, 2, af, bf, preshuffle_scales=True)
+    a, sa = m.quantize(torch.randn(M, K, device="cuda") * 3, af)
+    b, sb = m.quantize(torch.randn(N, K, device="cuda") * 0.2, bf)
+    _check(k(a, b, preshuffle_mx_scales(sa, 256, bk), preshuffle_mx_scales(sb, 256, bk)), a, b, sa, sb, af, bf)

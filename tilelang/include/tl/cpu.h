@@ -250,7 +250,14 @@ inline void mxfp4_gemv(const bfloat16_t* X, const uint8_t* Bq, const uint8_t* S,
 }
 
 // C[M][N] += sum_k (A[m][k] * 2^(SA[m][k/32]-127)) * (B[n][k] * 2^(SB[n][k/32]-127))
-template <int FA, int FB, int M, int N, int K, int A_COLS, int B_COLS, int SA_STRIDE, int SB_STRIDE>
+// PS = 1: pre-shuffled scale tiles (tl::mx_ps_index, T.gemm_scaled(scale_layout="preshuffled"))
+template <int R>
+inline int cpu_mx_ps_index(int row, int kb) {
+  const int f = row >> 4, kk = kb >> 2, g = kb & 3;
+  return ((((kk * (R / 64) + (f >> 2)) * 4 + g) * 16 + (row & 15)) * 4) + (f & 3);
+}
+
+template <int FA, int FB, int M, int N, int K, int A_COLS, int B_COLS, int SA_STRIDE, int SB_STRIDE, int PS = 0>
 inline void cpu_gemm_mx(const void* A_, const void* B_, const void* SA_, const void* SB_, float* C) {
   const uint8_t* A = (const uint8_t*)A_;
   const uint8_t* B = (const uint8_t*)B_;
@@ -263,7 +270,9 @@ inline void cpu_gemm_mx(const void* A_, const void* B_, const void* SA_, const v
         float part = 0.0f;
         for (int k = kb * 32; k < kb * 32 + 32; ++k)
           part += mx_elem<FA>(A + i * A_COLS, k) * mx_elem<FB>(B + j * B_COLS, k);
-        acc += part * e8m0(SA[i * SA_STRIDE + kb]) * e8m0(SB[j * SB_STRIDE + kb]);
+        const int ia = PS ? cpu_mx_ps_index<M>(i, kb) : i * SA_STRIDE + kb;
+        const int ib = PS ? cpu_mx_ps_index<N>(j, kb) : j * SB_STRIDE + kb;
+        acc += part * e8m0(SA[ia]) * e8m0(SB[ib]);
       }
       C[i * N + j] += acc;
     }

@@ -34,6 +34,13 @@ template <uint32_t SWZ> TL_DEVICE int swz_term(int row) {
 }
 
 // element offset of (row, col) inside a swizzled [*][COLS] tile of T
+// highest row bit (1-based) the swizzle code reads; 0 = unswizzled
+template <uint32_t SWZ> constexpr int swz_row_bits() {
+  int m = 0;
+  for (int cb = 0; cb < 8; ++cb) m = ((SWZ >> (4 * cb)) & 15u) > (uint32_t)m ? (int)((SWZ >> (4 * cb)) & 15u) : m;
+  return m;
+}
+
 template <typename T, int COLS, uint32_t SWZ> TL_DEVICE int swz_offset(int row, int col) {
   constexpr int EPC = 16 / (int)sizeof(T);
   if constexpr (SWZ == 0u) {
@@ -364,8 +371,29 @@ TL_DEVICE intx8 ld_mx_operand(const uint8_t* base, int row, int bcol0, int g) {
   }
 }
 
+// Scaled MFMA with the scale bytes picked by op_sel (2-bit byte select per scale operand; the
+// builtin needs immediates, the switch folds once the fragment loops are unrolled).
+#define TL_MXS_CASE(OB, OA) \
+  case OB * 4 + OA:         \
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b, a, c, FB, FA, OB, sb, OA, sa);
+template <int FA, int FB>
+TL_DEVICE floatx4 mfma_mx_sel(intx8 b, intx8 a, floatx4 c, int sb, int sa, int ob, int oa) {
+  switch (ob * 4 + oa) {
+    TL_MXS_CASE(0, 0) TL_MXS_CASE(0, 1) TL_MXS_CASE(0, 2) TL_MXS_CASE(0, 3)
+    TL_MXS_CASE(1, 0) TL_MXS_CASE(1, 1) TL_MXS_CASE(1, 2) TL_MXS_CASE(1, 3)
+    TL_MXS_CASE(2, 0) TL_MXS_CASE(2, 1) TL_MXS_CASE(2, 2) TL_MXS_CASE(2, 3)
+    TL_MXS_CASE(3, 0) TL_MXS_CASE(3, 1) TL_MXS_CASE(3, 2) TL_MXS_CASE(3, 3)
+  }
+  return c;
+}
+#undef TL_MXS_CASE
+
+// Pre-shuffled scale tile of R rows (T.gemm_scaled(scale_layout="preshuffled")): row = 16 f + r,
+// scale column kb = 4 kk + g; byte ((((kk * R/64 + f/4) * 4 + g) * 16 + r) * 4 + f % 4.  Lane (r, g)
+// then finds the scales of 4 consecutive 16-row fragments in one dword (one ds_read_b32 instead
+// of four ds_read_u8) and the MFMA's op_sel picks fragment f % 4's byte.
 template <int FA, int FB, int M, int N, int K, int WARP_M, int WARP_N, int A_COLS, uint32_t SWZ_A, int B_COLS,
-          uint32_t SWZ_B, int SA_STRIDE, int SB_STRIDE>
+          uint32_t SWZ_B, int SA_STRIDE, int SB_STRIDE, int SCALE_PS = 0>
 TL_DEVICE void gemm_ss_mx(const void* __restrict__ A_, const void* __restrict__ B_, const void* __restrict__ SA_,
                           const void* __restrict__ SB_, float* __restrict__ C, int wave_in = -1) {
   constexpr int WM = M / WARP_M, WN = N / WARP_N;
@@ -381,28 +409,74 @@ TL_DEVICE void gemm_ss_mx(const void* __restrict__ A_, const void* __restrict__ 
   const int wm = wave / WARP_N, wn = wave % WARP_N;
   const int r = lane & 15, g = lane >> 4;
   floatx4* acc = reinterpret_cast<floatx4*>(C);
+  // The operand with fewer fragments per wave stays in registers for the 128-K step; the other is
+  // streamed one fragment ahead of its MFMAs.  Holding both (M_REP + N_REP fragments + scales next
+  // to the 128-register accumulator of a 256x256 / 8-wave tile) reached 256 VGPRs and the compiler
+  // re-read A between MFMA groups behind lgkmcnt(0) waits.
+  // Addresses: the swizzle reads row bits 0..3 only (static_assert), so a lane's swizzled byte
+  // offsets are the same for every 16-row fragment; fragment i is i * 16 rows further on, an
+  // immediate of the ds_read.  Written as swz_offset(row, col) per fragment the compiler rebuilt
+  // each address from three registers every K step (~60 VALU adds per step, half the loop's VALU).
+  static_assert(swz_row_bits<SWZ_A>() <= 4 && swz_row_bits<SWZ_B>() <= 4, "MX swizzle must use row bits 0..3");
+  constexpr bool HOLD_B = N_REP <= M_REP;
+  constexpr int NH = HOLD_B ? N_REP : M_REP, NS = HOLD_B ? M_REP : N_REP;
+  constexpr int KS = K / 128;
+  int oa[KS][2], ob[KS][2];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      oa[kk][h] = swz_offset<uint8_t, A_COLS, SWZ_A>(r, kk * 4 * BA + 16 * g + 64 * h);
+      ob[kk][h] = swz_offset<uint8_t, B_COLS, SWZ_B>(r, kk * 4 * BB + 16 * g + 64 * h);
+    }
+  const uint8_t* Aw = A + wm * WM * A_COLS;
+  const uint8_t* Bw = B + wn * WN * B_COLS;
+  static_assert(!SCALE_PS || (WM % 64 == 0 && WN % 64 == 0), "pre-shuffled scales: 64-row warp tiles");
+  const uint8_t* SAw = SCALE_PS ? SA + (wm * WM / 64) * 256 + (g * 16 + r) * 4 : SA + (wm * WM + r) * SA_STRIDE + g;
+  const uint8_t* SBw = SCALE_PS ? SB + (wn * WN / 64) * 256 + (g * 16 + r) * 4 : SB + (wn * WN + r) * SB_STRIDE + g;
+  auto frag = [&](const uint8_t* base, int cols, const int (&o)[2], int i, bool two) -> intx8 {
+    const uint8_t* p = base + i * 16 * cols;
+    intx4 lo = *reinterpret_cast<const intx4*>(p + o[0]);
+    intx4 hi = two ? *reinterpret_cast<const intx4*>(p + o[1]) : intx4{0, 0, 0, 0};
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto ld_scale = [&](const uint8_t* w, int rows, int stride, int i, int kk) -> int {
+    if constexpr (SCALE_PS) return *reinterpret_cast<const int*>(w + (i >> 2) * 256 + kk * rows * 4);
+    return (int)w[i * 16 * stride + kk * 4];
+  };
+  auto ld_a = [&](int i, int kk, int& sc) -> intx8 {
+    sc = ld_scale(SAw, M, SA_STRIDE, i, kk);
+    return frag(Aw, A_COLS, oa[kk], i, BA == 32);
+  };
+  auto ld_b = [&](int i, int kk, int& sc) -> intx8 {
+    sc = ld_scale(SBw, N, SB_STRIDE, i, kk);
+    return frag(Bw, B_COLS, ob[kk], i, BB == 32);
+  };
+  auto ld_held = [&](int i, int kk, int& sc) -> intx8 { return HOLD_B ? ld_b(i, kk, sc) : ld_a(i, kk, sc); };
+  auto ld_stream = [&](int i, int kk, int& sc) -> intx8 { return HOLD_B ? ld_a(i, kk, sc) : ld_b(i, kk, sc); };
+  // one streamed fragment in flight ahead of its MFMAs: distances 0-3 measured within 0.5 % of each
+  // other once the addresses were immediates (profiles/r3/s3/lowp/mx_pd_ab_after_addr.log)
+  constexpr int PD = NS < 1 ? NS : 1;
 #pragma unroll
   for (int kk = 0; kk < K / 128; ++kk) {
-    intx8 a[M_REP], b[N_REP];
-    int sa[M_REP], sb[N_REP];
+    intx8 h[NH], sv[NS];
+    int sh[NH], ss[NS];
 #pragma unroll
-    for (int mi = 0; mi < M_REP; ++mi) {
-      const int row = wm * WM + mi * 16 + r;
-      a[mi] = ld_mx_operand<FA, A_COLS, SWZ_A>(A, row, kk * 4 * BA, g);
-      sa[mi] = (int)SA[row * SA_STRIDE + kk * 4 + g];
+    for (int i = 0; i < NH; ++i) h[i] = ld_held(i, kk, sh[i]);
+#pragma unroll
+    for (int j = 0; j < PD; ++j) sv[j] = ld_stream(j, kk, ss[j]);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      if (j + PD < NS) sv[j + PD] = ld_stream(j + PD, kk, ss[j + PD]);
+#pragma unroll
+      for (int i = 0; i < NH; ++i) {
+        const int mi = HOLD_B ? j : i, ni = HOLD_B ? i : j;
+        const intx8 av = HOLD_B ? sv[j] : h[i], bv = HOLD_B ? h[i] : sv[j];
+        const int sav = HOLD_B ? ss[j] : sh[i], sbv = HOLD_B ? sh[i] : ss[j];
+        acc[mi * N_REP + ni] = mfma_mx_sel<FA, FB>(bv, av, acc[mi * N_REP + ni], sbv, sav, SCALE_PS ? ni & 3 : 0,
+                                                   SCALE_PS ? mi & 3 : 0);
+      }
     }
-#pragma unroll
-    for (int ni = 0; ni < N_REP; ++ni) {
-      const int row = wn * WN + ni * 16 + r;
-      b[ni] = ld_mx_operand<FB, B_COLS, SWZ_B>(B, row, kk * 4 * BB, g);
-      sb[ni] = (int)SB[row * SB_STRIDE + kk * 4 + g];
-    }
-#pragma unroll
-    for (int mi = 0; mi < M_REP; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < N_REP; ++ni)
-        acc[mi * N_REP + ni] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-            b[ni], a[mi], acc[mi * N_REP + ni], FB, FA, 0, sb[ni], 0, sa[mi]);
   }
 }
 

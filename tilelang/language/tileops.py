@@ -157,7 +157,7 @@ def _mx_format(region, fmt):
 
 
 def gemm_scaled(A, B, C, scale_A, scale_B, transpose_A=False, transpose_B=True, policy=GemmWarpPolicy.Square,
-                clear_accum=False, a_format=None, b_format=None):
+                clear_accum=False, a_format=None, b_format=None, scale_layout="rows"):
     """Block-scaled MX GEMM: ``C (+)= (A * 2^(scale_A-127)) @ (B * 2^(scale_B-127))^T``.
 
     gfx950 ``v_mfma_scale_f32_16x16x128_f8f6f4``: the hardware applies one e8m0 scale per
@@ -165,14 +165,22 @@ def gemm_scaled(A, B, C, scale_A, scale_B, transpose_A=False, transpose_B=True, 
     packed fp4 pairs (``float4_e2m1fn_x2`` / uint8 with ``a_format="e2m1"``, low nibble =
     even element); ``B``: ``[N, K]`` likewise (``transpose_B=True``, both K-contiguous);
     ``scale_A``: ``[M, K/32]`` and ``scale_B``: ``[N, K/32]`` e8m0 bytes (shared or global).
-    K must be a multiple of 128."""
+    K must be a multiple of 128.
+
+    ``scale_layout="preshuffled"``: the scale tiles are 1-D shared buffers of ``rows * K / 32``
+    bytes in the order ``tilelang.quantize.preshuffle_mx_scales`` writes (four 16-row fragments'
+    bytes per dword): one ds_read_b32 per four fragments instead of a byte read per fragment, the
+    MFMA's op_sel picks the byte.  Needs warp tiles of 64 rows / columns."""
     A, B, C = to_region(A), to_region(B), to_region(C)
     fa, fb = _mx_format(A, a_format), _mx_format(B, b_format)
+    if scale_layout not in ("rows", "preshuffled"):
+        raise ValueError(f"T.gemm_scaled: scale_layout must be 'rows' or 'preshuffled', got {scale_layout!r}")
     if transpose_A or not transpose_B:
         raise ValueError("T.gemm_scaled needs K-contiguous operands: A [M, K] and B [N, K] (transpose_B=True)")
     op = O.GemmOp(A, B, C, transpose_A, transpose_B, int(policy), clear_accum, 1, 0, to_region(scale_A),
                   to_region(scale_B))
     op.a_fmt, op.b_fmt = fa, fb
+    op.scale_ps = scale_layout == "preshuffled"
     return _emit(op)
 
 

@@ -141,3 +141,20 @@ def dequantize_mxfp4(packed, scales_e8m0, block: int = 32):
 __all__ = ["int4_to_float", "uint4_to_float", "e2m1_to_float", "fp4_to_float", "e8m0_to_float", "pack_int4",
            "unpack_int4", "quantize_int4_groupwise", "dequantize_int4_groupwise", "float_to_e2m1",
            "e2m1_to_float_torch", "quantize_mxfp4", "dequantize_mxfp4"]
+
+
+def preshuffle_mx_scales(scales, block_rows: int, block_K: int):
+    """e8m0 scales ``[rows, K/32]`` -> the pre-shuffled tile order of
+    ``T.gemm_scaled(scale_layout="preshuffled")``: one contiguous
+    ``block_rows * block_K / 32``-byte tile per (row tile, K tile), row tiles outer.  Inside a tile,
+    row = 64 q + 16 b + r and scale column = 4 kk + g go to byte
+    ``(((kk * block_rows/64 + q) * 4 + g) * 16 + r) * 4 + b`` (tl/gemm.h gemm_ss_mx).  A one-time
+    transform for weights; activations' quantizers can write this order directly.  Returned as
+    ``[rows * K / 32 / 64, 64]`` (2-D, the same bytes) so tiles are 2-D operands."""
+    R, C = scales.shape
+    ks = block_K // 128
+    if block_rows % 64 or block_K % 128 or R % block_rows or C % (block_K // 32):
+        raise ValueError(f"preshuffle_mx_scales: shape {tuple(scales.shape)} does not tile by "
+                         f"{block_rows} rows x {block_K} K (rows % 64, K % 128)")
+    x = scales.reshape(R // block_rows, block_rows // 64, 4, 16, C * 32 // block_K, ks, 4)
+    return x.permute(0, 4, 5, 1, 6, 3, 2).reshape(-1, 64).contiguous()

@@ -62,7 +62,11 @@ def _mx_plan(op: O.GemmOp, plan: Dict, num_threads: int, a_ext, b_ext, is_cpu: b
     if A.scope != "shared" or B.scope != "shared":
         raise ValueError("T.gemm_scaled: A and B must be shared-memory tiles")
     sa, sb = _trailing2(op.scale_A), _trailing2(op.scale_B)
-    if tuple(sa) != (M, K // 32) or tuple(sb) != (N, K // 32):
+    if getattr(op, "scale_ps", False):  # pre-shuffled tiles: [rows * K/32 / 64, 64] bytes
+        if tuple(sa) != (M * K // 2048, 64) or tuple(sb) != (N * K // 2048, 64):
+            raise ValueError(f"T.gemm_scaled(scale_layout='preshuffled'): scale tiles must be "
+                             f"[{M * K // 2048}, 64] and [{N * K // 2048}, 64], got {sa} and {sb}")
+    elif tuple(sa) != (M, K // 32) or tuple(sb) != (N, K // 32):
         raise ValueError(f"T.gemm_scaled: scales must be [M, K/32]=[{M}, {K // 32}] and [N, K/32]=[{N}, {K // 32}], "
                          f"got {sa} and {sb}")
     for r in (op.scale_A, op.scale_B):

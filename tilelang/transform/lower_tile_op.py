@@ -1119,12 +1119,18 @@ class TileOpLowerer(Mutator):
         if sa_shape is None or sb_shape is None:
             raise LoweringError("T.gemm_scaled: scale buffers need static shapes (row stride)")
         targs = [plan["a_code"], plan["b_code"], plan["M"], plan["N"], plan["K"]]
+        ps = int(getattr(op, "scale_ps", False))
+        if ps:
+            # tile shapes checked at plan time (gemm_lower._mx_plan)
+            if not self.ctx.is_cpu and ((plan["M"] // plan["warp_m"]) % 64 or (plan["N"] // plan["warp_n"]) % 64):
+                raise LoweringError("T.gemm_scaled(scale_layout='preshuffled') needs warp tiles of 64 rows and "
+                                    f"columns (got {plan['M'] // plan['warp_m']} x {plan['N'] // plan['warp_n']})")
         if self.ctx.is_cpu:
-            targs += [A.static_shape()[-1], B.static_shape()[-1], sa_shape[-1], sb_shape[-1]]
+            targs += [A.static_shape()[-1], B.static_shape()[-1], sa_shape[-1], sb_shape[-1], ps]
             out.append(L.CallStmt("tl::cpu_gemm_mx", [pa, pb, psa, psb, L.BufferPtr(cl, 0)], targs))
             return S.SeqStmt(out)
         targs += [plan["warp_m"], plan["warp_n"], A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
-                  B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u", sa_shape[-1], sb_shape[-1]]
+                  B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u", sa_shape[-1], sb_shape[-1], ps]
         out.append(L.CallStmt("tl::gemm_ss_mx", [pa, pb, psa, psb, L.BufferPtr(cl, 0), self.ctx.wave_expr()], targs))
         return S.SeqStmt(out)
 
