@@ -161,6 +161,14 @@ def main(M=8192, N=8192, K=8192, a_fmt="e4m3", b_fmt="e4m3"):
     torch.testing.assert_close(c.float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
     lat = kernel.get_profiler().do_bench(lambda: kernel(a, b, sa, sb))
     print(f"MX {a_fmt}x{b_fmt} gemm {M}x{N}x{K}: {lat:.3f} ms, {2 * M * N * K / lat * 1e-9:.1f} TFLOPS")
+    # the same GEMM with the scales pre-shuffled once (weights offline, activations by their quantizer)
+    from tilelang.quantize import preshuffle_mx_scales
+    bk = 256 if a_fmt == b_fmt == "e2m1" else 128
+    kps = mx_matmul(M, N, K, a_fmt=a_fmt, b_fmt=b_fmt, preshuffle_scales=True)
+    pa, pb = preshuffle_mx_scales(sa, 256, bk), preshuffle_mx_scales(sb, 256, bk)
+    torch.testing.assert_close(kps(a, b, pa, pb).float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+    lat = kps.get_profiler().do_bench(lambda: kps(a, b, pa, pb))
+    print(f"MX {a_fmt}x{b_fmt} gemm, pre-shuffled scales: {lat:.3f} ms, {2 * M * N * K / lat * 1e-9:.1f} TFLOPS")
 
 
 if __name__ == "__main__":
