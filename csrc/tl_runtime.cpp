@@ -463,8 +463,11 @@ py::dict device_info(int dev) {
 }
 
 // ---- mesh workspaces: symmetric device memory shared across processes over xGMI ----------
-// flags: 0 = hipMalloc (coarse-grained; the protocol uses system-scope fences),
-//        1 = uncached fine-grained (hipDeviceMallocUncached) for debugging coherence issues.
+// flags: 0 = hipMalloc (coarse-grained: coherent only at kernel boundaries; kept for A/B),
+//        1 = uncached fine-grained (hipDeviceMallocUncached): every access bypasses the caches,
+//        2 = fine-grained (hipDeviceMallocFinegrained): coherent at system scope, so peer xGMI
+//            stores ordered by a system-scope release/acquire pair are visible mid-kernel — the
+//            memory class the device protocols (tl/mesh.h, tl/ep.h) are written against; default.
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev) {
@@ -480,6 +483,7 @@ int64_t ws_alloc(int64_t nbytes, int device, int flags) {
   DeviceGuard g(device);
   void* p = nullptr;
   if (flags == 1) TL_HIP_CHECK(hipExtMallocWithFlags(&p, (size_t)nbytes, hipDeviceMallocUncached));
+  else if (flags == 2) TL_HIP_CHECK(hipExtMallocWithFlags(&p, (size_t)nbytes, hipDeviceMallocFinegrained));
   else TL_HIP_CHECK(hipMalloc(&p, (size_t)nbytes));
   TL_HIP_CHECK(hipMemset(p, 0, (size_t)nbytes));
   TL_HIP_CHECK(hipDeviceSynchronize());
@@ -538,7 +542,7 @@ bool can_access_peer(int dev, int peer) {
 }  // namespace
 
 PYBIND11_MODULE(_tl_runtime, m) {
-  m.def("ws_alloc", &ws_alloc, py::arg("nbytes"), py::arg("device"), py::arg("flags") = 0);
+  m.def("ws_alloc", &ws_alloc, py::arg("nbytes"), py::arg("device"), py::arg("flags") = 2);
   m.def("ws_free", &ws_free);
   m.def("ws_zero", &ws_zero);
   m.def("ipc_get_handle", &ipc_get_handle);

@@ -26,7 +26,7 @@ from example_mha_fwd import FAST_MATH, ref_program
 def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=256, block_N=64,
                         threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
                         young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd", mfma="16x16",
-                        sum_mfma=False, sink=False, sm_scale=None):
+                        sum_mfma=False, sink=False, sm_scale=None, fold_max=False, prescale_q=False):
     """``young_prio``: the second-dispatched half of the waves runs at issue priority 1 (one
     ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4).
     ``seq_kv`` (default ``seq_len``): key/value length; with ``is_causal`` the mask is aligned
@@ -39,7 +39,17 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     reduction and the running-sum update leave the VALU stream (the loop is VALU-issue bound:
     an MFMA holds the SIMD's vector issue for half its cycles).
     ``sink``: a learned per-head logit ``Sinks[heads]`` joins every row's softmax normaliser (the
-    gpt-oss attention of examples/attention_sink); it contributes nothing to the output."""
+    gpt-oss attention of examples/attention_sink); it contributes nothing to the output.
+    ``fold_max``: the running row max enters the QK^T MFMA chain as its initial accumulator, so
+    the scores arrive max-subtracted and a probability is ``v_exp_f32(c * s)``; a row moves its
+    max (lazy rescale, threshold 2^8) only on the first tile or when a score beats it by 8 in
+    log2 units, and only then are that tile's scores shifted (skipped by an exec-mask branch
+    otherwise).  Schedule: QK^T(t) | rescale(t-1) | max-and-decide(t) | PV(t-1) + exp(t), so the
+    exponentials of tile t issue between the PV MFMAs of tile t-1.
+    ``prescale_q`` (with ``fold_max``): the log2-domain scale c is folded into the Q registers
+    once, so a probability is ONE ``v_exp_f32`` with no multiply; the price is Q rounded to bf16
+    after scaling: a relative error of 2^-9 in every logit (at |c s| ~ 40 the probabilities of a
+    row are off by ~5 %, against ~1.5 % without it)."""
     scale = ((1.0 / dim)**0.5 if sm_scale is None else sm_scale) * 1.44269504
     head_kv = heads // groups
     seq_kv = seq_len if seq_kv is None else seq_kv
@@ -56,6 +66,11 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     group = [[0], [1, 2], list(range(3, 3 + n_softmax))]
     group += [[3 + n_softmax], [4 + n_softmax], [5 + n_softmax] + ([6 + n_softmax] if sum_mfma else [])]
     n_ones = 16 if mfma == "16x16" else 32
+    n_pv = 2 if sum_mfma else 1
+    sc2 = 1.0 if prescale_q else scale  # scale still to apply to the (max-folded) scores
+    thr = 8.0 / sc2  # lazy-rescale threshold in the scores' own units
+    fold_group = [[0], [1, 2], [3], [4, 5, 6, 7], [8], list(range(9, 9 + n_pv)),
+                  list(range(9 + n_pv, 9 + n_pv + (2 if sum_mfma else 4)))]
 
     @T.macro
     def body(Q, K, V, Output, Sinks):
@@ -102,68 +117,134 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
             else:
                 loop_range = T.ceildiv(seq_kv, block_N)
 
-            for k in T.Pipelined(loop_range, num_stages=num_stages, order=[-1, 0, 3, 1, -1, 2],
-                                 stage=[-1, 0, 0, 1, -1, 1], group=group):
-                # 0: K tile (producer)
-                if bhsd:
-                    T.copy(K[bz, by // groups, k * block_N:(k + 1) * block_N, :], K_shared)
-                else:
-                    T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
-                # 1-2: S = Q K^T
-                if is_causal:
-                    # only the diagonal blocks pay for the per-element mask (uniform branch)
-                    if (k + 1) * block_N <= bx * block_M + past + 1:
-                        T.clear(acc_s)
+            if fold_max:
+                if prescale_q:  # log2-domain scale folded into the Q registers once: S' = (c Q) K^T
+                    for i, j in T.Parallel(block_M, dim):
+                        Q_s[i, j] = T.Cast(dtype, T.Cast(accum_dtype, Q_s[i, j]) * scale)
+                T.fill(scores_max, 0)
+                for k in T.Pipelined(loop_range, num_stages=num_stages, order=[-1, 0, 1, 2, -1, 3, 4],
+                                     stage=[-1, 0, 1, 0, -1, 1, 0], group=fold_group):
+                    # 0: K tile (producer)
+                    if bhsd:
+                        T.copy(K[bz, by // groups, k * block_N:(k + 1) * block_N, :], K_shared)
+                    else:
+                        T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
+                    # 1-2: acc_s = S' - m: the running max enters as the MFMA chain's initial
+                    # accumulator, so exp2 needs no per-element subtraction
+                    if is_causal:
+                        if (k + 1) * block_N <= bx * block_M + past + 1:
+                            for i, j in T.Parallel(block_M, block_N):
+                                acc_s[i, j] = -scores_max[i]
+                        else:
+                            for i, j in T.Parallel(block_M, block_N):
+                                acc_s[i, j] = T.if_then_else(bx * block_M + i + past >= k * block_N + j,
+                                                             -scores_max[i], -T.infinity(acc_s.dtype))
                     else:
                         for i, j in T.Parallel(block_M, block_N):
-                            acc_s[i, j] = T.if_then_else(bx * block_M + i + past >= k * block_N + j, 0,
-                                                         -T.infinity(acc_s.dtype))
-                else:
-                    T.clear(acc_s)
-                T.gemm(Q_s, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
-                # softmax group
-                T.copy(scores_max, scores_max_prev)
-                if lazy_rescale:
-                    T.reduce_max(acc_s, scores_max_prev, dim=1, clear=False)
+                            acc_s[i, j] = -scores_max[i]
+                    T.gemm(Q_s, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
+                    # 3: rescale group (one tile behind)
+                    if rescale != 0:
+                        for i, j in T.Parallel(block_M, dim):
+                            acc_o[i, j] *= scores_scale[i]
+                        if sum_mfma:
+                            for i, j in T.Parallel(block_M, n_ones):
+                                acc_l[i, j] *= scores_scale[i]
+                    # 4-6: decide: a row moves its max only when a score beats it by 2^8 (or on the
+                    # first tile); the rare move subtracts the shift from that tile's scores
+                    T.reduce_max(acc_s, scores_max_prev, dim=1, clear=True)
                     rescale = 0
                     for i in T.Parallel(block_M):
-                        if (scores_max_prev[i] - scores_max[i]) * scale > 8.0:
-                            scores_scale[i] = T.exp2((scores_max[i] - scores_max_prev[i]) * scale)
-                            scores_max[i] = scores_max_prev[i]
+                        if scores_max_prev[i] > thr or k == 0:
+                            scores_scale[i] = T.if_then_else(k == 0, 1.0, T.exp2(-scores_max_prev[i] * sc2))
+                            scores_max[i] = scores_max[i] + scores_max_prev[i]
                             rescale = 1
                         else:
                             scores_scale[i] = 1.0
-                else:
-                    T.reduce_max(acc_s, scores_max, dim=1, clear=False)
-                    for i in T.Parallel(block_M):
-                        scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
-                for i, j in T.Parallel(block_M, block_N):
-                    acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
-                if not sum_mfma:
-                    T.reduce_sum(acc_s, scores_sum, dim=1)
-                    for i in T.Parallel(block_M):
-                        logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
-                T.copy(acc_s, acc_s_cast)
-                # rescale group (one tile behind)
-                if rescale != 0:
-                    for i, j in T.Parallel(block_M, dim):
-                        acc_o[i, j] *= scores_scale[i]
+                            scores_max_prev[i] = 0.0
+                    if rescale != 0:
+                        for i, j in T.Parallel(block_M, block_N):
+                            acc_s[i, j] = acc_s[i, j] - scores_max_prev[i]
+                    # 7: V tile (producer); 8-9: O += P V (one tile behind)
+                    if bhsd:
+                        T.copy(V[bz, by // groups, k * block_N:(k + 1) * block_N, :], V_shared)
+                    else:
+                        T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
+                    T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
                     if sum_mfma:
-                        for i, j in T.Parallel(block_M, n_ones):
-                            acc_l[i, j] *= scores_scale[i]
-                # V tile (producer) and O += P V (one tile behind)
-                if bhsd:
-                    T.copy(V[bz, by // groups, k * block_N:(k + 1) * block_N, :], V_shared)
-                else:
-                    T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
-                T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
-                if sum_mfma:
-                    T.gemm(acc_s_cast, ones_s, acc_l, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
+                        T.gemm(acc_s_cast, ones_s, acc_l, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
+                    # 10-11: P = exp2(acc_s) -> bf16
+                    for i, j in T.Parallel(block_M, block_N):
+                        acc_s[i, j] = T.exp2(acc_s[i, j] * sc2) if not prescale_q else T.exp2(acc_s[i, j])
+                    if not sum_mfma:
+                        T.reduce_sum(acc_s, scores_sum, dim=1)
+                        for i in T.Parallel(block_M):
+                            logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
+                    T.copy(acc_s, acc_s_cast)
+            else:
+                for k in T.Pipelined(loop_range, num_stages=num_stages, order=[-1, 0, 3, 1, -1, 2],
+                                     stage=[-1, 0, 0, 1, -1, 1], group=group):
+                    # 0: K tile (producer)
+                    if bhsd:
+                        T.copy(K[bz, by // groups, k * block_N:(k + 1) * block_N, :], K_shared)
+                    else:
+                        T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
+                    # 1-2: S = Q K^T
+                    if is_causal:
+                        # only the diagonal blocks pay for the per-element mask (uniform branch)
+                        if (k + 1) * block_N <= bx * block_M + past + 1:
+                            T.clear(acc_s)
+                        else:
+                            for i, j in T.Parallel(block_M, block_N):
+                                acc_s[i, j] = T.if_then_else(bx * block_M + i + past >= k * block_N + j, 0,
+                                                             -T.infinity(acc_s.dtype))
+                    else:
+                        T.clear(acc_s)
+                    T.gemm(Q_s, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
+                    # softmax group
+                    T.copy(scores_max, scores_max_prev)
+                    if lazy_rescale:
+                        T.reduce_max(acc_s, scores_max_prev, dim=1, clear=False)
+                        rescale = 0
+                        for i in T.Parallel(block_M):
+                            if (scores_max_prev[i] - scores_max[i]) * scale > 8.0:
+                                scores_scale[i] = T.exp2((scores_max[i] - scores_max_prev[i]) * scale)
+                                scores_max[i] = scores_max_prev[i]
+                                rescale = 1
+                            else:
+                                scores_scale[i] = 1.0
+                    else:
+                        T.reduce_max(acc_s, scores_max, dim=1, clear=False)
+                        for i in T.Parallel(block_M):
+                            scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
+                    for i, j in T.Parallel(block_M, block_N):
+                        acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
+                    if not sum_mfma:
+                        T.reduce_sum(acc_s, scores_sum, dim=1)
+                        for i in T.Parallel(block_M):
+                            logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
+                    T.copy(acc_s, acc_s_cast)
+                    # rescale group (one tile behind)
+                    if rescale != 0:
+                        for i, j in T.Parallel(block_M, dim):
+                            acc_o[i, j] *= scores_scale[i]
+                        if sum_mfma:
+                            for i, j in T.Parallel(block_M, n_ones):
+                                acc_l[i, j] *= scores_scale[i]
+                    # V tile (producer) and O += P V (one tile behind)
+                    if bhsd:
+                        T.copy(V[bz, by // groups, k * block_N:(k + 1) * block_N, :], V_shared)
+                    else:
+                        T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
+                    T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
+                    if sum_mfma:
+                        T.gemm(acc_s_cast, ones_s, acc_l, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
             if sum_mfma:  # every column of acc_l holds the row sum: spread it in the row layout
                 T.reduce_max(acc_l, logsum, dim=1)
             if sink:
                 for i in T.Parallel(block_M):
-                    logsum[i] += T.exp2(T.Cast(accum_dtype, Sinks[by]) * 1.44269504 - scores_max[i] * scale)
+                    logsum[i] += T.exp2(T.Cast(accum_dtype, Sinks[by]) * 1.44269504 -
+                                        scores_max[i] * (sc2 if fold_max else scale))
             for i, j in T.Parallel(block_M, dim):
                 acc_o[i, j] /= logsum[i]
             if staged_epilogue:  # O tile through row-padded LDS: 16-byte row-contiguous stores

@@ -1,0 +1,67 @@
+"""A/B of flashattn_pipelined variants in ONE process (guide rule 24): correctness against the fp32
+definition on random data AND on data whose logits move the row max by far more than the lazy-rescale
+threshold (q scaled x8: the rescale branch fires), then warm and cold TFLOPS.
+
+    python scripts/fa_variants.py '[{"sum_mfma": true}, {"sum_mfma": true, "fold_max": true}]' [--causal]
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "examples", "flash_attention")]
+import torch  # noqa: E402
+
+import tilelang  # noqa: E402
+from example_mha_fwd_pipelined import flashattn_pipelined  # noqa: E402
+from tilelang.profiler import do_bench  # noqa: E402
+
+causal = "--causal" in sys.argv
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+variants = json.loads(args[0]) if args else [{"sum_mfma": True}, {"sum_mfma": True, "fold_max": True}]
+B, H, S, D = 1, 64, 4096, 128
+flops = 4.0 * B * H * S * S * D * (0.5 if causal else 1.0)
+torch.manual_seed(0)
+q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+k = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+v = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+
+
+def ref(qq, heads):
+    qh, kh, vh = (t[:, :, heads].float().transpose(1, 2) for t in (qq, k, v))
+    s = qh @ kh.transpose(-1, -2) / D**0.5
+    if causal:
+        s = s.masked_fill(torch.ones(S, S, device=s.device, dtype=torch.bool).triu(1), float("-inf"))
+    return (torch.softmax(s, -1) @ vh).transpose(1, 2)
+
+
+heads = [0, 17, 40, 63]
+q_hot = (q.float() * 8).to(torch.bfloat16)
+refs = {"rand": ref(q, heads), "hot": ref(q_hot, heads)}
+for kw in variants:
+    a = dict(block_M=256, block_N=64, threads=512, num_stages=2, q_in_regs=True)
+    a.update(kw)
+    tag = json.dumps(kw, sort_keys=True)
+    try:
+        f = flashattn_pipelined.get_tir(B, H, S, D, causal, 1, **a)
+        kern = tilelang.compile(f, out_idx=[3], target="hip", pass_configs=flashattn_pipelined.pass_configs)
+        errs = []
+        for name, qq in (("rand", q), ("hot", q_hot)):
+            o = kern(qq, k, v)
+            errs.append((o[:, :, heads].float() - refs[name]).abs().max().item())
+        fn = lambda: kern(q, k, v)  # noqa: E731
+        fn()
+        cold = do_bench(fn, warmup=5, rep=30)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(30):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        warm = e0.elapsed_time(e1) / 30
+        ok = max(errs) < 2e-2
+        print(f"{tag}: err rand {errs[0]:.3g} hot {errs[1]:.3g} {'OK' if ok else 'WRONG'} | "
+              f"cold {flops / cold * 1e-9:.1f} TF | warm {flops / warm * 1e-9:.1f} TF", flush=True)
+    except Exception as e:  # noqa: BLE001
+        print(f"{tag}: FAILED {type(e).__name__}: {str(e)[:400]}", flush=True)

@@ -233,3 +233,34 @@ def test_register_set_under_thread_guard_is_not_uniform():
                 B[tx] = S[255 - tx]
     with pytest.raises(RuntimeError):
         tilelang.lower(bad, target="hip")
+
+
+def test_cross_thread_hazard_with_2d_threads_is_refused():
+    """threads=(X, Y): the ownership proof must give tx and ty their own components of the flat
+    id; with both set to the flat id, s[ty, tx] / s[ty, tx ^ 1] would look like one thread."""
+    import pytest
+    import tilelang
+    import tilelang.language as T
+
+    @T.prim_func
+    def bad(A: T.Tensor((8, 32), "float32"), B: T.Tensor((8, 32), "float32")):
+        with T.Kernel(1, threads=(32, 8)) as bx:
+            S = T.alloc_shared((8, 32), "float32")
+            tx = T.get_thread_binding(0)
+            ty = T.get_thread_binding(1)
+            if tx < 16:
+                S[ty, tx] = A[ty, tx]
+                B[ty, tx] = S[ty, tx ^ 1]  # the neighbouring lane's element
+    with pytest.raises(RuntimeError, match="thread-dependent branch"):
+        tilelang.lower(bad, target="hip")
+
+    @T.prim_func
+    def ok(A: T.Tensor((8, 32), "float32"), B: T.Tensor((8, 32), "float32")):
+        with T.Kernel(1, threads=(32, 8)) as bx:
+            S = T.alloc_shared((8, 32), "float32")
+            tx = T.get_thread_binding(0)
+            ty = T.get_thread_binding(1)
+            if tx < 16:
+                S[ty, tx] = A[ty, tx] * 2.0
+                B[ty, tx] = S[ty, tx] + 1.0  # own element
+    tilelang.lower(ok, target="hip")

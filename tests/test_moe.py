@@ -254,3 +254,82 @@ def test_moe_tail_ksplit_cpu():
 @pytest.mark.parametrize("S", [2, 4])
 def test_moe_tail_ksplit_gpu(S):
     _tail_ksplit_check("cuda", S)
+
+
+def _dead_peer_worker(rank, world, port, q):
+    """Rank 1 skips the expert-parallel layer of step 1 (a dead or diverged peer): rank 0's
+    device exchange must raise MeshError within ONE wait budget (TL_EP_TIMEOUT_S = 2 s; every
+    later wait of the step gives up at once), then both ranks fall back to the host all-to-all
+    (bench.py's fallback) and post a result checked against the fp32 definition."""
+    import os
+    import time
+    import torch.distributed as dist
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TL_EP_TIMEOUT_S="2")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from tilelang.parallel import init_mesh, shutdown_mesh
+        from tilelang.parallel.mesh import MeshError
+        from tilelang.runtime import errors
+        from tilelang.ops import moe as K
+        dev = f"cuda:{rank % torch.cuda.device_count()}"
+        torch.cuda.set_device(dev)
+        mesh = init_mesh(1, world, device=dev)
+        cfg = MoEConfig(hidden=512, ffn=256, n_experts=8, topk=2, dtype=torch.bfloat16, block_M=128)
+        layer = MoELayer(cfg, "ep", mesh=mesh, device=dev)
+        g, w1, w2 = (t.to(dev) for t in init_moe_weights(cfg))
+        torch.manual_seed(7 + rank)
+        x = torch.randn(256, cfg.hidden, device=dev).to(cfg.dtype)
+        layer(x)
+        errors.check()  # step 0: both ranks healthy
+        dist.barrier()
+        elapsed, raised = None, None
+        if rank == 0:
+            t0 = time.time()
+            try:
+                layer(x)
+                errors.check()
+                mesh.check()
+            except MeshError as e:
+                raised = str(e)
+            elapsed = time.time() - t0
+        dist.barrier()
+        if rank == 0:
+            if raised is None:
+                raise AssertionError("no MeshError although the peer skipped its dispatch")
+            # one 2 s budget (plus launch/compile slack), not one per wait: W waits x 4 kernels
+            # would be >= 16 s with serialised budgets
+            if elapsed > 8.0:
+                raise AssertionError(f"MeshError after {elapsed:.1f} s: waits were serialised ({raised})")
+        mesh.err.zero_()
+        layer.ep_mode = "host"  # bench.py's fallback: RCCL/gloo all_to_all_v
+        out = layer(x).float()
+        ids, w = K.route(x, g, cfg.topk)
+        ref = moe_reference(x, g, w1, w2, cfg.topk, routing=(ids, w))
+        err = (out - ref).abs().max().item()
+        if not err <= 3e-2 * ref.abs().max().item():
+            raise AssertionError(f"rank {rank}: host fallback max err {err}")
+        shutdown_mesh()
+        dist.destroy_process_group()
+        q.put((rank, "ok" if rank else f"ok {elapsed:.2f}s"))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.gpu
+def test_ep_dead_peer_fails_fast_gpu():
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_dead_peer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+    assert res[1] == "ok" and res[0].startswith("ok"), res
+    print("dead peer detected after", res[0])

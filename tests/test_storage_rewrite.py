@@ -93,3 +93,32 @@ def test_inplace_detection():
         src = tilelang.compile(f, out_idx=[2], target="hip",
                                pass_configs={"tl.storage_rewrite_detect_inplace": True}).get_kernel_source()
         assert ("v[" in src) == shifted
+
+
+def _reread_prog(n=64):
+
+    @T.prim_func
+    def main(A: T.Tensor((n, 8), "float32"), I: T.Tensor((n, ), "int32"), C: T.Tensor((n, ), "float32")):
+        with T.Kernel(n, threads=64) as bx:
+            u = T.alloc_local((8, ), "float32")
+            v = T.alloc_local((8, ), "float32")
+            w = T.alloc_local((8, ), "float32")
+            for j in T.serial(8):
+                u[j] = A[bx, j]
+            for j in T.serial(8):
+                v[j] = u[j] * 2.0
+                w[j] = u[j] + 1.0  # reads u[j] AFTER v[j] was written: v must not take u's storage
+            C[bx] = v[I[bx] % 8] + w[I[bx] % 8]
+
+    return main
+
+
+def test_inplace_rejects_read_after_write():
+    _, merged = rewrite_local_storage(_kernel_of(_reread_prog()), detect_inplace=True)
+    assert merged.get("v") != "u"
+    k = tilelang.compile(_reread_prog(), out_idx=[2], target="cpu",
+                         pass_configs={"tl.storage_rewrite_detect_inplace": True})
+    A = torch.randn(64, 8)
+    I = torch.randint(0, 100, (64, ), dtype=torch.int32)
+    x = A[torch.arange(64), (I % 8).long()]
+    torch.testing.assert_close(k(A, I), 3 * x + 1)

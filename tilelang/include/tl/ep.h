@@ -20,8 +20,15 @@
 // writer waits for that peer's "consumed" word (RFREE / TFREE, stored into the writer's buffer
 // by the consumer at its next kernel, which stream order places after the consuming kernel).
 // All waits are bounded by wall clock (s_memrealtime, 100 MHz) and record a mesh error code in
-// `err` (raised by the host: tilelang/runtime/errors.py) instead of hanging the GPU.
-// Memory model: payload = plain 16-byte stores over xGMI, then every storing wave's
+// `err` (raised by the host: tilelang/runtime/errors.py) instead of hanging the GPU; once `err` is
+// set every later wait returns at once (a dead peer costs one budget in total).  Codes: 1 slot
+// not freed, 2 data not arrived, 16 routing overflow (a row that would not fit its slot region).
+// Memory model: the workspace (control words AND payload) is FINE-GRAINED device memory
+// (hipDeviceMallocFinegrained, runtime ws_alloc flags=2, the default): HIP/HSA define
+// system-scope coherence for fine-grained memory, so a peer's stores that precede its
+// system-scope release (and the flag store after it) are visible to this GPU after its
+// system-scope acquire that follows reading the flag — no reliance on L2 write-back of
+// coarse-grained memory.  Payload = plain 16-byte stores over xGMI, then every storing wave's
 // vmcnt(0) + workgroup barrier + system-scope release fence before the arrival counter; the
 // last arriving block publishes with another release + system-scope flag store; readers poll
 // relaxed system-scope loads and acquire (system scope) before touching the payload.
@@ -53,13 +60,16 @@ TL_DEVICE void st_sys(unsigned* p, unsigned v) {
 }
 TL_DEVICE unsigned ld_sys(unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 
-// one lane: wait until *p == v (exact) or (int)(*p - v) >= 0; bounded; error code on timeout
+// one lane: wait until *p == v (exact) or (int)(*p - v) >= 0; bounded; error code on timeout.
+// Once this rank's error word is set (by any wait of this or an earlier kernel that has not been
+// raised yet) every later wait gives up at once: a dead peer costs ONE budget, not one per wait.
+TL_DEVICE bool failed(int* err) { return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0; }
 TL_DEVICE void spin(unsigned* p, unsigned v, bool at_least, int* err, int code) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (true) {
     const unsigned x = ld_sys(p);
     if (at_least ? ((int)(x - v) >= 0) : (x == v)) return;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > TL_EP_TIMEOUT_TICKS) {
+    if (failed(err) || __builtin_amdgcn_s_memrealtime() - t0 > TL_EP_TIMEOUT_TICKS) {
       __hip_atomic_fetch_or(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
@@ -153,12 +163,19 @@ TL_DEVICE void dispatch(const void* x_, const int* ids, int* ret_index, long lon
     const int base = __shfl(run, d < 0 ? 0 : d, 64);
     run += chunk_cnt_mine;
     const int slot = base + rank_in_chunk;
-    if (j < P && wave == 0 && blockIdx.x == 0) ret_index[j] = d * cap + slot;
+    // an overflowing pair (flagged below, rows dropped) reads row 0: in range, and raised
+    if (j < P && wave == 0 && blockIdx.x == 0) ret_index[j] = (d >= 0 && d < W && slot < cap) ? d * cap + slot : 0;
     // rows are dealt round-robin over every wave of the grid; a wave moves a row with all lanes
     const int gw = blockIdx.x * nw + wave, nwaves = gridDim.x * nw;
     for (int l = (gw - j0 % nwaves + nwaves) % nwaves; l < 64 && j0 + l < P; l += nwaves) {
       const int dl = __shfl(d, l, 64), sl = __shfl(slot, l, 64);
       const int jl = j0 + l;
+      if (dl < 0 || dl >= W || sl >= cap) {
+        // a routing id out of range, or more pairs for one destination than its RECV region
+        // holds (cap assumes distinct experts per token): record it, never store past the slot
+        if (lane == 0) __hip_atomic_fetch_or(err, 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        continue;
+      }
       char* dst = ws[dl] + L.recv_off() + (((long long)p * W + me) * cap + sl) * row_bytes;
       copy_row(dst, x + (long long)(jl / topk) * row_bytes, row_bytes, lane);
       if (lane == 0) {

@@ -2,9 +2,10 @@
 //
 // The reference fork lowers T.comm.* to an opaque `tl.broadcast_` intrinsic that has no code
 // generator (src/op/comm.cc:27-48).  Here a mesh "core" is one GPU of the node.  Every rank
-// owns a symmetric workspace (hipMalloc'ed, exported with hipIpcGetMemHandle and opened by
-// every peer), so a workgroup stores its tile straight into a peer's HBM over xGMI — every
-// GPU pair has its own link, so transfers are direct (no 2-D mesh routing).
+// owns a symmetric workspace (fine-grained device memory — hipDeviceMallocFinegrained, coherent
+// at system scope across GPUs — exported with hipIpcGetMemHandle and opened by every peer), so a
+// workgroup stores its tile straight into a peer's HBM over xGMI — every GPU pair has its own
+// link, so transfers are direct (no 2-D mesh routing).
 //
 // Workspace of one rank (F = align256(nblocks * nops * nranks * 4)):
 //   [0, F)        u32 flag [blk][op][src]   data from `src` is in my slot (or barrier arrival)
@@ -94,13 +95,16 @@ TL_DEVICE void store_flag(unsigned* p, unsigned v) {
 }
 TL_DEVICE unsigned load_flag(unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 
-// one lane spins until *p == v (exact) or (int)(*p - v) >= 0 (at_least); bounded by wall clock
+// one lane spins until *p == v (exact) or (int)(*p - v) >= 0 (at_least); bounded by wall clock.
+// A set error word (an earlier wait of this rank timed out and was not raised yet) ends every
+// later wait at once, so a dead peer costs one budget, not one per wait.
 TL_DEVICE void spin(const Ctx& c, unsigned* p, unsigned v, bool at_least, unsigned code) {
   unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (true) {
     unsigned x = load_flag(p);
     if (at_least ? ((int)(x - v) >= 0) : (x == v)) return;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > TL_MESH_TIMEOUT_TICKS) {
+    if (__hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+        __builtin_amdgcn_s_memrealtime() - t0 > TL_MESH_TIMEOUT_TICKS) {
       atomicOr(c.err, code);
       return;
     }

@@ -45,6 +45,9 @@ template <int MASK, typename T> TL_DEVICE T shfl_xor_c(T v) {
     if constexpr (MASK == 32) {
       auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
       return from_u32<T>(__lane_id_lt32() ? r[1] : r[0]);
+    } else if constexpr (MASK == 16) {
+      auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+      return from_u32<T>((threadIdx.x & 16) == 0 ? r[1] : r[0]);
     } else {
       return from_u32<T>((uint32_t)__shfl_xor((int)u, MASK, 64));
     }
@@ -71,10 +74,24 @@ template <typename T> TL_DEVICE T shfl(T v, int src, int width = 64) {
 }
 
 // all-reduce over the lane bits selected by MASKBITS (a set of xor strides, each a power of 2)
+// xor-32 / xor-16 step of a commutative reduction: one v_permlane{32,16}_swap leaves {own, partner}
+// in its two results (which is which depends on the lane's half), and op(r0, r1) is the same
+// either way, so no per-lane select is needed.
+template <int MASK, typename Op, typename T> TL_DEVICE T swap_step(Op op, T v) {
+  if constexpr (sizeof(T) == 4) {
+    const uint32_t u = as_u32(v);
+    auto r = MASK == 32 ? __builtin_amdgcn_permlane32_swap(u, u, false, false)
+                        : __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return op(from_u32<T>(r[0]), from_u32<T>(r[1]));
+  } else {
+    return op(v, shfl_xor_c<MASK>(v));
+  }
+}
+
 template <typename Op, int MASKBITS, typename T> TL_DEVICE T lane_allreduce(T v) {
   Op op;
-  if constexpr ((MASKBITS & 32) != 0) v = op(v, shfl_xor_c<32>(v));
-  if constexpr ((MASKBITS & 16) != 0) v = op(v, shfl_xor_c<16>(v));
+  if constexpr ((MASKBITS & 32) != 0) v = swap_step<32>(op, v);
+  if constexpr ((MASKBITS & 16) != 0) v = swap_step<16>(op, v);
   if constexpr ((MASKBITS & 8) != 0) v = op(v, shfl_xor_c<8>(v));
   if constexpr ((MASKBITS & 4) != 0) v = op(v, shfl_xor_c<4>(v));
   if constexpr ((MASKBITS & 2) != 0) v = op(v, shfl_xor_c<2>(v));

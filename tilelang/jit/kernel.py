@@ -111,12 +111,22 @@ class JITKernel:
         """One code object (gfx950) or shared object (cpu) per device kernel of the program."""
         a = self.artifact
         out = []
+        hip_flags = self.hip_flags()
         for dk in a.kernels:
             if a.is_cpu:
                 out.append(_cache.compile_cpu_cached(dk.source, self.compile_flags, self.verbose))
             else:
-                out.append(_cache.compile_hip_cached(dk.source, self.compile_flags, self.verbose))
+                out.append(_cache.compile_hip_cached(dk.source, hip_flags, self.verbose))
         return out
+
+    def hip_flags(self) -> List[str]:
+        """hipcc flags of this kernel's gfx950 compile: the user's plus what the pass configs imply."""
+        flags = list(self.compile_flags)
+        if self.pass_configs.get("tl.enable_fast_math") and not self.pass_configs.get("tl.disable_fast_math"):
+            # fast math promises no NaN inputs: fmaxf on MFMA results then needs no canonicalising
+            # v_max_f32 x, x per operand (the softmax row max of every attention kernel)
+            flags.append("-fno-honor-nans")
+        return flags
 
     def _param_specs(self, dk, with_outputs: bool):
         symtab = {}
@@ -296,7 +306,7 @@ class JITKernel:
     def get_assembly(self) -> str:
         if self.artifact.is_cpu:
             return ""
-        return hipcc.compile_hip(self.artifact.kernel_source, options=self.compile_flags, asm=True).decode()
+        return hipcc.compile_hip(self.artifact.kernel_source, options=self.hip_flags(), asm=True).decode()
 
     def export_sources(self, directory: str):
         Path(directory).mkdir(parents=True, exist_ok=True)

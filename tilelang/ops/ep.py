@@ -29,6 +29,14 @@ import tilelang.language as T
 _CTRL = 4096
 
 
+def _flags():
+    """hipcc flags of the exchange kernels: ``TL_EP_TIMEOUT_S`` (seconds) overrides the wall-clock
+    budget of every bounded wait (tl/ep.h TL_EP_TIMEOUT_TICKS, 100 MHz ticks; default 20 s)."""
+    import os
+    s = os.environ.get("TL_EP_TIMEOUT_S")
+    return [f"-DTL_EP_TIMEOUT_TICKS={int(float(s) * 1e8)}ull"] if s else []
+
+
 def _tdt(dtype: torch.dtype) -> str:
     return {torch.float16: "float16", torch.bfloat16: "bfloat16", torch.float32: "float32"}[dtype]
 
@@ -53,7 +61,7 @@ def dispatch_kernel(n_tok: int, H: int, topk: int, W: int, n_loc: int, cap: int,
             T.evaluate(T.call_extern("void", f"tl::ep::dispatch<{W}>", T.address_of(x[0, 0]), T.address_of(ids[0]),
                                      T.address_of(ret_index[0]), ws, me, epoch, err, P, topk, n_loc, cap, H * eb))
 
-    return tilelang.compile(ep_dispatch, target="hip")
+    return tilelang.compile(ep_dispatch, target="hip", compile_flags=_flags())
 
 
 @functools.lru_cache(maxsize=None)
@@ -66,7 +74,7 @@ def recv_wait_kernel(W: int, cap: int, row_bytes: int, blocks: int = 16):
             T.evaluate(T.call_extern("void", f"tl::ep::recv_wait<{W}>", T.address_of(ids_out[0]),
                                      T.address_of(cnt_out[0]), ws, me, epoch, err, cap, row_bytes))
 
-    return tilelang.compile(ep_recv_wait, target="hip")
+    return tilelang.compile(ep_recv_wait, target="hip", compile_flags=_flags())
 
 
 @functools.lru_cache(maxsize=None)
@@ -80,7 +88,7 @@ def ret_kernel(rows: int, H: int, W: int, cap: int, dtype: str, blocks: int = 12
             T.evaluate(T.call_extern("void", f"tl::ep::ret<{W}>", T.address_of(y[0, 0]), T.address_of(ydest[0]),
                                      T.address_of(cnt[0]), ws, me, epoch, err, cap, H * eb))
 
-    return tilelang.compile(ep_ret, target="hip")
+    return tilelang.compile(ep_ret, target="hip", compile_flags=_flags())
 
 
 @functools.lru_cache(maxsize=None)
@@ -91,7 +99,7 @@ def ret_wait_kernel(W: int):
         with T.Kernel(1, threads=64) as bx:
             T.evaluate(T.call_extern("void", f"tl::ep::ret_wait<{W}>", ws, me, epoch, err))
 
-    return tilelang.compile(ep_ret_wait, target="hip")
+    return tilelang.compile(ep_ret_wait, target="hip", compile_flags=_flags())
 
 
 class EPExchange:

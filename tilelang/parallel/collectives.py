@@ -54,6 +54,16 @@ def _virtual_gather(ctx: VirtualRank, name: str, t: torch.Tensor, direction: str
 _OPS = {"sum", "max", "min", "avg", "prod"}
 
 
+def _device_native(ctx, t: torch.Tensor, direction: str = "all") -> bool:
+    """True when the process group moves ``t`` where it lives: a GPU tensor on an ``nccl`` (RCCL)
+    group.  A GPU tensor on a gloo group (tests with several ranks sharing one GPU) is staged
+    through host memory instead."""
+    if not t.is_cuda:
+        return False
+    import torch.distributed as dist
+    return dist.get_backend(ctx.group(direction)) == "nccl"
+
+
 def _dist_op(op: str):
     import torch.distributed as dist
     return {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
@@ -98,13 +108,15 @@ def all_gather(t: torch.Tensor, direction: str = "all", ctx=None) -> torch.Tenso
     if isinstance(ctx, ProcessMesh):
         import torch.distributed as dist
         G = len(ctx.group_ranks(direction))
-        out = torch.empty((G,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         grp = ctx.group(direction)
-        if t.is_cuda:
+        if _device_native(ctx, t, direction):
+            out = torch.empty((G,) + tuple(t.shape), dtype=t.dtype, device=t.device)
             dist.all_gather_into_tensor(out, t.contiguous(), group=grp)
-        else:
-            dist.all_gather(list(out.unbind(0)), t.contiguous(), group=grp)
-        return out
+            return out
+        th = t.detach().cpu().contiguous()
+        out = torch.empty((G,) + tuple(t.shape), dtype=t.dtype)
+        dist.all_gather(list(out.unbind(0)), th, group=grp)
+        return out.to(t.device)
     return torch.stack(_virtual_gather(ctx, "all_gather", t.clone(), direction))
 
 
@@ -216,7 +228,7 @@ def all_to_all_v(t: torch.Tensor, send_counts: List[int], direction: str = "all"
     both = torch.cat([all_cnt[:, k], cnt]).tolist()     # the one host sync of the exchange
     recv_counts = [int(x) for x in both[:G]]
     send_counts = [int(x) for x in both[G:]]
-    if isinstance(ctx, ProcessMesh) and t.is_cuda:
+    if isinstance(ctx, ProcessMesh) and _device_native(ctx, t, direction):
         import torch.distributed as dist
         out = torch.empty((sum(recv_counts),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         if sum(send_counts) != t.shape[0]:

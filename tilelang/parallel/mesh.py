@@ -198,7 +198,11 @@ class MeshContext:
             what.append("waiting for data from a sender")
         if e & 4:
             what.append("waiting at a mesh barrier")
-        return MeshError(f"{label}: timed out " + ", ".join(what) + " (a peer did not run the same kernel sequence)")
+        msg = f"{label}: timed out " + ", ".join(what) + " (a peer did not run the same kernel sequence)" \
+            if what else f"{label}:"
+        if e & 16:
+            msg += " routing overflow: a token's expert ids are not distinct or out of range (rows dropped)"
+        return MeshError(msg)
 
     def check(self):
         """Raise if any bounded wait of a mesh kernel on this rank timed out."""
@@ -266,7 +270,7 @@ class ProcessMesh(MeshContext):
     for CPU meshes).  Row/column groups back the host collectives; the symmetric workspace
     is shared through HIP IPC (GPU) or /dev/shm (CPU)."""
 
-    def __init__(self, nrow: int, ncol: int, device=None, ws_flags: int = 0):
+    def __init__(self, nrow: int, ncol: int, device=None, ws_flags: Optional[int] = None):
         import torch
         import torch.distributed as dist
         if not dist.is_initialized():
@@ -287,7 +291,10 @@ class ProcessMesh(MeshContext):
             devs = [None] * world
             dist.all_gather_object(devs, (os.uname().nodename, self.device.index))
             self.ranks_on_device = sum(1 for d in devs if d == devs[rank])
-        self.ws_flags = ws_flags
+        # workspace memory class (runtime ws_alloc): 2 = fine-grained, coherent at system scope
+        # (the default the device protocols are written for), 1 = uncached, 0 = coarse-grained
+        # hipMalloc (A/B only); TL_MESH_WS_FLAGS overrides
+        self.ws_flags = int(os.environ.get("TL_MESH_WS_FLAGS", "2")) if ws_flags is None else int(ws_flags)
         self.world_group = dist.group.WORLD
         # every rank creates every row and column group in the same order (new_group is collective)
         self.row_groups = [dist.new_group([r * ncol + c for c in range(ncol)]) for r in range(nrow)]
@@ -580,7 +587,7 @@ class _VirtualCollectives:
 
 
 def init_mesh(nrow: Optional[int] = None, ncol: Optional[int] = None, backend: Optional[str] = None,
-              ws_flags: int = 0, device=None) -> ProcessMesh:
+              ws_flags: Optional[int] = None, device=None) -> ProcessMesh:
     """Initialise ``torch.distributed`` from the torchrun environment if needed (``nccl``
     = RCCL when a GPU is visible, else ``gloo``) and make this rank's ``ProcessMesh`` the
     active context.  The default shape is the most square factorisation of the world."""

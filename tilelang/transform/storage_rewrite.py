@@ -18,7 +18,9 @@ and its ``InplaceOpVerifier``): a buffer whose first statement is the LAST state
 buffer of the same dtype and shape may take over its storage when that statement is a pure
 element-wise map ``dst[idx] = f(src[idx], ...)``: every access of either buffer uses one index
 tuple made of distinct loop variables covering every enclosing loop (so no iteration reads an
-element another iteration has already overwritten), ``src`` is only read and ``dst`` only written.
+element another iteration has already overwritten), ``src`` is only read and ``dst`` only written,
+and no read of ``src`` follows the first write of ``dst`` in program order (a second same-index read
+after the store would see the new value once the two share storage).
 """
 from __future__ import annotations
 
@@ -39,6 +41,7 @@ def _inplace_ok(stmt, src, dst) -> bool:
     loops = []
     idx_seen = []
     ok = [True]
+    stored = [False]  # a store to dst has been seen (program order)
 
     def visit_expr(e):
         for n in post_order(e):
@@ -46,6 +49,9 @@ def _inplace_ok(stmt, src, dst) -> bool:
                 if n.buffer is dst:
                     ok[0] = False
                 elif n.buffer is src:
+                    if stored[0]:
+                        # src read after dst was written: once merged, it reads the new value
+                        ok[0] = False
                     idx_seen.append(tuple(n.indices))
 
     def visit(x):
@@ -66,6 +72,8 @@ def _inplace_ok(stmt, src, dst) -> bool:
             for i in x.indices:
                 visit_expr(i)
             visit_expr(x.value)
+            if x.buffer is dst:
+                stored[0] = True
         elif isinstance(x, S.LetStmt):
             visit_expr(x.value)
         else:

@@ -113,6 +113,7 @@ class ThreadSync:
     def __init__(self):
         self.managed: Set = set()
         self.tvars = ()
+        self.tdims = None
         self.nthreads = 0
         self.loop_ranges = {}  # enclosing constant-bounded loops (for the divergent-branch proof)
         self.uniform = set()
@@ -213,7 +214,7 @@ class ThreadSync:
                 # only when a thread reads back exactly the elements it wrote itself (same
                 # index expression); anything else crosses threads (possibly waves) and is
                 # refused rather than emitted as a silent race.
-                _check_divergent_hazards(c, self.managed, self.nthreads, self.tvars, self.loop_ranges)
+                _check_divergent_hazards(c, self.managed, self.nthreads, self.tvars, self.loop_ranges, self.tdims)
                 out.append(c)
                 return c, _State(st.reads | r0, st.writes | w0)
             # block-uniform condition: scan the branches for internal hazards
@@ -224,6 +225,7 @@ class ThreadSync:
             return nc, st_t.merge(st_e)
         if isinstance(c, S.KernelStmt):
             self.tvars = tuple(c.thread_vars or ())
+            self.tdims = [int(n) for n in (c.threads or [1])]
             self.nthreads = 1
             for n in (c.threads or [1]):
                 self.nthreads *= int(n)
@@ -326,13 +328,33 @@ def _thread_env(t, tvars):
     return env
 
 
-def _elements_by_thread(accs, cond, nthreads, tvars, ranges):
+def _elements_by_thread(accs, cond, nthreads, tvars, ranges, tdims=None):
     """{(kind, element): {threads}} over every guard-satisfying thread and loop point, or None
-    when an index cannot be evaluated (unknown variable, register load, pointer access)."""
+    when an index cannot be evaluated (unknown variable, register load, pointer access).
+    Thread ``t`` is the flat id; with several thread dimensions (``tdims`` = (X, Y, ...)) each
+    thread variable takes its own component ``(t // (X..)) % dim`` — without the dimensions a
+    multi-dimensional block is not provable here."""
     import itertools
     from ..ir.expr import EvalError, Var, evaluate, free_vars
-    names = {"tid": lambda t: t, "tid_": lambda t: t, "tx": lambda t: t, "lane": lambda t: t % 64,
+    tvars = tuple(tvars)
+    multi = len(tvars) > 1
+    if multi and (tdims is None or len(tdims) != len(tvars)):
+        return None
+    strides = []
+    acc = 1
+    for d in (tdims or [nthreads])[:max(1, len(tvars))]:
+        strides.append(acc)
+        acc *= int(d)
+    x_dim = int(tdims[0]) if multi else nthreads
+    names = {"tid": lambda t: t, "tid_": lambda t: t, "tx": lambda t: t % x_dim, "lane": lambda t: t % 64,
              "lane_": lambda t: t % 64, "wave": lambda t: t // 64, "wave_": lambda t: t // 64}
+
+    def tval(v, t):
+        if v in tvars:
+            d = tvars.index(v)
+            return (t // strides[d]) % int(tdims[d]) if multi else t
+        return names[v.name](t)
+
     out = {}
     for kind, idx, width in accs:
         if idx is None or any(not isinstance(i, PrimExpr) for i in idx):
@@ -352,9 +374,9 @@ def _elements_by_thread(accs, cond, nthreads, tvars, ranges):
         if pts * nthreads > _MAX_ENUM:
             return None
         for t in range(nthreads):
-            env = {v: (t if v in tvars else names[v.name](t)) for v in thread_like}
+            env = {v: tval(v, t) for v in thread_like}
             try:
-                cenv = {v: (t if v in tvars else names[v.name](t)) for v in free_vars(cond)
+                cenv = {v: tval(v, t) for v in free_vars(cond)
                         if v in tvars or v.name in names} if cond is not None else {}
                 if cond is not None and not evaluate(cond, cenv):
                     continue
@@ -373,7 +395,7 @@ def _elements_by_thread(accs, cond, nthreads, tvars, ranges):
     return out
 
 
-def _owned_per_instance(b, accs, cond, nthreads, tvars, inner, outer):
+def _owned_per_instance(b, accs, cond, nthreads, tvars, inner, outer, tdims=None):
     """True if, for every instance of the enclosing loops (barriers separate instances: the
     scan puts one in front of a loop-carried hazard), no element of ``b`` is written by one
     thread and read by another inside the branch; raises on a proven cross-thread pair;
@@ -394,7 +416,7 @@ def _owned_per_instance(b, accs, cond, nthreads, tvars, inner, outer):
         fixed = dict(zip(outer_vars, combo))
         from ..ir.expr import substitute
         accs_i = [(k, [substitute(i, fixed) for i in idx] if idx is not None else None, w) for k, idx, w in accs]
-        owners = _elements_by_thread(accs_i, cond, nthreads, tvars, inner)
+        owners = _elements_by_thread(accs_i, cond, nthreads, tvars, inner, tdims)
         if owners is None:
             return False
         for (kind, el), ts in owners.items():
@@ -410,7 +432,7 @@ def _owned_per_instance(b, accs, cond, nthreads, tvars, inner, outer):
     return True
 
 
-def _check_divergent_hazards(c: "S.IfStmt", managed, nthreads=0, tvars=(), outer_ranges=None):
+def _check_divergent_hazards(c: "S.IfStmt", managed, nthreads=0, tvars=(), outer_ranges=None, tdims=None):
     """Raise on an LDS hazard between accesses INSIDE a thread-dependent branch that crosses
     threads: a barrier cannot be placed there (it would deadlock), and leaving it out would be a
     race.  A write and a read (either order) of one element by two different threads is such a
@@ -435,7 +457,8 @@ def _check_divergent_hazards(c: "S.IfStmt", managed, nthreads=0, tvars=(), outer
             kinds = {k for k, _, _ in accs}
             if kinds != {"r", "w"}:
                 continue
-            if nthreads and _owned_per_instance(b, accs, c.cond, nthreads, tvars, inner, outer_ranges or {}):
+            if nthreads and _owned_per_instance(b, accs, c.cond, nthreads, tvars, inner, outer_ranges or {},
+                                                tdims):
                 continue
             keys_w = {repr(i) for k, i, _ in accs if k == "w"}
             keys_r = {repr(i) for k, i, _ in accs if k == "r"}
