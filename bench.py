@@ -46,8 +46,10 @@ GEMM_CFG = dict(M=4096, N=4096, K=4096, block_M=256, block_N=256, block_K=64, th
 # FA (scripts/sweep_fa.py, profiles/r2/fa_staged.log): 256x64 tile, 8 waves, Q in registers, 2-stage K/V
 # ring, T.Pipelined(order, stage) schedule: QK^T(t) | rescale+PV(t-1) | softmax(t)
 # sum_mfma: softmax row sums on the matrix cores (P x ones), +1.7-2 % (profiles/r3/s3/fa_sum_mfma_ab.log)
+# fold_max: running max as the QK^T accumulator's initial value, exp(t) between the PV(t-1) MFMAs
+# (+5-8 %), young_prio: waves 4-7 at issue priority 1 (+1-2 %) (profiles/r4/fa_fold_ab.log)
 ATTN_CFG = dict(batch=1, heads=64, seq_len=4096, dim=128, block_M=256, block_N=64, threads=512, num_stages=2,
-                q_in_regs=True, sum_mfma=True)
+                q_in_regs=True, sum_mfma=True, fold_max=True, young_prio=True)
 MOE_CFG = dict(tokens=2048, hidden=4096, ffn=2048, experts=8, topk=2)
 # --device cpu (CI plumbing run on the CPU target under gloo): same program, tiny shapes
 TINY = dict(gemm=dict(M=128, N=128, K=128, block_M=64, block_N=64, block_K=32, threads=128, num_stages=2),
@@ -95,7 +97,8 @@ def build_attn(device="cuda", a=None):
     a = a or ATTN_CFG
     f = flashattn.get_tir(a["batch"], a["heads"], a["seq_len"], a["dim"], False, 1, a["block_M"], a["block_N"],
                           a["threads"], a["num_stages"], "bfloat16", True, a.get("q_in_regs", False),
-                          sum_mfma=a.get("sum_mfma", False))
+                          sum_mfma=a.get("sum_mfma", False), fold_max=a.get("fold_max", False),
+                          young_prio=a.get("young_prio", False))
     k = tilelang.compile(f, out_idx=[3], target=_target(device), pass_configs=flashattn.pass_configs)
     shp = (a["batch"], a["seq_len"], a["heads"], a["dim"])
     return k, tuple(torch.randn(shp, device=device).to(torch.bfloat16) for _ in range(3))

@@ -4,9 +4,11 @@
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/deepseek_v32/inference/generate.py \
         --config examples/deepseek_v32/inference/config_671B_v3.2.json --layers 4
 
-Tensor + expert parallel over RCCL (``torch.distributed`` backend "nccl" on ROCm).  Weights are
-random (no checkpoint is available offline); ``--layers`` truncates the 61-layer config so a
-slice of the full-width model fits a quick run.  Prints tokens/s of the decode phase.
+Tensor + expert parallel over RCCL (``torch.distributed`` backend "nccl" on ROCm).  With
+``--ckpt-path`` every rank loads ``model{rank}-mp{world}.safetensors`` written by convert.py
+(reference generate.py:119); without it the weights are random.  ``--layers`` truncates the
+61-layer config so a slice of the full-width model fits a quick run.  Prints tokens/s of the
+decode phase.
 """
 import argparse
 import os
@@ -30,6 +32,7 @@ def main():
     ap.add_argument("--max-new-tokens", type=int, default=16)
     ap.add_argument("--max-seq-len", type=int, default=512)
     ap.add_argument("--temperature", type=float, default=0.0)
+    ap.add_argument("--ckpt-path", default=None, help="directory of convert.py shards")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -46,6 +49,9 @@ def main():
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     torch.manual_seed(0)
     model = Transformer(args, seed=0, device=dev)
+    if a.ckpt_path:
+        from tilelang.models.deepseek_v32_ckpt import load_model
+        load_model(model, os.path.join(a.ckpt_path, f"model{rank}-mp{world}.safetensors"))
     prompts = [torch.randint(0, args.vocab_size, (a.prompt_len, )).tolist() for _ in range(a.batch)]
     generate(model, prompts, 2)  # warm-up: compiles every kernel shape used by prefill + decode
     if dev == "cuda":

@@ -71,3 +71,73 @@ def test_fp8_checkpoint_format_model():
     assert rel < 0.15, rel
     m2 = Transformer(ModelArgs.tiny(gemm_impl="fp8", scale_fmt="ue8m0"), seed=0, device="cpu")
     assert torch.isfinite(m2(toks, 0)).all()
+
+
+def _ckpt_worker(rank, world, port, shard_dir, toks, out_path, over):
+    import torch.distributed as dist
+    from tilelang.models.deepseek_v32_ckpt import load_model
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = Transformer(ModelArgs.tiny(**over), seed=7, device="cpu")  # different random weights
+        load_model(m, os.path.join(shard_dir, f"model{rank}-mp{world}.safetensors"))
+        logits = m(toks, 0)
+        # the same global weights built directly for this world size: the loaded shards must
+        # reproduce them exactly (same kernels, same reduction order)
+        direct = Transformer(ModelArgs.tiny(**over), seed=0, device="cpu")(toks, 0)
+        torch.testing.assert_close(logits, direct, rtol=0, atol=0)
+        if rank == 0:
+            torch.save(logits, out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("gemm_impl", ["bf16", "fp8"])
+def test_checkpoint_convert_load_roundtrip(tmp_path, gemm_impl):
+    """HF-named safetensors (exported from a seed-0 model) -> convert.py-style per-rank shards
+    -> load into models built from a different seed: world 1 reproduces the logits exactly; at
+    world 2 (gloo, TP + EP shards) every rank reproduces the seed-0 world-2 model exactly, and
+    the bf16 logits match world 1 up to the reduction order (the fp8 model's routing is not
+    stable under a different all-reduce order: tiny sum differences flip fp8 activation codes)."""
+    from safetensors import safe_open
+    from tilelang.models.deepseek_v32_ckpt import convert, export_hf, load_model
+    over = dict(moe_inter_dim=256, gemm_impl=gemm_impl)
+    args = ModelArgs.tiny(**over)
+    toks = torch.randint(0, args.vocab_size, (2, 8), generator=torch.Generator().manual_seed(11))
+    src = Transformer(args, seed=0, device="cpu")
+    ref = src(toks, 0)
+    hf = tmp_path / "hf"
+    export_hf(src, str(hf), shard_size=40)
+    with safe_open(str(sorted(hf.glob("*.safetensors"))[0]), framework="pt") as f:
+        assert all(k.startswith("model.") or k.startswith("lm_head") for k in f.keys())
+    for mp_ in (1, 2):
+        paths = convert(str(hf), str(tmp_path / f"mp{mp_}"), args.n_routed_experts, mp_)
+        assert [os.path.basename(p) for p in paths] == [f"model{i}-mp{mp_}.safetensors" for i in range(mp_)]
+    if gemm_impl == "fp8":
+        with safe_open(str(tmp_path / "mp2" / "model0-mp2.safetensors"), framework="pt") as f:
+            assert f.get_tensor("layers.0.attn.wq_b.weight").dtype == torch.float8_e4m3fn
+            assert f.get_tensor("layers.0.attn.wq_b.scale").shape[0] * 2 == \
+                src.layers[0].attn.wq_b.scale.shape[0]
+    m1 = Transformer(args, seed=7, device="cpu")
+    assert not torch.equal(m1(toks, 0), ref)
+    m1 = Transformer(args, seed=7, device="cpu")
+    stats = load_model(m1, str(tmp_path / "mp1" / "model0-mp1.safetensors"))
+    assert stats["params"] == len(dict(m1.named_parameters()))
+    torch.testing.assert_close(m1(toks, 0), ref, rtol=0, atol=0)
+    out = str(tmp_path / "mp2.pt")
+    port = 29500 + (os.getpid() % 1500) + (7 if gemm_impl == "fp8" else 3)
+    mp.spawn(_ckpt_worker, args=(2, port, str(tmp_path / "mp2"), toks, out, over), nprocs=2, join=True)
+    if gemm_impl == "bf16":
+        torch.testing.assert_close(torch.load(out, weights_only=True), ref, rtol=3e-2, atol=3e-2)
+
+
+def test_checkpoint_load_is_strict(tmp_path):
+    from safetensors.torch import save_file
+    from tilelang.models.deepseek_v32_ckpt import load_model
+    m = Transformer(ModelArgs.tiny(), seed=0, device="cpu")
+    p = str(tmp_path / "bad.safetensors")
+    save_file({"embed.weight": m.embed.weight.detach().clone()}, p)
+    with pytest.raises(KeyError, match="checkpoint misses|no checkpoint tensor"):
+        load_model(m, p)

@@ -21,11 +21,16 @@ RCCL over xGMI); every projection is a tilelang MFMA GEMM; fp8 is OCP e4m3 (gfx9
 in the checkpoint's fp8 format -- OCP e4m3 with one fp32 scale per 128x128 block -- and runs it
 as ``act_quant`` (per-token, 128-wide groups; ``scale_fmt="ue8m0"`` for power-of-two scales) +
 the block-scaled fp8 GEMM (``tilelang.ops.fp8_gemm``, 2xAcc promotion), as the reference's
-``linear`` does (model.py:140-168).  The absorbed MLA up-projection dequantises ``wkv_b``
-(``weight_dequant``, model.py:514); routed experts stay on the bf16 grouped-GEMM kernels.
+``linear`` does (model.py:140-168).  The absorbed MLA up-projection dequantises ``wkv_b`` once
+(``weight_dequant``, model.py:514, cached as model.py:625 does) and runs as per-head MFMA GEMMs
+(``tilelang.ops.gemm.head_bmm``); routed experts stay on the bf16 grouped-GEMM kernels.
+Checkpoints: ``tilelang.models.deepseek_v32_ckpt`` converts HF-named safetensors into per-rank
+``model{rank}-mp{world}.safetensors`` shards and loads them (reference convert.py /
+generate.py:119).
 
-Simplifications (documented, weights are random -- no checkpoint is available): plain RoPE
-(no YaRN rescaling), no Hadamard rotation before the indexer's fp8 cast.
+Simplifications (documented; no real checkpoint is available offline, so tests round-trip
+synthetic weights through convert -> load): plain RoPE (no YaRN rescaling), no Hadamard rotation
+before the indexer's fp8 cast.
 """
 from __future__ import annotations
 
@@ -37,7 +42,7 @@ import torch.distributed as dist
 from torch import nn
 
 from ..ops import dsa
-from ..ops.gemm import linear
+from ..ops.gemm import head_bmm, linear
 from ..ops.moe import expert_ffn
 from ..ops.norm import rms_norm
 from ..ops.quant import act_quant
@@ -309,6 +314,16 @@ class MLA(nn.Module):
         B, S = args.max_batch_size, args.max_seq_len
         self.register_buffer("kv_cache", torch.zeros(B, S, self.kv_lora, dtype=dt), persistent=False)
         self.register_buffer("pe_cache", torch.zeros(B, S, self.rope, dtype=dt), persistent=False)
+        self._absorb = None
+
+    def absorbed(self):
+        """(W_uk^T [h, kv_lora, nope], W_uv [h, v, kv_lora]) in the compute dtype, dequantised from
+        the fp8 ``wkv_b`` ONCE and cached (reference model.py:625 keeps the dequantised weight);
+        ``load_model`` drops the cache when it replaces ``wkv_b``."""
+        if self._absorb is None:
+            w = self.wkv_b.dequant_weight().view(self.n_local_heads, self.nope + self.vdim, self.kv_lora)
+            self._absorb = (w[:, :self.nope].transpose(1, 2).contiguous(), w[:, self.nope:].contiguous())
+        return self._absorb
 
     def forward(self, x, start_pos, freqs):
         b, s, _ = x.shape
@@ -320,16 +335,16 @@ class MLA(nn.Module):
         latent, k_pe = kv[..., :self.kv_lora], kv[..., self.kv_lora:]
         self.kv_cache[:b, start_pos:end] = self.kv_norm(latent.contiguous())
         self.pe_cache[:b, start_pos:end] = apply_rotary_emb(k_pe.contiguous().unsqueeze(2), freqs).squeeze(2)
-        # absorb W_uk into the query: q_lat = q_nope @ W_uk  (per head)
-        wkv_b = self.wkv_b.dequant_weight().view(self.n_local_heads, self.nope + self.vdim, self.kv_lora)
-        q_lat = torch.einsum("bshd,hdc->bshc", q_nope.float(), wkv_b[:, :self.nope].float()).to(x.dtype)
+        # absorb W_uk into the query: q_lat[h] = q_nope[h] @ W_uk[h]  (one per-head MFMA GEMM)
+        w_uk_t, w_uv = self.absorbed()
+        q_lat = head_bmm(q_nope.contiguous(), w_uk_t)                           # [b, s, h, 512]
         qf = torch.cat([q_lat, q_pe], -1).contiguous()                          # [b, s, h, 576]
         kvf = torch.cat([self.kv_cache[:b, :end], self.pe_cache[:b, :end]], -1).unsqueeze(2).contiguous()
         idx = self.indexer(x, qr, start_pos, freqs).unsqueeze(2).contiguous()    # [b, s, 1, topk]
         kern = dsa.for_target("sparse_mla_fwd", _target(x), b, s, None, self.n_local_heads, self.kv_lora, self.rope,
                               idx.shape[-1], 1, self.softmax_scale, 64, None, _tdt(x.dtype))
         o_lat, _ = kern(qf, kvf, idx)                                             # [b, s, h, 512]
-        o = torch.einsum("bshc,hdc->bshd", o_lat.float(), wkv_b[:, -self.vdim:].float()).to(x.dtype)
+        o = head_bmm(o_lat.contiguous(), w_uv)                                  # [b, s, h, 128]
         return self.wo(o.reshape(b, s, -1))
 
 

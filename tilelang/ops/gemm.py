@@ -71,3 +71,47 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         K += pad
     k = _linear_kernel(M, N, K, _tdt(x2.dtype), "cpu" if x2.device.type == "cpu" else "hip")
     return k(x2, w2).reshape(*shp[:-1], N)
+
+
+@functools.lru_cache(maxsize=None)
+def _head_bmm_kernel(M, H, N, K, dtype, target):
+    bm, bn, bk, threads = _tiles(M, N, K, dtype)
+
+    @T.prim_func
+    def main(A: T.Tensor((M, H, K), dtype), W: T.Tensor((H, N, K), dtype), C: T.Tensor((M, H, N), dtype)):
+        with T.Kernel(T.ceildiv(N, bn), T.ceildiv(M, bm), H, threads=threads) as (bx, by, h):
+            A_s = T.alloc_shared((bm, bk), dtype)
+            W_s = T.alloc_shared((bn, bk), dtype)
+            acc = T.alloc_fragment((bm, bn), "float")
+            out = T.alloc_fragment((bm, bn), dtype)
+            T.clear(acc)
+            for k in T.Pipelined(T.ceildiv(K, bk), num_stages=2):
+                T.copy(A[by * bm:(by + 1) * bm, h, k * bk:(k + 1) * bk], A_s)
+                T.copy(W[h, bx * bn:(bx + 1) * bn, k * bk:(k + 1) * bk], W_s)
+                T.gemm(A_s, W_s, acc, transpose_B=True)
+            T.copy(acc, out)
+            T.copy(out, C[by * bm:(by + 1) * bm, h, bx * bn:(bx + 1) * bn])
+
+    return tilelang.compile(main, out_idx=[-1], target=target)
+
+
+def head_bmm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """Per-head GEMM: x [..., H, K] and w [H, N, K] -> [..., H, N], out[..., h, :] = x[..., h, :] @ w[h]^T
+    (MFMA, fp32 accumulation).  The absorbed MLA projections (query x W_uk, latent output x W_uv:
+    reference examples/deepseek_v32/inference/model.py:625-642) are this shape: one launch over
+    every head instead of a per-head loop or an fp32 einsum."""
+    shp = x.shape
+    H, N, K = w.shape
+    if shp[-2] != H or shp[-1] != K:
+        raise ValueError(f"head_bmm: x {tuple(shp)} does not match w {tuple(w.shape)}")
+    if w.dtype != x.dtype:
+        raise TypeError(f"head_bmm: x is {x.dtype} but w is {w.dtype}")
+    x3 = x.reshape(-1, H, K).contiguous()
+    w3 = w.contiguous()
+    if K % 32:
+        pad = (-K) % 32
+        x3 = torch.nn.functional.pad(x3, (0, pad))
+        w3 = torch.nn.functional.pad(w3, (0, pad))
+        K += pad
+    k = _head_bmm_kernel(x3.shape[0], H, N, K, _tdt(x3.dtype), "cpu" if x3.device.type == "cpu" else "hip")
+    return k(x3, w3).reshape(*shp[:-1], N)
