@@ -20,20 +20,24 @@ from tilelang.intrinsics import MatrixCoreIntrinEmitter, make_mfma_swizzle_layou
 @tilelang.jit(out_idx=[2])
 def tl_matmul(M, N, K, in_dtype="float16", out_dtype="float16", accum_dtype="float32", block_row_warps=2,
               block_col_warps=4, warp_row_tiles=128, warp_col_tiles=64, chunk=None, stage=2, micro_size=32,
-              k_pack=1, b_preshuffle=False, b_transposed=True, fp8_k_dim=None):
+              k_pack=1, b_preshuffle=False, b_transposed=True, fp8_k_dim=None, reduce_k=1):
+    """``reduce_k``: split every K stage over that many wave groups (thread binding 1) and sum the
+    partial accumulators through LDS before the store (the reference emitter's ``reduce_k``)."""
     emitter = MatrixCoreIntrinEmitter(in_dtype, in_dtype, accum_dtype, a_transposed=False, b_transposed=b_transposed,
                                       block_row_warps=block_row_warps, block_col_warps=block_col_warps,
                                       warp_row_tiles=warp_row_tiles, warp_col_tiles=warp_col_tiles,
                                       chunk=chunk or 1 << 30, micro_size=micro_size, k_pack=k_pack,
-                                      b_preshuffle=b_preshuffle, fp8_k_dim=fp8_k_dim)
+                                      b_preshuffle=b_preshuffle, fp8_k_dim=fp8_k_dim, reduce_k=reduce_k)
     pk = emitter.micro_size_k * k_pack
     if chunk is None:
         chunk = max(pk, 128 // (1 if in_dtype.startswith(("float8", "int8")) else 2))
-    emitter.chunk = chunk
+    emitter.chunk = chunk  # K per wave group per stage
     assert chunk % pk == 0
+    assert not (reduce_k > 1 and b_preshuffle), "reduce_k with LDS-staged operands only"
     block_M = block_row_warps * warp_row_tiles
     block_N = block_col_warps * warp_col_tiles
-    block_K = chunk
+    block_K = chunk * reduce_k
+    threads = emitter.threads if reduce_k == 1 else (emitter.threads // reduce_k, reduce_k)
     ms = micro_size
     if b_preshuffle:
         B_shape = (N // ms, K // pk, ms, pk) if b_transposed else (K // pk, N // ms, pk, ms)
@@ -44,7 +48,7 @@ def tl_matmul(M, N, K, in_dtype="float16", out_dtype="float16", accum_dtype="flo
     @T.prim_func
     def gemm_intrinsics(A: T.Tensor((M, K), in_dtype), B: T.Tensor(B_shape, in_dtype),
                         C: T.Tensor((M, N), out_dtype)):
-        with T.Kernel(T.ceildiv(N, block_N), T.ceildiv(M, block_M), threads=emitter.threads) as (bx, by):
+        with T.Kernel(T.ceildiv(N, block_N), T.ceildiv(M, block_M), threads=threads) as (bx, by):
             A_shared = T.alloc_shared((block_M, block_K), in_dtype)
             A_local = T.alloc_local((emitter.warp_rows * emitter.local_size_a, ), in_dtype)
             B_local = T.alloc_local((emitter.warp_cols * emitter.local_size_b, ), in_dtype)
@@ -57,6 +61,7 @@ def tl_matmul(M, N, K, in_dtype="float16", out_dtype="float16", accum_dtype="flo
                 T.annotate_layout({A_shared: make_mfma_swizzle_layout(A_shared)})
             T.use_swizzle(panel_size=8)
             T.clear(C_local)
+            rk = T.get_thread_binding(1) if reduce_k > 1 else 0
             for ko in T.Pipelined(K // block_K, num_stages=stage):
                 T.copy(A[by * block_M, ko * block_K], A_shared)
                 if not b_preshuffle:
@@ -64,14 +69,20 @@ def tl_matmul(M, N, K, in_dtype="float16", out_dtype="float16", accum_dtype="flo
                         T.copy(B[bx * block_N, ko * block_K], B_shared)
                     else:
                         T.copy(B[ko * block_K, bx * block_N], B_shared)
-                for ki in T.unroll(block_K // pk):
-                    emitter.ldmatrix_a(A_local, A_shared, ki)
+                for ki in T.unroll(chunk // pk):
+                    emitter.ldmatrix_a(A_local, A_shared, ki, rk=rk)
                     if b_preshuffle:
                         emitter.ldmatrix_b(B_local, B, ko * (block_K // pk) + ki, pid_m=by, pid_n=bx)
                     else:
-                        emitter.ldmatrix_b(B_local, B_shared, ki)
+                        emitter.ldmatrix_b(B_local, B_shared, ki, rk=rk)
                     emitter.mfma(A_local, B_local, C_local)
-            emitter.stmatrix(C_local, C, pid_m=by, pid_n=bx)
+            if reduce_k > 1:
+                C_red = T.alloc_shared(emitter.reduce_k_scratch_shape(), accum_dtype)
+                emitter.reduce_k_sum(C_local, C_red)
+                if rk == 0:
+                    emitter.stmatrix(C_local, C, pid_m=by, pid_n=bx)
+            else:
+                emitter.stmatrix(C_local, C, pid_m=by, pid_n=bx)
 
     return gemm_intrinsics
 

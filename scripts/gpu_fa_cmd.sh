@@ -1,4 +1,5 @@
 set -o pipefail
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_intrinsics.py -m gpu -k reduce_k > gpurun_out/rk_tests.log 2>&1 && \
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/r4pmc
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_r4a.log 2>&1 && \

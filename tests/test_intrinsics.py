@@ -92,3 +92,32 @@ def test_intrinsics_gemm_gpu(dt, kw):
         torch.testing.assert_close(c.cpu(), ref.int())
     else:
         torch.testing.assert_close(c.float().cpu(), ref, rtol=2e-2, atol=2e-2 * (K ** 0.5))
+
+
+_RK_CASES = [dict(reduce_k=2, block_row_warps=2, block_col_warps=2, warp_row_tiles=64, warp_col_tiles=64),
+             dict(reduce_k=4, micro_size=16, block_row_warps=1, block_col_warps=2, warp_row_tiles=64,
+                  warp_col_tiles=64, chunk=32)]
+
+
+@pytest.mark.parametrize("kw", _RK_CASES)
+def test_intrinsics_reduce_k_compiles(kw):
+    """reduce_k: the block runs (waves, reduce_k) threads, each wave group takes its K slice of
+    every stage, and the partial accumulators are summed through LDS behind a barrier."""
+    k = tilelang.compile(tl_matmul.get_tir(512, 512, 512, "float16", "float16", "float32", **kw), out_idx=[2],
+                         target="hip")
+    src = k.get_kernel_source()
+    assert "__launch_bounds__(%d)" % (64 * kw["block_row_warps"] * kw["block_col_warps"] * kw["reduce_k"]) in src
+    body = src[src.index("C_red"):]
+    first_store = body.index("C_red[")
+    assert "sync_threads" in body[first_store:] or "barrier" in body[first_store:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", _RK_CASES)
+def test_intrinsics_reduce_k_gpu(kw):
+    M, N, K = 512, 768, 1024
+    k = tl_matmul(M, N, K, "float16", "float16", "float32", **kw)
+    a = torch.randn(M, K, device="cuda").half()
+    b = torch.randn(N, K, device="cuda").half()
+    ref = a.cpu().float() @ b.cpu().float().T
+    torch.testing.assert_close(k(a, b).float().cpu(), ref, rtol=2e-2, atol=2e-2 * (K ** 0.5))

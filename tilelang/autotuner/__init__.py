@@ -6,7 +6,11 @@ with the non-tuned arguments it
   1. compiles every config concurrently (hipcc runs as subprocesses, so a thread pool
      scales; worker count from ``TILELANG_AUTO_TUNING_CPU_COUNTS`` / ``..._MAX_CPU_COUNT``),
   2. benchmarks the compiled kernels one at a time on the GPU (L2+MALL flush between
-     runs, per-config timeout, optional correctness check against ``ref_prog``),
+     runs, per-config timeout, optional correctness check against ``ref_prog``) -- on the
+     tensors captured by ``set_autotune_inputs`` when a capture is active; with
+     ``isolate=True`` (or ``TILELANG_AUTOTUNE_ISOLATE=1``) each config is checked and timed in a
+     child process that is killed at the timeout (``autotuner/worker.py``), so a kernel that
+     never returns costs one config, not the run,
   3. returns the fastest ``JITKernel`` with ``.config`` / ``.latency`` set, and
   4. persists the winner under ``$TILELANG_CACHE_DIR/autotuner/<sha256>.json`` so the
      next process skips the search.
@@ -53,6 +57,7 @@ class ProfileArgs:
     skip_check: bool = False
     manual_check_prog: Optional[Callable] = None
     cache_input_tensors: bool = True
+    isolate: Optional[bool] = None  # None: TILELANG_AUTOTUNE_ISOLATE
 
 
 @dataclass
@@ -137,9 +142,56 @@ class AutoTuner:
             src = inspect.getsource(fn)
         except (OSError, TypeError):
             src = fn.__qualname__
+        from .capture import get_autotune_inputs
+        cap = get_autotune_inputs()
+        cap_sig = None if cap is None else [(tuple(getattr(t, "shape", ())), str(getattr(t, "dtype", type(t))))
+                                            for t in cap]
         payload = json.dumps({"v": __version__, "src": src, "args": repr(args), "kwargs": repr(sorted(kwargs.items())),
-                              "configs": repr(self.configs), "target": str(self.compile_args.target)}, sort_keys=True)
+                              "configs": repr(self.configs), "target": str(self.compile_args.target),
+                              "captured": repr(cap_sig)}, sort_keys=True)
         return hashlib.sha256(payload.encode()).hexdigest()
+
+    def _bench_isolated(self, args, kwargs, cfg, inputs, warmup, rep, timeout) -> float:
+        """Check + time one config in a child process (new session, killed at ``timeout``)."""
+        import subprocess
+        import sys
+        import tempfile
+        import cloudpickle
+        import torch
+        pa = self.profile_args
+        with tempfile.TemporaryDirectory(prefix="tl_tune_") as d:
+            job = dict(fn=self.fn, args=args, kwargs=kwargs, cfg=cfg, warmup=warmup, rep=rep,
+                       supply_type=pa.supply_type, ref_prog=None if pa.skip_check else pa.ref_prog,
+                       manual_check_prog=None if pa.skip_check else pa.manual_check_prog, atol=pa.atol, rtol=pa.rtol,
+                       max_mismatched_ratio=pa.max_mismatched_ratio)
+            with open(os.path.join(d, "job.pkl"), "wb") as f:
+                cloudpickle.dump(job, f)
+            torch.save([t.detach().cpu() if isinstance(t, torch.Tensor) else t for t in inputs],
+                       os.path.join(d, "inputs.pt"))
+            env_ = dict(os.environ)
+            # the child resolves pickled-by-reference functions exactly as this process does
+            root = str(Path(__file__).resolve().parents[2])
+            paths = [root] + [p_ for p_ in sys.path if p_ and os.path.isdir(p_)]
+            env_["PYTHONPATH"] = os.pathsep.join(dict.fromkeys(paths))
+            p = subprocess.Popen([sys.executable, "-m", "tilelang.autotuner.worker", d], env=env_,
+                                 start_new_session=True, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+            try:
+                _, err = p.communicate(timeout=timeout)
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+                raise TimeoutException(f"config {cfg} exceeded {timeout}s in its worker process (killed)")
+            rp = os.path.join(d, "result.json")
+            if not os.path.exists(rp):
+                raise RuntimeError(f"worker exited with {p.returncode}: {err.decode(errors='replace')[-500:]}")
+            with open(rp) as f:
+                res = json.load(f)
+        if "latency" not in res:
+            raise RuntimeError(res.get("error", "worker failed"))
+        return float(res["latency"])
 
     def _compile(self, args, kwargs, cfg):
         merged = dict(kwargs)
@@ -174,8 +226,10 @@ class AutoTuner:
         logger.info("autotune: compiled %d/%d configs in %.1fs", sum(k is not None for k in kernels),
                     len(self.configs), time.time() - t0)
         best = AutotuneResult()
-        inputs = None
-        ref_out = None
+        from .capture import get_autotune_inputs
+        captured = get_autotune_inputs()
+        inputs = list(captured) if captured is not None else None
+        isolate = pa.isolate if pa.isolate is not None else os.environ.get("TILELANG_AUTOTUNE_ISOLATE", "0") == "1"
         for i, k in enumerate(kernels):
             cfg = self.configs[i]
             if k is None:
@@ -183,8 +237,14 @@ class AutoTuner:
                 continue
             try:
                 prof = k.get_profiler(pa.supply_type)
-                if inputs is None or not pa.cache_input_tensors:
+                if captured is None and (inputs is None or not pa.cache_input_tensors):
                     inputs = pa.supply_prog(k.params) if pa.supply_prog else prof._get_inputs()
+                if isolate:
+                    lat = self._bench_isolated(args, kwargs, cfg, inputs, warmup, rep, timeout)
+                    best.all_results.append({"config": cfg, "latency": lat})
+                    if lat < best.latency:
+                        best.latency, best.config, best.kernel = lat, cfg, k
+                    continue
                 if not pa.skip_check:
                     if pa.manual_check_prog is not None:
                         run_with_timeout(pa.manual_check_prog, timeout, k(*inputs), *inputs)
@@ -199,7 +259,8 @@ class AutoTuner:
             if lat < best.latency:
                 best.latency, best.config, best.kernel = lat, cfg, k
         if best.kernel is None:
-            raise RuntimeError(f"autotune: no config succeeded; errors: {list(errors.values())[:3]}")
+            errs = [r["error"] for r in best.all_results if r.get("error")]
+            raise RuntimeError(f"autotune: no config succeeded; errors: {errs[:3]}")
         if pa.ref_prog is not None and inputs is not None:
             try:
                 from ..profiler.bench import do_bench
@@ -235,11 +296,12 @@ class AutoTuneImpl:
 
 def autotune(func: Callable = None, *, configs=None, warmup: int = 25, rep: int = 100, timeout: int = 100,
              supply_type=None, ref_prog=None, supply_prog=None, rtol=1e-2, atol=1e-2, max_mismatched_ratio=0.01,
-             skip_check=False, manual_check_prog=None, cache_input_tensors=True):
+             skip_check=False, manual_check_prog=None, cache_input_tensors=True, isolate=None):
     """Decorator: ``@tilelang.autotune(configs=[{...}, ...])`` over ``@tilelang.jit``."""
     kw = dict(warmup=warmup, rep=rep, timeout=timeout, supply_type=supply_type, ref_prog=ref_prog,
               supply_prog=supply_prog, rtol=rtol, atol=atol, max_mismatched_ratio=max_mismatched_ratio,
-              skip_check=skip_check, manual_check_prog=manual_check_prog, cache_input_tensors=cache_input_tensors)
+              skip_check=skip_check, manual_check_prog=manual_check_prog, cache_input_tensors=cache_input_tensors,
+              isolate=isolate)
 
     def deco(fn):
         return AutoTuneImpl(fn, configs, **kw)
@@ -249,4 +311,7 @@ def autotune(func: Callable = None, *, configs=None, warmup: int = 25, rep: int 
     return deco
 
 
-__all__ = ["autotune", "AutoTuner", "AutotuneResult", "CompileArgs", "ProfileArgs", "run_with_timeout"]
+from .capture import set_autotune_inputs, get_autotune_inputs, AutotuneInputsCapture  # noqa: E402
+
+__all__ = ["autotune", "AutoTuner", "AutotuneResult", "CompileArgs", "ProfileArgs", "run_with_timeout",
+           "set_autotune_inputs", "get_autotune_inputs", "AutotuneInputsCapture"]

@@ -83,8 +83,8 @@ class MatrixCoreIntrinEmitter:
             raise ValueError("MatrixCoreIntrinEmitter: A and B need the same dtype (fp8 formats may mix)")
         if micro_size not in (16, 32):
             raise ValueError("MFMA emitter: micro_size is 16 or 32")
-        if reduce_k != 1:
-            raise NotImplementedError("MFMA emitter: reduce_k > 1 (split-K inside a block) is not supported")
+        if reduce_k < 1:
+            raise ValueError("MFMA emitter: reduce_k >= 1")
         if num_elems_per_byte != 1:
             raise NotImplementedError("MFMA emitter: packed sub-byte operands go through T.gemm / the MX path")
         int_acc = accum_dtype in ("int32", )
@@ -124,7 +124,11 @@ class MatrixCoreIntrinEmitter:
             raise ValueError(f"MFMA emitter: warp tiles must be multiples of {micro_size} and chunk of {pk}")
         self.warp_rows = warp_row_tiles // micro_size
         self.warp_cols = warp_col_tiles // micro_size
-        self.threads = WAVE * block_row_warps * block_col_warps
+        # reduce_k > 1: split-K inside the block.  The block is launched with threads
+        # (WAVE * block_row_warps * block_col_warps, reduce_k); wave group rk (thread binding 1)
+        # takes K slice [rk * chunk, (rk + 1) * chunk) of every stage (``ldmatrix_*(..., rk=rk)``)
+        # and ``reduce_k_sum`` adds the groups' accumulators through LDS.
+        self.threads = WAVE * block_row_warps * block_col_warps * reduce_k
         self.thread_var = thread_var
 
     # -- thread geometry -------------------------------------------------------------------
@@ -246,6 +250,32 @@ class MatrixCoreIntrinEmitter:
                                              T.address_of(B_local[j * self.local_size_b + p * kp])))
 
     mma = mfma
+
+    # -- split-K inside the block ------------------------------------------------------------
+    def reduce_k_scratch_shape(self):
+        """Shape of the LDS scratch ``reduce_k_sum`` needs: [reduce_k, acc, threads per group]
+        (thread-minor: a wave's 64 lanes store 64 consecutive dwords, no bank conflicts)."""
+        return (self.reduce_k, self.warp_rows * self.warp_cols * self.local_size_out,
+                WAVE * self.block_row_warps * self.block_col_warps)
+
+    def reduce_k_sum(self, C_local, scratch, rk=None):
+        """Sum the ``reduce_k`` wave groups' partial accumulators (reference: the ``reduce_k``
+        split of ``mfma_macro_generator.py:74``, summed in examples/dequantize_gemm/
+        example_dequant_gemm_fine_grained.py:316-335): every group stores its accumulators into
+        ``scratch`` (``reduce_k_scratch_shape()``, accum dtype, LDS), then every group reads the
+        total back into ``C_local`` (the barrier between the two is placed by ThreadSync)."""
+        if self.reduce_k == 1:
+            return
+        tx = self._tx()
+        rk = T.get_thread_binding(1) if rk is None else rk
+        n = self.warp_rows * self.warp_cols * self.local_size_out
+        for v in range(n):
+            scratch[rk, v, tx] = C_local[v]
+        for v in range(n):
+            acc = scratch[0, v, tx]
+            for r in range(1, self.reduce_k):
+                acc = acc + scratch[r, v, tx]
+            C_local[v] = acc
 
     # -- accumulator stores ------------------------------------------------------------------
     def _c_coord(self, lane, v):

@@ -7,6 +7,10 @@ writes 256 MB, sized for NVIDIA L2).  Reading matters on MI355X: a zero-fill lea
 streaming copy measured 4.4 TB/s after a write flush (gpurun_out r3 membound sweep), i.e. the
 flush's write-back was being billed to the kernel.  Timing uses HIP events on the
 current stream; ``backend="profiler"`` uses torch.profiler device time (rocprofiler).
+
+``flush_mode="write"`` (or ``TL_BENCH_FLUSH=write``) restores the reference's zero-fill flush for
+like-for-like comparisons with numbers measured that way; docs/RESULTS.md says which rows used
+which flush.
 """
 from __future__ import annotations
 
@@ -24,18 +28,26 @@ def _flush_buffer(device):
     return _FLUSH[device]
 
 
-def _flush(cache):
-    """Evict L2 + Infinity Cache without leaving dirty lines (a max-reduction over 512 MiB)."""
+def _flush(cache, mode: str = "read"):
+    """Evict L2 + Infinity Cache: "read" = a max-reduction over 512 MiB (leaves no dirty lines),
+    "write" = the reference's zero-fill."""
     import torch
     buf, out = cache
-    torch.amax(buf, dim=0, keepdim=True, out=out)
+    if mode == "write":
+        buf.zero_()
+    else:
+        torch.amax(buf, dim=0, keepdim=True, out=out)
 
 
 def do_bench(fn: Callable, warmup: float = 25, rep: float = 100, _n_warmup: int = 0, _n_repeat: int = 0,
              quantiles: Optional[List[float]] = None, fast_flush: bool = True, return_mode: str = "mean",
-             backend: str = "event", flush_l2: bool = True) -> float:
+             backend: str = "event", flush_l2: bool = True, flush_mode: Optional[str] = None) -> float:
     """Median/mean runtime of ``fn`` in milliseconds."""
+    import os
     import torch
+    flush_mode = flush_mode or os.environ.get("TL_BENCH_FLUSH", "read")
+    if flush_mode not in ("read", "write"):
+        raise ValueError(f"flush_mode must be 'read' or 'write', got {flush_mode!r}")
     assert return_mode in ("min", "max", "mean", "median")
     if backend in ("cupti", "profiler"):
         return _bench_profiler(fn, warmup, rep)
@@ -48,7 +60,7 @@ def do_bench(fn: Callable, warmup: float = 25, rep: float = 100, _n_warmup: int 
     s.record()
     for _ in range(5):
         if cache is not None:
-            _flush(cache)
+            _flush(cache, flush_mode)
         fn()
     e.record()
     torch.cuda.synchronize()
@@ -61,7 +73,7 @@ def do_bench(fn: Callable, warmup: float = 25, rep: float = 100, _n_warmup: int 
         fn()
     for i in range(n_repeat):
         if cache is not None:
-            _flush(cache)
+            _flush(cache, flush_mode)
         starts[i].record()
         fn()
         ends[i].record()
