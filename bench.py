@@ -324,6 +324,8 @@ def main():
     tp = tp_phase(mesh, dev, m, X, dist, timed, reps, cpu) if (moe is not None and mesh is not None) else None
     # box-speed normaliser: the vendor library (hipBLASLt via torch.matmul) on the same fp16 GEMM,
     # same process, same clocks; the driver-vs-builder gap of a run can be read against it
+    for _ in range(3):  # hipBLASLt loads and selects its kernel on the first calls
+        torch.matmul(A, B)
     vendor_ms = timed(lambda: torch.matmul(A, B), reps)
     dev_id = -1 if cpu else torch.cuda.current_device()
     bus = "cpu" if cpu else str(getattr(torch.cuda.get_device_properties(dev_id), "pci_bus_id", dev_id))
