@@ -1,6 +1,7 @@
 """Mamba-2 SSD chunk scan forward, b8 h80 g1 chunk 256 headdim 64 dstate 128, seq 1K ... 32K on one
 MI355X (reference: benchmark/mamba2/benchmark_mamba_chunk_scan.py and README.md:41-46, H800 SXM,
-same FLOP count).  Candidate tilings of examples/linear_attention/example_mamba_chunk_scan.py,
+same FLOP count).  Candidate tilings of examples/linear_attention/example_mamba_chunk_scan.py (the row-tiled
+``chunk_scan_fwd`` and the whole-chunk ``chunk_scan_fwd_fused``),
 checked against the fp32 einsum definition on the smallest row, fastest per row.
 """
 import os
@@ -11,14 +12,18 @@ from common import out_dir_arg, table, tune  # noqa: E402
 
 import torch  # noqa: E402
 
-from example_mamba_chunk_scan import chunk_scan_fwd, flops, make_inputs, ref_program  # noqa: E402
+from example_mamba_chunk_scan import chunk_scan_fwd, chunk_scan_fwd_fused, flops, make_inputs, ref_program  # noqa
 
 B, H, G, CH, P, N = 8, 80, 1, 256, 64, 128
 H800 = {1024: 126.477, 2048: 130.195, 4096: 133.054, 8192: 134.362, 16384: 135.711, 32768: 135.379}
 
 
 def configs():
-    return [dict(block_M=256, block_N=64, block_K=64, threads=256, num_stages=2),
+    return [dict(kernel="fused", block_K=64, threads=512, num_stages=2),
+            dict(kernel="fused", block_K=32, threads=512, num_stages=2),
+            dict(kernel="fused", block_K=64, threads=256, num_stages=2),
+            dict(kernel="fused", block_K=64, threads=512, num_stages=1),
+            dict(block_M=256, block_N=64, block_K=64, threads=256, num_stages=2),
             dict(block_M=256, block_N=64, block_K=64, threads=512, num_stages=2),
             dict(block_M=256, block_N=64, block_K=32, threads=256, num_stages=2),
             dict(block_M=128, block_N=64, block_K=64, threads=256, num_stages=2),
@@ -36,7 +41,9 @@ def main():
         ref = ref_program(*[t[:1] if t.dim() > 1 and t.shape[0] == B else t for t in args]) if L <= 2048 else None
 
         def build(cfg, L=L):
-            k = chunk_scan_fwd(B, L, CH, G, H, P, N, **cfg)
+            cfg = dict(cfg)
+            fac = chunk_scan_fwd_fused if cfg.pop("kernel", None) == "fused" else chunk_scan_fwd
+            k = fac(B, L, CH, G, H, P, N, **cfg)
             return lambda: k(*args)
 
         def check(fn):

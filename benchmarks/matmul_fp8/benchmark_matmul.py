@@ -20,9 +20,10 @@ H800 = {256: 569, 512: 858, 1024: 1129, 2048: 1343, 4096: 1467, 8192: 1507, 1638
 
 def configs(K):
     return [dict(block_M=256, block_N=256, block_K=128, threads=512, num_stages=2),
-            dict(block_M=256, block_N=256, block_K=256, threads=512, num_stages=2),
-            dict(block_M=256, block_N=128, block_K=128, threads=256, num_stages=2),
-            dict(block_M=128, block_N=128, block_K=128, threads=256, num_stages=3)]
+            dict(block_M=256, block_N=256, block_K=128, threads=512, num_stages=2, staged_epilogue=True),
+            dict(block_M=256, block_N=256, block_K=256, threads=512, num_stages=1, staged_epilogue=True),
+            dict(block_M=256, block_N=128, block_K=128, threads=256, num_stages=2, staged_epilogue=True),
+            dict(block_M=128, block_N=128, block_K=128, threads=256, num_stages=3, staged_epilogue=True)]
 
 
 def main():

@@ -8,11 +8,14 @@ import argparse
 
 import tilelang
 import tilelang.language as T
+from tilelang.layout import PaddedLayout
 
 
 @tilelang.jit(out_idx=[-1])
 def matmul(M, N, K, block_M=256, block_N=256, block_K=128, threads=512, num_stages=2, dtype="float8_e4m3fn",
-           out_dtype="bfloat16", accum_dtype="float", panel=8):
+           out_dtype="bfloat16", accum_dtype="float", panel=8, staged_epilogue=False):
+    """``staged_epilogue``: the C tile goes through row-padded LDS (the A/B ring's space, dead after
+    the loop) and leaves as row-contiguous 16-byte stores -- the small-K shapes are store-bound."""
 
     @T.prim_func
     def gemm_fp8(
@@ -30,7 +33,13 @@ def matmul(M, N, K, block_M=256, block_N=256, block_K=128, threads=512, num_stag
                 T.copy(A[by * block_M, k * block_K], A_shared)
                 T.copy(B[bx * block_N, k * block_K], B_shared)
                 T.gemm(A_shared, B_shared, C_local, transpose_B=True)
-            T.copy(C_local, C[by * block_M, bx * block_N])
+            if staged_epilogue:
+                C_shared = T.alloc_shared((block_M, block_N), out_dtype)
+                T.annotate_layout({C_shared: PaddedLayout((block_M, block_N), 8)})
+                T.copy(C_local, C_shared)
+                T.copy(C_shared, C[by * block_M, bx * block_N])
+            else:
+                T.copy(C_local, C[by * block_M, bx * block_N])
 
     return gemm_fp8
 

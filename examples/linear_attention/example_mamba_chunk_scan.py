@@ -89,6 +89,69 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
     return main
 
 
+@tilelang.jit(out_idx=[7], pass_configs=FAST_MATH)
+def chunk_scan_fwd_fused(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, block_K=64, num_stages=2,
+                         threads=512, dtype="float16"):
+    """One workgroup per (batch, chunk, head): the whole chunk's rows at once, so the per-chunk
+    vectors (dA in log2 units, dt) are loaded once into LDS as f32, the inter-chunk term is one
+    [chunk x dstate] x [dstate x headdim] MFMA GEMM, and the intra-chunk product streams ``cb``
+    and ``x`` in ``block_K``-wide slices through a pipelined LDS ring (LDS-DMA).  The slice loop
+    covers every row (masked entries are zeros), trading some wasted MFMA work on the upper
+    triangle for full-width GEMMs and no per-row-tile prologue."""
+    accum_dtype = "float"
+    nchunks = seqlen // chunk_size
+    assert seqlen % chunk_size == 0 and chunk_size % block_K == 0
+    hpg = nheads // ngroups
+
+    @T.prim_func
+    def main(cb: T.Tensor((batch, nchunks, ngroups, chunk_size, chunk_size), dtype),
+             x: T.Tensor((batch, seqlen, nheads, headdim), dtype),
+             dt: T.Tensor((batch, nheads, nchunks, chunk_size), dtype),
+             dA_cumsum: T.Tensor((batch, nheads, nchunks, chunk_size), dtype),
+             C: T.Tensor((batch, seqlen, ngroups, dstate), dtype),
+             prev_states: T.Tensor((batch, nchunks, nheads, headdim, dstate), dtype),
+             D: T.Tensor((nheads, ), dtype),
+             Output: T.Tensor((batch, seqlen, nheads, headdim), dtype)):
+        with T.Kernel(nheads, batch * nchunks, threads=threads) as (bz, by):
+            acc_o = T.alloc_fragment((chunk_size, headdim), accum_dtype)
+            a_s = T.alloc_shared((chunk_size, ), accum_dtype)
+            w_s = T.alloc_shared((chunk_size, ), accum_dtype)
+            C_shared = T.alloc_shared((chunk_size, dstate), dtype)
+            st_shared = T.alloc_shared((headdim, dstate), dtype)
+            cb_shared = T.alloc_shared((chunk_size, block_K), dtype)
+            cb_local = T.alloc_fragment((chunk_size, block_K), dtype)
+            x_shared = T.alloc_shared((block_K, headdim), dtype)
+            x_res = T.alloc_fragment((chunk_size, headdim), dtype)
+            o_cast = T.alloc_fragment((chunk_size, headdim), dtype)
+            b = by % batch
+            c = by // batch
+            g = bz // hpg
+            row0 = c * chunk_size
+            T.copy(C[b, row0:row0 + chunk_size, g, :], C_shared)
+            T.copy(prev_states[b, c, bz, :, :], st_shared)
+            for i in T.Parallel(chunk_size):
+                a_s[i] = T.Cast(accum_dtype, dA_cumsum[b, bz, c, i]) * LOG2E
+                w_s[i] = T.Cast(accum_dtype, dt[b, bz, c, i])
+            T.clear(acc_o)
+            T.gemm(C_shared, st_shared, acc_o, transpose_B=True)
+            for i, j in T.Parallel(chunk_size, headdim):
+                acc_o[i, j] *= T.exp2(a_s[i])
+            for k in T.Pipelined(chunk_size // block_K, num_stages=num_stages):
+                T.copy(cb[b, c, g, :, k * block_K:(k + 1) * block_K], cb_shared)
+                T.copy(x[b, row0 + k * block_K:row0 + (k + 1) * block_K, bz, :], x_shared)
+                for i, j in T.Parallel(chunk_size, block_K):
+                    cb_local[i, j] = T.if_then_else(
+                        i >= k * block_K + j,
+                        cb_shared[i, j] * T.exp2(a_s[i] - a_s[k * block_K + j]) * w_s[k * block_K + j], 0)
+                T.gemm(cb_local, x_shared, acc_o)
+            T.copy(x[b, row0:row0 + chunk_size, bz, :], x_res)
+            for i, j in T.Parallel(chunk_size, headdim):
+                o_cast[i, j] = acc_o[i, j] + x_res[i, j] * D[bz]
+            T.copy(o_cast, Output[b, row0:row0 + chunk_size, bz, :])
+
+    return main
+
+
 def ref_program(cb, x, dt, dA_cumsum, C, prev_states, D):
     import torch
     from einops import rearrange, repeat
