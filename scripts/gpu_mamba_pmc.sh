@@ -1,4 +1,5 @@
 set -o pipefail
+timeout -k 10 120 ./csrc/probes/mfma_fp6_probe > gpurun_out/fp6_probe.log 2>&1 && \
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/mpmc
 cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_ACTIVE_INST_LDS --output-format csv -d $R/gpurun_out/mpmc/p1 -o p -- python3 $R/scripts/prof_mamba.py 4096 5 > $R/gpurun_out/mpmc/p1.log 2>&1 && \
