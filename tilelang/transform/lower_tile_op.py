@@ -581,7 +581,12 @@ def vectorize_group(ctx: LowerCtx, stmts: List[S.Stmt], known_div) -> Optional[L
             if any(g is None for g in guards):
                 continue
             vload = L.VecLoadStmt(tmp, 0, ld0.buffer, ld0.indices[0], W)
-            if any(guards):
+            # an LDS read needs no guard: gfx950 bounds-checks DS addresses against the workgroup's
+            # allocation (out-of-range reads return 0, never fault), and a select then discards
+            # the value -- guarding it turned a masked T.Parallel into per-element exec-mask
+            # branches (SALU-bound; the Mamba chunk scan's causal CB mask, profiles/r4).  The CPU
+            # target keeps the guard: a host array read out of range can fault.
+            if any(guards) and (ld0.buffer.scope != "shared" or ctx.is_cpu):
                 # the element loads sit under bounds guards (selects): the vector load may only
                 # run when every lane's guard holds, otherwise fall back to guarded scalar loads
                 pred = None
