@@ -26,7 +26,8 @@ from example_mha_fwd import FAST_MATH, ref_program
 def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=256, block_N=64,
                         threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
                         young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd", mfma="16x16",
-                        sum_mfma=False, sink=False, sm_scale=None, fold_max=False, prescale_q=False):
+                        sum_mfma=False, sink=False, sm_scale=None, fold_max=False, prescale_q=False,
+                        pingpong=False):
     """``young_prio``: the second-dispatched half of the waves runs at issue priority 1 (one
     ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4).
     ``seq_kv`` (default ``seq_len``): key/value length; with ``is_causal`` the mask is aligned
@@ -49,7 +50,11 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     ``prescale_q`` (with ``fold_max``): the log2-domain scale c is folded into the Q registers
     once, so a probability is ONE ``v_exp_f32`` with no multiply; the price is Q rounded to bf16
     after scaling: a relative error of 2^-9 in every logit (at |c s| ~ 40 the probabilities of a
-    row are off by ~5 %, against ~1.5 % without it)."""
+    row are off by ~5 %, against ~1.5 % without it).
+    ``pingpong`` (with ``fold_max``): waves 4-7 run the same iteration in the order
+    rescale(t-1) | PV(t-1) | QK^T(t) | decide(t) | exp(t) (``T.Pipelined(order_alt=)``), so on every
+    SIMD one wave's softmax VALU phase sits under its partner's MFMAs instead of both waves
+    reaching their VALU phase together after each barrier."""
     scale = ((1.0 / dim)**0.5 if sm_scale is None else sm_scale) * 1.44269504
     head_kv = heads // groups
     seq_kv = seq_len if seq_kv is None else seq_kv
@@ -123,7 +128,9 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                         Q_s[i, j] = T.Cast(dtype, T.Cast(accum_dtype, Q_s[i, j]) * scale)
                 T.fill(scores_max, 0)
                 for k in T.Pipelined(loop_range, num_stages=num_stages, order=[-1, 0, 1, 2, -1, 3, 4],
-                                     stage=[-1, 0, 1, 0, -1, 1, 0], group=fold_group):
+                                     stage=[-1, 0, 1, 0, -1, 1, 0], group=fold_group,
+                                     order_alt=[-1, 2, 0, 3, -1, 1, 4] if pingpong else None,
+                                     alt_cond=(T.get_thread_binding() >= threads // 2) if pingpong else None):
                     # 0: K tile (producer)
                     if bhsd:
                         T.copy(K[bz, by // groups, k * block_N:(k + 1) * block_N, :], K_shared)

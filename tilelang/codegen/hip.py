@@ -261,6 +261,9 @@ class CodeGen:
             ws = self.name_of(ex["tl_gsync_ws"]["var"], "tl_gsync_ws")
             err = self.name_of(ex["tl_dev_err"]["var"], "tl_dev_err")
             return f"tl::sync_grid({ws}, {err})"
+        if op == "tl.unswitch":
+            c = self.e(args[0])
+            return f"({c})" if self.is_cpu else f"__builtin_amdgcn_readfirstlane((int)({c}))"
         if op == "tl.setprio":
             return "(void)0" if self.is_cpu else f"__builtin_amdgcn_s_setprio({int(args[0].value)})"
         raise CodeGenError(f"unknown intrinsic {op}")
@@ -305,7 +308,14 @@ class CodeGen:
             self.ind -= 1
             self.w("}")
         elif isinstance(st, S.IfStmt):
-            self.w(f"if ({self.e(st.cond)}) {{")
+            if not self.is_cpu and self._wave_uniform(st.cond):
+                # a condition on the thread index that is constant within every wave (e.g. wave
+                # >= 4 written as tid >= 256): evaluated per lane it is a VGPR compare and an
+                # exec-mask branch, so s_setprio / other scalar instructions inside run in EVERY
+                # wave (guide T5); readfirstlane makes it a scalar branch
+                self.w(f"if (__builtin_amdgcn_readfirstlane((int)({self.e(st.cond)}))) {{")
+            else:
+                self.w(f"if ({self.e(st.cond)}) {{")
             self.ind += 1
             self.s(st.then_body)
             self.ind -= 1
@@ -514,6 +524,53 @@ class CodeGen:
             out.append("}")
         ks.source = "\n".join(out) + "\n"
         return ks
+
+    def _wave_uniform(self, cond) -> bool:
+        """True if ``cond`` depends on thread indices only and takes one value per wave64 (checked
+        by evaluation over the workgroup's threads)."""
+        from ..ir.expr import EvalError, evaluate, free_vars
+        k = self.kernel
+        tvars = list(k.thread_vars or [])
+        tid = k.attrs.get("tid")
+        wave = k.attrs.get("wave")
+        lane = k.attrs.get("lane")
+        fv = free_vars(cond)
+        if not fv:
+            return False
+        dims = [int(t) for t in (k.threads or [1])]
+        n = 1
+        for d in dims:
+            n *= d
+        if n % 64 or n > 1024:
+            return False
+
+        def env_of(t):
+            env = {}
+            rem = t
+            for v, d in zip(tvars, dims):
+                env[v] = rem % d
+                rem //= d
+            if tid is not None:
+                env[tid] = t
+            if wave is not None:
+                env[wave] = t // 64
+            if lane is not None:
+                env[lane] = t % 64
+            return env
+
+        known = set(map(id, tvars)) | {id(x) for x in (tid, wave, lane) if x is not None}
+        if any(id(v) not in known for v in fv):
+            return False
+        if all(v is wave for v in fv):
+            return False  # already scalar (readfirstlane'd wave index)
+        try:
+            for w0 in range(0, n, 64):
+                first = bool(evaluate(cond, env_of(w0)))
+                if any(bool(evaluate(cond, env_of(t))) != first for t in range(w0 + 1, w0 + 64)):
+                    return False
+        except EvalError:
+            return False
+        return True
 
     def preamble(self, k: S.KernelStmt):
         tid = k.attrs.get("tid")

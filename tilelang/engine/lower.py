@@ -141,6 +141,8 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
         lk = hoist_dma_sources(lk)  # per-thread LDS-DMA source addresses out of pipelined loops
     if target.kind == "hip" and not cfg.get("tl.disable_thread_storage_sync", False):
         lk = insert_thread_sync(lk)
+    from ..transform.unswitch import unswitch_marked
+    lk = unswitch_marked(lk)  # T.Pipelined(order_alt=): one loop per wave group (after barriers)
     lk, offsets, total = plan_lds(lk, reuse=bool(cfg.get("tl.lds_reuse", True)),
                                   aggressive=bool(cfg.get("tl.enable_aggressive_shared_memory_merge", True)))
     if cfg.get("tl.layout_visualization_enable"):

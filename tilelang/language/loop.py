@@ -118,7 +118,8 @@ def grid(*extents):
     b.emit(body)
 
 
-def Pipelined(start, stop=None, num_stages: int = 0, order=None, stage=None, sync=None, group=None):
+def Pipelined(start, stop=None, num_stages: int = 0, order=None, stage=None, sync=None, group=None, order_alt=None,
+              alt_cond=None):
     """Software-pipelined loop: copies into shared buffers are multi-buffered ``num_stages`` deep.
 
     On gfx950 the global->LDS copies become ``global_load_lds_dwordx4`` DMA issued
@@ -138,6 +139,11 @@ def Pipelined(start, stop=None, num_stages: int = 0, order=None, stage=None, syn
         ann["sync"] = sync
     if group is not None:
         ann["group"] = group
+    if (order_alt is None) != (alt_cond is None):
+        raise ValueError("T.Pipelined: order_alt and alt_cond go together")
+    if order_alt is not None:
+        ann["order_alt"] = list(order_alt)
+        ann["alt_cond"] = alt_cond
     return _loop("pipelined", start, stop, None, ann, name="k")
 
 

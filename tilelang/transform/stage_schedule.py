@@ -87,6 +87,12 @@ class _StageSchedule(Mutator):
             raise ValueError(f"T.Pipelined group={group} must partition the {len(stmts)} statements of the loop body")
         if len(order) != len(group) or len(stage) != len(group):
             raise ValueError(f"T.Pipelined order={order} / stage={stage} need one entry per group ({len(group)})")
+        order_alt = list(ann.get("order_alt") or [])
+        if order_alt:
+            if len(order_alt) != len(group):
+                raise ValueError(f"T.Pipelined order_alt={order_alt} needs one entry per group ({len(group)})")
+            if any((order_alt[g] == -1) != (order[g] == -1) for g in range(len(group))):
+                raise ValueError("T.Pipelined: order_alt must keep the producers (order -1) of order")
         groups = [[stmts[i] for i in g] for g in group]
         compute = [gi for gi in range(len(groups)) if not (order[gi] == -1 and stage[gi] == -1)]
         producers = [gi for gi in range(len(groups)) if order[gi] == -1 and stage[gi] == -1]
@@ -111,9 +117,15 @@ class _StageSchedule(Mutator):
                 plan.append((stage[gi], groups[pi]))
             plan.append((stage[gi], groups[gi]))
         self._check_hazards(seq, stage, order, groups)
+        alt_plan = None
+        if order_alt:
+            seq_alt = sorted(compute, key=lambda gi: order_alt[gi])
+            self._check_hazards(seq_alt, stage, order_alt, groups)
+            alt_plan = [(stage[gi], groups[gi]) for gi in seq_alt]
         S_max = max(st for st, _ in plan)
         k, n, mn = s.var, s.extent, s.min
-        main_ann = {kk: v for kk, v in ann.items() if kk not in ("order", "stage", "group", "sync")}
+        main_ann = {kk: v for kk, v in ann.items() if kk not in ("order", "stage", "group", "sync", "order_alt",
+                                                                  "alt_cond")}
         if S_max == 0:
             return S.ForStmt(k, mn, n, "pipelined", S.seq(*[x for _, g in plan for x in g]), main_ann)
         nv = as_int(n)
@@ -134,8 +146,25 @@ class _StageSchedule(Mutator):
             prologue += parts
         # the main loop reuses the loop variable as the new-loop iteration counter t
         main_body = []
-        for st_, g in plan:
-            main_body += [subst_stmt(x, {k: binop("-", k, st_)}) for x in g]
+        if alt_plan is None:
+            for st_, g in plan:
+                main_body += [subst_stmt(x, {k: binop("-", k, st_)}) for x in g]
+        else:
+            # producers first (their copies become LDS-DMA issued ahead by the pipeline pass, so
+            # their place in the body only sets the issue point), then the compute in either order
+            prod_set = {id(x) for pi in producers for x in groups[pi]}
+            for st_, g in plan:
+                if all(id(x) in prod_set for x in g):
+                    main_body += [subst_stmt(x, {k: binop("-", k, st_)}) for x in g]
+            comp = [subst_stmt(x, {k: binop("-", k, st_)}) for st_, g in plan for x in g if id(x) not in prod_set]
+            comp_alt = [subst_stmt(x, {k: binop("-", k, st_)}) for st_, g in alt_plan for x in g]
+            # tl.unswitch: the condition is loop-invariant and wave-uniform; after pipelining and
+            # barrier placement the loop is unswitched (transform/unswitch.py) so each wave group
+            # runs a loop of its own order (one loop with the branch inside spilled: both orders'
+            # live ranges meet at the join)
+            from ..ir.expr import call as _call
+            cond = _call("tl.unswitch", [ann["alt_cond"]], "bool")
+            main_body.append(S.IfStmt(cond, S.seq(*comp_alt), S.seq(*comp)))
         main = S.ForStmt(k, binop("+", mn, S_max), binop("-", n, S_max), "pipelined", S.seq(*main_body), main_ann)
         if nv is not None and nv <= S_max:
             main = None
