@@ -127,3 +127,27 @@ def test_mx_gemm_preshuffled_gpu(af, bf):
     a, sa = m.quantize(torch.randn(M, K, device="cuda") * 3, af)
     b, sb = m.quantize(torch.randn(N, K, device="cuda") * 0.2, bf)
     _check(k(a, b, preshuffle_mx_scales(sa, 256, bk), preshuffle_mx_scales(sb, 256, bk)), a, b, sa, sb, af, bf)
+
+
+def test_mx_gemm_rejects_high_row_bit_swizzle():
+    """gemm_ss_mx derives each lane's swizzled address from row bits 0..3 only: an annotated LDS
+    swizzle on a higher row bit is a lowering error naming the tile, not a hipcc static_assert."""
+    import tilelang.language as T
+    from tilelang.layout.layout import SwizzleLayout
+
+    @T.prim_func
+    def prog(A: T.Tensor((64, 128), "float8_e4m3fn"), B: T.Tensor((64, 128), "float8_e4m3fn"),
+             SA: T.Tensor((64, 4), "uint8"), SB: T.Tensor((64, 4), "uint8"), C: T.Tensor((64, 64), "float32")):
+        with T.Kernel(1, threads=256):
+            A_s = T.alloc_shared((64, 128), "float8_e4m3fn")
+            B_s = T.alloc_shared((64, 128), "float8_e4m3fn")
+            C_l = T.alloc_fragment((64, 64), "float32")
+            T.annotate_layout({A_s: SwizzleLayout((64, 128), 1, [(5, 0), (1, 1)])})
+            T.copy(A, A_s)
+            T.copy(B, B_s)
+            T.clear(C_l)
+            T.gemm_scaled(A_s, B_s, C_l, SA, SB, transpose_B=True)
+            T.copy(C_l, C)
+
+    with pytest.raises(Exception, match="A_s.*row bit 5"):
+        tilelang.compile(prog, target="hip")

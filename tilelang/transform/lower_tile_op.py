@@ -1134,6 +1134,15 @@ class TileOpLowerer(Mutator):
             targs += [A.static_shape()[-1], B.static_shape()[-1], sa_shape[-1], sb_shape[-1], ps]
             out.append(L.CallStmt("tl::cpu_gemm_mx", [pa, pb, psa, psb, L.BufferPtr(cl, 0)], targs))
             return S.SeqStmt(out)
+        for buf in (A, B):
+            # gemm_ss_mx computes each lane's swizzled address once from row bits 0..3 (the 16 rows
+            # a lane group covers) and strides by 16 rows; a swizzle on a higher row bit breaks that
+            swz = gemm_lower.encode_swizzle(buf.layout)
+            hi = max(((swz >> (4 * cb)) & 15) for cb in range(8))
+            if hi > 4:
+                raise LoweringError(f"T.gemm_scaled: the LDS swizzle of {buf.name} XORs row bit {hi - 1} into the "
+                                    "column; block-scaled GEMM operands may only swizzle on row bits 0..3 "
+                                    "(drop the annotate_layout or use make_mfma_swizzle_layout)")
         targs += [plan["warp_m"], plan["warp_n"], A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
                   B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u", sa_shape[-1], sb_shape[-1], ps]
         out.append(L.CallStmt("tl::gemm_ss_mx", [pa, pb, psa, psb, L.BufferPtr(cl, 0), self.ctx.wave_expr()], targs))
