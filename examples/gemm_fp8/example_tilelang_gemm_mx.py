@@ -16,7 +16,12 @@ import argparse
 import tilelang
 import tilelang.language as T
 
-_DT = {"e4m3": "float8_e4m3fn", "e5m2": "float8_e5m2", "e2m1": "uint8"}
+_DT = {"e4m3": "float8_e4m3fn", "e5m2": "float8_e5m2", "e2m1": "uint8", "e2m3": "uint8", "e3m2": "uint8"}
+
+
+def _cols(k, fmt):
+    """Bytes of K elements: fp8 1 each, packed fp4 1/2, packed fp6 3/4."""
+    return k // 2 if fmt == "e2m1" else k * 3 // 4 if fmt in ("e2m3", "e3m2") else k
 
 
 @tilelang.jit(out_idx=[-1])
@@ -33,15 +38,13 @@ def mx_matmul(M, N, K, block_M=256, block_N=None, block_K=None, threads=512, num
     # fp4 x fp4 256x256x256 3.33 PF (256x128x256 3-stage 2.49), fp8 x fp8 256x256x128 1.86 PF
     # (256x128x128 3-stage 1.44), fp8 x fp4 256x256x128 2.26 PF
     if block_K is None:
-        block_K = 256 if a_fmt == b_fmt == "e2m1" else 128
+        block_K = 256 if a_fmt in _NARROW and b_fmt in _NARROW else 128
     if block_N is None:
         block_N = 256
     if num_stages is None:
         num_stages = 2
-    ac = K // 2 if a_fmt == "e2m1" else K
-    bc = K // 2 if b_fmt == "e2m1" else K
-    bka = block_K // 2 if a_fmt == "e2m1" else block_K
-    bkb = block_K // 2 if b_fmt == "e2m1" else block_K
+    ac, bc = _cols(K, a_fmt), _cols(K, b_fmt)
+    bka, bkb = _cols(block_K, a_fmt), _cols(block_K, b_fmt)
     sk = block_K // 32
     nk = K // block_K
     if preshuffle_scales:
@@ -80,6 +83,7 @@ def mx_matmul(M, N, K, block_M=256, block_N=None, block_K=None, threads=512, num
     return main
 
 
+_NARROW = ("e2m1", "e2m3", "e3m2")
 E2M1 = [0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0, -0.0, -0.5, -1.0, -1.5, -2.0, -3.0, -4.0, -6.0]
 
 
@@ -118,6 +122,9 @@ def _mx_matmul_ps(M, N, K, block_M, block_N, block_K, threads, num_stages, a_fmt
 def quantize(x, fmt):
     """fp32 [R, K] -> (MX elements as stored, e8m0 scales [R, K/32]) with per-block power-of-2 scales."""
     import torch
+    if fmt in ("e2m3", "e3m2"):
+        from tilelang.quantize import quantize_mxfp6
+        return quantize_mxfp6(x, fmt)
     R, K = x.shape
     blk = x.float().reshape(R, K // 32, 32)
     amax = blk.abs().amax(-1).clamp(min=1e-30)
@@ -138,6 +145,9 @@ def quantize(x, fmt):
 
 def dequantize(q, s, fmt):
     import torch
+    if fmt in ("e2m3", "e3m2"):
+        from tilelang.quantize import dequantize_mxfp6
+        return dequantize_mxfp6(q, s, fmt)
     if fmt == "e2m1":
         lut = torch.tensor(E2M1, device=q.device)
         lo, hi = (q & 15).long(), (q >> 4).long()
@@ -163,7 +173,7 @@ def main(M=8192, N=8192, K=8192, a_fmt="e4m3", b_fmt="e4m3"):
     print(f"MX {a_fmt}x{b_fmt} gemm {M}x{N}x{K}: {lat:.3f} ms, {2 * M * N * K / lat * 1e-9:.1f} TFLOPS")
     # the same GEMM with the scales pre-shuffled once (weights offline, activations by their quantizer)
     from tilelang.quantize import preshuffle_mx_scales
-    bk = 256 if a_fmt == b_fmt == "e2m1" else 128
+    bk = 256 if a_fmt in _NARROW and b_fmt in _NARROW else 128
     kps = mx_matmul(M, N, K, a_fmt=a_fmt, b_fmt=b_fmt, preshuffle_scales=True)
     pa, pb = preshuffle_mx_scales(sa, 256, bk), preshuffle_mx_scales(sb, 256, bk)
     torch.testing.assert_close(kps(a, b, pa, pb).float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())

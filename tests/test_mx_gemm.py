@@ -151,3 +151,34 @@ def test_mx_gemm_rejects_high_row_bit_swizzle():
 
     with pytest.raises(Exception, match="A_s.*row bit 5"):
         tilelang.compile(prog, target="hip")
+
+
+@pytest.mark.parametrize("af,bf", [("e2m3", "e2m3"), ("e3m2", "e4m3"), ("e2m1", "e3m2")])
+def test_mx_gemm_fp6_cpu(af, bf):
+    """Packed MXFP6 operands (4 elements per 3 bytes) against the fp32 dequantised product."""
+    import example_tilelang_gemm_mx as m
+    M = N = 64
+    K = 256
+    f = m.mx_matmul.get_tir(M, N, K, 64, 64, 128, 128, 2, af, bf)
+    k = tilelang.compile(f, out_idx=[-1], target="cpu")
+    a, sa = m.quantize(torch.randn(M, K) * 3, af)
+    b, sb = m.quantize(torch.randn(N, K) * 0.2, bf)
+    assert len(set(sa.flatten().tolist())) > 1
+    _check(k(a, b, sa, sb), a, b, sa, sb, af, bf)
+
+
+def test_fp6_pack_and_grid():
+    from tilelang.quantize import (dequantize_mxfp6, fp6_grid, pack_fp6, quantize_mxfp6, unpack_fp6)
+    assert fp6_grid("e2m3")[-1] == 7.5 and fp6_grid("e3m2")[-1] == 28.0
+    assert fp6_grid("e2m3")[1] == 0.125 and fp6_grid("e3m2")[1] == 0.0625  # subnormals
+    c = torch.randint(0, 64, (3, 64), dtype=torch.uint8)
+    p = pack_fp6(c)
+    assert p.shape == (3, 48) and torch.equal(unpack_fp6(p), c)
+    # element k at bits 6k..6k+5 of the row's little-endian bit stream
+    one = torch.zeros(1, 4, dtype=torch.uint8)
+    one[0, 1] = 63
+    assert pack_fp6(one).tolist() == [[0b11000000, 0b00001111, 0]]
+    w = torch.randn(4, 128)
+    for fmt, tol in (("e2m3", 0.05), ("e3m2", 0.09)):
+        q, s = quantize_mxfp6(w, fmt)
+        assert ((dequantize_mxfp6(q, s, fmt) - w).norm() / w.norm()).item() < tol

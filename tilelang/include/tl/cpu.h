@@ -213,7 +213,8 @@ inline void cpu_gemm(const T* A, const T* B, TC* C) {
     }
 }
 
-// OCP MX element decode (FMT: 0 e4m3, 1 e5m2, 4 e2m1 packed two per byte, low nibble first)
+// OCP MX element decode (FMT: 0 e4m3, 1 e5m2, 2 e2m3 / 3 e3m2 packed 4 per 3 bytes as a
+// little-endian bit stream (element k at bits 6k..6k+5), 4 e2m1 packed two per byte, low nibble first)
 template <int FMT> inline float mx_elem(const uint8_t* row, int k) {
   if constexpr (FMT == 0) {
     fp8_e4_t v;
@@ -223,6 +224,15 @@ template <int FMT> inline float mx_elem(const uint8_t* row, int k) {
     fp8_e5_t v;
     v.v = row[k];
     return (float)v;
+  } else if constexpr (FMT == 2 || FMT == 3) {
+    const int bit = 6 * k;
+    // the second byte only when the field straddles (the last field of a row ends on a byte)
+    const unsigned w = (unsigned)row[bit >> 3] | ((bit & 7) > 2 ? (unsigned)row[(bit >> 3) + 1] << 8 : 0u);
+    const unsigned c = (w >> (bit & 7)) & 63u;
+    constexpr int MB = FMT == 2 ? 3 : 2, BIAS = FMT == 2 ? 1 : 3;
+    const int e = (int)((c & 31u) >> MB), m = (int)(c & ((1u << MB) - 1));
+    const float mag = e == 0 ? std::ldexp((float)m, 1 - BIAS - MB) : std::ldexp((float)((1 << MB) + m), e - BIAS - MB);
+    return (c & 32u) ? -mag : mag;
   } else {
     static const float lut[8] = {0.0f, 0.5f, 1.0f, 1.5f, 2.0f, 3.0f, 4.0f, 6.0f};
     const uint8_t nib = (row[k >> 1] >> (4 * (k & 1))) & 15;

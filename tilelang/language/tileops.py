@@ -149,10 +149,9 @@ def _mx_format(region, fmt):
                              f"a_format/b_format (one of {sorted(_MX_FORMATS)})")
     if fmt not in _MX_FORMATS:
         raise ValueError(f"T.gemm_scaled: unknown MX format {fmt!r} (one of {sorted(_MX_FORMATS)})")
-    if fmt in ("e2m3", "e3m2"):
-        raise NotImplementedError("T.gemm_scaled: fp6 operands (e2m3/e3m2) are not lowered yet; use fp8 or fp4")
     if dt.bits != 8:
-        raise ValueError(f"T.gemm_scaled: MX operands are byte buffers (fp8, or packed fp4 pairs), got {dt}")
+        raise ValueError(f"T.gemm_scaled: MX operands are byte buffers (fp8, packed fp6 or packed fp4 pairs), "
+                         f"got {dt}")
     return fmt
 
 
@@ -163,7 +162,8 @@ def gemm_scaled(A, B, C, scale_A, scale_B, transpose_A=False, transpose_B=True, 
     gfx950 ``v_mfma_scale_f32_16x16x128_f8f6f4``: the hardware applies one e8m0 scale per
     32 consecutive K elements of every row.  ``A``: ``[M, K]`` fp8 (e4m3/e5m2) or ``[M, K/2]``
     packed fp4 pairs (``float4_e2m1fn_x2`` / uint8 with ``a_format="e2m1"``, low nibble =
-    even element); ``B``: ``[N, K]`` likewise (``transpose_B=True``, both K-contiguous);
+    even element) or ``[M, 3K/4]`` packed fp6 (uint8 with ``a_format="e2m3"`` / ``"e3m2"``, four
+    elements per three bytes, ``tilelang.quantize.pack_fp6``); ``B``: ``[N, K]`` likewise (``transpose_B=True``, both K-contiguous);
     ``scale_A``: ``[M, K/32]`` and ``scale_B``: ``[N, K/32]`` e8m0 bytes (shared or global).
     K must be a multiple of 128.
 

@@ -138,9 +138,92 @@ def dequantize_mxfp4(packed, scales_e8m0, block: int = 32):
     return (v.reshape(*shp[:-1], shp[-1] // block, block) * s.unsqueeze(-1)).reshape(shp)
 
 
+def fp6_grid(fmt: str):
+    """The non-negative values of an OCP fp6 format, indexed by the 5-bit magnitude code:
+    e2m3 (bias 1, max 7.5) or e3m2 (bias 3, max 28); subnormals at exponent 0, no inf/nan."""
+    if fmt == "e2m3":
+        eb, mb, bias = 2, 3, 1
+    elif fmt == "e3m2":
+        eb, mb, bias = 3, 2, 3
+    else:
+        raise ValueError(f"fp6 format must be 'e2m3' or 'e3m2', got {fmt!r}")
+    out = []
+    for code in range(32):
+        e, m = code >> mb, code & ((1 << mb) - 1)
+        if e == 0:
+            out.append(m / (1 << mb) * 2.0**(1 - bias))
+        else:
+            out.append((1 + m / (1 << mb)) * 2.0**(e - bias))
+    return out
+
+
+def float_to_fp6(x, fmt: str):
+    """Round-to-nearest onto the fp6 grid (saturating); uint8 codes, bit 5 = sign."""
+    import torch
+    grid = torch.tensor(fp6_grid(fmt), device=x.device)
+    mag = x.abs().clamp(max=grid[-1].item())
+    code = (mag.unsqueeze(-1) - grid).abs().argmin(-1).to(torch.uint8)
+    return code | ((x < 0).to(torch.uint8) << 5)
+
+
+def fp6_to_float_torch(code, fmt: str):
+    import torch
+    grid = torch.tensor(fp6_grid(fmt), device=code.device)
+    mag = grid[(code & 31).long()]
+    return torch.where((code & 32) != 0, -mag, mag)
+
+
+def pack_fp6(codes):
+    """``[..., K]`` 6-bit codes -> ``[..., 3K/4]`` bytes: a little-endian bit stream, element k at
+    bits 6k..6k+5 of its row (4 elements per 3 bytes)."""
+    import torch
+    c = codes.to(torch.int32)
+    shp = c.shape
+    if shp[-1] % 4:
+        raise ValueError(f"pack_fp6: the last dim ({shp[-1]}) must be a multiple of 4")
+    q = c.reshape(*shp[:-1], shp[-1] // 4, 4)
+    w = q[..., 0] | (q[..., 1] << 6) | (q[..., 2] << 12) | (q[..., 3] << 18)
+    b = torch.stack([w & 255, (w >> 8) & 255, (w >> 16) & 255], -1)
+    return b.reshape(*shp[:-1], shp[-1] // 4 * 3).to(torch.uint8).contiguous()
+
+
+def unpack_fp6(packed):
+    import torch
+    b = packed.to(torch.int32)
+    shp = b.shape
+    t = b.reshape(*shp[:-1], shp[-1] // 3, 3)
+    w = t[..., 0] | (t[..., 1] << 8) | (t[..., 2] << 16)
+    q = torch.stack([(w >> (6 * i)) & 63 for i in range(4)], -1)
+    return q.reshape(*shp[:-1], shp[-1] // 3 * 4).to(torch.uint8)
+
+
+def quantize_mxfp6(W, fmt: str = "e2m3", block: int = 32) -> Tuple:
+    """OCP MXFP6: per 32 elements an e8m0 scale 2^(floor(log2(amax)) - emax) with emax the
+    format's largest exponent (2 for e2m3, 4 for e3m2), elements rounded to the fp6 grid and
+    packed with ``pack_fp6``.  Returns (packed bytes ``[..., 3K/4]``, scales ``[..., K/32]``)."""
+    import torch
+    emax = {"e2m3": 2, "e3m2": 4}[fmt]
+    shp = W.shape
+    g = W.float().reshape(*shp[:-1], shp[-1] // block, block)
+    amax = g.abs().amax(-1).clamp(min=2.0**-126)
+    e = torch.floor(torch.log2(amax)) - emax
+    codes = float_to_fp6(g / torch.exp2(e).unsqueeze(-1), fmt).reshape(shp)
+    return pack_fp6(codes), (e + 127).clamp(0, 254).to(torch.uint8)
+
+
+def dequantize_mxfp6(packed, scales_e8m0, fmt: str = "e2m3", block: int = 32):
+    import torch
+    v = fp6_to_float_torch(unpack_fp6(packed), fmt)
+    shp = v.shape
+    s = torch.exp2(scales_e8m0.float() - 127.0)
+    return (v.reshape(*shp[:-1], shp[-1] // block, block) * s.unsqueeze(-1)).reshape(shp)
+
+
 __all__ = ["int4_to_float", "uint4_to_float", "e2m1_to_float", "fp4_to_float", "e8m0_to_float", "pack_int4",
            "unpack_int4", "quantize_int4_groupwise", "dequantize_int4_groupwise", "float_to_e2m1",
-           "e2m1_to_float_torch", "quantize_mxfp4", "dequantize_mxfp4"]
+           "e2m1_to_float_torch", "quantize_mxfp4", "dequantize_mxfp4", "fp6_grid", "float_to_fp6",
+           "fp6_to_float_torch", "pack_fp6", "unpack_fp6", "quantize_mxfp6", "dequantize_mxfp6",
+           "preshuffle_mx_scales"]
 
 
 def preshuffle_mx_scales(scales, block_rows: int, block_K: int):

@@ -47,13 +47,26 @@ def encode_swizzle(layout) -> int:
 MX_CODES = {"e4m3": 0, "e5m2": 1, "e2m3": 2, "e3m2": 3, "e2m1": 4}
 
 
+_FP6 = ("e2m3", "e3m2")
+
+
+def _mx_k(cols: int, fmt: str, name: str) -> int:
+    """K elements in a row of ``cols`` bytes: fp8 1 per byte, fp4 2, fp6 4 per 3 bytes."""
+    if fmt == "e2m1":
+        return cols * 2
+    if fmt in ("e2m3", "e3m2"):
+        if cols % 3:
+            raise ValueError(f"T.gemm_scaled: packed fp6 operand {name} has {cols} bytes per row, not a multiple of 3")
+        return cols * 4 // 3
+    return cols
+
+
 def _mx_plan(op: O.GemmOp, plan: Dict, num_threads: int, a_ext, b_ext, is_cpu: bool = False) -> Dict:
     """Block-scaled MX GEMM (v_mfma_scale_f32_16x16x128_f8f6f4): both operands K-contiguous in LDS,
     one e8m0 scale per 32 K of every row of A and of B."""
     A, B = op.A.buffer, op.B.buffer
     M, N = plan["M"], plan["N"]
-    ka = a_ext[1] * (2 if op.a_fmt == "e2m1" else 1)
-    kb = b_ext[1] * (2 if op.b_fmt == "e2m1" else 1)
+    ka, kb = _mx_k(a_ext[1], op.a_fmt, "A"), _mx_k(b_ext[1], op.b_fmt, "B")
     if ka != kb:
         raise ValueError(f"T.gemm_scaled: A holds K={ka} and B holds K={kb} elements")
     K = ka
@@ -80,6 +93,9 @@ def _mx_plan(op: O.GemmOp, plan: Dict, num_threads: int, a_ext, b_ext, is_cpu: b
         return plan
     if num_threads % 64:
         raise ValueError(f"block size {num_threads} is not a multiple of the 64-lane wavefront")
+    if op.a_fmt in _FP6 or op.b_fmt in _FP6:
+        raise NotImplementedError("T.gemm_scaled: packed fp6 operands run on the CPU target; the gfx950 "
+                                  "lowering is not available yet")
     warp_m, warp_n = MF.compute_warp_partition(M, N, num_threads // 64, op.policy)
     plan.update(K=K, warp_m=warp_m, warp_n=warp_n, mfma=(16, 16, 128), mx=True,
                 a_code=MX_CODES[op.a_fmt], b_code=MX_CODES[op.b_fmt])
