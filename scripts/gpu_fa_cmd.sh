@@ -1,7 +1,3 @@
 set -o pipefail
-R=$GRAFT_REPO_ROOT
-mkdir -p gpurun_out/benchmarks
-timeout -k 10 500 python -u scripts/fa_variants.py '[{"sum_mfma": true, "fold_max": true}, {"sum_mfma": true, "fold_max": true, "young_prio": true}, {"sum_mfma": true, "fold_max": true, "pingpong": true}, {"sum_mfma": true, "fold_max": true, "pingpong": true, "young_prio": true}, {"fold_max": true, "pingpong": true}, {"sum_mfma": true, "fold_max": true}]' > gpurun_out/fa_v4.log 2>&1 && \
-timeout -k 10 120 ./csrc/probes/mfma_fp6_probe2 > gpurun_out/fp6_probe2.log 2>&1 && \
-timeout -k 10 600 python -u benchmarks/mamba2/benchmark_mamba_chunk_scan.py --out gpurun_out/benchmarks --rows 1024,4096,16384 > gpurun_out/benchmarks/mamba2_b.log 2>&1 && \
-timeout -k 10 600 python -u benchmarks/matmul_fp8/benchmark_matmul.py --out gpurun_out/benchmarks --rows 256,512,1024,4096 > gpurun_out/benchmarks/matmul_fp8_b.log 2>&1
+mkdir -p gpurun_out
+timeout -k 10 500 python -u scripts/fa_variants.py '[{"sum_mfma": true, "fold_max": true}, {"sum_mfma": true, "fold_max": true, "young_prio": true}, {"sum_mfma": true, "fold_max": true, "pingpong": true}, {"sum_mfma": true, "fold_max": true, "pingpong": true, "young_prio": true}, {"sum_mfma": true, "fold_max": true}]' > gpurun_out/fa_v4.log 2>&1

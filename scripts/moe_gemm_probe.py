@@ -25,8 +25,9 @@ n = T_ * TOP
 
 
 def run(ids, tag, BM=256, **kw):
-    max_rows = K.max_padded_rows(K._bucket(n), E, BM)
-    dest, row_src, te, counts, trows = K.dispatch_plan(ids, E, BM, max_rows, TOP)
+    ext = kw.get("ext_M", 0)
+    max_rows = K.max_padded_rows(K._bucket(n), E, BM + ext)
+    dest, row_src, te, counts, trows = K.dispatch_plan(ids, E, BM + ext, max_rows, TOP, even=ext > 0)
     act = torch.empty(max_rows, F, dtype=x.dtype, device=dev)
     y = torch.empty(max_rows, H, dtype=x.dtype, device=dev)
     k1 = K.expert_gemm_sk_kernel(max_rows, H, 2 * F, E, "bfloat16", "hip", BM, n_src=T_, swiglu=True, **kw)
@@ -42,12 +43,22 @@ def run(ids, tag, BM=256, **kw):
 
 bal = torch.arange(n, device=dev, dtype=torch.int32) % E  # exactly n/E rows per expert
 rnd = torch.randint(0, E, (n, ), device=dev, dtype=torch.int32)
-for kw in ({}, dict(BM=128), dict(BM=128, threads=256), {}):
+VARIANTS = eval(sys.argv[1]) if len(sys.argv) > 1 else ({}, dict(BM=128), dict(BM=128, threads=256), {})
+for kw in VARIANTS:
     try:
         run(bal, "balanced", **kw)
         run(rnd, "random  ", **kw)
     except Exception as e:  # noqa: BLE001
         print(kw, "failed", str(e)[:200], flush=True)
+# the whole bench layer (router, dispatch, both GEMMs, combine) per gemm_cfg
+from tilelang.models.moe import MoEConfig, MoELayer  # noqa: E402
+for ext in (0, 32, 0, 32):
+    cfg = MoEConfig(hidden=H, ffn=F, n_experts=E, topk=TOP, dtype=torch.bfloat16, block_M=BM,
+                    gemm_cfg=dict(block_N=256, block_K=64, num_stages=2, threads=512, ext_M=ext))
+    layer = MoELayer(cfg, "local", device=dev)
+    xs = torch.randn(T_, H, device=dev, dtype=torch.bfloat16)
+    t = do_bench(lambda: layer(xs), warmup=10, rep=50)
+    print(f"MoE layer ext_M={ext}: {t * 1e3:.1f} us {6.0 * n * H * F / t * 1e-9:.0f} TF", flush=True)
 from example_gemm import matmul  # noqa: E402
 g = matmul(4096, 4096, 4096, 256, 256, 64, 512, 2, staged_epilogue=True)
 a, b = torch.randn(4096, 4096, device=dev).half(), torch.randn(4096, 4096, device=dev).half()

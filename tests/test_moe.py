@@ -110,13 +110,15 @@ def test_tp_expert_gemm_workspace_and_grid():
     assert meta["ws_bytes"] * 10 <= one_shot_per_tile, (meta, one_shot_per_tile)
 
 
+@pytest.mark.parametrize("ext", [0, 16])
 @pytest.mark.parametrize("n_cu", [3, 5, 8])
-def test_moe_tail_balanced_cpu(n_cu):
+def test_moe_tail_balanced_cpu(n_cu, ext):
     """Tail-balanced expert GEMMs: whole leading units, the trailing partial round as narrow tiles
-    (n_cu chosen so the tail has 1-2 rounds of narrow tiles, or is empty)."""
+    (n_cu chosen so the tail has 1-2 rounds of narrow tiles, or is empty); ``ext``: row-tile slots
+    of block_M + ext rows with every expert's rows spread evenly over its slots."""
     cfg = MoEConfig(hidden=64, ffn=64, n_experts=4, topk=2, dtype=torch.float32, block_M=16,
                     gemm_cfg=dict(block_N=64, block_K=32, num_stages=2, threads=128, stream_k=True, n_cu=n_cu,
-                                  tail_split=2))
+                                  tail_split=2, ext_M=ext))
     layer = MoELayer(cfg, "local", device="cpu")
     x = torch.randn(50, 64)
     out = layer(x).float()
@@ -136,11 +138,13 @@ def test_moe_tail_balanced_gpu():
     g, w1, w2 = (t.to("cuda") for t in init_moe_weights(cfg))
     from tilelang.ops import moe as K
     ref = moe_reference(x, g, w1, w2, cfg.topk, routing=K.route(x, g, cfg.topk))
-    for sk, ph, skip in ((True, False, True), (False, False, True), (True, True, True), (True, True, False)):
+    for sk, ph, skip, ext in ((True, False, True, 0), (False, False, True, 0), (True, True, True, 0),
+                              (True, True, False, 0), (True, False, True, 32)):
         # phased: K-half ring with register-prefetched fragments; skip: padding waves skip
-        # their reads and MFMAs (T.gemm(valid_m=)) inside the prefetched schedule too
+        # their reads and MFMAs (T.gemm(valid_m=)) inside the prefetched schedule too; ext: 288-row
+        # slots (256 + a 32-row extension GEMM on the same W tile), rows spread evenly per expert
         layer.cfg.gemm_cfg = dict(block_N=256, block_K=64, num_stages=2, threads=512, stream_k=sk, phased=ph,
-                                  skip_padding=skip)
+                                  skip_padding=skip, ext_M=ext)
         out = layer(x).float()
         torch.testing.assert_close(out, ref, rtol=3e-2, atol=3e-2 * ref.abs().max().item())
 

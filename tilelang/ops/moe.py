@@ -175,7 +175,7 @@ def max_padded_rows(n_assign: int, E: int, block_M: int) -> int:
 
 @functools.lru_cache(maxsize=None)
 def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: str, stable: bool = False,
-                 threads: int = 1024, full_first: bool = True):
+                 threads: int = 1024, full_first: bool = True, even: bool = False):
     """Dispatch plan of ``n`` assignments (``expert_ids[n]``; assignment ``j`` reads source row
     ``j // div``; a negative id is an empty slot: not placed, ``dest[j] = -1``): ``dest[j]`` (its
     padded row), ``row_src[max_rows]``, ``tile_expert``, ``counts[E]``,
@@ -191,11 +191,32 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
     per expert with a remainder.  The tail-balanced expert GEMM runs the leading units as whole
     tiles and splits only the trailing ones: with the partial tiles (usually a few valid rows)
     last, the whole-tile rounds are all full tiles and the split tail is the nearly-empty work
-    (before, an expert's partial tile sat between full ones and full tiles landed in the tail)."""
+    (before, an expert's partial tile sat between full ones and full tiles landed in the tail).
+
+    ``even``: an expert's ``cnt`` rows are spread evenly over its ``ceil(cnt / block_M)`` row tiles
+    (the first ``cnt % n`` tiles hold one row more), not filled tile by tile.  With ``block_M`` a
+    row-tile *slot* of ``main + ext`` rows (``expert_gemm_sk_kernel(ext_M=)``) an expert of 529
+    rows becomes two tiles of 265 / 264 rows -- two units of a one-round grid -- instead of two
+    full tiles plus a 17-row tile that costs a whole extra round."""
+    if even:
+        full_first = False
     n_tiles = max_rows // block_M
     if stable:
         threads = 256
     c = -(-n // threads)
+
+    def _units(c):  # row tiles of an expert with c rows
+        return (c + block_M - 1) // block_M
+
+    def _even_row(sl, c):
+        """Padded offset of the expert's sl-th row under the even split: tile j holds q + (j < r)
+        rows, q = c // n, r = c % n, n = _units(c)."""
+        nu = T.max(_units(c), 1)
+        q = c // nu
+        big = (q + 1) * (c % nu)
+        j = T.if_then_else(sl < big, sl // (q + 1), c % nu + (sl - big) // T.max(q, 1))
+        off = T.if_then_else(sl < big, sl % (q + 1), (sl - big) % T.max(q, 1))
+        return j * block_M + off
 
     @T.prim_func
     def moe_align(expert_ids: T.Tensor((n,), "int32"), dest: T.Tensor((n,), "int32"),
@@ -273,6 +294,11 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                         if cnt[e] % block_M > 0 and tt * block_M == pstart[e]:
                             te = e
                             tr = cnt[e] % block_M
+                    elif even:
+                        if tt * block_M >= start[e] and tt * block_M < start[e] + _units(cnt[e]) * block_M:
+                            te = e
+                            tr = cnt[e] // _units(cnt[e]) + T.if_then_else(
+                                (tt * block_M - start[e]) // block_M < cnt[e] % _units(cnt[e]), 1, 0)
                     else:
                         if tt * block_M >= start[e] and tt * block_M < start[e] + cnt[e]:
                             te = e
@@ -292,6 +318,8 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                                 sl = d - start[e_]
                                 d = T.if_then_else(sl < cnt[e_] // block_M * block_M, d,
                                                    pstart[e_] + sl - cnt[e_] // block_M * block_M)
+                            if even:
+                                d = start[e_] + _even_row(d - start[e_], cnt[e_])
                             dest[t * c + i] = d
                             row_src[d] = (t * c + i) // div
                         if t * c + i < n and expert_ids[t * c + i] < 0:
@@ -306,6 +334,10 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                                                pstart[e_] + slot - cnt[e_] // block_M * block_M)
                             dest[j] = d
                             row_src[d] = j // div
+                        elif even:
+                            d = start[e_] + _even_row(slot, cnt[e_])
+                            dest[j] = d
+                            row_src[d] = j // div
                         else:
                             dest[j] = start[e_] + slot
                             row_src[start[e_] + slot] = j // div
@@ -313,6 +345,7 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                         dest[j] = -1
 
     return tilelang.compile(moe_align, out_idx=None, target=target)
+
 
 
 @functools.lru_cache(maxsize=None)
@@ -417,8 +450,15 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
                           block_N: int = 256, block_K: int = 64, num_stages: int = 2, threads: int = 512,
                           n_src: Optional[int] = None, swiglu: bool = False, n_cu: int = 256, tail_split: int = 4,
                           phased: bool = False, skip_padding: bool = True, partial_first: bool = False,
-                          tail_ksplit: int = 0, tail_stages: Optional[int] = None):
+                          tail_ksplit: int = 0, tail_stages: Optional[int] = None, ext_M: int = 0):
     """Tail-balanced variant of ``expert_gemm_kernel`` (same arguments and output).
+
+    ``ext_M`` > 0: a row tile is a slot of ``block_M + ext_M`` rows (the dispatch layout's
+    ``block_M`` is that slot, ``align_kernel(even=True)``): the first ``block_M`` rows run as the
+    usual tile, rows ``block_M..`` as an ``ext_M x block_N`` extension GEMM on the SAME W tile in
+    the same K loop (its own small gather; waves split it by columns so every wave skips the same
+    empty fragments).  A 529-row expert is then two units of 265 / 264 rows, 12.5 % more MFMA
+    work on one of them, instead of a 17-row third unit that needs its own pass over W.
 
     ``tail_ksplit`` = S > 0: the trailing units run as S K-chunks each (full tile width) instead of
     narrow tiles.  Measured SLOWER on the bench layer (GEMM1 173 -> 255 / 357 / 572 us for S = 2 /
@@ -443,7 +483,9 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
     one short round instead of a long one).  No K split, so no partial sums, workspace or second
     kernel; the SwiGLU epilogue's 4-column groups stay inside a narrow tile.  Every workgroup
     derives U and R from ``tile_expert`` (the real tiles are a prefix): nothing waits on the host."""
-    n_tiles = max_rows // block_M
+    slot = block_M + ext_M
+    assert not (ext_M and tail_ksplit), "ext_M runs with the narrow-tile tail"
+    n_tiles = max_rows // slot
     n_by = (N + block_N - 1) // block_N
     nk = (K + block_K - 1) // block_K
     bn_t = block_N // tail_split
@@ -461,29 +503,47 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
     n_out = N // 2 if swiglu else N
 
     @T.macro
-    def tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, bx_raw, e_raw, col0, bn, stages):
+    def tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, bx_raw, e_raw, col0, bn, stages, A_x=None, C_x=None):
         # tile / expert ids come from device tables: clamp them so the operand copies are provably
         # in bounds (LDS-DMA instead of guarded register staging) and read them once per tile
         bx = T.min(bx_raw, n_tiles - 1)  # expressions, so the bounds prover sees the clamps
         e = T.min(T.max(e_raw, 0), E - 1)
         nrows = T.alloc_var("int32")
         nrows = tile_rows[bx]
+        r0 = bx * slot
         T.clear(C_l)
+        if ext_M:
+            T.clear(C_x)
         for k in T.Pipelined(nk, num_stages=stages):
             if n_src is not None:
-                T.gather_rows(A[:, k * block_K:(k + 1) * block_K], row_src[bx * block_M:(bx + 1) * block_M], A_s,
-                              row_dim=0)
+                T.gather_rows(A[:, k * block_K:(k + 1) * block_K], row_src[r0:r0 + block_M], A_s, row_dim=0)
+                if ext_M:
+                    T.gather_rows(A[:, k * block_K:(k + 1) * block_K], row_src[r0 + block_M:r0 + slot], A_x,
+                                  row_dim=0)
             else:
-                T.copy(A[bx * block_M, k * block_K], A_s)
+                T.copy(A[r0, k * block_K], A_s)
+                if ext_M:
+                    T.copy(A[r0 + block_M, k * block_K], A_x)
             T.copy(W[e, col0, k * block_K], W_s)
             T.gemm(A_s, W_s, C_l, transpose_B=True, valid_m=nrows if skip_padding else None)
+            if ext_M:
+                # column-split waves (when the tile is wide enough) all skip the same empty fragments
+                T.gemm(A_x, W_s, C_x, transpose_B=True, valid_m=nrows - block_M,
+                       policy=T.GemmWarpPolicy.FullCol if bn // 16 >= threads // 64 else T.GemmWarpPolicy.Square)
         if swiglu:
             for i, j in T.Parallel(block_M, bn):
                 if j % 4 < 2:
-                    C[bx * block_M + i, col0 // 2 + (j // 4) * 2 + j % 4] = T.Cast(
+                    C[r0 + i, col0 // 2 + (j // 4) * 2 + j % 4] = T.Cast(
                         dtype, C_l[i, j] / (1.0 + T.exp(-C_l[i, j])) * C_l[i, j + 2])
+            if ext_M:
+                for i, j in T.Parallel(ext_M, bn):
+                    if j % 4 < 2:
+                        C[r0 + block_M + i, col0 // 2 + (j // 4) * 2 + j % 4] = T.Cast(
+                            dtype, C_x[i, j] / (1.0 + T.exp(-C_x[i, j])) * C_x[i, j + 2])
         else:
-            T.copy(C_l, C[bx * block_M, col0])
+            T.copy(C_l, C[r0, col0])
+            if ext_M:
+                T.copy(C_x, C[r0 + block_M, col0])
 
     S_ = max(1, tail_ksplit)
     nks = nk // S_
@@ -590,6 +650,11 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
             C_l = T.alloc_fragment((block_M, block_N), accum)
             Wt_s = T.alloc_shared((bn_t, block_K), dtype)
             Ct_l = T.alloc_fragment((block_M, bn_t), accum)
+            A_x = C_x = Ct_x = None
+            if ext_M:
+                A_x = T.alloc_shared((ext_M, block_K), dtype)
+                C_x = T.alloc_fragment((ext_M, block_N), accum)
+                Ct_x = T.alloc_fragment((ext_M, bn_t), accum)
             nt = T.alloc_var("int32")
             nfull = T.alloc_var("int32")
             nt = 0
@@ -597,7 +662,7 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
             for t in T.serial(n_tiles):
                 if tile_expert[t] >= 0:
                     nt = t + 1
-                    if tile_rows[t] == block_M:
+                    if tile_rows[t] >= block_M:
                         nfull = t + 1
             units = nt * n_by
             full = units - units % n_cu
@@ -606,13 +671,13 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
             for it in T.serial(full // n_cu):  # whole tiles
                 u = (pid + it * n_cu + shift) % units
                 tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, u // n_by, tile_expert[u // n_by],
-                     (u % n_by) * block_N, block_N, num_stages)
+                     (u % n_by) * block_N, block_N, num_stages, A_x, C_x)
             for it in T.serial(T.ceildiv((units - full) * tail_split, n_cu)):  # narrow tail tiles
                 q = pid + it * n_cu
                 if q < (units - full) * tail_split:
                     u = (full + q // tail_split + shift) % units
                     tile(A, W, row_src, tile_rows, C, A_s, Wt_s, Ct_l, u // n_by, tile_expert[u // n_by],
-                         (u % n_by) * block_N + (q % tail_split) * bn_t, bn_t, t_stages)
+                         (u % n_by) * block_N + (q % tail_split) * bn_t, bn_t, t_stages, A_x, Ct_x)
 
     # K-half phased main loop (row gathers included) measured slower here: 382-403 vs 300-356 us per
     # layer (profiles/r2/session2/moe_phased_tail_sweep.log), so off by default
@@ -702,8 +767,9 @@ def route(x: torch.Tensor, gate_w: torch.Tensor, topk: int):
 
 
 def dispatch_plan(expert_ids: torch.Tensor, E: int, block_M: int, max_rows: int, div: int = 1,
-                  stable: bool = False):
-    """Device-side padded placement: ``(dest[n], row_src[max_rows], tile_expert, counts[E], tile_rows)``."""
+                  stable: bool = False, even: bool = False):
+    """Device-side padded placement: ``(dest[n], row_src[max_rows], tile_expert, counts[E], tile_rows)``.
+    ``even``: rows spread evenly over each expert's row tiles (``align_kernel(even=True)``)."""
     dev = expert_ids.device
     n = expert_ids.numel()
     ids = expert_ids.reshape(-1).to(torch.int32).contiguous()
@@ -712,7 +778,8 @@ def dispatch_plan(expert_ids: torch.Tensor, E: int, block_M: int, max_rows: int,
     te = torch.empty(max_rows // block_M, dtype=torch.int32, device=dev)
     counts = torch.empty(E, dtype=torch.int32, device=dev)
     tile_rows = torch.empty(max_rows // block_M, dtype=torch.int32, device=dev)
-    align_kernel(n, E, block_M, max_rows, div, _target(dev), stable)(ids, dest, row_src, te, counts, tile_rows)
+    align_kernel(n, E, block_M, max_rows, div, _target(dev), stable, even=even)(ids, dest, row_src, te, counts,
+                                                                                tile_rows)
     return dest, row_src, te, counts, tile_rows
 
 
@@ -748,17 +815,22 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
     dev = src_rows.device
     tgt = _tdt(src_rows.dtype)
     target = _target(dev)
-    max_rows = max_padded_rows(_bucket(n), E, block_M)
-    n_src = _bucket(src_rows.shape[0])
-    if src_rows.shape[0] != n_src:
-        src_rows = torch.cat([src_rows, src_rows.new_zeros(n_src - src_rows.shape[0], src_rows.shape[1])])
-    dest, row_src, te, _, trows = dispatch_plan(expert_ids, E, block_M, max_rows, div, stable=reduce_mesh is not None)
-    act = torch.empty(max_rows, F, dtype=src_rows.dtype, device=dev)
     sk = cfg.pop("stream_k", None)
     n_cu = cfg.pop("n_cu", 256)
     if sk is None:
         sk = target == "hip"
-    if sk and reduce_mesh is None and w1_interleaved:
+    sk = sk and reduce_mesh is None and w1_interleaved
+    ext = cfg.pop("ext_M", 0) if sk else 0
+    cfg.pop("ext_M", None)
+    slot = block_M + ext
+    max_rows = max_padded_rows(_bucket(n), E, slot)
+    n_src = _bucket(src_rows.shape[0])
+    if src_rows.shape[0] != n_src:
+        src_rows = torch.cat([src_rows, src_rows.new_zeros(n_src - src_rows.shape[0], src_rows.shape[1])])
+    dest, row_src, te, _, trows = dispatch_plan(expert_ids, E, slot, max_rows, div, stable=reduce_mesh is not None,
+                                                even=ext > 0)
+    act = torch.empty(max_rows, F, dtype=src_rows.dtype, device=dev)
+    if sk:
         # tail-balanced grid: whole tiles for the leading rounds, narrow tiles for the trailing partial round
         skc = {k: v for k, v in cfg.items() if k in ("block_N", "block_K", "num_stages", "threads", "tail_split",
                                                       "phased", "skip_padding", "tail_ksplit", "tail_stages")}
@@ -768,9 +840,10 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
         if skc.get("tail_ksplit"):
             ws = _tail_workspace(dev, n_cu, skc["tail_ksplit"], block_M, skc.get("block_N", 256))
         k1 = expert_gemm_sk_kernel(max_rows, H, F2, E, tgt, target, block_M, n_src=n_src, swiglu=True, n_cu=n_cu,
-                                   **skc)
+                                   ext_M=ext, **skc)
         k1(src_rows.contiguous(), w1, te, row_src, trows, act, *ws)
-        k2 = expert_gemm_sk_kernel(max_rows, F, H, E, tgt, target, block_M, n_cu=n_cu, partial_first=pf2, **skc)
+        k2 = expert_gemm_sk_kernel(max_rows, F, H, E, tgt, target, block_M, n_cu=n_cu, partial_first=pf2,
+                                   ext_M=ext, **skc)
         y = torch.empty(max_rows, H, dtype=src_rows.dtype, device=dev)
         k2(act, w2, te, row_src, trows, y, *ws)
         return y, dest
