@@ -163,7 +163,8 @@ def gemm_scaled(A, B, C, scale_A, scale_B, transpose_A=False, transpose_B=True, 
     32 consecutive K elements of every row.  ``A``: ``[M, K]`` fp8 (e4m3/e5m2) or ``[M, K/2]``
     packed fp4 pairs (``float4_e2m1fn_x2`` / uint8 with ``a_format="e2m1"``, low nibble =
     even element) or ``[M, 3K/4]`` packed fp6 (uint8 with ``a_format="e2m3"`` / ``"e3m2"``, four
-    elements per three bytes, ``tilelang.quantize.pack_fp6``); ``B``: ``[N, K]`` likewise (``transpose_B=True``, both K-contiguous);
+    elements per three bytes, ``tilelang.quantize.pack_fp6``); ``B``: ``[N, K]`` likewise
+    (``transpose_B=True``, both K-contiguous);
     ``scale_A``: ``[M, K/32]`` and ``scale_B``: ``[N, K/32]`` e8m0 bytes (shared or global).
     K must be a multiple of 128.
 
