@@ -3,6 +3,7 @@ definition on random data AND on data whose logits move the row max by far more 
 threshold (q scaled x8: the rescale branch fires), then warm and cold TFLOPS.
 
     python scripts/fa_variants.py '[{"sum_mfma": true}, {"sum_mfma": true, "fold_max": true}]' [--causal]
+    (a variant's "_pc" entry adds pass configs: {"fold_max": true, "_pc": {"tl.gemm_rs_pipe": 4}})
 """
 import json
 import os
@@ -40,11 +41,14 @@ q_hot = (q.float() * 8).to(torch.bfloat16)
 refs = {"rand": ref(q, heads), "hot": ref(q_hot, heads)}
 for kw in variants:
     a = dict(block_M=256, block_N=64, threads=512, num_stages=2, q_in_regs=True)
-    a.update(kw)
     tag = json.dumps(kw, sort_keys=True)
+    kw = dict(kw)
+    pc = dict(flashattn_pipelined.pass_configs)
+    pc.update(kw.pop("_pc", {}))  # extra pass configs, e.g. {"tl.gemm_rs_pipe": 4}
+    a.update(kw)
     try:
         f = flashattn_pipelined.get_tir(B, H, S, D, causal, 1, **a)
-        kern = tilelang.compile(f, out_idx=[3], target="hip", pass_configs=flashattn_pipelined.pass_configs)
+        kern = tilelang.compile(f, out_idx=[3], target="hip", pass_configs=pc)
         errs = []
         for name, qq in (("rand", q), ("hot", q_hot)):
             o = kern(qq, k, v)

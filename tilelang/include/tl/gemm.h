@@ -225,7 +225,15 @@ TL_DEVICE void gemm_ss_mma(const ss_frags<T, M, N, K, WARP_M, WARP_N>& __restric
 
 // A operand in registers (gemm_rs): a_regs holds the A fragment, 8 elements per (mi, kk) at
 // a_regs + (mi*KSTEPS + kk)*8.  KPERM=1 when the fragment came from an accumulator layout.
-template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TB, int B_COLS, uint32_t SWZ_B, int KPERM>
+//
+// PIPE = G > 0 (pass config tl.gemm_rs_pipe): the B fragments stream through the MFMAs in groups
+// of G: group g+1's ds_reads are pinned 1:1 (or 1 : reads-per-MFMA) between group g's MFMAs,
+// across K steps too, so at most two groups are in flight.  Without it the compiler issues every
+// read of a K step first and then waits for all of them: with 16 transposed reads (the PV GEMM of
+// attention, 8 fragments x 2 ds_read_b64_tr_b16) that is more than the 15 the lgkmcnt counter can
+// track, so the first MFMA waits on lgkmcnt(0) -- the whole K step's LDS latency, exposed.
+template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TB, int B_COLS, uint32_t SWZ_B, int KPERM,
+          int PIPE = 0>
 TL_DEVICE void gemm_rs(const T* __restrict__ a_regs, const T* __restrict__ B, float* __restrict__ C,
                        int wave_in = -1) {
   typedef mfma_traits<T> MT;
@@ -237,6 +245,65 @@ TL_DEVICE void gemm_rs(const T* __restrict__ a_regs, const T* __restrict__ B, fl
   const int wave = wave_or(wave_in);
   const int wn = wave % WARP_N;
   floatx4* acc = reinterpret_cast<floatx4*>(C);
+  if constexpr (PIPE > 0 && N_REP % PIPE == 0 && KSTEPS * N_REP > PIPE) {
+    constexpr int G = PIPE, NG = KSTEPS * N_REP / G;  // groups of G fragments, in (kk, ni) order
+    constexpr int RPF = TB ? 1 : 2;                    // ds_reads per fragment
+    F b[NG][G];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        const int q = g * G + j, kk = q / N_REP, ni = q % N_REP;
+        b[g][j] = ld_operand<T, (TB ? N : K), B_COLS, SWZ_B, !TB, KPERM>(B, wn * WN + ni * 16, kk * 32, lane);
+      }
+      if (g > 0) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          const int q = (g - 1) * G + j, kk = q / N_REP, ni = q % N_REP;
+#pragma unroll
+          for (int mi = 0; mi < M_REP; ++mi) {
+            F a;
+            __builtin_memcpy(&a, a_regs + (mi * KSTEPS + kk) * 8, sizeof(F));
+            acc[mi * N_REP + ni] = MT::mma16(b[g - 1][j], a, acc[mi * N_REP + ni]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int q = (NG - 1) * G + j, kk = q / N_REP, ni = q % N_REP;
+#pragma unroll
+      for (int mi = 0; mi < M_REP; ++mi) {
+        F a;
+        __builtin_memcpy(&a, a_regs + (mi * KSTEPS + kk) * 8, sizeof(F));
+        acc[mi * N_REP + ni] = MT::mma16(b[NG - 1][j], a, acc[mi * N_REP + ni]);
+      }
+    }
+    // schedule: group 0's reads, then each later group's reads spread over the previous group's
+    // MFMAs (M_REP MFMAs per fragment against RPF reads), then the last group's MFMAs
+    constexpr int MF = G * M_REP, RD = G * RPF;
+    __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
+#pragma unroll
+    for (int g = 1; g < NG; ++g) {
+      if constexpr (MF >= RD) {
+#pragma unroll
+        for (int i = 0; i < RD; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, MF / RD, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        if constexpr (MF % RD) __builtin_amdgcn_sched_group_barrier(0x008, MF % RD, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, RD / MF, 0);
+        }
+        if constexpr (RD % MF) __builtin_amdgcn_sched_group_barrier(0x100, RD % MF, 0);
+      }
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);
+    return;
+  }
 #pragma unroll
   for (int kk = 0; kk < KSTEPS; ++kk) {
     F b[N_REP];

@@ -1109,7 +1109,7 @@ class TileOpLowerer(Mutator):
                 raise LoweringError("register A operand cannot be transposed")
             out.append(L.CallStmt("tl::gemm_rs", [L.BufferPtr(al, 0), pb, L.BufferPtr(cl, 0), ctx.wave_expr()], [
                 ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_B), b_cols,
-                f"{swz_b}u", plan.get("a_kperm", 0)
+                f"{swz_b}u", plan.get("a_kperm", 0), int(getattr(ctx.target, "gemm_rs_pipe", None) or 0)
             ]))
         else:
             raise LoweringError(f"T.gemm: A operand scope {A.scope} unsupported")
