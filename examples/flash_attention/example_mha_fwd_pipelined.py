@@ -27,7 +27,7 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                         threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
                         young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd", mfma="16x16",
                         sum_mfma=False, sink=False, sm_scale=None, fold_max=False, prescale_q=False,
-                        pingpong=False):
+                        pingpong=False, pk_scale=False):
     """``young_prio``: the second-dispatched half of the waves runs at issue priority 1 (one
     ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4).
     ``seq_kv`` (default ``seq_len``): key/value length; with ``is_causal`` the mask is aligned
@@ -54,7 +54,10 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     ``pingpong`` (with ``fold_max``): waves 4-7 run the same iteration in the order
     rescale(t-1) | PV(t-1) | QK^T(t) | decide(t) | exp(t) (``T.Pipelined(order_alt=)``), so on every
     SIMD one wave's softmax VALU phase sits under its partner's MFMAs instead of both waves
-    reaching their VALU phase together after each barrier."""
+    reaching their VALU phase together after each barrier.
+    ``pk_scale`` (with ``fold_max``): the log2-domain scale is applied by its own element-wise loop
+    before the exponentials, so the compiler pairs it into ``v_pk_mul_f32`` (16 instead of 32
+    multiplies per wave and tile) instead of one ``v_mul_f32`` in front of every ``v_exp_f32``."""
     scale = ((1.0 / dim)**0.5 if sm_scale is None else sm_scale) * 1.44269504
     head_kv = heads // groups
     seq_kv = seq_len if seq_kv is None else seq_kv
@@ -74,8 +77,9 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     n_pv = 2 if sum_mfma else 1
     sc2 = 1.0 if prescale_q else scale  # scale still to apply to the (max-folded) scores
     thr = 8.0 / sc2  # lazy-rescale threshold in the scores' own units
+    pk = pk_scale and not prescale_q
     fold_group = [[0], [1, 2], [3], [4, 5, 6, 7], [8], list(range(9, 9 + n_pv)),
-                  list(range(9 + n_pv, 9 + n_pv + (2 if sum_mfma else 4)))]
+                  list(range(9 + n_pv, 9 + n_pv + (2 if sum_mfma else 4) + (1 if pk else 0)))]
 
     @T.macro
     def body(Q, K, V, Output, Sinks):
@@ -181,8 +185,14 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                     if sum_mfma:
                         T.gemm(acc_s_cast, ones_s, acc_l, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
                     # 10-11: P = exp2(acc_s) -> bf16
-                    for i, j in T.Parallel(block_M, block_N):
-                        acc_s[i, j] = T.exp2(acc_s[i, j] * sc2) if not prescale_q else T.exp2(acc_s[i, j])
+                    if pk:
+                        for i, j in T.Parallel(block_M, block_N):
+                            acc_s[i, j] = acc_s[i, j] * sc2
+                        for i, j in T.Parallel(block_M, block_N):
+                            acc_s[i, j] = T.exp2(acc_s[i, j])
+                    else:
+                        for i, j in T.Parallel(block_M, block_N):
+                            acc_s[i, j] = T.exp2(acc_s[i, j] * sc2) if not prescale_q else T.exp2(acc_s[i, j])
                     if not sum_mfma:
                         T.reduce_sum(acc_s, scores_sum, dim=1)
                         for i in T.Parallel(block_M):

@@ -283,8 +283,14 @@ class CodeGen:
             if scoped:
                 self.w("{")
                 self.ind += 1
-            for c in st.stmts:
-                self.s(c)
+            stmts = st.stmts
+            i = 0
+            while i < len(stmts):
+                if i + 1 < len(stmts) and not self.is_cpu and self._emit_pk_pair(stmts[i], stmts[i + 1]):
+                    i += 2
+                    continue
+                self.s(stmts[i])
+                i += 1
             if scoped:
                 self.ind -= 1
                 self.w("}")
@@ -382,6 +388,50 @@ class CodeGen:
             raise CodeGenError(f"unlowered tile op {st.op.kind}")
         else:
             raise CodeGenError(f"cannot emit {type(st).__name__}")
+
+    # -- packed fp32 pairs ----------------------------------------------------------------------
+    def _emit_pk_pair(self, a, b) -> bool:
+        """``x[2m] = f(.., y[2m], ..); x[2m+1] = f(.., y[2m+1], ..)`` on fp32 registers (unrolled
+        fragment loops) as ONE ``tl::floatx2`` expression: mul / add / sub (and the fma the
+        compiler contracts them into) issue as ``v_pk_mul_f32`` / ``v_pk_add_f32`` /
+        ``v_pk_fma_f32``, two lanes' worth per VALU slot.  Only + - * of same-index register
+        pairs, thread-invariant scalars and constants; anything else keeps the scalar form."""
+        if not (isinstance(a, S.StoreStmt) and isinstance(b, S.StoreStmt) and a.buffer is b.buffer):
+            return False
+        buf = a.buffer
+        if buf.scope != "local" or str(buf.dtype) not in ("float32", "float") or len(a.indices) != 1:
+            return False
+        ia, ib = as_int(a.indices[0]), as_int(b.indices[0])
+        if ia is None or ib != ia + 1 or ia % 2:
+            return False
+        vexpr = self._pk_expr(a.value, b.value, buf)
+        if vexpr is None or not vexpr[1]:
+            return False
+        ref = self.buf_ref(buf)
+        self.w(f"{{ const tl::floatx2 _pk = {vexpr[0]}; {ref}[{ia}] = _pk.x; {ref}[{ia + 1}] = _pk.y; }}")
+        return True
+
+    def _pk_expr(self, x, y, dst):
+        """(C expression, is_vector) of the element pair (x, y), or None.  ``dst``: the stored
+        buffer (a splatted scalar must not read it: the second store would see the first's value)."""
+        if isinstance(x, BufferLoad) and isinstance(y, BufferLoad) and x.buffer is y.buffer and \
+                x.buffer.scope == "local" and str(x.buffer.dtype) in ("float32", "float") and len(x.indices) == 1:
+            i0, i1 = as_int(x.indices[0]), as_int(y.indices[0])
+            if i0 is not None and i1 == i0 + 1 and i0 % 2 == 0:
+                r = self.buf_ref(x.buffer)
+                return f"tl::floatx2{{{r}[{i0}], {r}[{i1}]}}", True
+        if isinstance(x, BinOp) and isinstance(y, BinOp) and x.op == y.op and x.op in ("+", "-", "*") and \
+                str(x.dtype) in ("float32", "float"):
+            l, r = self._pk_expr(x.a, y.a, dst), self._pk_expr(x.b, y.b, dst)
+            if l is None or r is None:
+                return None
+            return f"({l[0]} {x.op} {r[0]})", l[1] or r[1]
+        # the same scalar on both sides (a constant, or a per-row value both elements share)
+        if str(getattr(x, "dtype", "")) in ("float32", "float") and not _has_local_call(x) and not _reads(x, dst):
+            ex, ey = self.e(x), self.e(y)
+            if ex == ey:
+                return f"(float)({ex})", False
+        return None
 
     def alloc(self, b: Buffer):
         ct = self.ctype(b.dtype)
@@ -622,3 +672,14 @@ class CodeGen:
 
 def generate(func, kernel, target, lds_offsets, lds_total, name, pass_cfg=None) -> KernelSource:
     return CodeGen(func, kernel, target, lds_offsets, lds_total, pass_cfg).generate(name)
+
+
+def _reads(e, buf) -> bool:
+    from ..ir.expr import post_order
+    return any(isinstance(n, BufferLoad) and n.buffer is buf for n in post_order(e))
+
+
+def _has_local_call(e) -> bool:
+    """Calls (possibly impure or costly) anywhere in ``e``: such a scalar is not splatted."""
+    from ..ir.expr import post_order
+    return any(isinstance(n, Call) for n in post_order(e))
