@@ -51,6 +51,9 @@ GEMM_CFG = dict(M=4096, N=4096, K=4096, block_M=256, block_N=256, block_K=64, th
 ATTN_CFG = dict(batch=1, heads=64, seq_len=4096, dim=128, block_M=256, block_N=64, threads=512, num_stages=2,
                 q_in_regs=True, sum_mfma=True, fold_max=True, young_prio=True)
 MOE_CFG = dict(tokens=2048, hidden=4096, ffn=2048, experts=8, topk=2)
+# expert row tiles of 256 + MOE_EXT_M rows, every expert's rows spread evenly over its tiles
+# (ops/moe.py expert_gemm_sk_kernel ext_M): a random-routing expert of ~529 rows is two units, not three
+MOE_EXT_M = 0
 # --device cpu (CI plumbing run on the CPU target under gloo): same program, tiny shapes
 TINY = dict(gemm=dict(M=128, N=128, K=128, block_M=64, block_N=64, block_K=32, threads=128, num_stages=2),
             attn=dict(batch=1, heads=2, seq_len=128, dim=64, block_M=64, block_N=32, threads=128, num_stages=2,
@@ -98,8 +101,11 @@ def build_attn(device="cuda", a=None):
     f = flashattn.get_tir(a["batch"], a["heads"], a["seq_len"], a["dim"], False, 1, a["block_M"], a["block_N"],
                           a["threads"], a["num_stages"], "bfloat16", True, a.get("q_in_regs", False),
                           sum_mfma=a.get("sum_mfma", False), fold_max=a.get("fold_max", False),
-                          young_prio=a.get("young_prio", False))
-    k = tilelang.compile(f, out_idx=[3], target=_target(device), pass_configs=flashattn.pass_configs)
+                          young_prio=a.get("young_prio", False), pk_scale=a.get("pk_scale", False),
+                          pingpong=a.get("pingpong", False))
+    pc = dict(flashattn.pass_configs)
+    pc.update(a.get("pass_configs", {}))
+    k = tilelang.compile(f, out_idx=[3], target=_target(device), pass_configs=pc)
     shp = (a["batch"], a["seq_len"], a["heads"], a["dim"])
     return k, tuple(torch.randn(shp, device=device).to(torch.bfloat16) for _ in range(3))
 
@@ -111,7 +117,7 @@ def build_moe(mesh, device="cuda", m=None, mode=None):
     dt = torch.bfloat16 if device != "cpu" else torch.float32
     bm = 256 if device != "cpu" else 16
     # expert GEMM tile: 256x256x64, 8 waves, 2-stage LDS-DMA (scripts/prof_moe.py --sweep, profiles/r2)
-    gc = dict(block_N=256, block_K=64, num_stages=2, threads=512) if device != "cpu" else None
+    gc = dict(block_N=256, block_K=64, num_stages=2, threads=512, ext_M=MOE_EXT_M) if device != "cpu" else None
     cfg = MoEConfig(hidden=m["hidden"], ffn=m["ffn"], n_experts=m["experts"], topk=m["topk"], dtype=dt, block_M=bm,
                     gemm_cfg=gc)
     layer = MoELayer(cfg, mode or ("ep" if mesh is not None else "local"), mesh=mesh, device=device)
