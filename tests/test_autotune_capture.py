@@ -66,3 +66,23 @@ def test_isolated_config_is_killed_at_timeout(monkeypatch):
     assert res.config["slow"] == 0
     errs = [r for r in res.all_results if "error" in r]
     assert len(errs) == 1 and errs[0]["config"]["slow"] == 600 and "killed" in errs[0]["error"]
+
+
+@pytest.mark.timeout(300)
+def test_process_compile_backend_fills_kernel_cache(monkeypatch, tmp_path):
+    """compile_backend="process": worker processes lower + compile every config into the disk kernel
+    cache; the parent's compiles are then cache hits, an invalid config's error still surfaces."""
+    from tilelang.cache import kernel_cache
+    monkeypatch.setenv("TILELANG_AUTO_TUNING_DISABLE_CACHE", "1")
+    monkeypatch.setenv("TILELANG_CACHE_DIR", str(tmp_path))
+    from tilelang.env import env
+    monkeypatch.setattr(env, "TILELANG_CACHE_DIR", str(tmp_path), raising=False)
+    cfgs = [{"block": 64}, {"block": 128}, {"block": 96}, {"block": 0}]  # block 0: invalid
+    tuner = AutoTuner(_scale_factory, cfgs).set_profile_args(warmup=1, rep=2, ref_prog=lambda a: a * 2)
+    tuner.set_compile_args(backend="process")
+    errs = tuner._prefetch_compile((256, ), {})
+    assert set(errs) == {3}
+    assert kernel_cache.entries() == 3
+    res = tuner.run(256)
+    assert res.config in cfgs[:3]
+    assert any(r.get("error") for r in res.all_results if r["config"] == {"block": 0})

@@ -4,7 +4,9 @@
 with the non-tuned arguments it
 
   1. compiles every config concurrently (hipcc runs as subprocesses, so a thread pool
-     scales; worker count from ``TILELANG_AUTO_TUNING_CPU_COUNTS`` / ``..._MAX_CPU_COUNT``),
+     scales; worker count from ``TILELANG_AUTO_TUNING_CPU_COUNTS`` / ``..._MAX_CPU_COUNT``);
+     ``compile_backend="process"`` / ``TILELANG_AUTOTUNE_COMPILE=process`` lowers in worker
+     processes too (the Python passes are GIL-bound in threads; ``compile_worker.py``),
   2. benchmarks the compiled kernels one at a time on the GPU (L2+MALL flush between
      runs, per-config timeout, optional correctness check against ``ref_prog``) -- on the
      tensors captured by ``set_autotune_inputs`` when a capture is active; with
@@ -41,6 +43,7 @@ class CompileArgs:
     out_idx: Any = None
     target: str = "auto"
     pass_configs: Optional[dict] = None
+    backend: Optional[str] = None  # "thread" | "process"; None: TILELANG_AUTOTUNE_COMPILE (default thread)
 
 
 @dataclass
@@ -125,9 +128,46 @@ class AutoTuner:
     def from_kernel(cls, kernel: Callable, configs: List[dict]):
         return cls(kernel, configs)
 
-    def set_compile_args(self, out_idx=None, target="auto", pass_configs=None, **kwargs):
-        self.compile_args = CompileArgs(out_idx, target, pass_configs)
+    def set_compile_args(self, out_idx=None, target="auto", pass_configs=None, backend=None, **kwargs):
+        if backend not in (None, "thread", "process"):
+            raise ValueError(f"compile backend must be 'thread' or 'process', got {backend!r}")
+        self.compile_args = CompileArgs(out_idx, target, pass_configs, backend)
         return self
+
+    def _prefetch_compile(self, args, kwargs) -> Dict[int, str]:
+        """Lower + compile every config in worker processes into the disk kernel cache (see
+        ``compile_worker.py``); returns {config index: error} from the workers."""
+        import subprocess
+        import sys
+        import tempfile
+        import cloudpickle
+        n = min(_num_workers(), len(self.configs))
+        errors: Dict[int, str] = {}
+        with tempfile.TemporaryDirectory(prefix="tl_tune_compile_") as d:
+            procs = []
+            env_ = dict(os.environ)
+            root = str(Path(__file__).resolve().parents[2])
+            paths = [root] + [p_ for p_ in sys.path if p_ and os.path.isdir(p_)]
+            env_["PYTHONPATH"] = os.pathsep.join(dict.fromkeys(paths))
+            env_["OMP_NUM_THREADS"] = "1"
+            for w in range(n):
+                share = [(i, c) for i, c in enumerate(self.configs) if i % n == w]
+                jp = os.path.join(d, f"job{w}.pkl")
+                with open(jp, "wb") as f:
+                    cloudpickle.dump(dict(fn=self.fn, args=args, kwargs=kwargs, configs=share), f)
+                procs.append((jp, subprocess.Popen([sys.executable, "-m", "tilelang.autotuner.compile_worker", jp],
+                                                   env=env_, stdout=subprocess.DEVNULL,
+                                                   stderr=subprocess.PIPE, start_new_session=True)))
+            for jp, p in procs:
+                _, err = p.communicate()
+                rp = jp + ".result.json"
+                if os.path.exists(rp):
+                    with open(rp) as f:
+                        errors.update({int(k): v for k, v in json.load(f)["errors"].items()})
+                else:
+                    logger.warning("autotune compile worker exited with %s: %s", p.returncode,
+                                   err.decode(errors="replace")[-300:])
+        return errors
 
     def set_profile_args(self, **kwargs):
         for k, v in kwargs.items():
@@ -214,6 +254,12 @@ class AutoTuner:
         t0 = time.time()
         kernels: List[Any] = [None] * len(self.configs)
         errors: Dict[int, str] = {}
+        backend = self.compile_args.backend or os.environ.get("TILELANG_AUTOTUNE_COMPILE", "thread")
+        if backend == "process" and env.is_cache_enabled() and len(self.configs) > 1:
+            # workers fill the kernel cache; the thread-pool compile below is then all cache hits
+            self._prefetch_compile(args, kwargs)
+            logger.info("autotune: worker processes compiled %d configs in %.1fs", len(self.configs),
+                        time.time() - t0)
 
         def comp(i):
             try:
@@ -275,9 +321,10 @@ class AutoTuner:
 
 class AutoTuneImpl:
 
-    def __init__(self, fn, configs, **profile_kwargs):
+    def __init__(self, fn, configs, compile_backend=None, **profile_kwargs):
         self.fn = fn
         self.configs = configs
+        self.compile_backend = compile_backend
         self.profile_kwargs = profile_kwargs
         self._cache = {}
         functools.update_wrapper(self, getattr(fn, "fn", fn))
@@ -289,6 +336,8 @@ class AutoTuneImpl:
             return self._cache[key]
         configs = self.configs(*args, **kwargs) if callable(self.configs) else self.configs
         tuner = AutoTuner(self.fn, configs).set_profile_args(**self.profile_kwargs)
+        if self.compile_backend is not None:
+            tuner.set_compile_args(backend=self.compile_backend)
         res = tuner.run(*args, **kwargs)
         self._cache[key] = res.kernel
         return res.kernel
@@ -296,15 +345,17 @@ class AutoTuneImpl:
 
 def autotune(func: Callable = None, *, configs=None, warmup: int = 25, rep: int = 100, timeout: int = 100,
              supply_type=None, ref_prog=None, supply_prog=None, rtol=1e-2, atol=1e-2, max_mismatched_ratio=0.01,
-             skip_check=False, manual_check_prog=None, cache_input_tensors=True, isolate=None):
-    """Decorator: ``@tilelang.autotune(configs=[{...}, ...])`` over ``@tilelang.jit``."""
+             skip_check=False, manual_check_prog=None, cache_input_tensors=True, isolate=None,
+             compile_backend=None):
+    """Decorator: ``@tilelang.autotune(configs=[{...}, ...])`` over ``@tilelang.jit``.
+    ``compile_backend="process"``: lower + compile the configs in worker processes."""
     kw = dict(warmup=warmup, rep=rep, timeout=timeout, supply_type=supply_type, ref_prog=ref_prog,
               supply_prog=supply_prog, rtol=rtol, atol=atol, max_mismatched_ratio=max_mismatched_ratio,
               skip_check=skip_check, manual_check_prog=manual_check_prog, cache_input_tensors=cache_input_tensors,
               isolate=isolate)
 
     def deco(fn):
-        return AutoTuneImpl(fn, configs, **kw)
+        return AutoTuneImpl(fn, configs, compile_backend=compile_backend, **kw)
 
     if func is not None and callable(func):
         return deco(func)
