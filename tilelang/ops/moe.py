@@ -733,7 +733,9 @@ def combine_kernel(n_tok: int, H: int, topk: int, max_rows: int, dtype: str, tar
         with T.Kernel(n_tok, H // block_H, threads=threads) as (bx, by):
             acc = T.alloc_fragment((block_H,), "float32")
             T.clear(acc)
-            for k in T.serial(topk):
+            # unrolled over k: every row's index load and its row loads issue before the first
+            # accumulate (one memory round trip per phase instead of one per routed row)
+            for k in T.unroll(topk):
                 r = dest[bx * topk + k]
                 wk = w[bx, k]
                 for h in T.Parallel(block_H):
