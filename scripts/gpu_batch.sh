@@ -2,6 +2,7 @@ set -o pipefail
 mkdir -p gpurun_out/benchmarks
 timeout -k 10 120 ./csrc/probes/mfma_fp6_probe2 > gpurun_out/fp6_probe2.log 2>&1 && \
 bash scripts/gpu_moe_ext.sh && \
+timeout -k 10 120 python -u scripts/moe_combine_probe.py > gpurun_out/moe_combine.log 2>&1 && \
 bash scripts/gpu_fa_cmd.sh && \
 timeout -k 10 300 python -u scripts/fa_bwd_ab.py '[{}, {"tl.gemm_rs_pipe": 4}]' > gpurun_out/fa_bwd_ab.log 2>&1 && \
 timeout -k 10 300 python -u bench.py > gpurun_out/bench_b.log 2>&1
