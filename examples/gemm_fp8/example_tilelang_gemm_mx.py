@@ -3,8 +3,9 @@
 ``T.gemm_scaled`` lowers to ``v_mfma_scale_f32_16x16x128_f8f6f4``: the hardware multiplies every
 32-element K block of each row of A and B by its e8m0 scale (2^(s-127)) inside the MFMA, so the
 MX tensors are consumed as stored — no dequantisation pass.  Peak rates (dense): fp8 ~5 PF,
-fp4 ~10 PF (4x bf16).  Operands are K-contiguous: A ``[M, K]`` and B ``[N, K]`` bytes (fp8), or
-``[M, K/2]`` / ``[N, K/2]`` packed e2m1 pairs (low nibble = even element); scales ``[M, K/32]``,
+fp4 / fp6 ~10 PF (4x bf16).  Operands are K-contiguous: A ``[M, K]`` and B ``[N, K]`` bytes (fp8),
+``[M, K/2]`` / ``[N, K/2]`` packed e2m1 pairs (low nibble = even element), or ``[M, 3K/4]`` packed
+e2m3 / e3m2 (``tilelang.quantize.pack_fp6``: 4 elements per 3 bytes); scales ``[M, K/32]``,
 ``[N, K/32]`` read straight from global memory (a few bytes per 32 K per lane; L1/L2 resident).
 
 The reference has no MX path (its AMD fp8 GEMM is CDNA3 fnuz, ``examples/gemm_fp8/
@@ -37,8 +38,8 @@ def mx_matmul(M, N, K, block_M=256, block_N=None, block_K=None, threads=512, num
     # scale tiles on small-tile LDS-DMA the 256x256 2-stage tiles win for every pair:
     # fp4 x fp4 256x256x256 3.33 PF (256x128x256 3-stage 2.49), fp8 x fp8 256x256x128 1.86 PF
     # (256x128x128 3-stage 1.44), fp8 x fp4 256x256x128 2.26 PF
-    if block_K is None:
-        block_K = 256 if a_fmt in _NARROW and b_fmt in _NARROW else 128
+    if block_K is None:  # fp4 x fp4: 128-byte rows at block_K 256; fp6 rows would be 192 bytes
+        block_K = 256 if a_fmt == b_fmt == "e2m1" else 128
     if block_N is None:
         block_N = 256
     if num_stages is None:
@@ -173,7 +174,7 @@ def main(M=8192, N=8192, K=8192, a_fmt="e4m3", b_fmt="e4m3"):
     print(f"MX {a_fmt}x{b_fmt} gemm {M}x{N}x{K}: {lat:.3f} ms, {2 * M * N * K / lat * 1e-9:.1f} TFLOPS")
     # the same GEMM with the scales pre-shuffled once (weights offline, activations by their quantizer)
     from tilelang.quantize import preshuffle_mx_scales
-    bk = 256 if a_fmt in _NARROW and b_fmt in _NARROW else 128
+    bk = 256 if a_fmt == b_fmt == "e2m1" else 128
     kps = mx_matmul(M, N, K, a_fmt=a_fmt, b_fmt=b_fmt, preshuffle_scales=True)
     pa, pb = preshuffle_mx_scales(sa, 256, bk), preshuffle_mx_scales(sb, 256, bk)
     torch.testing.assert_close(kps(a, b, pa, pb).float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())

@@ -52,8 +52,11 @@ def test_mx_gemm_rejects_bad_scales():
     assert m is not None
 
 
+FP6_FMTS = [("e2m3", "e2m3"), ("e3m2", "e3m2"), ("e2m3", "e4m3"), ("e2m1", "e2m3")]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("af,bf", FMTS)
+@pytest.mark.parametrize("af,bf", FMTS + FP6_FMTS)
 def test_mx_gemm_gpu(af, bf):
     import example_tilelang_gemm_mx as m
     M, N, K = 512, 512, 1024
@@ -165,6 +168,9 @@ def test_mx_gemm_fp6_cpu(af, bf):
     b, sb = m.quantize(torch.randn(N, K) * 0.2, bf)
     assert len(set(sa.flatten().tolist())) > 1
     _check(k(a, b, sa, sb), a, b, sa, sb, af, bf)
+    kh = tilelang.compile(f, out_idx=[-1], target="hip")
+    assert f"gemm_ss_mx<{'234'['e2m3 e3m2 e2m1'.split().index(af)] if af != 'e4m3' else 0}" in \
+        kh.get_kernel_source() and len(kh.code[0]) > 0
 
 
 def test_fp6_pack_and_grid():

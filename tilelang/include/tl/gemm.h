@@ -420,9 +420,19 @@ namespace tl {
 //   For fp8 block g therefore spans bytes 0-15 (g < 2) or 16-31 (g >= 2) of lane groups 2(g&1)
 //   and 2(g&1)+1, not the scale lane's own bytes: the data is fetched in the hardware K order
 //   above (two 16-byte reads at 16g and 64+16g) so contiguous MX blocks line up with the scales.
-// FMT codes: 0 e4m3, 1 e5m2, 4 e2m1.  Operands are swapped at issue like gemm_ss.
+//   fp6 : packed 4 per 3 bytes (element k at bits 6k..6k+5 of the row), the 24 bytes at 24g
+//         (= k 32g..32g+31, the fp4 order) in registers 0-5 -- three 8-byte reads.
+// FMT codes: 0 e4m3, 1 e5m2, 2 e2m3, 3 e3m2, 4 e2m1.  Operands are swapped at issue like gemm_ss.
 // ---------------------------------------------------------------------------
-template <int FMT> struct mx_fmt { static constexpr int lane_bytes = FMT == 4 ? 16 : 32; };
+template <int FMT> struct mx_fmt {
+  static constexpr int lane_bytes = FMT == 4 ? 16 : (FMT == 2 || FMT == 3) ? 24 : 32;
+  static constexpr int step_bytes = lane_bytes * 4;  // bytes of one 128-K step of a row
+  static constexpr int nreads = FMT == 4 ? 1 : (FMT == 2 || FMT == 3) ? 3 : 2;
+};
+// byte column (in the 128-K step) of a lane group's read j
+template <int FMT> TL_DEVICE constexpr int mx_read_col(int g, int j) {
+  return mx_fmt<FMT>::lane_bytes == 24 ? 24 * g + 8 * j : 16 * g + 64 * j;
+}
 
 // bcol0: byte column of the 128-K step in the row
 template <int FMT, int COLS, uint32_t SWZ>
@@ -488,23 +498,29 @@ TL_DEVICE void gemm_ss_mx(const void* __restrict__ A_, const void* __restrict__ 
   constexpr bool HOLD_B = N_REP <= M_REP;
   constexpr int NH = HOLD_B ? N_REP : M_REP, NS = HOLD_B ? M_REP : N_REP;
   constexpr int KS = K / 128;
-  int oa[KS][2], ob[KS][2];
+  int oa[KS][3], ob[KS][3];
 #pragma unroll
   for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      oa[kk][h] = swz_offset<uint8_t, A_COLS, SWZ_A>(r, kk * 4 * BA + 16 * g + 64 * h);
-      ob[kk][h] = swz_offset<uint8_t, B_COLS, SWZ_B>(r, kk * 4 * BB + 16 * g + 64 * h);
+    for (int h = 0; h < 3; ++h) {
+      oa[kk][h] = swz_offset<uint8_t, A_COLS, SWZ_A>(r, kk * 4 * BA + mx_read_col<FA>(g, h));
+      ob[kk][h] = swz_offset<uint8_t, B_COLS, SWZ_B>(r, kk * 4 * BB + mx_read_col<FB>(g, h));
     }
   const uint8_t* Aw = A + wm * WM * A_COLS;
   const uint8_t* Bw = B + wn * WN * B_COLS;
   static_assert(!SCALE_PS || (WM % 64 == 0 && WN % 64 == 0), "pre-shuffled scales: 64-row warp tiles");
   const uint8_t* SAw = SCALE_PS ? SA + (wm * WM / 64) * 256 + (g * 16 + r) * 4 : SA + (wm * WM + r) * SA_STRIDE + g;
   const uint8_t* SBw = SCALE_PS ? SB + (wn * WN / 64) * 256 + (g * 16 + r) * 4 : SB + (wn * WN + r) * SB_STRIDE + g;
-  auto frag = [&](const uint8_t* base, int cols, const int (&o)[2], int i, bool two) -> intx8 {
+  auto frag = [&](const uint8_t* base, int cols, const int (&o)[3], int i, int lane_bytes) -> intx8 {
     const uint8_t* p = base + i * 16 * cols;
+    if (lane_bytes == 24) {  // fp6: 3 x 8 bytes (8-byte aligned, never across a 16-byte chunk)
+      intx2 a = *reinterpret_cast<const intx2*>(p + o[0]);
+      intx2 b = *reinterpret_cast<const intx2*>(p + o[1]);
+      intx2 c = *reinterpret_cast<const intx2*>(p + o[2]);
+      return intx8{a.x, a.y, b.x, b.y, c.x, c.y, 0, 0};
+    }
     intx4 lo = *reinterpret_cast<const intx4*>(p + o[0]);
-    intx4 hi = two ? *reinterpret_cast<const intx4*>(p + o[1]) : intx4{0, 0, 0, 0};
+    intx4 hi = lane_bytes == 32 ? *reinterpret_cast<const intx4*>(p + o[1]) : intx4{0, 0, 0, 0};
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   };
   auto ld_scale = [&](const uint8_t* w, int rows, int stride, int i, int kk) -> int {
@@ -513,11 +529,11 @@ TL_DEVICE void gemm_ss_mx(const void* __restrict__ A_, const void* __restrict__ 
   };
   auto ld_a = [&](int i, int kk, int& sc) -> intx8 {
     sc = ld_scale(SAw, M, SA_STRIDE, i, kk);
-    return frag(Aw, A_COLS, oa[kk], i, BA == 32);
+    return frag(Aw, A_COLS, oa[kk], i, BA);
   };
   auto ld_b = [&](int i, int kk, int& sc) -> intx8 {
     sc = ld_scale(SBw, N, SB_STRIDE, i, kk);
-    return frag(Bw, B_COLS, ob[kk], i, BB == 32);
+    return frag(Bw, B_COLS, ob[kk], i, BB);
   };
   auto ld_held = [&](int i, int kk, int& sc) -> intx8 { return HOLD_B ? ld_b(i, kk, sc) : ld_a(i, kk, sc); };
   auto ld_stream = [&](int i, int kk, int& sc) -> intx8 { return HOLD_B ? ld_a(i, kk, sc) : ld_b(i, kk, sc); };

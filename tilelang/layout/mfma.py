@@ -203,6 +203,14 @@ def _read_patterns(kind: str, rows: int, cols: int, elem_bytes: int, row_base_st
                 for half in range(2):
                     pats.append([(r0 + (l & 15), k0 + (l >> 4) * 16 + 64 * half) for l in range(64)])
         return pats
+    if kind == "k_rows24mx":
+        # packed-fp6 operand of the block-scaled 16x16x128 MFMA: 96 bytes per row per K step,
+        # lane group g takes the 24 bytes (32 fp6) at 24 g: three 8-byte reads (tl/gemm.h)
+        for r0 in range(0, min(rows, 64), row_base_step):
+            for k0 in range(0, cols, 96):
+                for j in range(3):
+                    pats.append([(r0 + (l & 15), k0 + (l >> 4) * 24 + 8 * j) for l in range(64)])
+        return pats
     if kind == "k_rows32":
         # 8-bit operand of the scaled 16x16x128 MFMA: 32 consecutive bytes per lane, two b128 reads
         for r0 in range(0, min(rows, 64), row_base_step):
@@ -243,6 +251,8 @@ def _instr_for(kind: str, elem_bytes: int) -> str:
         return "ds_read_b64_tr_b16"
     if kind == "k_rows":
         return "ds_read_b128" if elem_bytes == 2 else "ds_read_b64"
+    if kind == "k_rows24mx":
+        return "ds_read_b64"
     return "ds_read_b64_tr_b16"
 
 
@@ -270,6 +280,9 @@ def choose_swizzle(kind: str, rows: int, cols: int, elem_bytes: int) -> Tuple[Tu
     """Pick the chunk-XOR swizzle with the fewest modelled LDS cycles for this read pattern
     (exhaustive over row-bit -> chunk-bit assignments, scored with the gfx950 bank model)."""
     cpr = cols * elem_bytes // 16
+    # XOR on chunk bits below the largest power of two dividing the row keeps every chunk in its
+    # row (a 12-chunk fp6 row: bits 0-1 only)
+    cpr &= -cpr
     if cpr <= 1:
         return ()
     cands = [tuple(b) for b in _candidates(cpr, max_row_bit=min(6, max(1, rows.bit_length() - 1)))]
@@ -296,6 +309,7 @@ def choose_swizzle_multi(kinds: Tuple[str, ...], rows: int, cols: int, elem_byte
     if len(kinds) == 1:
         return choose_swizzle(kinds[0], rows, cols, elem_bytes)
     cpr = cols * elem_bytes // 16
+    cpr &= -cpr
     if cpr <= 1:
         return ()
     cands = [tuple(b) for b in _candidates(cpr, max_row_bit=min(6, max(1, rows.bit_length() - 1)))]

@@ -48,6 +48,8 @@ MX_CODES = {"e4m3": 0, "e5m2": 1, "e2m3": 2, "e3m2": 3, "e2m1": 4}
 
 
 _FP6 = ("e2m3", "e3m2")
+# LDS read pattern of each operand format (layout/mfma.py _read_patterns)
+_MX_KIND = {"e2m1": "k_rows16", "e2m3": "k_rows24mx", "e3m2": "k_rows24mx"}
 
 
 def _mx_k(cols: int, fmt: str, name: str) -> int:
@@ -93,15 +95,11 @@ def _mx_plan(op: O.GemmOp, plan: Dict, num_threads: int, a_ext, b_ext, is_cpu: b
         return plan
     if num_threads % 64:
         raise ValueError(f"block size {num_threads} is not a multiple of the 64-lane wavefront")
-    if op.a_fmt in _FP6 or op.b_fmt in _FP6:
-        raise NotImplementedError("T.gemm_scaled: packed fp6 operands run on the CPU target; the gfx950 "
-                                  "lowering is not available yet")
     warp_m, warp_n = MF.compute_warp_partition(M, N, num_threads // 64, op.policy)
     plan.update(K=K, warp_m=warp_m, warp_n=warp_n, mfma=(16, 16, 128), mx=True,
                 a_code=MX_CODES[op.a_fmt], b_code=MX_CODES[op.b_fmt])
     plan["c_layout"] = MF.mfma_c_fragment(M, N, warp_m, warp_n)
-    ka_kind = "k_rows16" if op.a_fmt == "e2m1" else "k_rows32mx"
-    kb_kind = "k_rows16" if op.b_fmt == "e2m1" else "k_rows32mx"
+    ka_kind, kb_kind = _MX_KIND.get(op.a_fmt, "k_rows32mx"), _MX_KIND.get(op.b_fmt, "k_rows32mx")
     plan["a_kind"], plan["b_kind"] = ka_kind, kb_kind
     plan["a_smem_layout"] = MF.operand_swizzle(ka_kind, A.static_shape(), 1)
     plan["b_smem_layout"] = MF.operand_swizzle(kb_kind, B.static_shape(), 1)
