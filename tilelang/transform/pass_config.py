@@ -46,6 +46,7 @@ class PassConfigKey(str, Enum):
     TL_GEMM_INTERLEAVE = "tl.gemm_interleave"      # 1 MFMA : 1 ds_read sched_group_barrier pattern
     TL_DISABLE_ADDRESS_HOIST = "tl.disable_address_hoist"  # keep LDS-DMA source addresses in the loop
     TL_GEMM_RS_PIPE = "tl.gemm_rs_pipe"            # register-A GEMM: B fragments streamed in groups of N
+    TL_PACK_F32 = "tl.pack_f32"                    # fp32 register pairs as packed v_pk_* math
 
     def __str__(self):
         return self.value
@@ -85,6 +86,9 @@ EFFECT = {
     "tl.storage_rewrite_detect_inplace": "a local array first written by the element-wise statement that last "
                                          "reads another of the same dtype/shape takes over its storage "
                                          "(transform/storage_rewrite.py _inplace_ok)",
+    "tl.pack_f32": "True: fp32 register pairs of unrolled fragment loops are emitted as packed floatx2 math "
+                   "(v_pk_mul/add/fma_f32; codegen/hip.py _emit_pk_pair) -- for VALU-bound code: beside MFMAs "
+                   "a packed op costs more than the two scalar ones",
     "tl.gemm_rs_pipe": "N > 0: a T.gemm with its A operand in registers streams the B fragments through the "
                        "MFMAs in groups of N (group g+1's ds_reads pinned between group g's MFMAs, across K "
                        "steps; tl::gemm_rs PIPE) instead of reading a whole K step before its first MFMA",
