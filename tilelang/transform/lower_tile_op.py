@@ -1413,6 +1413,8 @@ class TileOpLowerer(Mutator):
         epc = 16 // p["eb"]
         nw = p["nwaves"]
         wave = ctx.wave_expr()
+        if p.get("dup"):
+            wave = binop("%", wave, nw)  # waves past the tile re-fetch a covered piece
         lane = ctx.lane_expr()
         stage = self.expr(dst.mins[0])
         base_off = ctx.flat_index(NB, [stage, 0, 0])
@@ -1486,6 +1488,8 @@ class TileOpLowerer(Mutator):
         epc = 16 // p["eb"]
         nw, cpr, rdim = p["nwaves"], p["cpr"], p["rdim"]
         wave, lane = ctx.wave_expr(), ctx.lane_expr()
+        if p.get("dup"):
+            wave = binop("%", wave, nw)  # waves past the tile re-fetch a covered chunk
         stage = self.expr(dst.mins[0])
         base_off = ctx.flat_index(NB, [stage, 0, 0])
         smins = [self.expr(m) for m in src.mins]
@@ -1527,7 +1531,8 @@ class TileOpLowerer(Mutator):
         wave, lane = ctx.wave_expr(), ctx.lane_expr()
         out = []
         for i in range(p["instrs"]):
-            _, row, _ = _gather_geom(i, p["nwaves"], p["cpr"], wave, lane)
+            _, row, _ = _gather_geom(i, p["nwaves"], p["cpr"], binop("%", wave, p["nwaves"]) if p.get("dup") else wave,
+                                     lane)
             # (kept in VGPRs: a scalar row base per instruction measured slower, 416 vs 531 TF
             # on sparse MLA -- the SALU address chains serialise the DMA issue)
             v = cast(self.expr(_gather_index(op.idx, row)), _dt.int32)

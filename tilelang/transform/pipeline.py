@@ -128,10 +128,18 @@ def glds_plan(op: O.CopyOp, num_threads: int, ranges, target) -> Optional[dict]:
     dshape = db.static_shape()
     if dext is None or dshape is None or dext != dshape or len(dshape) not in (1, 2):
         return None
-    if len(dshape) == 1 or (dshape[0] * dshape[1] * eb) % (1024 * (num_threads // 64)):
+    nw = num_threads // 64
+    dw = nw
+    if len(dshape) == 1 or (dshape[0] * dshape[1] * eb) % (1024 * nw):
         if getattr(target, "disable_small_dma", False):
             return None
-        return _small_dma_plan(op, num_threads, ranges)
+        sp = _small_dma_plan(op, num_threads, ranges)
+        nbytes = dshape[0] * dshape[1] * eb if len(dshape) == 2 else 0
+        if sp is not None or len(dshape) == 1 or nbytes % 1024 or nw % (nbytes // 1024):
+            return sp
+        # whole 1 KiB wave pieces, fewer than the waves: the extra waves re-fetch a covered piece
+        # (same bytes, same LDS address; uniform DMA count per wave for the counted waits)
+        dw = nbytes // 1024
     R, C = dshape
     if (C * eb) % 16:
         return None
@@ -189,9 +197,8 @@ def glds_plan(op: O.CopyOp, num_threads: int, ranges, target) -> Optional[dict]:
             return None
         nbytes = numel * eb
     n_chunks = R * C * eb // 16
-    nw = num_threads // 64
-    return dict(R=R, C=C, eb=eb, rdim=rdim, cdim=cdim, instrs=n_chunks // 64 // nw, nwaves=nw, cpr=C * eb // 16,
-                oob_bytes=nbytes)
+    return dict(R=R, C=C, eb=eb, rdim=rdim, cdim=cdim, instrs=n_chunks // 64 // dw, nwaves=dw, cpr=C * eb // 16,
+                oob_bytes=nbytes, dup=dw < nw)
 
 
 def _small_dma_plan(op: O.CopyOp, num_threads: int, ranges) -> Optional[dict]:
@@ -294,8 +301,17 @@ def gather_plan(op: O.GatherRowsOp, num_threads: int, target) -> Optional[dict]:
         return None
     R, C = dshape
     nw = num_threads // 64
-    if (C * eb) % 16 or (R * C * eb) % (1024 * nw):
+    if (C * eb) % 16:
         return None
+    # a tile smaller than one 16-byte chunk per lane of the workgroup (e.g. a 32-row MoE
+    # extension tile): the first ``dw`` waves' chunks cover it and every further wave re-fetches
+    # the chunk of wave (w mod dw) -- identical bytes to the same LDS address -- so each wave still
+    # issues the same number of DMA instructions per stage (the counted vmcnt waits stay uniform)
+    dw = nw
+    if (R * C * eb) % (1024 * nw):
+        if (R * C * eb) % 1024 or nw % ((R * C * eb) // 1024):
+            return None
+        dw = (R * C * eb) // 1024
     lay = db.layout
     if lay is not None and not isinstance(lay, (SwizzleLayout, LinearLayout)):
         return None
@@ -318,8 +334,8 @@ def gather_plan(op: O.GatherRowsOp, num_threads: int, target) -> Optional[dict]:
     iext = [as_int(e) for e in op.idx.extents]
     if None in iext or [e for e in iext if e != 1] not in ([R], []) or _prod_i(iext) != R:
         return None
-    return dict(R=R, C=C, eb=eb, rdim=rdim, cdim=cdim, instrs=R * C * eb // 16 // 64 // nw, nwaves=nw, cpr=cpr,
-                gather=True)
+    return dict(R=R, C=C, eb=eb, rdim=rdim, cdim=cdim, instrs=R * C * eb // 16 // 64 // dw, nwaves=dw, cpr=cpr,
+                gather=True, dup=dw < nw)
 
 
 def _prod_i(xs):
