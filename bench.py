@@ -53,7 +53,7 @@ ATTN_CFG = dict(batch=1, heads=64, seq_len=4096, dim=128, block_M=256, block_N=6
 MOE_CFG = dict(tokens=2048, hidden=4096, ffn=2048, experts=8, topk=2)
 # expert row tiles of 256 + MOE_EXT_M rows, every expert's rows spread evenly over its tiles
 # (ops/moe.py expert_gemm_sk_kernel ext_M): a random-routing expert of ~529 rows is two units, not three
-MOE_EXT_M = 0
+MOE_EXT_M = 32
 # --device cpu (CI plumbing run on the CPU target under gloo): same program, tiny shapes
 TINY = dict(gemm=dict(M=128, N=128, K=128, block_M=64, block_N=64, block_K=32, threads=128, num_stages=2),
             attn=dict(batch=1, heads=2, seq_len=128, dim=64, block_M=64, block_N=32, threads=128, num_stages=2,
