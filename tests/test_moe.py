@@ -175,7 +175,12 @@ def _mesh_moe_worker(rank, world, port, mode, q):
         dev = f"cuda:{rank % torch.cuda.device_count()}"
         torch.cuda.set_device(dev)
         mesh = init_mesh(1, world, device=dev)
-        cfg = MoEConfig(hidden=512, ffn=256, n_experts=8, topk=2, dtype=torch.bfloat16, block_M=128)
+        gcfg = None
+        if mode.endswith("_ext"):  # the bench's expert GEMM config: 256 + 32-row slots (ext_M)
+            mode = mode[:-4]
+            gcfg = dict(block_N=256, block_K=64, num_stages=2, threads=512, ext_M=32)
+        cfg = MoEConfig(hidden=512, ffn=256, n_experts=8, topk=2, dtype=torch.bfloat16,
+                        block_M=256 if gcfg else 128, gemm_cfg=gcfg)
         layer = MoELayer(cfg, mode, mesh=mesh, device=dev)
         g, w1, w2 = (t.to(dev) for t in init_moe_weights(cfg))
         for step in range(4):  # several steps: both buffer parities, flag reuse across steps
@@ -198,7 +203,7 @@ def _mesh_moe_worker(rank, world, port, mode, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["ep", "tp"])
+@pytest.mark.parametrize("mode", ["ep", "tp", "ep_ext"])
 def test_moe_mesh_two_processes_gpu(mode):
     import socket
     import torch.multiprocessing as mp
