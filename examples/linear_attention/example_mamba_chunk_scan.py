@@ -24,12 +24,19 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[7], pass_configs=FAST_MATH)
 def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, block_M=128, block_N=64,
-                   block_K=32, num_stages=2, threads=256, dtype="float16"):
+                   block_K=32, num_stages=2, threads=256, dtype="float16", xcd_group=False):
+    """``xcd_group``: every workgroup of one (batch, chunk) -- all heads and row tiles, which share
+    that chunk's ``cb`` and ``C`` tiles (one group) -- is placed on the same XCD (workgroups go
+    round-robin over the 8 XCDs by dispatch id), so the shared tiles are fetched into one XCD's L2
+    once instead of into all eight."""
     accum_dtype = "float"
     nchunks = seqlen // chunk_size
     assert seqlen % chunk_size == 0 and chunk_size % block_M == 0 and chunk_size % block_K == 0
     n_n = headdim // block_N
     hpg = nheads // ngroups
+    n_tiles = (chunk_size // block_M) * n_n
+    per_group = nheads * n_tiles  # workgroups of one (batch, chunk)
+    xcd_group = xcd_group and (batch * nchunks) % 8 == 0 and ngroups == 1
 
     @T.prim_func
     def main(cb: T.Tensor((batch, nchunks, ngroups, chunk_size, chunk_size), dtype),
@@ -40,7 +47,15 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
              prev_states: T.Tensor((batch, nchunks, nheads, headdim, dstate), dtype),
              D: T.Tensor((nheads, ), dtype),
              Output: T.Tensor((batch, seqlen, nheads, headdim), dtype)):
-        with T.Kernel(nheads, (chunk_size // block_M) * n_n, batch * nchunks, threads=threads) as (bz, bx, by):
+        with T.Kernel(nheads, n_tiles, batch * nchunks, threads=threads) as (bz_, bx_, by_):
+            if xcd_group:
+                pid = bz_ + nheads * (bx_ + n_tiles * by_)  # dispatch order; XCD = pid % 8
+                jj = pid // 8
+                by = (jj // per_group) * 8 + pid % 8
+                bz = jj % per_group % nheads
+                bx = jj % per_group // nheads
+            else:
+                bz, bx, by = bz_, bx_, by_
             acc_o = T.alloc_fragment((block_M, block_N), accum_dtype)
             cb_shared = T.alloc_shared((block_M, block_K), dtype)
             cb_local = T.alloc_fragment((block_M, block_K), dtype)
