@@ -145,10 +145,14 @@ def test_linear_attention_fwd():
     torch.testing.assert_close(h, rh, rtol=1e-3, atol=1e-3)
 
 
-def test_mamba_chunk_scan():
+@pytest.mark.parametrize("xcd_group", [False, True])
+def test_mamba_chunk_scan(xcd_group):
+    """xcd_group: the grid decoded so every workgroup of a (batch, chunk) shares one XCD."""
     import example_mamba_chunk_scan as m
-    args = m.make_inputs(1, 512, 128, 1, 2, 64, 64, device="cpu")
-    k = _both(m.chunk_scan_fwd, 1, 512, 128, 1, 2, 64, 64)
+    B = 2 if xcd_group else 1
+    args = m.make_inputs(B, 2048, 128, 1, 2, 64, 64, device="cpu") if xcd_group else \
+        m.make_inputs(1, 512, 128, 1, 2, 64, 64, device="cpu")
+    k = _both(m.chunk_scan_fwd, B, 2048 if xcd_group else 512, 128, 1, 2, 64, 64, xcd_group=xcd_group)
     torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=1e-2, atol=2e-2)
 
 

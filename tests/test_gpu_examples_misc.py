@@ -150,10 +150,11 @@ def test_linear_attention_fwd():
     torch.testing.assert_close(h, rh, rtol=1e-2, atol=2e-2)
 
 
-def test_mamba_chunk_scan():
+@pytest.mark.parametrize("xcd_group", [False, True])
+def test_mamba_chunk_scan(xcd_group):
     import example_mamba_chunk_scan as m
-    args = m.make_inputs(2, 1024, 256, 1, 8, 64, 128)
-    k = m.chunk_scan_fwd(2, 1024, 256, 1, 8, 64, 128)
+    args = m.make_inputs(2, 4096, 256, 1, 8, 64, 128)
+    k = m.chunk_scan_fwd(2, 4096, 256, 1, 8, 64, 128, xcd_group=xcd_group)
     torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=2e-2, atol=5e-2)
 
 

@@ -91,3 +91,50 @@ def test_small_tile_dma_and_lds_overflow_fallback():
     # 158 KiB of other LDS: 3 padded 1 KiB slots (4 waves x 256 B) no longer fit
     src = tilelang.lower(_small_tile_kernel(158 * 256), target="hip").kernel_source
     assert "tl::buffer_lds4(" not in src and re.search(r"\bstage\d+\[", src)
+
+
+def test_moe_ext_rows_gather_is_lds_dma():
+    """The 32-row extension tile of ext_M (4 KiB: fewer 16-byte chunks than lanes) is a row-gather
+    LDS-DMA whose extra waves re-fetch a covered piece -- not a synchronous SIMT gather (which put
+    a global round trip and a barrier into every K step: GEMM1 147 -> 213 us)."""
+    from tilelang.ops.moe import expert_gemm_sk_kernel, max_padded_rows
+    mr = max_padded_rows(4096, 8, 288)
+    for sw in (True, False):
+        kw = dict(n_src=2048, swiglu=True) if sw else {}
+        src = expert_gemm_sk_kernel(mr, 2048, 4096, 8, "bfloat16", "hip", 256, 256, 64, 2, 512, ext_M=32,
+                                    **kw).get_kernel_source()
+        dma, staged = _counts(src)
+        assert staged == 0 and "% 4)" in src, (sw, dma)
+        loop = src[src.index("for (int k"):]
+        loop = loop[:loop.index("tl::gemm_ss<")]
+        assert "tl::sync_threads()" not in loop  # no synchronous gather before the MFMAs
+
+
+def test_gemm_rs_pipe_template_arg():
+    """tl.gemm_rs_pipe reaches the register-A GEMM as its PIPE template argument."""
+    from example_mha_fwd_pipelined import flashattn_pipelined as fa
+    f = fa.get_tir(1, 8, 512, 128, False, 1, 256, 64, 512, 2, "bfloat16", True, True, sum_mfma=True, fold_max=True)
+    for pipe in (0, 4):
+        cfg = dict(fa.pass_configs)
+        cfg["tl.gemm_rs_pipe"] = pipe
+        src = tilelang.compile(f, out_idx=[3], target="hip", pass_configs=cfg).get_kernel_source()
+        args = [m for m in re.findall(r"tl::gemm_rs<([^>]*)>", src)]
+        assert args and all(a.split(",")[-1].strip() == str(pipe) for a in args), (pipe, args)
+
+
+def test_pack_f32_pairs():
+    """tl.pack_f32: fp32 register pairs of an unrolled fragment loop become floatx2 math."""
+    import tilelang.language as T
+
+    @T.prim_func
+    def main(A: T.Tensor((256, 64), "float32"), B: T.Tensor((256, 64), "float32")):
+        with T.Kernel(1, threads=256):
+            a = T.alloc_fragment((256, 64), "float32")
+            T.copy(A, a)
+            for i, j in T.Parallel(256, 64):
+                a[i, j] = a[i, j] * 0.5 + 1.0
+            T.copy(a, B)
+
+    plain = tilelang.lower(main, target="hip").kernel_source
+    packed = tilelang.lower(main, target="hip", pass_configs={"tl.pack_f32": True}).kernel_source
+    assert "tl::floatx2" not in plain and "tl::floatx2" in packed
