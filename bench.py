@@ -102,7 +102,7 @@ def build_attn(device="cuda", a=None):
                           a["threads"], a["num_stages"], "bfloat16", True, a.get("q_in_regs", False),
                           sum_mfma=a.get("sum_mfma", False), fold_max=a.get("fold_max", False),
                           young_prio=a.get("young_prio", False), pk_scale=a.get("pk_scale", False),
-                          pingpong=a.get("pingpong", False))
+                          pingpong=a.get("pingpong", False), xcd_heads=a.get("xcd_heads", False))
     pc = dict(flashattn.pass_configs)
     pc.update(a.get("pass_configs", {}))
     k = tilelang.compile(f, out_idx=[3], target=_target(device), pass_configs=pc)

@@ -27,7 +27,7 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                         threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
                         young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd", mfma="16x16",
                         sum_mfma=False, sink=False, sm_scale=None, fold_max=False, prescale_q=False,
-                        pingpong=False, pk_scale=False):
+                        pingpong=False, pk_scale=False, xcd_heads=False):
     """``young_prio``: the second-dispatched half of the waves runs at issue priority 1 (one
     ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4).
     ``seq_kv`` (default ``seq_len``): key/value length; with ``is_causal`` the mask is aligned
@@ -55,6 +55,10 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     rescale(t-1) | PV(t-1) | QK^T(t) | decide(t) | exp(t) (``T.Pipelined(order_alt=)``), so on every
     SIMD one wave's softmax VALU phase sits under its partner's MFMAs instead of both waves
     reaching their VALU phase together after each barrier.
+    ``xcd_heads`` (non-causal): workgroups are dealt round-robin over the 8 XCDs by dispatch id;
+    the grid is decoded so that all query tiles of one head run on the same XCD (consecutive slots
+    of that XCD), so the head's K/V stream is fetched into ONE XCD's L2 and read by all its tiles
+    there, instead of into every XCD.
     ``pk_scale`` (with ``fold_max``): the log2-domain scale is applied by its own element-wise loop
     before the exponentials, so the compiler pairs it into ``v_pk_mul_f32`` (16 instead of 32
     multiplies per wave and tile) instead of one ``v_mul_f32`` in front of every ``v_exp_f32``."""
@@ -78,13 +82,21 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     sc2 = 1.0 if prescale_q else scale  # scale still to apply to the (max-folded) scores
     thr = 8.0 / sc2  # lazy-rescale threshold in the scores' own units
     pk = pk_scale and not prescale_q
+    xcd_h = xcd_heads and not is_causal and (heads * batch) % 8 == 0
     fold_group = [[0], [1, 2], [3], [4, 5, 6, 7], [8], list(range(9, 9 + n_pv)),
                   list(range(9 + n_pv, 9 + n_pv + (2 if sum_mfma else 4) + (1 if pk else 0)))]
 
     @T.macro
     def body(Q, K, V, Output, Sinks):
         # causal: heads on the fastest grid axis and the longest (last) query tiles dispatched first
-        with T.Kernel(*((heads, n_qt, batch) if is_causal else (n_qt, heads, batch)), threads=threads) as (g0, g1, bz):
+        with T.Kernel(*((heads, n_qt, batch) if is_causal else (n_qt, heads, batch)), threads=threads) as (g0_, g1_, bz_):
+            if xcd_h:
+                pid = g0_ + n_qt * (g1_ + heads * bz_)  # dispatch id: XCD = pid % 8
+                jj = pid // 8
+                hb = (jj // n_qt) * 8 + pid % 8  # (batch, head) of this slot
+                g0, g1, bz = jj % n_qt, hb % heads, hb // heads
+            else:
+                g0, g1, bz = g0_, g1_, bz_
             bx = (n_qt - 1 - g1) if is_causal else g0
             by = g0 if is_causal else g1
             if q_in_regs:
