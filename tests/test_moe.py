@@ -342,3 +342,17 @@ def test_ep_dead_peer_fails_fast_gpu():
         p.join(timeout=60)
     assert res[1] == "ok" and res[0].startswith("ok"), res
     print("dead peer detected after", res[0])
+
+
+def test_router_k_split_matches_fused(monkeypatch):
+    """K-split router (partial logits by plain stores, summed + rounded in the top-k kernel) picks
+    the same experts with the same weights as the fused one-pass router."""
+    from tilelang.ops import moe as K
+    torch.manual_seed(0)
+    x = torch.randn(256, 1024).to(torch.bfloat16)
+    g = (torch.randn(8, 1024) * 0.05).to(torch.bfloat16)
+    ids0, w0 = K.route(x, g, 2)
+    monkeypatch.setattr(K, "ROUTER_SPLITS", 4)
+    ids1, w1 = K.route(x, g, 2)
+    assert torch.equal(ids0, ids1)
+    torch.testing.assert_close(w0, w1)

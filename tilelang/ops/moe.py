@@ -50,12 +50,18 @@ def _bucket(n: int, lo: int = 256) -> int:
 
 
 @functools.lru_cache(maxsize=None)
-def router_topk_kernel(n_tok: int, E: int, topk: int, target: str, threads: int = 256):
+def router_topk_kernel(n_tok: int, E: int, topk: int, target: str, threads: int = 256, parts: int = 0,
+                       E_stride: int = 0, round_dtype: Optional[str] = None):
     """``ids[t] = topk(logits[t])``, ``w[t] = softmax(logits[t])[ids] / sum`` — the renormalised
-    top-k weights equal ``exp(l_k - m) / sum_k' exp(l_k' - m)`` (the softmax denominator cancels)."""
+    top-k weights equal ``exp(l_k - m) / sum_k' exp(l_k' - m)`` (the softmax denominator cancels).
+    ``parts`` > 0: ``L`` is ``[parts, n_tok, E_stride]`` fp32 partial logits (a K-split router GEMM),
+    summed here; ``round_dtype``: the summed logit is rounded to that dtype first (as a library
+    GEMM's output would be)."""
+    Es = E_stride or E
+    L_shape = (parts, n_tok, Es) if parts else (n_tok, E)
 
     @T.prim_func
-    def moe_router_topk(L: T.Tensor((n_tok, E), "float32"), ids: T.Tensor((n_tok, topk), "int32"),
+    def moe_router_topk(L: T.Tensor(L_shape, "float32"), ids: T.Tensor((n_tok, topk), "int32"),
              w: T.Tensor((n_tok, topk), "float32")):
         with T.Kernel(T.ceildiv(n_tok, threads), threads=threads) as bx:
             for i in T.Parallel(threads):
@@ -67,7 +73,14 @@ def router_topk_kernel(n_tok: int, E: int, topk: int, target: str, threads: int 
                 tot = T.alloc_var("float32")
                 if bx * threads + i < n_tok:
                     for e in T.serial(E):
-                        v[e] = L[bx * threads + i, e]
+                        if parts:
+                            v[e] = L[0, bx * threads + i, e]
+                            for q in T.serial(parts - 1):
+                                v[e] = v[e] + L[q + 1, bx * threads + i, e]
+                        else:
+                            v[e] = L[bx * threads + i, e]
+                        if round_dtype is not None:
+                            v[e] = T.Cast("float32", T.Cast(round_dtype, v[e]))
                     for k in T.serial(topk):
                         best = -T.infinity("float32")
                         bi = 0
@@ -147,6 +160,38 @@ def router_fused_kernel(n_tok: int, H: int, E: int, topk: int, dtype: str, targe
                         w[bx * block_T + i, kk] = p[kk] / tot
 
     return tilelang.compile(moe_router_fused, out_idx=None, target=target)
+
+
+@functools.lru_cache(maxsize=None)
+def router_logits_sk_kernel(n_tok: int, H: int, E: int, dtype: str, target: str, splits: int = 4, block_T: int = 16,
+                            block_K: int = 256, num_stages: int = 3):
+    """Router logits as a K-split MFMA GEMM: workgroup (token block, split) writes the fp32 partial
+    ``x[:, split] Wg[:, split]^T`` of its 16 tokens to ``P[split]`` (plain stores; the top-k kernel
+    sums the ``splits`` partials).  The fused router streams each token block's whole ``H`` through
+    ONE wave (n_tok / 16 waves on the chip: 128 for the bench layer, latency-bound); this puts
+    ``splits`` times as many waves -- and bytes in flight -- on the same pass over x."""
+    Ep = max(16, -(-E // 16) * 16)
+    Hs = H // splits
+    assert H % splits == 0 and Hs % block_K == 0
+
+    @T.prim_func
+    def moe_router_logits_sk(X: T.Tensor((n_tok, H), dtype), Wg: T.Tensor((Ep, H), dtype),
+                             P: T.Tensor((splits, n_tok, Ep), "float32")):
+        with T.Kernel(T.ceildiv(n_tok, block_T), splits, threads=64) as (bx, sk):
+            X_s = T.alloc_shared((block_T, block_K), dtype)
+            W_s = T.alloc_shared((Ep, block_K), dtype)
+            L = T.alloc_fragment((block_T, Ep), "float32")
+            T.clear(L)
+            for k in T.Pipelined(Hs // block_K, num_stages=num_stages):
+                T.copy(X[bx * block_T, sk * Hs + k * block_K], X_s)
+                T.copy(Wg[0, sk * Hs + k * block_K], W_s)
+                T.gemm(X_s, W_s, L, transpose_B=True)
+            T.copy(L, P[sk, bx * block_T, 0])
+
+    return tilelang.compile(moe_router_logits_sk, out_idx=None, target=target)
+
+
+ROUTER_SPLITS = int(__import__("os").environ.get("TL_MOE_ROUTER_SPLITS", "0"))  # 0: the fused one-pass router
 
 
 _GATE_PAD = {}
@@ -756,6 +801,15 @@ def route(x: torch.Tensor, gate_w: torch.Tensor, topk: int):
     if x.dtype in (torch.float16, torch.bfloat16) and H % 256 == 0 and gate_w.dtype == x.dtype and E <= 64:
         ids = torch.empty(n_tok, topk, dtype=torch.int32, device=x.device)
         w = torch.empty(n_tok, topk, dtype=torch.float32, device=x.device)
+        sp = ROUTER_SPLITS
+        if sp > 1 and H % (sp * 256) == 0 and n_tok % 16 == 0:
+            Ep = max(16, -(-E // 16) * 16)
+            part = torch.empty(sp, n_tok, Ep, dtype=torch.float32, device=x.device)
+            router_logits_sk_kernel(n_tok, H, E, _tdt(x.dtype), _target(x.device), sp)(x.contiguous(),
+                                                                                       _padded_gate(gate_w), part)
+            router_topk_kernel(n_tok, E, topk, _target(x.device), parts=sp, E_stride=Ep,
+                               round_dtype=_tdt(x.dtype))(part, ids, w)
+            return ids, w
         router_fused_kernel(n_tok, H, E, topk, _tdt(x.dtype), _target(x.device))(x.contiguous(), _padded_gate(gate_w),
                                                                                   ids, w)
         return ids, w
