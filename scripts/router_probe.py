@@ -24,3 +24,12 @@ for sp in (0, 2, 4, 8, 0, 4):
     same = bool(torch.equal(ids, ref[0])) and bool(torch.allclose(w, ref[1]))
     t = do_bench(lambda: K.route(x, g, 2), warmup=10, rep=100)
     print(f"router splits={sp}: {t * 1e3:.2f} us (incl. host launch), same={same}", flush=True)
+# whole bench layer (GPU runs ahead of the host as in the bench step)
+from tilelang.models.moe import MoEConfig, MoELayer  # noqa: E402
+cfg = MoEConfig(hidden=4096, ffn=2048, n_experts=8, topk=2, dtype=torch.bfloat16, block_M=256,
+                gemm_cfg=dict(block_N=256, block_K=64, num_stages=2, threads=512, ext_M=32))
+layer = MoELayer(cfg, "local", device="cuda")
+for sp in (0, 4, 0, 4):
+    K.ROUTER_SPLITS = sp
+    t = do_bench(lambda: layer(x), warmup=10, rep=50)
+    print(f"MoE layer router splits={sp}: {t * 1e3:.1f} us", flush=True)
