@@ -26,11 +26,14 @@ def main():
         a = torch.randn(g["M"], g["K"], device="cuda").half()
         b = torch.randn(g["K"], g["N"], device="cuda").half()
         fn = lambda: k(a, b)  # noqa: E731
+    elif which == "fa":  # the bench's attention kernel, exactly as bench.py builds it
+        k, (q, kk, v) = bench.build_attn("cuda")
+        fn = lambda: k(q, kk, v)  # noqa: E731
     else:
         from example_mha_fwd_pipelined import flashattn_pipelined
         c = dict(bench.ATTN_CFG)
         k = flashattn_pipelined(c["batch"], c["heads"], c["seq_len"], c["dim"], False, 1, c["block_M"], c["block_N"],
-                                c["threads"], c["num_stages"], mfma="32x32" if which == "fa32" else "16x16")
+                                c["threads"], c["num_stages"], mfma="32x32")
         q, kk, v = (torch.randn(c["batch"], c["seq_len"], c["heads"], c["dim"], device="cuda",
                                 dtype=torch.bfloat16) for _ in range(3))
         fn = lambda: k(q, kk, v)  # noqa: E731
