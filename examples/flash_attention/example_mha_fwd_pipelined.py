@@ -27,7 +27,7 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                         threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
                         young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd", mfma="16x16",
                         sum_mfma=False, sink=False, sm_scale=None, fold_max=False, prescale_q=False,
-                        pingpong=False, pk_scale=False, xcd_heads=False):
+                        pingpong=False, pk_scale=False, xcd_heads=False, skip_masked=False):
     """``young_prio``: the second-dispatched half of the waves runs at issue priority 1 (one
     ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4).
     ``seq_kv`` (default ``seq_len``): key/value length; with ``is_causal`` the mask is aligned
@@ -59,6 +59,9 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     the grid is decoded so that all query tiles of one head run on the same XCD (consecutive slots
     of that XCD), so the head's K/V stream is fetched into ONE XCD's L2 and read by all its tiles
     there, instead of into every XCD.
+    ``skip_masked`` (causal, ``fold_max``): on a diagonal KV tile the waves whose query rows see
+    none of its keys skip the QK^T, PV and row-sum MFMAs (``T.gemm(valid_m_min=)``): up to 6 of
+    the 8 waves on the last diagonal tile.
     ``pk_scale`` (with ``fold_max``): the log2-domain scale is applied by its own element-wise loop
     before the exponentials, so the compiler pairs it into ``v_pk_mul_f32`` (16 instead of 32
     multiplies per wave and tile) instead of one ``v_mul_f32`` in front of every ``v_exp_f32``."""
@@ -165,7 +168,10 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                     else:
                         for i, j in T.Parallel(block_M, block_N):
                             acc_s[i, j] = -scores_max[i]
-                    T.gemm(Q_s, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
+                    # rows below m_lo see none of this tile's keys (causal diagonal)
+                    m_lo = (k * block_N - bx * block_M - past) if (is_causal and skip_masked) else None
+                    T.gemm(Q_s, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma,
+                           valid_m_min=m_lo)
                     # 3: rescale group (one tile behind)
                     if rescale != 0:
                         for i, j in T.Parallel(block_M, dim):
@@ -193,9 +199,11 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                         T.copy(V[bz, by // groups, k * block_N:(k + 1) * block_N, :], V_shared)
                     else:
                         T.copy(V[bz, k * block_N:(k + 1) * block_N, by // groups, :], V_shared)
-                    T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
+                    T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma,
+                           valid_m_min=m_lo)
                     if sum_mfma:
-                        T.gemm(acc_s_cast, ones_s, acc_l, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)
+                        T.gemm(acc_s_cast, ones_s, acc_l, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma,
+                               valid_m_min=m_lo)
                     # 10-11: P = exp2(acc_s) -> bf16
                     if pk:
                         for i, j in T.Parallel(block_M, block_N):

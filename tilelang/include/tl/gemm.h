@@ -235,7 +235,7 @@ TL_DEVICE void gemm_ss_mma(const ss_frags<T, M, N, K, WARP_M, WARP_N>& __restric
 template <typename T, int M, int N, int K, int WARP_M, int WARP_N, bool TB, int B_COLS, uint32_t SWZ_B, int KPERM,
           int PIPE = 0>
 TL_DEVICE void gemm_rs(const T* __restrict__ a_regs, const T* __restrict__ B, float* __restrict__ C,
-                       int wave_in = -1) {
+                       int wave_in = -1, int m_min = 0) {
   typedef mfma_traits<T> MT;
   typedef typename MT::frag F;
   constexpr int WM = M / WARP_M, WN = N / WARP_N;
@@ -244,6 +244,8 @@ TL_DEVICE void gemm_rs(const T* __restrict__ a_regs, const T* __restrict__ B, fl
   const int lane = threadIdx.x & 63;
   const int wave = wave_or(wave_in);
   const int wn = wave % WARP_N;
+  // T.gemm(valid_m_min=): a wave whose rows all lie below m_min has nothing to add (uniform branch)
+  if ((wave / WARP_N + 1) * WM <= m_min) return;
   floatx4* acc = reinterpret_cast<floatx4*>(C);
   if constexpr (PIPE > 0 && N_REP % PIPE == 0 && KSTEPS * N_REP > PIPE) {
     constexpr int G = PIPE, NG = KSTEPS * N_REP / G;  // groups of G fragments, in (kk, ni) order

@@ -198,6 +198,8 @@ class Printer:
                 extra += f", mfma_shape={op.mfma_shape!r}"
             if getattr(op, "valid_m", None) is not None:
                 extra += f", valid_m={self.e(op.valid_m)}"
+            if getattr(op, "valid_m_min", None) is not None:
+                extra += f", valid_m_min={self.e(op.valid_m_min)}"
             if getattr(op, "is_mx", False):
                 return (f"T.gemm_scaled({self.region(op.A)}, {self.region(op.B)}, {self.region(op.C)}, "
                         f"{self.region(op.scale_A)}, {self.region(op.scale_B)}{extra}, a_format={op.a_fmt!r}, "

@@ -108,6 +108,7 @@ class GemmOp(TileOp):
         self.mfma_shape = None  # "16x16" / "32x32" (T.gemm(mfma_shape=...))
         self.E = None  # 2:4 sparse metadata of A (T.gemm_sp): A is then the compressed [M, K/2] tile
         self.valid_m = None  # T.gemm(valid_m=): block-uniform count of rows that need results
+        self.valid_m_min = None  # T.gemm(valid_m_min=): rows below it need no update (register-A GEMMs)
 
     @property
     def is_mx(self) -> bool:

@@ -90,7 +90,7 @@ class GemmWarpPolicy(IntEnum):
 
 def gemm(A, B, C, transpose_A: bool = False, transpose_B: bool = False, policy=GemmWarpPolicy.Square,
          clear_accum=False, k_pack: int = 1, wg_wait: int = 0, mbar=None, mfma_shape: Optional[str] = None,
-         valid_m=None):
+         valid_m=None, valid_m_min=None):
     """Tile GEMM ``C (+)= op(A) @ op(B)`` on the gfx950 matrix cores.  Inputs f16/bf16 (MFMA
     16x16x32, or 32x32x16 with ``mfma_shape="32x32"`` / pass config ``tl.mfma_shape``), fp8
     (16x16x32 / scaled 16x16x128), int8 (int32 accumulator; 16x16x64 or 32x32x32) and fp32
@@ -99,7 +99,13 @@ def gemm(A, B, C, transpose_A: bool = False, transpose_B: bool = False, policy=G
     ``valid_m`` (MI355X extension, f16/bf16 shared-operand GEMMs): a block-uniform row count; waves
     whose accumulator rows all lie at or past it skip their MFMAs and operand reads, leaving those
     rows of C unspecified.  For row tiles that are only partly filled (the padded per-expert row
-    tiles of a MoE grouped GEMM): a 20-row tail tile costs one wave's MFMAs, not the whole tile's."""
+    tiles of a MoE grouped GEMM): a 20-row tail tile costs one wave's MFMAs, not the whole tile's.
+
+    ``valid_m_min`` (register-A GEMMs, MI355X extension): a block-uniform row index; waves whose
+    accumulator rows all lie BELOW it skip their MFMAs.  The caller guarantees those rows would
+    receive nothing (e.g. the query rows of a causal-diagonal attention tile that see none of its
+    keys: -inf scores, zero probabilities), so C is the same either way (the CPU target computes
+    them)."""
     if wg_wait not in (0, None) or mbar is not None:
         raise NotImplementedError("T.gemm: wg_wait / mbar are WGMMA / mbarrier (NVIDIA) features")
     A, B, C = to_region(A), to_region(B), to_region(C)
@@ -107,6 +113,8 @@ def gemm(A, B, C, transpose_A: bool = False, transpose_B: bool = False, policy=G
     op.mfma_shape = mfma_shape
     if valid_m is not None:
         op.valid_m = convert(valid_m)
+    if valid_m_min is not None:
+        op.valid_m_min = convert(valid_m_min)
     return _emit(op)
 
 

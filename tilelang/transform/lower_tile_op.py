@@ -1107,7 +1107,8 @@ class TileOpLowerer(Mutator):
             al = ctx.local_of(A)
             if op.trans_A:
                 raise LoweringError("register A operand cannot be transposed")
-            out.append(L.CallStmt("tl::gemm_rs", [L.BufferPtr(al, 0), pb, L.BufferPtr(cl, 0), ctx.wave_expr()], [
+            vmin = [self.expr(op.valid_m_min)] if getattr(op, "valid_m_min", None) is not None else []
+            out.append(L.CallStmt("tl::gemm_rs", [L.BufferPtr(al, 0), pb, L.BufferPtr(cl, 0), ctx.wave_expr()] + vmin, [
                 ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_B), b_cols,
                 f"{swz_b}u", plan.get("a_kperm", 0), int(getattr(ctx.target, "gemm_rs_pipe", None) or 0)
             ]))

@@ -25,7 +25,7 @@ class Mutator:
         import copy
         op = copy.copy(op)
         for name in ("src", "dst", "A", "B", "C", "buf", "send", "recv", "tmp", "img", "col", "scale_A", "scale_B", "E",
-                     "valid_m"):
+                     "valid_m", "valid_m_min"):
             v = getattr(op, name, None)
             if isinstance(v, BufferRegion):
                 setattr(op, name, self.region(v))
