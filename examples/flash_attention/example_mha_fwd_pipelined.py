@@ -92,7 +92,8 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     @T.macro
     def body(Q, K, V, Output, Sinks):
         # causal: heads on the fastest grid axis and the longest (last) query tiles dispatched first
-        with T.Kernel(*((heads, n_qt, batch) if is_causal else (n_qt, heads, batch)), threads=threads) as (g0_, g1_, bz_):
+        grid = (heads, n_qt, batch) if is_causal else (n_qt, heads, batch)
+        with T.Kernel(*grid, threads=threads) as (g0_, g1_, bz_):
             if xcd_h:
                 pid = g0_ + n_qt * (g1_ + heads * bz_)  # dispatch id: XCD = pid % 8
                 jj = pid // 8
