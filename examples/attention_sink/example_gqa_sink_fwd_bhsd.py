@@ -31,14 +31,16 @@ LOG2E = 1.44269504
 @tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
 def flashattn_sink(batch, heads, seq_q, seq_kv, dim, groups=1, window_size=None, sm_scale=None, block_M=256,
                    block_N=64, num_stages=2, threads=512, dtype="bfloat16", causal=True, lazy_rescale=True,
-                   impl="staged"):
+                   impl="staged", fold=False):
     """``lazy_rescale``: rows keep their running max until a score exceeds it by 2^8 (O is
     rescaled only then, per wave), see example_mha_fwd.py.
 
     Without a sliding window the kernel is the staged FA of
     examples/flash_attention/example_mha_fwd_pipelined.py with its ``sink`` term (Q in registers,
     QK^T(t) next to PV(t-1), softmax row sums on the matrix cores, diagonal-only masks); the
-    windowed form keeps the split-loop schedule below."""
+    windowed form keeps the split-loop schedule below.  ``fold``: the staged kernel's ``fold_max``
+    schedule (running max as the QK^T accumulator init) with ``skip_masked`` (diagonal-tile waves
+    that see no key skip their MFMAs)."""
     if window_size is None and seq_kv % block_N == 0 and impl == "staged":
         import os
         import sys
@@ -46,7 +48,8 @@ def flashattn_sink(batch, heads, seq_q, seq_kv, dim, groups=1, window_size=None,
         from example_mha_fwd_pipelined import flashattn_pipelined
         return flashattn_pipelined.get_tir(batch, heads, seq_q, dim, causal, groups, block_M, block_N, threads,
                                            num_stages, dtype, lazy_rescale, True, seq_kv=seq_kv, layout="bhsd",
-                                           sum_mfma=True, sink=True, sm_scale=sm_scale)
+                                           sum_mfma=True, sink=True, sm_scale=sm_scale, fold_max=fold,
+                                           skip_masked=fold)
     if window_size is not None:
         assert window_size % block_N == 0, "window_size must be divisible by block_N"
     if sm_scale is None:

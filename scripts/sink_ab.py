@@ -21,8 +21,8 @@ flops = 4.0 * b * h * s * s * d * 0.5
 for win in (None, 128):
     ref = m.ref_program(q, k, v, sk, win).float()
     res = {}
-    for impl in ("split", "staged"):
-        kern = m.flashattn_sink(b, h, s, s, d, g, win, impl=impl)
+    for impl in ("split", "staged", "staged+fold"):
+        kern = m.flashattn_sink(b, h, s, s, d, g, win, impl=impl.split("+")[0], fold=impl.endswith("fold"))
         err = (kern(q, k, v, sk).float() - ref).abs().max().item()
         best = 0.0
         for _ in range(3):
