@@ -31,7 +31,7 @@ LOG2E = 1.44269504
 @tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
 def flashattn_sink(batch, heads, seq_q, seq_kv, dim, groups=1, window_size=None, sm_scale=None, block_M=256,
                    block_N=64, num_stages=2, threads=512, dtype="bfloat16", causal=True, lazy_rescale=True,
-                   impl="staged", fold=False):
+                   impl="staged", fold=True):
     """``lazy_rescale``: rows keep their running max until a score exceeds it by 2^8 (O is
     rescaled only then, per wave), see example_mha_fwd.py.
 

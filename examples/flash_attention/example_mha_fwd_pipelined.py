@@ -27,7 +27,7 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                         threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
                         young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd", mfma="16x16",
                         sum_mfma=False, sink=False, sm_scale=None, fold_max=False, prescale_q=False,
-                        pingpong=False, pk_scale=False, xcd_heads=False, skip_masked=False):
+                        pingpong=False, pk_scale=False, xcd_heads=False, skip_masked=True):
     """``young_prio``: the second-dispatched half of the waves runs at issue priority 1 (one
     ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4).
     ``seq_kv`` (default ``seq_len``): key/value length; with ``is_causal`` the mask is aligned
