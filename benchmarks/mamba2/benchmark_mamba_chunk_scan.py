@@ -28,6 +28,9 @@ def configs():
             dict(block_M=256, block_N=64, block_K=32, threads=256, num_stages=2),
             dict(block_M=128, block_N=64, block_K=64, threads=256, num_stages=2),
             dict(block_M=128, block_N=64, block_K=64, threads=256, num_stages=2, xcd_group=True),
+            dict(block_M=128, block_N=64, block_K=64, threads=256, num_stages=2, xcd_group=True, lean=True),
+            dict(block_M=128, block_N=64, block_K=32, threads=256, num_stages=2, xcd_group=True, lean=True),
+            dict(block_M=64, block_N=64, block_K=64, threads=256, num_stages=2, xcd_group=True, lean=True),
             dict(block_M=64, block_N=64, block_K=64, threads=256, num_stages=2, xcd_group=True),
             dict(block_M=128, block_N=64, block_K=32, threads=256, num_stages=2),
             dict(block_M=64, block_N=64, block_K=64, threads=256, num_stages=2)]

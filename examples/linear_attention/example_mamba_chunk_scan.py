@@ -24,8 +24,12 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[7], pass_configs=FAST_MATH)
 def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, block_M=128, block_N=64,
-                   block_K=32, num_stages=2, threads=256, dtype="float16", xcd_group=False):
-    """``xcd_group``: every workgroup of one (batch, chunk) -- all heads and row tiles, which share
+                   block_K=32, num_stages=2, threads=256, dtype="float16", xcd_group=False, lean=False):
+    """``lean``: the intra-chunk loop split into the tiles wholly below the causal diagonal (no
+    mask: no index compare / select per element) and the diagonal tiles, with the row decays in
+    log2 units precomputed once -- the kernel is VALU-bound (PMC: 20x more VALU than MFMA
+    instructions), this trims the per-element decay arithmetic.
+    ``xcd_group``: every workgroup of one (batch, chunk) -- all heads and row tiles, which share
     that chunk's ``cb`` and ``C`` tiles (one group) -- is placed on the same XCD (workgroups go
     round-robin over the 8 XCDs by dispatch id), so the shared tiles are fetched into one XCD's L2
     once instead of into all eight."""
@@ -37,6 +41,14 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
     n_tiles = (chunk_size // block_M) * n_n
     per_group = nheads * n_tiles  # workgroups of one (batch, chunk)
     xcd_group = xcd_group and (batch * nchunks) % 8 == 0 and ngroups == 1
+
+    @T.macro
+    def load_k(cb, x, dA_cumsum, dt, cb_shared, x_shared, dA_k, dt_k, b, c, g, bz, m_idx, n_idx, k):
+        T.copy(cb[b, c, g, m_idx * block_M:(m_idx + 1) * block_M, k * block_K:(k + 1) * block_K], cb_shared)
+        T.copy(x[b, c * chunk_size + k * block_K:c * chunk_size + (k + 1) * block_K, bz,
+                 n_idx * block_N:(n_idx + 1) * block_N], x_shared)
+        T.copy(dA_cumsum[b, bz, c, k * block_K:(k + 1) * block_K], dA_k)
+        T.copy(dt[b, bz, c, k * block_K:(k + 1) * block_K], dt_k)
 
     @T.prim_func
     def main(cb: T.Tensor((batch, nchunks, ngroups, chunk_size, chunk_size), dtype),
@@ -84,18 +96,35 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
             T.gemm(C_shared, st_shared, acc_o, transpose_B=True)
             for i, j in T.Parallel(block_M, block_N):
                 acc_o[i, j] *= scale_m[i]
-            for k in T.Pipelined(T.ceildiv((m_idx + 1) * block_M, block_K), num_stages=num_stages):
-                T.copy(cb[b, c, g, m_idx * block_M:(m_idx + 1) * block_M, k * block_K:(k + 1) * block_K], cb_shared)
-                T.copy(x[b, c * chunk_size + k * block_K:c * chunk_size + (k + 1) * block_K, bz,
-                         n_idx * block_N:(n_idx + 1) * block_N], x_shared)
-                T.copy(dA_cumsum[b, bz, c, k * block_K:(k + 1) * block_K], dA_k)
-                T.copy(dt[b, bz, c, k * block_K:(k + 1) * block_K], dt_k)
-                for i, j in T.Parallel(block_M, block_K):
-                    cb_local[i, j] = T.if_then_else(
-                        m_idx * block_M + i >= k * block_K + j,
-                        cb_shared[i, j] * T.exp2(dA_m[i] * LOG2E - T.Cast(accum_dtype, dA_k[j]) * LOG2E) *
-                        T.Cast(accum_dtype, dt_k[j]), 0)
-                T.gemm(cb_local, x_shared, acc_o)
+            n_tot = T.ceildiv((m_idx + 1) * block_M, block_K)
+            if lean:
+                am = T.alloc_fragment((block_M, ), accum_dtype)
+                for i in T.Parallel(block_M):
+                    am[i] = dA_m[i] * LOG2E
+                n_full = (m_idx * block_M) // block_K  # tiles whose every key precedes every row
+                for k in T.Pipelined(n_full, num_stages=num_stages):
+                    load_k(cb, x, dA_cumsum, dt, cb_shared, x_shared, dA_k, dt_k, b, c, g, bz, m_idx, n_idx, k)
+                    for i, j in T.Parallel(block_M, block_K):
+                        cb_local[i, j] = T.Cast(accum_dtype, cb_shared[i, j]) * T.exp2(
+                            am[i] - T.Cast(accum_dtype, dA_k[j]) * LOG2E) * T.Cast(accum_dtype, dt_k[j])
+                    T.gemm(cb_local, x_shared, acc_o)
+                for k in T.Pipelined(n_full, n_tot, num_stages=num_stages):
+                    load_k(cb, x, dA_cumsum, dt, cb_shared, x_shared, dA_k, dt_k, b, c, g, bz, m_idx, n_idx, k)
+                    for i, j in T.Parallel(block_M, block_K):
+                        cb_local[i, j] = T.if_then_else(
+                            m_idx * block_M + i >= k * block_K + j,
+                            T.Cast(accum_dtype, cb_shared[i, j]) * T.exp2(am[i] - T.Cast(accum_dtype, dA_k[j]) * LOG2E) *
+                            T.Cast(accum_dtype, dt_k[j]), 0)
+                    T.gemm(cb_local, x_shared, acc_o)
+            else:
+                for k in T.Pipelined(n_tot, num_stages=num_stages):
+                    load_k(cb, x, dA_cumsum, dt, cb_shared, x_shared, dA_k, dt_k, b, c, g, bz, m_idx, n_idx, k)
+                    for i, j in T.Parallel(block_M, block_K):
+                        cb_local[i, j] = T.if_then_else(
+                            m_idx * block_M + i >= k * block_K + j,
+                            cb_shared[i, j] * T.exp2(dA_m[i] * LOG2E - T.Cast(accum_dtype, dA_k[j]) * LOG2E) *
+                            T.Cast(accum_dtype, dt_k[j]), 0)
+                    T.gemm(cb_local, x_shared, acc_o)
             T.copy(x[b, row0:row0 + block_M, bz, n_idx * block_N:(n_idx + 1) * block_N], x_res)
             for i, j in T.Parallel(block_M, block_N):
                 o_cast[i, j] = acc_o[i, j] + x_res[i, j] * D[bz]

@@ -145,14 +145,14 @@ def test_linear_attention_fwd():
     torch.testing.assert_close(h, rh, rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("xcd_group", [False, True])
-def test_mamba_chunk_scan(xcd_group):
+@pytest.mark.parametrize("xcd_group,lean", [(False, False), (True, False), (True, True)])
+def test_mamba_chunk_scan(xcd_group, lean):
     """xcd_group: the grid decoded so every workgroup of a (batch, chunk) shares one XCD."""
     import example_mamba_chunk_scan as m
     B = 2 if xcd_group else 1
     args = m.make_inputs(B, 2048, 128, 1, 2, 64, 64, device="cpu") if xcd_group else \
         m.make_inputs(1, 512, 128, 1, 2, 64, 64, device="cpu")
-    k = _both(m.chunk_scan_fwd, B, 2048 if xcd_group else 512, 128, 1, 2, 64, 64, xcd_group=xcd_group)
+    k = _both(m.chunk_scan_fwd, B, 2048 if xcd_group else 512, 128, 1, 2, 64, 64, xcd_group=xcd_group, lean=lean)
     torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=1e-2, atol=2e-2)
 
 

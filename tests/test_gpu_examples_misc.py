@@ -150,11 +150,11 @@ def test_linear_attention_fwd():
     torch.testing.assert_close(h, rh, rtol=1e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("xcd_group", [False, True])
-def test_mamba_chunk_scan(xcd_group):
+@pytest.mark.parametrize("xcd_group,lean", [(False, False), (True, False), (True, True)])
+def test_mamba_chunk_scan(xcd_group, lean):
     import example_mamba_chunk_scan as m
     args = m.make_inputs(2, 4096, 256, 1, 8, 64, 128)
-    k = m.chunk_scan_fwd(2, 4096, 256, 1, 8, 64, 128, xcd_group=xcd_group)
+    k = m.chunk_scan_fwd(2, 4096, 256, 1, 8, 64, 128, block_K=64, xcd_group=xcd_group, lean=lean)
     torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=2e-2, atol=5e-2)
 
 
