@@ -113,8 +113,8 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
                     for i, j in T.Parallel(block_M, block_K):
                         cb_local[i, j] = T.if_then_else(
                             m_idx * block_M + i >= k * block_K + j,
-                            T.Cast(accum_dtype, cb_shared[i, j]) * T.exp2(am[i] - T.Cast(accum_dtype, dA_k[j]) * LOG2E) *
-                            T.Cast(accum_dtype, dt_k[j]), 0)
+                            T.Cast(accum_dtype, cb_shared[i, j]) *
+                            T.exp2(am[i] - T.Cast(accum_dtype, dA_k[j]) * LOG2E) * T.Cast(accum_dtype, dt_k[j]), 0)
                     T.gemm(cb_local, x_shared, acc_o)
             else:
                 for k in T.Pipelined(n_tot, num_stages=num_stages):

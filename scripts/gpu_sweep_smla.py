@@ -23,7 +23,7 @@ idx = r.topk(topk, dim=-1).indices.int()
 idx = torch.where(torch.gather(r, 1, idx.long()) >= 0, idx, torch.full_like(idx, SKV)).view(B, S, 1, topk)
 print(f"indices in {time.time() - t0:.1f}s", flush=True)
 flops = B * S * (DQK + DV) * topk * 2 * H
-configs = [dict(), dict(wide=True), dict(wide=True, lazy_rescale=False)]
+configs = eval(sys.argv[1]) if len(sys.argv) > 1 else [dict(), dict(wide=True), dict(wide=True, lazy_rescale=False)]
 for cfg in configs:
     try:
         k = sparse_mla_fwd(B, S, SKV, H, DV, DQK - DV, topk, **cfg)

@@ -264,3 +264,31 @@ def test_cross_thread_hazard_with_2d_threads_is_refused():
                 S[ty, tx] = A[ty, tx] * 2.0
                 B[ty, tx] = S[ty, tx] + 1.0  # own element
     tilelang.lower(ok, target="hip")
+
+
+def test_lds_atomics_commute_without_barriers():
+    """LDS atomics of one buffer commute: a histogram over several iterations per thread needs
+    the barrier after the zero-fill and the one before the plain read, none between the atomic
+    iterations (they were one barrier per unrolled iteration, each waiting on a global load)."""
+    import re
+    import tilelang
+    import tilelang.language as T
+
+    @T.prim_func
+    def hist(ids: T.Tensor((1024, ), "int32"), out: T.Tensor((8, ), "int32")):
+        with T.Kernel(1, threads=256) as bx:
+            cnt = T.alloc_shared((8, ), "int32")
+            for e in T.Parallel(8):
+                cnt[e] = 0
+            for j in T.Parallel(1024):
+                T.atomic_add(cnt[ids[j]], 1)
+            for e in T.Parallel(8):
+                out[e] = cnt[e]
+    src = tilelang.lower(hist, target="hip").kernel_source
+    body = src[src.find("__global__"):]
+    assert body.count("atomic_add") == 4
+    assert len(re.findall(r"sync_threads\(\)", body)) == 2
+    # the barriers sit after the zero-fill and after the last atomic
+    first_atomic, last_atomic = body.find("atomic_add"), body.rfind("atomic_add")
+    bars = [m.start() for m in re.finditer(r"sync_threads\(\)", body)]
+    assert bars[0] < first_atomic and bars[1] > last_atomic

@@ -26,11 +26,31 @@ def _shared(b) -> bool:
     return isinstance(b, Buffer) and b.scope == "shared"
 
 
-def _expr_reads(e, out: Set):
+def _atomic_targets(e) -> list:
+    """The LDS element loads that are the *target* of an atomic call in ``e`` (``tl.atomic_*``
+    first argument): an atomic read-modify-write, not a plain read."""
+    from ..ir.expr import Call
+    out = []
+    for n in post_order(e):
+        if isinstance(n, Call) and n.op.startswith("tl.atomic") and n.args:
+            a0 = n.args[0]
+            if isinstance(a0, BufferLoad) and _shared(a0.buffer):
+                out.append(a0)
+    return out
+
+
+def _expr_reads(e, out: Set, atoms: Set = None):
+    """Shared buffers ``e`` reads; with ``atoms`` given, buffers it updates atomically go there
+    instead of ``out`` (atomics of one buffer commute, so they need no barrier between them)."""
     if not isinstance(e, PrimExpr):
         return
+    skip = set()
+    if atoms is not None:
+        for a0 in _atomic_targets(e):
+            skip.add(id(a0))
+            atoms.add(a0.buffer)
     for n in post_order(e):
-        if isinstance(n, BufferLoad) and _shared(n.buffer):
+        if isinstance(n, BufferLoad) and _shared(n.buffer) and id(n) not in skip:
             out.add(n.buffer)
         if isinstance(n, L.BufferPtr) and _shared(n.buffer):
             out.add(n.buffer)
@@ -38,44 +58,50 @@ def _expr_reads(e, out: Set):
 
 class _State:
 
-    def __init__(self, reads=None, writes=None):
+    def __init__(self, reads=None, writes=None, atoms=None):
         self.reads: Set = set(reads or ())
         self.writes: Set = set(writes or ())
+        self.atoms: Set = set(atoms or ())  # buffers updated by atomics since the last barrier
 
     def copy(self):
-        return _State(self.reads, self.writes)
+        return _State(self.reads, self.writes, self.atoms)
 
     def merge(self, o):
-        return _State(self.reads | o.reads, self.writes | o.writes)
+        return _State(self.reads | o.reads, self.writes | o.writes, self.atoms | o.atoms)
+
+    def add(self, r, w, a):
+        return _State(self.reads | r, self.writes | w, self.atoms | a)
 
 
-def _stmt_access(s, managed) -> Tuple[Set, Set, bool]:
-    """(reads, writes, is_barrier) of a leaf statement."""
-    r, w = set(), set()
+def _stmt_access(s, managed) -> Tuple[Set, Set, Set, bool]:
+    """(reads, writes, atomics, is_barrier) of a leaf statement.  ``atomics``: shared buffers
+    updated by ``tl.atomic_*`` (with or without a returned old value) -- they conflict with plain
+    reads and writes of the buffer but not with each other."""
+    r, w, a = set(), set(), set()
     if isinstance(s, L.CallStmt):
         if s.name in _BARRIERS:
-            return r, w, True
+            return r, w, a, True
         if s.name in ("tl::glds16", "tl::glds4", "tl::buffer_lds16", "tl::glds16_nt"):
             # async LDS-DMA is only produced by the software pipeline, which orders it with
             # counted vmcnt waits + raw barriers itself (a __syncthreads here would drain it)
-            return r, w, False
-        for a in s.args:
-            _expr_reads(a, r)
+            return r, w, a, False
+        for x in s.args:
+            _expr_reads(x, r, a)
         if s.name.startswith("tl::mesh") or s.name.startswith("tl::comm"):
-            for a in s.args:
-                if isinstance(a, L.BufferPtr) and _shared(a.buffer):
-                    w.add(a.buffer)
-        return r - managed, w - managed, False
+            for x in s.args:
+                if isinstance(x, L.BufferPtr) and _shared(x.buffer):
+                    w.add(x.buffer)
+        return r - managed, w - managed, a - managed, False
     if isinstance(s, S.StoreStmt):
         for i in s.indices:
-            _expr_reads(i, r)
-        _expr_reads(s.value, r)
+            _expr_reads(i, r, a)
+        _expr_reads(s.value, r, a)
         if _shared(s.buffer):
             w.add(s.buffer)
     elif isinstance(s, L.VecStoreStmt):
-        _expr_reads(s.index, r)
+        _expr_reads(s.index, r, a)
         for v in s.values:
-            _expr_reads(v, r)
+            _expr_reads(v, r, a)
         if _shared(s.buffer):
             w.add(s.buffer)
     elif isinstance(s, L.VecLoadStmt):
@@ -89,19 +115,15 @@ def _stmt_access(s, managed) -> Tuple[Set, Set, bool]:
         if _shared(s.dst):
             w.add(s.dst)
     elif isinstance(s, S.LetStmt):
-        _expr_reads(s.value, r)
+        _expr_reads(s.value, r, a)
     elif isinstance(s, S.EvaluateStmt):
-        _expr_reads(s.expr, r)
         from ..ir.expr import Call
         if isinstance(s.expr, Call) and s.expr.op in ("tl.sync_threads", "tl.sync_grid"):
-            return r, w, True
-        if isinstance(s.expr, Call) and s.expr.op.startswith("tl.atomic"):
-            a0 = s.expr.args[0]
-            if isinstance(a0, BufferLoad) and _shared(a0.buffer):
-                w.add(a0.buffer)
+            return r, w, a, True
+        _expr_reads(s.expr, r, a)
     elif isinstance(s, S.AssertStmt):
-        _expr_reads(s.cond, r)
-    return r - managed, w - managed, False
+        _expr_reads(s.cond, r, a)
+    return r - managed, w - managed, a - managed, False
 
 
 def _sync():
@@ -118,10 +140,12 @@ class ThreadSync:
         self.loop_ranges = {}  # enclosing constant-bounded loops (for the divergent-branch proof)
         self.uniform = set()
 
-    def needs(self, st: _State, r, w) -> bool:
+    def needs(self, st: _State, r, w, a=frozenset()) -> bool:
         # RAW and WAR hazards; WAW between different threads writing the same location is
-        # a program race in the tile model and is not ordered by the compiler (as in the reference)
-        return bool((r & st.writes) or (w & st.reads))
+        # a program race in the tile model and is not ordered by the compiler (as in the reference).
+        # An atomic update conflicts with plain accesses of its buffer, never with another atomic
+        # (they commute: a histogram's per-element atomics need no barrier between iterations).
+        return bool((r & st.writes) or (w & st.reads) or ((r | w) & st.atoms) or (a & (st.reads | st.writes)))
 
     def scan(self, s, st: _State):
         """Returns (new_stmt, state_after, inserted_at_front)."""
@@ -137,16 +161,17 @@ class ThreadSync:
         ns, st = self.scan_one(s, st, out)
         return (out[0] if len(out) == 1 else S.SeqStmt(out)), st
 
-    def first_access(self, s) -> Tuple[Set, Set]:
+    def first_access(self, s) -> Tuple[Set, Set, Set]:
         """Accesses of ``s`` before its first unconditional barrier (conservative)."""
-        r_all, w_all = set(), set()
+        r_all, w_all, a_all = set(), set(), set()
         for x in _leaves(s):
-            r, w, bar = _stmt_access(x, self.managed)
+            r, w, a, bar = _stmt_access(x, self.managed)
             if bar:
                 break
             r_all |= r
             w_all |= w
-        return r_all, w_all
+            a_all |= a
+        return r_all, w_all, a_all
 
     def scan_one(self, c, st: _State, out: List):
         if isinstance(c, S.SeqStmt):
@@ -176,14 +201,14 @@ class ThreadSync:
                 if lo is not None and ext is not None:
                     self.loop_ranges = {**self.loop_ranges, c.var: range(lo, lo + ext)}
             # hazard with what precedes the loop: barrier in front
-            r0, w0 = self.first_access(body)
-            if self.needs(st, r0, w0):
+            r0, w0, a0 = self.first_access(body)
+            if self.needs(st, r0, w0, a0):
                 out.append(_sync())
                 st = _State()
             nb, st_end = self.scan(body, st.copy())
             # loop-carried: entry of iteration i+1 after end of iteration i
-            r1, w1 = self.first_access(nb)
-            if self.needs(st_end, r1, w1):
+            r1, w1, a1 = self.first_access(nb)
+            if self.needs(st_end, r1, w1, a1):
                 nb = S.SeqStmt([_sync(), nb])
                 nb, st_end = self.scan(nb, _State())
             self.managed = saved
@@ -196,15 +221,13 @@ class ThreadSync:
             return nc, st.merge(st_end)
         if isinstance(c, S.IfStmt):
             # barriers must not be inside divergent branches: pre-sync if any branch conflicts
-            r0, w0 = set(), set()
+            r0, w0, a0 = set(), set(), set()
             for x in _leaves(c):
-                r, w, _ = _stmt_access(x, self.managed)
+                r, w, a, _ = _stmt_access(x, self.managed)
                 r0 |= r
                 w0 |= w
-            rc = set()
-            _expr_reads(c.cond, rc)
-            r0 |= rc
-            if self.needs(st, r0, w0):
+                a0 |= a
+            if self.needs(st, r0, w0, a0):
                 out.append(_sync())
                 st = _State()
             if _thread_dependent(c.cond, self.tvars, self.uniform):
@@ -216,7 +239,7 @@ class ThreadSync:
                 # refused rather than emitted as a silent race.
                 _check_divergent_hazards(c, self.managed, self.nthreads, self.tvars, self.loop_ranges, self.tdims)
                 out.append(c)
-                return c, _State(st.reads | r0, st.writes | w0)
+                return c, st.add(r0, w0, a0)
             # block-uniform condition: scan the branches for internal hazards
             tb, st_t = self.scan(c.then_body, st.copy())
             eb, st_e = (self.scan(c.else_body, st.copy()) if c.else_body is not None else (None, st.copy()))
@@ -235,16 +258,15 @@ class ThreadSync:
             k.attrs = dict(c.attrs)
             out.append(k)
             return k, st2
-        r, w, bar = _stmt_access(c, self.managed)
+        r, w, a, bar = _stmt_access(c, self.managed)
         if bar:
             out.append(c)
             return c, _State()
-        if self.needs(st, r, w):
+        if self.needs(st, r, w, a):
             out.append(_sync())
             st = _State()
         out.append(c)
-        st = _State(st.reads | r, st.writes | w)
-        return c, st
+        return c, st.add(r, w, a)
 
 
 def _indexed_access(s, managed):
@@ -255,8 +277,12 @@ def _indexed_access(s, managed):
     def reads_of(e):
         if not isinstance(e, PrimExpr):
             return
+        tgt = _atomic_targets(e)
+        skip = {id(a0) for a0 in tgt}
+        for a0 in tgt:  # an atomic target is an update (ordered like a write), not a plain read
+            out.append((a0.buffer, "w", list(a0.indices), 1))
         for n in post_order(e):
-            if isinstance(n, BufferLoad) and _shared(n.buffer):
+            if isinstance(n, BufferLoad) and _shared(n.buffer) and id(n) not in skip:
                 out.append((n.buffer, "r", list(n.indices), 1))
             elif isinstance(n, L.BufferPtr) and _shared(n.buffer):
                 out.append((n.buffer, "r", None, 0))
@@ -294,11 +320,6 @@ def _indexed_access(s, managed):
             out.append((s.dst, "w", [s.dst_index], max(1, s.nbytes // s.dst.dtype.bytes)))
     elif isinstance(s, S.EvaluateStmt):
         reads_of(s.expr)
-        from ..ir.expr import Call
-        if isinstance(s.expr, Call) and s.expr.op.startswith("tl.atomic"):
-            a0 = s.expr.args[0]
-            if isinstance(a0, BufferLoad) and _shared(a0.buffer):
-                out.append((a0.buffer, "w", list(a0.indices), 1))
     elif isinstance(s, (S.LetStmt, S.AssertStmt)):
         reads_of(s.value if isinstance(s, S.LetStmt) else s.cond)
     return [a for a in out if a[0] not in managed]
