@@ -292,3 +292,36 @@ def test_lds_atomics_commute_without_barriers():
     first_atomic, last_atomic = body.find("atomic_add"), body.rfind("atomic_add")
     bars = [m.start() for m in re.finditer(r"sync_threads\(\)", body)]
     assert bars[0] < first_atomic and bars[1] > last_atomic
+
+
+def test_barrier_before_vector_load_addressed_through_lds():
+    """Regression: a vectorised global load whose row id is read from LDS (``X[pos[r], c]``)
+    reads ``pos``; the barrier between the write of ``pos`` and that load was missing when the
+    load was emitted as one ``load_vec`` (its address expression was not scanned)."""
+    import re
+    import tilelang
+    import tilelang.language as T
+
+    @T.prim_func
+    def rows(X: T.Tensor((64, 64), "bfloat16"), order: T.Tensor((64, ), "int32"),
+             out: T.Tensor((64, ), "float32")):
+        with T.Kernel(1, threads=128) as bx:
+            pos = T.alloc_shared((16, ), "int32")
+            acc = T.alloc_fragment((16, 64), "float32")
+            red = T.alloc_fragment((64, ), "float32")
+            T.clear(acc)
+            for it in T.serial(4):
+                for r in T.Parallel(16):
+                    pos[r] = order[it * 16 + r]
+                for r, c in T.Parallel(16, 64):
+                    acc[r, c] += T.Cast("float32", X[pos[r], c])
+            T.reduce_sum(acc, red, dim=0)
+            T.copy(red, out)
+    src = tilelang.lower(rows, target="hip", pass_configs={"tl.disable_safe_memory_legalize": True}).kernel_source
+    body = src[src.find("for (int"):]
+    loop = body[:body.find("reduce") if "reduce" in body else len(body)]
+    assert "load_vec" in loop
+    first_load = loop.find("load_vec")
+    write = loop.find("&pos[")  # the staged row ids (a 16-byte copy into pos)
+    assert 0 <= write < first_load
+    assert re.search(r"sync_threads\(\)", loop[write:first_load]), loop[:800]

@@ -445,9 +445,15 @@ def test_sparse_mla_bwd_cpu():
     rq, rkv = m.ref_bwd(q, kv, do, idx, D)
     torch.testing.assert_close(dq.float(), rq, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(dkv, rkv, rtol=2e-2, atol=2e-2)
+    da = m.sparse_mla_bwd(q, kv, o, do, idx, lse, dkv="atomic")[1]
+    torch.testing.assert_close(da, rkv, rtol=2e-2, atol=2e-2)
+    order, offs = m.inverse_index(idx, SKV, 32)
+    assert int(offs[-1]) == B * S * topk and order.numel() == B * S * topk + 32
     for impl, args in ((m.sparse_mla_bwd_dq, (1, 64, 256, 64, 512, 64, 128)),
-                       (m.sparse_mla_bwd_dkv, (1, 64, 256, 64, 512, 64, 128))):
-        tilelang.compile(impl.get_tir(*args), out_idx=impl.out_idx, target="hip")
+                       (m.sparse_mla_bwd_dkv, (1, 64, 256, 64, 512, 64, 128)),
+                       (m.sparse_mla_bwd_dkv_contrib, (1, 64, 64, 512, 64, 128)),
+                       (m.sparse_mla_bwd_dkv_reduce, (1, 256, 64 * 128, 512, 64))):
+        tilelang.compile(impl.get_tir(*args), out_idx=impl.out_idx, target="hip", pass_configs=impl.pass_configs)
 
 
 def test_attention_sink_bwd_cpu():

@@ -334,7 +334,8 @@ def test_mxfp4_gemv_gpu(M, N, K):
     torch.testing.assert_close(k(A, Bq, S).float(), ref_program(A, Bq, S).float(), rtol=2e-2, atol=1.0)
 
 
-def test_sparse_mla_bwd_gpu():
+@pytest.mark.parametrize("dkv", ["gather", "atomic"])
+def test_sparse_mla_bwd_gpu(dkv):
     import sparse_mla_bwd as m
     from tilelang.ops.dsa import sparse_mla_fwd
     B, S, SKV, H, topk = 1, 64, 256, 64, 128
@@ -347,10 +348,10 @@ def test_sparse_mla_bwd_gpu():
     idx = r.topk(topk, -1).indices.int()
     idx = torch.where(torch.gather(r, 1, idx.long()) >= 0, idx, torch.full_like(idx, SKV)).view(B, S, 1, topk)
     o, lse = sparse_mla_fwd(B, S, SKV, H, 512, 64, topk)(q, kv, idx)
-    dq, dkv = m.sparse_mla_bwd(q, kv, o, do, idx, lse)
+    dq, dkv_ = m.sparse_mla_bwd(q, kv, o, do, idx, lse, dkv=dkv)
     rq, rkv = m.ref_bwd(q, kv, do, idx)
     torch.testing.assert_close(dq.float().cpu(), rq, rtol=3e-2, atol=3e-2)
-    torch.testing.assert_close(dkv.cpu(), rkv, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(dkv_.cpu(), rkv, rtol=3e-2, atol=3e-2)
 
 
 def test_attention_sink_autograd_gpu():

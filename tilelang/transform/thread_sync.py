@@ -105,11 +105,15 @@ def _stmt_access(s, managed) -> Tuple[Set, Set, Set, bool]:
         if _shared(s.buffer):
             w.add(s.buffer)
     elif isinstance(s, L.VecLoadStmt):
+        # the address may itself read LDS (a row id staged in shared memory: Contrib[pos[r], c])
+        _expr_reads(s.src_index, r, a)
         if _shared(s.src):
             r.add(s.src)
         if _shared(s.dst):
             w.add(s.dst)
     elif isinstance(s, L.CopyBytesStmt):
+        _expr_reads(s.src_index, r, a)
+        _expr_reads(s.dst_index, r, a)
         if _shared(s.src):
             r.add(s.src)
         if _shared(s.dst):
@@ -311,9 +315,12 @@ def _indexed_access(s, managed):
         if _shared(s.buffer):
             out.append((s.buffer, "w", [s.index], len(s.values)))
     elif isinstance(s, L.VecLoadStmt):
+        reads_of(s.src_index)
         if _shared(s.src):
             out.append((s.src, "r", [s.src_index], s.n))
     elif isinstance(s, L.CopyBytesStmt):
+        reads_of(s.src_index)
+        reads_of(s.dst_index)
         if _shared(s.src):
             out.append((s.src, "r", [s.src_index], max(1, s.nbytes // s.src.dtype.bytes)))
         if _shared(s.dst):
