@@ -281,6 +281,9 @@ def inverse_index(indices, SKV, pad):
     return order.to(torch.int32), offs.to(torch.int32)
 
 
+_KERNELS = {}
+
+
 def sparse_mla_bwd(q, kv, o, do, indices, lse, sm_scale=None, target=None, dkv="gather"):
     """(dQ, dKV fp32) for the sparse MLA forward (tilelang.ops.dsa.sparse_mla_fwd).
     ``dkv``: "gather" (bf16 partial rows + sorted-index reduction, deterministic) or "atomic"
@@ -294,8 +297,11 @@ def sparse_mla_bwd(q, kv, o, do, indices, lse, sm_scale=None, target=None, dkv="
     tgt = target or ("cpu" if q.device.type == "cpu" else "hip")
 
     def k_(impl, *args, **kw):
-        return tilelang.compile(impl.get_tir(*args, **kw), out_idx=impl.out_idx, target=tgt,
-                                pass_configs=getattr(impl, "pass_configs", None))
+        key = (id(impl), args, tuple(sorted(kw.items())), tgt)
+        if key not in _KERNELS:  # building + hashing the program costs ms of host time per call
+            _KERNELS[key] = tilelang.compile(impl.get_tir(*args, **kw), out_idx=impl.out_idx, target=tgt,
+                                             pass_configs=getattr(impl, "pass_configs", None))
+        return _KERNELS[key]
 
     delta = k_(sparse_mla_bwd_preprocess, B, S, H, D, dtype=_dt(q))(o, do)
     dq, p, ds = k_(sparse_mla_bwd_dq, B, S, SKV, H, D, DT, topk, sm_scale, dtype=_dt(q))(q, kv, do, indices, lse,
