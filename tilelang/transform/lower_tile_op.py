@@ -1235,7 +1235,11 @@ class TileOpLowerer(Mutator):
             ws = ctx.new_workspace(nd * ctx.T, dt)
             wsf = ctx.flat_of(ws)
             keys = sorted(red_vals)
-            out.append(L.CallStmt("tl::sync_threads", []))
+            # barriers: only the one between the workspace stores and the partner loads is
+            # structural; the ones before the stores (WAR against an earlier use of this
+            # workspace) and after the loads are left to ThreadSync, which places them only
+            # where an access since the last barrier conflicts (a softmax's max and sum
+            # reductions in one tile had 3 barriers each, 2 of them redundant)
             for j, d in enumerate(keys):
                 out.append(S.StoreStmt(wsf, [binop("+", j * ctx.T, ctx.tid)], red_vals[d]))
             out.append(L.CallStmt("tl::sync_threads", []))
@@ -1249,15 +1253,13 @@ class TileOpLowerer(Mutator):
                 v3 = Var(f"redw{d}", dt, nonneg=False)
                 out.append(S.LetStmt(v3, acc))
                 new_vals[d] = v3
-            out.append(L.CallStmt("tl::sync_threads", []))
             red_vals = new_vals
         if redistribute is not None:
             # natural-layout results -> LDS (logical row-major) -> the consumer's layout
             n = _prod(dshape)
             ws = ctx.new_workspace(n, dt)
             wsf = ctx.flat_of(ws)
-            out.append(L.CallStmt("tl::sync_threads", []))
-            for d, v in red_vals.items():
+            for d, v in red_vals.items():  # (surrounding barriers: ThreadSync, as above)
                 idx = D_lay.inverse(ctx.tid, d)
                 out.append(S.StoreStmt(wsf, [_row_major(idx, dshape)], v))
             out.append(L.CallStmt("tl::sync_threads", []))
@@ -1267,7 +1269,6 @@ class TileOpLowerer(Mutator):
                 v = Var(f"redx{r}", dt, nonneg=False)
                 out.append(S.LetStmt(v, BufferLoad(wsf, [_row_major(idx, dshape)])))
                 red_vals[r] = v
-            out.append(L.CallStmt("tl::sync_threads", []))
         for d, v in red_vals.items():
             if op.clear:
                 out.append(S.StoreStmt(dl, [IntImm(d)], cast(v, db.dtype)))
