@@ -33,7 +33,18 @@ def configs():
             dict(block_M=64, block_N=64, block_K=64, threads=256, num_stages=2, xcd_group=True, lean=True),
             dict(block_M=64, block_N=64, block_K=64, threads=256, num_stages=2, xcd_group=True),
             dict(block_M=128, block_N=64, block_K=32, threads=256, num_stages=2),
-            dict(block_M=64, block_N=64, block_K=64, threads=256, num_stages=2)]
+            dict(block_M=64, block_N=64, block_K=64, threads=256, num_stages=2),
+            dict(block_M=128, block_N=64, block_K=64, threads=256, num_stages=2, xcd_group=True, factored=True),
+            dict(block_M=128, block_N=64, block_K=32, threads=256, num_stages=2, xcd_group=True, factored=True),
+            dict(block_M=64, block_N=64, block_K=64, threads=256, num_stages=2, xcd_group=True, factored=True),
+            dict(block_M=256, block_N=64, block_K=64, threads=256, num_stages=2, xcd_group=True, factored=True)]
+
+
+def selected():
+    """``TL_MAMBA_CFGS="8,15,16"``: only those configs (indices into ``configs()``)."""
+    sel = os.environ.get("TL_MAMBA_CFGS")
+    cfgs = configs()
+    return [cfgs[int(i)] for i in sel.split(",")] if sel else cfgs
 
 
 def main():
@@ -57,7 +68,7 @@ def main():
                 torch.testing.assert_close(out[:1].float(), ref, rtol=2e-2, atol=5e-2)
             assert torch.isfinite(out).all()
 
-        cfgs = configs()[:1] if a.quick else configs()
+        cfgs = configs()[:1] if a.quick else selected()
         best = tune(f"mamba2 L={L}", cfgs, build, check)
         tf = flops(B, L, CH, H, P, N) / best["ms"] * 1e-9
         rows.append([L, f"{best['ms']:.4f}", f"{tf:.1f}", H800[L], f"{tf / H800[L]:.2f}x"])

@@ -24,8 +24,17 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[7], pass_configs=FAST_MATH)
 def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, block_M=128, block_N=64,
-                   block_K=32, num_stages=2, threads=256, dtype="float16", xcd_group=False, lean=False):
-    """``lean``: the intra-chunk loop split into the tiles wholly below the causal diagonal (no
+                   block_K=32, num_stages=2, threads=256, dtype="float16", xcd_group=False, lean=False,
+                   factored=False):
+    """``factored``: the decay ``exp(a_i - b_j)`` (a = row, b = key cumulative dA) of every
+    (row, key) element as ``exp(a_i - c) * exp(c - b_j)`` with ``c`` the key window's last (smallest)
+    ``b``: one exp per row and one per key per K step instead of one per element (the kernel is
+    VALU-bound and the exponential issues at a quarter of the VALU rate).  Needs ``dA_cumsum``
+    non-increasing inside a chunk (Mamba-2: ``A < 0``, ``dt > 0``): then ``exp(c - b_j) <= 1`` never
+    overflows, and where ``exp(a_i - c)`` underflows the exact product is below fp32 range too.
+    Rows inside the key window have ``a_i - c`` up to the window's span: a K step whose span is
+    not far below fp32's range (2^96) takes the per-element exp instead (uniform branch).
+``lean``: the intra-chunk loop split into the tiles wholly below the causal diagonal (no
     mask: no index compare / select per element) and the diagonal tiles, with the row decays in
     log2 units precomputed once -- the kernel is VALU-bound (PMC: 20x more VALU than MFMA
     instructions), this trims the per-element decay arithmetic.
@@ -115,6 +124,32 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
                             m_idx * block_M + i >= k * block_K + j,
                             T.Cast(accum_dtype, cb_shared[i, j]) *
                             T.exp2(am[i] - T.Cast(accum_dtype, dA_k[j]) * LOG2E) * T.Cast(accum_dtype, dt_k[j]), 0)
+                    T.gemm(cb_local, x_shared, acc_o)
+            elif factored:
+                am = T.alloc_fragment((block_M, ), accum_dtype)
+                rf = T.alloc_fragment((block_M, ), accum_dtype)
+                gk = T.alloc_shared((block_K, ), accum_dtype)
+                for i in T.Parallel(block_M):
+                    am[i] = dA_m[i] * LOG2E
+                for k in T.Pipelined(n_tot, num_stages=num_stages):
+                    load_k(cb, x, dA_cumsum, dt, cb_shared, x_shared, dA_k, dt_k, b, c, g, bz, m_idx, n_idx, k)
+                    # rows inside the key window see exp(a_i - c) up to exp(window span): factor only
+                    # when the span is far from fp32's range (block-uniform test; Mamba-2 steps are small)
+                    if (T.Cast(accum_dtype, dA_k[0]) - T.Cast(accum_dtype, dA_k[block_K - 1])) * LOG2E < 96.0:
+                        for j in T.Parallel(block_K):  # key factors exp(c - b_j) dt_j, c = b of the last key
+                            gk[j] = T.exp2((T.Cast(accum_dtype, dA_k[block_K - 1]) - T.Cast(accum_dtype, dA_k[j])) *
+                                           LOG2E) * T.Cast(accum_dtype, dt_k[j])
+                        for i in T.Parallel(block_M):
+                            rf[i] = T.exp2(am[i] - T.Cast(accum_dtype, dA_k[block_K - 1]) * LOG2E)
+                        for i, j in T.Parallel(block_M, block_K):
+                            cb_local[i, j] = T.if_then_else(m_idx * block_M + i >= k * block_K + j,
+                                                            T.Cast(accum_dtype, cb_shared[i, j]) * (rf[i] * gk[j]), 0)
+                    else:
+                        for i, j in T.Parallel(block_M, block_K):
+                            cb_local[i, j] = T.if_then_else(
+                                m_idx * block_M + i >= k * block_K + j,
+                                T.Cast(accum_dtype, cb_shared[i, j]) *
+                                T.exp2(am[i] - T.Cast(accum_dtype, dA_k[j]) * LOG2E) * T.Cast(accum_dtype, dt_k[j]), 0)
                     T.gemm(cb_local, x_shared, acc_o)
             else:
                 for k in T.Pipelined(n_tot, num_stages=num_stages):

@@ -53,3 +53,15 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def isa(src: str) -> str:
+    """gfx950 assembly of a generated kernel source (for instruction counts per loop)."""
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "k.hip")
+        open(p, "w").write(src)
+        inc = os.path.join(ROOT, "tilelang", "include")
+        out = os.path.join(d, "k.s")
+        subprocess.run([clang_path(), "-x", "hip", "--offload-arch=gfx950", "--offload-device-only",
+                        "--no-gpu-bundle-output", "-O3", "-std=c++17", f"-I{inc}", "-S", p, "-o", out], check=True)
+        return open(out).read()
