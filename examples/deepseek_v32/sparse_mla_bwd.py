@@ -109,7 +109,8 @@ def sparse_mla_bwd_dq(B, S, SKV, H, D, DT, topk, sm_scale=None, block_I=32, num_
                 T.gemm(dO_frag, KV_s, dp, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 for h, r in T.Parallel(H_blk, block_I):
                     ok = (idx_s[r] <= bx + past) & (idx_s[r] >= 0)
-                    pv = T.if_then_else(ok, T.exp2(s[h, r] * scale - lse[h]), 0.0)
+                    # the mask selects the exponent (exp2(-inf) = 0): no per-element branch
+                    pv = T.exp2(T.if_then_else(ok, s[h, r] * scale - lse[h], -T.infinity(accum)))
                     p_cast[h, r] = pv
                     ds_cast[h, r] = pv * (dp[h, r] - delta[h]) * sm_scale
                 T.copy(p_cast, Pout[bz, bx, h0:h0 + H_blk, i * block_I:(i + 1) * block_I])

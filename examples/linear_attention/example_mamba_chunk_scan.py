@@ -120,10 +120,10 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
                 for k in T.Pipelined(n_full, n_tot, num_stages=num_stages):
                     load_k(cb, x, dA_cumsum, dt, cb_shared, x_shared, dA_k, dt_k, b, c, g, bz, m_idx, n_idx, k)
                     for i, j in T.Parallel(block_M, block_K):
-                        cb_local[i, j] = T.if_then_else(
-                            m_idx * block_M + i >= k * block_K + j,
-                            T.Cast(accum_dtype, cb_shared[i, j]) *
-                            T.exp2(am[i] - T.Cast(accum_dtype, dA_k[j]) * LOG2E) * T.Cast(accum_dtype, dt_k[j]), 0)
+                        cb_local[i, j] = T.Cast(accum_dtype, cb_shared[i, j]) * T.exp2(
+                            T.if_then_else(m_idx * block_M + i >= k * block_K + j,
+                                           am[i] - T.Cast(accum_dtype, dA_k[j]) * LOG2E,
+                                           -T.infinity(accum_dtype))) * T.Cast(accum_dtype, dt_k[j])
                     T.gemm(cb_local, x_shared, acc_o)
             elif factored:
                 am = T.alloc_fragment((block_M, ), accum_dtype)
@@ -146,19 +146,21 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
                                                             T.Cast(accum_dtype, cb_shared[i, j]) * (rf[i] * gk[j]), 0)
                     else:
                         for i, j in T.Parallel(block_M, block_K):
-                            cb_local[i, j] = T.if_then_else(
-                                m_idx * block_M + i >= k * block_K + j,
-                                T.Cast(accum_dtype, cb_shared[i, j]) *
-                                T.exp2(am[i] - T.Cast(accum_dtype, dA_k[j]) * LOG2E) * T.Cast(accum_dtype, dt_k[j]), 0)
+                            cb_local[i, j] = T.Cast(accum_dtype, cb_shared[i, j]) * T.exp2(
+                                T.if_then_else(m_idx * block_M + i >= k * block_K + j,
+                                               am[i] - T.Cast(accum_dtype, dA_k[j]) * LOG2E,
+                                               -T.infinity(accum_dtype))) * T.Cast(accum_dtype, dt_k[j])
                     T.gemm(cb_local, x_shared, acc_o)
             else:
                 for k in T.Pipelined(n_tot, num_stages=num_stages):
                     load_k(cb, x, dA_cumsum, dt, cb_shared, x_shared, dA_k, dt_k, b, c, g, bz, m_idx, n_idx, k)
                     for i, j in T.Parallel(block_M, block_K):
-                        cb_local[i, j] = T.if_then_else(
-                            m_idx * block_M + i >= k * block_K + j,
-                            cb_shared[i, j] * T.exp2(dA_m[i] * LOG2E - T.Cast(accum_dtype, dA_k[j]) * LOG2E) *
-                            T.Cast(accum_dtype, dt_k[j]), 0)
+                        # the causal mask selects the exponent (exp2(-inf) = 0), not the product: a
+                        # select around the exp became a per-element exec-mask branch (5 SALU each)
+                        cb_local[i, j] = cb_shared[i, j] * T.exp2(
+                            T.if_then_else(m_idx * block_M + i >= k * block_K + j,
+                                           dA_m[i] * LOG2E - T.Cast(accum_dtype, dA_k[j]) * LOG2E,
+                                           -T.infinity(accum_dtype))) * T.Cast(accum_dtype, dt_k[j])
                     T.gemm(cb_local, x_shared, acc_o)
             T.copy(x[b, row0:row0 + block_M, bz, n_idx * block_N:(n_idx + 1) * block_N], x_res)
             for i, j in T.Parallel(block_M, block_N):
