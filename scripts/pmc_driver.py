@@ -1,6 +1,6 @@
 """Run one bench kernel (the headline GEMM or FA) N times for a rocprofv3 --pmc pass.
 
-    rocprofv3 --pmc <counters> -- python3 scripts/pmc_driver.py gemm|fa|fa32 [iters]
+    rocprofv3 --pmc <counters> -- python3 scripts/pmc_driver.py gemm|gemm_nt|fa|fa32 [iters]
 """
 import os
 import sys
@@ -25,6 +25,13 @@ def main():
         k = matmul(**g)
         a = torch.randn(g["M"], g["K"], device="cuda").half()
         b = torch.randn(g["K"], g["N"], device="cuda").half()
+        fn = lambda: k(a, b)  # noqa: E731
+    elif which == "gemm_nt":  # B given as [N, K] (K-contiguous, "NT"), the bench's tile config
+        from example_gemm import matmul
+        g = dict(bench.GEMM_CFG)
+        k = matmul(**g, trans_B=True)
+        a = torch.randn(g["M"], g["K"], device="cuda").half()
+        b = torch.randn(g["N"], g["K"], device="cuda").half()
         fn = lambda: k(a, b)  # noqa: E731
     elif which == "fa":  # the bench's attention kernel, exactly as bench.py builds it
         k, (q, kk, v) = bench.build_attn("cuda")
