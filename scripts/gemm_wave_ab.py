@@ -21,17 +21,19 @@ CFGS = [dict(block_M=256, block_N=256, block_K=64, threads=512, num_stages=2, st
 if os.environ.get("TL_GEMM_CFGS"):  # JSON list of extra matmul() kwargs merged into the first config
     CFGS = [dict(CFGS[0], **c) for c in json.loads(os.environ["TL_GEMM_CFGS"])]
 shapes = [tuple(int(v) for v in s.split(",")) for s in sys.argv[1:]] or [(8192, 8192, 8192), (4096, 4096, 4096)]
+NN = os.environ.get("TL_GEMM_NN") == "1"  # B as [K, N] (the bench's layout) instead of [N, K]
 for M, N, K in shapes:
     torch.manual_seed(0)
     A = torch.randn(M, K, device="cuda").half()
-    B = torch.randn(N, K, device="cuda").half()
-    ref = (A[:64].float() @ B.float().T)
+    B = torch.randn(K, N, device="cuda").half() if NN else torch.randn(N, K, device="cuda").half()
+    Bt = B if NN else B.T
+    ref = (A[:64].float() @ Bt.float())
     fl = 2.0 * M * N * K
-    t = do_bench(lambda: A @ B.T, warmup=10, rep=50)
+    t = do_bench(lambda: A @ Bt, warmup=10, rep=50)
     print(f"{M}x{N}x{K} hipBLASLt: {t:.4f} ms {fl / t * 1e-9:.0f} TF", flush=True)
     for cfg in CFGS + CFGS[:1]:
         try:
-            k = matmul(M, N, K, trans_B=True, **cfg)
+            k = matmul(M, N, K, trans_B=not NN, **cfg)
             c = k(A, B)
             err = (c[:64].float() - ref).abs().max().item()
             t = do_bench(lambda: k(A, B), warmup=10, rep=50)
