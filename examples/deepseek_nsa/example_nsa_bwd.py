@@ -201,7 +201,8 @@ def nsa_bwd_dq(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=Non
                     ok = (blk >= 0) & (blk * BS <= pos)
                     if is_causal:
                         ok = ok & (i_s + j <= pos)
-                    p = T.if_then_else(ok, T.exp2(s[g, j] * scale - lse_s[g]), 0.0)
+                    # the mask selects the exponent (exp2(-inf) = 0): no per-element branch around the exp
+                    p = T.exp2(T.if_then_else(ok, s[g, j] * scale - lse_s[g], -T.infinity("float32")))
                     ds_s[g, j] = p * (dp[g, j] - dl_s[g]) * sm
                 T.gemm(ds_s, k_s, dq, policy=pol)
             T.copy(dq, dQ[b, bx, h * G:(h + 1) * G, :])
@@ -293,7 +294,7 @@ def nsa_bwd_dkv(batch, heads, seq_len, seq_len_kv, dim, selected_blocks, is_caus
                         ok = tok_s[r // G] >= 0
                         if is_causal:
                             ok = ok & (j * BS + c <= tok_s[r // G] + past)
-                        p = T.if_then_else(ok, T.exp2(s[r, c] * scale - lse_s[r]), 0.0)
+                        p = T.exp2(T.if_then_else(ok, s[r, c] * scale - lse_s[r], -T.infinity("float32")))
                         p_s[r, c] = p
                         ds_s[r, c] = p * (dp[r, c] - dl_s[r]) * sm
                     T.gemm(p_s, do_s, dv, transpose_A=True)

@@ -180,7 +180,7 @@ def varlen_bwd_dkv(batch, heads, total_q, total_k, max_seqlen_k, dim, is_causal=
                             ok = (kq * block_N + j < q_len) & (by * block_M + i < k_len)
                             if is_causal:
                                 ok = ok & (kq * block_N + j + off >= by * block_M + i)
-                            qkT[i, j] = T.if_then_else(ok, T.exp2(qkT[i, j] * scale - lse_s[j]), 0.0)
+                            qkT[i, j] = T.exp2(T.if_then_else(ok, qkT[i, j] * scale - lse_s[j], -T.infinity("float32")))
                     T.clear(dsT)
                     T.gemm(V_s, do, dsT, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                     T.copy(qkT, qkT_cast)

@@ -64,7 +64,8 @@ def chunk_scaled_dot_kkt(B, S, H, DK, C=64, threads=256, dtype="bfloat16"):
             T.clear(acc)
             T.gemm(k_s, k_s, acc, transpose_B=True)
             for s, t in T.Parallel(C, C):
-                acc[s, t] = T.if_then_else(t < s, acc[s, t] * be_s[s] * T.exp2((g_s[s] - g_s[t]) * LOG2E), 0.0)
+                acc[s, t] = acc[s, t] * be_s[s] * T.exp2(
+                    T.if_then_else(t < s, (g_s[s] - g_s[t]) * LOG2E, -T.infinity("float32")))
             T.copy(acc, A[b, bc * C:(bc + 1) * C, h, :])
 
     return main
@@ -200,7 +201,7 @@ def chunk_o(B, S, H, DK, DV, C=64, scale=None, threads=256, dtype="bfloat16"):
             T.clear(qk)
             T.gemm(q_s, k_s, qk, transpose_B=True)
             for s, t in T.Parallel(C, C):
-                p_s[s, t] = T.if_then_else(t <= s, qk[s, t] * T.exp2((g_s[s] - g_s[t]) * LOG2E), 0.0)
+                p_s[s, t] = qk[s, t] * T.exp2(T.if_then_else(t <= s, (g_s[s] - g_s[t]) * LOG2E, -T.infinity("float32")))
             T.clear(o)
             T.gemm(q_s, h_s, o)
             for s, v in T.Parallel(C, DV):
