@@ -230,11 +230,10 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
                 T.clear(qkT)
                 T.gemm(K_shared, q, qkT, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 T.copy(lse[bz, hq, k * block_N:(k + 1) * block_N], lse_shared)
+                # the causal mask selects the exponent (exp2(-inf) = 0): one pass, no branch
                 for i, j in T.Parallel(block_M, block_N):
-                    qkT[i, j] = T.exp2(qkT[i, j] * scale - lse_shared[j])
-                if is_causal:
-                    for i, j in T.Parallel(block_M, block_N):
-                        qkT[i, j] = T.if_then_else(by * block_M + i <= k * block_N + j, qkT[i, j], 0)
+                    qkT[i, j] = T.exp2(T.if_then_else((by * block_M + i <= k * block_N + j) | (not is_causal),
+                                                      qkT[i, j] * scale - lse_shared[j], -T.infinity(accum_dtype)))
                 T.copy(dO[bz, k * block_N:(k + 1) * block_N, hq, :], do)
                 T.clear(dsT)
                 T.gemm(V_shared, do, dsT, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
@@ -326,9 +325,9 @@ def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N
                 T.clear(dp)
                 T.gemm(do, V_shared, dp, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 for i, j in T.Parallel(block_M, block_N):
-                    ds_cast[i, j] = T.if_then_else(
+                    ds_cast[i, j] = T.exp2(T.if_then_else(
                         (by * block_M + i >= k * block_N + j) | (not is_causal),
-                        T.exp2(s[i, j] * scale - lse_f[i]) * (dp[i, j] - delta_f[i]) * sm_scale, 0)
+                        s[i, j] * scale - lse_f[i], -T.infinity(accum_dtype))) * (dp[i, j] - delta_f[i]) * sm_scale
                 T.gemm(ds_cast, K_shared, dq, policy=T.GemmWarpPolicy.FullRow)
             T.copy(dq, dq_cast)
             T.copy(dq_cast, dQ[bz, by * block_M:(by + 1) * block_M, bx, :])
