@@ -47,7 +47,8 @@ def sparse_mla_topk_reducesum(seq_len, heads, dqk, topk, sm_scale=None, block_I=
                     T.gemm(kv_s, q_s, st, transpose_B=True)
                     for i, h in T.Parallel(block_I, H_blk):
                         idx = Idx[t, ib * block_I + i]
-                        st[i, h] = T.if_then_else((idx >= 0) & (idx <= t), T.exp2(st[i, h] * scale - lse_s[h]), 0.0)
+                        st[i, h] = T.exp2(T.if_then_else((idx >= 0) & (idx <= t), st[i, h] * scale - lse_s[h],
+                                                         -T.infinity("float32")))
                     T.reduce_sum(st, cs, dim=1)
                     for i in T.Parallel(block_I):
                         acc[ib * block_I + i] = acc[ib * block_I + i] + cs[i]

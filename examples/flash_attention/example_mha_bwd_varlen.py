@@ -256,8 +256,8 @@ def varlen_bwd_dq(batch, heads, total_q, total_k, max_seqlen_q, dim, is_causal=T
                             ok = (k * block_N + j < k_len) & (bx * block_M + i < q_len)
                             if is_causal:
                                 ok = ok & (bx * block_M + i + off >= k * block_N + j)
-                            ds_cast[i, j] = T.if_then_else(
-                                ok, T.exp2(s[i, j] * scale - lse_s[i]) * (dp[i, j] - delta_s[i]) * sm_scale, 0.0)
+                            pe = T.exp2(T.if_then_else(ok, s[i, j] * scale - lse_s[i], -T.infinity("float32")))
+                            ds_cast[i, j] = pe * (dp[i, j] - delta_s[i]) * sm_scale
                     T.gemm(ds_cast, K_s, dq, policy=T.GemmWarpPolicy.FullRow)
                 for i, d in T.Parallel(block_M, dim):
                     if bx * block_M + i < q_len:
