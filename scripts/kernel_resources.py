@@ -45,9 +45,11 @@ def main():
         for kw in variants:
             a = dict(block_M=256, block_N=64, threads=512, num_stages=2, q_in_regs=True, sum_mfma=True,
                      fold_max=True)
-            a.update(kw)
+            pc = dict(flashattn_pipelined.pass_configs)
+            pc.update(kw.get("_pc", {}))  # extra pass configs, e.g. {"tl.min_waves_per_eu": 2}
+            a.update({k: v for k, v in kw.items() if k != "_pc"})
             f = flashattn_pipelined.get_tir(1, 64, 4096, 128, False, 1, **a)
-            src = tilelang.lower(f, target="hip", pass_configs=flashattn_pipelined.pass_configs).kernel_source
+            src = tilelang.lower(f, target="hip", pass_configs=pc).kernel_source
             print(json.dumps(kw), resources(src), flush=True)
 
 
