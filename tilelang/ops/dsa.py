@@ -78,6 +78,7 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
             acc_s_cast = T.alloc_fragment([H_blk, block_I], dtype)
             P_shared = T.alloc_shared([H_blk, block_I], dtype)
             alpha_s = T.alloc_shared([H_blk], accum_dtype)
+            any_s = T.alloc_shared([1], "int32")  # wide: some row of this tile moved its max
             acc_o = T.alloc_fragment([H_blk, D], accum_dtype)
             o_cast = T.alloc_fragment([H_blk, D], dtype)
             m_cur = T.alloc_fragment([H_blk], accum_dtype)
@@ -103,6 +104,9 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
                                                  -T.infinity(accum_dtype))
                 T.gemm(Q_frag, KV_shared, acc_s, transpose_B=True, policy=s_policy)
                 T.gemm(Qt_frag, Kt_shared, acc_s, transpose_B=True, policy=s_policy)
+                if wide:
+                    for z in T.Parallel(1):  # previous tile's readers are past the stage barrier
+                        any_s[z] = 0
                 T.copy(m_cur, m_prev)
                 T.reduce_max(acc_s, m_prev, dim=1, clear=False)
                 # lazy rescale: a row keeps its running max until a new score exceeds it by
@@ -115,6 +119,8 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
                         alpha[h] = T.exp2((m_cur[h] - m_prev[h]) * scale)
                         m_cur[h] = m_prev[h]
                         rescale = 1
+                        if wide:
+                            any_s[0] = 1
                     else:
                         alpha[h] = 1.0
                 for h, r in T.Parallel(H_blk, block_I):
@@ -126,8 +132,11 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
                     # O is partitioned over D, not over heads: alpha reaches its waves through LDS
                     T.copy(alpha, alpha_s)
                     T.copy(acc_s, P_shared)
-                    for h, d in T.Parallel(H_blk, D):
-                        acc_o[h, d] *= alpha_s[h]
+                    # lazy rescale across the D-split waves: skipped (block-uniform flag) on the
+                    # tiles where no row moved its max -- most of them after the first few
+                    if any_s[0] != 0:
+                        for h, d in T.Parallel(H_blk, D):
+                            acc_o[h, d] *= alpha_s[h]
                     T.gemm(P_shared, KV_shared, acc_o)
                 else:
                     if rescale != 0:  # per-thread flag: waves whose rows all kept their max skip it
