@@ -49,9 +49,12 @@ def mla_decode(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, bl
 
             T.copy(Q[bx, by * VALID_BLOCK_H:(by + 1) * VALID_BLOCK_H, :], Q_local)
             T.copy(Q_pe[bx, by * VALID_BLOCK_H:(by + 1) * VALID_BLOCK_H, :], Q_pe_local)
+            any_s = T.alloc_shared([1], "int32")
             T.fill(acc_o, 0)
             T.fill(logsum, 0)
-            T.fill(scores_max, -T.infinity(accum_dtype))
+            # wide: lazy rescale (a row keeps its max until a score beats it by 2^8, P <= 256), so
+            # the D-split O accumulator is rescaled only on tiles where some row moved (flag in LDS)
+            T.fill(scores_max, -(2.0**30) if wide else -T.infinity(accum_dtype))
 
             for k in T.Pipelined(T.ceildiv(split_len, block_N), num_stages=num_stages):
                 kv_start = split_len * bz + k * block_N
@@ -60,10 +63,23 @@ def mla_decode(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, bl
                 T.clear(acc_s)
                 T.gemm(Q_local, KV_shared, acc_s, transpose_B=True, policy=s_policy)
                 T.gemm(Q_pe_local, K_pe_shared, acc_s, transpose_B=True, policy=s_policy)
-                T.copy(scores_max, scores_max_prev)
-                T.reduce_max(acc_s, scores_max, dim=1, clear=False)
-                for i in T.Parallel(block_H):
-                    scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
+                if wide:
+                    for z in T.Parallel(1):  # previous tile's readers are past the stage barrier
+                        any_s[z] = 0
+                    T.copy(scores_max, scores_max_prev)
+                    T.reduce_max(acc_s, scores_max_prev, dim=1, clear=False)  # candidate max
+                    for i in T.Parallel(block_H):
+                        if (scores_max_prev[i] - scores_max[i]) * scale > 8.0:
+                            scores_scale[i] = T.exp2((scores_max[i] - scores_max_prev[i]) * scale)
+                            scores_max[i] = scores_max_prev[i]
+                            any_s[0] = 1
+                        else:
+                            scores_scale[i] = 1.0
+                else:
+                    T.copy(scores_max, scores_max_prev)
+                    T.reduce_max(acc_s, scores_max, dim=1, clear=False)
+                    for i in T.Parallel(block_H):
+                        scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
                 for i, j in T.Parallel(block_H, block_N):
                     acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
                 T.reduce_sum(acc_s, scores_sum, dim=1)
@@ -72,8 +88,9 @@ def mla_decode(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, bl
                 if wide:
                     T.copy(scores_scale, sc_shared)
                     T.copy(acc_s, P_shared)
-                    for i, j in T.Parallel(block_H, dim):
-                        acc_o[i, j] *= sc_shared[i]
+                    if any_s[0] != 0:
+                        for i, j in T.Parallel(block_H, dim):
+                            acc_o[i, j] *= sc_shared[i]
                     T.gemm(P_shared, KV_shared, acc_o)
                 else:
                     T.copy(acc_s, acc_s_cast)
