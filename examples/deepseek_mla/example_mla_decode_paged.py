@@ -49,6 +49,7 @@ def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe
             acc_s_cast = T.alloc_fragment([block_H, block_N], dtype)
             P_shared = T.alloc_shared([block_H, block_N], dtype)
             sc_shared = T.alloc_shared([block_H], accum_dtype)
+            any_s = T.alloc_shared([1], "int32")
             acc_o = T.alloc_fragment([block_H, dim], accum_dtype)
             m = T.alloc_fragment([block_H], accum_dtype)
             m_prev = T.alloc_fragment([block_H], accum_dtype)
@@ -76,10 +77,23 @@ def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe
                     acc_s[i, j] = T.if_then_else(tok + j < seqlen, 0, -T.infinity(accum_dtype))
                 T.gemm(Q_local, KV_shared, acc_s, transpose_B=True, policy=s_policy)
                 T.gemm(Q_pe_local, K_pe_shared, acc_s, transpose_B=True, policy=s_policy)
-                T.copy(m, m_prev)
-                T.reduce_max(acc_s, m, dim=1, clear=False)
-                for i in T.Parallel(block_H):
-                    alpha[i] = T.exp2((m_prev[i] - m[i]) * scale)
+                if wide:  # lazy rescale + block-uniform skip flag (example_mla_decode.py)
+                    for z in T.Parallel(1):
+                        any_s[z] = 0
+                    T.copy(m, m_prev)
+                    T.reduce_max(acc_s, m_prev, dim=1, clear=False)  # candidate max
+                    for i in T.Parallel(block_H):
+                        if (m_prev[i] - m[i]) * scale > 8.0:
+                            alpha[i] = T.exp2((m[i] - m_prev[i]) * scale)
+                            m[i] = m_prev[i]
+                            any_s[0] = 1
+                        else:
+                            alpha[i] = 1.0
+                else:
+                    T.copy(m, m_prev)
+                    T.reduce_max(acc_s, m, dim=1, clear=False)
+                    for i in T.Parallel(block_H):
+                        alpha[i] = T.exp2((m_prev[i] - m[i]) * scale)
                 for i, j in T.Parallel(block_H, block_N):
                     acc_s[i, j] = T.exp2(acc_s[i, j] * scale - m[i] * scale)
                 T.reduce_sum(acc_s, r_sum, dim=1)
@@ -88,8 +102,9 @@ def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe
                 if wide:
                     T.copy(alpha, sc_shared)
                     T.copy(acc_s, P_shared)
-                    for i, j in T.Parallel(block_H, dim):
-                        acc_o[i, j] *= sc_shared[i]
+                    if any_s[0] != 0:
+                        for i, j in T.Parallel(block_H, dim):
+                            acc_o[i, j] *= sc_shared[i]
                     T.gemm(P_shared, KV_shared, acc_o)
                 else:
                     T.copy(acc_s, acc_s_cast)
