@@ -325,3 +325,45 @@ def test_barrier_before_vector_load_addressed_through_lds():
     write = loop.find("&pos[")  # the staged row ids (a 16-byte copy into pos)
     assert 0 <= write < first_load
     assert re.search(r"sync_threads\(\)", loop[write:first_load]), loop[:800]
+
+
+def test_cross_wave_reduction_barriers_left_to_thread_sync():
+    """Two cross-wave row reductions per loop iteration (a softmax's max and sum over a tile split
+    across waves) need one barrier each between the workspace stores and the partner loads; the
+    barriers before the stores / after the loads are placed by ThreadSync only when a conflicting
+    access since the last barrier exists (there were 3 per reduction)."""
+    import re
+    import tilelang
+    import tilelang.language as T
+
+    @T.prim_func
+    def two_reduce(A: T.Tensor((8, 64, 64), "float16"), B: T.Tensor((64, 64), "float16"),
+                   O: T.Tensor((64, ), "float32")):
+        with T.Kernel(1, threads=512) as bx:
+            a_s = T.alloc_shared((64, 64), "float16")
+            b_s = T.alloc_shared((64, 64), "float16")
+            s = T.alloc_fragment((64, 64), "float32")
+            mx = T.alloc_fragment((64, ), "float32")
+            sm = T.alloc_fragment((64, ), "float32")
+            tot = T.alloc_fragment((64, ), "float32")
+            T.copy(B, b_s)
+            T.fill(tot, 0)
+            for k in T.serial(8):
+                T.copy(A[k, :, :], a_s)
+                T.clear(s)
+                T.gemm(a_s, b_s, s, policy=T.GemmWarpPolicy.Square)
+                T.reduce_max(s, mx, dim=1)
+                for i, j in T.Parallel(64, 64):
+                    s[i, j] = s[i, j] - mx[i]
+                T.reduce_sum(s, sm, dim=1)
+                for i in T.Parallel(64):
+                    tot[i] += sm[i]
+            T.copy(tot, O)
+    src = tilelang.lower(two_reduce, target="hip").kernel_source
+    m = re.search(r"for \(int \w+ = 0; \w+ < 8;", src)
+    loop = src[m.start():]  # the loop and the short tail after it
+    assert "red_ws" in loop  # the row reductions cross waves (Square policy)
+    n = len(re.findall(r"sync_threads\(\)", loop))
+    # one each for: the a_s tile store -> gemm read, the max stores -> loads, the sum stores -> loads
+    # (+ the loop-carried WAR / tail): with 3 barriers per reduction it would be >= 7
+    assert n <= 5, (n, loop[:1500])
