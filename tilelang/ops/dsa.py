@@ -161,9 +161,14 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
 
 @tilelang.jit(out_idx=[3])
 def mqa_attn_return_logits(seq_len, seq_len_kv, heads, index_dim, block_N=64, threads=256, block_Q=None):
+    """Lightning-indexer logits.  One block per ``block_Q`` query tokens (K tiles reused across
+    them); per token and KV tile: S = K Q_t^T [block_N x heads] on the fp8 MFMA (FullRow: each
+    wave owns whole key rows), relu * head weight in registers, then the sum over heads as an
+    in-wave row reduction, and the key scale applied once per (token, key) after the sum
+    (``k_scale[n]`` factors out of the head sum).  Before: the weighted scores went through LDS
+    and one lane per (token, key) summed its heads serially."""
     if block_Q is None:
         block_Q = max(1, 128 // heads)
-    QH = block_Q * heads
     if seq_len_kv is None:
         seq_len_kv = T.dynamic("seq_len_kv")
     dtype = "float8_e4m3fn"
@@ -175,28 +180,30 @@ def mqa_attn_return_logits(seq_len, seq_len_kv, heads, index_dim, block_N=64, th
              Weights: T.Tensor([seq_len, heads], accum_dtype), CuSeqLenKS: T.Tensor([seq_len], "int32"),
              CuSeqLenKE: T.Tensor([seq_len], "int32")):
         with T.Kernel(T.ceildiv(seq_len, block_Q), threads=threads) as bx:
-            q_shared = T.alloc_shared([QH, index_dim], dtype)
+            q_s = [T.alloc_shared([heads, index_dim], dtype) for _ in range(block_Q)]
             k_shared = T.alloc_shared([block_N, index_dim], dtype)
-            s = T.alloc_fragment([block_N, QH], accum_dtype)
-            s_shared = T.alloc_shared([block_N, QH], accum_dtype)
+            ks_shared = T.alloc_shared([block_N], accum_dtype)
+            w_shared = T.alloc_shared([block_Q, heads], accum_dtype)
+            s = [T.alloc_fragment([block_N, heads], accum_dtype) for _ in range(block_Q)]
+            r = [T.alloc_fragment([block_N], accum_dtype) for _ in range(block_Q)]
             q0 = bx * block_Q
-            T.copy(IndexQ[q0 * heads, 0], q_shared)
+            for bq in list(range(block_Q)):  # trace-time unrolled (a plain range becomes a DSL loop)
+                T.copy(IndexQ[(q0 + bq) * heads, 0], q_s[bq])
+            T.copy(Weights[q0, 0], w_shared)
             for nb in T.Pipelined(T.ceildiv(seq_len_kv, block_N), num_stages=2):
                 T.copy(IndexK[nb * block_N, 0], k_shared)
-                T.clear(s)
-                T.gemm(k_shared, q_shared, s, transpose_B=True)
-                for n, c in T.Parallel(block_N, QH):
-                    s_shared[n, c] = T.max(s[n, c], 0) * Weights[q0 + c // heads, c % heads] * \
-                        IndexKScale[nb * block_N + n]
-                for bq, n in T.Parallel(block_Q, block_N):
-                    acc = T.alloc_var(accum_dtype)
-                    acc = 0.0
-                    for h in T.serial(heads):
-                        acc += s_shared[n, bq * heads + h]
-                    kv_pos = nb * block_N + n
-                    Logits[q0 + bq, kv_pos] = T.if_then_else(
-                        (kv_pos >= CuSeqLenKS[q0 + bq]) & (kv_pos < CuSeqLenKE[q0 + bq]), acc,
-                        -T.infinity(accum_dtype))
+                T.copy(IndexKScale[nb * block_N], ks_shared)
+                for bq in list(range(block_Q)):
+                    T.clear(s[bq])
+                    T.gemm(k_shared, q_s[bq], s[bq], transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                    for n, h in T.Parallel(block_N, heads):
+                        s[bq][n, h] = T.max(s[bq][n, h], 0) * w_shared[bq, h]
+                    T.reduce_sum(s[bq], r[bq], dim=1)
+                    for n in T.Parallel(block_N):
+                        kv_pos = nb * block_N + n
+                        Logits[q0 + bq, kv_pos] = T.if_then_else(
+                            (kv_pos >= CuSeqLenKS[q0 + bq]) & (kv_pos < CuSeqLenKE[q0 + bq]), r[bq][n] * ks_shared[n],
+                            -T.infinity(accum_dtype))
 
     return main
 
