@@ -160,7 +160,7 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
 
 
 @tilelang.jit(out_idx=[3])
-def mqa_attn_return_logits(seq_len, seq_len_kv, heads, index_dim, block_N=64, threads=256, block_Q=None):
+def mqa_attn_return_logits(seq_len, seq_len_kv, heads, index_dim, block_N=128, threads=512, block_Q=None):
     """Lightning-indexer logits.  One block per ``block_Q`` query tokens (K tiles reused across
     them); per token and KV tile: S = K Q_t^T [block_N x heads] on the fp8 MFMA (FullRow: each
     wave owns whole key rows), relu * head weight in registers, then the sum over heads as an
