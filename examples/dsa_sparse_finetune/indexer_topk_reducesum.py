@@ -25,8 +25,11 @@ from index import prepare_token_indices  # noqa: F401  (re-exported for callers)
 
 @tilelang.jit(out_idx=[5])
 def index_logits(seq_len, heads, dim, block_N=64, threads=256, sm_scale=None, dtype="bfloat16"):
+    """Indexer logits of ``block_Q`` query tokens per block: per token, S = K Q_t^T [block_N x
+    heads] (FullRow MFMA: whole key rows per wave), relu * weight, and the head sum as an in-wave
+    row reduction (the scores used to go through LDS and one lane per (token, key) summed its heads
+    serially -- the same change took the fp8 lightning indexer from 282 to ~1.4 PF)."""
     block_Q = max(1, 128 // heads)
-    QH = block_Q * heads
     scale = dim**-0.5 if sm_scale is None else sm_scale
 
     @T.prim_func
@@ -34,17 +37,18 @@ def index_logits(seq_len, heads, dim, block_N=64, threads=256, sm_scale=None, dt
              Weights: T.Tensor([seq_len, heads], dtype), Offsets: T.Tensor([seq_len + 1], "int32"),
              TokenIndices: T.Tensor([seq_len, 2], "int32"), Logits: T.Tensor([seq_len, seq_len], "float32")):
         with T.Kernel(T.ceildiv(seq_len, block_Q), threads=threads) as bx:
-            q_s = T.alloc_shared([QH, dim], dtype)
+            q_s = [T.alloc_shared([heads, dim], dtype) for _ in range(block_Q)]
             k_s = T.alloc_shared([block_N, dim], dtype)
-            s = T.alloc_fragment([block_N, QH], "float32")
-            s_s = T.alloc_shared([block_N, QH], "float32")
-            w_s = T.alloc_shared([QH], "float32")
+            s = [T.alloc_fragment([block_N, heads], "float32") for _ in range(block_Q)]
+            r = [T.alloc_fragment([block_N], "float32") for _ in range(block_Q)]
+            w_s = T.alloc_shared([block_Q, heads], "float32")
             lo_s = T.alloc_shared([block_Q], "int32")
             q0 = bx * block_Q
-            T.copy(IndexQ[q0 * heads, 0], q_s)
-            for c in T.Parallel(QH):
-                t = T.min(q0 + c // heads, seq_len - 1)
-                w_s[c] = T.cast(Weights[t, c % heads], "float32") * scale
+            for bq in list(range(block_Q)):  # trace-time unrolled (a plain range becomes a DSL loop)
+                T.copy(IndexQ[(q0 + bq) * heads, 0], q_s[bq])
+            for u, h in T.Parallel(block_Q, heads):
+                t = T.min(q0 + u, seq_len - 1)
+                w_s[u, h] = T.cast(Weights[t, h], "float32") * scale
             for u in T.Parallel(block_Q):
                 t = T.min(q0 + u, seq_len - 1)
                 lo_s[u] = Offsets[TokenIndices[t, 0]]
@@ -52,20 +56,22 @@ def index_logits(seq_len, heads, dim, block_N=64, threads=256, sm_scale=None, dt
             for nb in T.Pipelined(T.ceildiv(seq_len, block_N), num_stages=2):
                 T.copy(IndexK[nb * block_N, 0], k_s)
                 if nb * block_N <= t_hi:
-                    T.clear(s)
-                    T.gemm(k_s, q_s, s, transpose_B=True)
-                    for n, c in T.Parallel(block_N, QH):
-                        s_s[n, c] = T.max(s[n, c], 0) * w_s[c]
-                for u, n in T.Parallel(block_Q, block_N):
-                    acc = T.alloc_var("float32")
-                    acc = 0.0
-                    key = nb * block_N + n
-                    if key <= t_hi:
-                        for h in T.serial(heads):
-                            acc += s_s[n, u * heads + h]
-                    if (q0 + u < seq_len) & (key < seq_len):
-                        Logits[q0 + u, key] = T.if_then_else((key >= lo_s[u]) & (key <= q0 + u), acc,
-                                                             -T.infinity("float32"))
+                    for bq in list(range(block_Q)):
+                        T.clear(s[bq])
+                        T.gemm(k_s, q_s[bq], s[bq], transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                        for n, h in T.Parallel(block_N, heads):
+                            s[bq][n, h] = T.max(s[bq][n, h], 0) * w_s[bq, h]
+                        T.reduce_sum(s[bq], r[bq], dim=1)
+                        for n in T.Parallel(block_N):
+                            key = nb * block_N + n
+                            if (q0 + bq < seq_len) & (key < seq_len):
+                                Logits[q0 + bq, key] = T.if_then_else((key >= lo_s[bq]) & (key <= q0 + bq),
+                                                                      r[bq][n], -T.infinity("float32"))
+                else:  # every key of the tile is after every query of the block: causally masked
+                    for u, n in T.Parallel(block_Q, block_N):
+                        key = nb * block_N + n
+                        if (q0 + u < seq_len) & (key < seq_len):
+                            Logits[q0 + u, key] = -T.infinity("float32")
 
     return main
 
