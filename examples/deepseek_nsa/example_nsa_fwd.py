@@ -77,17 +77,27 @@ def nsa_fwd(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=None, 
                         ok = ok & (i_s + j <= pos)
                     acc_s[g, j] = T.if_then_else(ok, 0, -T.infinity(accum_dtype))
                 T.gemm(Q_shared, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                # lazy rescale: a row keeps its max until a score beats it by 2^8 (P <= 256), so
+                # the O accumulator is rescaled only on the steps where one of the lane's rows moved
                 T.copy(m, m_prev)
-                T.reduce_max(acc_s, m, dim=1, clear=False)
+                T.reduce_max(acc_s, m_prev, dim=1, clear=False)  # candidate max
+                rescale = T.alloc_var("int32")
+                rescale = 0
                 for g in T.Parallel(G):
-                    alpha[g] = T.exp2((m_prev[g] - m[g]) * scale)
+                    if (m_prev[g] - m[g]) * scale > 8.0:
+                        alpha[g] = T.exp2((m[g] - m_prev[g]) * scale)
+                        m[g] = m_prev[g]
+                        rescale = 1
+                    else:
+                        alpha[g] = 1.0
                 for g, j in T.Parallel(G, BT):
                     acc_s[g, j] = T.exp2(acc_s[g, j] * scale - m[g] * scale)
                 T.reduce_sum(acc_s, r_sum, dim=1)
                 for g in T.Parallel(G):
                     l_sum[g] = l_sum[g] * alpha[g] + r_sum[g]
-                for g, d in T.Parallel(G, D):
-                    acc_o[g, d] *= alpha[g]
+                if rescale != 0:  # per-thread flag: a wave whose rows all kept their max skips it
+                    for g, d in T.Parallel(G, D):
+                        acc_o[g, d] *= alpha[g]
                 T.copy(acc_s, acc_s_cast)
                 T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
             for g, d in T.Parallel(G, D):
