@@ -72,17 +72,26 @@ def _program(mode, batch, heads, heads_kv, dim, block_size, max_sel, num_split, 
                 for i, j in T.Parallel(block_H, BN):
                     acc_s[i, j] = T.if_then_else((blk >= 0) & (kv0 + j < seqlen), 0, -T.infinity(accum))
                 T.gemm(Q_s, K_s, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                # lazy rescale: O is rescaled only when a row's max moves by more than 2^8
                 T.copy(m, m_prev)
-                T.reduce_max(acc_s, m, dim=1, clear=False)
+                T.reduce_max(acc_s, m_prev, dim=1, clear=False)  # candidate max
+                rescale = T.alloc_var("int32")
+                rescale = 0
                 for i in T.Parallel(block_H):
-                    alpha[i] = T.exp2((m_prev[i] - m[i]) * scale)
+                    if (m_prev[i] - m[i]) * scale > 8.0:
+                        alpha[i] = T.exp2((m[i] - m_prev[i]) * scale)
+                        m[i] = m_prev[i]
+                        rescale = 1
+                    else:
+                        alpha[i] = 1.0
                 for i, j in T.Parallel(block_H, BN):
                     acc_s[i, j] = T.exp2(acc_s[i, j] * scale - m[i] * scale)
                 T.reduce_sum(acc_s, r_sum, dim=1)
                 for i in T.Parallel(block_H):
                     l_sum[i] = l_sum[i] * alpha[i] + r_sum[i]
-                for i, d in T.Parallel(block_H, dim):
-                    acc_o[i, d] *= alpha[i]
+                if rescale != 0:
+                    for i, d in T.Parallel(block_H, dim):
+                        acc_o[i, d] *= alpha[i]
                 T.copy(acc_s, acc_s_cast)
                 T.gemm(acc_s_cast, V_s, acc_o, policy=T.GemmWarpPolicy.FullRow)
             for i, d in T.Parallel(block_H, dim):

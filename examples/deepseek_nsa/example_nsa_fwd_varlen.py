@@ -77,17 +77,26 @@ def native_sparse_attention_varlen(batch, heads, c_seq_len, dim, is_causal=True,
                         ok = ok & (i_s + j <= i_t)
                     acc_s[g, j] = T.if_then_else(ok, 0, -T.infinity(accum))
                 T.gemm(Q_s, K_s, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                # lazy rescale (example_nsa_fwd.py): O is rescaled only when a row's max moves by 2^8
                 T.copy(m, m_prev)
-                T.reduce_max(acc_s, m, dim=1, clear=False)
+                T.reduce_max(acc_s, m_prev, dim=1, clear=False)  # candidate max
+                rescale = T.alloc_var("int32")
+                rescale = 0
                 for g in T.Parallel(G):
-                    alpha[g] = T.exp2((m_prev[g] - m[g]) * scale)
+                    if (m_prev[g] - m[g]) * scale > 8.0:
+                        alpha[g] = T.exp2((m[g] - m_prev[g]) * scale)
+                        m[g] = m_prev[g]
+                        rescale = 1
+                    else:
+                        alpha[g] = 1.0
                 for g, j in T.Parallel(G, BT):
                     acc_s[g, j] = T.exp2(acc_s[g, j] * scale - m[g] * scale)
                 T.reduce_sum(acc_s, r_sum, dim=1)
                 for g in T.Parallel(G):
                     l_sum[g] = l_sum[g] * alpha[g] + r_sum[g]
-                for g, d in T.Parallel(G, D):
-                    acc_o[g, d] *= alpha[g]
+                if rescale != 0:
+                    for g, d in T.Parallel(G, D):
+                        acc_o[g, d] *= alpha[g]
                 T.copy(acc_s, acc_s_cast)
                 T.gemm(acc_s_cast, V_s, acc_o, policy=T.GemmWarpPolicy.FullRow)
             for g, d in T.Parallel(G, D):

@@ -97,17 +97,26 @@ def blocksparse_flashattn(batch, heads, seq_q, seq_kv, dim, downsample_len, is_c
                     for r, c in T.Parallel(B_M, B_N):
                         acc_s[r, c] = T.if_then_else(kb * B_N + c < seq_kv, 0, -T.infinity(accum_dtype))
                 T.gemm(Q_shared, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+                # lazy rescale: O is rescaled only when a row's max moves by more than 2^8
                 T.copy(m, m_prev)
-                T.reduce_max(acc_s, m, dim=1, clear=False)
+                T.reduce_max(acc_s, m_prev, dim=1, clear=False)  # candidate max
+                rescale = T.alloc_var("int32")
+                rescale = 0
                 for r in T.Parallel(B_M):
-                    alpha[r] = T.exp2((m_prev[r] - m[r]) * scale)
+                    if (m_prev[r] - m[r]) * scale > 8.0:
+                        alpha[r] = T.exp2((m[r] - m_prev[r]) * scale)
+                        m[r] = m_prev[r]
+                        rescale = 1
+                    else:
+                        alpha[r] = 1.0
                 for r, c in T.Parallel(B_M, B_N):
                     acc_s[r, c] = T.exp2(acc_s[r, c] * scale - m[r] * scale)
                 T.reduce_sum(acc_s, r_sum, dim=1)
                 for r in T.Parallel(B_M):
                     l_sum[r] = l_sum[r] * alpha[r] + r_sum[r]
-                for r, d in T.Parallel(B_M, dim):
-                    acc_o[r, d] *= alpha[r]
+                if rescale != 0:
+                    for r, d in T.Parallel(B_M, dim):
+                        acc_o[r, d] *= alpha[r]
                 T.copy(acc_s, acc_s_cast)
                 T.gemm(acc_s_cast, V_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
             for r, d in T.Parallel(B_M, dim):
