@@ -49,6 +49,7 @@ def mla_decode_persistent(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, blo
             acc_s = T.alloc_fragment([block_H, block_N], accum_dtype)
             P_shared = T.alloc_shared([block_H, block_N], dtype)
             sc_shared = T.alloc_shared([block_H], accum_dtype)
+            any_s = T.alloc_shared([1], "int32")
             acc_o = T.alloc_fragment([block_H, dim], accum_dtype)
             scores_max = T.alloc_fragment([block_H], accum_dtype)
             scores_max_prev = T.alloc_fragment([block_H], accum_dtype)
@@ -71,7 +72,7 @@ def mla_decode_persistent(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, blo
                     T.copy(Q_pe[bid, hid * VALID_BLOCK_H:(hid + 1) * VALID_BLOCK_H, :], Q_pe_local)
                     T.fill(acc_o, 0)
                     T.fill(logsum, 0)
-                    T.fill(scores_max, -T.infinity(accum_dtype))
+                    T.fill(scores_max, -(2.0**30))  # lazy rescale (example_mla_decode.py)
                     for k in T.Pipelined(T.ceildiv(split_len, block_N), num_stages=num_stages):
                         kv_start = split_len * sid + k * block_N
                         T.copy(KV[bid, kv_start:kv_start + block_N, 0, :], KV_shared)
@@ -79,10 +80,17 @@ def mla_decode_persistent(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, blo
                         T.clear(acc_s)
                         T.gemm(Q_local, KV_shared, acc_s, transpose_B=True)
                         T.gemm(Q_pe_local, K_pe_shared, acc_s, transpose_B=True)
+                        for z in T.Parallel(1):  # previous tile's readers are past the stage barrier
+                            any_s[z] = 0
                         T.copy(scores_max, scores_max_prev)
-                        T.reduce_max(acc_s, scores_max, dim=1, clear=False)
+                        T.reduce_max(acc_s, scores_max_prev, dim=1, clear=False)  # candidate max
                         for i in T.Parallel(block_H):
-                            scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
+                            if (scores_max_prev[i] - scores_max[i]) * scale > 8.0:
+                                scores_scale[i] = T.exp2((scores_max[i] - scores_max_prev[i]) * scale)
+                                scores_max[i] = scores_max_prev[i]
+                                any_s[0] = 1
+                            else:
+                                scores_scale[i] = 1.0
                         for i, j in T.Parallel(block_H, block_N):
                             acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
                         T.reduce_sum(acc_s, scores_sum, dim=1)
@@ -90,8 +98,9 @@ def mla_decode_persistent(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, blo
                             logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
                         T.copy(scores_scale, sc_shared)
                         T.copy(acc_s, P_shared)
-                        for i, j in T.Parallel(block_H, dim):
-                            acc_o[i, j] *= sc_shared[i]
+                        if any_s[0] != 0:
+                            for i, j in T.Parallel(block_H, dim):
+                                acc_o[i, j] *= sc_shared[i]
                         T.gemm(P_shared, KV_shared, acc_o)
                     T.copy(logsum, sc_shared)
                     for i, j in T.Parallel(block_H, dim):
