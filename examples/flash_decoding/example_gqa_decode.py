@@ -89,8 +89,10 @@ def _decode_program(batch, heads, groups, dim, block_N, block_H, num_split, thre
                         scores_max[i] == -T.infinity(accum_dtype), 1.0,
                         T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale))
                 for i, j in T.Parallel(block_H, block_N):
-                    acc_s[i, j] = T.if_then_else(acc_s[i, j] == -T.infinity(accum_dtype), 0.0,
-                                                 T.exp2(acc_s[i, j] * scale - scores_max[i] * scale))
+                    # masked scores select a -inf exponent (exp2(-inf) = 0): no per-element branch
+                    ninf = -T.infinity(accum_dtype)
+                    acc_s[i, j] = T.exp2(T.if_then_else(acc_s[i, j] == ninf, ninf,
+                                                        acc_s[i, j] * scale - scores_max[i] * scale))
                 T.reduce_sum(acc_s, scores_sum, dim=1)
                 for i in T.Parallel(block_H):
                     logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
