@@ -55,8 +55,9 @@ def chunk_retention_fwd(B, S, H, DK, DV, chunk_size=64, BV=64, threads=256, dtyp
                 T.clear(s)
                 T.gemm(q, k, s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 for i, j in T.Parallel(chunk_size, chunk_size):
-                    s_cast[i, j] = T.if_then_else(i >= j, s[i, j] * (T.exp2(T.Cast(accum_dtype, i - j) * log_decay) *
-                                                                     scale), 0)
+                    # causal decay: the mask selects the exponent (exp2(-inf) = 0), no per-element branch
+                    s_cast[i, j] = s[i, j] * T.exp2(T.if_then_else(i >= j, T.Cast(accum_dtype, i - j) * log_decay,
+                                                                   -T.infinity(accum_dtype))) * scale
                 T.clear(o)
                 T.gemm(s_cast, v, o, policy=T.GemmWarpPolicy.FullRow)
                 T.copy(h, h_shared)
