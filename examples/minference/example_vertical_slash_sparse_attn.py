@@ -68,12 +68,21 @@ def vs_sparse_flashattn(batch, heads, seq_len, dim, max_blocks, max_cols, block_
 
     @T.macro
     def softmax_step(acc_s, acc_s_cast, acc_o, m, m_prev, alpha, l_sum, r_sum, V_s):
+        # lazy rescale: O is rescaled only when one of the thread's rows moved its max by > 2^8
         T.copy(m, m_prev)
-        T.reduce_max(acc_s, m, dim=1, clear=False)
+        T.reduce_max(acc_s, m_prev, dim=1, clear=False)  # candidate max
+        rescale = T.alloc_var("int32")
+        rescale = 0
         for i in T.Parallel(block_M):
-            alpha[i] = T.exp2((m_prev[i] - m[i]) * scale)
-        for i, d in T.Parallel(block_M, dim):
-            acc_o[i, d] *= alpha[i]
+            if (m_prev[i] - m[i]) * scale > 8.0:
+                alpha[i] = T.exp2((m[i] - m_prev[i]) * scale)
+                m[i] = m_prev[i]
+                rescale = 1
+            else:
+                alpha[i] = 1.0
+        if rescale != 0:
+            for i, d in T.Parallel(block_M, dim):
+                acc_o[i, d] *= alpha[i]
         for i, j in T.Parallel(block_M, block_N):
             acc_s[i, j] = T.exp2(acc_s[i, j] * scale - m[i] * scale)
         T.reduce_sum(acc_s, r_sum, dim=1)
