@@ -169,6 +169,10 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-moe", action="store_true", help="time GEMM + attention only")
+    ap.add_argument("--prewarm-ms", type=float, default=None,
+                    help="untimed, time-based pre-warm before the --warmup steps (default 300 ms on a GPU): the "
+                         "MI355X clocks ramp over the first ~20 ms of dense MFMA work after idle (per-step "
+                         "times below); reported as prewarm_ms, never part of the timed region")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: tiny shapes on the CPU target under gloo (CI plumbing check)")
     args = ap.parse_args()
@@ -275,15 +279,33 @@ def main():
         if moe is not None:
             moe(X)
 
+    # disclosed pre-warm (the reference's do_bench convention: run for a fixed time before
+    # timing, tilelang/profiler/bench.py:63-135): whole steps until prewarm_ms of wall time
+    prewarm_ms = (0.0 if cpu else 300.0) if args.prewarm_ms is None else args.prewarm_ms
+    prewarm_steps = 0
+    sync()
+    tp0 = time.perf_counter()
+    while (time.perf_counter() - tp0) * 1e3 < prewarm_ms:
+        for _ in range(4):
+            step()
+            prewarm_steps += 1
+        sync()
+    prewarm_ms = (time.perf_counter() - tp0) * 1e3
     for _ in range(args.warmup):
         step()
     sync()
     if dist is not None:
         dist.barrier()
     sync()
+    # per-step device timestamps (events do not synchronise; read after the timed region)
+    evs = None if cpu else [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if evs is not None:
+            evs[i].record()
         step()
+    if evs is not None:
+        evs[-1].record()
     sync()
     if dist is not None:
         dist.barrier()
@@ -301,6 +323,7 @@ def main():
         sync()
         return (time.perf_counter() - t) / n * 1e3
 
+    step_ms = [] if evs is None else [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     reps = 2 if cpu else 10
     gemm_ms = timed(lambda: gemm(A, B), reps)
     attn_ms = timed(lambda: attn(Q, K, V), reps)
@@ -384,10 +407,18 @@ def main():
             "moe_comm_fraction": round(moe_comm_ms / moe_ms, 3) if moe is not None and moe_ms > 0 else None,
             "ep_exchange": (None if mesh is None or moe is None else
                             ("device (tl/ep.h, IPC over xGMI, no host sync)" if moe._device_ep() else
-                             "host (RCCL all_to_all_v)")),
+                             f"host ({'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} "
+                             "all_to_all_v)")),
             "ep_fallback_reason": ep_note,
             "tp_moe": tp,
             "pct_of_mfma_peak": round(100.0 * tflops / world / PEAK_BF16_TF, 1),
+            "prewarm_ms": round(prewarm_ms, 1),
+            "prewarm_steps": prewarm_steps,
+            "step_ms_first": round(step_ms[0], 4) if step_ms else None,
+            "step_ms_median": round(sorted(step_ms)[len(step_ms) // 2], 4) if step_ms else None,
+            "step_ms_last": round(step_ms[-1], 4) if step_ms else None,
+            "step_ms_min": round(min(step_ms), 4) if step_ms else None,
+            "step_ms_rank0": [round(x, 3) for x in step_ms],
             "gemm_dtype": "float16",
             "attn_dtype": "bfloat16",
             "moe_dtype": "bfloat16",

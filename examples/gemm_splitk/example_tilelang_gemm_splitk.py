@@ -3,8 +3,9 @@
 C[M,N] (fp32, zero-initialised) += A[:, kslice] @ B[kslice, :] for ``split_k`` K slices in
 parallel: grid (N/bn, M/bm, split_k).  Small-M/N, large-K problems otherwise leave most of
 the 256 CUs idle; splitting K multiplies the block count.  Each block finishes with a
-tile-wide ``T.atomic_add`` into C (``global_atomic_add_f32``; the packed ``pk_add_bf16/f16``
-forms are used for 16-bit outputs).
+tile-wide ``T.atomic_add`` into C (``global_atomic_add_f32`` per element for fp32 output; for
+fp16 / bf16 output the lowering pairs the two adjacent columns each lane holds into one
+``global_atomic_pk_add_{f16,bf16}`` -- AtomicAddVectorize, tests/test_language_atomic.py).
 """
 import argparse
 

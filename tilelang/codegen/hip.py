@@ -34,6 +34,11 @@ _C_KEYWORDS = {"int", "float", "double", "char", "long", "short", "void", "for",
                "abs", "exp", "log", "tid", "lane", "wave", "tl", "smem", "tl_smem"}
 
 
+
+# T.atomic_*(memory_order=...) -> clang __ATOMIC_* (same numbering as the reference's ids)
+_MEMORY_ORDER_C = {"relaxed": "__ATOMIC_RELAXED", "consume": "__ATOMIC_CONSUME", "acquire": "__ATOMIC_ACQUIRE",
+                   "release": "__ATOMIC_RELEASE", "acq_rel": "__ATOMIC_ACQ_REL", "seq_cst": "__ATOMIC_SEQ_CST"}
+
 class CodeGenError(Exception):
     pass
 
@@ -216,19 +221,25 @@ class CodeGen:
             return "tl::lane_id()" if not self.is_cpu else "0"
         if op == "tl.wave_id":
             return "tl::wave_id()" if not self.is_cpu else "0"
-        if op in ("tl.shfl_xor", "tl.shfl_down", "tl.shfl_up", "tl.shfl"):
+        if op in ("tl.shfl_xor", "tl.shfl_down", "tl.shfl_up", "tl.shfl") and not self.is_cpu:
             fn = op.split(".")[1]
             return f"tl::{fn}({', '.join(self.e(a) for a in args)})"
+        if op.startswith("tl.wave_reduce_") or op in ("tl.shfl_xor", "tl.shfl_down", "tl.shfl_up", "tl.shfl"):
+            if self.is_cpu:
+                # the CPU target runs one thread per block: there is no wave to reduce over
+                raise CodeGenError(f"T.{op[3:]}: wave-level reductions / shuffles need the 64 lanes of a "
+                                   "gfx950 wave; the CPU target (one thread per block) cannot emulate them")
         if op.startswith("tl.wave_reduce_"):
             return f"tl::{op[3:]}({self.e(args[0])})"
         if op.startswith("tl.atomic_"):
             kind = op[len("tl.atomic_"):]
-            if kind in ("add", "max", "min"):
-                return f"tl::atomic_{kind}(&{self.e(args[0])}, {self.e(args[1])})"
+            mo = x.attrs.get("memory_order")
+            targ = f"<{_MEMORY_ORDER_C[mo]}>" if mo else ""
+            if kind in ("add", "max", "min", "addx2", "addx4", "store"):
+                rest = ", ".join(self.e(a) for a in args[1:])
+                return f"tl::atomic_{kind}{targ}(&{self.e(args[0])}, {rest})"
             if kind == "load":
-                return f"tl::atomic_load(&{self.e(args[0])})"
-            if kind == "store":
-                return f"tl::atomic_store(&{self.e(args[0])}, {self.e(args[1])})"
+                return f"tl::atomic_load{targ}(&{self.e(args[0])})"
         if op == "tl.clock":
             return "clock64()" if not self.is_cpu else "0"
         if op == "tl.ballot":

@@ -190,13 +190,67 @@ struct BitAndOp {};
 struct BitOrOp {};
 struct BitXorOp {};
 template <typename Op, int M, typename T> inline T lane_allreduce(T v) { return v; }
-template <typename T> inline T wave_reduce_sum(T v) { return v; }
-template <typename T> inline T wave_reduce_max(T v) { return v; }
-template <typename T> inline T wave_reduce_min(T v) { return v; }
+// (no wave_reduce_* here: user-level wave reductions / shuffles need 64 lanes, which the
+// one-thread-per-block CPU target does not have -- codegen refuses them for target "cpu")
 
-template <typename T, typename V> inline T atomic_add(T* p, V v) { T o = *p; *p = (T)((float)o + (float)v); return o; }
-template <typename T, typename V> inline T atomic_max(T* p, V v) { T o = *p; if ((T)v > o) *p = (T)v; return o; }
-template <typename T, typename V> inline T atomic_min(T* p, V v) { T o = *p; if ((T)v < o) *p = (T)v; return o; }
+// Atomics: blocks of a kernel that uses T.sync_grid run as concurrent host threads, so these are
+// real read-modify-writes (CAS on the containing word), with the requested memory order.
+namespace atomic_detail {
+template <typename T> struct word {
+  typedef typename std::conditional<sizeof(T) == 2, uint16_t,
+          typename std::conditional<sizeof(T) == 4, uint32_t, uint64_t>::type>::type type;
+};
+template <int MO, typename T, typename F> inline T rmw(T* p, F f) {
+  typedef typename word<T>::type W;
+  W* wp = reinterpret_cast<W*>(p);
+  W old = __atomic_load_n(wp, __ATOMIC_RELAXED);
+  for (;;) {
+    T cur;
+    memcpy(&cur, &old, sizeof(T));
+    T nv = f(cur);
+    W nw;
+    memcpy(&nw, &nv, sizeof(T));
+    if (__atomic_compare_exchange_n(wp, &old, nw, false, MO == __ATOMIC_RELAXED ? __ATOMIC_RELAXED : __ATOMIC_SEQ_CST,
+                                    __ATOMIC_RELAXED))
+      return cur;
+  }
+}
+}  // namespace atomic_detail
+template <int MO = __ATOMIC_RELAXED, typename T, typename V> inline T atomic_add(T* p, V v) {
+  return atomic_detail::rmw<MO>(p, [&](T c) { return (T)((double)c + (double)v); });
+}
+template <int MO = __ATOMIC_RELAXED, typename T, typename V> inline T atomic_max(T* p, V v) {
+  return atomic_detail::rmw<MO>(p, [&](T c) { return (T)v > c ? (T)v : c; });
+}
+template <int MO = __ATOMIC_RELAXED, typename T, typename V> inline T atomic_min(T* p, V v) {
+  return atomic_detail::rmw<MO>(p, [&](T c) { return (T)v < c ? (T)v : c; });
+}
+template <int MO = __ATOMIC_RELAXED, typename T, typename V0, typename V1> inline T atomic_addx2(T* p, V0 a, V1 b) {
+  T r = atomic_add<MO>(p, a);
+  atomic_add<MO>(p + 1, b);
+  return r;
+}
+template <int MO = __ATOMIC_RELAXED, typename T, typename V0, typename V1, typename V2, typename V3>
+inline T atomic_addx4(T* p, V0 a, V1 b, V2 c, V3 d) {
+  T r = atomic_addx2<MO>(p, a, b);
+  atomic_addx2<MO>(p + 2, c, d);
+  return r;
+}
+template <int MO = __ATOMIC_SEQ_CST, typename T> inline T atomic_load(const T* p) {
+  typedef typename atomic_detail::word<T>::type W;
+  W w = __atomic_load_n(reinterpret_cast<const W*>(p), MO == __ATOMIC_RELEASE ? __ATOMIC_SEQ_CST : MO);
+  T r;
+  memcpy(&r, &w, sizeof(T));
+  return r;
+}
+template <int MO = __ATOMIC_SEQ_CST, typename T, typename V> inline void atomic_store(T* p, V v) {
+  typedef typename atomic_detail::word<T>::type W;
+  T t = (T)v;
+  W w;
+  memcpy(&w, &t, sizeof(T));
+  const bool acq = MO == __ATOMIC_ACQUIRE || MO == __ATOMIC_CONSUME || MO == __ATOMIC_ACQ_REL;
+  __atomic_store_n(reinterpret_cast<W*>(p), w, acq ? __ATOMIC_SEQ_CST : MO);
+}
 
 // C[M,N] += op(A) * op(B); C is the thread-local fp32 accumulator (row-major M x N).
 template <typename T, int M, int N, int K, int TA, int TB, int A_COLS, int B_COLS, typename TC>

@@ -80,6 +80,8 @@ class Printer:
             return f"T.if_then_else({self.e(x.cond)}, {self.e(x.t)}, {self.e(x.f)})"
         if isinstance(x, Call):
             args = ", ".join(self.e(a) for a in x.args)
+            if x.attrs.get("memory_order"):
+                args += f", memory_order={x.attrs['memory_order']!r}"
             return f"T.{x.op}({args})"
         if isinstance(x, BufferLoad):
             return f"{self.names(x.buffer, x.buffer.name)}[{', '.join(self.e(i) for i in x.indices)}]"

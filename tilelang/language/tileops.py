@@ -290,6 +290,7 @@ def warp_reduce_bitor(value):
 
 
 def _atomic(op, dst, value, memory_order=None, return_prev=False):
+    _check_order(memory_order)
     if isinstance(dst, BufferLoad) and isinstance(value, (Buffer, BufferRegion)):
         # tile form with a point destination: T.atomic_add(C[by * bm, bx * bn], C_local)
         dst = to_region(dst, _extents_of(value))
@@ -321,21 +322,66 @@ def atomic_min(dst, value, memory_order=None, return_prev=False):
     return _atomic("min", dst, value, memory_order, return_prev)
 
 
-def atomic_addx2(dst, value, return_prev=False):
-    return _atomic("add", dst, value, None, return_prev)
+_MEMORY_ORDERS = ("relaxed", "consume", "acquire", "release", "acq_rel", "seq_cst")
 
 
-def atomic_addx4(dst, value, return_prev=False):
-    return _atomic("add", dst, value, None, return_prev)
+def _check_order(memory_order):
+    if memory_order is not None and memory_order not in _MEMORY_ORDERS:
+        raise KeyError(f"unknown memory_order {memory_order!r}; one of {_MEMORY_ORDERS}")
+    return memory_order
+
+
+def _point(x):
+    """The first element of a point load / region / buffer, as a BufferLoad."""
+    if isinstance(x, BufferLoad):
+        return x
+    if isinstance(x, BufferRegion):
+        return BufferLoad(x.buffer, list(x.mins))
+    if isinstance(x, Buffer):
+        return BufferLoad(x, [const(0, "int32")] * x.ndim)
+    return None
+
+
+def _atomic_vec(n, dst, value, return_prev, memory_order):
+    """``AtomicAddx2`` / ``AtomicAddx4`` (reference ``tilelang/language/atomic.py:221-296``): add
+    ``n`` consecutive elements of ``value`` to ``n`` consecutive elements of ``dst`` starting at
+    the given (naturally aligned) element.  f16 / bf16 pairs are one packed atomic
+    (``global_atomic_pk_add_{f16,bf16}``, ``ds_pk_add_*`` on LDS); f32 is ``n`` scalar adds.
+    With ``return_prev`` the previous value of the first element is returned."""
+    d = _point(dst)
+    v = _point(value)
+    if d is None or v is None:
+        raise TypeError(f"T.atomic_addx{n}: dst and value must be buffer elements (a load, region or buffer)")
+    vals = []
+    for k in range(n):
+        idx = list(v.indices)
+        idx[-1] = idx[-1] + k if k else idx[-1]
+        vals.append(BufferLoad(v.buffer, idx))
+    e = call(f"tl.atomic_addx{n}", [d] + vals, d.dtype, memory_order=_check_order(memory_order),
+             return_prev=return_prev)
+    if return_prev:
+        return e
+    current_builder().emit(S.EvaluateStmt(e))
+    return None
+
+
+def atomic_addx2(dst, value, return_prev=False, memory_order=None):
+    return _atomic_vec(2, dst, value, return_prev, memory_order)
+
+
+def atomic_addx4(dst, value, return_prev=False, memory_order=None):
+    return _atomic_vec(4, dst, value, return_prev, memory_order)
 
 
 def atomic_load(src, memory_order="seq_cst"):
-    return call("tl.atomic_load", [src], src.dtype, memory_order=memory_order)
+    src = _point(src)
+    return call("tl.atomic_load", [src], src.dtype, memory_order=_check_order(memory_order))
 
 
 def atomic_store(dst, value, memory_order="seq_cst"):
+    dst = _point(dst)
     current_builder().emit(S.EvaluateStmt(call("tl.atomic_store", [dst, convert(value)], dst.dtype,
-                                               memory_order=memory_order)))
+                                               memory_order=_check_order(memory_order))))
 
 
 # ---- views --------------------------------------------------------------------------------

@@ -407,6 +407,8 @@ class _IterRewriter(Mutator):
         def fn(n):
             if isinstance(n, BufferLoad):
                 return self._access(n.buffer, n.indices)
+            if isinstance(n, Call):
+                return _hoist_atomic_guard(n)
             return None
 
         # fragments must be resolved on the ORIGINAL (loop-var) indices, so transform first,
@@ -612,6 +614,53 @@ def vectorize_group(ctx: LowerCtx, stmts: List[S.Stmt], known_div) -> Optional[L
     return pre + [L.VecStoreStmt(b, base, vals)]
 
 
+def _atomic_add_call(s) -> Optional[Call]:
+    """The ``tl.atomic_add(dst[i], v)`` call of an atomic-add statement (no returned value)."""
+    if isinstance(s, S.EvaluateStmt) and isinstance(s.expr, Call) and s.expr.op == "tl.atomic_add" and \
+            len(s.expr.args) == 2 and isinstance(s.expr.args[0], BufferLoad) and not s.expr.attrs.get("return_prev"):
+        return s.expr
+    return None
+
+
+def vectorize_atomic_group(ctx: LowerCtx, stmts: List[S.Stmt], known_div) -> Optional[List[S.Stmt]]:
+    """AtomicAddVectorize (reference ``src/transform/atomicadd_vectorize.cc``), gfx950 form:
+    ``stmts[i]`` are the per-element atomic adds of one thread (i = 0..W-1).  When they hit
+    consecutive f16 / bf16 elements whose first element is pair-aligned, pairs become one
+    ``tl.atomic_addx2`` (``global_atomic_pk_add_{f16,bf16}`` / ``ds_pk_add_*``).  f32 has no vector
+    atomic on gfx950: those groups stay scalar (``global_atomic_add_f32`` each)."""
+    W = len(stmts)
+    if W < 2:
+        return None
+    from ..ir.expr import structural_equal
+    if all(isinstance(s, S.IfStmt) and s.else_body is None for s in stmts):
+        c0 = stmts[0].cond
+        if not all(structural_equal(s.cond, c0) for s in stmts):
+            return None
+        inner = vectorize_atomic_group(ctx, [s.then_body for s in stmts], known_div)
+        return [S.IfStmt(c0, S.SeqStmt(inner))] if inner is not None else None
+    calls = [_atomic_add_call(s) for s in stmts]
+    if any(c is None for c in calls):
+        return None
+    b = calls[0].args[0].buffer
+    if b.dtype.name not in ("float16", "bfloat16") or b.scope not in ("global", "shared") or \
+            any(c.args[0].buffer is not b or len(c.args[0].indices) != 1 for c in calls):
+        return None
+    base = calls[0].args[0].indices[0]
+    for i, c in enumerate(calls):
+        if _const_diff(c.args[0].indices[0], base, []) != i:
+            return None
+    if not divisible_by(base, 2, known_div):
+        return None
+    out = []
+    for i in range(0, W - 1, 2):
+        c0, c1 = calls[i], calls[i + 1]
+        out.append(S.EvaluateStmt(Call("tl.atomic_addx2", [c0.args[0], c0.args[1], c1.args[1]], c0.dtype,
+                                       dict(c0.attrs))))
+    if W % 2:
+        out.append(stmts[-1])
+    return out
+
+
 def _is_cast_of(v, ld):
     from ..ir.expr import Cast
     return isinstance(v, Cast) and v.value is ld
@@ -773,6 +822,7 @@ class TileOpLowerer(Mutator):
         W = layout.inner_vector_width(len(nest.vars) - 1)
         out = []
         body_is_single_store = isinstance(nest.body, S.StoreStmt)
+        body_is_atomic_add = _atomic_add_call(nest.body) is not None
         for r0 in range(0, layout.local_size, W):
             group = []
             for r in range(r0, r0 + W):
@@ -780,6 +830,11 @@ class TileOpLowerer(Mutator):
                 vmap = {v: binop("+", m, i) for v, m, i in zip(nest.vars, nest.mins, idx)}
                 rw = _IterRewriter(ctx, res, r, vmap)
                 group.append(rw.stmt(nest.body))
+            if body_is_atomic_add and W > 1 and not ctx.no_vectorize:
+                vec = vectorize_atomic_group(ctx, group, self.known_div)
+                if vec is not None:
+                    out.extend(vec)
+                    continue
             if body_is_single_store and W > 1 and not ctx.no_vectorize:
                 vec = vectorize_group(ctx, group, self.known_div)
                 if vec is not None:
@@ -823,6 +878,11 @@ class TileOpLowerer(Mutator):
             guard = None
             if (o + 1) * T > slots:
                 guard = binop("<", slot, slots)
+            # inside the tail guard only threads tid < slots - o*T run: tighten tid's range so the
+            # bounds prover can drop per-element guards that only the idle threads would fail
+            saved = ctx.ranges.get(ctx.tid)
+            if guard is not None and saved is not None and slots - o * T - 1 < saved[1]:
+                ctx.ranges[ctx.tid] = (saved[0], slots - o * T - 1)
             group = []
             for v in range(vec):
                 lin = binop("+", binop("*", slot, vec), v) if vec > 1 else slot
@@ -830,11 +890,17 @@ class TileOpLowerer(Mutator):
                 vmap = {var: binop("+", m, x) for var, m, x in zip(nest.vars, nest.mins, vals)}
                 rw = _SimtRewriter(ctx, vmap)
                 group.append(rw.stmt(nest.body))
+            if saved is not None:
+                ctx.ranges[ctx.tid] = saved
             stmts = None
             if single_store and vec > 1:
                 kd = dict(self.known_div)
                 kd[ctx.tid] = (1, 0)
                 stmts = vectorize_group(ctx, group, _slot_div(kd, ctx.tid, o, T, vec))
+            elif vec > 1 and _atomic_add_call(nest.body) is not None:
+                kd = dict(self.known_div)
+                kd[ctx.tid] = (1, 0)
+                stmts = vectorize_atomic_group(ctx, group, _slot_div(kd, ctx.tid, o, T, vec))
             if stmts is None:
                 stmts = [_scoped(g) for g in group] if not single_store else group
             blk = S.SeqStmt(stmts)
@@ -1372,15 +1438,19 @@ class TileOpLowerer(Mutator):
 
     def lower_AtomicOp(self, op: O.AtomicOp):
         dst = op.dst
+        if op.return_prev:
+            raise LoweringError("T.atomic_*(return_prev=True) returns one element's previous value: use the "
+                                "element form (T.atomic_add(dst[i, j], v, return_prev=True)), not a tile")
+        mo = {"memory_order": op.memory_order} if op.memory_order else {}
         if isinstance(op.src, BufferRegion):
             src = op.src
-            nest = _copy_nest(src, dst, None, atomic=op.op)
+            nest = _copy_nest(src, dst, None, atomic=op.op, atomic_attrs=mo)
             lay = None
             if src.buffer.scope == "fragment":
                 lay = _squeeze_fragment(src.buffer.layout, src.buffer.static_shape())
             return self.lower_nest(nest, lay)
         val = op.src
-        nest = _region_nest(dst, lambda idx: None, atomic=(op.op, val))
+        nest = _region_nest(dst, lambda idx: None, atomic=(op.op, val), atomic_attrs=mo)
         return self.lower_nest(nest)
 
     def lower_FinalizeReducerOp(self, op):
@@ -1742,7 +1812,7 @@ def _gather_index(idx: BufferRegion, row) -> PrimExpr:
     return BufferLoad(idx.buffer, ii)
 
 
-def _copy_nest(src: BufferRegion, dst: BufferRegion, coalesced_width, atomic=None) -> S.ForStmt:
+def _copy_nest(src: BufferRegion, dst: BufferRegion, coalesced_width, atomic=None, atomic_attrs=None) -> S.ForStmt:
     sd, dd = _squeeze_pairs(src, dst)
     exts = [dst.extents[d] for d in dd] if dd else []
     vars_ = [Var(f"c{i}") for i in range(len(exts))]
@@ -1753,7 +1823,8 @@ def _copy_nest(src: BufferRegion, dst: BufferRegion, coalesced_width, atomic=Non
         didx[d] = binop("+", didx[d], v)
     val = BufferLoad(src.buffer, sidx)
     if atomic is not None:
-        body = S.EvaluateStmt(call(f"tl.atomic_{atomic}", [BufferLoad(dst.buffer, didx), val], dst.buffer.dtype))
+        body = S.EvaluateStmt(call(f"tl.atomic_{atomic}", [BufferLoad(dst.buffer, didx), val], dst.buffer.dtype,
+                                   **(atomic_attrs or {})))
     else:
         body = S.StoreStmt(dst.buffer, didx, cast(val, dst.buffer.dtype))
     if not exts:
@@ -1765,13 +1836,14 @@ def _copy_nest(src: BufferRegion, dst: BufferRegion, coalesced_width, atomic=Non
     return body
 
 
-def _region_nest(r: BufferRegion, mk, atomic=None) -> S.ForStmt:
+def _region_nest(r: BufferRegion, mk, atomic=None, atomic_attrs=None) -> S.ForStmt:
     exts = list(r.extents)
     vars_ = [Var(f"f{i}") for i in range(len(exts))]
     idx = [binop("+", m, v) for m, v in zip(r.mins, vars_)]
     if atomic is not None:
         kind, val = atomic
-        body = S.EvaluateStmt(call(f"tl.atomic_{kind}", [BufferLoad(r.buffer, idx), convert(val)], r.buffer.dtype))
+        body = S.EvaluateStmt(call(f"tl.atomic_{kind}", [BufferLoad(r.buffer, idx), convert(val)], r.buffer.dtype,
+                                   **(atomic_attrs or {})))
     else:
         b, _, val = mk(idx)
         body = S.StoreStmt(b, idx, val)
@@ -1790,6 +1862,19 @@ def _squeeze_fragment(lay: Fragment, shape) -> Fragment:
     td = [Digit(remap[d.dim], d.stride, d.size) if d.dim >= 0 else d for d in lay.thread_digits]
     ld = [Digit(remap[d.dim], d.stride, d.size) for d in lay.local_digits]
     return Fragment([shape[d] for d in keep], td, ld, lay.name)
+
+
+def _hoist_atomic_guard(n: Call):
+    """An atomic used as a value (``T.atomic_load``, ``return_prev``) takes its first argument by
+    address: a bounds-guarded element ``cond ? A[i] : 0`` becomes ``cond ? atomic(&A[i]) : 0``."""
+    from ..ir.expr import Select
+    if not (isinstance(n.op, str) and n.op.startswith("tl.atomic_") and n.args):
+        return None
+    a0 = n.args[0]
+    if isinstance(a0, Select) and isinstance(a0.t, BufferLoad):
+        inner = Call(n.op, [a0.t] + list(n.args[1:]), n.dtype, dict(n.attrs))
+        return select(a0.cond, inner, const(0, n.dtype))
+    return None
 
 
 def _rewrite_atomic(rw, s: S.EvaluateStmt):
@@ -1831,6 +1916,8 @@ class _SimtRewriter(Mutator):
             ld = BufferLoad(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)])
             g = safe_guard(self.ctx, b, idx)
             return select(g, ld, const(0, b.dtype)) if g is not None else ld
+        if isinstance(n, Call):
+            return _hoist_atomic_guard(n)
         return None
 
     def expr(self, e):
