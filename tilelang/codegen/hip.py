@@ -98,7 +98,9 @@ class CodeGen:
         return name
 
     def buf_name(self, b: Buffer) -> str:
-        key = getattr(b, "orig", None)
+        base = getattr(b, "reinterpret", None)
+        if base is not None:  # dtype view of a tensor: the same address as another element type
+            return f"(({self.ctype(b.dtype)}*)({self.buf_name(base)}))"
         return self.name_of(b, b.name)
 
     # -- expressions ---------------------------------------------------------------------
@@ -311,11 +313,13 @@ class CodeGen:
             v = self.e(st.var)
             mn, ext = st.min, st.extent
             end = mn + ext
-            if st.kind == "unroll" or (as_int(ext) is not None and as_int(ext) <= 8 and st.kind != "serial"):
-                self.w("#pragma unroll")
-            elif st.annotations.get("unroll_factor"):
+            if st.annotations.get("unroll_factor"):
                 self.w(f"#pragma unroll {int(st.annotations['unroll_factor'])}")
-            self.w(f"for (int {v} = {self.e(mn)}; {v} < {self.e(end)}; ++{v}) {{")
+            elif st.kind == "unroll" or (as_int(ext) is not None and as_int(ext) <= 8 and st.kind != "serial"):
+                self.w("#pragma unroll")
+            step = as_int(st.annotations.get("step", 1)) or 1
+            inc = f"++{v}" if step == 1 else f"{v} += {step}"
+            self.w(f"for (int {v} = {self.e(mn)}; {v} < {self.e(end)}; {inc}) {{")
             self.ind += 1
             self.s(st.body)
             self.ind -= 1

@@ -136,7 +136,14 @@ class Buffer:
         from ..language.builder import current_builder
         key = self._norm_index(key)
         if any(isinstance(k, slice) for k in key):
-            raise IndexError("slice assignment to a buffer is not supported; use T.copy / T.fill")
+            # ``A[0, 4:8] = A[0, 0:4]`` is a tile copy, ``A[0, 4:8] = 0`` a fill
+            from ..language import tileops
+            dst = BufferRegion.from_key(self, key)
+            if isinstance(value, (Buffer, BufferRegion)):
+                tileops.copy(value, dst)
+            else:
+                tileops.fill(dst, value)
+            return
         if len(key) != self.ndim:
             raise IndexError(f"{self.name}: expected {self.ndim} indices, got {len(key)}")
         current_builder().store(self, [_neg_index(k, s) for k, s in zip(key, self.shape)], value)

@@ -238,6 +238,20 @@ def lor(a, b_thunk):
     return logical_or(a, b_thunk())
 
 
+def ifexp(c, t_thunk, f_thunk):
+    if isinstance(c, Buffer):
+        c = c.as_scalar()
+    if not isinstance(c, PrimExpr):
+        return t_thunk() if c else f_thunk()
+    if is_static(c):
+        return t_thunk() if static_value(c) else f_thunk()
+    from ..ir.expr import select
+    t, f = t_thunk(), f_thunk()
+    t = t.as_scalar() if isinstance(t, Buffer) else t
+    f = f.as_scalar() if isinstance(f, Buffer) else f
+    return select(c, t, f)
+
+
 def lnot(a):
     if isinstance(a, Buffer):
         a = a.as_scalar()
@@ -271,6 +285,7 @@ class _Helpers:
     land = staticmethod(land)
     lor = staticmethod(lor)
     lnot = staticmethod(lnot)
+    ifexp = staticmethod(ifexp)
     range = staticmethod(tl_range)
     loop_break = staticmethod(loop_break)
     loop_continue = staticmethod(loop_continue)

@@ -119,8 +119,13 @@ def min(a, b, *rest):  # noqa: A001
     return r
 
 
-def clamp(x, lo, hi):
-    return min_expr(max_expr(x, lo), hi)
+def clamp(x, min_val=None, max_val=None):
+    """``min(max(x, min_val), max_val)``; a bound left as None is not applied."""
+    if min_val is not None:
+        x = max_expr(x, min_val)
+    if max_val is not None:
+        x = min_expr(x, max_val)
+    return x
 
 
 def if_then_else(cond, t, f):

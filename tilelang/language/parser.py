@@ -139,6 +139,30 @@ class _Rewriter(ast.NodeTransformer):
             acc = self._call(fn, [acc, ast.Lambda(args=_no_args(), body=v)])
         return acc
 
+    def visit_IfExp(self, node: ast.IfExp):
+        # ``a if c else b``: a select when c is symbolic, Python's own choice when static
+        test = self.visit(node.test)
+        body = self.visit(node.body)
+        orelse = self.visit(node.orelse)
+        return self._call("ifexp", [test, ast.Lambda(args=_no_args(), body=body),
+                                    ast.Lambda(args=_no_args(), body=orelse)])
+
+    def visit_Compare(self, node: ast.Compare):
+        # chained ``a < b < c`` -> ``(a < b) and (b < c)`` (Python would ask bool(a < b))
+        node = self.generic_visit(node)
+        if len(node.ops) == 1:
+            return node
+        import copy
+        parts = []
+        left = node.left
+        for op, right in zip(node.ops, node.comparators):
+            parts.append(ast.Compare(left=copy.deepcopy(left), ops=[op], comparators=[copy.deepcopy(right)]))
+            left = right
+        acc = parts[0]
+        for p in parts[1:]:
+            acc = self._call("land", [acc, ast.Lambda(args=_no_args(), body=p)])
+        return acc
+
     def visit_UnaryOp(self, node: ast.UnaryOp):
         operand = self.visit(node.operand)
         if isinstance(node.op, ast.Not):

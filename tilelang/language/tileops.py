@@ -396,7 +396,16 @@ def reshape(src: Buffer, shape):
 
 
 def view(src: Buffer, shape=None, dtype=None):
+    """A view of ``src`` with a new shape and/or dtype (same bytes, reference ``T.view``)."""
+    from ..ir import dtypes as _dt
     shape = list(shape) if shape is not None else list(src.shape)
-    b = Buffer(src.name + "_view", shape, dtype or src.dtype, src.scope)
+    ndt = _dt.as_dtype(dtype) if dtype is not None else src.dtype
+    n_old, n_new = src.static_numel(), 1
+    for d in shape:
+        n_new = None if n_new is None or as_int(d) is None else n_new * as_int(d)
+    if n_old is not None and n_new is not None:
+        assert n_old * src.dtype.bits == n_new * ndt.bits, (
+            f"T.view({src.name}): {n_old} x {src.dtype.name} cannot be viewed as {shape} x {ndt.name}")
+    b = Buffer(src.name + "_view", shape, ndt, src.scope)
     b.alias_of = (src, 0)
     return b

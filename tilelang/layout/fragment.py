@@ -92,6 +92,55 @@ class Fragment:
             if acc != ext:
                 raise ValueError(f"{self.name}: digits of dim {dim} cover {acc}, extent is {ext}")
 
+    def reshape(self, new_shape: Sequence[int]) -> "Fragment":
+        """The same thread / register assignment of the same elements, indexed by a row-major
+        reshape of the tile (``T.reshape`` / ``T.view`` of a fragment).  Each digit keeps its
+        place in the thread or register number; a digit that straddles a boundary of the new
+        shape is split in two (high part more significant), so the register index of every
+        element is unchanged and the view shares the source's registers."""
+        new_shape = [int(s) for s in new_shape]
+        total = 1
+        for s in self.shape:
+            total *= s
+        nt = 1
+        for s in new_shape:
+            nt *= s
+        if nt != total:
+            raise ValueError(f"{self.name}: cannot reshape {self.shape} to {new_shape}")
+
+        def inner(shape, d):
+            r = 1
+            for s in shape[d + 1:]:
+                r *= s
+            return r
+
+        def convert(d: Digit) -> List[Digit]:
+            if d.dim < 0:
+                return [d]
+            lin, size = d.stride * inner(self.shape, d.dim), d.size
+            parts = []  # least significant first
+            while size > 1:
+                nd = max(i for i in range(len(new_shape)) if inner(new_shape, i) <= lin)
+                inn = inner(new_shape, nd)
+                if lin % inn:
+                    raise ValueError(f"{self.name}: digit {d} does not map onto {new_shape}")
+                st = lin // inn
+                room = new_shape[nd] // st
+                take = min(room, size)
+                if size % take or new_shape[nd] % st:
+                    raise ValueError(f"{self.name}: digit {d} does not map onto {new_shape}")
+                parts.append(Digit(nd, st, take))
+                lin *= take
+                size //= take
+            return list(reversed(parts)) or [Digit(0 if not new_shape else len(new_shape) - 1, 1, 1)]
+
+        td = [x for d in self.thread_digits for x in convert(d)]
+        ld = [x for d in self.local_digits for x in convert(d)]
+        # size-1 placeholder digits would break the tiling check: drop them
+        td = [x for x in td if x.size > 1 or x.dim < 0]
+        ld = [x for x in ld if x.size > 1]
+        return Fragment(new_shape, td, ld, self.name + "_reshape", self.thread_offset)
+
     # -- maps --------------------------------------------------------------------
     def _digit_values(self, idx):
         vals = {}

@@ -31,6 +31,14 @@ class LayoutConflictError(Exception):
     pass
 
 
+def _frag_view_base(b: Buffer):
+    """The fragment a ``T.reshape`` / ``T.view`` buffer aliases (None for other buffers)."""
+    a = getattr(b, "alias_of", None)
+    if b.scope == "fragment" and a is not None and a[0].scope == "fragment":
+        return a[0]
+    return None
+
+
 def _is_frag(b: Buffer) -> bool:
     return b.scope == "fragment"
 
@@ -248,6 +256,8 @@ class LayoutInference:
 
     # ------------------------------------------------------------------------------
     def set_frag(self, buf: Buffer, lay: Fragment, why: str, strict: bool = False):
+        if _frag_view_base(buf) is not None:
+            return False  # a reshaped view of a fragment: its layout follows the base's
         old = self.frag.get(buf)
         if old is not None:
             if old.is_equal(lay):
@@ -342,6 +352,12 @@ class LayoutInference:
         self.assign_shared_layouts()
         for b, lay in self.frag.items():
             b.layout = lay
+        # views of fragments (T.reshape / T.view): the base's layout over the view's shape
+        for op in ops:
+            for r in op.regions():
+                base = _frag_view_base(r.buffer)
+                if base is not None and isinstance(base.layout, Fragment):
+                    r.buffer.layout = base.layout.reshape(r.buffer.static_shape())
         for n in nests:
             if n.layout is not None:
                 n.outer.annotations["_layout"] = n.layout

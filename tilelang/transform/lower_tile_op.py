@@ -161,6 +161,17 @@ class LowerCtx:
         if fb is None:
             if b.alias_of is not None:
                 base = self.flat_of(b.alias_of[0])
+                if b.dtype != base.dtype:
+                    # T.view(..., dtype=): the same bytes read as another type
+                    if base.scope != "global":
+                        raise LoweringError(f"T.view({b.alias_of[0].name}, dtype={b.dtype.name}): a dtype view of a "
+                                            f"{base.scope} buffer is not supported; view the global tensor")
+                    fb = Buffer(b.name, [b.numel()], b.dtype, base.scope)
+                    fb.reinterpret = base
+                    fb.param_index = base.param_index
+                    fb._auto_name = False
+                    self.flat[b] = fb
+                    return fb
                 self.flat[b] = base
                 return base
             size = None
@@ -177,6 +188,13 @@ class LowerCtx:
 
     def local_of(self, b: Buffer) -> Buffer:
         lb = self.frag_local.get(b)
+        a = getattr(b, "alias_of", None)
+        if lb is None and a is not None and a[0].scope == "fragment":
+            if a[0].dtype != b.dtype:
+                raise LoweringError(f"T.view of fragment {a[0].name} with another dtype is not supported")
+            lb = self.local_of(a[0])  # a reshaped view shares the base's registers
+            self.frag_local[b] = lb
+            return lb
         if lb is None:
             lay = b.layout
             if not isinstance(lay, Fragment):
@@ -187,7 +205,18 @@ class LowerCtx:
             self.frag_local[b] = lb
         return lb
 
+    def legal_index(self, b: Buffer, indices):
+        """LegalizeNegativeIndex (reference ``src/transform/legalize_negative_index.cc``): an
+        index that is provably negative counts from the end of its dimension (``A[-i - 1]`` for
+        ``i`` in [0, 4) is ``A[n - 1 - i]``); an index of unknown sign is left alone."""
+        out = []
+        for i, s in zip(indices, b.shape):
+            bd = bound(i, self.ranges)
+            out.append(binop("+", i, s) if bd is not None and bd[1] < 0 else i)
+        return out
+
     def flat_index(self, b: Buffer, indices) -> PrimExpr:
+        indices = self.legal_index(b, indices)
         if b.scope == "shared":
             lay = b.layout
             if lay is None:
@@ -382,7 +411,7 @@ class _IterRewriter(Mutator):
         ld = BufferLoad(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx2)])
         g = safe_guard(self.ctx, b, idx2)
         if g is not None:
-            return select(g, ld, const(0, b.dtype))
+            return select(g, ld, _safe_value(b))
         return ld
 
     def _load_sub(self, n):
@@ -472,16 +501,29 @@ def _const_diff(a: PrimExpr, b: PrimExpr, probe_vars: List[Var]) -> Optional[int
     return int(vals) if vals is not None else None
 
 
+def _safe_value(b: Buffer) -> PrimExpr:
+    """What an out-of-bounds guarded load reads: ``T.annotate_safe_value`` or 0."""
+    v = getattr(b, "safe_value", None)
+    return cast(v, b.dtype) if v is not None else const(0, b.dtype)
+
+
 def safe_guard(ctx: LowerCtx, b: Buffer, idx) -> Optional[PrimExpr]:
     """Bounds condition for a global access that cannot be proven in range (ragged tiles,
     dynamic shapes); None when every index is provably inside the tensor."""
     if b.scope != "global" or ctx.pass_cfg.get("tl.disable_safe_memory_legalize") or getattr(b, "no_guard", False):
         return None
+    idx = ctx.legal_index(b, idx)
     cond = None
     for i, s in zip(idx, b.shape):
         bd = bound(i, ctx.ranges)
         sv = as_int(s)
         if bd is not None and sv is not None and bd[0] >= 0 and bd[1] < sv:
+            continue
+        if bd is not None and bd[0] < 0:
+            # can go below the tensor (a shifted window, ``A[i - 10]``): guard the low side too
+            c = binop(">=", i, 0)
+            cond = c if cond is None else logical_and(cond, c)
+        if bd is not None and sv is not None and bd[1] < sv:
             continue
         c = binop("<", i, s)
         if as_int(c) == 1:
@@ -767,12 +809,73 @@ class TileOpLowerer(Mutator):
     def visit_ForStmt(self, s: S.ForStmt):
         if s.kind == "parallel":
             return self.lower_nest(s)
+        if s.kind == "vectorized" and not self.ctx.is_cpu:
+            r = self.lower_vectorized(s)
+            if r is not None:
+                return r
         mn, ext = as_int(s.min), as_int(s.extent)
         if mn is not None and ext is not None and ext > 0:
             self.ctx.ranges[s.var] = (mn, mn + ext - 1)
         body = self.stmt(s.body)
         kind = s.kind if s.kind in ("serial", "unroll") else "serial"
         return S.ForStmt(s.var, self.expr(s.min), self.expr(s.extent), kind, body, s.annotations)
+
+    def lower_vectorized(self, s: S.ForStmt):
+        """``T.vectorized(n)`` over one store: chunks of W consecutive iterations become one
+        vector access when every access is contiguous in the loop variable and W-aligned (the
+        width follows the strides' common alignment, 16 bytes at most).  Anything else stays
+        a serial loop (clang may still combine it)."""
+        ctx = self.ctx
+        ext = as_int(s.extent)
+        if ext is None or ext < 2 or ctx.no_vectorize:
+            return None
+        body = list(s.body.stmts) if isinstance(s.body, S.SeqStmt) else [s.body]
+        stores = [b for b in body if isinstance(b, S.StoreStmt)]
+        if len(stores) != 1 or any(not isinstance(b, (S.StoreStmt, S.AttrStmt)) for b in body):
+            return None
+        eb = max([stores[0].buffer.dtype.bytes] + [n.buffer.dtype.bytes for n in post_order(stores[0].value)
+                                                   if isinstance(n, BufferLoad)])
+        W = 16 // eb
+        while W >= 2:
+            if ext % W == 0:
+                o = Var("vo")
+                saved = dict(ctx.ranges)
+                ctx.ranges[o] = (0, ext // W - 1)
+                group, pre = [], []
+                for i in range(W):
+                    it = binop("+", binop("+", s.min, binop("*", o, W)), i)
+                    for b in body:
+                        if isinstance(b, S.AttrStmt):
+                            pre.append(self.stmt(S.AttrStmt(b.key, substitute(b.value, {s.var: it}), None)))
+                        else:
+                            group.append(self.stmt(Substituter({s.var: it}).stmt(b)))
+                kd = dict(self.known_div)
+                kd[o] = (1, 0)
+                vec = vectorize_group(ctx, group, kd)
+                ctx.ranges.clear()
+                ctx.ranges.update(saved)
+                if vec is not None:
+                    return S.ForStmt(o, 0, ext // W, "serial", S.SeqStmt(pre + vec))
+            W //= 2
+        return None
+
+    def visit_AttrStmt(self, s):
+        if s.key != "assume":
+            return S.AttrStmt(s.key, s.value, self.stmt(s.body) if s.body is not None else None)
+        # T.assume(cond): divisibility facts (``N % 4 == 0``) feed the vectoriser, and the
+        # condition reaches clang as __builtin_assume on the GPU
+        from ..ir.expr import BinOp as _B
+        stack = [s.value]
+        while stack:
+            c = stack.pop()
+            if isinstance(c, _B) and c.op == "&&":
+                stack += [c.a, c.b]
+            elif isinstance(c, _B) and c.op == "==" and as_int(c.b) == 0 and isinstance(c.a, _B) and \
+                    c.a.op == "%" and isinstance(c.a.a, Var) and as_int(c.a.b):
+                self.known_div[c.a.a] = (as_int(c.a.b), 0)
+        if self.ctx.is_cpu:
+            return S.SeqStmt([])
+        return L.CallStmt("__builtin_assume", [self.expr(s.value)])
 
     def visit_TileOpStmt(self, s):
         op = s.op
@@ -811,7 +914,14 @@ class TileOpLowerer(Mutator):
                                        self.expr(s.value))
                 return _SimtRewriter.store(self, s)
 
+        saved = dict(ctx.ranges)
+        for l in nest.loops:  # the loop vars' ranges let the bounds prover drop guards
+            mn, ext = as_int(l.min), as_int(l.extent)
+            if mn is not None and ext is not None and ext > 0:
+                ctx.ranges[l.var] = (mn, mn + ext - 1)
         body = _Cpu(ctx, {}).stmt(nest.body)
+        ctx.ranges.clear()
+        ctx.ranges.update(saved)
         for l in reversed(nest.loops):
             body = S.ForStmt(l.var, l.min, l.extent, "serial", body)
         return body
@@ -1245,6 +1355,8 @@ class TileOpLowerer(Mutator):
     def lower_ReduceOp(self, op: O.ReduceOp):
         ctx = self.ctx
         sb, db = op.src.buffer, op.dst.buffer
+        if ctx.is_cpu:
+            return self.lower_reduce_cpu(op)
         if sb.scope != "fragment" or db.scope != "fragment":
             return self.lower_reduce_simt(op)
         S_lay: Fragment = sb.layout
@@ -1357,6 +1469,46 @@ class TileOpLowerer(Mutator):
             groups.setdefault(li, []).append(r)
         return groups
 
+    def lower_reduce_cpu(self, op: O.ReduceOp):
+        """CPU target: one thread owns every element (fragments are row-major local arrays), so a
+        reduction is a loop nest -- not the GPU path's unrolled per-register combine tree, whose
+        65k-term expressions host clang cannot digest for a 256x256 tile."""
+        ctx = self.ctx
+        src, dst = op.src, op.dst
+        sext = src.static_extents()
+        if sext is None:
+            raise LoweringError("reduce needs static extents")
+        dim = op.dim
+        outer = [e for d, e in enumerate(sext) if d != dim]
+        ovars = [Var(f"ro{i}") for i in range(len(outer))]
+        k = Var("rk")
+        sidx = list(ovars)
+        sidx.insert(dim, k)
+        sidx = [binop("+", m, i) for m, i in zip(src.mins, sidx)]
+        didx = list(ovars)
+        if len(dst.region) == len(src.region):
+            didx.insert(dim, IntImm(0))
+        didx = [binop("+", m, i) for m, i in zip(dst.mins, didx)]
+        dt = src.buffer.dtype
+        accb = ctx.new_local(f"racc{ctx.ws_counter}", 1, dt)
+        ctx.ws_counter += 1
+        x = BufferLoad(src.buffer, sidx)
+        if op.reduce_type in ("abssum", "absmax"):
+            x = call("abs", [x], dt)
+        res = BufferLoad(accb, [IntImm(0)])
+        if not op.clear:
+            res = _combine(op.reduce_type, BufferLoad(dst.buffer, didx), res)
+        body = S.SeqStmt([
+            S.StoreStmt(accb, [IntImm(0)], _reduce_init(op.reduce_type, dt)),
+            S.ForStmt(k, 0, sext[dim], "serial",
+                      S.StoreStmt(accb, [IntImm(0)], _combine(op.reduce_type, BufferLoad(accb, [IntImm(0)]), x))),
+            S.StoreStmt(dst.buffer, didx, cast(res, dst.buffer.dtype))])
+        if not ovars:
+            ovars, outer = [Var("ro0")], [1]
+        for v, e in reversed(list(zip(ovars, outer))):
+            body = S.ForStmt(v, 0, e, "parallel", body)
+        return self.lower_cpu_nest(ParallelNest(_nest_loops(body)))
+
     def lower_reduce_simt(self, op: O.ReduceOp):
         """Reduction over shared/local buffers: each thread reduces whole rows serially."""
         ctx = self.ctx
@@ -1404,8 +1556,11 @@ class TileOpLowerer(Mutator):
         """Inclusive scan along ``dim`` for shared/global buffers (one thread per row)."""
         ctx = self.ctx
         src, dst = op.src, op.dst
-        if src.buffer.scope == "fragment" or dst.buffer.scope == "fragment":
-            raise LoweringError("T.cumsum on fragments is not supported yet; stage through shared memory")
+        frag = src.buffer.scope == "fragment" or dst.buffer.scope == "fragment"
+        if frag and ctx.is_cpu:
+            return self.lower_cumsum_cpu(op)
+        if frag:
+            return self.lower_cumsum_fragment(op)
         sext = src.static_extents()
         dim = op.dim
         outer = [e for d, e in enumerate(sext) if d != dim]
@@ -1434,6 +1589,106 @@ class TileOpLowerer(Mutator):
             blk = self.stmt(S.SeqStmt(body))
             out.append(S.IfStmt(binop("<", slot, n_out), blk) if (o + 1) * ctx.T > n_out else blk)
         out.append(L.CallStmt("tl::sync_threads", []))
+        return S.SeqStmt(out)
+
+    def lower_cumsum_cpu(self, op: O.CumSumOp):
+        """CPU target: fragments are row-major local arrays of the one thread -- a serial scan
+        per row, as a loop nest over the other dims."""
+        src, dst = op.src, op.dst
+        sext = src.static_extents()
+        dim = op.dim
+        outer = [e for d, e in enumerate(sext) if d != dim]
+        ovars = [Var(f"co{i}") for i in range(len(outer))]
+        n = sext[dim]
+        k = Var("ck")
+        kk = binop("-", n - 1, k) if op.reverse else k
+        idx = list(ovars)
+        idx.insert(dim, kk)
+        sidx = [binop("+", m, i) for m, i in zip(src.mins, idx)]
+        didx = [binop("+", m, i) for m, i in zip(dst.mins, idx)]
+        dt = dst.buffer.dtype
+        accb = self.ctx.new_local(f"cacc{self.ctx.ws_counter}", 1, dt)
+        self.ctx.ws_counter += 1
+        body = S.SeqStmt([
+            S.StoreStmt(accb, [IntImm(0)], const(0, dt)),
+            S.ForStmt(k, 0, n, "serial", S.SeqStmt([
+                S.StoreStmt(accb, [IntImm(0)], BufferLoad(accb, [IntImm(0)]) + cast(BufferLoad(src.buffer, sidx), dt)),
+                S.StoreStmt(dst.buffer, didx, BufferLoad(accb, [IntImm(0)]))]))])
+        if not ovars:
+            ovars, outer = [Var("co0")], [1]
+        for v, e in reversed(list(zip(ovars, outer))):
+            body = S.ForStmt(v, 0, e, "parallel", body)
+        return self.lower_cpu_nest(ParallelNest(_nest_loops(body)))
+
+    def lower_cumsum_fragment(self, op: O.CumSumOp):
+        """``T.cumsum`` of a register fragment (reference ``src/op/reduce.cc:496-560``): the
+        fragment goes to an LDS workspace through its layout, one thread per row scans it there,
+        and the result comes back through the destination's layout.  A scan crosses the lanes
+        that own a row; staging once through LDS costs two barriers and no shuffles."""
+        ctx = self.ctx
+        src, dst = op.src, op.dst
+        for r in (src, dst):
+            if r.buffer.scope == "fragment" and not _full(r):
+                raise LoweringError("T.cumsum on a fragment must cover the whole fragment")
+        sext = src.static_extents()
+        if sext is None:
+            raise LoweringError("T.cumsum needs static extents")
+        dt = dst.buffer.dtype
+        n_all = _prod(sext)
+        ws = ctx.new_workspace(n_all, dt)
+
+        def to_ws(r: BufferRegion):
+            b = r.buffer
+            if b.scope == "fragment":
+                lay, lb = b.layout, ctx.local_of(b)
+                return [S.StoreStmt(ws, [_row_major(lay.inverse(ctx.tid, i), sext)], cast(BufferLoad(lb, [IntImm(i)]),
+                                                                                            dt))
+                        for i in range(lay.local_size)]
+            vars_ = [Var(f"cw{i}") for i in range(len(sext))]
+            body = S.StoreStmt(ws, [_row_major(vars_, sext)],
+                               cast(BufferLoad(b, [binop("+", m, v) for m, v in zip(r.mins, vars_)]), dt))
+            for v, e in reversed(list(zip(vars_, sext))):
+                body = S.ForStmt(v, 0, e, "parallel", body)
+            return [self.lower_nest(body)]
+
+        def from_ws(r: BufferRegion):
+            b = r.buffer
+            if b.scope == "fragment":
+                lay, lb = b.layout, ctx.local_of(b)
+                return [S.StoreStmt(lb, [IntImm(i)], cast(BufferLoad(ws, [_row_major(lay.inverse(ctx.tid, i), sext)]),
+                                                          b.dtype))
+                        for i in range(lay.local_size)]
+            vars_ = [Var(f"cr{i}") for i in range(len(sext))]
+            body = S.StoreStmt(b, [binop("+", m, v) for m, v in zip(r.mins, vars_)],
+                               cast(BufferLoad(ws, [_row_major(vars_, sext)]), b.dtype))
+            for v, e in reversed(list(zip(vars_, sext))):
+                body = S.ForStmt(v, 0, e, "parallel", body)
+            return [self.lower_nest(body)]
+
+        out = to_ws(src)
+        out.append(L.CallStmt("tl::sync_threads", []))
+        dim = op.dim
+        outer = [e for d, e in enumerate(sext) if d != dim]
+        n_out = _prod(outer)
+        n = sext[dim]
+        steps = -(-n_out // ctx.T)
+        for o in range(steps):
+            slot = binop("+", o * ctx.T, ctx.tid)
+            oidx = _unflatten(slot, outer)
+            k = Var("ck")
+            kk = binop("-", n - 1, k) if op.reverse else k
+            idx = list(oidx)
+            idx.insert(dim, kk)
+            flat = _row_major(idx, sext)
+            accb = ctx.new_local(f"cacc{ctx.ws_counter}", 1, dt)
+            ctx.ws_counter += 1
+            blk = S.SeqStmt([S.StoreStmt(accb, [IntImm(0)], const(0, dt)),
+                             S.ForStmt(k, 0, n, "serial", S.SeqStmt([
+                                 S.StoreStmt(accb, [IntImm(0)], BufferLoad(accb, [IntImm(0)]) + BufferLoad(ws, [flat])),
+                                 S.StoreStmt(ws, [flat], BufferLoad(accb, [IntImm(0)]))]))])
+            out.append(S.IfStmt(binop("<", slot, n_out), blk) if (o + 1) * ctx.T > n_out else blk)
+        out.append(L.CallStmt("tl::sync_threads", []))
+        out.extend(from_ws(dst))
         return S.SeqStmt(out)
 
     def lower_AtomicOp(self, op: O.AtomicOp):
@@ -1915,7 +2170,7 @@ class _SimtRewriter(Mutator):
                 raise LoweringError(f"fragment {b.name} in a non-fragment T.Parallel nest")
             ld = BufferLoad(self.ctx.flat_of(b), [self.ctx.flat_index(b, idx)])
             g = safe_guard(self.ctx, b, idx)
-            return select(g, ld, const(0, b.dtype)) if g is not None else ld
+            return select(g, ld, _safe_value(b)) if g is not None else ld
         if isinstance(n, Call):
             return _hoist_atomic_guard(n)
         return None
