@@ -49,13 +49,17 @@ def mla_decode(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, bl
 
             T.copy(Q[bx, by * VALID_BLOCK_H:(by + 1) * VALID_BLOCK_H, :], Q_local)
             T.copy(Q_pe[bx, by * VALID_BLOCK_H:(by + 1) * VALID_BLOCK_H, :], Q_pe_local)
-            any_s = T.alloc_shared([1], "int32")
+            any_s = T.alloc_shared([2], "int32")
             T.fill(acc_o, 0)
             T.fill(logsum, 0)
             # wide: lazy rescale (a row keeps its max until a score beats it by 2^8, P <= 256), so
             # the D-split O accumulator is rescaled only on tiles where some row moved (flag in LDS)
             T.fill(scores_max, -(2.0**30) if wide else -T.infinity(accum_dtype))
 
+            # lazy-rescale flag, double-buffered by iteration parity: iteration t resets the slot
+            # of t + 1 (ordered by the stage barrier against t - 1's readers and t + 1's setters)
+            for z in T.Parallel(2):
+                any_s[z] = 0
             for k in T.Pipelined(T.ceildiv(split_len, block_N), num_stages=num_stages):
                 kv_start = split_len * bz + k * block_N
                 T.copy(KV[bx, kv_start:kv_start + block_N, 0, :], KV_shared)
@@ -65,14 +69,14 @@ def mla_decode(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, bl
                 T.gemm(Q_pe_local, K_pe_shared, acc_s, transpose_B=True, policy=s_policy)
                 if wide:
                     for z in T.Parallel(1):  # previous tile's readers are past the stage barrier
-                        any_s[z] = 0
+                        any_s[z + (k + 1) % 2] = 0
                     T.copy(scores_max, scores_max_prev)
                     T.reduce_max(acc_s, scores_max_prev, dim=1, clear=False)  # candidate max
                     for i in T.Parallel(block_H):
                         if (scores_max_prev[i] - scores_max[i]) * scale > 8.0:
                             scores_scale[i] = T.exp2((scores_max[i] - scores_max_prev[i]) * scale)
                             scores_max[i] = scores_max_prev[i]
-                            any_s[0] = 1
+                            any_s[k % 2] = 1
                         else:
                             scores_scale[i] = 1.0
                 else:
@@ -88,7 +92,7 @@ def mla_decode(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, bl
                 if wide:
                     T.copy(scores_scale, sc_shared)
                     T.copy(acc_s, P_shared)
-                    if any_s[0] != 0:
+                    if any_s[k % 2] != 0:
                         for i, j in T.Parallel(block_H, dim):
                             acc_o[i, j] *= sc_shared[i]
                     T.gemm(P_shared, KV_shared, acc_o)

@@ -49,7 +49,7 @@ def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe
             acc_s_cast = T.alloc_fragment([block_H, block_N], dtype)
             P_shared = T.alloc_shared([block_H, block_N], dtype)
             sc_shared = T.alloc_shared([block_H], accum_dtype)
-            any_s = T.alloc_shared([1], "int32")
+            any_s = T.alloc_shared([2], "int32")
             acc_o = T.alloc_fragment([block_H, dim], accum_dtype)
             m = T.alloc_fragment([block_H], accum_dtype)
             m_prev = T.alloc_fragment([block_H], accum_dtype)
@@ -67,6 +67,10 @@ def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe
             T.fill(acc_o, 0)
             T.fill(l_sum, 0)
             T.fill(m, -(2.0**30))
+            # lazy-rescale flag, double-buffered by iteration parity: iteration t resets the slot
+            # of t + 1 (ordered by the stage barrier against t - 1's readers and t + 1's setters)
+            for z in T.Parallel(2):
+                any_s[z] = 0
             for t in T.Pipelined(t_begin, t_end, num_stages=num_stages):
                 tok = t * block_N
                 page = BlockTable[bx, tok // page_size]
@@ -79,14 +83,14 @@ def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe
                 T.gemm(Q_pe_local, K_pe_shared, acc_s, transpose_B=True, policy=s_policy)
                 if wide:  # lazy rescale + block-uniform skip flag (example_mla_decode.py)
                     for z in T.Parallel(1):
-                        any_s[z] = 0
+                        any_s[z + (t + 1) % 2] = 0
                     T.copy(m, m_prev)
                     T.reduce_max(acc_s, m_prev, dim=1, clear=False)  # candidate max
                     for i in T.Parallel(block_H):
                         if (m_prev[i] - m[i]) * scale > 8.0:
                             alpha[i] = T.exp2((m[i] - m_prev[i]) * scale)
                             m[i] = m_prev[i]
-                            any_s[0] = 1
+                            any_s[t % 2] = 1
                         else:
                             alpha[i] = 1.0
                 else:
@@ -102,7 +106,7 @@ def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe
                 if wide:
                     T.copy(alpha, sc_shared)
                     T.copy(acc_s, P_shared)
-                    if any_s[0] != 0:
+                    if any_s[t % 2] != 0:
                         for i, j in T.Parallel(block_H, dim):
                             acc_o[i, j] *= sc_shared[i]
                     T.gemm(P_shared, KV_shared, acc_o)

@@ -49,7 +49,7 @@ def mla_decode_persistent(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, blo
             acc_s = T.alloc_fragment([block_H, block_N], accum_dtype)
             P_shared = T.alloc_shared([block_H, block_N], dtype)
             sc_shared = T.alloc_shared([block_H], accum_dtype)
-            any_s = T.alloc_shared([1], "int32")
+            any_s = T.alloc_shared([2], "int32")
             acc_o = T.alloc_fragment([block_H, dim], accum_dtype)
             scores_max = T.alloc_fragment([block_H], accum_dtype)
             scores_max_prev = T.alloc_fragment([block_H], accum_dtype)
@@ -73,6 +73,10 @@ def mla_decode_persistent(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, blo
                     T.fill(acc_o, 0)
                     T.fill(logsum, 0)
                     T.fill(scores_max, -(2.0**30))  # lazy rescale (example_mla_decode.py)
+                    # lazy-rescale flag, double-buffered by iteration parity: iteration t resets the slot
+                    # of t + 1 (ordered by the stage barrier against t - 1's readers and t + 1's setters)
+                    for z in T.Parallel(2):
+                        any_s[z] = 0
                     for k in T.Pipelined(T.ceildiv(split_len, block_N), num_stages=num_stages):
                         kv_start = split_len * sid + k * block_N
                         T.copy(KV[bid, kv_start:kv_start + block_N, 0, :], KV_shared)
@@ -81,14 +85,14 @@ def mla_decode_persistent(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, blo
                         T.gemm(Q_local, KV_shared, acc_s, transpose_B=True)
                         T.gemm(Q_pe_local, K_pe_shared, acc_s, transpose_B=True)
                         for z in T.Parallel(1):  # previous tile's readers are past the stage barrier
-                            any_s[z] = 0
+                            any_s[z + (k + 1) % 2] = 0
                         T.copy(scores_max, scores_max_prev)
                         T.reduce_max(acc_s, scores_max_prev, dim=1, clear=False)  # candidate max
                         for i in T.Parallel(block_H):
                             if (scores_max_prev[i] - scores_max[i]) * scale > 8.0:
                                 scores_scale[i] = T.exp2((scores_max[i] - scores_max_prev[i]) * scale)
                                 scores_max[i] = scores_max_prev[i]
-                                any_s[0] = 1
+                                any_s[k % 2] = 1
                             else:
                                 scores_scale[i] = 1.0
                         for i, j in T.Parallel(block_H, block_N):
@@ -98,7 +102,7 @@ def mla_decode_persistent(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, blo
                             logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
                         T.copy(scores_scale, sc_shared)
                         T.copy(acc_s, P_shared)
-                        if any_s[0] != 0:
+                        if any_s[k % 2] != 0:
                             for i, j in T.Parallel(block_H, dim):
                                 acc_o[i, j] *= sc_shared[i]
                         T.gemm(P_shared, KV_shared, acc_o)

@@ -285,10 +285,21 @@ def inverse_index(indices, SKV, pad):
 _KERNELS = {}
 
 
-def sparse_mla_bwd(q, kv, o, do, indices, lse, sm_scale=None, target=None, dkv="gather"):
+GATHER_BUDGET_BYTES = 4 << 30
+
+
+def sparse_mla_bwd(q, kv, o, do, indices, lse, sm_scale=None, target=None, dkv="gather",
+                   gather_budget_bytes=GATHER_BUDGET_BYTES):
     """(dQ, dKV fp32) for the sparse MLA forward (tilelang.ops.dsa.sparse_mla_fwd).
     ``dkv``: "gather" (bf16 partial rows + sorted-index reduction, deterministic) or "atomic"
-    (fp32 atomic scatter)."""
+    (fp32 atomic scatter).
+
+    The gather path holds one bf16 partial row per (token, slot): B*S*topk*576*2 bytes (4.8 GB
+    at S=4096, topk=2048) plus a sort of B*S*topk keys.  Past ``gather_budget_bytes`` it falls
+    back to the atomic path, whose footprint is the O(SKV*576) fp32 dKV alone.  Numerics: each
+    partial row is rounded to bf16 before the fp32 sum (the atomic path adds fp32 partials), an
+    extra ~2^-9 relative error per partial that averages out over the rows a KV row collects;
+    tests/test_examples_cpu.py and test_gpu_examples_misc.py check both paths against fp32."""
     import torch
     B, S, H, DQK = q.shape
     SKV = kv.shape[1]
@@ -307,6 +318,8 @@ def sparse_mla_bwd(q, kv, o, do, indices, lse, sm_scale=None, target=None, dkv="
     delta = k_(sparse_mla_bwd_preprocess, B, S, H, D, dtype=_dt(q))(o, do)
     dq, p, ds = k_(sparse_mla_bwd_dq, B, S, SKV, H, D, DT, topk, sm_scale, dtype=_dt(q))(q, kv, do, indices, lse,
                                                                                       delta)
+    if dkv == "gather" and B * S * topk * DQK * q.element_size() > gather_budget_bytes:
+        dkv = "atomic"
     if dkv == "atomic":
         dkv_ = torch.zeros(B, SKV, 1, DQK, dtype=torch.float32, device=q.device)
         k_(sparse_mla_bwd_dkv, B, S, SKV, H, D, DT, topk, dtype=_dt(q))(q, do, indices, p, ds, dkv_)

@@ -19,10 +19,10 @@ import tilelang
 import tilelang.language as T
 from tilelang.layout import PaddedLayout
 
-from example_mha_fwd import FAST_MATH, ref_program
+from example_mha_fwd import FAST_MATH_NO_NANS, ref_program
 
 
-@tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
+@tilelang.jit(out_idx=[3], pass_configs=FAST_MATH_NO_NANS)
 def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=256, block_N=64,
                         threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
                         young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd", mfma="16x16",

@@ -463,6 +463,9 @@ def test_sparse_mla_bwd_cpu():
     torch.testing.assert_close(dkv, rkv, rtol=2e-2, atol=2e-2)
     da = m.sparse_mla_bwd(q, kv, o, do, idx, lse, dkv="atomic")[1]
     torch.testing.assert_close(da, rkv, rtol=2e-2, atol=2e-2)
+    # past the memory budget the gather path falls back to the atomic one (same fp32 result)
+    db = m.sparse_mla_bwd(q, kv, o, do, idx, lse, gather_budget_bytes=0)[1]
+    torch.testing.assert_close(db, da, rtol=0, atol=0)
     order, offs = m.inverse_index(idx, SKV, 32)
     assert int(offs[-1]) == B * S * topk and order.numel() == B * S * topk + 32
     for impl, args in ((m.sparse_mla_bwd_dq, (1, 64, 256, 64, 512, 64, 128)),

@@ -1046,3 +1046,46 @@ def test_device_assert():
     ref = A * 2
     k(A)
     torch.testing.assert_close(A, ref)
+
+
+# ---- cross-wave reductions without ThreadSync (tl.disable_thread_storage_sync) ------------
+
+
+def softmax_rows_program(M, N):
+    """Row max then row sum of exp over rows that span all 4 waves: two cross-wave exchanges
+    through the reduction workspace back to back."""
+
+    @T.prim_func
+    def main(A: T.Tensor((M, N), "float32"), B: T.Tensor((M, N), "float32")):
+        with T.Kernel(1, threads=256):
+            S_ = T.alloc_fragment((M, N), "float32")
+            mx = T.alloc_fragment((M, ), "float32")
+            sm = T.alloc_fragment((M, ), "float32")
+            T.copy(A, S_)
+            T.reduce_max(S_, mx, dim=1)
+            for i, j in T.Parallel(M, N):
+                S_[i, j] = T.exp(S_[i, j] - mx[i])
+            T.reduce_sum(S_, sm, dim=1)
+            for i, j in T.Parallel(M, N):
+                S_[i, j] = S_[i, j] / sm[i]
+            T.copy(S_, B)
+
+    return main
+
+
+def test_reduction_barriers_without_thread_sync():
+    cfg = {"tl.disable_thread_storage_sync": True}
+    with_ts = tilelang.lower(softmax_rows_program(4, 1024), target="hip").kernel_source
+    without = tilelang.lower(softmax_rows_program(4, 1024), target="hip", pass_configs=cfg).kernel_source
+    # the reductions keep their leading / trailing barriers themselves when ThreadSync is off
+    assert without.count("__syncthreads()") >= with_ts.count("__syncthreads()")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [{}, {"tl.disable_thread_storage_sync": True}])
+def test_reduction_barriers_without_thread_sync_gpu(cfg):
+    k = tilelang.compile(softmax_rows_program(4, 1024), target="hip", pass_configs=cfg)
+    A = torch.randn(4, 1024, device="cuda")
+    B = torch.zeros_like(A)
+    k(A, B)
+    torch.testing.assert_close(B, torch.softmax(A, 1), rtol=1e-4, atol=1e-6)

@@ -98,3 +98,32 @@ def test_fa_staged_gpu(causal, mfma, sum_mfma):
     v = torch.randn_like(kk)
     torch.testing.assert_close(k(q, kk, v).float(), ref_program(q, kk, v, causal, 2).float(), rtol=2e-2,
                                atol=2e-2)
+
+
+def alt_chain(cond_fn, n=4):
+    """Two compute orders selected per wave by ``alt_cond`` (T.Pipelined(order_alt=, alt_cond=))."""
+
+    @T.prim_func
+    def main(A: T.Tensor((n, 128), "float32"), O: T.Tensor((128, ), "float32")):
+        with T.Kernel(1, threads=128):
+            acc = T.alloc_fragment((128, ), "float32")
+            tmp = T.alloc_fragment((128, ), "float32")
+            T.clear(acc)
+            for k in T.Pipelined(n, num_stages=2, order=[1, 0], stage=[0, 1], order_alt=[1, 0],
+                                 alt_cond=cond_fn()):
+                for i in T.Parallel(128):
+                    tmp[i] = A[k, i] + 1.0
+                for i in T.Parallel(128):
+                    acc[i] = acc[i] * 2.0 + tmp[i]
+            T.copy(acc, O)
+
+    return main
+
+
+def test_alt_cond_must_be_wave_uniform():
+    # wave-constant: one scalar branch per wave (readfirstlane) is exact
+    src = tilelang.lower(alt_chain(lambda: T.get_thread_binding() >= 64), target="hip").kernel_source
+    assert "__builtin_amdgcn_readfirstlane" in src
+    # lane-varying: readfirstlane would silently give every lane lane 0's choice -> refused
+    with pytest.raises(Exception, match="same for every lane"):
+        tilelang.lower(alt_chain(lambda: T.get_thread_binding() % 2 == 0), target="hip")

@@ -277,6 +277,10 @@ class CodeGen:
             return f"tl::sync_grid({ws}, {err})"
         if op == "tl.unswitch":
             c = self.e(args[0])
+            if not self.is_cpu and not self._uniform_cond(args[0]):
+                raise CodeGenError(f"T.Pipelined(alt_cond={args[0]}): the condition must be the same for every lane "
+                                   "of a wave (block indices, scalar parameters, the wave index or a thread "
+                                   "expression constant over each wave); it becomes one scalar branch")
             return f"({c})" if self.is_cpu else f"__builtin_amdgcn_readfirstlane((int)({c}))"
         if op == "tl.setprio":
             return "(void)0" if self.is_cpu else f"__builtin_amdgcn_s_setprio({int(args[0].value)})"
@@ -595,6 +599,24 @@ class CodeGen:
             out.append("}")
         ks.source = "\n".join(out) + "\n"
         return ks
+
+    def _uniform_cond(self, cond) -> bool:
+        """True if ``cond`` provably takes one value per wave: it depends only on block indices,
+        scalar kernel parameters and the wave index, plus thread indices in a wave-constant way
+        (checked by evaluation).  Loop variables and let-bound values are rejected: a register
+        value need not be uniform."""
+        from ..ir.expr import free_vars, substitute, IntImm
+        k = self.kernel
+        uniform = set(map(id, k.block_vars))
+        uniform |= {id(p) for p in getattr(self.func, "params", []) if isinstance(p, Var)}
+        if k.attrs.get("wave") is not None:
+            uniform.add(id(k.attrs["wave"]))
+        fv = free_vars(cond)
+        rest = [v for v in fv if id(v) not in uniform]
+        if not rest:
+            return True
+        sub = substitute(cond, {v: IntImm(0) for v in fv if id(v) in uniform})
+        return self._wave_uniform(sub)
 
     def _wave_uniform(self, cond) -> bool:
         """True if ``cond`` depends on thread indices only and takes one value per wave64 (checked

@@ -92,10 +92,11 @@ class Buffer:
         off = convert(self.offset) if not isinstance(self.offset, int) or self.offset else const(0)
         if wide:
             off = cast(off, _dt.int64)
+        from .expr import widen_int64
         for i, s in zip(indices, strides):
             t = convert(i)
             if wide and t.dtype.bits < 64:
-                t = cast(t, _dt.int64)
+                t = widen_int64(t)
             off = off + t * s
         return off
 

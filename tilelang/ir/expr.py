@@ -752,6 +752,22 @@ def transform(e, fn):
     return n if r is None else r
 
 
+def widen_int64(e):
+    """``e`` re-evaluated in int64 from the leaves up.  Casting an int32 result to int64 keeps
+    its overflow (``(int64_t)(bx * 512 + t)`` past 2^31); widening the leaves does not."""
+    e = convert(e)
+    if not e.dtype.is_int or e.dtype.bits >= 64:
+        return e
+
+    def fn(n):
+        if isinstance(n, (Var, BufferLoad, Call, Cast)) and n.dtype.is_int and n.dtype.bits < 64:
+            return Cast(_dt.int64, n)
+        return None
+
+    r = transform(e, fn)
+    return r if r.dtype.bits >= 64 else cast(r, _dt.int64)
+
+
 def structural_equal(a, b) -> bool:
     if a is b:
         return True

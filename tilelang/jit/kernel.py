@@ -122,9 +122,9 @@ class JITKernel:
     def hip_flags(self) -> List[str]:
         """hipcc flags of this kernel's gfx950 compile: the user's plus what the pass configs imply."""
         flags = list(self.compile_flags)
-        if self.pass_configs.get("tl.enable_fast_math") and not self.pass_configs.get("tl.disable_fast_math"):
-            # fast math promises no NaN inputs: fmaxf on MFMA results then needs no canonicalising
-            # v_max_f32 x, x per operand (the softmax row max of every attention kernel)
+        if self.pass_configs.get("tl.no_nans"):
+            # the kernel promises no NaN values: fmaxf on MFMA results then needs no canonicalising
+            # v_max_f32 x, x per operand (the softmax row max of the attention kernels that set it)
             flags.append("-fno-honor-nans")
         return flags
 

@@ -78,7 +78,7 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
             acc_s_cast = T.alloc_fragment([H_blk, block_I], dtype)
             P_shared = T.alloc_shared([H_blk, block_I], dtype)
             alpha_s = T.alloc_shared([H_blk], accum_dtype)
-            any_s = T.alloc_shared([1], "int32")  # wide: some row of this tile moved its max
+            any_s = T.alloc_shared([2], "int32")  # wide: some row of this tile moved its max
             acc_o = T.alloc_fragment([H_blk, D], accum_dtype)
             o_cast = T.alloc_fragment([H_blk, D], dtype)
             m_cur = T.alloc_fragment([H_blk], accum_dtype)
@@ -94,6 +94,10 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
             T.fill(acc_o, 0)
             T.fill(l_sum, 0)
             T.fill(m_cur, -(2.0**30))
+            # lazy-rescale flag, double-buffered by iteration parity: iteration t resets the slot
+            # of t + 1 (ordered by the stage barrier against t - 1's readers and t + 1's setters)
+            for z in T.Parallel(2):
+                any_s[z] = 0
             for i in T.Pipelined(NI, num_stages=num_stages):
                 # selected latent rows; indices outside the cache read zeros, causal ones are masked
                 T.gather_rows(KV[b, :, g, 0:D], Indices[b, bx, g, i * block_I:(i + 1) * block_I], KV_shared)
@@ -106,7 +110,7 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
                 T.gemm(Qt_frag, Kt_shared, acc_s, transpose_B=True, policy=s_policy)
                 if wide:
                     for z in T.Parallel(1):  # previous tile's readers are past the stage barrier
-                        any_s[z] = 0
+                        any_s[z + (i + 1) % 2] = 0
                 T.copy(m_cur, m_prev)
                 T.reduce_max(acc_s, m_prev, dim=1, clear=False)
                 # lazy rescale: a row keeps its running max until a new score exceeds it by
@@ -120,7 +124,7 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
                         m_cur[h] = m_prev[h]
                         rescale = 1
                         if wide:
-                            any_s[0] = 1
+                            any_s[i % 2] = 1
                     else:
                         alpha[h] = 1.0
                 for h, r in T.Parallel(H_blk, block_I):
@@ -134,7 +138,7 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
                     T.copy(acc_s, P_shared)
                     # lazy rescale across the D-split waves: skipped (block-uniform flag) on the
                     # tiles where no row moved its max -- most of them after the first few
-                    if any_s[0] != 0:
+                    if any_s[i % 2] != 0:
                         for h, d in T.Parallel(H_blk, D):
                             acc_o[h, d] *= alpha_s[h]
                     T.gemm(P_shared, KV_shared, acc_o)

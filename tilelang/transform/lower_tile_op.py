@@ -135,6 +135,10 @@ class LowerCtx:
         # tl.dynamic_alignment: dynamic extents are multiples of this (enables vector accesses)
         self.dynamic_alignment = int(self.pass_cfg.get("tl.dynamic_alignment", 0) or 0)
         self.uses_grid_sync = False
+        self.thread_range = None  # (lo, hi): inside ``if lo <= tx < hi`` (thread-range partitioning)
+        # ThreadSync is off (tl.disable_thread_storage_sync): the workspace exchanges this pass
+        # emits carry their own leading / trailing barriers instead of relying on it
+        self.self_sync = bool(self.pass_cfg.get("tl.disable_thread_storage_sync", False))
         self.dynamic_vars = set()
         if self.dynamic_alignment > 1:
             from .pipeline import _referenced_buffers
@@ -238,6 +242,8 @@ class LowerCtx:
         n = b.static_numel()
         if bits != 32 and n is not None and n >= (1 << 31):
             return True
+        if bits != 32 and any(isinstance(d, PrimExpr) and d.dtype.is_int and d.dtype.bits >= 64 for d in b.shape):
+            return True  # an int64 symbolic extent (T.symbolic("n", "int64")): sized past 2^31
         if bits == 32 and n is not None and n >= (1 << 31):
             raise LoweringError(f"{b.name} has {n} elements but tl.config_index_bitwidth=32")
         self.narrow_index.add(b)
@@ -513,6 +519,9 @@ def safe_guard(ctx: LowerCtx, b: Buffer, idx) -> Optional[PrimExpr]:
     if b.scope != "global" or ctx.pass_cfg.get("tl.disable_safe_memory_legalize") or getattr(b, "no_guard", False):
         return None
     idx = ctx.legal_index(b, idx)
+    if ctx.wide_index(b):
+        from ..ir.expr import widen_int64
+        idx = [widen_int64(i) for i in idx]
     cond = None
     for i, s in zip(idx, b.shape):
         bd = bound(i, ctx.ranges)
@@ -820,6 +829,62 @@ class TileOpLowerer(Mutator):
         kind = s.kind if s.kind in ("serial", "unroll") else "serial"
         return S.ForStmt(s.var, self.expr(s.min), self.expr(s.extent), kind, body, s.annotations)
 
+    def visit_IfStmt(self, s):
+        rng = self._thread_range(s.cond)
+        then = None
+        if rng is not None:
+            saved, saved_r = self.ctx.thread_range, self.ctx.ranges.get(self.ctx.tid)
+            self.ctx.thread_range = rng
+            self.ctx.ranges[self.ctx.tid] = (rng[0], rng[1] - 1)
+            then = self.stmt(s.then_body)
+            self.ctx.thread_range = saved
+            self.ctx.ranges[self.ctx.tid] = saved_r
+        else:
+            then = self.stmt(s.then_body)
+        return S.IfStmt(self.expr(s.cond), then, self.stmt(s.else_body) if s.else_body is not None else None)
+
+    def _thread_range(self, cond):
+        """``[lo, hi)`` when ``cond`` is a conjunction of comparisons of the (1-D) thread index
+        with constants (``tx < 128``, ``tx >= 128 and tx < 256``) that narrows the block --
+        tile ops under it are partitioned over those threads (the reference's thread-range
+        aware layout inference, testing/python/language/test_tilelang_language_mask_op.py)."""
+        from ..ir.expr import BinOp as _B
+        k = self.ctx.kernel
+        tvars = {self.ctx.tid}
+        if len(k.threads) == 1:
+            tvars |= set(k.thread_vars)
+            if k.attrs.get("tid") is not None:
+                tvars.add(k.attrs["tid"])
+        lo, hi = 0, self.ctx.T
+        stack = [cond]
+        flip = {"<": ">", "<=": ">=", ">": "<", ">=": "<="}
+        while stack:
+            c = stack.pop()
+            if not isinstance(c, _B):
+                return None
+            if c.op == "&&":
+                stack += [c.a, c.b]
+                continue
+            if c.op not in flip:
+                return None
+            op, a, b = c.op, c.a, c.b
+            if a not in tvars:
+                op, a, b = flip[op], b, a
+            if a not in tvars or as_int(b) is None:
+                return None
+            v = as_int(b)
+            if op == "<":
+                hi = min(hi, v)
+            elif op == "<=":
+                hi = min(hi, v + 1)
+            elif op == ">":
+                lo = max(lo, v + 1)
+            else:
+                lo = max(lo, v)
+        if not (0 <= lo < hi <= self.ctx.T) or (lo, hi) == (0, self.ctx.T):
+            return None
+        return lo, hi
+
     def lower_vectorized(self, s: S.ForStmt):
         """``T.vectorized(n)`` over one store: chunks of W consecutive iterations become one
         vector access when every access is contiguous in the loop variable and W-aligned (the
@@ -964,7 +1029,11 @@ class TileOpLowerer(Mutator):
         if any(e is None for e in exts):
             return self.lower_dynamic_nest(nest)
         total = _prod(exts)
-        T = ctx.T
+        T, tid = ctx.T, ctx.tid
+        if ctx.thread_range is not None:
+            # under ``if lo <= tx < hi``: the nest is partitioned over those hi - lo threads only
+            lo, hi = ctx.thread_range
+            T, tid = hi - lo, (binop("-", ctx.tid, lo) if lo else ctx.tid)
         inner_var = nest.vars[-1]
         # vector width: contiguous along the innermost loop var for every access
         vec = 1
@@ -984,15 +1053,16 @@ class TileOpLowerer(Mutator):
         out = []
         single_store = isinstance(nest.body, S.StoreStmt)
         for o in range(steps):
-            slot = binop("+", binop("*", o, T), ctx.tid) if steps > 1 else ctx.tid
+            slot = binop("+", binop("*", o, T), tid) if steps > 1 else tid
             guard = None
             if (o + 1) * T > slots:
                 guard = binop("<", slot, slots)
             # inside the tail guard only threads tid < slots - o*T run: tighten tid's range so the
             # bounds prover can drop per-element guards that only the idle threads would fail
             saved = ctx.ranges.get(ctx.tid)
-            if guard is not None and saved is not None and slots - o * T - 1 < saved[1]:
-                ctx.ranges[ctx.tid] = (saved[0], slots - o * T - 1)
+            lo = ctx.thread_range[0] if ctx.thread_range is not None else 0
+            if guard is not None and saved is not None and lo + slots - o * T - 1 < saved[1]:
+                ctx.ranges[ctx.tid] = (saved[0], lo + slots - o * T - 1)
             group = []
             for v in range(vec):
                 lin = binop("+", binop("*", slot, vec), v) if vec > 1 else slot
@@ -1418,6 +1488,8 @@ class TileOpLowerer(Mutator):
             # workspace) and after the loads are left to ThreadSync, which places them only
             # where an access since the last barrier conflicts (a softmax's max and sum
             # reductions in one tile had 3 barriers each, 2 of them redundant)
+            if ctx.self_sync:
+                out.append(L.CallStmt("tl::sync_threads", []))  # WAR vs an earlier use of the workspace
             for j, d in enumerate(keys):
                 out.append(S.StoreStmt(wsf, [binop("+", j * ctx.T, ctx.tid)], red_vals[d]))
             out.append(L.CallStmt("tl::sync_threads", []))
@@ -1432,11 +1504,15 @@ class TileOpLowerer(Mutator):
                 out.append(S.LetStmt(v3, acc))
                 new_vals[d] = v3
             red_vals = new_vals
+            if ctx.self_sync:
+                out.append(L.CallStmt("tl::sync_threads", []))
         if redistribute is not None:
             # natural-layout results -> LDS (logical row-major) -> the consumer's layout
             n = _prod(dshape)
             ws = ctx.new_workspace(n, dt)
             wsf = ctx.flat_of(ws)
+            if ctx.self_sync:
+                out.append(L.CallStmt("tl::sync_threads", []))
             for d, v in red_vals.items():  # (surrounding barriers: ThreadSync, as above)
                 idx = D_lay.inverse(ctx.tid, d)
                 out.append(S.StoreStmt(wsf, [_row_major(idx, dshape)], v))
@@ -1447,6 +1523,8 @@ class TileOpLowerer(Mutator):
                 v = Var(f"redx{r}", dt, nonneg=False)
                 out.append(S.LetStmt(v, BufferLoad(wsf, [_row_major(idx, dshape)])))
                 red_vals[r] = v
+            if ctx.self_sync:
+                out.append(L.CallStmt("tl::sync_threads", []))
         for d, v in red_vals.items():
             if op.clear:
                 out.append(S.StoreStmt(dl, [IntImm(d)], cast(v, db.dtype)))
@@ -1665,7 +1743,8 @@ class TileOpLowerer(Mutator):
                 body = S.ForStmt(v, 0, e, "parallel", body)
             return [self.lower_nest(body)]
 
-        out = to_ws(src)
+        out = [L.CallStmt("tl::sync_threads", [])] if ctx.self_sync else []
+        out += to_ws(src)
         out.append(L.CallStmt("tl::sync_threads", []))
         dim = op.dim
         outer = [e for d, e in enumerate(sext) if d != dim]
@@ -1689,6 +1768,8 @@ class TileOpLowerer(Mutator):
             out.append(S.IfStmt(binop("<", slot, n_out), blk) if (o + 1) * ctx.T > n_out else blk)
         out.append(L.CallStmt("tl::sync_threads", []))
         out.extend(from_ws(dst))
+        if ctx.self_sync:
+            out.append(L.CallStmt("tl::sync_threads", []))
         return S.SeqStmt(out)
 
     def lower_AtomicOp(self, op: O.AtomicOp):
@@ -1718,13 +1799,29 @@ class TileOpLowerer(Mutator):
         lb = ctx.local_of(b)
         out = []
         opname = _REDUCE_OPS[kind][0]
-        if wave_digits:
-            raise LoweringError("finalize_reducer across waves is not supported; keep replicas within a wave")
         if lane_mask:
             for i in range(lb.shape[0]):
                 out.append(S.StoreStmt(lb, [IntImm(i)], call("extern", ["tl::lane_allreduce<%s, %d>" % (opname,
                                                                                                        lane_mask),
                                                                          BufferLoad(lb, [IntImm(i)])], b.dtype)))
+        if wave_digits and not ctx.is_cpu:
+            # replicas in other waves: every thread publishes its (lane-combined) partials to an
+            # LDS workspace ws[i][tid] and folds in its partner waves' copies
+            n = lb.shape[0]
+            ws = ctx.new_workspace(n * ctx.T, b.dtype)
+            out.append(L.CallStmt("tl::sync_threads", []))
+            for i in range(n):
+                out.append(S.StoreStmt(ws, [binop("+", i * ctx.T, ctx.tid)], BufferLoad(lb, [IntImm(i)])))
+            out.append(L.CallStmt("tl::sync_threads", []))
+            partners = _partner_offsets(ctx.tid, wave_digits)
+            for i in range(n):
+                acc = None
+                for p in partners:
+                    x = BufferLoad(ws, [binop("+", i * ctx.T, p)])
+                    acc = x if acc is None else _combine(kind, acc, x)
+                out.append(S.StoreStmt(lb, [IntImm(i)], cast(acc, b.dtype)))
+            if ctx.self_sync:
+                out.append(L.CallStmt("tl::sync_threads", []))
         return S.SeqStmt(out)
 
     def lower_AsyncCopyOp(self, op: AsyncCopyOp):

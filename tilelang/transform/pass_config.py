@@ -18,6 +18,7 @@ class PassConfigKey(str, Enum):
     TL_DISABLE_TMA_LOWER = "tl.disable_tma_lower"
     TL_ENABLE_FAST_MATH = "tl.enable_fast_math"
     TL_DISABLE_FAST_MATH = "tl.disable_fast_math"
+    TL_NO_NANS = "tl.no_nans"
     TL_PTXAS_REGISTER_USAGE_LEVEL = "tl.ptxas_register_usage_level"
     TL_CONFIG_INDEX_BITWIDTH = "tl.config_index_bitwidth"
     TL_DISABLE_SAFE_MEMORY_ACCESS = "tl.disable_safe_memory_legalize"
@@ -56,6 +57,8 @@ class PassConfigKey(str, Enum):
 EFFECT = {
     "tl.enable_fast_math": "exp/log/exp2/log2/sin/cos on the hardware transcendental unit (codegen/hip.py)",
     "tl.disable_fast_math": "forces the precise OCML math even if tl.enable_fast_math is set",
+    "tl.no_nans": "the kernel promises no NaN values (-fno-honor-nans): fmaxf of MFMA results needs no "
+                  "canonicalising v_max per operand; isnan checks and NaN-propagating selects may fold",
     "tl.config_index_bitwidth": "32 or 64: width of global-memory offsets (default: 64 only for tensors of "
                                 ">= 2^31 elements; the launcher refuses tensors too large for a 32-bit kernel)",
     "tl.disable_safe_memory_legalize": "no bounds guards on global accesses",
