@@ -173,6 +173,9 @@ def main():
                     help="untimed, time-based pre-warm before the --warmup steps (default 300 ms on a GPU): the "
                          "MI355X clocks ramp over the first ~20 ms of dense MFMA work after idle (per-step "
                          "times below); reported as prewarm_ms, never part of the timed region")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the process group and the mesh even at world size 1 (RCCL on a GPU), so "
+                         "the MoE runs expert-parallel through the mesh exchange (checked like N > 1)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: tiny shapes on the CPU target under gloo (CI plumbing check)")
     args = ap.parse_args()
@@ -192,8 +195,11 @@ def main():
         torch.cuda.set_device(local_rank)
     dist = None
     mesh = None
-    if world > 1:
+    if world > 1 or args.dist:
         import torch.distributed as dist
+        if env_world is None:  # --dist without torchrun: a one-rank rendezvous on this host
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+                              LOCAL_RANK="0")
         if cpu:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
@@ -398,7 +404,7 @@ def main():
                              + (" (EP)" if mesh is not None else " (all experts local)"))),
                 "global_batch": world,
                 "seq_len": a_["seq_len"],
-                "parallelism": (f"dp{world}" if moe is None or world == 1 else f"dp{world}+ep{world}"),
+                "parallelism": (f"dp{world}" if moe is None or mesh is None else f"dp{world}+ep{world}"),
             },
             "gemm_tflops": round(gemm_flops / gemm_ms / 1e9, 1),
             "gemm_vendor_tflops": round(gemm_flops / vendor_ms / 1e9, 1),

@@ -176,7 +176,10 @@ class Kernel {
     int per_cu = 0;
     int64_t threads = 1;
     for (auto b : block_) threads *= b;
-    TL_HIP_CHECK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func_, (int)threads, (size_t)lds_));
+    // the kernel's LDS is static (__shared__ in the code object, already part of func_'s
+    // resources): the dynamic-LDS argument is 0 -- passing lds_ again double-counted it and an
+    // 81+ KB kernel read as 0 resident blocks
+    TL_HIP_CHECK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, func_, (int)threads, 0));
     int dev = 0;
     TL_HIP_CHECK(hipGetDevice(&dev));
     hipDeviceProp_t prop;

@@ -3,7 +3,8 @@
 // The reference's DeepSeek-V3.2 demo reaches its experts with host collectives
 // (examples/deepseek_v32/inference/model.py:787-850: local experts + dist.all_reduce).  A
 // host all-to-all-v needs the split sizes on the host — one device->host sync per MoE layer.
-// Here every rank owns a symmetric buffer (hipMalloc + HIP IPC, opened by every peer) and the
+// Here every rank owns a symmetric buffer (fine-grained device memory, see "Memory model"
+// below; exported with HIP IPC and opened by every peer) and the
 // routed rows are stored straight into the destination GPU's buffer at a slot the SENDER
 // computes (its own running count per destination), so no rank ever needs another rank's
 // counts before moving data, and nothing waits on the host:

@@ -245,7 +245,9 @@ TL_DEVICE void gemm_rs(const T* __restrict__ a_regs, const T* __restrict__ B, fl
   const int wave = wave_or(wave_in);
   const int wn = wave % WARP_N;
   // T.gemm(valid_m_min=): a wave whose rows all lie below m_min has nothing to add (uniform branch)
-  if ((wave / WARP_N + 1) * WM <= m_min) return;
+  // (m_min > 0 first: with the default 0 the branch folds away at compile time -- a kept early
+  // return would force the accumulator's initial values to stay materialised in registers)
+  if (m_min > 0 && (wave / WARP_N + 1) * WM <= m_min) return;
   floatx4* acc = reinterpret_cast<floatx4*>(C);
   if constexpr (PIPE > 0 && N_REP % PIPE == 0 && KSTEPS * N_REP > PIPE) {
     constexpr int G = PIPE, NG = KSTEPS * N_REP / G;  // groups of G fragments, in (kk, ni) order

@@ -278,7 +278,11 @@ class Printer:
         for p in f.params:
             if isinstance(p, Buffer):
                 shape = "(" + ", ".join(self.e(x) for x in p.shape) + ("," if len(p.shape) == 1 else "") + ")"
-                params.append(f"{self.names(p, p.name)}: T.Tensor({shape}, {p.dtype.name!r})")
+                if p.strides is not None:  # T.StridedTensor: the strides are part of the program
+                    st = "(" + ", ".join(self.e(x) for x in p.strides) + ("," if len(p.strides) == 1 else "") + ")"
+                    params.append(f"{self.names(p, p.name)}: T.StridedTensor({shape}, {st}, {p.dtype.name!r})")
+                else:
+                    params.append(f"{self.names(p, p.name)}: T.Tensor({shape}, {p.dtype.name!r})")
             else:
                 params.append(f"{self.e(p)}: T.{p.dtype.name}")
         self.w("@T.prim_func")

@@ -54,20 +54,35 @@ def memory_fence(scope="agent"):
     _eval(call("tl.fence", [StringImm(scope)], _dt.void))
 
 
-def get_lane_idx(warp_size=64):
-    return call("tl.lane_id", [], _dt.int32)
+def _tid():
+    from .kernel import get_thread_binding
+    return get_thread_binding(0)
 
 
-def get_warp_idx(warp_size=64):
-    return call("tl.wave_id", [], _dt.int32)
+def get_lane_idx(warp_size=None):
+    """Lane within a wave (64 on gfx950); with ``warp_size``, within groups of that many threads
+    (the reference's argument: 32 gives CUDA-warp numbering)."""
+    if warp_size is None or int(warp_size) == 64:
+        return call("tl.lane_id", [], _dt.int32)
+    return _tid() % int(warp_size)
 
 
-def get_warp_idx_sync(warp_size=64):
+def get_warp_idx(warp_size=None):
+    if warp_size is None or int(warp_size) == 64:
+        return call("tl.wave_id", [], _dt.int32)
+    return _tid() // int(warp_size)
+
+
+def get_warp_idx_sync(warp_size=None):
     return get_warp_idx(warp_size)
 
 
-def get_warp_group_idx(*args):
-    return call("tl.wave_id", [], _dt.int32) // 4
+def get_warp_group_idx(warp_size=None, warps_per_group=None):
+    """Warp group = ``warps_per_group`` (default 4) consecutive waves."""
+    wpg = 4 if warps_per_group is None else int(warps_per_group)
+    if warp_size is None or int(warp_size) == 64:
+        return call("tl.wave_id", [], _dt.int32) // wpg
+    return _tid() // (int(warp_size) * wpg)
 
 
 def shfl_xor(value, offset, width=64):

@@ -359,7 +359,7 @@ def make_linear_fragment(shape: Sequence[int], num_threads: int, vec: int = 1, n
                 continue
             take = _gcd_pow(f, avail)
             if take == 1:
-                raise ValueError(f"cannot map linear fragment of {shape} with vec={vec}, threads={num_threads}")
+                return _greedy_fragment(shape, num_threads, vec, name)
             placed.append((kind, Digit(cur_dim, cur_stride, take)))
             cur_stride *= take
             f //= take
@@ -374,6 +374,32 @@ def make_linear_fragment(shape: Sequence[int], num_threads: int, vec: int = 1, n
         digits_t = [Digit(-1, 1, rep)] + digits_t
     # dims of extent 1 need no digits
     return Fragment(shape, digits_t or [Digit(-1, 1, num_threads)] if not digits_t else digits_t, digits_l, name)
+
+
+def _greedy_fragment(shape, num_threads: int, vec: int, name: str) -> Fragment:
+    """Fallback of make_linear_fragment for extents the row-major split cannot tile (a thread
+    factor straddling a non-power-of-two dim, e.g. [32, 576] over 128 threads): ``vec`` on the
+    innermost dim, then the threads take the largest factors they can from the innermost dims
+    outward, and whatever a dim has left over goes to registers."""
+    import math
+    t_left = num_threads
+    td, ld_inner, ld_outer = [], [], []
+    for dim in range(len(shape) - 1, -1, -1):
+        ext, stride = shape[dim], 1
+        if dim == len(shape) - 1 and vec > 1:
+            ld_inner.append(Digit(dim, 1, vec))
+            stride = vec
+        avail = ext // stride
+        take = math.gcd(t_left, avail)
+        if take > 1:
+            td.insert(0, Digit(dim, stride, take))
+            stride *= take
+            t_left //= take
+        if ext // stride > 1:
+            ld_outer.insert(0, Digit(dim, stride, ext // stride))
+    if t_left > 1:
+        td.insert(0, Digit(-1, 1, t_left))  # fewer elements than threads: replicate
+    return Fragment(shape, td, ld_outer + ld_inner, name)
 
 
 def _gcd_pow(a: int, b: int) -> int:

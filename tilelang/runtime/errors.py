@@ -33,7 +33,7 @@ GRID_SYNC_CODE = 8
 
 _lock = threading.Lock()
 _words = {}                       # device index -> int32 device tensor [1] (grid-barrier kernels)
-_pending = collections.deque()   # (event, pinned host tensor, device word, label, decoder)
+_pending = collections.deque()   # (ring, slot, device word, label, decoder)
 
 
 def device_word(device):
@@ -59,19 +59,59 @@ def _grid_decoder(label, code):
     return GridSyncTimeout(f"{label}: " + "; ".join(what))
 
 
+class _Ring:
+    """Per-device pool of pinned 4-byte read-back slots and their events, allocated once: a
+    launch's read-back is one async copy + one event record, no pinned allocation or event
+    creation on the launch path (EP / TP mesh kernels launch every layer)."""
+    SIZE = 1024
+
+    def __init__(self, dev_idx: int):
+        import torch
+        self.host = torch.zeros(self.SIZE, dtype=torch.int32, pin_memory=True)
+        self.views = [self.host[i:i + 1] for i in range(self.SIZE)]
+        with torch.cuda.device(dev_idx):
+            self.events = [torch.cuda.Event() for _ in range(self.SIZE)]
+        self.busy = [False] * self.SIZE
+        self.next = 0
+
+
+_rings = {}
+
+
+def _ring(word) -> _Ring:
+    idx = word.device.index
+    r = _rings.get(idx)
+    if r is None:
+        r = _rings[idx] = _Ring(idx)
+    return r
+
+
 def record(word, label: str, decoder=None):
     """Queue a non-blocking read-back of ``word`` behind the launch just issued on the current
     stream (call right after the launch)."""
-    import torch
-    host = torch.empty(1, dtype=torch.int32, pin_memory=True)
-    host.copy_(word, non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record()
     with _lock:
-        _pending.append((ev, host, word, label, decoder or _grid_decoder))
-        # bound the queue: completed clean entries are dropped by poll(); keep the newest ones
-        while len(_pending) > 4096:
-            _pending.popleft()
+        ring = _ring(word)
+        i = ring.next
+        ring.next = (i + 1) % ring.SIZE
+    if ring.busy[i]:
+        # the ring wrapped onto a read-back that was never polled: retire the oldest entries
+        _drain_slot(ring, i)
+    ring.views[i].copy_(word, non_blocking=True)
+    ring.events[i].record()
+    with _lock:
+        ring.busy[i] = True
+        _pending.append((ring, i, word, label, decoder or _grid_decoder))
+
+
+def _drain_slot(ring, i):
+    ring.events[i].synchronize()
+    poll()
+    if ring.busy[i]:  # still queued behind an unfinished entry: drop it (it was clean or raised)
+        with _lock:
+            keep = [p for p in _pending if not (p[0] is ring and p[1] == i)]
+            _pending.clear()
+            _pending.extend(keep)
+            ring.busy[i] = False
 
 
 def poll():
@@ -82,15 +122,19 @@ def poll():
     with _lock:
         keep = collections.deque()
         while _pending:
-            ev, host, word, label, dec = _pending.popleft()
-            if not ev.query():
-                keep.append((ev, host, word, label, dec))
+            ring, i, word, label, dec = _pending.popleft()
+            if not ring.events[i].query():
+                keep.append((ring, i, word, label, dec))
                 continue
-            code = int(host.item())
+            code = int(ring.host[i])
+            ring.busy[i] = False
             if code and err is None:
                 err = dec(label, code)
                 word.zero_()
                 # later launches copied the same (not yet cleared) word: one timeout raises once
+                for p in list(keep) + list(_pending):
+                    if p[2] is word:
+                        p[0].busy[p[1]] = False
                 keep = collections.deque(p for p in keep if p[2] is not word)
                 rest = [p for p in _pending if p[2] is not word]
                 _pending.clear()

@@ -129,6 +129,33 @@ def _index_map(indices, loop_vars) -> Optional[List[Optional[int]]]:
     return out
 
 
+def _is_flat_index(indices, loop_vars, loop_shape, buf_shape) -> bool:
+    """True when a buffer of the loop domain's size is indexed by the row-major flattening of the
+    loop vars (``B[i * bn + j]`` in ``T.Parallel(bm, bn)``, the reference's composable index):
+    its layout is then the nest's, reshaped (Fragment.reshape)."""
+    import random
+    from ..ir.expr import EvalError, evaluate
+    n_loop, n_buf = 1, 1
+    for e in loop_shape:
+        n_loop *= int(e)
+    for e in buf_shape or [0]:
+        n_buf *= int(e)
+    if n_loop != n_buf or len(indices) != 1 or len(buf_shape) != 1:
+        return False
+    rnd = random.Random(11)
+    for _ in range(8):
+        env = {v: rnd.randrange(int(e)) for v, e in zip(loop_vars, loop_shape)}
+        flat = 0
+        for v, e in zip(loop_vars, loop_shape):
+            flat = flat * int(e) + env[v]
+        try:
+            if int(evaluate(indices[0], env)) != flat:
+                return False
+        except (EvalError, TypeError, KeyError):
+            return False
+    return True
+
+
 def project_layout(loop_layout: Fragment, dim_map: List[Optional[int]], buf_shape: List[int]) -> Fragment:
     """Layout of a buffer accessed as ``buf[loop_vars[dim_map[0]], ...]`` inside a nest
     partitioned by ``loop_layout`` (loop dims not used by the buffer become replication)."""
@@ -493,6 +520,13 @@ class LayoutInference:
                 if b in self.frag:
                     dm = _index_map(idx, n.vars)
                     if dm is None:
+                        if _is_flat_index(idx, n.vars, shape, b.static_shape()) and all(as_int(m) == 0 for m in n.mins):
+                            try:
+                                n.layout = self.frag[b].reshape(shape)
+                                changed = True
+                                break
+                            except ValueError:
+                                pass
                         continue
                     lifted = lift_layout(self.frag[b], dm, shape)
                     if lifted is not None and all(as_int(m) == 0 for m in n.mins):
@@ -528,9 +562,14 @@ class LayoutInference:
                 if b in self.frag:
                     continue
                 dm = _index_map(idx, n.vars)
-                if dm is None:
-                    continue
                 bshape = b.static_shape()
+                if dm is None:
+                    if _is_flat_index(idx, n.vars, shape, bshape) and all(as_int(m) == 0 for m in n.mins):
+                        try:
+                            changed |= self.set_frag(b, n.layout.reshape(bshape), "parallel (flattened index)")
+                        except ValueError:
+                            pass
+                    continue
                 try:
                     lay = project_layout(n.layout, dm, bshape)
                 except ValueError:
