@@ -14,6 +14,15 @@
 
 #include <type_traits>
 
+// The T.gemm(valid_m= / valid_m_min=) wave guards are tested only when the argument is not its
+// default, so the branch folds away at compile time otherwise: a kept early-return path forces
+// the accumulator's initial values (T.clear zeros, fold_max's -m) to stay materialised in
+// registers (FA fwd: 35 v_mov per KV tile; FA bwd dQ: 96 AGPR writes per tile).
+// -DTL_GEMM_FOLD_DEFAULT_GUARD=0 restores the unconditional test (A/B only).
+#ifndef TL_GEMM_FOLD_DEFAULT_GUARD
+#define TL_GEMM_FOLD_DEFAULT_GUARD 1
+#endif
+
 namespace tl {
 
 // the wave index: callers in loops pass the kernel's own (computed once before the loop); a
@@ -137,7 +146,7 @@ TL_DEVICE void gemm_ss(const T* __restrict__ A, const T* __restrict__ B, float* 
   const int wm = wave / WARP_N, wn = wave % WARP_N;
   // T.gemm(valid_m=): a wave whose rows all lie at or past the tile's valid-row count issues
   // nothing (its accumulator rows are don't-care padding); uniform branch, folded when unused
-  if (wm * WM >= m_limit) return;
+  if ((!TL_GEMM_FOLD_DEFAULT_GUARD || m_limit < 0x3fffffff) && wm * WM >= m_limit) return;  // see gemm_rs
   floatx4* acc = reinterpret_cast<floatx4*>(C);
 #pragma unroll
   for (int kk = 0; kk < KSTEPS; ++kk) {
@@ -245,9 +254,7 @@ TL_DEVICE void gemm_rs(const T* __restrict__ a_regs, const T* __restrict__ B, fl
   const int wave = wave_or(wave_in);
   const int wn = wave % WARP_N;
   // T.gemm(valid_m_min=): a wave whose rows all lie below m_min has nothing to add (uniform branch)
-  // (m_min > 0 first: with the default 0 the branch folds away at compile time -- a kept early
-  // return would force the accumulator's initial values to stay materialised in registers)
-  if (m_min > 0 && (wave / WARP_N + 1) * WM <= m_min) return;
+  if ((!TL_GEMM_FOLD_DEFAULT_GUARD || m_min > 0) && (wave / WARP_N + 1) * WM <= m_min) return;
   floatx4* acc = reinterpret_cast<floatx4*>(C);
   if constexpr (PIPE > 0 && N_REP % PIPE == 0 && KSTEPS * N_REP > PIPE) {
     constexpr int G = PIPE, NG = KSTEPS * N_REP / G;  // groups of G fragments, in (kk, ni) order
@@ -638,7 +645,7 @@ TL_DEVICE void gemm_ss_32(const T* __restrict__ A, const T* __restrict__ B, floa
   const int lane = threadIdx.x & 63;
   const int wave = wave_or(wave_in);
   const int wm = wave / WARP_N, wn = wave % WARP_N;
-  if (wm * WM >= m_limit) return;  // T.gemm(valid_m=), as gemm_ss
+  if ((!TL_GEMM_FOLD_DEFAULT_GUARD || m_limit < 0x3fffffff) && wm * WM >= m_limit) return;  // valid_m
   floatx16* acc = reinterpret_cast<floatx16*>(C);
 #pragma unroll
   for (int kk = 0; kk < KSTEPS; ++kk) {
