@@ -46,6 +46,8 @@ enum ParamKind { kBuffer = 0, kScalar = 1, kDyn = 2 };
 struct Dim {
   bool is_static;
   int64_t value;   // static extent, or symbol id
+  int64_t mul = 1;  // symbolic extent = mul * symbol + add (T.Tensor((n * 4 + 1,)) ...)
+  int64_t add = 0;
 };
 
 struct Param {
@@ -149,8 +151,13 @@ class Kernel {
       p.sym = d["sym"].cast<int>();
       p.max_elems = d.contains("max_elems") ? d["max_elems"].cast<int64_t>() : 0;
       for (auto s : d["shape"].cast<py::list>()) {
-        auto t = s.cast<std::pair<bool, int64_t>>();
-        p.shape.push_back({t.first, t.second});
+        auto tp = s.cast<py::tuple>();
+        Dim dm{tp[0].cast<bool>(), tp[1].cast<int64_t>()};
+        if (tp.size() >= 4) {
+          dm.mul = tp[2].cast<int64_t>();
+          dm.add = tp[3].cast<int64_t>();
+        }
+        p.shape.push_back(dm);
       }
       for (auto s : d["strides"].cast<py::list>()) {
         auto t = s.cast<std::pair<bool, int64_t>>();
@@ -223,6 +230,7 @@ class Kernel {
       for (auto& d : p.shape) {
         int64_t v = d.is_static ? d.value : syms.at(d.value);
         if (v < 0) throw py::value_error(label_ + ": cannot infer output '" + p.name + "' shape (unbound symbol)");
+        if (!d.is_static) v = d.mul * v + d.add;
         shape.push_back(v);
       }
       auto opts = at::TensorOptions().dtype(static_cast<c10::ScalarType>(p.scalar_type));
@@ -323,9 +331,17 @@ class Kernel {
           throw py::value_error(os.str());
         }
       } else {
+        // extent = mul * symbol + add: solve for the symbol
+        if ((got - dm.add) < 0 || (got - dm.add) % dm.mul != 0) {
+          std::ostringstream os;
+          os << label_ << ": argument '" << p.name << "' dim " << d << " is " << got << ", not of the form "
+             << dm.mul << " * n + " << dm.add;
+          throw py::value_error(os.str());
+        }
+        const int64_t v = (got - dm.add) / dm.mul;
         int64_t& s = syms.at(dm.value);
-        if (s < 0) s = got;
-        else if (validate_ && s != got) {
+        if (s < 0) s = v;
+        else if (validate_ && s != v) {
           std::ostringstream os;
           os << label_ << ": argument '" << p.name << "' dim " << d << " is " << got
              << " but the same symbol was bound to " << s << " by an earlier argument";

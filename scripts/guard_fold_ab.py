@@ -21,8 +21,11 @@ OLD = ["-DTL_GEMM_FOLD_DEFAULT_GUARD=0"]
 
 
 def build(impl, args, kwargs=None, flags=None):
+    pc = dict(getattr(impl, "pass_configs", None) or {})
+    pc.pop("tl.gemm_fold_default_guard", None)  # the A/B sets the macro itself
+    pc.pop(tilelang.PassConfigKey.TL_GEMM_FOLD_DEFAULT_GUARD, None)
     return tilelang.compile(impl.get_tir(*args, **(kwargs or {})), out_idx=impl.out_idx, target="hip",
-                            pass_configs=getattr(impl, "pass_configs", None), compile_flags=flags)
+                            pass_configs=pc, compile_flags=flags)
 
 
 def cases():
@@ -51,6 +54,36 @@ def cases():
     out.append(("FA bwd dQ", 3 * 2.0 * B * H * S * S * D, [build(m.flashattn_bwd_dq, (B, H, S, D, False),
                                                                  dict(dtype="float16", **dqt), f)
                                                            for f in (None, OLD)], (qq, kk, vv, do, lse, delta)))
+    import example_mla_decode as md
+    bb, hh, ctx, dd, pe = 64, 128, 8192, 512, 64
+    mq = torch.randn(bb, hh, dd, device="cuda", dtype=torch.float16)
+    mqp = torch.randn(bb, hh, pe, device="cuda", dtype=torch.float16)
+    mkv = torch.randn(bb, ctx, 1, dd, device="cuda", dtype=torch.float16)
+    mkp = torch.randn(bb, ctx, 1, pe, device="cuda", dtype=torch.float16)
+    glse = torch.empty(bb, hh, 4, device="cuda")
+    part = torch.empty(bb, hh, 4, dd, device="cuda")
+    out.append(("MLA decode b64 h128 kv8192", md.flops(bb, hh, ctx, dd, pe),
+                [build(md.mla_decode, (bb, hh, 1, ctx, dd, pe), dict(num_split=4), f) for f in (None, OLD)],
+                (mq, mqp, mkv, mkp, glse, part)))
+    from tilelang.ops import dsa
+    Bs, Ss, SKV, Hs, topk = 1, 2048, 8192, 128, 2048
+    sq = torch.randn(Bs, Ss, Hs, 576, device="cuda", dtype=torch.bfloat16)
+    skv = torch.randn(Bs, SKV, 1, 576, device="cuda", dtype=torch.bfloat16)
+    r = torch.rand(Ss, SKV, device="cuda")
+    pos = torch.arange(Ss, device="cuda")[:, None] + SKV - Ss
+    r = torch.where(torch.arange(SKV, device="cuda")[None, :] <= pos, r, torch.full_like(r, -1.0))
+    idx = r.topk(topk, dim=-1).indices.int().view(Bs, Ss, 1, topk)
+    out.append(("sparse MLA fwd s2048 h128 topk2048", 2.0 * Bs * Ss * Hs * topk * (576 + 512),
+                [build(dsa.sparse_mla_fwd, (Bs, Ss, SKV, Hs, 512, 64, topk), None, f) for f in (None, OLD)],
+                (sq, skv, idx)))
+    import example_gqa_sink_fwd_bhsd as sk
+    gq = torch.randn(1, 64, 4096, 128, device="cuda", dtype=torch.bfloat16)
+    gk = torch.randn(1, 8, 4096, 128, device="cuda", dtype=torch.bfloat16)
+    gv = torch.randn_like(gk)
+    gs = torch.randn(64, device="cuda", dtype=torch.bfloat16)
+    out.append(("GQA+sink fwd causal s4096", sk.flops(1, 64, 4096, 4096, 128),
+                [build(sk.flashattn_sink, (1, 64, 4096, 4096, 128, 8), None, f) for f in (None, OLD)],
+                (gq, gk, gv, gs)))
     return out
 
 

@@ -54,6 +54,23 @@ def _scalar_type_code(dtype) -> int:
     return _SCALAR_TYPES[key]
 
 
+def _affine_of(e, symtab):
+    """(symbol id, a, b) when ``e`` is ``a * n + b`` (a > 0) in one shape symbol ``n``, else None."""
+    from ..ir.expr import free_vars, evaluate, EvalError
+    fv = [v for v in free_vars(e)]
+    if len(fv) != 1 or fv[0] not in symtab:
+        return None
+    n = fv[0]
+    try:
+        f0, f1, f7 = (int(evaluate(e, {n: x})) for x in (0, 1, 7))
+    except (EvalError, TypeError, ValueError):
+        return None
+    a, b = f1 - f0, f0
+    if a <= 0 or f7 != 7 * a + b:
+        return None
+    return (symtab[n], a, b)
+
+
 class JITKernel:
 
     def __init__(self, func: S.PrimFunc = None, out_idx: Union[List[int], int, None] = None, target="auto",
@@ -122,6 +139,8 @@ class JITKernel:
     def hip_flags(self) -> List[str]:
         """hipcc flags of this kernel's gfx950 compile: the user's plus what the pass configs imply."""
         flags = list(self.compile_flags)
+        if self.pass_configs.get("tl.gemm_fold_default_guard") is False:
+            flags.append("-DTL_GEMM_FOLD_DEFAULT_GUARD=0")
         if self.pass_configs.get("tl.no_nans"):
             # the kernel promises no NaN values: fmaxf on MFMA results then needs no canonicalising
             # v_max_f32 x, x per operand (the softmax row max of the attention kernels that set it)
@@ -153,7 +172,11 @@ class JITKernel:
                     elif isinstance(s, Var) and s in symtab:
                         d["shape"].append((False, symtab[s]))
                     else:
-                        raise ValueError(f"unsupported dynamic shape expression {s} for {b.name}")
+                        aff = _affine_of(s, symtab)
+                        if aff is None:
+                            raise ValueError(f"unsupported dynamic shape expression {s} for {b.name} (an extent "
+                                             "must be a * n + b in one symbol n)")
+                        d["shape"].append((False, ) + aff)
                 if b.strides is not None:
                     for s in b.strides:
                         v = as_int(s)

@@ -44,6 +44,15 @@ from ..layout import Layout, Fragment
 
 ceildiv = ceildiv  # noqa: F405 (from math)
 
+# C-style dtype aliases (reference frontend v2 dtypes): T.short, T.int, T.long, T.half, T.float,
+# T.double (T.bool is the boolean dtype above)
+short = int16
+int = int32  # noqa: A001
+long = int64
+half = float16
+float = float32  # noqa: A001
+double = float64
+
 
 def int_(x):
     return IntImm(x)

@@ -171,6 +171,17 @@ class _Rewriter(ast.NodeTransformer):
         return node
 
     def visit_Assign(self, node: ast.Assign):
+        if len(node.targets) == 1 and isinstance(node.targets[0], ast.Tuple) and isinstance(node.value, ast.Tuple) \
+                and len(node.targets[0].elts) == len(node.value.elts):
+            # ``a, b = b, a`` / ``A[0], A[1] = A[1], A[0]``: every right-hand value is bound to a
+            # temporary first (loads are let-bound there), so no target sees an earlier store
+            tmps = [self._tmp() for _ in node.value.elts]
+            out = []
+            for t, v in zip(tmps, node.value.elts):
+                out.append(self.visit_Assign(ast.Assign(targets=[ast.Name(id=t, ctx=ast.Store())], value=v)))
+            for tgt, t in zip(node.targets[0].elts, tmps):
+                out.append(self.visit_Assign(ast.Assign(targets=[tgt], value=ast.Name(id=t, ctx=ast.Load()))))
+            return _flatten(out)
         node.value = self.visit(node.value)
         if len(node.targets) == 1 and isinstance(node.targets[0], ast.Name):
             name = node.targets[0].id

@@ -43,6 +43,10 @@ def copy(src, dst, coalesced_width: Optional[int] = None, disable_tma: bool = Fa
     if isinstance(src, (int, float, PrimExpr)) and not isinstance(src, BufferLoad):
         # T.copy(scalar, dst) == fill
         return fill(dst, src)
+    if isinstance(src, BufferLoad) and isinstance(dst, BufferLoad):
+        # one element to one element (also inside T.Parallel): a plain store
+        current_builder().store(dst.buffer, list(dst.indices), src)
+        return None
     s, d = _pair_regions(src, dst)
     if eviction_policy not in (None, "evict_normal", "evict_first", "evict_last"):
         raise ValueError(f"T.copy: eviction_policy must be evict_normal / evict_first / evict_last, "

@@ -12,7 +12,7 @@ import tilelang.language as T
 LOG2E = 1.44269504
 
 
-@tilelang.jit(out_idx=[3, 4])
+@tilelang.jit(out_idx=[3, 4], pass_configs={tilelang.PassConfigKey.TL_GEMM_FOLD_DEFAULT_GUARD: False})
 def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_group=1, sm_scale=None, block_I=64,
                    threads=None, dtype="bfloat16", num_stages=2, block_H=None, xcd_pair=True, lazy_rescale=True,
                    wide=None):

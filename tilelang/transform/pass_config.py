@@ -19,6 +19,7 @@ class PassConfigKey(str, Enum):
     TL_ENABLE_FAST_MATH = "tl.enable_fast_math"
     TL_DISABLE_FAST_MATH = "tl.disable_fast_math"
     TL_NO_NANS = "tl.no_nans"
+    TL_GEMM_FOLD_DEFAULT_GUARD = "tl.gemm_fold_default_guard"
     TL_PTXAS_REGISTER_USAGE_LEVEL = "tl.ptxas_register_usage_level"
     TL_CONFIG_INDEX_BITWIDTH = "tl.config_index_bitwidth"
     TL_DISABLE_SAFE_MEMORY_ACCESS = "tl.disable_safe_memory_legalize"
@@ -57,6 +58,10 @@ class PassConfigKey(str, Enum):
 EFFECT = {
     "tl.enable_fast_math": "exp/log/exp2/log2/sin/cos on the hardware transcendental unit (codegen/hip.py)",
     "tl.disable_fast_math": "forces the precise OCML math even if tl.enable_fast_math is set",
+    "tl.gemm_fold_default_guard": "default True: T.gemm's valid_m wave guards are compiled out when unused (the "
+                                  "accumulator's initial values need not stay materialised); False keeps the "
+                                  "runtime test (same-process A/B, scripts/guard_fold_ab.py: FA bwd dK/dV +3-4 % "
+                                  "folded; FA fwd 0 to -4 % and sparse MLA fwd -3 % folded, so those two keep it)",
     "tl.no_nans": "the kernel promises no NaN values (-fno-honor-nans): fmaxf of MFMA results needs no "
                   "canonicalising v_max per operand; isnan checks and NaN-propagating selects may fold",
     "tl.config_index_bitwidth": "32 or 64: width of global-memory offsets (default: 64 only for tensors of "
