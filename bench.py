@@ -47,7 +47,8 @@ GEMM_CFG = dict(M=4096, N=4096, K=4096, block_M=256, block_N=256, block_K=64, th
 # ring, T.Pipelined(order, stage) schedule: QK^T(t) | rescale+PV(t-1) | softmax(t)
 # sum_mfma: softmax row sums on the matrix cores (P x ones), +1.7-2 % (profiles/r3/s3/fa_sum_mfma_ab.log)
 # fold_max: running max as the QK^T accumulator's initial value, exp(t) between the PV(t-1) MFMAs
-# (+5-8 %), young_prio: waves 4-7 at issue priority 1 (+1-2 %) (profiles/r4/fa_fold_ab.log)
+# (+5-8 %), young_prio: waves 4-7 at issue priority 1 (+1-2 %, profiles/r4/fa_fold_ab.log; re-measured
+# r5 round-robin in one process: 937.5 vs 928.4 TF sustained, profiles/r5/fa_ab_roundrobin.log)
 # xcd_heads: all query tiles of a head on one XCD, K/V read through one L2 (+2-5 %, profiles/r4/fa_xcd.log)
 ATTN_CFG = dict(batch=1, heads=64, seq_len=4096, dim=128, block_M=256, block_N=64, threads=512, num_stages=2,
                 q_in_regs=True, sum_mfma=True, fold_max=True, young_prio=True, xcd_heads=True)
