@@ -89,3 +89,40 @@ def test_phased_numerics(K, phased):
     b = torch.randn(K, N, device="cuda", dtype=torch.float16)
     c = k(a, b)
     torch.testing.assert_close(c.float(), a.float() @ b.float(), rtol=1e-2, atol=1e-2 * K ** 0.5)
+
+
+def _nt_src(M, N, K, threads=512, dtype="float16", **cfg):
+    f = matmul.get_tir(M, N, K, 256, 256, 64, threads, 2, dtype, trans_B=True, staged_epilogue=True)
+    return tilelang.lower(f, target="hip", pass_configs=cfg).kernel_source
+
+
+def test_quad_structure():
+    """The 256x256x64 NT tile on 512 threads runs the whole K loop as tl::gemm_quad_nt
+    (tl/gemm_quad.h); tl.gemm_quad=False, NN layouts and other block sizes keep the K-half
+    schedule."""
+    src = _nt_src(4096, 4096, 4096)
+    assert src.count("tl::gemm_quad_nt<half_t>(") == 1 and "gemm_ss_load" not in src and "for (int k" not in src
+    assert "tl::gemm_quad_nt<bfloat16_t>(" in _nt_src(512, 768, 192, dtype="bfloat16")
+    off = _nt_src(4096, 4096, 4096, **{"tl.gemm_quad": False})
+    assert "gemm_quad" not in off and "A_shared_k0" in off
+    assert "gemm_quad" not in _src(4096, 4096, 4096)  # NN
+    assert "gemm_quad" not in _nt_src(4096, 4096, 4096, threads=256)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [64, 128, 192, 1024, 4160])
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+def test_quad_numerics(K, dtype):
+    """1, 2, 3, 16 and 65 K tiles (odd counts end on a half iteration) against fp32 torch."""
+    M, N = 512, 768
+    f = matmul.get_tir(M, N, K, 256, 256, 64, 512, 2, dtype, trans_B=True, staged_epilogue=True)
+    k = tilelang.compile(f, out_idx=[-1], target="hip")
+    assert "gemm_quad_nt" in k.get_kernel_source()
+    td = getattr(torch, dtype)
+    a = torch.randn(M, K, device="cuda", dtype=td)
+    b = torch.randn(N, K, device="cuda", dtype=td)
+    for _ in range(2):  # a rerun with new data: stale LDS would show here
+        c = k(a, b)
+        ref = a.float() @ b.float().T
+        torch.testing.assert_close(c.float(), ref, rtol=2e-2, atol=2e-2 * K ** 0.5)
+        a = torch.randn_like(a)

@@ -126,7 +126,8 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
     phased = cfg.get("tl.gemm_phased")
     if target.kind == "hip" and phased is not False:  # default on: +15 % at 4096^3 (profiles/r2/gemm_phased.log)
         from ..transform.gemm_ksplit import split_gemm_k_halves
-        kernel = split_gemm_k_halves(kernel, True if phased is None else phased)
+        kernel = split_gemm_k_halves(kernel, True if phased is None else phased,
+                                     quad=cfg.get("tl.gemm_quad", True) is not False, threads=T, target=target)
     t = time.perf_counter()
     li = infer_layouts(S.PrimFunc(func.name, func.params, kernel, func.attrs), T, target)
     timings["layout_inference"] = timings.get("layout_inference", 0) + time.perf_counter() - t

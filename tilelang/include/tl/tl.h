@@ -3,6 +3,7 @@
 #include "common.h"
 #include "copy.h"
 #include "gemm.h"
+#include "gemm_quad.h"
 #include "reduce.h"
 #include "atomic.h"
 #include "swizzle.h"

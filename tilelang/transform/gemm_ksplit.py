@@ -22,6 +22,10 @@ no ``s_waitcnt vmcnt(0)`` sits in the main loop (guide §5 "The 256^2 8-phase te
 
 Applied when the loop matches that shape, both operands are 16-bit, BK = 64 (two 32-deep MFMA
 K steps), num_stages = 2, and ``tl.gemm_phased`` is not disabled.
+
+The 256x256x64 NT tile on 512 threads (``tl.gemm_quad``, default on) is instead marked
+``quad``: the pipeline pass replaces the whole loop with ``tl::gemm_quad_nt`` (tl/gemm_quad.h,
+the guide's 8-phase quadrant schedule; +8-10 % over the K-half schedule at 4096^3 / 8192^3).
 """
 from __future__ import annotations
 
@@ -79,13 +83,41 @@ def _split_gather(gp: O.GatherRowsOp, kdim_dst: int, half: int, new_dst: Buffer,
     return O.GatherRowsOp(BufferRegion(gp.src.buffer, region), gp.idx, BufferRegion(new_dst, dreg), gp.row_dim)
 
 
+def _quad_ok(g: O.GemmOp, cps, threads, target) -> bool:
+    """The loop is the 256x256x64 NT tile GEMM that ``tl::gemm_quad_nt`` (tl/gemm_quad.h)
+    implements: A_s [256][64], B_s [256][64] (transpose_B), 16-bit, 512 threads on a 4x2 wave
+    grid with 16x16x32 MFMAs, plain global copies, fp32 fragment accumulator."""
+    from ..ir import dtypes as _dt
+    from . import gemm_lower
+    if threads != 512 or g.trans_A or not g.trans_B:
+        return False
+    if getattr(g, "valid_m", None) is not None or getattr(g, "valid_m_min", None) is not None:
+        return False
+    if g.clear_accum not in (False, None, 0):
+        return False
+    A, B = g.A.buffer, g.B.buffer
+    if A.static_shape() != [256, 64] or B.static_shape() != [256, 64] or g.C.buffer.dtype != _dt.float32:
+        return False
+    if A.dtype not in (_dt.float16, _dt.bfloat16):
+        return False
+    if any(not isinstance(c, O.CopyOp) for c in cps.values()):
+        return False
+    try:
+        plan = gemm_lower.gemm_plan(g, threads, target)
+    except Exception:  # noqa: BLE001 -- not a plannable GEMM: leave it to the generic path
+        return False
+    return plan.get("warp_m") == 4 and plan.get("warp_n") == 2 and tuple(plan.get("mfma") or ()) == (16, 16, 32)
+
+
 class _KSplit(Mutator):
 
-    def __init__(self, mode=True):
+    def __init__(self, mode=True, quad=False, threads=None, target=None):
         self.mode = mode
+        self.quad, self.threads, self.target = quad, threads, target
         self.new_allocs = {}  # old buffer -> (half0, half1)
         self.pairs = {}       # A tile <-> B tile of one split GEMM
         self.applied = 0
+        self.quads = 0
 
     def visit_ForStmt(self, s: S.ForStmt):
         body = self.stmt(s.body)
@@ -110,6 +142,12 @@ class _KSplit(Mutator):
         cps = {c.op.dst.buffer: c.op for c in copies}
         if set(cps) != {A, B} or any(c.op.src.buffer.scope != "global" for c in copies):
             return loop
+        if self.quad and _quad_ok(g, cps, self.threads, self.target):
+            # whole-loop quadrant schedule (pipeline.py _quad_schedule): not K-split
+            self.quads += 1
+            ann = dict(s.annotations)
+            ann["quad"] = True
+            return S.ForStmt(s.var, s.min, s.extent, s.kind, body, ann)
         ka, kb = _k_dims(g)
         sa, sb = A.static_shape(), B.static_shape()
         if sa is None or sb is None or len(sa) != 2 or len(sb) != 2 or sa[ka] != 64 or sb[kb] != 64:
@@ -184,12 +222,13 @@ class _AllocSplit(Mutator):
         return s
 
 
-def split_gemm_k_halves(kernel: S.KernelStmt, mode=True) -> S.KernelStmt:
-    """``mode``: True, or "prio" to also raise the wave priority around each MFMA cluster."""
-    ks = _KSplit(mode)
+def split_gemm_k_halves(kernel: S.KernelStmt, mode=True, quad=False, threads=None, target=None) -> S.KernelStmt:
+    """``mode``: True, or "prio" to also raise the wave priority around each MFMA cluster.
+    ``quad``: loops that ``tl::gemm_quad_nt`` implements are marked for it instead of split."""
+    ks = _KSplit(mode, quad, threads, target)
     k = ks.stmt(kernel)
     if not ks.applied:
-        return kernel
+        return k if ks.quads else kernel
     from .pipeline import _referenced_buffers
     used = _referenced_buffers(k)
     return _AllocSplit(ks.new_allocs, used, ks.pairs).stmt(k)

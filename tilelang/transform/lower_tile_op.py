@@ -1871,6 +1871,21 @@ class TileOpLowerer(Mutator):
                                                  L.BufferPtr(ctx.flat_of(NB), lds_off)]))
         return S.SeqStmt(out)
 
+    def lower_QuadGemmLoopOp(self, op):
+        """``tl::gemm_quad_nt``: the whole 256x256x64 NT main loop (transform/pipeline.py
+        _quad_schedule, tl/gemm_quad.h); the accumulator keeps tl::gemm_ss's register layout."""
+        ctx = self.ctx
+        args = []
+        for r, rdim in ((op.a, op.a_rdim), (op.b, op.b_rdim)):
+            sb = r.buffer
+            mins = [self.expr(m) for m in r.mins]
+            args.append(L.BufferPtr(ctx.flat_of(sb), ctx.flat_index(sb, mins)))
+            args.append(cast(self.expr(convert(sb.get_strides()[rdim])), _dt.int32))
+        args.append(cast(self.expr(convert(op.n)), _dt.int32))
+        args += [L.BufferPtr(ctx.flat_of(op.lds_a), 0), L.BufferPtr(ctx.flat_of(op.lds_b), 0),
+                 L.BufferPtr(ctx.local_of(op.C.buffer), 0), ctx.wave_expr()]
+        return S.SeqStmt([L.CallStmt("tl::gemm_quad_nt", args, [_dt.hip_type(op.a.buffer.dtype)])])
+
     def lower_async_small(self, op: AsyncCopyOp):
         """Small-tile DMA (pipeline._small_dma_plan): one 4-byte buffer LDS-DMA per wave; lane chunk
         ``P = wave * 64 + lane`` of the row-major tile, lanes past the tile (or the tensor) get an

@@ -44,6 +44,7 @@ class PassConfigKey(str, Enum):
     TL_LDS_REUSE = "tl.lds_reuse"                  # liveness-based LDS arena sharing (default on)
     TL_MFMA_SHAPE = "tl.mfma_shape"                # "16x16" (default) or "32x32" MFMA tiles
     TL_GEMM_PHASED = "tl.gemm_phased"              # K-half phased GEMM main loop (gemm_ksplit)
+    TL_GEMM_QUAD = "tl.gemm_quad"                  # 256x256x64 NT tile: whole-loop quadrant schedule
     TL_GEMM_PREFETCH = "tl.gemm_prefetch"          # fragments read one phase ahead of their MFMAs
     TL_GEMM_INTERLEAVE = "tl.gemm_interleave"      # 1 MFMA : 1 ds_read sched_group_barrier pattern
     TL_DISABLE_ADDRESS_HOIST = "tl.disable_address_hoist"  # keep LDS-DMA source addresses in the loop
@@ -86,6 +87,9 @@ EFFECT = {
     "tl.gemm_phased": "default on; False keeps BK=64 16-bit GEMM main loops whole instead of splitting them "
                       "into K halves refilled one phase apart (transform/gemm_ksplit.py + the phased "
                       "pipeline schedule); 'prio' also raises wave priority around the MFMA clusters",
+    "tl.gemm_quad": "default on; False keeps the 256x256x64 NT GEMM main loop (512 threads, 4x2 waves) on the "
+                    "K-half phased schedule instead of tl::gemm_quad_nt (tl/gemm_quad.h: 8-phase quadrant "
+                    "schedule, one half-tile restaged per phase, counted vmcnt(6) once per K tile)",
     "tl.gemm_prefetch": "default on; False: in the phased K-half schedule, read each half's MFMA fragments "
                         "after its own barrier instead of one phase ahead (transform/pipeline.py "
                         "_prefetch_schedule, tl::gemm_ss_load / gemm_ss_mma)",

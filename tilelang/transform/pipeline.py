@@ -55,6 +55,27 @@ class AsyncCopyOp(O.TileOp):
         return [self.dst]
 
 
+class QuadGemmLoopOp(O.TileOp):
+    """A whole 256x256x64 NT GEMM main loop as ``tl::gemm_quad_nt`` (tl/gemm_quad.h): ``a`` / ``b``
+    are the global tiles of the first K step (``rdim`` their row dims), ``lds_a`` / ``lds_b`` the
+    2-stage LDS rings, ``n`` the K-step count; ``C`` keeps the GEMM's fragment layout."""
+    kind = "gemm_quad_loop"
+
+    def __init__(self, a: BufferRegion, a_rdim: int, b: BufferRegion, b_rdim: int, lds_a: Buffer, lds_b: Buffer,
+                 C: BufferRegion, n, gemm: O.GemmOp):
+        self.a, self.a_rdim, self.b, self.b_rdim = a, a_rdim, b, b_rdim
+        self.lds_a, self.lds_b, self.C, self.n, self.gemm = lds_a, lds_b, C, n, gemm
+
+    def regions(self):
+        return [self.a, self.b, self.C]
+
+    def reads(self):
+        return [self.a, self.b, self.C]
+
+    def writes(self):
+        return [self.C]
+
+
 class GatherIndexOp(O.TileOp):
     """Prefetch of a gather's row indices into registers (one per LDS-DMA instruction and lane),
     issued a step ahead of the DMA that consumes them, so the index load latency never sits
@@ -558,6 +579,11 @@ class PipelineInjector(Mutator):
             prologue.append(S.seq(*st) if nv is not None and nv > 0 else S.IfStmt(binop("<", 0, n), S.seq(*st)))
 
         consumer_stmts = [st for st in stmts if not any(st is p for p, _ in prods)]
+        if loop.annotations.get("quad") and nstages == 2 and not staged and len(asyncs) == 2:
+            q = _quad_schedule(self, loop, asyncs, consumer_stmts, newbufs)
+            if q is not None:
+                return q
+            _log.debug("quad GEMM loop %s: falling back to the generic pipeline", loop.var)
         if loop.annotations.get("phased") and nstages == 2 and not staged and len(asyncs) == 4 and \
                 all(getattr(p.op, "khalf", None) is not None for p, _, _ in asyncs):
             ph = _phased_schedule(self, loop, asyncs, issue_async, consumer_stmts, mapping, newbufs, kk, n, lets)
@@ -680,6 +706,60 @@ def _phased_schedule(self, loop, asyncs, issue_async, consumer_stmts, mapping, n
         if NB not in lst:
             lst.append(NB)
     return S.SeqStmt(prologue + [new_loop, L.CallStmt("tl::barrier_raw", [])])
+
+
+def _k_coeff(e, k) -> Optional[int]:
+    """Coefficient of ``k`` in ``e`` if ``e`` is affine in ``k`` (other terms free), else None."""
+    from ..ir.expr import BinOp
+    if not any(v is k for v in free_vars(e)):
+        return 0
+    if e is k:
+        return 1
+    if isinstance(e, BinOp) and e.op in ("+", "-"):
+        ca, cb = _k_coeff(e.a, k), _k_coeff(e.b, k)
+        if ca is None or cb is None:
+            return None
+        return ca + cb if e.op == "+" else ca - cb
+    if isinstance(e, BinOp) and e.op == "*":
+        if as_int(e.b) is not None:
+            c = _k_coeff(e.a, k)
+            return None if c is None else c * as_int(e.b)
+        if as_int(e.a) is not None:
+            c = _k_coeff(e.b, k)
+            return None if c is None else c * as_int(e.a)
+    return None
+
+
+def _quad_schedule(self, loop, asyncs, consumer_stmts, newbufs):
+    """The whole loop as ``tl::gemm_quad_nt`` (loops marked ``quad`` by gemm_ksplit): both tiles
+    plain in-bounds LDS-DMA copies whose K start advances by exactly 64 per step along the
+    contiguous dim, the GEMM the only consumer.  None: the generic pipeline handles the loop."""
+    if len(consumer_stmts) != 1 or not isinstance(consumer_stmts[0], S.TileOpStmt) or \
+            not isinstance(consumer_stmts[0].op, O.GemmOp):
+        return None
+    g = consumer_stmts[0].op
+    k = loop.var
+    tiles = {}
+    for p, src, plan in asyncs:
+        if not isinstance(p.op, O.CopyOp) or plan.get("gather") or plan.get("small") or plan.get("oob_bytes") or \
+                plan.get("dup") or plan["rdim"] is None:
+            return None
+        for d, (m, _) in enumerate(src.region):
+            if _k_coeff(m, k) != (64 if d == plan["cdim"] else 0):
+                return None
+        tiles[p.op.dst.buffer] = (_subst_region(src, {k: loop.min}), plan["rdim"])
+    A, B = g.A.buffer, g.B.buffer
+    if set(tiles) != {A, B}:
+        return None
+    op = QuadGemmLoopOp(tiles[A][0], tiles[A][1], tiles[B][0], tiles[B][1], newbufs[A], newbufs[B], g.C,
+                        loop.extent, g)
+    self.replaced = getattr(self, "replaced", {})
+    for Bf in (A, B):
+        lst = self.replaced.setdefault(Bf, [])
+        if newbufs[Bf] not in lst:
+            lst.append(newbufs[Bf])
+    # the barrier ahead: earlier readers of the LDS the DMAs overwrite are done
+    return S.SeqStmt([L.CallStmt("tl::barrier_raw", []), S.TileOpStmt(op), L.CallStmt("tl::barrier_raw", [])])
 
 
 def _prefetchable(op, target) -> bool:
