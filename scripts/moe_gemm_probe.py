@@ -52,13 +52,14 @@ for kw in VARIANTS:
         print(kw, "failed", str(e)[:200], flush=True)
 # the whole bench layer (router, dispatch, both GEMMs, combine) per gemm_cfg
 from tilelang.models.moe import MoEConfig, MoELayer  # noqa: E402
-for ext in (0, 32, 0, 32):
+LAYERS = eval(sys.argv[2]) if len(sys.argv) > 2 else ((0, True), (32, True), (0, True), (32, True))
+for ext, quad in LAYERS:
     cfg = MoEConfig(hidden=H, ffn=F, n_experts=E, topk=TOP, dtype=torch.bfloat16, block_M=BM,
-                    gemm_cfg=dict(block_N=256, block_K=64, num_stages=2, threads=512, ext_M=ext))
+                    gemm_cfg=dict(block_N=256, block_K=64, num_stages=2, threads=512, ext_M=ext, quad=quad))
     layer = MoELayer(cfg, "local", device=dev)
     xs = torch.randn(T_, H, device=dev, dtype=torch.bfloat16)
     t = do_bench(lambda: layer(xs), warmup=10, rep=50)
-    print(f"MoE layer ext_M={ext}: {t * 1e3:.1f} us {6.0 * n * H * F / t * 1e-9:.0f} TF", flush=True)
+    print(f"MoE layer ext_M={ext} quad={quad}: {t * 1e3:.1f} us {6.0 * n * H * F / t * 1e-9:.0f} TF", flush=True)
 from example_gemm import matmul  # noqa: E402
 g = matmul(4096, 4096, 4096, 256, 256, 64, 512, 2, staged_epilogue=True)
 a, b = torch.randn(4096, 4096, device=dev).half(), torch.randn(4096, 4096, device=dev).half()

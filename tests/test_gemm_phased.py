@@ -49,7 +49,7 @@ def test_prefetch_valid_m_structure():
     from tilelang.ops.moe import expert_gemm_sk_kernel, max_padded_rows
     mr = max_padded_rows(4096, 8, 256)
     k = expert_gemm_sk_kernel(mr, 2048, 4096, 8, "bfloat16", "hip", 256, phased=True, skip_padding=True,
-                              block_N=256, block_K=64, num_stages=2, threads=512)
+                              block_N=256, block_K=64, num_stages=2, threads=512, quad=False)
     src = k.get_kernel_source()
     body = src[src.index("for (int k"):]
     guard = "if ((((wave_ / 2) * 64) < nrows[0])) {"
@@ -101,12 +101,28 @@ def test_quad_structure():
     (tl/gemm_quad.h); tl.gemm_quad=False, NN layouts and other block sizes keep the K-half
     schedule."""
     src = _nt_src(4096, 4096, 4096)
-    assert src.count("tl::gemm_quad_nt<half_t>(") == 1 and "gemm_ss_load" not in src and "for (int k" not in src
-    assert "tl::gemm_quad_nt<bfloat16_t>(" in _nt_src(512, 768, 192, dtype="bfloat16")
+    assert src.count("tl::gemm_quad_nt_x<half_t, false, 0>(") == 1 and "gemm_ss_load" not in src
+    assert "for (int k" not in src
+    assert "tl::gemm_quad_nt_x<bfloat16_t, false, 0>(" in _nt_src(512, 768, 192, dtype="bfloat16")
     off = _nt_src(4096, 4096, 4096, **{"tl.gemm_quad": False})
     assert "gemm_quad" not in off and "A_shared_k0" in off
     assert "gemm_quad" not in _src(4096, 4096, 4096)  # NN
     assert "gemm_quad" not in _nt_src(4096, 4096, 4096, threads=256)
+
+
+def test_quad_moe_structure():
+    """The MoE expert GEMMs (row gather + 32-row extension GEMM + valid_m; dense A with an
+    unprovable row range) take the quad loop with the range-checked row modes."""
+    from tilelang.ops.moe import expert_gemm_sk_kernel, max_padded_rows
+    mr = max_padded_rows(4096, 8, 288)
+    g1 = expert_gemm_sk_kernel(mr, 4096, 4096, 8, "bfloat16", "hip", 256, n_src=2048, swiglu=True, ext_M=32,
+                               block_N=256, block_K=64, num_stages=2, threads=512).get_kernel_source()
+    assert "tl::gemm_quad_nt_x<bfloat16_t, true, 32>((&A[0]), 4096, (&row_src[" in g1
+    g2 = expert_gemm_sk_kernel(mr, 2048, 4096, 8, "bfloat16", "hip", 256, ext_M=32, block_N=256, block_K=64,
+                               num_stages=2, threads=512).get_kernel_source()
+    assert "tl::gemm_quad_nt_x<bfloat16_t, true, 32>((&A[0]), 2048, tl::quad::no_rows()," in g2
+    # the narrow tail tiles (256 x 64) keep the generic pipeline
+    assert "for (int k" in g2
 
 
 @pytest.mark.gpu

@@ -138,13 +138,16 @@ def test_moe_tail_balanced_gpu():
     g, w1, w2 = (t.to("cuda") for t in init_moe_weights(cfg))
     from tilelang.ops import moe as K
     ref = moe_reference(x, g, w1, w2, cfg.topk, routing=K.route(x, g, cfg.topk))
-    for sk, ph, skip, ext in ((True, False, True, 0), (False, False, True, 0), (True, True, True, 0),
-                              (True, True, False, 0), (True, False, True, 32)):
+    for sk, ph, skip, ext, quad in ((True, False, True, 0, True), (False, False, True, 0, True),
+                                    (True, True, True, 0, False), (True, True, False, 0, False),
+                                    (True, False, True, 32, True), (True, False, True, 32, False),
+                                    (True, False, False, 32, True)):
         # phased: K-half ring with register-prefetched fragments; skip: padding waves skip
         # their reads and MFMAs (T.gemm(valid_m=)) inside the prefetched schedule too; ext: 288-row
-        # slots (256 + a 32-row extension GEMM on the same W tile), rows spread evenly per expert
+        # slots (256 + a 32-row extension GEMM on the same W tile), rows spread evenly per expert;
+        # quad: the whole-tile loop as tl::gemm_quad_nt_x (gather + extension + valid_m)
         layer.cfg.gemm_cfg = dict(block_N=256, block_K=64, num_stages=2, threads=512, stream_k=sk, phased=ph,
-                                  skip_padding=skip, ext_M=ext)
+                                  skip_padding=skip, ext_M=ext, quad=quad)
         out = layer(x).float()
         torch.testing.assert_close(out, ref, rtol=3e-2, atol=3e-2 * ref.abs().max().item())
 

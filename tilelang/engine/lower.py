@@ -123,11 +123,13 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
         from ..transform.storage_rewrite import rewrite_local_storage
         # local arrays with disjoint lifetimes share storage (+ element-wise in-place reuse if asked)
         kernel, _ = rewrite_local_storage(kernel, bool(cfg.get("tl.storage_rewrite_detect_inplace")))
+    if target.kind == "hip" and cfg.get("tl.gemm_quad", True) is not False:
+        from ..transform.gemm_ksplit import mark_quad_loops
+        kernel = mark_quad_loops(kernel, T, target)  # 256x256x64 NT loops -> tl::gemm_quad_nt_x
     phased = cfg.get("tl.gemm_phased")
     if target.kind == "hip" and phased is not False:  # default on: +15 % at 4096^3 (profiles/r2/gemm_phased.log)
         from ..transform.gemm_ksplit import split_gemm_k_halves
-        kernel = split_gemm_k_halves(kernel, True if phased is None else phased,
-                                     quad=cfg.get("tl.gemm_quad", True) is not False, threads=T, target=target)
+        kernel = split_gemm_k_halves(kernel, True if phased is None else phased)
     t = time.perf_counter()
     li = infer_layouts(S.PrimFunc(func.name, func.params, kernel, func.attrs), T, target)
     timings["layout_inference"] = timings.get("layout_inference", 0) + time.perf_counter() - t

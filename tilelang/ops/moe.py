@@ -495,8 +495,13 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
                           block_N: int = 256, block_K: int = 64, num_stages: int = 2, threads: int = 512,
                           n_src: Optional[int] = None, swiglu: bool = False, n_cu: int = 256, tail_split: int = 4,
                           phased: bool = False, skip_padding: bool = True, partial_first: bool = False,
-                          tail_ksplit: int = 0, tail_stages: Optional[int] = None, ext_M: int = 0):
+                          tail_ksplit: int = 0, tail_stages: Optional[int] = None, ext_M: int = 0,
+                          quad: bool = True):
     """Tail-balanced variant of ``expert_gemm_kernel`` (same arguments and output).
+
+    ``quad``: the whole-tile main loop (256x256x64, 512 threads, row gather + ``ext_M`` = 32
+    extension included) runs the 8-phase quadrant schedule ``tl::gemm_quad_nt_x`` (tl.gemm_quad);
+    False keeps the generic 2-stage pipeline.
 
     ``ext_M`` > 0: a row tile is a slot of ``block_M + ext_M`` rows (the dispatch layout's
     ``block_M`` is that slot, ``align_kernel(even=True)``): the first ``block_M`` rows run as the
@@ -726,7 +731,7 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
 
     # K-half phased main loop (row gathers included) measured slower here: 382-403 vs 300-356 us per
     # layer (profiles/r2/session2/moe_phased_tail_sweep.log), so off by default
-    cfg = {"tl.gemm_phased": bool(phased)}
+    cfg = {"tl.gemm_phased": bool(phased), "tl.gemm_quad": bool(quad)}
     if swiglu:
         cfg[tilelang.PassConfigKey.TL_ENABLE_FAST_MATH] = True
     return tilelang.compile(moe_expert_gemm_tb, out_idx=None, target=target, pass_configs=cfg)
@@ -889,7 +894,7 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
     if sk:
         # tail-balanced grid: whole tiles for the leading rounds, narrow tiles for the trailing partial round
         skc = {k: v for k, v in cfg.items() if k in ("block_N", "block_K", "num_stages", "threads", "tail_split",
-                                                      "phased", "skip_padding", "tail_ksplit", "tail_stages")}
+                                                      "phased", "skip_padding", "tail_ksplit", "tail_stages", "quad")}
         # partial_first for the down projection: measured neutral (profiles/r3/s3/moe/), off
         pf2 = cfg.get("partial_first2", False)
         ws = ()
@@ -903,7 +908,7 @@ def expert_ffn_padded(src_rows: torch.Tensor, expert_ids: torch.Tensor, div: int
         y = torch.empty(max_rows, H, dtype=src_rows.dtype, device=dev)
         k2(act, w2, te, row_src, trows, y, *ws)
         return y, dest
-    for key in ("tail_split", "phased", "partial_first2", "tail_ksplit", "tail_stages"):  # tail-balanced grid only
+    for key in ("tail_split", "phased", "partial_first2", "tail_ksplit", "tail_stages", "quad"):  # tail-balanced only
         cfg.pop(key, None)
     if w1_interleaved:
         # gate/up rows interleaved: the activation is the first GEMM's epilogue

@@ -34,7 +34,7 @@ from typing import Optional
 from ..ir import stmt as S
 from ..ir import tileop as O
 from ..ir.buffer import Buffer, BufferRegion
-from ..ir.expr import IntImm, binop
+from ..ir.expr import IntImm, as_int, binop
 from .utils import Mutator, flatten_seq
 
 
@@ -83,48 +83,129 @@ def _split_gather(gp: O.GatherRowsOp, kdim_dst: int, half: int, new_dst: Buffer,
     return O.GatherRowsOp(BufferRegion(gp.src.buffer, region), gp.idx, BufferRegion(new_dst, dreg), gp.row_dim)
 
 
-def _quad_ok(g: O.GemmOp, cps, threads, target) -> bool:
-    """The loop is the 256x256x64 NT tile GEMM that ``tl::gemm_quad_nt`` (tl/gemm_quad.h)
-    implements: A_s [256][64], B_s [256][64] (transpose_B), 16-bit, 512 threads on a 4x2 wave
-    grid with 16x16x32 MFMAs, plain global copies, fp32 fragment accumulator."""
+def _plus_const(e, base, c) -> bool:
+    """``e`` is ``base + c`` (structurally)."""
+    from ..ir.expr import BinOp, as_int, structural_equal
+    return isinstance(e, BinOp) and e.op == "+" and as_int(e.b) == c and structural_equal(e.a, base)
+
+
+def _minus_const(e, base, c) -> bool:
+    from ..ir.expr import BinOp, as_int, structural_equal
+    return isinstance(e, BinOp) and e.op == "-" and as_int(e.b) == c and structural_equal(e.a, base)
+
+
+def quad_loop_ok(stmts, threads, target) -> bool:
+    """The loop body is the 256x256x64 NT tile GEMM that ``tl::gemm_quad_nt_x`` (tl/gemm_quad.h)
+    implements: A_s [256][64] (a plain copy or a row gather), B_s [256][64] (transpose_B), 16-bit,
+    512 threads on a 4x2 wave grid with 16x16x32 MFMAs, fp32 fragment accumulator; optionally
+    T.gemm(valid_m=) and the MoE extension GEMM -- A_x [32][64] (rows 256..287 of the same copy or
+    gather), the same B_s, 1x8 waves (FullCol), valid_m = the main valid_m - 256."""
     from ..ir import dtypes as _dt
     from . import gemm_lower
-    if threads != 512 or g.trans_A or not g.trans_B:
+    if threads != 512:
         return False
-    if getattr(g, "valid_m", None) is not None or getattr(g, "valid_m_min", None) is not None:
+    gemms = [x.op for x in stmts if isinstance(x, S.TileOpStmt) and isinstance(x.op, O.GemmOp)]
+    prods = [x.op for x in stmts if isinstance(x, S.TileOpStmt) and isinstance(x.op, (O.CopyOp, O.GatherRowsOp))]
+    if len(gemms) + len(prods) != len(stmts) or len(gemms) not in (1, 2):
         return False
-    if g.clear_accum not in (False, None, 0):
+    main = [g for g in gemms if g.A.buffer.static_shape() == [256, 64]]
+    if len(main) != 1:
         return False
+    g = main[0]
+    ext = [x for x in gemms if x is not g]
+    x = ext[0] if ext else None
+
+    def plain(op):
+        return not (op.trans_A or not op.trans_B or op.is_mx or op.is_sp or op.clear_accum not in (False, None, 0) or
+                    getattr(op, "valid_m_min", None) is not None or op.C.buffer.dtype != _dt.float32 or
+                    op.A.buffer.scope != "shared" or op.B.buffer.scope != "shared")
+
+    def warps(op, wm, wn):
+        try:
+            plan = gemm_lower.gemm_plan(op, threads, target)
+        except Exception:  # noqa: BLE001 -- not plannable: the generic path reports it
+            return False
+        return plan.get("warp_m") == wm and plan.get("warp_n") == wn and tuple(plan.get("mfma") or ()) == (16, 16, 32)
+
     A, B = g.A.buffer, g.B.buffer
-    if A.static_shape() != [256, 64] or B.static_shape() != [256, 64] or g.C.buffer.dtype != _dt.float32:
+    if not plain(g) or B.static_shape() != [256, 64] or A.dtype not in (_dt.float16, _dt.bfloat16) or B.dtype != A.dtype:
         return False
-    if A.dtype not in (_dt.float16, _dt.bfloat16):
+    if not warps(g, 4, 2):
         return False
-    if any(not isinstance(c, O.CopyOp) for c in cps.values()):
+    dsts = {A, B}
+    if x is not None:
+        if not plain(x) or x.B.buffer is not B or x.A.buffer.static_shape() != [32, 64] or x.A.buffer.dtype != A.dtype:
+            return False
+        if x.C.buffer.static_shape() != [32, 256] or not warps(x, 1, 8):
+            return False
+        vm, vx = getattr(g, "valid_m", None), getattr(x, "valid_m", None)
+        if (vm is None) != (vx is None) or (vm is not None and not _minus_const(vx, vm, 256)):
+            return False
+        dsts.add(x.A.buffer)
+    by_dst = {p.dst.buffer: p for p in prods}
+    if set(by_dst) != dsts or len(by_dst) != len(prods) or any(p.src.buffer.scope != "global" for p in prods):
         return False
-    try:
-        plan = gemm_lower.gemm_plan(g, threads, target)
-    except Exception:  # noqa: BLE001 -- not a plannable GEMM: leave it to the generic path
+    if not isinstance(by_dst[B], O.CopyOp):
         return False
-    return plan.get("warp_m") == 4 and plan.get("warp_n") == 2 and tuple(plan.get("mfma") or ()) == (16, 16, 32)
+    pa = by_dst[A]
+    if x is not None:
+        px = by_dst[x.A.buffer]
+        if type(px) is not type(pa) or px.src.buffer is not pa.src.buffer:
+            return False
+        if isinstance(pa, O.GatherRowsOp):
+            (mm, em), (mx, ex) = pa.idx.region[-1], px.idx.region[-1]
+            if pa.row_dim != 0 or px.row_dim != 0 or as_int(em) != 256 or as_int(ex) != 32 or \
+                    not _plus_const(mx, mm, 256):
+                return False
+        else:
+            if not _plus_const(px.src.region[0][0], pa.src.region[0][0], 256):
+                return False
+    elif isinstance(pa, O.GatherRowsOp) and (pa.row_dim != 0 or as_int(pa.idx.region[-1][1]) != 256):
+        return False
+    return True
+
+
+class _QuadMark(Mutator):
+    """Marks the T.Pipelined loops ``quad_loop_ok`` accepts (``quad`` annotation): the pipeline
+    pass replaces them with ``tl::gemm_quad_nt_x`` (pipeline.py _quad_schedule), ksplit skips them."""
+
+    def __init__(self, threads, target):
+        self.threads, self.target = threads, target
+        self.count = 0
+
+    def visit_ForStmt(self, s: S.ForStmt):
+        body = self.stmt(s.body)
+        ann = dict(s.annotations)
+        if s.kind == "pipelined" and int(ann.get("num_stages", 0)) == 2 and not ann.get("order") and \
+                not ann.get("stage") and quad_loop_ok(flatten_seq(body), self.threads, self.target):
+            ann["quad"] = True
+            self.count += 1
+        return S.ForStmt(s.var, s.min, s.extent, s.kind, body, ann)
+
+    def visit_AllocStmt(self, s):
+        return s
+
+
+def mark_quad_loops(kernel: S.KernelStmt, threads: int, target) -> S.KernelStmt:
+    qm = _QuadMark(threads, target)
+    k = qm.stmt(kernel)
+    return k if qm.count else kernel
 
 
 class _KSplit(Mutator):
 
-    def __init__(self, mode=True, quad=False, threads=None, target=None):
+    def __init__(self, mode=True):
         self.mode = mode
-        self.quad, self.threads, self.target = quad, threads, target
         self.new_allocs = {}  # old buffer -> (half0, half1)
         self.pairs = {}       # A tile <-> B tile of one split GEMM
         self.applied = 0
-        self.quads = 0
 
     def visit_ForStmt(self, s: S.ForStmt):
         body = self.stmt(s.body)
         loop = S.ForStmt(s.var, s.min, s.extent, s.kind, body, s.annotations)
         if s.kind != "pipelined" or int(s.annotations.get("num_stages", 0)) != 2:
             return loop
-        if s.annotations.get("order") or s.annotations.get("stage"):
+        if s.annotations.get("order") or s.annotations.get("stage") or s.annotations.get("quad"):
             return loop
         stmts = flatten_seq(body)
         gemms = [x for x in stmts if isinstance(x, S.TileOpStmt) and isinstance(x.op, O.GemmOp)]
@@ -142,12 +223,6 @@ class _KSplit(Mutator):
         cps = {c.op.dst.buffer: c.op for c in copies}
         if set(cps) != {A, B} or any(c.op.src.buffer.scope != "global" for c in copies):
             return loop
-        if self.quad and _quad_ok(g, cps, self.threads, self.target):
-            # whole-loop quadrant schedule (pipeline.py _quad_schedule): not K-split
-            self.quads += 1
-            ann = dict(s.annotations)
-            ann["quad"] = True
-            return S.ForStmt(s.var, s.min, s.extent, s.kind, body, ann)
         ka, kb = _k_dims(g)
         sa, sb = A.static_shape(), B.static_shape()
         if sa is None or sb is None or len(sa) != 2 or len(sb) != 2 or sa[ka] != 64 or sb[kb] != 64:
@@ -222,13 +297,13 @@ class _AllocSplit(Mutator):
         return s
 
 
-def split_gemm_k_halves(kernel: S.KernelStmt, mode=True, quad=False, threads=None, target=None) -> S.KernelStmt:
+def split_gemm_k_halves(kernel: S.KernelStmt, mode=True) -> S.KernelStmt:
     """``mode``: True, or "prio" to also raise the wave priority around each MFMA cluster.
-    ``quad``: loops that ``tl::gemm_quad_nt`` implements are marked for it instead of split."""
-    ks = _KSplit(mode, quad, threads, target)
+    Loops marked ``quad`` (mark_quad_loops) are left whole."""
+    ks = _KSplit(mode)
     k = ks.stmt(kernel)
     if not ks.applied:
-        return k if ks.quads else kernel
+        return kernel
     from .pipeline import _referenced_buffers
     used = _referenced_buffers(k)
     return _AllocSplit(ks.new_allocs, used, ks.pairs).stmt(k)

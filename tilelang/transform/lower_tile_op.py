@@ -1872,19 +1872,37 @@ class TileOpLowerer(Mutator):
         return S.SeqStmt(out)
 
     def lower_QuadGemmLoopOp(self, op):
-        """``tl::gemm_quad_nt``: the whole 256x256x64 NT main loop (transform/pipeline.py
-        _quad_schedule, tl/gemm_quad.h); the accumulator keeps tl::gemm_ss's register layout."""
+        """``tl::gemm_quad_nt_x``: the whole 256x256x64 NT main loop (transform/pipeline.py
+        _quad_schedule, tl/gemm_quad.h); the accumulators keep their GEMMs' register layouts."""
         ctx = self.ctx
-        args = []
-        for r, rdim in ((op.a, op.a_rdim), (op.b, op.b_rdim)):
-            sb = r.buffer
-            mins = [self.expr(m) for m in r.mins]
-            args.append(L.BufferPtr(ctx.flat_of(sb), ctx.flat_index(sb, mins)))
-            args.append(cast(self.expr(convert(sb.get_strides()[rdim])), _dt.int32))
-        args.append(cast(self.expr(convert(op.n)), _dt.int32))
-        args += [L.BufferPtr(ctx.flat_of(op.lds_a), 0), L.BufferPtr(ctx.flat_of(op.lds_b), 0),
-                 L.BufferPtr(ctx.local_of(op.C.buffer), 0), ctx.wave_expr()]
-        return S.SeqStmt([L.CallStmt("tl::gemm_quad_nt", args, [_dt.hip_type(op.a.buffer.dtype)])])
+
+        def ptr(r):
+            return L.BufferPtr(ctx.flat_of(r.buffer), ctx.flat_index(r.buffer, [self.expr(m) for m in r.mins]))
+
+        def i32(e):
+            return cast(self.expr(convert(e)), _dt.int32)
+
+        a, b = op.a.buffer, op.b.buffer
+        gather = op.idx is not None or op.row_mode
+        no_rows = call("extern", ["tl::quad::no_rows"], _dt.handle)
+        if op.idx is not None:  # row gather: tensor base + the tile's row list
+            mins = [IntImm(0)] + [self.expr(m) for m in op.a.mins[1:]]
+            a_ptr = L.BufferPtr(ctx.flat_of(a), ctx.flat_index(a, mins))
+            rows, row0, a_rows = ptr(op.idx), IntImm(0), i32(a.shape[0])
+        elif op.row_mode:  # dense rows row0.. range-checked against the tensor
+            mins = [IntImm(0)] + [self.expr(m) for m in op.a.mins[1:]]
+            a_ptr = L.BufferPtr(ctx.flat_of(a), ctx.flat_index(a, mins))
+            rows, row0, a_rows = no_rows, i32(op.a.mins[0]), i32(a.shape[0])
+        else:
+            a_ptr, rows, row0, a_rows = ptr(op.a), no_rows, IntImm(0), IntImm(0)
+        cl = L.BufferPtr(ctx.local_of(op.C.buffer), 0)
+        args = [a_ptr, i32(a.get_strides()[op.a_rdim]), rows, row0, a_rows, ptr(op.b), i32(b.get_strides()[op.b_rdim]),
+                i32(op.n), L.BufferPtr(ctx.flat_of(op.lds_a), 0), L.BufferPtr(ctx.flat_of(op.lds_b), 0),
+                L.BufferPtr(ctx.flat_of(op.lds_x if op.lds_x is not None else op.lds_a), 0), cl,
+                L.BufferPtr(ctx.local_of(op.Cx.buffer), 0) if op.Cx is not None else cl,
+                i32(op.m_limit) if op.m_limit is not None else IntImm(0x3fffffff), ctx.wave_expr()]
+        return S.SeqStmt([L.CallStmt("tl::gemm_quad_nt_x", args, [
+            _dt.hip_type(a.dtype), _b(gather), 32 if op.Cx is not None else 0])])
 
     def lower_async_small(self, op: AsyncCopyOp):
         """Small-tile DMA (pipeline._small_dma_plan): one 4-byte buffer LDS-DMA per wave; lane chunk

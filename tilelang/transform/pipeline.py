@@ -56,24 +56,31 @@ class AsyncCopyOp(O.TileOp):
 
 
 class QuadGemmLoopOp(O.TileOp):
-    """A whole 256x256x64 NT GEMM main loop as ``tl::gemm_quad_nt`` (tl/gemm_quad.h): ``a`` / ``b``
-    are the global tiles of the first K step (``rdim`` their row dims), ``lds_a`` / ``lds_b`` the
-    2-stage LDS rings, ``n`` the K-step count; ``C`` keeps the GEMM's fragment layout."""
+    """A whole 256x256x64 NT GEMM main loop as ``tl::gemm_quad_nt_x`` (tl/gemm_quad.h): ``a`` / ``b``
+    are the global tiles of the first K step (``a_rdim`` / ``b_rdim`` their row dims); ``idx`` the
+    row list of a gathered A (None: dense); ``lds_a`` / ``lds_b`` / ``lds_x`` the 2-stage LDS rings;
+    ``n`` the K-step count; ``C`` (and the extension's ``Cx``) keep their GEMMs' fragment layouts;
+    ``m_limit`` the main GEMM's valid_m (None: all rows)."""
     kind = "gemm_quad_loop"
 
-    def __init__(self, a: BufferRegion, a_rdim: int, b: BufferRegion, b_rdim: int, lds_a: Buffer, lds_b: Buffer,
-                 C: BufferRegion, n, gemm: O.GemmOp):
-        self.a, self.a_rdim, self.b, self.b_rdim = a, a_rdim, b, b_rdim
-        self.lds_a, self.lds_b, self.C, self.n, self.gemm = lds_a, lds_b, C, n, gemm
+    def __init__(self, a: BufferRegion, a_rdim: int, idx: Optional[BufferRegion], b: BufferRegion, b_rdim: int,
+                 lds_a: Buffer, lds_b: Buffer, lds_x: Optional[Buffer], C: BufferRegion, Cx: Optional[BufferRegion],
+                 n, m_limit=None, row_mode=False):
+        # row_mode: dense A whose row range is not provable -- rows from the tile's first row,
+        # range-checked against the tensor (tl::gemm_quad_nt_x GATHER with a null row list)
+        self.row_mode = row_mode
+        self.a, self.a_rdim, self.idx, self.b, self.b_rdim = a, a_rdim, idx, b, b_rdim
+        self.lds_a, self.lds_b, self.lds_x, self.C, self.Cx, self.n, self.m_limit = \
+            lds_a, lds_b, lds_x, C, Cx, n, m_limit
 
     def regions(self):
-        return [self.a, self.b, self.C]
+        return [r for r in (self.a, self.idx, self.b, self.C, self.Cx) if r is not None]
 
     def reads(self):
-        return [self.a, self.b, self.C]
+        return [r for r in (self.a, self.idx, self.b, self.C, self.Cx) if r is not None]
 
     def writes(self):
-        return [self.C]
+        return [r for r in (self.C, self.Cx) if r is not None]
 
 
 class GatherIndexOp(O.TileOp):
@@ -579,8 +586,8 @@ class PipelineInjector(Mutator):
             prologue.append(S.seq(*st) if nv is not None and nv > 0 else S.IfStmt(binop("<", 0, n), S.seq(*st)))
 
         consumer_stmts = [st for st in stmts if not any(st is p for p, _ in prods)]
-        if loop.annotations.get("quad") and nstages == 2 and not staged and len(asyncs) == 2:
-            q = _quad_schedule(self, loop, asyncs, consumer_stmts, newbufs)
+        if loop.annotations.get("quad") and nstages == 2 and not staged:
+            q = _quad_schedule(self, loop, asyncs, consumer_stmts, newbufs, rng)
             if q is not None:
                 return q
             _log.debug("quad GEMM loop %s: falling back to the generic pipeline", loop.var)
@@ -730,31 +737,66 @@ def _k_coeff(e, k) -> Optional[int]:
     return None
 
 
-def _quad_schedule(self, loop, asyncs, consumer_stmts, newbufs):
-    """The whole loop as ``tl::gemm_quad_nt`` (loops marked ``quad`` by gemm_ksplit): both tiles
-    plain in-bounds LDS-DMA copies whose K start advances by exactly 64 per step along the
-    contiguous dim, the GEMM the only consumer.  None: the generic pipeline handles the loop."""
-    if len(consumer_stmts) != 1 or not isinstance(consumer_stmts[0], S.TileOpStmt) or \
-            not isinstance(consumer_stmts[0].op, O.GemmOp):
+def _in_bounds(src: BufferRegion, ranges) -> bool:
+    """Every dim of ``src`` provably inside its buffer over ``ranges``."""
+    for d, (m, e) in enumerate(src.region):
+        b, s, ev = bound(m, ranges), as_int(src.buffer.shape[d]), as_int(e)
+        if b is None or s is None or ev is None or b[0] < 0 or b[1] + ev > s:
+            return False
+    return True
+
+
+def _quad_schedule(self, loop, asyncs, consumer_stmts, newbufs, ranges):
+    """The whole loop as ``tl::gemm_quad_nt_x`` (loops marked ``quad`` by gemm_ksplit.mark_quad_loops):
+    the operand tiles' K start advances by exactly 64 per step along the contiguous dim, plain
+    copies are provably in bounds (gathers are range-checked by the buffer resource), and the
+    GEMM (+ the MoE extension GEMM) are the only consumers.  None: the generic pipeline runs it."""
+    gemms = [st.op for st in consumer_stmts if isinstance(st, S.TileOpStmt) and isinstance(st.op, O.GemmOp)]
+    if len(gemms) != len(consumer_stmts) or len(gemms) not in (1, 2):
         return None
-    g = consumer_stmts[0].op
+    g = [x for x in gemms if x.A.buffer.static_shape() == [256, 64]]
+    if len(g) != 1:
+        return None
+    g = g[0]
+    x = next((o for o in gemms if o is not g), None)
     k = loop.var
     tiles = {}
     for p, src, plan in asyncs:
-        if not isinstance(p.op, O.CopyOp) or plan.get("gather") or plan.get("small") or plan.get("oob_bytes") or \
-                plan.get("dup") or plan["rdim"] is None:
+        gather = isinstance(p.op, O.GatherRowsOp)
+        if not gather and (plan.get("gather") or plan.get("rdim") is None):
+            return None
+        rdim = p.op.row_dim if gather else plan["rdim"]
+        if not gather and not _in_bounds(src, ranges):
+            # only the outermost (row) dim unproven: rows past the tensor read zeros, as the
+            # generic pipeline's out-of-range LDS-DMA (the template's range-checked row mode)
+            if rdim != 0 or not _in_bounds(BufferRegion(src.buffer, [(IntImm(0), src.region[0][1])] +
+                                                        list(src.region[1:])), ranges):
+                return None
+            gather = "rows"
+        cdim = len(src.region) - 1
+        if as_int(src.buffer.get_strides()[cdim]) != 1:
             return None
         for d, (m, _) in enumerate(src.region):
-            if _k_coeff(m, k) != (64 if d == plan["cdim"] else 0):
+            if _k_coeff(m, k) != (64 if d == cdim else 0):
                 return None
-        tiles[p.op.dst.buffer] = (_subst_region(src, {k: loop.min}), plan["rdim"])
+        idx = _subst_region(p.op.idx, {k: loop.min}) if gather is True else None
+        if idx is not None and any(v is k for m, _ in idx.region for v in free_vars(m)):
+            return None
+        tiles[p.op.dst.buffer] = (_subst_region(src, {k: loop.min}), rdim, idx, gather)
     A, B = g.A.buffer, g.B.buffer
-    if set(tiles) != {A, B}:
+    want = {A, B} | ({x.A.buffer} if x is not None else set())
+    if set(tiles) != want or tiles[B][3]:
         return None
-    op = QuadGemmLoopOp(tiles[A][0], tiles[A][1], tiles[B][0], tiles[B][1], newbufs[A], newbufs[B], g.C,
-                        loop.extent, g)
+    a_src, a_rdim, idx, a_mode = tiles[A]
+    if x is not None and tiles[x.A.buffer][3] != a_mode:
+        return None
+    if a_mode and a_rdim != 0:
+        return None
+    op = QuadGemmLoopOp(a_src, a_rdim, idx, tiles[B][0], tiles[B][1], newbufs[A], newbufs[B],
+                        newbufs[x.A.buffer] if x is not None else None, g.C, x.C if x is not None else None,
+                        loop.extent, getattr(g, "valid_m", None), row_mode=a_mode == "rows")
     self.replaced = getattr(self, "replaced", {})
-    for Bf in (A, B):
+    for Bf in want:
         lst = self.replaced.setdefault(Bf, [])
         if newbufs[Bf] not in lst:
             lst.append(newbufs[Bf])
