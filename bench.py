@@ -41,8 +41,12 @@ REF_ATTN_TF = 497.13
 PEAK_BF16_TF = 2500.0  # MI355X dense fp16/bf16 MFMA (AMD spec, no sparsity)
 
 # staged_epilogue: C tile through LDS, row-contiguous 16-byte stores (+3-4 % cold, profiles/r2/session2/gemm_epi_ab.log)
+# trans_B: B stored [N, K], the layout of the reference's benchmark/matmul/benchmark_matmul.py:163,209
+# (the fp16 GEMM headline); its main loop is tl::gemm_quad_nt_x (tl/gemm_quad.h), 1179 -> 1311 TF
+# over the K-half schedule at 4096^3 (profiles/r5/gemm_quad_ab1.log).  The vendor normaliser below
+# runs the same layout (torch.matmul(A, B.T), hipBLASLt's NT kernel)
 GEMM_CFG = dict(M=4096, N=4096, K=4096, block_M=256, block_N=256, block_K=64, threads=512, num_stages=2,
-                staged_epilogue=True)
+                staged_epilogue=True, trans_B=True)
 # FA (scripts/sweep_fa.py, profiles/r2/fa_staged.log): 256x64 tile, 8 waves, Q in registers, 2-stage K/V
 # ring, T.Pipelined(order, stage) schedule: QK^T(t) | rescale+PV(t-1) | softmax(t)
 # sum_mfma: softmax row sums on the matrix cores (P x ones), +1.7-2 % (profiles/r3/s3/fa_sum_mfma_ab.log)
@@ -87,11 +91,13 @@ def build_gemm(device="cuda", g=None):
     import tilelang
     from example_gemm import matmul
     g = g or GEMM_CFG
+    tb = g.get("trans_B", False)
     f = matmul.get_tir(g["M"], g["N"], g["K"], g["block_M"], g["block_N"], g["block_K"], g["threads"],
-                       g["num_stages"], "float16", staged_epilogue=g.get("staged_epilogue", False))
+                       g["num_stages"], "float16", trans_B=tb, staged_epilogue=g.get("staged_epilogue", False))
     k = tilelang.compile(f, out_idx=[-1], target=_target(device))
     A = torch.randn(g["M"], g["K"], device=device).to(torch.float16)
-    B = torch.randn(g["K"], g["N"], device=device).to(torch.float16)
+    B = torch.randn(g["N"], g["K"], device=device).to(torch.float16) if tb else \
+        torch.randn(g["K"], g["N"], device=device).to(torch.float16)
     return k, (A, B)
 
 
@@ -170,6 +176,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-moe", action="store_true", help="time GEMM + attention only")
+    ap.add_argument("--gemm-nn", action="store_true",
+                    help="B [K, N] for the GEMM phase (the layout before round 5; A/B only)")
     ap.add_argument("--prewarm-ms", type=float, default=None,
                     help="untimed, time-based pre-warm before the --warmup steps (default 300 ms on a GPU): the "
                          "MI355X clocks ramp over the first ~20 ms of dense MFMA work after idle (per-step "
@@ -213,6 +221,8 @@ def main():
 
     torch.manual_seed(1234)  # identical expert weights on every rank (EP slices them)
     g, a_, m = (TINY["gemm"], TINY["attn"], TINY["moe"]) if cpu else (GEMM_CFG, ATTN_CFG, MOE_CFG)
+    if args.gemm_nn:
+        g = dict(g, trans_B=False)
     gemm, (A, B) = build_gemm(dev, g)
     attn, (Q, K, V) = build_attn(dev, a_)
     moe = None
@@ -228,7 +238,8 @@ def main():
     step = max(1, g["M"] // 64)
     i64 = torch.arange(min(64, g["M"]), device=A.device)
     rows = i64 * step + (i64 * 37) % step  # one row per 64-row band, at a varying offset inside it
-    ref = A[rows].float() @ B.float()
+    Bkn = B.T if g.get("trans_B", False) else B  # [K, N] view
+    ref = A[rows].float() @ Bkn.float()
     if not torch.allclose(C[rows].float(), ref, rtol=2e-2, atol=2e-1):
         raise SystemExit("GEMM result check failed")
     O = attn(Q, K, V)
@@ -364,8 +375,8 @@ def main():
     # box-speed normaliser: the vendor library (hipBLASLt via torch.matmul) on the same fp16 GEMM,
     # same process, same clocks; the driver-vs-builder gap of a run can be read against it
     for _ in range(3):  # hipBLASLt loads and selects its kernel on the first calls
-        torch.matmul(A, B)
-    vendor_ms = timed(lambda: torch.matmul(A, B), reps)
+        torch.matmul(A, Bkn)
+    vendor_ms = timed(lambda: torch.matmul(A, Bkn), reps)
     dev_id = -1 if cpu else torch.cuda.current_device()
     bus = "cpu" if cpu else str(getattr(torch.cuda.get_device_properties(dev_id), "pci_bus_id", dev_id))
     ids = [None] * world
@@ -429,6 +440,7 @@ def main():
             "step_ms_min": round(min(step_ms), 4) if step_ms else None,
             "step_ms_rank0": [round(x, 3) for x in step_ms],
             "gemm_dtype": "float16",
+            "gemm_layout": "NT (B [N, K])" if g.get("trans_B", False) else "NN (B [K, N])",
             "attn_dtype": "bfloat16",
             "moe_dtype": "bfloat16",
             "device": args.device,

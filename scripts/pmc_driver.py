@@ -1,6 +1,6 @@
 """Run one bench kernel (the headline GEMM or FA) N times for a rocprofv3 --pmc pass.
 
-    rocprofv3 --pmc <counters> -- python3 scripts/pmc_driver.py gemm|gemm_nt|fa|fa32 [iters]
+    rocprofv3 --pmc <counters> -- python3 scripts/pmc_driver.py gemm|gemm_nt|hipblaslt_nt|fa|fa32 [iters]
 """
 import os
 import sys
@@ -19,20 +19,25 @@ def main():
     which = sys.argv[1]
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     torch.manual_seed(0)
-    if which == "gemm":
+    if which == "gemm":  # B [K, N] ("NN")
         from example_gemm import matmul
-        g = bench.GEMM_CFG
+        g = dict(bench.GEMM_CFG, trans_B=False)
         k = matmul(**g)
         a = torch.randn(g["M"], g["K"], device="cuda").half()
         b = torch.randn(g["K"], g["N"], device="cuda").half()
         fn = lambda: k(a, b)  # noqa: E731
     elif which == "gemm_nt":  # B given as [N, K] (K-contiguous, "NT"), the bench's tile config
         from example_gemm import matmul
-        g = dict(bench.GEMM_CFG)
-        k = matmul(**g, trans_B=True)
+        g = dict(bench.GEMM_CFG, trans_B=True)
+        k = matmul(**g)
         a = torch.randn(g["M"], g["K"], device="cuda").half()
         b = torch.randn(g["N"], g["K"], device="cuda").half()
         fn = lambda: k(a, b)  # noqa: E731
+    elif which == "hipblaslt_nt":  # the vendor library on the same NT problem
+        g = bench.GEMM_CFG
+        a = torch.randn(g["M"], g["K"], device="cuda").half()
+        b = torch.randn(g["N"], g["K"], device="cuda").half()
+        fn = lambda: a @ b.T  # noqa: E731
     elif which == "fa":  # the bench's attention kernel, exactly as bench.py builds it
         k, (q, kk, v) = bench.build_attn("cuda")
         fn = lambda: k(q, kk, v)  # noqa: E731

@@ -34,11 +34,13 @@ def parse(v):
 
 
 def build(M, N, K, defines, src_file="gemm_8ph.hip", nn=False):
-    f = matmul.get_tir(M, N, K, 256, 256, 64, 512, 2, "float16", trans_B=not nn, staged_epilogue=True)
+    threads = 256 if src_file.startswith("gemm_4") else 512  # the 4-wave prototypes
+    f = matmul.get_tir(M, N, K, 256, 256, 64, threads, 2, "float16", trans_B=not nn, staged_epilogue=True)
     if defines is None:
         callback.unregister()
         return tilelang.compile(f, out_idx=[-1], target="hip")
     src = open(os.path.join(HERE, src_file)).read()
+    src = src.replace('#include "agpr_mfma.h"', open(os.path.join(HERE, "agpr_mfma.h")).read())
     head = "".join(f"#define {d[2:].replace('=', ' ', 1)}\n" for d in defines.split())
     head += f"#define GM {M}\n#define GN {N}\n#define GK {K}\n"
     callback.register_hip_postproc(lambda code, target: head + src)

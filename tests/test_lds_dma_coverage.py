@@ -15,7 +15,8 @@ import tilelang  # noqa: E402
 
 
 def _counts(src):
-    return len(re.findall(r"tl::(?:glds16|buffer_lds16)\(", src)), len(re.findall(r"\bstage\d+\[", src))
+    # tl::gemm_quad_nt_x (tl/gemm_quad.h) stages both operands by buffer LDS-DMA inside the template
+    return len(re.findall(r"tl::(?:glds16|buffer_lds16|gemm_quad_nt_x<)", src)), len(re.findall(r"\bstage\d+\[", src))
 
 
 def _hip(jf, *a, **kw):

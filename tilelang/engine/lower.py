@@ -18,6 +18,7 @@ current stream.
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -123,7 +124,8 @@ def _lower_one(func, kernel: S.KernelStmt, target: Target, cfg, name: str, timin
         from ..transform.storage_rewrite import rewrite_local_storage
         # local arrays with disjoint lifetimes share storage (+ element-wise in-place reuse if asked)
         kernel, _ = rewrite_local_storage(kernel, bool(cfg.get("tl.storage_rewrite_detect_inplace")))
-    if target.kind == "hip" and cfg.get("tl.gemm_quad", True) is not False:
+    quad_default = os.environ.get("TL_GEMM_QUAD", "1") != "0"  # process-wide A/B switch
+    if target.kind == "hip" and cfg.get("tl.gemm_quad", quad_default) is not False:
         from ..transform.gemm_ksplit import mark_quad_loops
         kernel = mark_quad_loops(kernel, T, target)  # 256x256x64 NT loops -> tl::gemm_quad_nt_x
     phased = cfg.get("tl.gemm_phased")

@@ -37,7 +37,8 @@ TL_DEVICE const int* no_rows() { return nullptr; }  // dense A: no row list
 TL_DEVICE int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 template <typename P> TL_DEVICE P* uni_ptr(P* p) {
   const unsigned long long v = (unsigned long long)p;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
   return (P*)(((unsigned long long)hi << 32) | lo);
 }
 

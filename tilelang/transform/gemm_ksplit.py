@@ -128,7 +128,8 @@ def quad_loop_ok(stmts, threads, target) -> bool:
         return plan.get("warp_m") == wm and plan.get("warp_n") == wn and tuple(plan.get("mfma") or ()) == (16, 16, 32)
 
     A, B = g.A.buffer, g.B.buffer
-    if not plain(g) or B.static_shape() != [256, 64] or A.dtype not in (_dt.float16, _dt.bfloat16) or B.dtype != A.dtype:
+    if not plain(g) or B.static_shape() != [256, 64] or A.dtype not in (_dt.float16, _dt.bfloat16) or \
+            B.dtype != A.dtype:
         return False
     if not warps(g, 4, 2):
         return False
