@@ -29,6 +29,12 @@
 #ifndef B1
 #define B1 0
 #endif
+#ifndef YPRIO
+#define YPRIO 0  // 1: waves 4-7 at issue priority 1 for the whole kernel (guide T5 static form)
+#endif
+#ifndef MERGE
+#define MERGE 0  // 1: two barriers per K tile (phases paired), A0/B0 restaged after the pair
+#endif
 #ifndef RPIPE
 #define RPIPE 0  // 1: fragments read one phase ahead (quadrant order alternating by tile parity)
 #endif
@@ -188,6 +194,9 @@ extern "C" __global__ void __launch_bounds__(512) gemm_kernel(half_t* __restrict
   // ONE B piece in registers; slots are restaged after their last read: P0 B1 of tile t+1,
   // P1 A0, P2 B0, P3 A1 of tile t+2
   F fa0[2][2], fa1[2][2], fb[4][2];
+#if YPRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
 #if RPIPE
   F fb1[4][2];
 #endif
@@ -201,9 +210,10 @@ extern "C" __global__ void __launch_bounds__(512) gemm_kernel(half_t* __restrict
       if ((T) + 1 < NT) stage((BUF) ^ 1, 3, (T) + 1);                                             \
     } else if constexpr (P == 1) {                                                                \
       read_a<SB + 1 * HALF>(smem, fa1, wm, lrow, cx);                                             \
-      if ((T) + 2 < NT) stage(BUF, 0, (T) + 2);                                                   \
+      if (!MERGE && (T) + 2 < NT) stage(BUF, 0, (T) + 2);                                         \
     } else if constexpr (P == 2) {                                                                \
       read_b<SB + 3 * HALF>(smem, fb, wn, lane, lrow, cx);                                        \
+      if (MERGE && (T) + 2 < NT) stage(BUF, 0, (T) + 2);                                          \
       if ((T) + 2 < NT) stage(BUF, 2, (T) + 2);                                                   \
     } else {                                                                                      \
       if ((T) + 2 < NT) stage(BUF, 1, (T) + 2);                                                   \
@@ -217,7 +227,7 @@ extern "C" __global__ void __launch_bounds__(512) gemm_kernel(half_t* __restrict
       if ((T) + 2 < NT) tl::wait_vmcnt<6>();                                                      \
       else if ((T) + 1 < NT) tl::wait_vmcnt<0>();                                                 \
     }                                                                                             \
-    bar();                                                                                        \
+    if (!MERGE || P == 1 || P == 3) bar();                                                        \
   }
 
 #else

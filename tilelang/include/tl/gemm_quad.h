@@ -15,10 +15,10 @@
 //     {wm*64 + qa*32 + r} (four 32-row groups), B half qb = block cols {wn*128 + qb*64 + c}
 //     (two 64-col groups), gathered by the per-lane LDS-DMA source address; 16-byte chunks are
 //     XOR-swizzled by (row >> 1) & 7, conflict-free for the ds_read_b128 operand pattern.
-//   * quadrant order (0,0) (1,0) (1,1) (0,1) reads A0+B0 / A1 / B1 / nothing; each phase
-//     restages ONE half-tile into a slot whose last read was in an earlier phase (P0: B1 of
-//     tile t+1; P1-P3: A0 / B0 / A1 of tile t+2) and one counted vmcnt(6) per K tile keeps three
-//     half-tiles in flight across the raw barriers.
+//   * quadrant order (0,0) (1,0) (1,1) (0,1) reads A0+B0 / A1 / B1 / nothing; a barrier after
+//     the second and the fourth phase; each half-tile is restaged into a slot whose last read
+//     precedes the barrier just passed (B1 of tile t+1 in phase 0; A0, B0, A1 of tile t+2 in
+//     phases 2-3), and one counted vmcnt(6) per K tile keeps three half-tiles in flight.
 // Requirements (checked by the pass): A [.., K] and B [.., K] K-contiguous global tensors with
 // the whole 256 x (64 n_tiles) blocks in bounds, 16-bit elements, 512 threads.
 #pragma once
@@ -210,7 +210,9 @@ TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __res
 
   F fa0[2][2], fa1[2][2], fb[4][2];
   // quadrant order (0,0) (1,0) (1,1) (0,1) -- reads A0+B0 / A1 (+ extension) / B1 / nothing;
-  // restaging: P0 B1 of tile t+1, P1 A0, P2 B0 (+ extension), P3 A1 of tile t+2
+  // a barrier after P1 and after P3 only (two per K tile: +2 % over one per phase,
+  // profiles/r5/proto_8pb_merge.log); restaging after the barrier that retires a slot's reads:
+  // P0 B1 of tile t+1, P2 A0 + B0 (+ extension), P3 A1 of tile t+2
 #define TL_QUAD_PHASE(BUF, P, T_)                                                              \
   {                                                                                            \
     constexpr int SA = (BUF) * 2 * HALF;                                                       \
@@ -223,7 +225,6 @@ TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __res
       if constexpr (LIVE_) mma<T, 0, 0>(fa0, fb, acc);                                                    \
     } else if constexpr (P == 1) {                                                             \
       if constexpr (LIVE_) read_a<T, SA + HALF>(lds_a, fa1, wm, lrow, cx);                                \
-      if ((T_) + 2 < NT) stage(BUF, 0, (T_) + 2);                                              \
       if constexpr (LIVE_) mma<T, 1, 0>(fa1, fb, acc);                                                    \
       if constexpr (EXT > 0) {                                                                 \
         if constexpr (XLIVE_) {                                                                           \
@@ -245,6 +246,7 @@ TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __res
     } else if constexpr (P == 2) {                                                             \
       if constexpr (LIVE_) read_b<T, SA + HALF>(lds_b, fb, wn, lrow, cx);                                 \
       if ((T_) + 2 < NT) {                                                                     \
+        stage(BUF, 0, (T_) + 2);                                                               \
         stage(BUF, 2, (T_) + 2);                                                               \
         stage_x(BUF, (T_) + 2);                                                                \
       }                                                                                        \
@@ -255,7 +257,7 @@ TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __res
       if ((T_) + 2 < NT) wait_vmcnt<6 + XW>();                                                 \
       else if ((T_) + 1 < NT) wait_vmcnt<0>();                                                 \
     }                                                                                          \
-    bar();                                                                                     \
+    if constexpr (P == 1 || P == 3) bar();                                                     \
   }
 
 #define TL_QUAD_LOOP(L_, X_)                                                                   \
