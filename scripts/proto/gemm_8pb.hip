@@ -32,6 +32,9 @@
 #ifndef YPRIO
 #define YPRIO 0  // 1: waves 4-7 at issue priority 1 for the whole kernel (guide T5 static form)
 #endif
+#ifndef SINGLE
+#define SINGLE 0  // 1: one barrier per K tile, the whole next tile staged in phase 0 (classic 2-stage)
+#endif
 #ifndef MERGE
 #define MERGE 0  // 1: two barriers per K tile (phases paired), A0/B0 restaged after the pair
 #endif
@@ -178,6 +181,13 @@ extern "C" __global__ void __launch_bounds__(512) gemm_kernel(half_t* __restrict
   stage(1, 3, 1);
   tl::wait_vmcnt<8>();
   bar();
+#elif SINGLE
+  stage(0, 0, 0);
+  stage(0, 2, 0);
+  stage(0, 1, 0);
+  stage(0, 3, 0);
+  tl::wait_vmcnt<0>();
+  bar();
 #else
   stage(0, 0, 0);
   stage(0, 2, 0);
@@ -207,16 +217,21 @@ extern "C" __global__ void __launch_bounds__(512) gemm_kernel(half_t* __restrict
     if constexpr (P == 0) {                                                                       \
       read_a<SB + 0 * HALF>(smem, fa0, wm, lrow, cx);                                             \
       read_b<SB + 2 * HALF>(smem, fb, wn, lane, lrow, cx);                                        \
-      if ((T) + 1 < NT) stage((BUF) ^ 1, 3, (T) + 1);                                             \
+      if (SINGLE) {                                                                               \
+        if ((T) + 1 < NT) {                                                                       \
+          stage((BUF) ^ 1, 0, (T) + 1); stage((BUF) ^ 1, 2, (T) + 1);                             \
+          stage((BUF) ^ 1, 1, (T) + 1); stage((BUF) ^ 1, 3, (T) + 1);                             \
+        }                                                                                         \
+      } else if ((T) + 1 < NT) stage((BUF) ^ 1, 3, (T) + 1);                                      \
     } else if constexpr (P == 1) {                                                                \
       read_a<SB + 1 * HALF>(smem, fa1, wm, lrow, cx);                                             \
-      if (!MERGE && (T) + 2 < NT) stage(BUF, 0, (T) + 2);                                         \
+      if (!SINGLE && !MERGE && (T) + 2 < NT) stage(BUF, 0, (T) + 2);                              \
     } else if constexpr (P == 2) {                                                                \
       read_b<SB + 3 * HALF>(smem, fb, wn, lane, lrow, cx);                                        \
-      if (MERGE && (T) + 2 < NT) stage(BUF, 0, (T) + 2);                                          \
-      if ((T) + 2 < NT) stage(BUF, 2, (T) + 2);                                                   \
+      if (!SINGLE && MERGE && (T) + 2 < NT) stage(BUF, 0, (T) + 2);                               \
+      if (!SINGLE && (T) + 2 < NT) stage(BUF, 2, (T) + 2);                                        \
     } else {                                                                                      \
-      if ((T) + 2 < NT) stage(BUF, 1, (T) + 2);                                                   \
+      if (!SINGLE && (T) + 2 < NT) stage(BUF, 1, (T) + 2);                                        \
     }                                                                                             \
     if (B1) bar();                                                                                \
     if constexpr (P == 0) mma<0, 0>(fa0, fb, acc);                                                \
@@ -224,10 +239,11 @@ extern "C" __global__ void __launch_bounds__(512) gemm_kernel(half_t* __restrict
     else if constexpr (P == 2) mma<1, 1>(fa1, fb, acc);                                           \
     else mma<0, 1>(fa0, fb, acc);                                                                 \
     if constexpr (P == 3) {                                                                       \
-      if ((T) + 2 < NT) tl::wait_vmcnt<6>();                                                      \
+      if (SINGLE) tl::wait_vmcnt<0>();                                                            \
+      else if ((T) + 2 < NT) tl::wait_vmcnt<6>();                                                 \
       else if ((T) + 1 < NT) tl::wait_vmcnt<0>();                                                 \
     }                                                                                             \
-    if (!MERGE || P == 1 || P == 3) bar();                                                        \
+    if (SINGLE ? P == 3 : (!MERGE || P == 1 || P == 3)) bar();                                    \
   }
 
 #else

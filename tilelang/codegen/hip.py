@@ -201,6 +201,11 @@ class CodeGen:
             return f"tl::floormod({a}, {b})"
         if op in ("&&", "||"):
             return f"({a} {op} {b})"
+        if op == "/" and self.fast_math and not self.is_cpu and x.dtype.is_float and x.dtype.bits == 32:
+            # fast math: a * v_rcp_f32(b) (1 ulp) instead of the IEEE division sequence
+            # (v_div_scale / v_div_fmas / v_div_fixup, ~10 instructions) -- nvcc -use_fast_math's
+            # __fdividef; e.g. the SwiGLU x / (1 + exp(-x)) epilogue of the MoE up projection
+            return f"({a} * __builtin_amdgcn_rcpf({b}))"
         return f"({a} {op} {b})"
 
     def _nt(self, buf) -> bool:

@@ -209,6 +209,9 @@ TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __res
   bar();
 
   F fa0[2][2], fa1[2][2], fb[4][2];
+  // the younger half of the workgroup (waves 4-7) at issue priority 1 for the loop (guide T5
+  // static form: +0.5 %, profiles/r5/proto_8pb_single.log)
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
   // quadrant order (0,0) (1,0) (1,1) (0,1) -- reads A0+B0 / A1 (+ extension) / B1 / nothing;
   // a barrier after P1 and after P3 only (two per K tile: +2 % over one per phase,
   // profiles/r5/proto_8pb_merge.log); restaging after the barrier that retires a slot's reads:
@@ -284,6 +287,7 @@ TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __res
   }
 #undef TL_QUAD_LOOP
 #undef TL_QUAD_PHASE
+  __builtin_amdgcn_s_setprio(0);
 }
 
 // Dense form: A = element (m0, 0) of the block's rows (row stride lda), B = element (n0, 0)
