@@ -359,3 +359,18 @@ def test_router_k_split_matches_fused(monkeypatch):
     ids1, w1 = K.route(x, g, 2)
     assert torch.equal(ids0, ids1)
     torch.testing.assert_close(w0, w1)
+
+
+@pytest.mark.gpu
+def test_router_wide_matches_fused(monkeypatch):
+    """router_wide_kernel (K chunks side by side in one tile GEMM, the default on gfx950) picks the
+    same experts with the same weights as the fused one-wave router."""
+    from tilelang.ops import moe as K
+    torch.manual_seed(0)
+    x = torch.randn(512, 2048, device="cuda").to(torch.bfloat16)
+    g = (torch.randn(8, 2048, device="cuda") * 0.05).to(torch.bfloat16)
+    ids0, w0 = K.route(x, g, 2)
+    monkeypatch.setattr(K, "ROUTER_WIDE", False)
+    ids1, w1 = K.route(x, g, 2)
+    assert torch.equal(ids0, ids1)
+    torch.testing.assert_close(w0, w1)

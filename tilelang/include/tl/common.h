@@ -93,6 +93,11 @@ template <typename T, int N> TL_DEVICE void load_vec(T (&vals)[N], const T* src)
 // thread / wave identity (wave64)
 // ---------------------------------------------------------------------------
 TL_DEVICE int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+// wave-vote helpers (a __ballot mask): set lanes, and set lanes below this one
+TL_DEVICE int popc64(unsigned long long m) { return __builtin_popcountll(m); }
+TL_DEVICE int mbcnt64(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
 TL_DEVICE int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 // ---------------------------------------------------------------------------

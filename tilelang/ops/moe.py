@@ -191,7 +191,82 @@ def router_logits_sk_kernel(n_tok: int, H: int, E: int, dtype: str, target: str,
     return tilelang.compile(moe_router_logits_sk, out_idx=None, target=target)
 
 
+@functools.lru_cache(maxsize=None)
+def router_wide_kernel(n_tok: int, H: int, E: int, topk: int, dtype: str, target: str, block_T: int = 8, kc: int = 4,
+                       block_K: int = 128, num_stages: int = 4, threads: int = 512):
+    """Router with the K dimension spread over ``kc`` chunks that run side by side in ONE tile
+    GEMM (the fused router streams a token block's whole ``H`` through a single wave: 128
+    latency-bound waves on the chip for the bench layer, ~9 us).  With x viewed as
+    ``[n_tok * kc, H / kc]`` (row ``t * kc + c`` = chunk c of token t) and the padded gate as
+    ``[Ep * kc, H / kc]`` (row ``e * kc + c``), P = x' Wg'^T holds every (token chunk, expert
+    chunk) product and the logit is the sum of its ``kc`` matching-chunk entries
+    ``P[t*kc + c, e*kc + c]`` -- kc times the (tiny) MFMA work, but ``block_T * kc`` rows of x in
+    flight per workgroup on 8 waves and ``n_tok / block_T`` workgroups.  Logits are rounded to the
+    activation dtype and the top-k / softmax rule is ``router_topk_kernel``'s.  Defaults from
+    scripts/router_wide_probe.py (bench layer 2048 x 4096 x 8, cold): 9.8 us vs 12.0 us fused, ids
+    identical (profiles/r5/router_wide2.log).
+    kernel(x [n_tok * kc, H / kc], Wg [Ep * kc, H / kc], ids, w)."""
+    Ep = max(16, -(-E // 16) * 16)
+    Hc = H // kc
+    R, Rw = block_T * kc, Ep * kc
+    assert H % kc == 0 and Hc % block_K == 0 and n_tok % block_T == 0 and R % 16 == 0
+
+    @T.prim_func
+    def moe_router_wide(X: T.Tensor((n_tok * kc, Hc), dtype), Wg: T.Tensor((Rw, Hc), dtype),
+                        ids: T.Tensor((n_tok, topk), "int32"), w: T.Tensor((n_tok, topk), "float32")):
+        with T.Kernel(n_tok // block_T, threads=threads) as bx:
+            X_s = T.alloc_shared((R, block_K), dtype)
+            W_s = T.alloc_shared((Rw, block_K), dtype)
+            P = T.alloc_fragment((R, Rw), "float32")
+            P_s = T.alloc_shared((R, Rw), "float32")
+            L_s = T.alloc_shared((block_T, Ep), "float32")
+            T.clear(P)
+            for k in T.Pipelined(Hc // block_K, num_stages=num_stages):
+                T.copy(X[bx * R, k * block_K], X_s)
+                T.copy(Wg[0, k * block_K], W_s)
+                T.gemm(X_s, W_s, P, transpose_B=True)
+            T.copy(P, P_s)
+            for i, e in T.Parallel(block_T, Ep):
+                acc = T.alloc_var("float32")
+                acc = 0.0
+                for c in T.serial(kc):
+                    acc = acc + P_s[i * kc + c, e * kc + c]
+                L_s[i, e] = T.Cast("float32", T.Cast(dtype, acc))
+            for i in T.Parallel(64):
+                v = T.alloc_local((Ep,), "float32")
+                sel = T.alloc_local((topk,), "int32")
+                p = T.alloc_local((topk,), "float32")
+                best = T.alloc_var("float32")
+                bi = T.alloc_var("int32")
+                tot = T.alloc_var("float32")
+                if i < block_T:
+                    for e in T.serial(E):
+                        v[e] = L_s[i, e]
+                    for kk in T.serial(topk):
+                        best = -T.infinity("float32")
+                        bi = 0
+                        for e in T.serial(E):
+                            if v[e] > best:
+                                best = v[e]
+                                bi = e
+                        sel[kk] = bi
+                        p[kk] = best
+                        v[bi] = -T.infinity("float32")
+                    tot = 0.0
+                    best = p[0]
+                    for kk in T.serial(topk):
+                        p[kk] = T.exp(p[kk] - best)
+                        tot = tot + p[kk]
+                    for kk in T.serial(topk):
+                        ids[bx * block_T + i, kk] = sel[kk]
+                        w[bx * block_T + i, kk] = p[kk] / tot
+
+    return tilelang.compile(moe_router_wide, out_idx=None, target=target)
+
+
 ROUTER_SPLITS = int(__import__("os").environ.get("TL_MOE_ROUTER_SPLITS", "0"))  # 0: the fused one-pass router
+# the wide router (router_wide_kernel) for the shapes it takes; TL_MOE_ROUTER_WIDE=0: the fused one
+ROUTER_WIDE = __import__("os").environ.get("TL_MOE_ROUTER_WIDE", "1") != "0"
 
 
 _GATE_PAD = {}
@@ -220,7 +295,7 @@ def max_padded_rows(n_assign: int, E: int, block_M: int) -> int:
 
 @functools.lru_cache(maxsize=None)
 def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: str, stable: bool = False,
-                 threads: int = 1024, full_first: bool = True, even: bool = False):
+                 threads: int = 1024, full_first: bool = True, even: bool = False, vote: Optional[bool] = None):
     """Dispatch plan of ``n`` assignments (``expert_ids[n]``; assignment ``j`` reads source row
     ``j // div``; a negative id is an empty slot: not placed, ``dest[j] = -1``): ``dest[j]`` (its
     padded row), ``row_src[max_rows]``, ``tile_expert``, ``counts[E]``,
@@ -229,8 +304,8 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
     One workgroup.  ``stable=False``: rows of one expert are placed in LDS-atomic order (each
     row's result is independent of its position, so the layer output does not depend on it).
     ``stable=True``: assignment order is kept inside every expert (per-thread runs + a scan of
-    the per-thread counts) — identical placement on every rank, which the tensor-parallel
-    in-kernel reduction needs.
+    the per-thread counts; on gfx950 ``vote``: per-wave ballot counts + a scan over the waves) —
+    identical placement on every rank, which the tensor-parallel in-kernel reduction needs.
 
     ``full_first``: every expert's FULL row tiles come first (expert order), then one partial tile
     per expert with a remainder.  The tail-balanced expert GEMM runs the leading units as whole
@@ -245,10 +320,16 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
     full tiles plus a 17-row tile that costs a whole extra round."""
     if even:
         full_first = False
+    if vote is None:
+        # measured (scripts/align_probe.py, profiles/r5/align_probe3.log): the vote form keeps
+        # assignment order at 12.4 us vs 27.8 us for the per-thread-run stable form; the unordered
+        # LDS-atomic form stays the default (11.3 vs 12.3 us)
+        vote = target == "hip" and stable
     n_tiles = max_rows // block_M
-    if stable:
+    if stable and not vote:
         threads = 256
     c = -(-n // threads)
+    nw = threads // 64
 
     def _units(c):  # row tiles of an expert with c rows
         return (c + block_M - 1) // block_M
@@ -274,7 +355,35 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
             start = T.alloc_shared((E + 1,), "int32")
             fill = T.alloc_shared((E,), "int32")
             acc = T.alloc_var("int32")
-            if stable:
+            if vote:
+                # wave votes (gfx950): wave w owns the c*64 consecutive assignments from w*c*64, its
+                # lanes cover 64 at a time; per expert the wave counts its lanes with a ballot, an
+                # exclusive scan over the waves gives each wave its offset, and a lane's slot is
+                # offset + the wave's running count + the set lanes below it -- assignment order
+                # inside every expert (stable) and no LDS atomics
+                wc = T.alloc_shared((nw, E), "int32")
+                for t in T.Parallel(threads):
+                    tot = T.alloc_local((E,), "int32")
+                    for e in T.serial(E):
+                        tot[e] = 0
+                    for it in T.serial(c):
+                        j = (t // 64) * (c * 64) + it * 64 + t % 64
+                        idv = T.alloc_var("int32")
+                        idv = T.if_then_else(j < n, expert_ids[T.min(j, n - 1)], -1)
+                        for e in T.serial(E):
+                            tot[e] = tot[e] + T.call_extern("int32", "tl::popc64", T.ballot(idv == e))
+                    if t % 64 == 0:
+                        for e in T.serial(E):
+                            wc[t // 64, e] = tot[e]
+                for e in T.Parallel(E):
+                    acc = 0
+                    for w_ in T.serial(nw):
+                        cq = T.alloc_var("int32")
+                        cq = wc[w_, e]
+                        wc[w_, e] = acc
+                        acc = acc + cq
+                    cnt[e] = acc
+            elif stable:
                 tc = T.alloc_shared((threads, E), "int32")
                 run = T.alloc_shared((threads, E), "int32")
                 for t in T.Parallel(threads):
@@ -350,7 +459,35 @@ def align_kernel(n: int, E: int, block_M: int, max_rows: int, div: int, target: 
                             tr = T.min(start[e] + cnt[e] - tt * block_M, block_M)
                 tile_expert[tt] = te
                 tile_rows[tt] = tr
-            if stable:
+            if vote:
+                for t in T.Parallel(threads):
+                    run_ = T.alloc_local((E,), "int32")
+                    for e in T.serial(E):
+                        run_[e] = wc[t // 64, e]
+                    for it in T.serial(c):
+                        j = (t // 64) * (c * 64) + it * 64 + t % 64
+                        idv = T.alloc_var("int32")
+                        sl = T.alloc_var("int32")
+                        idv = T.if_then_else(j < n, expert_ids[T.min(j, n - 1)], -1)
+                        sl = 0
+                        for e in T.serial(E):
+                            m = T.ballot(idv == e)
+                            if idv == e:
+                                sl = run_[e] + T.call_extern("int32", "tl::mbcnt64", m)
+                            run_[e] = run_[e] + T.call_extern("int32", "tl::popc64", m)
+                        if j < n and idv >= 0:
+                            e_ = T.min(idv, E - 1)
+                            d = start[e_] + sl
+                            if full_first:  # slot sl of expert e -> its full or partial tile
+                                d = T.if_then_else(sl < cnt[e_] // block_M * block_M, start[e_] + sl,
+                                                   pstart[e_] + sl - cnt[e_] // block_M * block_M)
+                            if even:
+                                d = start[e_] + _even_row(sl, cnt[e_])
+                            dest[j] = d
+                            row_src[d] = j // div
+                        if j < n and idv < 0:
+                            dest[j] = -1
+            elif stable:
                 for t in T.Parallel(threads):
                     for e in T.serial(E):
                         run[t, e] = start[e] + run[t, e] - tc[t, e]
@@ -814,6 +951,12 @@ def route(x: torch.Tensor, gate_w: torch.Tensor, topk: int):
                                                                                        _padded_gate(gate_w), part)
             router_topk_kernel(n_tok, E, topk, _target(x.device), parts=sp, E_stride=Ep,
                                round_dtype=_tdt(x.dtype))(part, ids, w)
+            return ids, w
+        kc = 4
+        if ROUTER_WIDE and _target(x.device) == "hip" and n_tok % 8 == 0 and H % (kc * 128) == 0 and E <= 16:
+            g = _padded_gate(gate_w)
+            router_wide_kernel(n_tok, H, E, topk, _tdt(x.dtype), "hip", kc=kc)(
+                x.contiguous().view(n_tok * kc, H // kc), g.view(g.shape[0] * kc, H // kc), ids, w)
             return ids, w
         router_fused_kernel(n_tok, H, E, topk, _tdt(x.dtype), _target(x.device))(x.contiguous(), _padded_gate(gate_w),
                                                                                   ids, w)
