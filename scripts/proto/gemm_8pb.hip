@@ -35,6 +35,10 @@
 #ifndef SINGLE
 #define SINGLE 0  // 1: one barrier per K tile, the whole next tile staged in phase 0 (classic 2-stage)
 #endif
+#ifndef PREB1
+#define PREB1 0  // 1 (with MERGE): B1 read in phase 1 into a second B register set, so the MFMAs after
+                 // the mid-tile barrier start on resident operands
+#endif
 #ifndef MERGE
 #define MERGE 0  // 1: two barriers per K tile (phases paired), A0/B0 restaged after the pair
 #endif
@@ -210,6 +214,14 @@ extern "C" __global__ void __launch_bounds__(512) gemm_kernel(half_t* __restrict
 #if RPIPE
   F fb1[4][2];
 #endif
+#if PREB1
+  F fbb[4][2];
+#endif
+#if PREB1
+#define FBB fbb
+#else
+#define FBB fb
+#endif
 #if !RPIPE
 #define PHASE(BUF, P, T)                                                                          \
   {                                                                                               \
@@ -225,9 +237,10 @@ extern "C" __global__ void __launch_bounds__(512) gemm_kernel(half_t* __restrict
       } else if ((T) + 1 < NT) stage((BUF) ^ 1, 3, (T) + 1);                                      \
     } else if constexpr (P == 1) {                                                                \
       read_a<SB + 1 * HALF>(smem, fa1, wm, lrow, cx);                                             \
+      if (PREB1) read_b<SB + 3 * HALF>(smem, FBB, wn, lane, lrow, cx);                            \
       if (!SINGLE && !MERGE && (T) + 2 < NT) stage(BUF, 0, (T) + 2);                              \
     } else if constexpr (P == 2) {                                                                \
-      read_b<SB + 3 * HALF>(smem, fb, wn, lane, lrow, cx);                                        \
+      if (!PREB1) read_b<SB + 3 * HALF>(smem, fb, wn, lane, lrow, cx);                            \
       if (!SINGLE && MERGE && (T) + 2 < NT) stage(BUF, 0, (T) + 2);                               \
       if (!SINGLE && (T) + 2 < NT) stage(BUF, 2, (T) + 2);                                        \
     } else {                                                                                      \
@@ -236,8 +249,8 @@ extern "C" __global__ void __launch_bounds__(512) gemm_kernel(half_t* __restrict
     if (B1) bar();                                                                                \
     if constexpr (P == 0) mma<0, 0>(fa0, fb, acc);                                                \
     else if constexpr (P == 1) mma<1, 0>(fa1, fb, acc);                                           \
-    else if constexpr (P == 2) mma<1, 1>(fa1, fb, acc);                                           \
-    else mma<0, 1>(fa0, fb, acc);                                                                 \
+    else if constexpr (P == 2) mma<1, 1>(fa1, FBB, acc);                                          \
+    else mma<0, 1>(fa0, FBB, acc);                                                                \
     if constexpr (P == 3) {                                                                       \
       if (SINGLE) tl::wait_vmcnt<0>();                                                            \
       else if ((T) + 2 < NT) tl::wait_vmcnt<6>();                                                 \
