@@ -125,6 +125,40 @@ def test_quad_moe_structure():
     assert "for (int k" in g2
 
 
+def _fp8_src(K, dtype="float8_e4m3fn", **cfg):
+    sys.path.insert(0, os.path.join(ROOT, "examples", "gemm_fp8"))
+    from example_tilelang_gemm_fp8 import matmul as mm8
+    f = mm8.get_tir(512, 768, K, dtype=dtype, staged_epilogue=True)
+    return tilelang.lower(f, target="hip", pass_configs=cfg).kernel_source
+
+
+def test_quad_fp8_structure():
+    """fp8 256x256x128 (128-byte K tiles, the same LDS bytes as fp16 x 64) runs on the quad loop
+    with the 16x16x128 f8f6f4 MFMA; tl.gemm_quad=False keeps the generic pipeline."""
+    assert "tl::gemm_quad_nt_x<fp8_e4_t, false, 0>(" in _fp8_src(4096)
+    assert "tl::gemm_quad_nt_x<fp8_e5_t, false, 0>(" in _fp8_src(256, dtype="float8_e5m2")
+    assert "gemm_quad" not in _fp8_src(4096, **{"tl.gemm_quad": False})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [128, 256, 384, 2048, 8320])
+@pytest.mark.parametrize("dtype", ["float8_e4m3fn", "float8_e5m2"])
+def test_quad_fp8_numerics(K, dtype):
+    """fp8 quad loop (1, 2, 3, 16, 65 K tiles) against the fp32 product of the same fp8 values."""
+    sys.path.insert(0, os.path.join(ROOT, "examples", "gemm_fp8"))
+    from example_tilelang_gemm_fp8 import matmul as mm8
+    M, N = 512, 768
+    k = tilelang.compile(mm8.get_tir(M, N, K, dtype=dtype, staged_epilogue=True), out_idx=[-1], target="hip")
+    assert "gemm_quad_nt_x<fp8_e" in k.get_kernel_source()
+    td = getattr(torch, dtype)
+    for _ in range(2):
+        a = torch.randn(M, K, device="cuda").to(td)
+        b = torch.randn(N, K, device="cuda").to(td)
+        c = k(a, b)
+        ref = a.float() @ b.float().T
+        torch.testing.assert_close(c.float(), ref, rtol=2e-2, atol=2e-2 * K ** 0.5)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("K", [64, 128, 192, 1024, 4160])
 @pytest.mark.parametrize("dtype", ["float16", "bfloat16"])

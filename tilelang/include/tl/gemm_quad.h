@@ -1,4 +1,5 @@
-// tl/gemm_quad.h — whole-K-loop "quadrant" GEMM schedule for the 256x256x64 NT tile (gfx950).
+// tl/gemm_quad.h — whole-K-loop "quadrant" GEMM schedule for the 256x256 NT tile with 128-byte K
+// tiles (K = 64 fp16/bf16, or K = 128 fp8 on the scaled 16x16x128 MFMA) on gfx950.
 //
 // Selected by the software-pipeline pass (transform/pipeline.py, _quad_schedule) for the canonical
 //     for k in T.Pipelined(K / 64, num_stages=2):
@@ -10,7 +11,8 @@
 // Schedule (MI355X guide, "The 256^2 8-phase template", T2-T5; measured against the K-half
 // schedule of pipeline.py in scripts/proto/gemm_8ph_ab.py):
 //   * a K tile is four phases; phase (qa, qb) computes, on every wave, the 32x64 quadrant
-//     rows wm*64 + qa*32 + [0, 32) x cols wn*128 + qb*64 + [0, 64): 16 MFMAs 16x16x32.
+//     rows wm*64 + qa*32 + [0, 32) x cols wn*128 + qb*64 + [0, 64): 16 MFMAs 16x16x32 (fp8: 8
+//     scaled 16x16x128 MFMAs of twice the cycles -- the same MFMA time per byte of tile).
 //   * LDS holds two K tiles as eight [128][64] half-tile slots: A half qa = block rows
 //     {wm*64 + qa*32 + r} (four 32-row groups), B half qb = block cols {wn*128 + qb*64 + c}
 //     (two 64-col groups), gathered by the per-lane LDS-DMA source address; 16-byte chunks are
@@ -20,13 +22,32 @@
 //     precedes the barrier just passed (B1 of tile t+1 in phase 0; A0, B0, A1 of tile t+2 in
 //     phases 2-3), and one counted vmcnt(6) per K tile keeps three half-tiles in flight.
 // Requirements (checked by the pass): A [.., K] and B [.., K] K-contiguous global tensors with
-// the whole 256 x (64 n_tiles) blocks in bounds, 16-bit elements, 512 threads.
+// the whole 256 x (K-tile n_tiles) blocks in bounds, 16-bit or fp8 elements, 512 threads.
 #pragma once
 
 namespace tl {
 namespace quad {
 
-constexpr int HALF = 128 * 64;  // elements of one half-tile slot (16 KiB)
+// K-tile geometry in bytes: every row of a K tile is 128 bytes (64 fp16/bf16 or 128 fp8 elements),
+// eight 16-byte chunks; a half-tile slot is 128 rows (16 KiB)
+template <typename T> struct geo {
+  static constexpr int ES = (int)sizeof(T);
+  static constexpr int KE = 128 / ES;     // elements of a K-tile row
+  static constexpr int CE = 16 / ES;      // elements of a 16-byte chunk
+  static constexpr int HALF = 128 * KE;   // elements of a half-tile slot
+};
+
+// operand fragments of one K tile: two 16x16x32 fp16/bf16 fragments (one 16-byte read each), or
+// ONE 32-byte fp8 fragment of the scaled 16x16x128 MFMA (its two 16-byte reads land in the two
+// halves of the 8-register tuple the MFMA takes: no copies)
+template <typename T, bool F8 = sizeof(T) == 1> struct qfrag {
+  typedef typename mfma_traits<T>::frag F;
+  static constexpr int KK = 2;
+};
+template <typename T> struct qfrag<T, true> {
+  typedef intx8 F;
+  static constexpr int KK = 1;
+};
 
 TL_DEVICE void bar() { asm volatile("s_barrier" ::: "memory"); }
 TL_DEVICE const int* no_rows() { return nullptr; }  // dense A: no row list
@@ -42,40 +63,53 @@ template <typename P> TL_DEVICE P* uni_ptr(P* p) {
   return (P*)(((unsigned long long)hi << 32) | lo);
 }
 
-template <typename T, int SLOT_OFF>
-TL_DEVICE void read_a(const T* lds, typename mfma_traits<T>::frag (&a)[2][2], int wm, int lrow,
-                      const int (&cx)[2]) {
+// fragments i = 0..N-1 of LDS rows r0 + 16 i + (lane & 15), chunks cx[0] / cx[1] of the K tile
+template <typename T, int SLOT_OFF, int N>
+TL_DEVICE void read_rows(const T* lds, typename qfrag<T>::F (&f)[N][qfrag<T>::KK], int r0, int lrow,
+                         const int (&cx)[2]) {
+  typedef typename qfrag<T>::F F;
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+  for (int i = 0; i < N; ++i) {
+    const T* p = lds + SLOT_OFF + (r0 + i * 16) * geo<T>::KE + lrow;
+    if constexpr (qfrag<T>::KK == 2) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-      a[mi][kk] = *reinterpret_cast<const typename mfma_traits<T>::frag*>(lds + SLOT_OFF + (wm * 32 + mi * 16) * 64 +
-                                                                          lrow + cx[kk]);
+      for (int kk = 0; kk < 2; ++kk) f[i][kk] = *reinterpret_cast<const F*>(p + cx[kk]);
+    } else {
+      const intx4 lo = *reinterpret_cast<const intx4*>(p + cx[0]);
+      const intx4 hi = *reinterpret_cast<const intx4*>(p + cx[1]);
+      f[i][0] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  }
 }
 
-template <typename T, int SLOT_OFF>
-TL_DEVICE void read_b(const T* lds, typename mfma_traits<T>::frag (&b)[4][2], int wn, int lrow,
-                      const int (&cx)[2]) {
+// acc[BASE + mi * RS + ni] += A fragment mi x B fragment ni over the K tile: two 16x16x32 MFMAs
+// (kk outer, so consecutive MFMAs hit different accumulators), or for fp8 ONE 16x16x128 f8f6f4
+// MFMA (the same chunk permutation of K on both operands).  Scale operands 0 select the unscaled
+// v_mfma_f32_16x16x128_f8f6f4; the unit-scale (127) form is the two-word v_mfma_scale, whose
+// register constraints spilled ~130 VGPRs of this loop (256 + spills vs 223).
+template <typename T, int BASE, int RS, int MR, int NR>
+TL_DEVICE void mma_blk(const typename qfrag<T>::F (&a)[MR][qfrag<T>::KK],
+                       const typename qfrag<T>::F (&b)[NR][qfrag<T>::KK], floatx4* acc) {
+  if constexpr (qfrag<T>::KK == 1) {
 #pragma unroll
-  for (int ni = 0; ni < 4; ++ni)
+    for (int mi = 0; mi < MR; ++mi)
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-      b[ni][kk] = *reinterpret_cast<const typename mfma_traits<T>::frag*>(lds + SLOT_OFF + (wn * 64 + ni * 16) * 64 +
-                                                                          lrow + cx[kk]);
-}
-
-template <typename T, int QA, int QB>
-TL_DEVICE void mma(const typename mfma_traits<T>::frag (&a)[2][2], const typename mfma_traits<T>::frag (&b)[4][2],
-                   floatx4* acc) {
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        floatx4& c = acc[(QA * 2 + mi) * 8 + QB * 4 + ni];
-        c = mfma_traits<T>::mma16(b[ni][kk], a[mi][kk], c);
+      for (int ni = 0; ni < NR; ++ni) {
+        floatx4& c = acc[BASE + mi * RS + ni];
+        c = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b[ni][0], a[mi][0], c, fp8_fmt<T>::code,
+                                                              fp8_fmt<T>::code, 0, 0, 0, 0);
       }
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mi = 0; mi < MR; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NR; ++ni) {
+          floatx4& c = acc[BASE + mi * RS + ni];
+          c = mfma_traits<T>::mma16(b[ni][kk], a[mi][kk], c);
+        }
+  }
 }
 
 }  // namespace quad
@@ -96,7 +130,8 @@ TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __res
                               const T* __restrict__ B, int ldb, int n_tiles, T* lds_a, T* lds_b, T* lds_x,
                               float* __restrict__ C, float* __restrict__ Cx, int m_limit, int wave) {
   using namespace quad;
-  typedef typename mfma_traits<T>::frag F;
+  typedef typename qfrag<T>::F F;
+  constexpr int KE = geo<T>::KE, CE = geo<T>::CE, HALF = geo<T>::HALF;
   static_assert(EXT == 0 || EXT == 32, "extension rows: 0 or 32");
   A = uni_ptr(A);
   B = uni_ptr(B);
@@ -133,62 +168,63 @@ TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __res
       for (int j = 0; j < 2; ++j) {
         const int br = (2 * j + (rr >> 5)) * 64 + qa * 32 + (rr & 31);
         const int src = rows ? rows[br] : row0 + br;
-        voffa[qa][j] = (src >= 0 && src < a_rows) ? (uint32_t)((src * lda + dc * 8) * ES) : 0xFFFFFFF0u;
+        voffa[qa][j] = (src >= 0 && src < a_rows) ? (uint32_t)((src * lda + dc * CE) * ES) : 0xFFFFFFF0u;
       }
     ra = make_rsrc(A, (uint32_t)(a_rows * lda * ES));
   } else {
-    const uint32_t v = (uint32_t)((((rr >> 5) * 64 + (rr & 31)) * lda + dc * 8) * ES);
+    const uint32_t v = (uint32_t)((((rr >> 5) * 64 + (rr & 31)) * lda + dc * CE) * ES);
 #pragma unroll
     for (int qa = 0; qa < 2; ++qa)
 #pragma unroll
       for (int j = 0; j < 2; ++j) voffa[qa][j] = v;
-    ra = make_rsrc(A, (uint32_t)(((255 + EXT) * lda + 64 * NT) * ES));
+    ra = make_rsrc(A, (uint32_t)(((255 + EXT) * lda + KE * NT) * ES));
   }
   uint32_t voffx = 0;
   if constexpr (EXT > 0) {
     const int xr = (tid & 255) >> 3;
     if constexpr (GATHER) {
       const int src = rows ? rows[256 + xr] : row0 + 256 + xr;
-      voffx = (src >= 0 && src < a_rows) ? (uint32_t)((src * lda + dc * 8) * ES) : 0xFFFFFFF0u;
+      voffx = (src >= 0 && src < a_rows) ? (uint32_t)((src * lda + dc * CE) * ES) : 0xFFFFFFF0u;
     } else {
-      voffx = (uint32_t)(((256 + xr) * lda + dc * 8) * ES);
+      voffx = (uint32_t)(((256 + xr) * lda + dc * CE) * ES);
     }
   }
-  const uint32_t voffb = (uint32_t)((rr * ldb + dc * 8) * ES);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B, (uint32_t)((255 * ldb + 64 * NT) * ES));
-  T* da = lds_a + wave * 512;
-  T* db = lds_b + wave * 512;
+  const uint32_t voffb = (uint32_t)((rr * ldb + dc * CE) * ES);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B, (uint32_t)((255 * ldb + KE * NT) * ES));
+  // each wave's 64 lanes fill 1 KiB of a slot per DMA (lane-linear destination)
+  T* da = lds_a + wave * 8 * KE;
+  T* db = lds_b + wave * 8 * KE;
   // slot s of buffer b: A slots (s = 0, 1) in lds_a, B slots (s = 2, 3) in lds_b
   auto stage = [&](int buf, int slot, int tile) {
-    const int kb = tile * 64 * ES;
+    const int kb = tile * 128;  // bytes
     if (slot < 2) {
       T* l = da + (buf * 2 + slot) * HALF;
       const int s0 = GATHER ? kb : kb + (slot * 32) * lda * ES;
       const int s1 = GATHER ? kb : kb + (128 + slot * 32) * lda * ES;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)l, 16, voffa[slot][0], s0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(l + 4096), 16, voffa[slot][1], s1, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(l + 64 * KE), 16, voffa[slot][1], s1, 0, 0);
     } else {
       T* l = db + (buf * 2 + slot - 2) * HALF;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)l, 16, voffb, kb + ((slot - 2) * 64) * ldb * ES,
                                                 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(l + 4096), 16, voffb,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(l + 64 * KE), 16, voffb,
                                                 kb + (128 + (slot - 2) * 64) * ldb * ES, 0, 0);
     }
   };
   auto stage_x = [&](int buf, int tile) {
     if constexpr (EXT > 0)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(lds_x + buf * 2048 + (wave & 3) * 512), 16, voffx,
-                                                tile * 64 * ES, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(lds_x + buf * 32 * KE + (wave & 3) * 8 * KE), 16,
+                                                voffx, tile * 128, 0, 0);
   };
   constexpr int XW = EXT > 0 ? 1 : 0;  // extension DMAs per thread per K tile
   // operand reads: LDS row r0 + (lane & 15), chunk kk*4 + (lane >> 4), swizzled by (lane >> 1) & 7
-  const int lrow = (lane & 15) * 64;
+  const int lrow = (lane & 15) * KE;
   const int sw = (lane >> 1) & 7;
-  const int cx[2] = {((lane >> 4) ^ sw) * 8, ((4 + (lane >> 4)) ^ sw) * 8};
+  const int cx[2] = {((lane >> 4) ^ sw) * CE, ((4 + (lane >> 4)) ^ sw) * CE};
   // extension operands of wave w: B cols w*32 + [0, 32) = half qb = (w >> 1) & 1, LDS rows
   // (w >> 2) * 64 + (w & 1) * 32 + [0, 32) of that slot
   const int xqb = (wave >> 1) & 1;
-  const int xrow = ((wave >> 2) * 64 + (wave & 1) * 32) * 64;
+  const int xrow = ((wave >> 2) * 64 + (wave & 1) * 32) * KE;
 
   // prologue: tile 0 (+ its extension rows) and what P1-P3 of tile -1 stage: tile 1's A0,
   // B0 + extension, A1
@@ -208,7 +244,8 @@ TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __res
   }
   bar();
 
-  F fa0[2][2], fa1[2][2], fb[4][2];
+  constexpr int KK = qfrag<T>::KK;
+  F fa0[2][KK], fa1[2][KK], fb[4][KK];
   // the younger half of the workgroup (waves 4-7) at issue priority 1 for the loop (guide T5
   // static form: +0.5 %, profiles/r5/proto_8pb_single.log)
   if (wave >= 4) __builtin_amdgcn_s_setprio(1);
@@ -220,43 +257,34 @@ TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __res
   {                                                                                            \
     constexpr int SA = (BUF) * 2 * HALF;                                                       \
     if constexpr (P == 0) {                                                                    \
-      if constexpr (LIVE_) {                                                                              \
-        read_a<T, SA>(lds_a, fa0, wm, lrow, cx);                                               \
-        read_b<T, SA>(lds_b, fb, wn, lrow, cx);                                                \
+      if constexpr (LIVE_) {                                                                   \
+        read_rows<T, SA>(lds_a, fa0, wm * 32, lrow, cx);                                       \
+        read_rows<T, SA>(lds_b, fb, wn * 64, lrow, cx);                                        \
       }                                                                                        \
       if ((T_) + 1 < NT) stage((BUF) ^ 1, 3, (T_) + 1);                                        \
-      if constexpr (LIVE_) mma<T, 0, 0>(fa0, fb, acc);                                                    \
+      if constexpr (LIVE_) mma_blk<T, 0, 8>(fa0, fb, acc);                                     \
     } else if constexpr (P == 1) {                                                             \
-      if constexpr (LIVE_) read_a<T, SA + HALF>(lds_a, fa1, wm, lrow, cx);                                \
-      if constexpr (LIVE_) mma<T, 1, 0>(fa1, fb, acc);                                                    \
+      if constexpr (LIVE_) read_rows<T, SA + HALF>(lds_a, fa1, wm * 32, lrow, cx);             \
+      if constexpr (LIVE_) mma_blk<T, 16, 8>(fa1, fb, acc);                                    \
       if constexpr (EXT > 0) {                                                                 \
-        if constexpr (XLIVE_) {                                                                           \
-          F xa[2][2], xb[2][2];                                                                \
-          const T* xs = lds_x + (BUF) * 2048;                                                  \
-          const T* bs = lds_b + (SA + xqb * HALF) + xrow;                                      \
-          _Pragma("unroll") for (int i = 0; i < 2; ++i)                                        \
-          _Pragma("unroll") for (int kk = 0; kk < 2; ++kk) {                                   \
-            xa[i][kk] = *reinterpret_cast<const F*>(xs + i * 16 * 64 + lrow + cx[kk]);          \
-            xb[i][kk] = *reinterpret_cast<const F*>(bs + i * 16 * 64 + lrow + cx[kk]);          \
-          }                                                                                    \
-          floatx4* accx = reinterpret_cast<floatx4*>(Cx);                                      \
-          _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                     \
-          _Pragma("unroll") for (int mi = 0; mi < 2; ++mi)                                     \
-          _Pragma("unroll") for (int ni = 0; ni < 2; ++ni)                                     \
-            accx[mi * 2 + ni] = mfma_traits<T>::mma16(xb[ni][kk], xa[mi][kk], accx[mi * 2 + ni]); \
+        if constexpr (XLIVE_) {                                                                \
+          F xa[2][KK], xb[2][KK];                                                              \
+          read_rows<T, 0>(lds_x + (BUF) * 32 * KE, xa, 0, lrow, cx);                           \
+          read_rows<T, 0>(lds_b + (SA + xqb * HALF) + xrow, xb, 0, lrow, cx);                  \
+          mma_blk<T, 0, 2>(xa, xb, reinterpret_cast<floatx4*>(Cx));                            \
         }                                                                                      \
       }                                                                                        \
     } else if constexpr (P == 2) {                                                             \
-      if constexpr (LIVE_) read_b<T, SA + HALF>(lds_b, fb, wn, lrow, cx);                                 \
+      if constexpr (LIVE_) read_rows<T, SA + HALF>(lds_b, fb, wn * 64, lrow, cx);              \
       if ((T_) + 2 < NT) {                                                                     \
         stage(BUF, 0, (T_) + 2);                                                               \
         stage(BUF, 2, (T_) + 2);                                                               \
         stage_x(BUF, (T_) + 2);                                                                \
       }                                                                                        \
-      if constexpr (LIVE_) mma<T, 1, 1>(fa1, fb, acc);                                                    \
+      if constexpr (LIVE_) mma_blk<T, 20, 8>(fa1, fb, acc);                                    \
     } else {                                                                                   \
       if ((T_) + 2 < NT) stage(BUF, 1, (T_) + 2);                                              \
-      if constexpr (LIVE_) mma<T, 0, 1>(fa0, fb, acc);                                                    \
+      if constexpr (LIVE_) mma_blk<T, 4, 8>(fa0, fb, acc);                                     \
       if ((T_) + 2 < NT) wait_vmcnt<6 + XW>();                                                 \
       else if ((T_) + 1 < NT) wait_vmcnt<0>();                                                 \
     }                                                                                          \

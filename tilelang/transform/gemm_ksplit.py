@@ -94,12 +94,21 @@ def _minus_const(e, base, c) -> bool:
     return isinstance(e, BinOp) and e.op == "-" and as_int(e.b) == c and structural_equal(e.a, base)
 
 
+def quad_k(dtype):
+    """K of one quad-loop tile: 128 bytes of a row (64 fp16/bf16, 128 fp8)."""
+    return 128 // max(1, dtype.bits // 8)
+
+
+QUAD_DTYPES = ("float16", "bfloat16", "float8_e4m3fn", "float8_e5m2")
+
+
 def quad_loop_ok(stmts, threads, target) -> bool:
-    """The loop body is the 256x256x64 NT tile GEMM that ``tl::gemm_quad_nt_x`` (tl/gemm_quad.h)
-    implements: A_s [256][64] (a plain copy or a row gather), B_s [256][64] (transpose_B), 16-bit,
-    512 threads on a 4x2 wave grid with 16x16x32 MFMAs, fp32 fragment accumulator; optionally
-    T.gemm(valid_m=) and the MoE extension GEMM -- A_x [32][64] (rows 256..287 of the same copy or
-    gather), the same B_s, 1x8 waves (FullCol), valid_m = the main valid_m - 256."""
+    """The loop body is the 256x256 NT tile GEMM with 128-byte K tiles that ``tl::gemm_quad_nt_x``
+    (tl/gemm_quad.h) implements: A_s [256][KE] (a plain copy or a row gather), B_s [256][KE]
+    (transpose_B), KE = 64 fp16/bf16 or 128 fp8 (OCP e4m3 / e5m2, the scaled 16x16x128 MFMA),
+    512 threads on a 4x2 wave grid, fp32 fragment accumulator; optionally T.gemm(valid_m=) and
+    the MoE extension GEMM -- A_x [32][KE] (rows 256..287 of the same copy or gather), the same
+    B_s, 1x8 waves (FullCol), valid_m = the main valid_m - 256."""
     from ..ir import dtypes as _dt
     from . import gemm_lower
     if threads != 512:
@@ -108,10 +117,11 @@ def quad_loop_ok(stmts, threads, target) -> bool:
     prods = [x.op for x in stmts if isinstance(x, S.TileOpStmt) and isinstance(x.op, (O.CopyOp, O.GatherRowsOp))]
     if len(gemms) + len(prods) != len(stmts) or len(gemms) not in (1, 2):
         return False
-    main = [g for g in gemms if g.A.buffer.static_shape() == [256, 64]]
+    main = [g for g in gemms if g.A.buffer.static_shape() == [256, quad_k(g.A.buffer.dtype)]]
     if len(main) != 1:
         return False
     g = main[0]
+    ke = quad_k(g.A.buffer.dtype)
     ext = [x for x in gemms if x is not g]
     x = ext[0] if ext else None
 
@@ -128,14 +138,13 @@ def quad_loop_ok(stmts, threads, target) -> bool:
         return plan.get("warp_m") == wm and plan.get("warp_n") == wn and tuple(plan.get("mfma") or ()) == (16, 16, 32)
 
     A, B = g.A.buffer, g.B.buffer
-    if not plain(g) or B.static_shape() != [256, 64] or A.dtype not in (_dt.float16, _dt.bfloat16) or \
-            B.dtype != A.dtype:
+    if not plain(g) or B.static_shape() != [256, ke] or A.dtype.name not in QUAD_DTYPES or B.dtype != A.dtype:
         return False
     if not warps(g, 4, 2):
         return False
     dsts = {A, B}
     if x is not None:
-        if not plain(x) or x.B.buffer is not B or x.A.buffer.static_shape() != [32, 64] or x.A.buffer.dtype != A.dtype:
+        if not plain(x) or x.B.buffer is not B or x.A.buffer.static_shape() != [32, ke] or x.A.buffer.dtype != A.dtype:
             return False
         if x.C.buffer.static_shape() != [32, 256] or not warps(x, 1, 8):
             return False

@@ -748,16 +748,19 @@ def _in_bounds(src: BufferRegion, ranges) -> bool:
 
 def _quad_schedule(self, loop, asyncs, consumer_stmts, newbufs, ranges):
     """The whole loop as ``tl::gemm_quad_nt_x`` (loops marked ``quad`` by gemm_ksplit.mark_quad_loops):
-    the operand tiles' K start advances by exactly 64 per step along the contiguous dim, plain
+    the operand tiles' K start advances by exactly one 128-byte tile (64 fp16 / 128 fp8) per step
+    along the contiguous dim, plain
     copies are provably in bounds (gathers are range-checked by the buffer resource), and the
     GEMM (+ the MoE extension GEMM) are the only consumers.  None: the generic pipeline runs it."""
     gemms = [st.op for st in consumer_stmts if isinstance(st, S.TileOpStmt) and isinstance(st.op, O.GemmOp)]
     if len(gemms) != len(consumer_stmts) or len(gemms) not in (1, 2):
         return None
-    g = [x for x in gemms if x.A.buffer.static_shape() == [256, 64]]
+    from .gemm_ksplit import quad_k
+    g = [x for x in gemms if x.A.buffer.static_shape() == [256, quad_k(x.A.buffer.dtype)]]
     if len(g) != 1:
         return None
     g = g[0]
+    ke = quad_k(g.A.buffer.dtype)
     x = next((o for o in gemms if o is not g), None)
     k = loop.var
     tiles = {}
@@ -777,7 +780,7 @@ def _quad_schedule(self, loop, asyncs, consumer_stmts, newbufs, ranges):
         if as_int(src.buffer.get_strides()[cdim]) != 1:
             return None
         for d, (m, _) in enumerate(src.region):
-            if _k_coeff(m, k) != (64 if d == cdim else 0):
+            if _k_coeff(m, k) != (ke if d == cdim else 0):
                 return None
         idx = _subst_region(p.op.idx, {k: loop.min}) if gather is True else None
         if idx is not None and any(v is k for m, _ in idx.region for v in free_vars(m)):
