@@ -395,8 +395,10 @@ TL_DEVICE void gemm_ss_f8(const TA* __restrict__ A_, const TB* __restrict__ B_, 
       for (int mi = 0; mi < M_REP; ++mi)
 #pragma unroll
         for (int ni = 0; ni < N_REP; ++ni)
+          // scale operands 0: the compiler selects the unscaled v_mfma_f32_16x16x128_f8f6f4 (unit
+          // scales; numerics in tests/test_gemm_phased.py), not the two-word v_mfma_scale form
           acc[mi * N_REP + ni] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-              b[ni], a[mi], acc[mi * N_REP + ni], fp8_fmt<TB>::code, fp8_fmt<TA>::code, 0, 127, 0, 127);
+              b[ni], a[mi], acc[mi * N_REP + ni], fp8_fmt<TB>::code, fp8_fmt<TA>::code, 0, 0, 0, 0);
     }
   } else {
     static_assert(K % 32 == 0, "fp8 MFMA needs K % 32 == 0");
@@ -876,10 +878,10 @@ TL_DEVICE void mfma_emit(TC* c, const TA* a, const TB* b) {
       const intx8 av = *reinterpret_cast<const intx8*>(a), bv = *reinterpret_cast<const intx8*>(b);
       if constexpr (MS == 16)
         cv = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, cv, fp8_fmt<TA>::code, fp8_fmt<TB>::code, 0,
-                                                              127, 0, 127);
+                                                              0, 0, 0);
       else
         cv = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, bv, cv, fp8_fmt<TA>::code, fp8_fmt<TB>::code, 0,
-                                                             127, 0, 127);
+                                                             0, 0, 0);
     }
     *reinterpret_cast<FAcc*>(c) = cv;
   } else {

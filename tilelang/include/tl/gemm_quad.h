@@ -294,7 +294,9 @@ TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __res
 #define TL_QUAD_LOOP(L_, X_)                                                                   \
   {                                                                                            \
     constexpr bool LIVE_ = L_, XLIVE_ = X_;                                                    \
-    for (int t = 0; t < NT; t += 2) {                                                          \
+    /* never unrolled: a compile-time K of 2-16 tiles was unrolled whole and spilled          \
+       (16-40 VGPRs; fp8 K = 1024: 110 -> 83 us) */                                             \
+    _Pragma("nounroll") for (int t = 0; t < NT; t += 2) {                                      \
       TL_QUAD_PHASE(0, 0, t)                                                                   \
       TL_QUAD_PHASE(0, 1, t)                                                                   \
       TL_QUAD_PHASE(0, 2, t)                                                                   \
