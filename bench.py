@@ -332,22 +332,41 @@ def main():
     sync()
     elapsed = time.perf_counter() - t0
 
-    # per-phase times, measured after the timed region (MoE includes its all-to-alls)
-    def timed(fn, n):
+    # per-phase times, measured after the timed region (MoE includes its all-to-alls).  On a GPU
+    # each phase is timed on the device: two attention calls ahead of the first event keep the
+    # queue busy while the host enqueues the n calls, so the span between the events is the
+    # phase's device time, as inside the step (the kernel trace of a step shows the same span);
+    # the host's enqueue cost of one call is reported on its own (host_ms_per_call)
+    host_ms = {}
+
+    def timed(fn, n, name=None):
         sync()
         if dist is not None:
             dist.barrier()
+        if cpu or dist is not None:  # collectives inside: wall time
+            t = time.perf_counter()
+            for _ in range(n):
+                fn()
+            sync()
+            return (time.perf_counter() - t) / n * 1e3
+        for _ in range(2):
+            attn(Q, K, V)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
         t = time.perf_counter()
         for _ in range(n):
             fn()
+        if name:
+            host_ms[name] = round((time.perf_counter() - t) / n * 1e3, 4)
+        e1.record()
         sync()
-        return (time.perf_counter() - t) / n * 1e3
+        return e0.elapsed_time(e1) / n
 
     step_ms = [] if evs is None else [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     reps = 2 if cpu else 10
-    gemm_ms = timed(lambda: gemm(A, B), reps)
-    attn_ms = timed(lambda: attn(Q, K, V), reps)
-    moe_ms = timed(lambda: moe(X), reps) if moe is not None else 0.0
+    gemm_ms = timed(lambda: gemm(A, B), reps, "gemm")
+    attn_ms = timed(lambda: attn(Q, K, V), reps, "attn")
+    moe_ms = timed(lambda: moe(X), reps, "moe") if moe is not None else 0.0
     moe_comm_ms = 0.0
     if moe is not None and mesh is not None:
         if moe._device_ep():
@@ -425,6 +444,9 @@ def main():
             "attn_tflops": round(attn_flops / attn_ms / 1e9, 1),
             "moe_tflops_per_gpu": round(moe_flops / moe_ms / 1e9, 1) if moe is not None else None,
             "moe_comm_fraction": round(moe_comm_ms / moe_ms, 3) if moe is not None and moe_ms > 0 else None,
+            "phase_timing": ("wall, 1 call per rep" if (cpu or dist is not None) else
+                             "device time (events behind a queue-filling blocker), 10 calls"),
+            "host_ms_per_call": host_ms or None,
             "ep_exchange": (None if mesh is None or moe is None else
                             ("device (tl/ep.h, IPC over xGMI, no host sync)" if moe._device_ep() else
                              f"host ({'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} "
