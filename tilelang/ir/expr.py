@@ -491,11 +491,23 @@ def binop(op: str, a, b) -> PrimExpr:
     return BinOp(op, a, b, rdt)
 
 
+_TERM_KEYS = {}
+
+
 def _term_key(e) -> str:
+    # memoised by identity (the entry holds the node, so its id cannot be reused while cached):
+    # the linear-form simplifier keys the same sub-terms over and over
+    hit = _TERM_KEYS.get(id(e))
+    if hit is not None and hit[0] is e:
+        return hit[1]
     from .printer import Printer
     p = Printer()
     p.names = _IdNames()
-    return p.e(e)
+    k = p.e(e)
+    if len(_TERM_KEYS) > 65536:
+        _TERM_KEYS.clear()
+    _TERM_KEYS[id(e)] = (e, k)
+    return k
 
 
 class _IdNames:
@@ -631,26 +643,54 @@ def ceildiv(a, b):
 # ---------------------------------------------------------------------------
 
 
-def children(e: PrimExpr):
-    if isinstance(e, BinOp):
-        return (e.a, e.b)
-    if isinstance(e, UnOp):
-        return (e.a, )
-    if isinstance(e, Cast):
-        return (e.value, )
-    if isinstance(e, Select):
-        return (e.cond, e.t, e.f)
-    if isinstance(e, Call):
-        return tuple(a for a in e.args if isinstance(a, PrimExpr))
-    if isinstance(e, BufferLoad):
-        return tuple(e.indices)
+def _no_children(e):
     return ()
 
 
+_CHILD_FNS = (
+    (BinOp, lambda e: (e.a, e.b)),
+    (UnOp, lambda e: (e.a, )),
+    (Cast, lambda e: (e.value, )),
+    (Select, lambda e: (e.cond, e.t, e.f)),
+    (Call, lambda e: tuple(a for a in e.args if isinstance(a, PrimExpr))),
+    (BufferLoad, lambda e: tuple(e.indices)),
+)
+_children_of_type = {}
+
+
+def _children_fn(t):
+    for cls, fn in _CHILD_FNS:
+        if issubclass(t, cls):
+            return fn
+    return _no_children
+
+
+def children(e: PrimExpr):
+    # one dict lookup per node instead of a chain of isinstance tests (the lowering passes walk
+    # ~10^5 nodes per kernel)
+    t = type(e)
+    fn = _children_of_type.get(t)
+    if fn is None:
+        fn = _children_of_type[t] = _children_fn(t)
+    return fn(e)
+
+
 def post_order(e: PrimExpr):
-    for c in children(e):
-        yield from post_order(c)
-    yield e
+    """Every node of ``e``, children (left to right) before their parent: the reverse of a
+    pre-order walk that visits the last child first (iterative; a list)."""
+    out = []
+    stack = [e]
+    get = _children_of_type.get
+    while stack:
+        n = stack.pop()
+        out.append(n)
+        t = type(n)
+        fn = get(t)
+        if fn is None:
+            fn = _children_of_type[t] = _children_fn(t)
+        stack.extend(fn(n))
+    out.reverse()
+    return out
 
 
 def free_vars(e) -> List[Var]:
