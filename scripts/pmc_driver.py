@@ -1,6 +1,6 @@
 """Run one bench kernel (the headline GEMM or FA) N times for a rocprofv3 --pmc pass.
 
-    rocprofv3 --pmc <counters> -- python3 scripts/pmc_driver.py gemm|gemm_nt|hipblaslt_nt|fa|fa32 [iters]
+    rocprofv3 --pmc <counters> -- python3 scripts/pmc_driver.py gemm|gemm_nt|hipblaslt_nt|fp8_nt|scaled_mm|fa|fa32 [iters]
 """
 import os
 import sys
@@ -38,6 +38,18 @@ def main():
         a = torch.randn(g["M"], g["K"], device="cuda").half()
         b = torch.randn(g["N"], g["K"], device="cuda").half()
         fn = lambda: a @ b.T  # noqa: E731
+    elif which in ("fp8_nt", "scaled_mm"):  # fp8 e4m3 8192^3, B [N, K]: the quad loop / hipBLASLt
+        sys.path.insert(0, os.path.join(HERE, "..", "examples", "gemm_fp8"))
+        n = 8192
+        a = torch.randn(n, n, device="cuda").to(torch.float8_e4m3fn)
+        b = torch.randn(n, n, device="cuda").to(torch.float8_e4m3fn)
+        if which == "fp8_nt":
+            from example_tilelang_gemm_fp8 import matmul as mm8
+            k = mm8(n, n, n, staged_epilogue=True)
+            fn = lambda: k(a, b)  # noqa: E731
+        else:
+            one = torch.ones((), device="cuda")
+            fn = lambda: torch._scaled_mm(a, b.T, scale_a=one, scale_b=one, out_dtype=torch.bfloat16)  # noqa: E731
     elif which == "fa":  # the bench's attention kernel, exactly as bench.py builds it
         k, (q, kk, v) = bench.build_attn("cuda")
         fn = lambda: k(q, kk, v)  # noqa: E731
