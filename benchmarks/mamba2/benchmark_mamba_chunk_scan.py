@@ -37,7 +37,12 @@ def configs():
             dict(block_M=128, block_N=64, block_K=64, threads=256, num_stages=2, xcd_group=True, factored=True),
             dict(block_M=128, block_N=64, block_K=32, threads=256, num_stages=2, xcd_group=True, factored=True),
             dict(block_M=64, block_N=64, block_K=64, threads=256, num_stages=2, xcd_group=True, factored=True),
-            dict(block_M=256, block_N=64, block_K=64, threads=256, num_stages=2, xcd_group=True, factored=True)]
+            dict(block_M=256, block_N=64, block_K=64, threads=256, num_stages=2, xcd_group=True, factored=True),
+            # r5: the interior / diagonal split without the XCD grouping (which cost 15 % alone)
+            dict(block_M=128, block_N=64, block_K=64, threads=256, num_stages=2, lean=True),
+            dict(block_M=128, block_N=64, block_K=32, threads=256, num_stages=2, lean=True),
+            dict(block_M=64, block_N=64, block_K=64, threads=256, num_stages=2, lean=True),
+            dict(block_M=128, block_N=64, block_K=64, threads=256, num_stages=2, factored=True)]
 
 
 def selected():
