@@ -59,3 +59,24 @@ def test_no_pch_for_other_sources(fresh_cache, monkeypatch):
     monkeypatch.setenv("TL_HIP_PCH", "1")
     hipcc.compile_hip("#include <hip/hip_runtime.h>\nextern \"C\" __global__ void k(float* a) { a[0] = 1.f; }\n")
     assert hipcc._pch_paths == {}
+
+
+def _compile_in_child(cache):
+    os.environ["TILELANG_CACHE_DIR"] = cache
+    os.environ["TL_HIP_PCH"] = "1"
+    from tilelang.contrib import hipcc as h
+    return len(h.compile_hip(SRC)), [p for p in h._pch_paths.values() if p]
+
+
+def test_pch_concurrent_builders(tmp_path):
+    """Several processes building the same PCH at once: each writes a private temp file and
+    renames it into place, so every compile succeeds and one PCH file remains."""
+    import multiprocessing as mp
+    cache = str(tmp_path / "cache")
+    with mp.get_context("spawn").Pool(3) as pool:
+        res = pool.map(_compile_in_child, [cache] * 3)
+    assert all(n > 0 for n, _ in res)
+    pchs = {p for _, ps in res for p in ps}
+    assert len(pchs) == 1 and os.path.exists(pchs.pop())
+    assert sorted(os.listdir(os.path.join(cache, "pch"))) == sorted(
+        [os.path.basename(p) for _, ps in res for p in ps][:1] + ["tl_pch.h"])
