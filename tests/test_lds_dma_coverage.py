@@ -139,3 +139,50 @@ def test_pack_f32_pairs():
     plain = tilelang.lower(main, target="hip").kernel_source
     packed = tilelang.lower(main, target="hip", pass_configs={"tl.pack_f32": True}).kernel_source
     assert "tl::floatx2" not in plain and "tl::floatx2" in packed
+
+
+def _persistent_kernel(iter_local):
+    import tilelang.language as T
+
+    @T.prim_func
+    def main(A: T.Tensor((8, 256, 128), "float32"), O: T.Tensor((8, 256, 128), "float32")):
+        with T.Kernel(2, threads=256) as bx:
+            big = T.alloc_shared((256, 128), "float32")  # 128 KiB: two of them do not fit
+            out = T.alloc_shared((256, 128), "float32")
+            for it in T.serial(4, annotations={"lds_iteration_local": True} if iter_local else None):
+                t = bx * 4 + it
+                T.copy(A[t, :, :], big)
+                for i, j in T.Parallel(256, 128):
+                    big[i, j] = big[i, j] * 2.0
+                T.copy(big, O[t, :, :])
+                for i, j in T.Parallel(256, 128):
+                    out[i, j] = O[t, i, j] + 1.0
+                T.copy(out, O[t, :, :])
+
+    return main
+
+
+def test_lds_iteration_local_loops():
+    """Loops annotated ``lds_iteration_local`` (transform/lds_plan.py): buffers confined to
+    disjoint stretches of one iteration share bytes, with a barrier where the tenants switch and
+    one at the top of the body (the late tenant of iteration i precedes the early one of i + 1);
+    without the annotation the loop is one statement and the two 128 KiB tiles do not fit."""
+    from tilelang.transform.lds_plan import LDSPlanError
+    src = tilelang.lower(_persistent_kernel(True), target="hip").kernel_source
+    assert "tl_smem[131072]" in src
+    body = src[src.index("for (int i = 0; i < 4;"):]
+    assert body.index("tl::sync_threads()") < body.index("big")
+    with pytest.raises(LDSPlanError):
+        tilelang.lower(_persistent_kernel(False), target="hip")
+
+
+@pytest.mark.gpu
+def test_lds_iteration_local_gpu():
+    """The shared-bytes persistent kernel computes the right thing on the GPU (barriers at the
+    tenant switches and at the top of every iteration)."""
+    import torch
+    k = tilelang.compile(_persistent_kernel(True), target="hip")
+    a = torch.randn(8, 256, 128, device="cuda")
+    o = torch.zeros_like(a)
+    k(a, o)
+    torch.testing.assert_close(o, a * 2.0 + 1.0)

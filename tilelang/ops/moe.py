@@ -31,6 +31,7 @@ import torch
 
 import tilelang
 import tilelang.language as T
+from tilelang.layout import PaddedLayout
 
 
 def _target(device) -> str:
@@ -633,8 +634,15 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
                           n_src: Optional[int] = None, swiglu: bool = False, n_cu: int = 256, tail_split: int = 4,
                           phased: bool = False, skip_padding: bool = True, partial_first: bool = False,
                           tail_ksplit: int = 0, tail_stages: Optional[int] = None, ext_M: int = 0,
-                          quad: bool = True):
+                          quad: bool = True, staged_epi: bool = True):
     """Tail-balanced variant of ``expert_gemm_kernel`` (same arguments and output).
+
+    ``staged_epi``: the tile's C (or its SwiGLU activation) goes through row-padded LDS and leaves
+    as row-contiguous 16-byte stores (the 32 extension rows keep direct stores).  The staging tile
+    shares bytes with the operand ring: the persistent tile loops are ``lds_iteration_local``
+    (transform/lds_plan.py), so the planner separates the two tenants inside every iteration.
+    Dense stand-in of GEMM2 (4608x4096x2048 bf16): 743 -> 811 TF; bench layer, random routing:
+    GEMM1 118 -> 115.5 us, GEMM2 69.5 -> 65.7 us (``profiles/r5/moe_epi/``).
 
     ``quad``: the whole-tile main loop (256x256x64, 512 threads, row gather + ``ext_M`` = 32
     extension included) runs the 8-phase quadrant schedule ``tl::gemm_quad_nt_x`` (tl.gemm_quad);
@@ -672,6 +680,7 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
     derives U and R from ``tile_expert`` (the real tiles are a prefix): nothing waits on the host."""
     slot = block_M + ext_M
     assert not (ext_M and tail_ksplit), "ext_M runs with the narrow-tile tail"
+    staged_epi = staged_epi and not tail_ksplit  # the K-split tail's loops are not iteration-local
     n_tiles = max_rows // slot
     n_by = (N + block_N - 1) // block_N
     nk = (K + block_K - 1) // block_K
@@ -717,7 +726,20 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
                 # column-split waves (when the tile is wide enough) all skip the same empty fragments
                 T.gemm(A_x, W_s, C_x, transpose_B=True, valid_m=nrows - block_M,
                        policy=T.GemmWarpPolicy.FullCol if bn // 16 >= threads // 64 else T.GemmWarpPolicy.Square)
-        if swiglu:
+        if swiglu and staged_epi:
+            # activation pairs into a row-padded LDS tile, then row-contiguous 16-byte stores
+            A_o = T.alloc_shared((block_M, bn // 2), dtype)
+            T.annotate_layout({A_o: PaddedLayout((block_M, bn // 2), 8)})
+            for i, j in T.Parallel(block_M, bn):
+                if j % 4 < 2:
+                    A_o[i, (j // 4) * 2 + j % 4] = T.Cast(dtype, C_l[i, j] / (1.0 + T.exp(-C_l[i, j])) * C_l[i, j + 2])
+            T.copy(A_o, C[r0, col0 // 2])
+            if ext_M:
+                for i, j in T.Parallel(ext_M, bn):
+                    if j % 4 < 2:
+                        C[r0 + block_M + i, col0 // 2 + (j // 4) * 2 + j % 4] = T.Cast(
+                            dtype, C_x[i, j] / (1.0 + T.exp(-C_x[i, j])) * C_x[i, j + 2])
+        elif swiglu:
             for i, j in T.Parallel(block_M, bn):
                 if j % 4 < 2:
                     C[r0 + i, col0 // 2 + (j // 4) * 2 + j % 4] = T.Cast(
@@ -727,6 +749,13 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
                     if j % 4 < 2:
                         C[r0 + block_M + i, col0 // 2 + (j // 4) * 2 + j % 4] = T.Cast(
                             dtype, C_x[i, j] / (1.0 + T.exp(-C_x[i, j])) * C_x[i, j + 2])
+        elif staged_epi:
+            C_s = T.alloc_shared((block_M, bn), dtype)
+            T.annotate_layout({C_s: PaddedLayout((block_M, bn), 8)})
+            T.copy(C_l, C_s)
+            T.copy(C_s, C[r0, col0])
+            if ext_M:
+                T.copy(C_x, C[r0 + block_M, col0])
         else:
             T.copy(C_l, C[r0, col0])
             if ext_M:
@@ -837,9 +866,13 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
             C_l = T.alloc_fragment((block_M, block_N), accum)
             Wt_s = T.alloc_shared((bn_t, block_K), dtype)
             Ct_l = T.alloc_fragment((block_M, bn_t), accum)
-            A_x = C_x = Ct_x = None
+            # the tail loop has operand tiles of its own: every LDS buffer then lives inside one
+            # iteration-local loop, so the staging tiles can take the rings' bytes
+            At_s = T.alloc_shared((block_M, block_K), dtype) if staged_epi else A_s
+            A_x = C_x = Ct_x = At_x = None
             if ext_M:
                 A_x = T.alloc_shared((ext_M, block_K), dtype)
+                At_x = T.alloc_shared((ext_M, block_K), dtype) if staged_epi else A_x
                 C_x = T.alloc_fragment((ext_M, block_N), accum)
                 Ct_x = T.alloc_fragment((ext_M, bn_t), accum)
             nt = T.alloc_var("int32")
@@ -855,16 +888,18 @@ def expert_gemm_sk_kernel(max_rows: int, K: int, N: int, E: int, dtype: str, tar
             full = units - units % n_cu
             # unit u -> tile (u + shift) % units: partial tiles first when asked
             shift = (nt - nfull) * n_by if partial_first else 0
-            for it in T.serial(full // n_cu):  # whole tiles
+            # no LDS value crosses a tile: the operand ring and the C staging tile share bytes
+            loc = {"lds_iteration_local": True}
+            for it in T.serial(full // n_cu, annotations=loc):  # whole tiles
                 u = (pid + it * n_cu + shift) % units
                 tile(A, W, row_src, tile_rows, C, A_s, W_s, C_l, u // n_by, tile_expert[u // n_by],
                      (u % n_by) * block_N, block_N, num_stages, A_x, C_x)
-            for it in T.serial(T.ceildiv((units - full) * tail_split, n_cu)):  # narrow tail tiles
+            for it in T.serial(T.ceildiv((units - full) * tail_split, n_cu), annotations=loc):  # narrow tail tiles
                 q = pid + it * n_cu
                 if q < (units - full) * tail_split:
                     u = (full + q // tail_split + shift) % units
-                    tile(A, W, row_src, tile_rows, C, A_s, Wt_s, Ct_l, u // n_by, tile_expert[u // n_by],
-                         (u % n_by) * block_N + (q % tail_split) * bn_t, bn_t, t_stages, A_x, Ct_x)
+                    tile(A, W, row_src, tile_rows, C, At_s, Wt_s, Ct_l, u // n_by, tile_expert[u // n_by],
+                         (u % n_by) * block_N + (q % tail_split) * bn_t, bn_t, t_stages, At_x, Ct_x)
 
     # K-half phased main loop (row gathers included) measured slower here: 382-403 vs 300-356 us per
     # layer (profiles/r2/session2/moe_phased_tail_sweep.log), so off by default

@@ -74,6 +74,36 @@ def _top_level(body) -> List:
     return top
 
 
+ITER_LOCAL = "lds_iteration_local"
+
+
+def _iter_local_body(st):
+    """(loop, body statements, guard) for a loop annotated ``lds_iteration_local`` (its shared
+    buffers hold nothing across iterations), else None.  A body that is one ``if`` without an else
+    (a persistent loop's bound check; block-uniform like every statement with a barrier inside)
+    is opened too: ``guard`` is that if."""
+    if not (isinstance(st, S.ForStmt) and st.annotations.get(ITER_LOCAL)):
+        return None
+    body, guard = st.body, None
+    if isinstance(body, S.IfStmt) and body.else_body is None:
+        guard, body = body, body.then_body
+    return st, _top_level(body), guard
+
+
+def _expand(body):
+    """Top-level statements, with the bodies of iteration-local loops expanded in place:
+    ``[(stmt, group)]``; group is None at the top level, else the index of its loop."""
+    out, loops = [], []
+    for st in _top_level(body):
+        il = _iter_local_body(st)
+        if il is None:
+            out.append((st, None))
+        else:
+            loops.append(il)
+            out += [(x, len(loops) - 1) for x in il[1]]
+    return out, loops
+
+
 def _dma_targets(s) -> set:
     out = set()
     for x in S.walk(s):
@@ -103,7 +133,14 @@ def plan_lds(kernel: S.KernelStmt, reuse: bool = True, aggressive: bool = False)
         if isinstance(s, S.AllocStmt) and s.buffer.scope == "shared" and s.buffer not in shared:
             shared.append(s.buffer)
     sizes = {b: int(b.shape[0]) * b.dtype.bytes for b in shared}
-    top = _top_level(kernel.body)
+    # statements in order; the bodies of loops annotated ``lds_iteration_local`` (T.serial(...,
+    # annotations={"lds_iteration_local": True}): no shared value crosses an iteration, e.g. a
+    # persistent tile loop whose operand ring and C staging tile are rewritten every tile) are
+    # expanded, so buffers confined to one iteration's stretch of statements can share bytes
+    top, loops = _expand(kernel.body) if reuse and not kernel.is_cpu else ([(x, None) for x in _top_level(
+        kernel.body)], [])
+    group = [g for _, g in top]
+    top = [x for x, _ in top]
     first, last = {}, {}
     for i, st in enumerate(top):
         t = set()
@@ -111,6 +148,18 @@ def plan_lds(kernel: S.KernelStmt, reuse: bool = True, aggressive: bool = False)
         for b in t:
             first.setdefault(b, i)
             last[b] = i
+    # a buffer touched in an iteration-local loop AND outside it lives across the whole loop
+    span = {}
+    for i, g in enumerate(group):
+        if g is not None:
+            lo, hi = span.get(g, (i, i))
+            span[g] = (min(lo, i), max(hi, i))
+    for b in list(first):
+        for g, (lo, hi) in span.items():
+            inside = lo <= first[b] and last[b] <= hi
+            touches = not (last[b] < lo or first[b] > hi)
+            if touches and not inside:
+                first[b], last[b] = min(first[b], lo), max(last[b], hi)
     dma = _dma_targets(kernel)
     pinned = set() if aggressive else dma
     n_top = len(top)
@@ -136,16 +185,45 @@ def plan_lds(kernel: S.KernelStmt, reuse: bool = True, aggressive: bool = False)
                 switch.add(f[i])
                 if a in dma:
                     drain.add(f[i])
+    # iteration wrap: a later tenant of iteration i precedes an earlier tenant of iteration i + 1
+    for g, (lo, hi) in span.items():
+        for i, b in enumerate(shared):
+            for j, a in enumerate(shared):
+                if a is b or not (lo <= f[i] <= l_[i] <= hi and lo <= f[j] <= l_[j] <= hi) or l_[i] >= f[j]:
+                    continue
+                oa, ob = offsets[a], offsets[b]
+                if oa < ob + sizes[b] and ob < oa + sizes[a]:
+                    switch.add(lo)
+                    if a in dma:
+                        drain.add(lo)
     if not switch:
         return kernel, offsets, total
     from .thread_sync import _sync
-    new_top = []
-    for i, st in enumerate(top):
+
+    def marks(i):
+        out = []
         if i in drain:
-            new_top.append(L.CallStmt("tl::wait_vmcnt", [], [0]))
+            out.append(L.CallStmt("tl::wait_vmcnt", [], [0]))
         if i in switch:
-            new_top.append(_sync())
-        new_top.append(st)
+            out.append(_sync())
+        return out
+
+    new_top, i = [], 0
+    while i < len(top):
+        g = group[i]
+        if g is None:
+            new_top += marks(i) + [top[i]]
+            i += 1
+            continue
+        loop, stmts, guard = loops[g]
+        body = []
+        for _ in stmts:
+            body += marks(i) + [top[i]]
+            i += 1
+        nb = S.SeqStmt(body)
+        if guard is not None:
+            nb = S.IfStmt(guard.cond, nb, None)
+        new_top.append(S.ForStmt(loop.var, loop.min, loop.extent, loop.kind, nb, loop.annotations))
     k = S.KernelStmt(kernel.grid, kernel.threads, kernel.block_vars, kernel.thread_vars, S.SeqStmt(new_top),
                      kernel.is_cpu, kernel.prelude)
     k.attrs = dict(kernel.attrs)
