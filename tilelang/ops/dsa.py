@@ -8,6 +8,7 @@ import functools
 
 import tilelang
 import tilelang.language as T
+from tilelang.layout import PaddedLayout
 
 LOG2E = 1.44269504
 
@@ -15,7 +16,7 @@ LOG2E = 1.44269504
 @tilelang.jit(out_idx=[3, 4], pass_configs={tilelang.PassConfigKey.TL_GEMM_FOLD_DEFAULT_GUARD: False})
 def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_group=1, sm_scale=None, block_I=64,
                    threads=None, dtype="bfloat16", num_stages=2, block_H=None, xcd_pair=True, lazy_rescale=True,
-                   wide=None):
+                   wide=None, staged_out=True):
     """Sparse MLA forward over the ``topk`` selected latent rows of every query token.
 
     Schedule (MI355X): one block per (token, 64-head slice); Q stays in registers (it is the
@@ -157,7 +158,16 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
                     o_cast[h, d] = acc_o[h, d] / l_sum[h]
             for h in T.Parallel(H_blk):
                 l_sum[h] = T.log2(l_sum[h]) + m_cur[h] * scale
-            T.copy(o_cast[0:valid_h, :], Output[b, bx, h0:h0 + valid_h, :])
+            if staged_out:
+                # the token's O rows leave as contiguous 16-byte row stores from a row-padded LDS
+                # tile (the gathered-KV ring's bytes, dead after the loop): 756 -> 767 TF at the
+                # reference's benchmark shape (profiles/r5/smla_epi/ab.log)
+                O_s = T.alloc_shared([H_blk, D], dtype)
+                T.annotate_layout({O_s: PaddedLayout((H_blk, D), 8)})
+                T.copy(o_cast, O_s)
+                T.copy(O_s[0:valid_h, :], Output[b, bx, h0:h0 + valid_h, :])
+            else:
+                T.copy(o_cast[0:valid_h, :], Output[b, bx, h0:h0 + valid_h, :])
             T.copy(l_sum[0:valid_h], Lse[b, bx, h0:h0 + valid_h])
 
     return main
