@@ -186,3 +186,22 @@ def test_lds_iteration_local_gpu():
     o = torch.zeros_like(a)
     k(a, o)
     torch.testing.assert_close(o, a * 2.0 + 1.0)
+
+
+def test_persistent_gemm_staged_epilogue_shares_lds():
+    """T.Persistent(lds_iteration_local=True): the persistent GEMM's C staging tile takes the
+    operand ring's bytes (135 KiB arena instead of 263 KiB)."""
+    from example_gemm_persistent import matmul_persistent
+    src = _hip(matmul_persistent, 8192, 8192, 1024, trans_B=True, staged_epilogue=True)
+    assert "tl_smem[135168]" in src and "gemm_quad_nt_x<" in src
+
+
+@pytest.mark.gpu
+def test_persistent_gemm_staged_epilogue_gpu():
+    import torch
+    from example_gemm_persistent import matmul_persistent
+    M, N, K = 1024, 1536, 512
+    k = matmul_persistent(M, N, K, trans_B=True, staged_epilogue=True, num_cus=4)
+    a = torch.randn(M, K, device="cuda", dtype=torch.float16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.float16)
+    torch.testing.assert_close(k(a, b).float(), a.float() @ b.float().T, rtol=2e-2, atol=2e-1)

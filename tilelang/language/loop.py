@@ -147,12 +147,15 @@ def Pipelined(start, stop=None, num_stages: int = 0, order=None, stage=None, syn
     return _loop("pipelined", start, stop, None, ann, name="k")
 
 
-def Persistent(domain, wave_size, index, group_size: Optional[int] = 8):
+def Persistent(domain, wave_size, index, group_size: Optional[int] = 8, lds_iteration_local: bool = False):
     """Persistent tile loop (reference ``src/ir.cc:115-187``).
 
     ``domain`` is the 2-D tile grid ``[tiles_m, tiles_n]``; ``wave_size`` the number of
     concurrently running blocks; ``index`` the block id.  Yields ``(bx, by)`` for each tile this
     block owns, walking tiles in waves with grouped (L2-friendly) ordering.
+    ``lds_iteration_local``: no shared-memory value crosses a tile, so the LDS planner may give
+    buffers used in different stretches of one tile (the operand ring, a C staging tile) the same
+    bytes (transform/lds_plan.py).
     """
     b = current_builder()
     if isinstance(domain, (list, tuple)):
@@ -192,7 +195,10 @@ def Persistent(domain, wave_size, index, group_size: Optional[int] = 8):
     guard.__exit__(None, None, None)
     body = b.pop()
     b.loop_stack.pop()
-    b.emit(S.ForStmt(w, 0, waves, "serial", body, {"persistent": True}))
+    ann = {"persistent": True}
+    if lds_iteration_local:
+        ann["lds_iteration_local"] = True
+    b.emit(S.ForStmt(w, 0, waves, "serial", body, ann))
 
 
 def S_min(a, b):
