@@ -30,7 +30,9 @@ def fast_flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_
     kv_shape = [batch, seq_len, head_kv, dim]
     accum_dtype = "float"
     num_q_blocks = (seq_len + block_M - 1) // block_M
-    assert seq_len % block_N == 0, "no key-padding mask: seq_len must be a multiple of block_N"
+    # key-padding mask on the last KV tile when seq_len is not a multiple of block_N (reference
+    # examples/flash_attention/example_mha_fwd_bshd.py:54); causal rows never see those keys
+    ragged_kv = seq_len % block_N != 0 and not is_causal
     if num_split_q is None:  # one resident 8-wave workgroup per CU over the whole grid
         num_split_q = max(1, min(num_q_blocks, 256 // max(1, batch * heads)))
     group = [[0], [1, 2], list(range(3, 11)), [11], [12], [13]]  # as example_mha_fwd_pipelined
@@ -66,7 +68,8 @@ def fast_flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_
                     T.fill(l_i, 0)
                     T.fill(m_i, -(2.0**30))
                     rescale = 1
-                    loop_end = T.ceildiv((bx + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N)
+                    loop_end = (T.min(T.ceildiv((bx + 1) * block_M, block_N), T.ceildiv(seq_len, block_N))
+                                if is_causal else T.ceildiv(seq_len, block_N))
                     for k in T.Pipelined(loop_end, num_stages=num_stages, order=[-1, 0, 3, 1, -1, 2],
                                          stage=[-1, 0, 0, 1, -1, 1], group=group):
                         T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
@@ -77,6 +80,13 @@ def fast_flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_
                                 for i, j in T.Parallel(block_M, block_N):
                                     acc_s[i, j] = T.if_then_else(bx * block_M + i >= k * block_N + j, 0,
                                                                  -T.infinity(accum_dtype))
+                        elif ragged_kv:
+                            if k == loop_end - 1:
+                                for i, j in T.Parallel(block_M, block_N):
+                                    acc_s[i, j] = T.if_then_else(k * block_N + j < seq_len, 0,
+                                                                 -T.infinity(accum_dtype))
+                            else:
+                                T.clear(acc_s)
                         else:
                             T.clear(acc_s)
                         T.gemm(Q_r, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow,

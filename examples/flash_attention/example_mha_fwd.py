@@ -37,6 +37,9 @@ def flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=128
     q_shape = [batch, seq_len, heads, dim]
     kv_shape = [batch, seq_len, head_kv, dim]
     accum_dtype = "float"
+    # keys at or past seq_len in a ragged last KV tile are masked to -inf (reference
+    # example_mha_fwd_bshd.py:54); causal rows never see them
+    ragged_kv = seq_len % block_N != 0 and not is_causal
 
     @T.prim_func
     def main(
@@ -69,7 +72,9 @@ def flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=128
             else:
                 T.fill(scores_max, -T.infinity(accum_dtype))
 
-            loop_range = (T.ceildiv((bx + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N))
+            # the causal range stops at the last key tile (a ragged last query tile would run past it)
+            loop_range = (T.min(T.ceildiv((bx + 1) * block_M, block_N), T.ceildiv(seq_len, block_N))
+                          if is_causal else T.ceildiv(seq_len, block_N))
 
             for k in T.Pipelined(loop_range, num_stages=num_stages):
                 T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
@@ -77,6 +82,12 @@ def flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=128
                     for i, j in T.Parallel(block_M, block_N):
                         acc_s[i, j] = T.if_then_else(bx * block_M + i >= k * block_N + j, 0,
                                                      -T.infinity(acc_s.dtype))
+                elif ragged_kv:  # key-padding mask on the last KV tile only (uniform branch)
+                    if k == loop_range - 1:
+                        for i, j in T.Parallel(block_M, block_N):
+                            acc_s[i, j] = T.if_then_else(k * block_N + j < seq_len, 0, -T.infinity(acc_s.dtype))
+                    else:
+                        T.clear(acc_s)
                 else:
                     T.clear(acc_s)
                 T.gemm(Q_shared, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)

@@ -70,7 +70,10 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
     seq_kv = seq_len if seq_kv is None else seq_kv
     past = seq_kv - seq_len
     assert past >= 0, "seq_kv must be >= seq_len"
-    assert seq_kv % block_N == 0, "no key-padding mask: seq_kv must be a multiple of block_N"
+    # key-padding mask (reference example_mha_fwd_bshd.py:54): with seq_kv not a multiple of
+    # block_N, keys at or past seq_kv get -inf in the LAST KV tile only (a uniform branch: the
+    # interior tiles pay nothing); the causal mask already hides them from every stored row
+    ragged_kv = seq_kv % block_N != 0 and not is_causal
     bhsd = layout == "bhsd"
     assert layout in ("bshd", "bhsd")
     q_shape = [batch, heads, seq_len, dim] if bhsd else [batch, seq_len, heads, dim]
@@ -137,7 +140,8 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                     T.set_priority(1)
 
             if is_causal:
-                loop_range = T.ceildiv((bx + 1) * block_M, block_N) if past == 0 else T.min(
+                exact = past == 0 and seq_len % block_M == 0  # no tile runs past the last key tile
+                loop_range = T.ceildiv((bx + 1) * block_M, block_N) if exact else T.min(
                     T.ceildiv((bx + 1) * block_M + past, block_N), T.ceildiv(seq_kv, block_N))
             else:
                 loop_range = T.ceildiv(seq_kv, block_N)
@@ -166,6 +170,14 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                             for i, j in T.Parallel(block_M, block_N):
                                 acc_s[i, j] = T.if_then_else(bx * block_M + i + past >= k * block_N + j,
                                                              -scores_max[i], -T.infinity(acc_s.dtype))
+                    elif ragged_kv:
+                        if k == loop_range - 1:
+                            for i, j in T.Parallel(block_M, block_N):
+                                acc_s[i, j] = T.if_then_else(k * block_N + j < seq_kv, -scores_max[i],
+                                                             -T.infinity(acc_s.dtype))
+                        else:
+                            for i, j in T.Parallel(block_M, block_N):
+                                acc_s[i, j] = -scores_max[i]
                     else:
                         for i, j in T.Parallel(block_M, block_N):
                             acc_s[i, j] = -scores_max[i]
@@ -236,6 +248,12 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                             for i, j in T.Parallel(block_M, block_N):
                                 acc_s[i, j] = T.if_then_else(bx * block_M + i + past >= k * block_N + j, 0,
                                                              -T.infinity(acc_s.dtype))
+                    elif ragged_kv:
+                        if k == loop_range - 1:
+                            for i, j in T.Parallel(block_M, block_N):
+                                acc_s[i, j] = T.if_then_else(k * block_N + j < seq_kv, 0, -T.infinity(acc_s.dtype))
+                        else:
+                            T.clear(acc_s)
                     else:
                         T.clear(acc_s)
                     T.gemm(Q_s, K_shared, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow, mfma_shape=mfma)

@@ -791,6 +791,34 @@ def test_mask_op(dev, kind):
     torch.testing.assert_close(k(a), a)
 
 
+def mask_dyn_program(lo, hi):
+    n = T.dynamic("n")
+
+    @T.prim_func
+    def main(A: T.Tensor((n, ), "float32"), B: T.Tensor((n, ), "float32")):
+        with T.Kernel(1, threads=256):
+            tx = T.get_thread_binding(0)
+            if tx >= lo and tx < hi:
+                for i in T.Parallel(A.shape[0]):  # dynamic extent: lower_dynamic_nest
+                    B[i] = A[i] * 2.0
+
+    return main
+
+
+def test_mask_op_dynamic_source():
+    # the dynamic-extent nest is strided over the hi - lo threads of the condition
+    src = tilelang.lower(mask_dyn_program(128, 256), target="hip").kernel_source
+    assert "* 128)" in src and "- 128)" in src
+
+
+@pytest.mark.parametrize("dev", GPU)
+@pytest.mark.parametrize("lo,hi", [(0, 128), (64, 192)])
+def test_mask_op_dynamic(dev, lo, hi):
+    k = _compile(mask_dyn_program(lo, hi), dev, out_idx=[1])
+    a = torch.randn(1000, device=dev)
+    torch.testing.assert_close(k(a), a * 2)
+
+
 # ---- test_tilelang_language_negative_index.py ---------------------------------------------
 
 

@@ -75,8 +75,30 @@ def _headers_digest() -> str:
         for f in sorted(Path(INCLUDE_DIR).rglob("*.h")):
             h.update(str(f.relative_to(INCLUDE_DIR)).encode())
             h.update(f.read_bytes())
+        # the ROCm HIP headers and clang's HIP wrappers that tl.h pulls in: a ROCm update that
+        # keeps the clang version line must not reuse a stale PCH (-fno-validate-pch below)
+        for d in _system_header_dirs():
+            for f in sorted(Path(d).rglob("*.h")):
+                st = f.stat()
+                h.update(f"{f}\0{st.st_size}\0{st.st_mtime_ns}".encode())
         _hdr_digest = h.hexdigest()
     return _hdr_digest
+
+
+def _system_header_dirs() -> List[str]:
+    """The HIP include dir and clang's resource include dir (HIP wrapper headers)."""
+    dirs = []
+    try:
+        rd = subprocess.run([clang_path(), "-print-resource-dir"], capture_output=True, text=True,
+                            timeout=60).stdout.strip()
+        if rd and os.path.isdir(os.path.join(rd, "include")):
+            dirs.append(os.path.join(rd, "include"))
+    except Exception:  # noqa: BLE001
+        pass
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    if os.path.isdir(os.path.join(rocm, "include", "hip")):
+        dirs.append(os.path.join(rocm, "include", "hip"))
+    return dirs
 
 
 def _base_cmd(arch: str) -> List[str]:
@@ -157,11 +179,15 @@ def compile_hip(source: str, arch: str = ARCH, options: Optional[List[str]] = No
 
         cmd, r = run(pch)
         if r.returncode != 0 and pch:
-            with _pch_lock:  # a PCH the toolchain rejects: drop it for this process
-                for k, v in list(_pch_paths.items()):
-                    if v == pch:
-                        _pch_paths[k] = None
             cmd, r = run(None)
+            if r.returncode == 0:
+                # only the PCH compile failed: the toolchain rejects the PCH, drop it for this
+                # process.  A kernel that fails both ways has an error of its own (an autotune
+                # config that does not compile) and keeps the PCH for every later kernel
+                with _pch_lock:
+                    for k, v in list(_pch_paths.items()):
+                        if v == pch:
+                            _pch_paths[k] = None
         if r.returncode != 0:
             numbered = "\n".join(f"{i + 1:4d}  {ln}" for i, ln in enumerate(source.splitlines()))
             raise CompileError(f"hipcc failed ({' '.join(cmd)}):\n{r.stderr}\n--- source ---\n{numbered}")

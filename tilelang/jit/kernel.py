@@ -54,21 +54,46 @@ def _scalar_type_code(dtype) -> int:
     return _SCALAR_TYPES[key]
 
 
+def _linear_in(e, n):
+    """(a, b) with ``e == a * n + b`` proved on the IR: only ``+``, ``-``, ``*`` by a constant and
+    casts are walked; ``min``/``max``/``//``/``%`` or anything else is not affine -> None."""
+    from ..ir.expr import BinOp, Cast, as_int
+    c = as_int(e)
+    if c is not None:
+        return (0, c)
+    if e is n:
+        return (1, 0)
+    if isinstance(e, Cast):
+        return _linear_in(e.value, n)
+    if isinstance(e, BinOp) and e.op in ("+", "-"):
+        la, lb = _linear_in(e.a, n), _linear_in(e.b, n)
+        if la is None or lb is None:
+            return None
+        sg = 1 if e.op == "+" else -1
+        return (la[0] + sg * lb[0], la[1] + sg * lb[1])
+    if isinstance(e, BinOp) and e.op == "*":
+        ca, cb = as_int(e.a), as_int(e.b)
+        if cb is not None:
+            la = _linear_in(e.a, n)
+            return None if la is None else (la[0] * cb, la[1] * cb)
+        if ca is not None:
+            lb = _linear_in(e.b, n)
+            return None if lb is None else (lb[0] * ca, lb[1] * ca)
+    return None
+
+
 def _affine_of(e, symtab):
-    """(symbol id, a, b) when ``e`` is ``a * n + b`` (a > 0) in one shape symbol ``n``, else None."""
-    from ..ir.expr import free_vars, evaluate, EvalError
+    """(symbol id, a, b) when ``e`` is ``a * n + b`` (a > 0) in one shape symbol ``n``, else None.
+    Proved structurally (``_linear_in``): sampling a few points accepted ``T.min(n, 64)`` or
+    ``n + n // 8`` as ``n``, and the launcher would then size outputs with the wrong formula."""
+    from ..ir.expr import free_vars
     fv = [v for v in free_vars(e)]
     if len(fv) != 1 or fv[0] not in symtab:
         return None
-    n = fv[0]
-    try:
-        f0, f1, f7 = (int(evaluate(e, {n: x})) for x in (0, 1, 7))
-    except (EvalError, TypeError, ValueError):
+    ab = _linear_in(e, fv[0])
+    if ab is None or ab[0] <= 0:
         return None
-    a, b = f1 - f0, f0
-    if a <= 0 or f7 != 7 * a + b:
-        return None
-    return (symtab[n], a, b)
+    return (symtab[fv[0]], ab[0], ab[1])
 
 
 class JITKernel:

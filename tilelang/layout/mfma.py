@@ -104,12 +104,16 @@ def mfma_c_fragment_direct(M: int, N: int, warp_m: int, warp_n: int) -> Fragment
     return Fragment([M, N], _drop_unit(thread), _drop_unit(local), "mfma_c16_direct")
 
 
-def mfma_a_fragment(M: int, K: int, warp_m: int, warp_n: int, kperm: int = 0, mn=(16, 16)) -> Fragment:
+def mfma_a_fragment(M: int, K: int, warp_m: int, warp_n: int, kperm: int = 0, mn=(16, 16),
+                    trans: bool = False) -> Fragment:
     """A operand held in registers (gemm_rs).  Replicated over the ``warp_n`` waves.
+    ``trans``: the tile is stored [K, M] (``T.gemm(transpose_A=True)``): same registers, dims swapped.
 
     kperm=0: natural  k = 32*kk + 8*g + j
     kperm=1: C-layout compatible  k = 32*kk + 16*h + 4*g + v   (local order kk, h, v)
     """
+    if trans:
+        return transpose_fragment(mfma_a_fragment(M, K, warp_m, warp_n, kperm, mn))
     WM = M // warp_m
     if mn == (32, 32):
         return _mfma_a_fragment32(M, K, warp_m, warp_n, kperm)
@@ -125,6 +129,19 @@ def mfma_a_fragment(M: int, K: int, warp_m: int, warp_n: int, kperm: int = 0, mn
         thread += [Digit(1, 4, 4), Digit(0, 1, 16)]
         local = [Digit(0, 16, m_rep), Digit(1, 16, 2 * kk), Digit(1, 1, 4)]
     return Fragment([M, K], _drop_unit(thread), _drop_unit(local), f"mfma_a_kperm{kperm}")
+
+
+def transpose_fragment(f: Fragment) -> Fragment:
+    """The same thread/register distribution over the transposed 2-D tile (dims 0 and 1 swapped):
+    a register A operand stored [K, M] (``transpose_A``) holds exactly the values, registers and
+    lanes of its [M, K] layout, so the MFMA consumes it unchanged."""
+    sw = {0: 1, 1: 0}
+
+    def flip(ds):
+        return [Digit(sw.get(d.dim, d.dim), d.stride, d.size) for d in ds]
+
+    return Fragment([f.shape[1], f.shape[0]], flip(f.thread_digits), flip(f.local_digits), f.name + "_t",
+                    f.thread_offset)
 
 
 def _mfma_a_fragment32(M: int, K: int, warp_m: int, warp_n: int, kperm: int) -> Fragment:

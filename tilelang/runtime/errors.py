@@ -76,6 +76,7 @@ class _Ring:
 
 
 _rings = {}
+_captured = {}  # id -> (error word, label, decoder) of launches recorded during a graph capture
 
 
 def _ring(word) -> _Ring:
@@ -89,11 +90,20 @@ def _ring(word) -> _Ring:
 def record(word, label: str, decoder=None):
     """Queue a non-blocking read-back of ``word`` behind the launch just issued on the current
     stream (call right after the launch)."""
+    import torch
+    if torch.cuda.is_current_stream_capturing():
+        # inside tilelang.runtime.graph.capture: an event record + host sync on the launch path
+        # is illegal there, and a captured read-back would only report the capture-time launch.
+        # Replayed graphs leave the error word set; errors.check() after a replay reads it
+        with _lock:
+            _captured[id(word)] = (word, label, decoder or _grid_decoder)
+        return
     with _lock:
         ring = _ring(word)
         i = ring.next
         ring.next = (i + 1) % ring.SIZE
-    if ring.busy[i]:
+        wrapped = ring.busy[i]
+    if wrapped:
         # the ring wrapped onto a read-back that was never polled: retire the oldest entries
         _drain_slot(ring, i)
     ring.views[i].copy_(word, non_blocking=True)
@@ -106,7 +116,9 @@ def record(word, label: str, decoder=None):
 def _drain_slot(ring, i):
     ring.events[i].synchronize()
     poll()
-    if ring.busy[i]:  # still queued behind an unfinished entry: drop it (it was clean or raised)
+    with _lock:
+        still = ring.busy[i]
+    if still:  # still queued behind an unfinished entry: drop it (it was clean or raised)
         with _lock:
             keep = [p for p in _pending if not (p[0] is ring and p[1] == i)]
             _pending.clear()
@@ -145,11 +157,19 @@ def poll():
 
 
 def check():
-    """Synchronise the current device and raise any recorded device error."""
+    """Synchronise the current device and raise any recorded device error (including the error
+    words of launches recorded inside a hipGraph capture, read here synchronously)."""
     import torch
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     poll()
+    with _lock:
+        words = list(_captured.values())
+    for word, label, dec in words:
+        code = int(word.item())
+        if code:
+            word.zero_()
+            raise dec(label, code)
 
 
 def pending() -> int:

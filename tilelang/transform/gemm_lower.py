@@ -131,10 +131,8 @@ def _try_32x32(op: O.GemmOp, plan: Dict, nw: int, num_threads: int = 0, a_layout
     plan.update(warp_m=warp_m, warp_n=warp_n, mfma=(32, 32, 16))
     plan["c_layout"] = MF.mfma_c_fragment(M, N, warp_m, warp_n, (32, 32))
     if A.scope == "fragment":
-        if op.trans_A:
-            return None
         if a_layout is not None:
-            k1 = MF.mfma_a_fragment(M, K, warp_m, warp_n, 1, (32, 32))
+            k1 = MF.mfma_a_fragment(M, K, warp_m, warp_n, 1, (32, 32), op.trans_A)
             k1r = k1 if k1.num_threads == num_threads else k1.replicate(num_threads // k1.num_threads)
             if a_layout.is_equal(k1r) or a_layout.is_equal(k1):
                 plan["a_kperm"] = 1
@@ -283,7 +281,7 @@ def gemm_plan(op: O.GemmOp, num_threads: int, target=None, a_layout: Optional[Fr
     if K % 32:
         raise ValueError(f"T.gemm K={K} must be a multiple of 32 on gfx950 (MFMA 16x16x32)")
     if a_layout is not None and A.scope == "fragment":
-        k1 = MF.mfma_a_fragment(M, K, warp_m, warp_n, 1)
+        k1 = MF.mfma_a_fragment(M, K, warp_m, warp_n, 1, trans=op.trans_A)
         k1r = k1 if k1.num_threads == num_threads else k1.replicate(num_threads // k1.num_threads)
         if a_layout.is_equal(k1r) or a_layout.is_equal(k1):
             plan["a_kperm"] = 1

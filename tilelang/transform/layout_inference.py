@@ -417,8 +417,8 @@ class LayoutInference:
         elif _is_frag(A):
             lay_cur = self.frag.get(A)
             mn = tuple(plan["mfma"][:2]) if plan["mfma"][:2] == (32, 32) else (16, 16)
-            k0 = MF.mfma_a_fragment(plan["M"], plan["K"], plan["warp_m"], plan["warp_n"], 0, mn)
-            k1 = MF.mfma_a_fragment(plan["M"], plan["K"], plan["warp_m"], plan["warp_n"], 1, mn)
+            k0 = MF.mfma_a_fragment(plan["M"], plan["K"], plan["warp_m"], plan["warp_n"], 0, mn, op.trans_A)
+            k1 = MF.mfma_a_fragment(plan["M"], plan["K"], plan["warp_m"], plan["warp_n"], 1, mn, op.trans_A)
             if lay_cur is not None:
                 if lay_cur.is_equal(k1) or _equal_rep(lay_cur, k1, self.T):
                     plan["a_kperm"] = 1

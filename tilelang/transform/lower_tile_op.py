@@ -1087,18 +1087,31 @@ class TileOpLowerer(Mutator):
             out.append(S.IfStmt(guard, blk) if guard is not None else blk)
         return S.SeqStmt(out)
 
+    def _no_thread_range(self, op):
+        """Paths that spread their work over all ctx.T threads refuse ``if lo <= tx < hi``
+        partitioning instead of silently skipping the elements of the idle threads."""
+        if self.ctx.thread_range is not None:
+            raise LoweringError(f"{type(op).__name__} inside a thread-range condition "
+                                f"(threads {self.ctx.thread_range[0]}..{self.ctx.thread_range[1] - 1} of "
+                                f"{self.ctx.T}) is not supported: move it out of the condition")
+
     def lower_dynamic_nest(self, nest: ParallelNest) -> S.Stmt:
         ctx = self.ctx
         total = const(1)
         for l in nest.loops:
             total = total * l.extent
         it = Var("it")
-        lin = binop("+", binop("*", it, ctx.T), ctx.tid)
+        T, tid = ctx.T, ctx.tid
+        if ctx.thread_range is not None:
+            # under ``if lo <= tx < hi`` only those hi - lo threads run the nest (as lower_simt_nest)
+            lo, hi = ctx.thread_range
+            T, tid = hi - lo, (binop("-", ctx.tid, lo) if lo else ctx.tid)
+        lin = binop("+", binop("*", it, T), tid)
         vals = _unflatten_dyn(lin, [l.extent for l in nest.loops])
         vmap = {var: binop("+", m, x) for var, m, x in zip(nest.vars, nest.mins, vals)}
         body = _SimtRewriter(ctx, vmap).stmt(nest.body)
         from ..ir.expr import ceildiv
-        n_it = ceildiv(total, ctx.T)
+        n_it = ceildiv(total, T)
         return S.ForStmt(it, 0, n_it, "serial", S.IfStmt(binop("<", lin, total), body))
 
     def _vec_ok(self, nest: ParallelNest, vec: int) -> bool:
@@ -1351,8 +1364,8 @@ class TileOpLowerer(Mutator):
             ]))
         elif A.scope == "fragment":
             al = ctx.local_of(A)
-            if op.trans_A:
-                raise LoweringError("register A operand cannot be transposed")
+            # transpose_A: the fragment is the [M, K] layout with its dims swapped
+            # (layout.mfma.transpose_fragment): the registers are consumed unchanged
             vmin = [self.expr(op.valid_m_min)] if getattr(op, "valid_m_min", None) is not None else []
             out.append(L.CallStmt("tl::gemm_rs", [L.BufferPtr(al, 0), pb, L.BufferPtr(cl, 0), ctx.wave_expr()] + vmin, [
                 ctype, plan["M"], plan["N"], plan["K"], plan["warp_m"], plan["warp_n"], _b(op.trans_B), b_cols,
@@ -1589,6 +1602,7 @@ class TileOpLowerer(Mutator):
 
     def lower_reduce_simt(self, op: O.ReduceOp):
         """Reduction over shared/local buffers: each thread reduces whole rows serially."""
+        self._no_thread_range(op)
         ctx = self.ctx
         src, dst = op.src, op.dst
         sext = src.static_extents()
@@ -1632,6 +1646,7 @@ class TileOpLowerer(Mutator):
 
     def lower_CumSumOp(self, op: O.CumSumOp):
         """Inclusive scan along ``dim`` for shared/global buffers (one thread per row)."""
+        self._no_thread_range(op)
         ctx = self.ctx
         src, dst = op.src, op.dst
         frag = src.buffer.scope == "fragment" or dst.buffer.scope == "fragment"
@@ -2395,6 +2410,8 @@ def _partner_offsets(tid, wave_digits):
 
 def _simt_copy_steps(ctx: LowerCtx, src: BufferRegion, dst: BufferRegion, known_div) -> List[dict]:
     """Thread mapping of a plain copy: list of per-step {src_idx, dst_idx, vec, guard}."""
+    if ctx.thread_range is not None:
+        raise LoweringError("a register-staged copy inside a thread-range condition is not supported")
     sd, dd = _squeeze_pairs(src, dst)
     exts = [as_int(dst.extents[d]) for d in dd]
     if any(e is None for e in exts):

@@ -793,6 +793,17 @@ def _quad_schedule(self, loop, asyncs, consumer_stmts, newbufs, ranges):
     a_src, a_rdim, idx, a_mode = tiles[A]
     if x is not None and tiles[x.A.buffer][3] != a_mode:
         return None
+    if a_mode:
+        # gathered / range-checked rows: tl::gemm_quad_nt_x forms the byte offsets of the rows and
+        # the buffer resource's range in 32 bits (tl/gemm_quad.h), as the dense DMA plan's own
+        # numel * eb < 2^31 condition; a larger A runs the generic pipeline
+        numel = 1
+        for s_ in a_src.buffer.shape:
+            if as_int(s_) is None:
+                return None
+            numel *= as_int(s_)
+        if numel * a_src.buffer.dtype.bytes >= (1 << 31):
+            return None
     if a_mode and a_rdim != 0:
         return None
     op = QuadGemmLoopOp(a_src, a_rdim, idx, tiles[B][0], tiles[B][1], newbufs[A], newbufs[B],
