@@ -54,8 +54,10 @@ GEMM_CFG = dict(M=4096, N=4096, K=4096, block_M=256, block_N=256, block_K=64, th
 # (+5-8 %), young_prio: waves 4-7 at issue priority 1 (+1-2 %, profiles/r4/fa_fold_ab.log; re-measured
 # r5 round-robin in one process: 937.5 vs 928.4 TF sustained, profiles/r5/fa_ab_roundrobin.log)
 # xcd_heads: all query tiles of a head on one XCD, K/V read through one L2 (+2-5 %, profiles/r4/fa_xcd.log)
+# unroll=2: the main loop as two copies, so both LDS ring slots are compile-time offsets (no per-tile
+# address VALU): 1089 -> 1094 TF, same process, round-robin (profiles/r6/fa_unroll_ab.log)
 ATTN_CFG = dict(batch=1, heads=64, seq_len=4096, dim=128, block_M=256, block_N=64, threads=512, num_stages=2,
-                q_in_regs=True, sum_mfma=True, fold_max=True, young_prio=True, xcd_heads=True)
+                q_in_regs=True, sum_mfma=True, fold_max=True, young_prio=True, xcd_heads=True, unroll=2)
 MOE_CFG = dict(tokens=2048, hidden=4096, ffn=2048, experts=8, topk=2)
 # expert row tiles of 256 + MOE_EXT_M rows, every expert's rows spread evenly over its tiles
 # (ops/moe.py expert_gemm_sk_kernel ext_M): a random-routing expert of ~529 rows is two units, not three
@@ -110,7 +112,8 @@ def build_attn(device="cuda", a=None):
                           a["threads"], a["num_stages"], "bfloat16", True, a.get("q_in_regs", False),
                           sum_mfma=a.get("sum_mfma", False), fold_max=a.get("fold_max", False),
                           young_prio=a.get("young_prio", False), pk_scale=a.get("pk_scale", False),
-                          pingpong=a.get("pingpong", False), xcd_heads=a.get("xcd_heads", False))
+                          pingpong=a.get("pingpong", False), xcd_heads=a.get("xcd_heads", False),
+                          unroll=a.get("unroll"))
     pc = dict(flashattn.pass_configs)
     pc.update(a.get("pass_configs", {}))
     k = tilelang.compile(f, out_idx=[3], target=_target(device), pass_configs=pc)
@@ -396,6 +399,18 @@ def main():
     for _ in range(3):  # hipBLASLt loads and selects its kernel on the first calls
         torch.matmul(A, Bkn)
     vendor_ms = timed(lambda: torch.matmul(A, Bkn), reps)
+    # the same normaliser for attention: PyTorch's fused SDPA (the ROCm flash-attention backend)
+    # on the bench shape, bf16, non-causal, same process
+    attn_vendor_ms = None
+    if not cpu:
+        try:
+            qs, ks_, vs_ = (t.transpose(1, 2) for t in (Q, K, V))
+            sdpa = torch.nn.functional.scaled_dot_product_attention
+            for _ in range(3):
+                sdpa(qs, ks_, vs_)
+            attn_vendor_ms = timed(lambda: sdpa(qs, ks_, vs_), reps)
+        except Exception:  # noqa: BLE001  (a normaliser only: never fatal)
+            attn_vendor_ms = None
     dev_id = -1 if cpu else torch.cuda.current_device()
     bus = "cpu" if cpu else str(getattr(torch.cuda.get_device_properties(dev_id), "pci_bus_id", dev_id))
     ids = [None] * world
@@ -442,6 +457,7 @@ def main():
             "gemm_tflops": round(gemm_flops / gemm_ms / 1e9, 1),
             "gemm_vendor_tflops": round(gemm_flops / vendor_ms / 1e9, 1),
             "attn_tflops": round(attn_flops / attn_ms / 1e9, 1),
+            "attn_vendor_tflops": (round(attn_flops / attn_vendor_ms / 1e9, 1) if attn_vendor_ms else None),
             "moe_tflops_per_gpu": round(moe_flops / moe_ms / 1e9, 1) if moe is not None else None,
             "moe_comm_fraction": round(moe_comm_ms / moe_ms, 3) if moe is not None and moe_ms > 0 else None,
             "phase_timing": ("wall, 1 call per rep" if (cpu or dist is not None) else

@@ -27,7 +27,7 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                         threads=512, num_stages=3, dtype="bfloat16", lazy_rescale=True, q_in_regs=True,
                         young_prio=False, staged_epilogue=False, seq_kv=None, layout="bshd", mfma="16x16",
                         sum_mfma=False, sink=False, sm_scale=None, fold_max=False, prescale_q=False,
-                        pingpong=False, pk_scale=False, xcd_heads=False, skip_masked=True):
+                        pingpong=False, pk_scale=False, xcd_heads=False, skip_masked=True, unroll=None):
     """``young_prio``: the second-dispatched half of the waves runs at issue priority 1 (one
     ``s_setprio`` before the main loop; MI355X notes 'Two waves per SIMD', item 4).
     ``seq_kv`` (default ``seq_len``): key/value length; with ``is_causal`` the mask is aligned
@@ -154,7 +154,8 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
                 for k in T.Pipelined(loop_range, num_stages=num_stages, order=[-1, 0, 1, 2, -1, 3, 4],
                                      stage=[-1, 0, 1, 0, -1, 1, 0], group=fold_group,
                                      order_alt=[-1, 2, 0, 3, -1, 1, 4] if pingpong else None,
-                                     alt_cond=(T.get_thread_binding() >= threads // 2) if pingpong else None):
+                                     alt_cond=(T.get_thread_binding() >= threads // 2) if pingpong else None,
+                                     unroll=unroll):
                     # 0: K tile (producer)
                     if bhsd:
                         T.copy(K[bz, by // groups, k * block_N:(k + 1) * block_N, :], K_shared)

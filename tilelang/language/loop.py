@@ -119,7 +119,7 @@ def grid(*extents):
 
 
 def Pipelined(start, stop=None, num_stages: int = 0, order=None, stage=None, sync=None, group=None, order_alt=None,
-              alt_cond=None):
+              alt_cond=None, unroll: Optional[int] = None):
     """Software-pipelined loop: copies into shared buffers are multi-buffered ``num_stages`` deep.
 
     On gfx950 the global->LDS copies become ``global_load_lds_dwordx4`` DMA issued
@@ -129,8 +129,12 @@ def Pipelined(start, stop=None, num_stages: int = 0, order=None, stage=None, syn
     accepted and recorded but has no effect, exactly as in the reference (``src/ir.cc:105`` sets
     ``tl_pipeline_sync`` and no pass reads it); LDS hazards between the scheduled statements get
     their barriers from the thread-sync pass, which proves them per access.
+    ``unroll``: the lowered main loop is emitted under ``#pragma unroll N`` (with N a multiple of
+    the ring depth every ring slot index of an unrolled copy is a compile-time constant).
     """
     ann = {"num_stages": int(num_stages)}
+    if unroll is not None:
+        ann["unroll_factor"] = int(unroll)
     if order is not None:
         ann["order"] = list(order)
     if stage is not None:

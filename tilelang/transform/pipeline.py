@@ -623,8 +623,10 @@ class PipelineInjector(Mutator):
         if staged:
             j1 = binop("+", kk, 1)
             body.append(S.IfStmt(binop("<", j1, n), S.seq(*staged_phase(j1, binop("%", j1, nstages), "store"))))
-        new_loop = S.ForStmt(k, loop.min, loop.extent, "serial", S.SeqStmt(body),
-                             {"pipelined": nstages, "_lets": lets})
+        ann_new = {"pipelined": nstages, "_lets": lets}
+        if loop.annotations.get("unroll_factor"):
+            ann_new["unroll_factor"] = loop.annotations["unroll_factor"]
+        new_loop = S.ForStmt(k, loop.min, loop.extent, "serial", S.SeqStmt(body), ann_new)
         # allocations for the new multi-versioned buffers replace the old ones (done by caller)
         self.replaced = getattr(self, "replaced", {})
         for B, NB in newbufs.items():
