@@ -421,7 +421,17 @@ def main():
 
     t = torch.tensor([elapsed, gemm_ms, attn_ms, moe_ms, moe_comm_ms, vendor_ms], dtype=torch.float64,
                      device="cpu" if cpu else "cuda")
+    # per-rank phase times (ms) and the world size the backend itself reports: a one-element
+    # all_reduce of ones over RCCL (nccl) / gloo
+    per_rank = [t.tolist()]
+    world_seen = 1
     if dist is not None:
+        g_ = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(g_, t)
+        per_rank = [x.tolist() for x in g_]
+        one = torch.ones(1, dtype=torch.int32, device="cpu" if cpu else "cuda")
+        dist.all_reduce(one)
+        world_seen = int(one.item())
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, gemm_ms, attn_ms, moe_ms, moe_comm_ms, vendor_ms = t.tolist()
     ms_per_step = elapsed / args.steps * 1e3
@@ -464,7 +474,8 @@ def main():
                              "device time (events behind a queue-filling blocker), 10 calls"),
             "host_ms_per_call": host_ms or None,
             "ep_exchange": (None if mesh is None or moe is None else
-                            ("device (tl/ep.h, IPC over xGMI, no host sync)" if moe._device_ep() else
+                            (("device (tl/ep_cpu.h protocol over /dev/shm, no host sync)" if cpu else
+                              "device (tl/ep.h, IPC over xGMI, no host sync)") if moe._device_ep() else
                              f"host ({'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()} "
                              "all_to_all_v)")),
             "ep_fallback_reason": ep_note,
@@ -483,6 +494,10 @@ def main():
             "moe_dtype": "bfloat16",
             "device": args.device,
             "world_size": (dist.get_world_size() if dist is not None else 1),
+            "dist_world_observed": world_seen,
+            "per_rank_ms": [{"rank": r, "steps_total": round(v[0] * 1e3, 3), "gemm": round(v[1], 4),
+                             "attn": round(v[2], 4), "moe": round(v[3], 4), "moe_comm": round(v[4], 4)}
+                            for r, v in enumerate(per_rank)],
             "backend": (dist.get_backend() if dist is not None else None),
             "ranks": [{"rank": r, "local_rank": lr, "device": d, "pci_bus": b} for r, lr, d, b in ids],
         }

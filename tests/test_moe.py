@@ -165,7 +165,7 @@ def test_fused_router_cpu(dt):
 
 
 def _mesh_moe_worker(rank, world, port, mode, q):
-    """One rank of a 2-process mesh sharing GPU 0 (or its own GPU on a multi-GPU box): the EP
+    """One rank of a 2- or 4-process mesh sharing GPU 0 (or its own GPU on a multi-GPU box): the EP
     (device exchange, tl/ep.h) or TP (in-kernel all-reduce) MoE layer vs the fp32 definition."""
     import os
     import torch.distributed as dist
@@ -206,8 +206,9 @@ def _mesh_moe_worker(rank, world, port, mode, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["ep", "tp", "ep_ext"])
-def test_moe_mesh_two_processes_gpu(mode):
+@pytest.mark.parametrize("mode,world", [("ep", 2), ("tp", 2), ("ep_ext", 2), ("ep", 4), ("tp", 4)])
+def test_moe_mesh_processes_gpu(mode, world):
+    """2 and 4 processes sharing the box's GPU (distinct GPUs on a multi-GPU box)."""
     import socket
     import torch.multiprocessing as mp
     with socket.socket() as s:
@@ -215,13 +216,13 @@ def test_moe_mesh_two_processes_gpu(mode):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_mesh_moe_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    ps = [ctx.Process(target=_mesh_moe_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=400) for _ in range(2))
+    res = dict(q.get(timeout=400) for _ in range(world))
     for p in ps:
         p.join(timeout=60)
-    assert res == {0: "ok", 1: "ok"}, res
+    assert res == {r: "ok" for r in range(world)}, res
 
 
 def test_ep_kernels_compile():
@@ -268,7 +269,7 @@ def test_moe_tail_ksplit_gpu(S):
     _tail_ksplit_check("cuda", S)
 
 
-def _dead_peer_worker(rank, world, port, q):
+def _dead_peer_worker(rank, world, port, q, device="cuda"):
     """Rank 1 skips the expert-parallel layer of step 1 (a dead or diverged peer): rank 0's
     device exchange must raise MeshError within ONE wait budget (TL_EP_TIMEOUT_S = 2 s; every
     later wait of the step gives up at once), then both ranks fall back to the host all-to-all
@@ -283,23 +284,29 @@ def _dead_peer_worker(rank, world, port, q):
         from tilelang.parallel.mesh import MeshError
         from tilelang.runtime import errors
         from tilelang.ops import moe as K
-        dev = f"cuda:{rank % torch.cuda.device_count()}"
-        torch.cuda.set_device(dev)
+        if device == "cpu":  # the CPU build of the exchange (tl/ep_cpu.h) over /dev/shm
+            dev = "cpu"
+            cfg = MoEConfig(hidden=64, ffn=128, n_experts=8, topk=2, dtype=torch.float32, block_M=16)
+        else:
+            dev = f"cuda:{rank % torch.cuda.device_count()}"
+            torch.cuda.set_device(dev)
+            cfg = MoEConfig(hidden=512, ffn=256, n_experts=8, topk=2, dtype=torch.bfloat16, block_M=128)
         mesh = init_mesh(1, world, device=dev)
-        cfg = MoEConfig(hidden=512, ffn=256, n_experts=8, topk=2, dtype=torch.bfloat16, block_M=128)
         layer = MoELayer(cfg, "ep", mesh=mesh, device=dev)
         g, w1, w2 = (t.to(dev) for t in init_moe_weights(cfg))
         torch.manual_seed(7 + rank)
         x = torch.randn(256, cfg.hidden, device=dev).to(cfg.dtype)
         layer(x)
-        errors.check()  # step 0: both ranks healthy
+        if dev != "cpu":
+            errors.check()  # step 0: both ranks healthy
         dist.barrier()
         elapsed, raised = None, None
         if rank == 0:
             t0 = time.time()
             try:
                 layer(x)
-                errors.check()
+                if dev != "cpu":
+                    errors.check()
                 mesh.check()
             except MeshError as e:
                 raised = str(e)
@@ -328,8 +335,8 @@ def _dead_peer_worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.gpu
-def test_ep_dead_peer_fails_fast_gpu():
+@pytest.mark.parametrize("device", [pytest.param("cuda", marks=pytest.mark.gpu), "cpu"])
+def test_ep_dead_peer_fails_fast(device):
     import socket
     import torch.multiprocessing as mp
     with socket.socket() as s:
@@ -337,7 +344,7 @@ def test_ep_dead_peer_fails_fast_gpu():
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_dead_peer_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_dead_peer_worker, args=(r, 2, port, q, device)) for r in range(2)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(2))

@@ -361,3 +361,4 @@ inline void cpu_gemm_sp(const T* A, const int16_t* E, const T* B, float* C) {
 
 }  // namespace tl
 #include "mesh_cpu.h"
+#include "ep_cpu.h"

@@ -144,10 +144,10 @@ class MoELayer(torch.nn.Module):
         return K.combine(y, torch.arange(y.shape[0], device=x.device, dtype=torch.int32), wts)
 
     def _device_ep(self) -> bool:
-        """GPU process meshes exchange tokens with device kernels over IPC (ops/ep.py); CPU and
-        virtual meshes use the host collectives."""
+        """Process meshes exchange tokens with the device protocol (ops/ep.py: tl/ep.h over IPC on
+        GPUs, tl/ep_cpu.h over /dev/shm on CPU gloo meshes); virtual meshes use the host collectives."""
         from ..parallel.mesh import ProcessMesh
-        return isinstance(self.mesh, ProcessMesh) and self.mesh.device.type == "cuda" and self.ep_mode == "device"
+        return isinstance(self.mesh, ProcessMesh) and self.ep_mode == "device"
 
     # "device" (ops/ep.py, no host sync) or "host" (RCCL all_to_all_v); TL_EP_MODE overrides
     ep_mode = os.environ.get("TL_EP_MODE", "device")

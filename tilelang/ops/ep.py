@@ -49,9 +49,16 @@ def layout_bytes(W: int, cap: int, row_bytes: int):
     return eids, recv, ret, ret + 2 * W * cap * row_bytes
 
 
+def _blocks(target: str, n: int) -> int:
+    # the CPU target runs blocks one after another: tl/ep_cpu.h does a whole grid's work in one
+    return 1 if target == "cpu" else n
+
+
 @functools.lru_cache(maxsize=None)
-def dispatch_kernel(n_tok: int, H: int, topk: int, W: int, n_loc: int, cap: int, dtype: str, blocks: int = 128):
+def dispatch_kernel(n_tok: int, H: int, topk: int, W: int, n_loc: int, cap: int, dtype: str, blocks: int = 128,
+                    target: str = "hip"):
     P = n_tok * topk
+    blocks = _blocks(target, blocks)
     eb = {"float16": 2, "bfloat16": 2, "float32": 4}[dtype]
 
     @T.prim_func
@@ -61,11 +68,12 @@ def dispatch_kernel(n_tok: int, H: int, topk: int, W: int, n_loc: int, cap: int,
             T.evaluate(T.call_extern("void", f"tl::ep::dispatch<{W}>", T.address_of(x[0, 0]), T.address_of(ids[0]),
                                      T.address_of(ret_index[0]), ws, me, epoch, err, P, topk, n_loc, cap, H * eb))
 
-    return tilelang.compile(ep_dispatch, target="hip", compile_flags=_flags())
+    return tilelang.compile(ep_dispatch, target=target, compile_flags=_flags())
 
 
 @functools.lru_cache(maxsize=None)
-def recv_wait_kernel(W: int, cap: int, row_bytes: int, blocks: int = 16):
+def recv_wait_kernel(W: int, cap: int, row_bytes: int, blocks: int = 16, target: str = "hip"):
+    blocks = _blocks(target, blocks)
 
     @T.prim_func
     def ep_recv_wait(ids_out: T.Tensor((W * cap, ), "int32"), cnt_out: T.Tensor((W, ), "int32"), ws: T.int64,
@@ -74,11 +82,12 @@ def recv_wait_kernel(W: int, cap: int, row_bytes: int, blocks: int = 16):
             T.evaluate(T.call_extern("void", f"tl::ep::recv_wait<{W}>", T.address_of(ids_out[0]),
                                      T.address_of(cnt_out[0]), ws, me, epoch, err, cap, row_bytes))
 
-    return tilelang.compile(ep_recv_wait, target="hip", compile_flags=_flags())
+    return tilelang.compile(ep_recv_wait, target=target, compile_flags=_flags())
 
 
 @functools.lru_cache(maxsize=None)
-def ret_kernel(rows: int, H: int, W: int, cap: int, dtype: str, blocks: int = 128):
+def ret_kernel(rows: int, H: int, W: int, cap: int, dtype: str, blocks: int = 128, target: str = "hip"):
+    blocks = _blocks(target, blocks)
     eb = {"float16": 2, "bfloat16": 2, "float32": 4}[dtype]
 
     @T.prim_func
@@ -88,22 +97,23 @@ def ret_kernel(rows: int, H: int, W: int, cap: int, dtype: str, blocks: int = 12
             T.evaluate(T.call_extern("void", f"tl::ep::ret<{W}>", T.address_of(y[0, 0]), T.address_of(ydest[0]),
                                      T.address_of(cnt[0]), ws, me, epoch, err, cap, H * eb))
 
-    return tilelang.compile(ep_ret, target="hip", compile_flags=_flags())
+    return tilelang.compile(ep_ret, target=target, compile_flags=_flags())
 
 
 @functools.lru_cache(maxsize=None)
-def ret_wait_kernel(W: int):
+def ret_wait_kernel(W: int, target: str = "hip"):
 
     @T.prim_func
     def ep_ret_wait(flag: T.Tensor((1, ), "int32"), ws: T.int64, me: T.int32, epoch: T.int32, err: T.int64):
         with T.Kernel(1, threads=64) as bx:
             T.evaluate(T.call_extern("void", f"tl::ep::ret_wait<{W}>", ws, me, epoch, err))
 
-    return tilelang.compile(ep_ret_wait, target="hip", compile_flags=_flags())
+    return tilelang.compile(ep_ret_wait, target=target, compile_flags=_flags())
 
 
 class EPExchange:
-    """Device-driven EP exchange for one MoE layer shape on a GPU ``ProcessMesh``."""
+    """Device-driven EP exchange for one MoE layer shape on a ``ProcessMesh``: a GPU mesh runs
+    tl/ep.h over IPC, a CPU (gloo) mesh runs the same protocol from tl/ep_cpu.h over /dev/shm."""
 
     def __init__(self, mesh, n_tok: int, H: int, topk: int, n_experts: int, dtype: torch.dtype, key: str = "ep"):
         W = mesh.world
@@ -120,15 +130,22 @@ class EPExchange:
         self.buf = mesh.symmetric_buffer(f"{key}:{W}x{self.cap}x{self.row_bytes}", total)
         self.epoch = 0
         dt = _tdt(dtype)
-        self.k_dispatch = dispatch_kernel(n_tok, H, topk, W, self.n_loc, self.cap, dt)
-        self.k_recv = recv_wait_kernel(W, self.cap, self.row_bytes)
-        self.k_ret_wait = ret_wait_kernel(W)
+        self.target = "cpu" if mesh.device.type == "cpu" else "hip"
+        self.k_dispatch = dispatch_kernel(n_tok, H, topk, W, self.n_loc, self.cap, dt, target=self.target)
+        self.k_recv = recv_wait_kernel(W, self.cap, self.row_bytes, target=self.target)
+        self.k_ret_wait = ret_wait_kernel(W, target=self.target)
         self._dummy = torch.zeros(1, dtype=torch.int32, device=mesh.device)
 
     def _args(self):
         return (int(self.buf.table.data_ptr()), int(self.mesh.rank), int(self.epoch), int(self.mesh.err.data_ptr()))
 
     def _watch(self, label):
+        if self.target == "cpu":  # the CPU kernels have returned: read the error word now
+            e = int(self.mesh.err.item())
+            if e:
+                self.mesh.err.zero_()
+                raise self.mesh.error_decoder(f"{label} (EP rank {self.mesh.rank})", e)
+            return
         from ..runtime import errors
         errors.record(self.mesh.err, f"{label} (EP rank {self.mesh.rank})", self.mesh.error_decoder)
 
@@ -145,8 +162,9 @@ class EPExchange:
     def dispatch(self, x: torch.Tensor, ids: torch.Tensor):
         """Send rows; returns (recv rows [W*cap, H], local expert ids [W*cap] (-1 empty),
         recv counts [W], ret_index [P])."""
-        from ..runtime import errors
-        errors.poll()
+        if self.target != "cpu":
+            from ..runtime import errors
+            errors.poll()
         self.epoch += 1
         p = self.epoch & 1
         flat = ids.reshape(-1).to(torch.int32).contiguous()
@@ -160,7 +178,7 @@ class EPExchange:
 
     def combine_rows(self, y: torch.Tensor, ydest: torch.Tensor, rcnt: torch.Tensor) -> torch.Tensor:
         """Return expert results; returns the RET row table [W*cap, H] (pair j: row ret_index[j])."""
-        k = ret_kernel(y.shape[0], self.H, self.W, self.cap, _tdt(self.dtype))
+        k = ret_kernel(y.shape[0], self.H, self.W, self.cap, _tdt(self.dtype), target=self.target)
         k(y.contiguous(), ydest.to(torch.int32).contiguous(), rcnt, *self._args())
         self.k_ret_wait(self._dummy, *self._args())
         self._watch("ep return")

@@ -306,6 +306,32 @@ class ProcessMesh(MeshContext):
         dist.broadcast_object_list(tok, src=0)
         self._uid = tok[0]
 
+    def _peer_preflight(self):
+        """Collective, once: every pair of distinct GPUs that the mesh's ranks use must have peer
+        access (hipDeviceCanAccessPeer over xGMI); fail fast with the pair instead of a kernel
+        that faults or times out on its first remote store."""
+        if self.__dict__.get("_peer_ok"):
+            return
+        import torch
+        import torch.distributed as dist
+        devs = [None] * self.world
+        dist.all_gather_object(devs, (os.uname().nodename, self.device.index))
+        mine = devs[self.rank]
+        bad = []
+        for r, d in enumerate(devs):
+            if d[0] != mine[0]:
+                bad.append((r, "on another node (IPC workspaces need one node)"))
+            elif d[1] != mine[1] and not torch.cuda.can_device_access_peer(mine[1], d[1]):
+                bad.append((r, f"GPU {mine[1]} cannot access GPU {d[1]} (hipDeviceCanAccessPeer)"))
+        flag = torch.tensor([len(bad)], dtype=torch.int32, device=self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if bad:
+            raise MeshError(f"mesh rank {self.rank}: no peer access to rank " +
+                            "; rank ".join(f"{r}: {why}" for r, why in bad))
+        if int(flag.item()):
+            raise MeshError(f"mesh rank {self.rank}: a peer rank reported missing peer access (see its error)")
+        self._peer_ok = True
+
     def group(self, direction: str):
         d = direction.lower()
         if d in ("h", "horizontal"):
@@ -330,6 +356,7 @@ class ProcessMesh(MeshContext):
         self._gen += 1
         ptrs = []
         if self.device.type == "cuda":
+            self._peer_preflight()
             from .. import _native
             rt = _native.runtime()
             dev = self.device.index
@@ -391,16 +418,30 @@ class ProcessMesh(MeshContext):
         re-allocates it (all ranks must request the same size at the same point)."""
         import torch
         import torch.distributed as dist
-        if self.device.type != "cuda":
-            raise MeshError("symmetric buffers are device memory: use a GPU mesh")
         bufs = self.__dict__.setdefault("_sym", {})
         b = bufs.get(key)
         if b is not None and b.nbytes >= nbytes:
             return b
-        torch.cuda.synchronize(self.device)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
         dist.barrier()
         if b is not None:
             b.release()
+        if self.device.type != "cuda":
+            # CPU process mesh: a zeroed /dev/shm mapping per rank, opened by every peer (the
+            # CPU build of the device protocols, tl/ep_cpu.h, runs on these)
+            self._gen += 1
+            tag = f"tl_sym_{self._uid}_{self._gen}"
+            own = _ShmBuffer(f"{tag}_{self.rank}", int(nbytes), create=True)
+            dist.barrier()
+            peers = [_ShmBuffer(f"{tag}_{r}", int(nbytes), create=False) for r in range(self.world) if r != self.rank]
+            it = iter(peers)
+            ptrs = [own.ptr() if r == self.rank else next(it).ptr() for r in range(self.world)]
+            b = _ShmSymmetricBuffer(self, own, peers, ptrs, int(nbytes))
+            bufs[key] = b
+            dist.barrier()
+            return b
+        self._peer_preflight()
         from .. import _native
         rt = _native.runtime()
         dev = self.device.index
@@ -429,6 +470,34 @@ class ProcessMesh(MeshContext):
         for b in self.__dict__.pop("_sym", {}).values():
             b.release()
         self._release()
+
+
+class _ShmSymmetricBuffer:
+    """``SymmetricBuffer`` of a CPU process mesh: /dev/shm mappings instead of IPC handles."""
+
+    def __init__(self, mesh, own, peers, ptrs, nbytes: int):
+        import torch
+        self.mesh, self.own, self.peers, self.nbytes = mesh, own, list(peers), nbytes
+        self.ptrs = list(ptrs)
+        self.local = own.tensor
+        self.table = torch.tensor(self.ptrs, dtype=torch.int64)
+
+    def view(self, offset: int, shape, dtype):
+        import math
+        import torch
+        n = math.prod(shape) * torch.empty((), dtype=dtype).element_size()
+        if offset % 16 or offset + n > self.nbytes:
+            raise ValueError(f"view [{offset}, {offset + n}) outside the {self.nbytes}-byte buffer or misaligned")
+        return self.local[offset:offset + n].view(dtype).view(*shape)
+
+    def release(self):
+        if self.own is None:
+            return
+        self.local = None
+        for q in self.peers:
+            q.close(unlink=False)
+        self.own.close(unlink=True)
+        self.own, self.peers = None, []
 
 
 class SymmetricBuffer:
