@@ -108,7 +108,8 @@ def test_amd_gemm_matrix_gpu(case):
 
 # ---- ragged shapes on the 256x256x64 / 512-thread tile (the quad-loop configuration) ----------
 
-RAGGED = [(4000, 4096, 4096), (4096, 4000, 4096), (4096, 4096, 4000), (1000, 1000, 1000), (4096, 4096, 4096)]
+RAGGED = [(4000, 4096, 4096), (4096, 4000, 4096), (4096, 4096, 4000), (1000, 1000, 1000), (4096, 4096, 4096),
+          (4000, 4000, 4000), (300, 520, 72), (257, 255, 8)]
 
 
 def _quad_kernel(M, N, K, target):
@@ -118,6 +119,18 @@ def _quad_kernel(M, N, K, target):
     from example_gemm import matmul as mm
     f = mm.get_tir(M, N, K, 256, 256, 64, 512, 2, "float16", trans_B=True, staged_epilogue=True)
     return tilelang.compile(f, out_idx=[-1], target=target)
+
+
+@pytest.mark.parametrize("M,N,K,mode", [(4096, 4096, 4096, "<half_t, false, 0>"),
+                                         (4000, 4096, 4096, "<half_t, true, 0>"),
+                                         (4096, 4000, 4096, "<half_t, false, 0, true, false>"),
+                                         (4096, 4096, 4000, "<half_t, false, 0, false, true>"),
+                                         (1000, 1000, 1000, "<half_t, true, 0, true, true>")])
+def test_quad_tile_ragged_selects_quad_loop(M, N, K, mode):
+    """Ragged M (range-checked A rows), N (range-checked B rows) and K (zero-filled last K tile)
+    all run the tl::gemm_quad_nt_x main loop, not the generic pipeline."""
+    src = _quad_kernel(M, N, K, "hip").get_kernel_source()
+    assert "tl::gemm_quad_nt_x" + mode in src
 
 
 @pytest.mark.parametrize("M,N,K", [(200, 264, 136), (256, 256, 200)])

@@ -125,10 +125,18 @@ TL_DEVICE void mma_blk(const typename qfrag<T>::F (&a)[MR][qfrag<T>::KK],
 //     the same DMAs) and multiplied in phase 1, where both B halves of the tile are resident.
 //   m_limit: T.gemm(valid_m=): waves whose 64 rows all lie at or past it skip their reads and
 //     MFMAs (not the DMAs or barriers); the extension runs only if m_limit > 256.
-template <typename T, bool GATHER, int EXT>
+//   BROWS: B's rows are b_row0 + 0..255 of the tensor B (its base), range-checked against b_rows
+//     (ragged N: rows past the tensor read zeros).
+//   KTAIL: the last K tile runs past the rows' end k_len (elements, k_len * sizeof(T) % 16 == 0):
+//     its 16-byte chunks at or past k_len read zeros (the lane's offset is replaced by the buffer
+//     resource's range for that tile only), so a ragged K needs no padded copy.
+// Every zero-filled load uses an offset equal to its resource's range (not a wrapping sentinel):
+// out of range whether or not the hardware adds the scalar offset before the range check.
+template <typename T, bool GATHER, int EXT, bool BROWS = false, bool KTAIL = false>
 TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __restrict__ rows, int row0, int a_rows,
                               const T* __restrict__ B, int ldb, int n_tiles, T* lds_a, T* lds_b, T* lds_x,
-                              float* __restrict__ C, float* __restrict__ Cx, int m_limit, int wave) {
+                              float* __restrict__ C, float* __restrict__ Cx, int m_limit, int wave, int b_row0 = 0,
+                              int b_rows = 0, int k_len = 0) {
   using namespace quad;
   typedef typename qfrag<T>::F F;
   constexpr int KE = geo<T>::KE, CE = geo<T>::CE, HALF = geo<T>::HALF;
@@ -141,6 +149,9 @@ TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __res
   row0 = uni(row0);
   a_rows = uni(a_rows);
   m_limit = uni(m_limit);
+  b_row0 = uni(b_row0);
+  b_rows = uni(b_rows);
+  k_len = uni(k_len);
   constexpr int ES = (int)sizeof(T);
   floatx4* acc = reinterpret_cast<floatx4*>(C);
   const int NT = n_tiles;
@@ -161,60 +172,106 @@ TL_DEVICE void gemm_quad_nt_x(const T* __restrict__ A, int lda, const int* __res
   const int dc = (tid & 7) ^ ((tid >> 4) & 7);
   uint32_t voffa[2][2];
   __amdgpu_buffer_rsrc_t ra;
+  uint32_t ra_n;  // the A resource's range in bytes: an offset equal to it reads zeros
   if constexpr (GATHER) {
+    ra_n = (uint32_t)(a_rows * lda * ES);
 #pragma unroll
     for (int qa = 0; qa < 2; ++qa)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int br = (2 * j + (rr >> 5)) * 64 + qa * 32 + (rr & 31);
         const int src = rows ? rows[br] : row0 + br;
-        voffa[qa][j] = (src >= 0 && src < a_rows) ? (uint32_t)((src * lda + dc * CE) * ES) : 0xFFFFFFF0u;
+        voffa[qa][j] = (src >= 0 && src < a_rows) ? (uint32_t)((src * lda + dc * CE) * ES) : ra_n;
       }
-    ra = make_rsrc(A, (uint32_t)(a_rows * lda * ES));
+    ra = make_rsrc(A, ra_n);
   } else {
+    ra_n = (uint32_t)(((255 + EXT) * lda + KE * NT) * ES);
     const uint32_t v = (uint32_t)((((rr >> 5) * 64 + (rr & 31)) * lda + dc * CE) * ES);
 #pragma unroll
     for (int qa = 0; qa < 2; ++qa)
 #pragma unroll
       for (int j = 0; j < 2; ++j) voffa[qa][j] = v;
-    ra = make_rsrc(A, (uint32_t)(((255 + EXT) * lda + KE * NT) * ES));
+    ra = make_rsrc(A, ra_n);
   }
   uint32_t voffx = 0;
   if constexpr (EXT > 0) {
     const int xr = (tid & 255) >> 3;
     if constexpr (GATHER) {
       const int src = rows ? rows[256 + xr] : row0 + 256 + xr;
-      voffx = (src >= 0 && src < a_rows) ? (uint32_t)((src * lda + dc * CE) * ES) : 0xFFFFFFF0u;
+      voffx = (src >= 0 && src < a_rows) ? (uint32_t)((src * lda + dc * CE) * ES) : ra_n;
     } else {
       voffx = (uint32_t)(((256 + xr) * lda + dc * CE) * ES);
     }
   }
-  const uint32_t voffb = (uint32_t)((rr * ldb + dc * CE) * ES);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B, (uint32_t)((255 * ldb + KE * NT) * ES));
+  // B: one per-lane offset (slot and half rows in the scalar offset), or per (half, j) row offsets
+  // range-checked against b_rows (BROWS; B is then the tensor base and rows start at b_row0)
+  uint32_t voffb[2][2];
+  uint32_t rb_n;
+  if constexpr (BROWS) {
+    rb_n = (uint32_t)(b_rows * ldb * ES);
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int src = b_row0 + j * 128 + qb * 64 + rr;
+        voffb[qb][j] = src < b_rows ? (uint32_t)((src * ldb + dc * CE) * ES) : rb_n;
+      }
+  } else {
+    rb_n = (uint32_t)((255 * ldb + KE * NT) * ES);
+    const uint32_t v = (uint32_t)((rr * ldb + dc * CE) * ES);
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) voffb[qb][j] = v;
+  }
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B, rb_n);
+  // KTAIL: the offsets of the LAST K tile, computed once: a lane whose chunk lies at or past k_len
+  // reads zeros there (the chunk index is per lane); stage() picks them with a uniform branch on
+  // the tile, so the other tiles' DMAs carry no per-lane select
+  const bool chunk_in = !KTAIL || (NT - 1) * KE + dc * CE < k_len;
+  uint32_t voffa_t[2][2], voffb_t[2][2], voffx_t = ra_n;
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      voffa_t[q][j] = chunk_in ? voffa[q][j] : ra_n;
+      voffb_t[q][j] = chunk_in ? voffb[q][j] : rb_n;
+    }
+  if constexpr (EXT > 0) voffx_t = chunk_in ? voffx : ra_n;
   // each wave's 64 lanes fill 1 KiB of a slot per DMA (lane-linear destination)
   T* da = lds_a + wave * 8 * KE;
   T* db = lds_b + wave * 8 * KE;
   // slot s of buffer b: A slots (s = 0, 1) in lds_a, B slots (s = 2, 3) in lds_b
-  auto stage = [&](int buf, int slot, int tile) {
+  auto stage_with = [&](int buf, int slot, int tile, const uint32_t (&va)[2][2], const uint32_t (&vb)[2][2]) {
     const int kb = tile * 128;  // bytes
     if (slot < 2) {
       T* l = da + (buf * 2 + slot) * HALF;
       const int s0 = GATHER ? kb : kb + (slot * 32) * lda * ES;
       const int s1 = GATHER ? kb : kb + (128 + slot * 32) * lda * ES;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)l, 16, voffa[slot][0], s0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(l + 64 * KE), 16, voffa[slot][1], s1, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)l, 16, va[slot][0], s0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(l + 64 * KE), 16, va[slot][1], s1, 0, 0);
     } else {
       T* l = db + (buf * 2 + slot - 2) * HALF;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)l, 16, voffb, kb + ((slot - 2) * 64) * ldb * ES,
-                                                0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(l + 64 * KE), 16, voffb,
-                                                kb + (128 + (slot - 2) * 64) * ldb * ES, 0, 0);
+      const int q = slot - 2;
+      const int s0 = BROWS ? kb : kb + (q * 64) * ldb * ES;
+      const int s1 = BROWS ? kb : kb + (128 + q * 64) * ldb * ES;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)l, 16, vb[q][0], s0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(l + 64 * KE), 16, vb[q][1], s1, 0, 0);
     }
+  };
+  auto stage = [&](int buf, int slot, int tile) {
+    if constexpr (KTAIL) {
+      if (tile == NT - 1) {
+        stage_with(buf, slot, tile, voffa_t, voffb_t);
+        return;
+      }
+    }
+    stage_with(buf, slot, tile, voffa, voffb);
   };
   auto stage_x = [&](int buf, int tile) {
     if constexpr (EXT > 0)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(lds_x + buf * 32 * KE + (wave & 3) * 8 * KE), 16,
-                                                voffx, tile * 128, 0, 0);
+                                                (KTAIL && tile == NT - 1) ? voffx_t : voffx, tile * 128, 0, 0);
   };
   constexpr int XW = EXT > 0 ? 1 : 0;  // extension DMAs per thread per K tile
   // operand reads: LDS row r0 + (lane & 15), chunk kk*4 + (lane >> 4), swizzled by (lane >> 1) & 7

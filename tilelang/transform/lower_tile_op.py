@@ -1911,13 +1911,24 @@ class TileOpLowerer(Mutator):
         else:
             a_ptr, rows, row0, a_rows = ptr(op.a), no_rows, IntImm(0), IntImm(0)
         cl = L.BufferPtr(ctx.local_of(op.C.buffer), 0)
-        args = [a_ptr, i32(a.get_strides()[op.a_rdim]), rows, row0, a_rows, ptr(op.b), i32(b.get_strides()[op.b_rdim]),
+        b_rm = getattr(op, "b_row_mode", False)
+        k_len = getattr(op, "k_len", None)
+        if b_rm:  # B rows n0.. range-checked against the tensor: tensor base + the tile's first row
+            bmins = [IntImm(0)] + [self.expr(m) for m in op.b.mins[1:]]
+            b_ptr, b_row0, b_rows = L.BufferPtr(ctx.flat_of(b), ctx.flat_index(b, bmins)), i32(op.b.mins[0]), \
+                i32(b.shape[0])
+        else:
+            b_ptr, b_row0, b_rows = ptr(op.b), IntImm(0), IntImm(0)
+        args = [a_ptr, i32(a.get_strides()[op.a_rdim]), rows, row0, a_rows, b_ptr, i32(b.get_strides()[op.b_rdim]),
                 i32(op.n), L.BufferPtr(ctx.flat_of(op.lds_a), 0), L.BufferPtr(ctx.flat_of(op.lds_b), 0),
                 L.BufferPtr(ctx.flat_of(op.lds_x if op.lds_x is not None else op.lds_a), 0), cl,
                 L.BufferPtr(ctx.local_of(op.Cx.buffer), 0) if op.Cx is not None else cl,
                 i32(op.m_limit) if op.m_limit is not None else IntImm(0x3fffffff), ctx.wave_expr()]
-        return S.SeqStmt([L.CallStmt("tl::gemm_quad_nt_x", args, [
-            _dt.hip_type(a.dtype), _b(gather), 32 if op.Cx is not None else 0])])
+        targs = [_dt.hip_type(a.dtype), _b(gather), 32 if op.Cx is not None else 0]
+        if b_rm or k_len is not None:  # ragged N / K (defaults otherwise: the aligned form's source)
+            args += [b_row0, b_rows, IntImm(k_len if k_len is not None else 0)]
+            targs += [_b(b_rm), _b(k_len is not None)]
+        return S.SeqStmt([L.CallStmt("tl::gemm_quad_nt_x", args, targs)])
 
     def lower_async_small(self, op: AsyncCopyOp):
         """Small-tile DMA (pipeline._small_dma_plan): one 4-byte buffer LDS-DMA per wave; lane chunk

@@ -65,10 +65,12 @@ class QuadGemmLoopOp(O.TileOp):
 
     def __init__(self, a: BufferRegion, a_rdim: int, idx: Optional[BufferRegion], b: BufferRegion, b_rdim: int,
                  lds_a: Buffer, lds_b: Buffer, lds_x: Optional[Buffer], C: BufferRegion, Cx: Optional[BufferRegion],
-                 n, m_limit=None, row_mode=False):
+                 n, m_limit=None, row_mode=False, b_row_mode=False, k_len=None):
         # row_mode: dense A whose row range is not provable -- rows from the tile's first row,
-        # range-checked against the tensor (tl::gemm_quad_nt_x GATHER with a null row list)
-        self.row_mode = row_mode
+        # range-checked against the tensor (tl::gemm_quad_nt_x GATHER with a null row list);
+        # b_row_mode: the same for B's rows (ragged N); k_len: the tensors' K when the last K
+        # tile runs past it (its chunks at or past k_len read zeros)
+        self.row_mode, self.b_row_mode, self.k_len = row_mode, b_row_mode, k_len
         self.a, self.a_rdim, self.idx, self.b, self.b_rdim = a, a_rdim, idx, b, b_rdim
         self.lds_a, self.lds_b, self.lds_x, self.C, self.Cx, self.n, self.m_limit = \
             lds_a, lds_b, lds_x, C, Cx, n, m_limit
@@ -141,8 +143,10 @@ def _squeeze(ext):
     return ext
 
 
-def glds_plan(op: O.CopyOp, num_threads: int, ranges, target) -> Optional[dict]:
-    """Decide whether a global->shared copy can be a lane-linear LDS-DMA; return its geometry."""
+def glds_plan(op: O.CopyOp, num_threads: int, ranges, target, k_tail: bool = False) -> Optional[dict]:
+    """Decide whether a global->shared copy can be a lane-linear LDS-DMA; return its geometry.
+    ``k_tail`` (the quad GEMM loop only): the innermost (contiguous) dim may also run past the
+    tensor -- a ragged last K tile, zero-filled chunk by chunk by tl::gemm_quad_nt_x (``ktail``)."""
     if target is not None and getattr(target, "kind", "hip") != "hip":
         return None
     if getattr(target, "disable_glds", False):
@@ -204,6 +208,8 @@ def glds_plan(op: O.CopyOp, num_threads: int, ranges, target) -> Optional[dict]:
     # zero-padded tile — no register staging needed.
     shape = sb.shape
     oob = False
+    ktail = None
+    last = len(src.region) - 1
     for d, (m, e) in enumerate(src.region):
         b = bound(m, ranges)
         s = as_int(shape[d])
@@ -211,6 +217,10 @@ def glds_plan(op: O.CopyOp, num_threads: int, ranges, target) -> Optional[dict]:
         if b is None or s is None or ev is None or b[0] < 0 or b[1] + ev > s:
             if d == 0 and ev is not None:
                 oob = True
+                continue
+            if k_tail and d == last and d > 0 and s is not None and b is not None and b[0] >= 0 and \
+                    (s * eb) % 16 == 0 and as_int(strides[d]) == 1:
+                ktail = s  # chunks at or past column s read zeros (whole 16-byte chunks: s*eb % 16 == 0)
                 continue
             return None
     nbytes = None
@@ -226,7 +236,7 @@ def glds_plan(op: O.CopyOp, num_threads: int, ranges, target) -> Optional[dict]:
         nbytes = numel * eb
     n_chunks = R * C * eb // 16
     return dict(R=R, C=C, eb=eb, rdim=rdim, cdim=cdim, instrs=n_chunks // 64 // dw, nwaves=dw, cpr=C * eb // 16,
-                oob_bytes=nbytes, dup=dw < nw)
+                oob_bytes=nbytes, dup=dw < nw, ktail=ktail)
 
 
 def _small_dma_plan(op: O.CopyOp, num_threads: int, ranges) -> Optional[dict]:
@@ -480,6 +490,11 @@ class PipelineInjector(Mutator):
                 asyncs.append((p, src, gather_plan(p.op, self.T, self.target)))
                 continue
             plan = glds_plan(O.CopyOp(src, p.op.dst), self.T, rng, self.target)
+            if plan is None and loop.annotations.get("quad") and nstages == 2:
+                # the quad GEMM loop zero-fills a ragged last K tile itself (tl/gemm_quad.h ktail)
+                plan = glds_plan(O.CopyOp(src, p.op.dst), self.T, rng, self.target, k_tail=True)
+            if plan is not None and plan.get("ktail") and not loop.annotations.get("quad"):
+                plan = None
             if plan is not None:
                 asyncs.append((p, src, plan))
             else:
@@ -588,6 +603,11 @@ class PipelineInjector(Mutator):
         consumer_stmts = [st for st in stmts if not any(st is p for p, _ in prods)]
         if loop.annotations.get("quad") and nstages == 2 and not staged:
             q = _quad_schedule(self, loop, asyncs, consumer_stmts, newbufs, rng)
+            if q is None and any(pl.get("ktail") for _, _, pl in asyncs):
+                # a k-tail plan only the quad template can run: the generic pipeline again, without
+                # the relaxed plans (those copies are register-staged)
+                ann = {kk_: v for kk_, v in loop.annotations.items() if kk_ != "quad"}
+                return self.pipeline(S.ForStmt(loop.var, loop.min, loop.extent, loop.kind, loop.body, ann))
             if q is not None:
                 return q
             _log.debug("quad GEMM loop %s: falling back to the generic pipeline", loop.var)
@@ -766,19 +786,31 @@ def _quad_schedule(self, loop, asyncs, consumer_stmts, newbufs, ranges):
     x = next((o for o in gemms if o is not g), None)
     k = loop.var
     tiles = {}
+    ktail = set()
     for p, src, plan in asyncs:
         gather = isinstance(p.op, O.GatherRowsOp)
         if not gather and (plan.get("gather") or plan.get("rdim") is None):
             return None
         rdim = p.op.row_dim if gather else plan["rdim"]
-        if not gather and not _in_bounds(src, ranges):
-            # only the outermost (row) dim unproven: rows past the tensor read zeros, as the
-            # generic pipeline's out-of-range LDS-DMA (the template's range-checked row mode)
-            if rdim != 0 or not _in_bounds(BufferRegion(src.buffer, [(IntImm(0), src.region[0][1])] +
-                                                        list(src.region[1:])), ranges):
-                return None
-            gather = "rows"
         cdim = len(src.region) - 1
+        kt = plan.get("ktail") if not gather else None
+        if kt is not None:
+            ktail.add(kt)
+        if not gather and not _in_bounds(src, ranges):
+            # the outermost (row) dim and / or a ragged last K tile unproven: rows past the tensor
+            # read zeros, as the generic pipeline's out-of-range LDS-DMA (the template's
+            # range-checked row mode), and so do K chunks past the row end (ktail)
+            reg = list(src.region)
+            row_oob = not _in_bounds(BufferRegion(src.buffer, reg[:cdim] + [(IntImm(0), reg[cdim][1])
+                                                                              if kt is not None else reg[cdim]]),
+                                     ranges)
+            if row_oob and rdim != 0:
+                return None
+            probe = [(IntImm(0), reg[0][1]) if row_oob else reg[0]] + reg[1:cdim] + \
+                [(IntImm(0), reg[cdim][1]) if kt is not None else reg[cdim]]
+            if not _in_bounds(BufferRegion(src.buffer, probe), ranges):
+                return None
+            gather = "rows" if row_oob else False
         if as_int(src.buffer.get_strides()[cdim]) != 1:
             return None
         for d, (m, _) in enumerate(src.region):
@@ -790,27 +822,36 @@ def _quad_schedule(self, loop, asyncs, consumer_stmts, newbufs, ranges):
         tiles[p.op.dst.buffer] = (_subst_region(src, {k: loop.min}), rdim, idx, gather)
     A, B = g.A.buffer, g.B.buffer
     want = {A, B} | ({x.A.buffer} if x is not None else set())
-    if set(tiles) != want or tiles[B][3]:
+    if set(tiles) != want or tiles[B][3] not in (False, "rows"):
         return None
+    if len(ktail) > 1 or (ktail and x is not None):
+        return None  # A and B must share the ragged K (the MoE extension GEMM: aligned K only)
+    k_len = next(iter(ktail)) if ktail else None
+    if k_len is not None and any(tiles[Bf][3] is True for Bf in tiles):
+        return None  # gathered rows: aligned K only
+    b_rows = tiles[B][3] == "rows"
     a_src, a_rdim, idx, a_mode = tiles[A]
     if x is not None and tiles[x.A.buffer][3] != a_mode:
         return None
-    if a_mode:
-        # gathered / range-checked rows: tl::gemm_quad_nt_x forms the byte offsets of the rows and
+    for Bf, checked in ((A, a_mode or k_len is not None), (B, b_rows or k_len is not None)):
+        if not checked:
+            continue
+        # gathered / range-checked rows or K chunks: tl::gemm_quad_nt_x forms the byte offsets and
         # the buffer resource's range in 32 bits (tl/gemm_quad.h), as the dense DMA plan's own
-        # numel * eb < 2^31 condition; a larger A runs the generic pipeline
+        # numel * eb < 2^31 condition; a larger tensor runs the generic pipeline
         numel = 1
-        for s_ in a_src.buffer.shape:
+        for s_ in tiles[Bf][0].buffer.shape:
             if as_int(s_) is None:
                 return None
             numel *= as_int(s_)
-        if numel * a_src.buffer.dtype.bytes >= (1 << 31):
+        if numel * tiles[Bf][0].buffer.dtype.bytes >= (1 << 31):
             return None
     if a_mode and a_rdim != 0:
         return None
     op = QuadGemmLoopOp(a_src, a_rdim, idx, tiles[B][0], tiles[B][1], newbufs[A], newbufs[B],
                         newbufs[x.A.buffer] if x is not None else None, g.C, x.C if x is not None else None,
-                        loop.extent, getattr(g, "valid_m", None), row_mode=a_mode == "rows")
+                        loop.extent, getattr(g, "valid_m", None), row_mode=a_mode == "rows", b_row_mode=b_rows,
+                        k_len=k_len)
     self.replaced = getattr(self, "replaced", {})
     for Bf in want:
         lst = self.replaced.setdefault(Bf, [])
