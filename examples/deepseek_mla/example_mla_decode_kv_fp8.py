@@ -31,9 +31,15 @@ FP8_MAX = 448.0
 
 @tilelang.jit(out_idx=[7], pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True})
 def mla_decode_kv_fp8(batch, heads, seqlen_kv, dim, pe_dim, block_N=64, block_H=64, num_split=2, threads=512,
-                      num_stages=1, dtype="bfloat16", qk_fp8=True):
+                      num_stages=1, dtype="bfloat16", qk_fp8=True, pv_fp8=None):
     """``qk_fp8``: scores on the fp8 MFMA with Q quantised per head row (default); False keeps Q in
-    ``dtype`` and runs both GEMMs on the widened tile (the reference's numerics)."""
+    ``dtype`` and runs both GEMMs on the widened tile (the reference's numerics).
+    ``pv_fp8`` (default: with ``qk_fp8``): O += P V on the fp8 MFMA too -- P in e4m3 (the lazy
+    rescale bounds it by 2^8, inside e4m3's range, so no scale is needed; 3 mantissa bits per
+    probability), V read straight from the fp8 cache tile with ds_read_b64_tr_b8: no widened copy
+    of the tile, half the LDS bytes per PV operand."""
+    if pv_fp8 is None:
+        pv_fp8 = qk_fp8
     scale = (1.0 / (dim + pe_dim))**0.5 * 1.44269504  # softmax in base 2
     accum_dtype = "float"
     VALID_BLOCK_H = min(block_H, heads)
@@ -54,10 +60,11 @@ def mla_decode_kv_fp8(batch, heads, seqlen_kv, dim, pe_dim, block_N=64, block_H=
                 Q_local = T.alloc_fragment([block_H, dim], dtype)
             Q_pe_local = T.alloc_fragment([block_H, pe_dim], dtype)
             KV8_shared = T.alloc_shared([block_N, dim], FP8)
-            V_shared = T.alloc_shared([block_N, dim], dtype)
+            if not pv_fp8:
+                V_shared = T.alloc_shared([block_N, dim], dtype)
             K_pe_shared = T.alloc_shared([block_N, pe_dim], dtype)
             acc_s = T.alloc_fragment([block_H, block_N], accum_dtype)
-            P_shared = T.alloc_shared([block_H, block_N], dtype)
+            P_shared = T.alloc_shared([block_H, block_N], FP8 if pv_fp8 else dtype)
             sc_shared = T.alloc_shared([block_H], accum_dtype)
             any_s = T.alloc_shared([2], "int32")
             acc_o = T.alloc_fragment([block_H, dim], accum_dtype)
@@ -99,7 +106,8 @@ def mla_decode_kv_fp8(batch, heads, seqlen_kv, dim, pe_dim, block_N=64, block_H=
                     for i, j in T.Parallel(block_H, block_N):
                         acc_s[i, j] *= qs_shared[i]
                     T.gemm(Q_pe_local, K_pe_shared, acc_s, transpose_B=True, policy=policy)
-                    T.copy(KV8_shared, V_shared)
+                    if not pv_fp8:
+                        T.copy(KV8_shared, V_shared)
                 else:
                     T.copy(KV8_shared, V_shared)
                     T.gemm(Q_local, V_shared, acc_s, transpose_B=True, clear_accum=True, policy=policy)
@@ -127,7 +135,10 @@ def mla_decode_kv_fp8(batch, heads, seqlen_kv, dim, pe_dim, block_N=64, block_H=
                 if any_s[k % 2] != 0:
                     for i, j in T.Parallel(block_H, dim):
                         acc_o[i, j] *= sc_shared[i]
-                T.gemm(P_shared, V_shared, acc_o)
+                if pv_fp8:
+                    T.gemm(P_shared, KV8_shared, acc_o)  # e4m3 x e4m3, B [keys, dim]: transposed reads
+                else:
+                    T.gemm(P_shared, V_shared, acc_o)
             for i in T.Parallel(block_H):
                 sc_shared[i] = kv_scale / logsum[i]
             for i, j in T.Parallel(block_H, dim):
@@ -206,9 +217,11 @@ def flops(batch, heads, seqlen_kv, dim, pe_dim):
     return 2 * batch * heads * seqlen_kv * (dim + pe_dim) + 2 * batch * heads * seqlen_kv * dim
 
 
-def main(batch=128, heads=128, kv_ctx=8192, dim=512, pe_dim=64, num_split=1, qk_fp8=True):
+def main(batch=128, heads=128, kv_ctx=8192, dim=512, pe_dim=64, num_split=1, qk_fp8=True, pv_fp8=None, block_N=64,
+         num_stages=1):
     import torch
-    kernel = mla_decode_kv_fp8(batch, heads, kv_ctx, dim, pe_dim, num_split=num_split, qk_fp8=qk_fp8)
+    kernel = mla_decode_kv_fp8(batch, heads, kv_ctx, dim, pe_dim, num_split=num_split, qk_fp8=qk_fp8, pv_fp8=pv_fp8,
+                               block_N=block_N, num_stages=num_stages)
     q = torch.randn(batch, heads, dim, device="cuda", dtype=torch.bfloat16)
     q_pe = torch.randn(batch, heads, pe_dim, device="cuda", dtype=torch.bfloat16)
     kv8, s = quantize_kv(torch.randn(batch, kv_ctx, 1, dim, device="cuda"))
@@ -218,7 +231,9 @@ def main(batch=128, heads=128, kv_ctx=8192, dim=512, pe_dim=64, num_split=1, qk_
     out = kernel(q, q_pe, kv8, k_pe, s, glse, part)
     torch.testing.assert_close(out.float(), ref_program(q, q_pe, kv8, s, k_pe, qk_fp8), rtol=2e-2, atol=2e-2)
     lat = kernel.get_profiler().do_bench(lambda: kernel(q, q_pe, kv8, k_pe, s, glse, part))
-    print(f"MLA decode fp8-KV ({'fp8' if qk_fp8 else 'bf16'} QK) b{batch} h{heads} kv{kv_ctx} split{num_split}: "
+    pv = qk_fp8 if pv_fp8 is None else pv_fp8
+    print(f"MLA decode fp8-KV ({'fp8' if qk_fp8 else 'bf16'} QK, {'fp8' if pv else 'bf16'} PV, block_N {block_N}, "
+          f"{num_stages} stage(s)) b{batch} h{heads} kv{kv_ctx} split{num_split}: "
           f"{lat:.3f} ms, "
           f"{flops(batch, heads, kv_ctx, dim, pe_dim) / lat * 1e-9:.1f} TFLOPS")
 
@@ -230,5 +245,9 @@ if __name__ == "__main__":
     p.add_argument("--kv_ctx", type=int, default=8192)
     p.add_argument("--num_split", type=int, default=1)
     p.add_argument("--bf16_qk", action="store_true", help="scores in bf16 on the widened tile")
+    p.add_argument("--bf16_pv", action="store_true", help="P V in bf16 on the widened tile")
+    p.add_argument("--block_N", type=int, default=64)
+    p.add_argument("--num_stages", type=int, default=1)
     a = p.parse_args()
-    main(a.batch, a.heads, a.kv_ctx, 512, 64, a.num_split, not a.bf16_qk)
+    main(a.batch, a.heads, a.kv_ctx, 512, 64, a.num_split, not a.bf16_qk, False if a.bf16_pv else None, a.block_N,
+         a.num_stages)

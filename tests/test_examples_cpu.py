@@ -587,18 +587,28 @@ def test_gqa_bwd_kv_split_cpu():
     torch.testing.assert_close(dvp.sum(0), vf.grad, rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("block_N,stages,qk_fp8", [(64, 1, True), (32, 2, True), (32, 2, False)])
-def test_mla_decode_kv_fp8_cpu(block_N, stages, qk_fp8):
-    """fp8 latent cache: fp8 (or bf16) score GEMM + widened V tile, against fp32 over the dequantised
-    cache (with the kernel's fp8 Q when ``qk_fp8``)."""
+@pytest.mark.parametrize("block_N,stages,qk_fp8,pv_fp8", [(64, 1, True, True), (32, 2, True, True),
+                                                         (64, 1, True, False), (32, 2, False, False),
+                                                         (128, 1, True, True)])
+def test_mla_decode_kv_fp8_cpu(block_N, stages, qk_fp8, pv_fp8):
+    """fp8 latent cache: fp8 (or bf16) score GEMM, P V on the fp8 MFMA (e4m3 P, transposed fp8 V
+    reads) or on the widened tile, against fp32 over the dequantised cache (with the kernel's fp8 Q
+    when ``qk_fp8``)."""
     from example_mla_decode_kv_fp8 import mla_decode_kv_fp8, quantize_kv, ref_program
-    b, h, S, D, P, ns = 2, 64, 128, 128, 32, 2
-    k = _both(mla_decode_kv_fp8, b, h, S, D, P, block_N, 64, ns, num_stages=stages, qk_fp8=qk_fp8)
+    b, h, S, D, P, ns = 2, 64, 256, 128, 32, 2
+    k = _both(mla_decode_kv_fp8, b, h, S, D, P, block_N, 64, ns, num_stages=stages, qk_fp8=qk_fp8, pv_fp8=pv_fp8)
     q, qpe = torch.randn(b, h, D).bfloat16(), torch.randn(b, h, P).bfloat16()
     kv8, s = quantize_kv(torch.randn(b, S, 1, D) * 2)
     kpe = torch.randn(b, S, 1, P).bfloat16()
     o = k(q, qpe, kv8, kpe, s, torch.empty(b, h, ns), torch.empty(b, h, ns, D))
-    torch.testing.assert_close(o.float(), ref_program(q, qpe, kv8, s, kpe, qk_fp8), rtol=2e-2, atol=2e-2)
+    rq = ref_program(q, qpe, kv8, s, kpe, qk_fp8)
+    if pv_fp8:
+        # e4m3 probabilities (3 mantissa bits): ~2 % relative error in the norm, and a few per cent
+        # of the row scale on rows dominated by one or two keys (measured: 1.8-1.9 % / 0.135 of 3.9)
+        assert (o.float() - rq).norm() / rq.norm() < 3e-2
+        assert (o.float() - rq).abs().max() < 0.08 * rq.abs().max()
+    else:
+        torch.testing.assert_close(o.float(), rq, rtol=2e-2, atol=2e-2)
     r = ref_program(q, qpe, kv8, s, kpe)
     assert (o.float() - r).norm() / r.norm() < 5e-2
 

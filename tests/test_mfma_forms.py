@@ -53,6 +53,11 @@ CASES = [
     ("i8_32x32", "int8", "int32", "int32", False, True, "32x32", (128, 128, 64, 256)),
     ("f32_16x16", "float32", "float32", "float32", False, False, None, (64, 64, 32, 256)),
     ("f32_16x16_tatb", "float32", "float32", "float32", True, True, None, (64, 64, 32, 256)),
+    # fp8 with B [K, N] (N contiguous): ds_read_b64_tr_b8 transposed operand reads, on the scaled
+    # 16x16x128 MFMA (K % 128 == 0) and on the 16x16x32 fp8 MFMA
+    ("f8_trb_k128", "float8_e4m3fn", "float32", "float32", False, False, None, (64, 128, 128, 256)),
+    ("f8_trb_k32", "float8_e4m3fn", "float32", "float32", False, False, None, (64, 128, 64, 256)),
+    ("f8_tb_k128", "float8_e4m3fn", "float32", "float32", False, True, None, (64, 128, 128, 256)),
 ]
 
 
@@ -62,6 +67,9 @@ def _inputs(dtype, ta, tb, M, N, K, device):
     if dtype == "int8":
         return (torch.randint(-128, 128, ash, dtype=torch.int8, device=device),
                 torch.randint(-128, 128, bsh, dtype=torch.int8, device=device))
+    if dtype.startswith("float8"):  # exactly representable small integers: an exact check
+        return (torch.randint(-4, 5, ash, device=device).float().to(getattr(torch, dtype)),
+                torch.randint(-4, 5, bsh, device=device).float().to(getattr(torch, dtype)))
     td = getattr(torch, dtype)
     return torch.randn(ash, device=device).to(td), torch.randn(bsh, device=device).to(td)
 
@@ -75,7 +83,8 @@ def test_mfma_form_cpu_and_codegen(case):
     src = kh.get_kernel_source()
     expect = {"bf16_32x32": "gemm_ss_32", "f16_32x32_tb": "gemm_ss_32", "bf16_32x32_ta": "gemm_ss_32",
               "i8_16x16": "gemm_ss_i8<16", "i8_32x32": "gemm_ss_i8<32", "f32_16x16": "gemm_ss_f32",
-              "f32_16x16_tatb": "gemm_ss_f32"}[name]
+              "f32_16x16_tatb": "gemm_ss_f32", "f8_trb_k128": "u, false>", "f8_trb_k32": "u, false>",
+              "f8_tb_k128": "u, true>"}[name]
     assert expect in src and len(kh.code[0]) > 0
     kc = tilelang.compile(f, target="cpu")
     a, b = _inputs(dt, ta, tb, M, N, K, "cpu")

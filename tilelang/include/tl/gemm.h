@@ -367,9 +367,41 @@ TL_DEVICE long ld_rows8_b8(const uint8_t* base, int row, int col) {
   return *reinterpret_cast<const long*>(base + swz_offset<uint8_t, COLS, SWZ>(row, col));
 }
 
-// A: [M][K] (K contiguous), B: [N][K] (K contiguous)
+// MN-contiguous 8-bit operand ([K][N] in LDS) via ds_read_b64_tr_b8: in each 16-lane group, lane i
+// supplies the address of row k0 + (i >> 1), columns n0 + 8 (i & 1) and receives column n0 + i of
+// rows k0 .. k0 + 7, one byte per row in order (measured on gfx950:
+// csrc/probes/ds_read_tr8_probe.hip, profiles/r6/ds_read_tr8_probe.log).  Lane group g = lane >> 4
+// reads its own 8-row block, so lane (g, i) gets rows k0 + 8 g .. + 7 of column n0 + i -- the k
+// assignment of the K-contiguous reads (8 consecutive k per lane group), as the MFMA needs.
+template <int COLS, uint32_t SWZ>
+TL_DEVICE long ld_tr8_b8(const uint8_t* base, int k0, int n0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  typedef int v2i __attribute__((ext_vector_type(2)));
+  const uint8_t* p = base + swz_offset<uint8_t, COLS, SWZ>(k0 + 8 * g + (i >> 1), n0 + 8 * (i & 1));
+  v2i v = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+      (__attribute__((address_space(3))) v2i*)((__attribute__((address_space(3))) char*)(p)));
+  return __builtin_bit_cast(long, v);
+}
+
+// the 32-byte operand of the scaled 16x16x128 MFMA from an MN-contiguous tile: lane group g needs
+// rows k0 + 32 g .. + 31 of its column: four transposed reads of 8 rows (rows 32 g + 8 t of the
+// read's lane group = its own group when the read's base row is k0 + 24 g + 8 t)
+template <int COLS, uint32_t SWZ>
+TL_DEVICE intx8 ld_tr32_b8(const uint8_t* base, int k0, int n0, int lane) {
+  const int g = lane >> 4;
+  long v[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) v[t] = ld_tr8_b8<COLS, SWZ>(base, k0 + 24 * g + 8 * t, n0, lane);
+  typedef int v2i __attribute__((ext_vector_type(2)));
+  const v2i a = __builtin_bit_cast(v2i, v[0]), b = __builtin_bit_cast(v2i, v[1]);
+  const v2i c = __builtin_bit_cast(v2i, v[2]), d = __builtin_bit_cast(v2i, v[3]);
+  return intx8{a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+}
+
+// A: [M][K] (K contiguous), B: [N][K] (K contiguous, TB) or [K][N] (N contiguous, !TB: transposed
+// LDS reads, ds_read_b64_tr_b8)
 template <typename TA, typename TB, int M, int N, int K, int WARP_M, int WARP_N, int A_COLS, uint32_t SWZ_A,
-          int B_COLS, uint32_t SWZ_B>
+          int B_COLS, uint32_t SWZ_B, bool B_KCONTIG = true>
 TL_DEVICE void gemm_ss_f8(const TA* __restrict__ A_, const TB* __restrict__ B_, float* __restrict__ C,
                           int wave_in = -1) {
   constexpr int WM = M / WARP_M, WN = N / WARP_N;
@@ -389,8 +421,12 @@ TL_DEVICE void gemm_ss_f8(const TA* __restrict__ A_, const TB* __restrict__ B_, 
       for (int mi = 0; mi < M_REP; ++mi)
         a[mi] = ld_rows32_b8<A_COLS, SWZ_A>(A, wm * WM + mi * 16 + r, kk * 128 + 32 * g);
 #pragma unroll
-      for (int ni = 0; ni < N_REP; ++ni)
-        b[ni] = ld_rows32_b8<B_COLS, SWZ_B>(B, wn * WN + ni * 16 + r, kk * 128 + 32 * g);
+      for (int ni = 0; ni < N_REP; ++ni) {
+        if constexpr (B_KCONTIG)
+          b[ni] = ld_rows32_b8<B_COLS, SWZ_B>(B, wn * WN + ni * 16 + r, kk * 128 + 32 * g);
+        else
+          b[ni] = ld_tr32_b8<B_COLS, SWZ_B>(B, kk * 128, wn * WN + ni * 16, lane);
+      }
 #pragma unroll
       for (int mi = 0; mi < M_REP; ++mi)
 #pragma unroll
@@ -408,7 +444,12 @@ TL_DEVICE void gemm_ss_f8(const TA* __restrict__ A_, const TB* __restrict__ B_, 
 #pragma unroll
       for (int mi = 0; mi < M_REP; ++mi) a[mi] = ld_rows8_b8<A_COLS, SWZ_A>(A, wm * WM + mi * 16 + r, kk * 32 + 8 * g);
 #pragma unroll
-      for (int ni = 0; ni < N_REP; ++ni) b[ni] = ld_rows8_b8<B_COLS, SWZ_B>(B, wn * WN + ni * 16 + r, kk * 32 + 8 * g);
+      for (int ni = 0; ni < N_REP; ++ni) {
+        if constexpr (B_KCONTIG)
+          b[ni] = ld_rows8_b8<B_COLS, SWZ_B>(B, wn * WN + ni * 16 + r, kk * 32 + 8 * g);
+        else
+          b[ni] = ld_tr8_b8<B_COLS, SWZ_B>(B, kk * 32, wn * WN + ni * 16, lane);
+      }
 #pragma unroll
       for (int mi = 0; mi < M_REP; ++mi)
 #pragma unroll

@@ -228,6 +228,17 @@ def _read_patterns(kind: str, rows: int, cols: int, elem_bytes: int, row_base_st
                 for j in range(3):
                     pats.append([(r0 + (l & 15), k0 + (l >> 4) * 24 + 8 * j) for l in range(64)])
         return pats
+    if kind in ("tr8", "tr8_32"):
+        # MN-contiguous 8-bit operand via ds_read_b64_tr_b8 (tl/gemm.h ld_tr8_b8): lane (g, i)
+        # supplies row k0 + 8 g + (i >> 1) [tr8_32: k0 + 32 g + 8 t + (i >> 1)], cols c0 + 8 (i & 1)
+        nt = 4 if kind == "tr8_32" else 1
+        kst = 128 if kind == "tr8_32" else 32
+        for c0 in range(0, min(cols, 64), 16):
+            for k0 in range(0, rows, kst):
+                for t in range(nt):
+                    pats.append([(k0 + (32 if nt == 4 else 8) * (l >> 4) + 8 * t + ((l & 15) >> 1),
+                                  c0 + 8 * (l & 1)) for l in range(64)])
+        return pats
     if kind == "k_rows32":
         # 8-bit operand of the scaled 16x16x128 MFMA: 32 consecutive bytes per lane, two b128 reads
         for r0 in range(0, min(rows, 64), row_base_step):

@@ -287,14 +287,15 @@ def gemm_plan(op: O.GemmOp, num_threads: int, target=None, a_layout: Optional[Fr
             plan["a_kperm"] = 1
     ebytes = A.dtype.bytes
     if eb == 8:
-        if op.trans_A or not op.trans_B or A.scope != "shared" or B.scope != "shared":
-            raise ValueError("fp8 T.gemm on gfx950 needs K-contiguous shared operands: A [M,K] and B [N,K] "
-                             "(transpose_B=True)")
+        if op.trans_A or A.scope != "shared" or B.scope != "shared":
+            raise ValueError("fp8 T.gemm on gfx950 needs shared operands with A K-contiguous ([M,K]); B is "
+                             "[N,K] (transpose_B=True) or [K,N] (ds_read_b64_tr_b8 transposed reads)")
         kind = "k_rows32" if K % 128 == 0 else "k_rows"
         plan["f8_kind"] = kind
-        plan["a_kind"] = plan["b_kind"] = kind
+        plan["a_kind"] = kind
+        plan["b_kind"] = kind if op.trans_B else ("tr8_32" if K % 128 == 0 else "tr8")
         plan["a_smem_layout"] = MF.operand_swizzle(kind, A.static_shape(), 1)
-        plan["b_smem_layout"] = MF.operand_swizzle(kind, B.static_shape(), 1)
+        plan["b_smem_layout"] = MF.operand_swizzle(plan["b_kind"], B.static_shape(), 1)
         return plan
     if A.scope == "shared":
         shp = A.static_shape()

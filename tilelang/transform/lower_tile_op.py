@@ -1313,7 +1313,7 @@ class TileOpLowerer(Mutator):
             out.append(L.CallStmt("tl::gemm_ss_f8", [pa, pb, L.BufferPtr(cl, 0), ctx.wave_expr()], [
                 _dt.hip_type(A.dtype), _dt.hip_type(B.dtype), plan["M"], plan["N"], plan["K"], plan["warp_m"],
                 plan["warp_n"], A.static_shape()[-1], f"{gemm_lower.encode_swizzle(A.layout)}u",
-                B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u"
+                B.static_shape()[-1], f"{gemm_lower.encode_swizzle(B.layout)}u", _b(op.trans_B)
             ]))
             return S.SeqStmt(out)
         b_cols = B.static_shape()[-1]
