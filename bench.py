@@ -188,6 +188,9 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="initialise the process group and the mesh even at world size 1 (RCCL on a GPU), so "
                          "the MoE runs expert-parallel through the mesh exchange (checked like N > 1)")
+    ap.add_argument("--streams", type=int, default=1, choices=[1, 2],
+                    help="2: the MoE layer runs on a second HIP stream beside GEMM + attention (the three phases "
+                         "are independent; the step ends when both streams have finished)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: tiny shapes on the CPU target under gloo (CI plumbing check)")
     args = ap.parse_args()
@@ -294,7 +297,19 @@ def main():
     attn_flops = 4.0 * a_["batch"] * a_["heads"] * a_["seq_len"]**2 * a_["dim"]
     moe_flops = 0.0 if moe is None else 6.0 * m["tokens"] * m["topk"] * m["hidden"] * m["ffn"]
 
+    side = torch.cuda.Stream() if (args.streams == 2 and not cpu and moe is not None) else None
+
     def step():
+        if side is not None:
+            # fork: the MoE layer on the side stream, GEMM + attention on the main one; join before
+            # the step's end event, so the step still covers all three phases' work
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                moe(X)
+            gemm(A, B)
+            attn(Q, K, V)
+            torch.cuda.current_stream().wait_stream(side)
+            return
         gemm(A, B)
         attn(Q, K, V)
         if moe is not None:
@@ -470,6 +485,7 @@ def main():
             "attn_vendor_tflops": (round(attn_flops / attn_vendor_ms / 1e9, 1) if attn_vendor_ms else None),
             "moe_tflops_per_gpu": round(moe_flops / moe_ms / 1e9, 1) if moe is not None else None,
             "moe_comm_fraction": round(moe_comm_ms / moe_ms, 3) if moe is not None and moe_ms > 0 else None,
+            "streams": args.streams if side is not None else 1,
             "phase_timing": ("wall, 1 call per rep" if (cpu or dist is not None) else
                              "device time (events behind a queue-filling blocker), 10 calls"),
             "host_ms_per_call": host_ms or None,
