@@ -165,8 +165,20 @@ def flops(batch, heads, seqlen_kv, dim, pe_dim):
     return 2 * batch * heads * seqlen_kv * (dim + pe_dim) + 2 * batch * heads * seqlen_kv * dim
 
 
-def main(batch=128, heads=128, kv_heads=1, kv_ctx=8192, dim=512, pe_dim=64, num_split=4):
+def auto_split(batch, heads, block_H=64, cus=256):
+    """Smallest KV split that puts at least one block on every CU: at b128 h128 (256 blocks without a
+    split) split 1 runs 711.5 TF against 642.3 for split 4 (profiles/r6/mla_bf16_sweep.log); small
+    batches split more to fill the chip (the LSE combine kernel sums the partials)."""
+    blocks = batch * max(1, heads // block_H)
+    split = 1
+    while blocks * split < cus and split < 16:
+        split *= 2
+    return split
+
+
+def main(batch=128, heads=128, kv_heads=1, kv_ctx=8192, dim=512, pe_dim=64, num_split=None):
     import torch
+    num_split = num_split or auto_split(batch, heads)
     kernel = mla_decode(batch, heads, kv_heads, kv_ctx, dim, pe_dim, num_split=num_split)
     q = torch.randn(batch, heads, dim, device="cuda", dtype=torch.float16)
     q_pe = torch.randn(batch, heads, pe_dim, device="cuda", dtype=torch.float16)
@@ -186,6 +198,6 @@ if __name__ == "__main__":
     p.add_argument("--batch", type=int, default=128)
     p.add_argument("--heads", type=int, default=128)
     p.add_argument("--kv_ctx", type=int, default=8192)
-    p.add_argument("--num_split", type=int, default=4)
+    p.add_argument("--num_split", type=int, default=None, help="default: auto_split (one block per CU at least)")
     a = p.parse_args()
     main(a.batch, a.heads, 1, a.kv_ctx, 512, 64, a.num_split)

@@ -224,9 +224,11 @@ def flops(batch, heads, seqlen_kv, dim, pe_dim):
     return 2 * batch * heads * seqlen_kv * (dim + pe_dim) + 2 * batch * heads * seqlen_kv * dim
 
 
-def main(batch=128, heads=128, kv_ctx=8192, dim=512, pe_dim=64, num_split=1, qk_fp8=True, pv_fp8=None, block_N=128,
-         num_stages=1):
+def main(batch=128, heads=128, kv_ctx=8192, dim=512, pe_dim=64, num_split=None, qk_fp8=True, pv_fp8=None,
+         block_N=128, num_stages=1):
     import torch
+    from example_mla_decode import auto_split
+    num_split = num_split or auto_split(batch, heads)
     kernel = mla_decode_kv_fp8(batch, heads, kv_ctx, dim, pe_dim, num_split=num_split, qk_fp8=qk_fp8, pv_fp8=pv_fp8,
                                block_N=block_N, num_stages=num_stages)
     q = torch.randn(batch, heads, dim, device="cuda", dtype=torch.bfloat16)
@@ -250,7 +252,7 @@ if __name__ == "__main__":
     p.add_argument("--batch", type=int, default=128)
     p.add_argument("--heads", type=int, default=128)
     p.add_argument("--kv_ctx", type=int, default=8192)
-    p.add_argument("--num_split", type=int, default=1)
+    p.add_argument("--num_split", type=int, default=None)
     p.add_argument("--bf16_qk", action="store_true", help="scores in bf16 on the widened tile")
     p.add_argument("--bf16_pv", action="store_true", help="P V in bf16 on the widened tile")
     p.add_argument("--block_N", type=int, default=128)

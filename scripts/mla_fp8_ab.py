@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--kv", type=int, default=8192)
     ap.add_argument("--variants", default="qk8_pv16_64_1,qk8_pv8_64_1,qk8_pv8_64_2,qk8_pv8_128_1")
     ap.add_argument("--splits", default="1")
+    ap.add_argument("--bf16-variants", default="", help="extra bf16 configs block_N_stages_split[_blockH], e.g. 64_2_2")
     a = ap.parse_args()
     B, H, S, D, P = a.batch, a.heads, a.kv, 512, 64
     torch.manual_seed(0)
@@ -44,6 +45,18 @@ def main():
     r = ref16(q, qpe, kv16, kpe).float()
     print(f"bf16: rel err {((o.float() - r).norm() / r.norm()).item():.2e}", flush=True)
     runs.append(("bf16 (split 4)", lambda: k16(q, qpe, kv16, kpe, g16, p16)))
+    for v in filter(None, a.bf16_variants.split(",")):
+        parts = [int(x) for x in v.split("_")]
+        bn, st, ns = parts[:3]
+        bh = parts[3] if len(parts) > 3 else 64
+        try:
+            kb = mla_decode(B, H, 1, S, D, P, block_N=bn, block_H=bh, num_split=ns, num_stages=st, dtype="bfloat16")
+            gb, pb = torch.empty(B, H, ns, device="cuda"), torch.empty(B, H, ns, D, device="cuda")
+            o = kb(q, qpe, kv16, kpe, gb, pb)
+            print(f"bf16 {v}: rel err {((o.float() - r).norm() / r.norm()).item():.2e}", flush=True)
+            runs.append((f"bf16 {v}", lambda kb=kb, gb=gb, pb=pb: kb(q, qpe, kv16, kpe, gb, pb)))
+        except Exception as e:  # noqa: BLE001
+            print(f"bf16 {v}: FAILED {type(e).__name__}: {str(e)[:300]}", flush=True)
     ref = ref8(q, qpe, kv8, s, kpe)
     for ns in (int(x) for x in a.splits.split(",")):
         for v in a.variants.split(","):
