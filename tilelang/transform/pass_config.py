@@ -50,6 +50,7 @@ class PassConfigKey(str, Enum):
     TL_DISABLE_ADDRESS_HOIST = "tl.disable_address_hoist"  # keep LDS-DMA source addresses in the loop
     TL_GEMM_RS_PIPE = "tl.gemm_rs_pipe"            # register-A GEMM: B fragments streamed in groups of N
     TL_PACK_F32 = "tl.pack_f32"                    # fp32 register pairs as packed v_pk_* math
+    TL_PIPELINE_UNROLL = "tl.pipeline_unroll"      # default #pragma unroll N of lowered pipelined loops
 
     def __str__(self):
         return self.value
@@ -106,6 +107,8 @@ EFFECT = {
                        "steps; tl::gemm_rs PIPE) instead of reading a whole K step before its first MFMA",
     "tl.gemm_interleave": "default on; False drops the 1 MFMA : 1 ds_read sched_group_barrier pattern of the "
                           "prefetched GEMM (the compiler schedules the two streams itself)",
+    "tl.pipeline_unroll": "N > 1: every lowered T.Pipelined main loop without its own unroll= is emitted under "
+                          "#pragma unroll N (N a multiple of the ring depth: the stage slots become constants)",
 }
 
 # NVIDIA-only features / TVM passes that do not exist here: the value meaning "off" is what

@@ -644,8 +644,9 @@ class PipelineInjector(Mutator):
             j1 = binop("+", kk, 1)
             body.append(S.IfStmt(binop("<", j1, n), S.seq(*staged_phase(j1, binop("%", j1, nstages), "store"))))
         ann_new = {"pipelined": nstages, "_lets": lets}
-        if loop.annotations.get("unroll_factor"):
-            ann_new["unroll_factor"] = loop.annotations["unroll_factor"]
+        uf = loop.annotations.get("unroll_factor") or getattr(self.target, "pipeline_unroll", None)
+        if uf and int(uf) > 1:
+            ann_new["unroll_factor"] = int(uf)
         new_loop = S.ForStmt(k, loop.min, loop.extent, "serial", S.SeqStmt(body), ann_new)
         # allocations for the new multi-versioned buffers replace the old ones (done by caller)
         self.replaced = getattr(self, "replaced", {})
