@@ -84,3 +84,15 @@ def test_matmul_template_recommendation():
     hs = MatmulTemplate(M=8192, N=8192, K=8192, in_dtype="float16").with_arch(ARCH).recommend_hints(3)
     c = hs[0].to_config()
     assert (c["block_M"], c["block_N"], c["threads"]) == (256, 256, 512)
+
+
+def test_rasterization_panel_from_l2_model():
+    """The rasterisation plan of a hint carries the panel width of the per-XCD L2 model
+    (roller/rasterization.py l2_panel_width) into to_config()['panel_size']."""
+    from tilelang.carver.roller.rasterization import l2_panel_width, Rasterization2DRow
+    assert l2_panel_width(8192, 8192, 4096, 256, 256, 2) == 8
+    assert l2_panel_width(1024, 8192, 4096, 256, 256, 2) == 4  # 4 tile rows only
+    assert l2_panel_width(256, 8192, 4096, 256, 256, 2) == 1
+    h = TensorCorePolicy(ARCH, 8192, 8192, 8192, trans_b=True).emit_config(1)[0]
+    assert isinstance(h.rasterization_plan, Rasterization2DRow) and h.to_config()["panel_size"] == 8
+    assert h.rasterization_plan.get_code() == ['T.use_swizzle(panel_size=8, order="row")']

@@ -34,6 +34,8 @@ class Hint:
             cfg["block_N"] = self.block[1]
         if self.rstep:
             cfg["block_K"] = self.rstep[0]
+        if self.rasterization_plan.panel_width:  # T.use_swizzle(panel_size=...) of the plan
+            cfg["panel_size"] = self.rasterization_plan.panel_width
         cfg.update(self.extra)
         return cfg
 

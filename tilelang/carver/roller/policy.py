@@ -20,7 +20,7 @@ from typing import List, Optional, Sequence
 
 from .bestfit import gemm_lds_bytes
 from .hint import Hint
-from .rasterization import NoRasterization, Rasterization2DRow
+from .rasterization import NoRasterization, Rasterization2DRow, l2_panel_width
 
 _EB = {"float16": 2, "bfloat16": 2, "float8_e4m3fn": 1, "float8_e5m2": 1, "int8": 1, "float32": 4, "float": 4}
 
@@ -151,8 +151,9 @@ class TensorCorePolicy:
                           trans_b=self.trans_b)
             if c is None:
                 continue
+            pw = l2_panel_width(self.M, self.N, self.K, bm, bn, _eb(self.in_dtype), cus=self.arch.compute_max_core)
             hints.append(Hint(block=[bm, bn], warp=list(c["warp"]), rstep=[bk], pipeline_stage=st, threads=th,
-                              rasterization_plan=Rasterization2DRow(8) if c["raster"] else NoRasterization(),
+                              rasterization_plan=Rasterization2DRow(pw) if c["raster"] else NoRasterization(),
                               estimated_us=c["us"], score=c))
         hints.sort(key=lambda h: (h.estimated_us, -h.block[0] * h.block[1]))
         return hints[:topk]
