@@ -37,12 +37,12 @@ def _core(ctx, c: Core) -> int:
     return int(c)
 
 
-_seq = {}
-
-
 def _key(ctx, name):
-    n = _seq.get(id(ctx), 0)
-    _seq[id(ctx)] = n + 1
+    # the per-rank collective sequence number lives on the rank object: a table keyed by id(ctx)
+    # handed a new VirtualRank the stale count of a collected one that had the same id, so ranks
+    # of one mesh deposited under different keys (intermittent None results)
+    n = getattr(ctx, "_coll_seq", 0)
+    ctx._coll_seq = n + 1
     return (name, n)
 
 
