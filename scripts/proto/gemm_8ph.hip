@@ -17,6 +17,11 @@
 //     (in P3) leaves the 3 half-tiles of tile t+2 in flight across the barrier.
 //   * PRIO: s_setprio(1) around the MFMA cluster (T5); B1: a barrier between the reads + DMA
 //     issue and the MFMAs (the guide's two-barrier phase).
+//   * STAGGER (needs B1): waves 4-7 run one barrier behind waves 0-3 (the guide template's
+//     `if (wr == 1) s_barrier`), so in every barrier interval one half of the workgroup issues its
+//     reads + DMAs while the other half runs its MFMA cluster.  A DMA is then visible to the other
+//     half one barrier later, so the counted wait moves into every phase: vmcnt(8) (the four newest
+//     half-tiles in flight) retires each half-tile two phases before its first read.
 #include "tl/tl.h"
 
 #ifndef GM
@@ -43,6 +48,9 @@
 #ifndef YPRIO
 #define YPRIO 0  // 1: waves 4-7 run at priority 1 for the whole kernel (guide T5 static form)
 #endif
+#ifndef STAGGER
+#define STAGGER 0
+#endif
 #ifndef RO
 #define RO 0  // 1: pin kk-major read order so the first MFMAs wait for half the reads only
 #endif
@@ -55,6 +63,7 @@ constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int HALF = 128 * BK;  // halfs per half-tile slot (16 KiB)
 constexpr int NT = GK / BK;
 static_assert(NT % 2 == 0 && NT >= 4, "K tiles: even, >= 4");
+static_assert(!STAGGER || B1, "the stagger needs the two-barrier phase");
 
 TL_DEVICE void bar() { asm volatile("s_barrier" ::: "memory"); }
 
@@ -180,6 +189,7 @@ extern "C" __global__ void __launch_bounds__(512) gemm_kernel(half_t* __restrict
   bar();
 
   Frags f;
+  if (STAGGER && wave >= 4) bar();
 #if YPRIO
   if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
@@ -204,12 +214,16 @@ extern "C" __global__ void __launch_bounds__(512) gemm_kernel(half_t* __restrict
     } else {                                                                                      \
       if ((T) + 2 < NT) stage(BUF, 3, (T) + 2);                                                   \
     }                                                                                             \
+    if (STAGGER) tl::wait_lgkmcnt<0>(); /* WAR: the other half restages a slot read here */     \
     if (B1) bar();                                                                                \
     if constexpr (P == 0) mma<0, 0>(f.a, f.b0, acc);                                              \
     else if constexpr (P == 1) mma<0, 1>(f.a, f.b1, acc);                                         \
     else if constexpr (P == 2) mma<1, 1>(f.a, f.b1, acc);                                         \
     else mma<1, 0>(f.a, f.b0, acc);                                                               \
-    if constexpr (P == 3) {                                                                       \
+    if (STAGGER) {                                                                                \
+      if ((T) + 2 < NT) tl::wait_vmcnt<8>();                                                      \
+      else tl::wait_vmcnt<0>();                                                                   \
+    } else if constexpr (P == 3) {                                                                \
       if ((T) + 2 < NT) tl::wait_vmcnt<6>();                                                      \
       else if ((T) + 1 < NT) tl::wait_vmcnt<0>();                                                 \
     }                                                                                             \
@@ -227,6 +241,7 @@ extern "C" __global__ void __launch_bounds__(512) gemm_kernel(half_t* __restrict
     PHASE(1, 3, t + 1)
   }
 #undef PHASE
+  if (STAGGER && wave < 4) bar();
 
   // epilogue: fragments -> row-padded LDS tile -> 16-byte row stores
   half_t* Cs = smem;

@@ -24,57 +24,74 @@ def build(jitfn, args, kwargs, extra):
     return tilelang.compile(f, out_idx=getattr(jitfn, "out_idx", None), target="hip", pass_configs=pc)
 
 
-def cases():
+def cases(only=None):
     out = []
-    import example_mha_bwd as E
-    B, H, S, D = 8, 32, 1024, 64
-    q, k, v, do = (torch.randn(B, S, H, D, device="cuda", dtype=torch.float16) for _ in range(4))
-    o, lse = E.flashattn_fwd(B, H, S, D, False, dtype="float16")(q, k, v)
-    delta = E.flashattn_bwd_preprocess(B, H, S, D, dtype="float16")(o, do)
-    fl = 2.0 * B * H * S * S * D
-    dkp = torch.empty(1, B, S, H, D, device="cuda")
-    dvp = torch.empty(1, B, S, H, D, device="cuda")
-    out.append(("FA bwd dK/dV fp16 b8 h32 s1024 d64", E.flashattn_bwd,
-                (B, H, S, D, False), dict(dq_mode="none"), (q, k, v, do, lse, delta, dkp, dvp), 4 * fl))
-    from tilelang.ops.dsa import sparse_mla_fwd
-    Bs, Ss, SKV, Hs, topk = 1, 4096, 8192, 128, 2048
-    qs = torch.randn(Bs, Ss, Hs, 576, device="cuda", dtype=torch.bfloat16)
-    kvs = torch.randn(Bs, SKV, 1, 576, device="cuda", dtype=torch.bfloat16)
-    r = torch.rand(Ss, SKV, device="cuda")
-    pos = torch.arange(Ss, device="cuda")[:, None] + SKV - Ss
-    r = torch.where(torch.arange(SKV, device="cuda")[None, :] <= pos, r, torch.full_like(r, -1.0))
-    idx = r.topk(topk, dim=-1).indices.int().view(Bs, Ss, 1, topk)
-    out.append(("sparse MLA fwd b1 s4096 h128 topk2048", sparse_mla_fwd, (Bs, Ss, SKV, Hs, 512, 64, topk), {},
-                (qs, kvs, idx), 2.0 * Bs * Ss * Hs * topk * (576 + 512)))
-    from example_mamba_chunk_scan import chunk_scan_fwd, make_inputs
-    L = 4096
-    margs = make_inputs(8, L, 256, 1, 80, 64, 128)
-    out.append(("Mamba-2 chunk scan 4K", chunk_scan_fwd, (8, L, 256, 1, 80, 64, 128),
-                dict(block_M=128, block_N=64, block_K=32, threads=256), margs, None))
+    if only in (None, "fa_bwd"):
+        import example_mha_bwd as E
+        B, H, S, D = 8, 32, 1024, 64
+        q, k, v, do = (torch.randn(B, S, H, D, device="cuda", dtype=torch.float16) for _ in range(4))
+        for causal in (False, True):
+            o, lse = E.flashattn_fwd(B, H, S, D, causal, dtype="float16")(q, k, v)
+            delta = E.flashattn_bwd_preprocess(B, H, S, D, dtype="float16")(o, do)
+            fl = 2.0 * B * H * S * S * D * (0.5 if causal else 1.0)
+            dk = torch.empty(B, S, H, D, device="cuda", dtype=torch.float16)
+            dv = torch.empty(B, S, H, D, device="cuda", dtype=torch.float16)
+            tag = "causal" if causal else "non-causal"
+            # the autograd path's tiles (example_mha_bwd._tiles); outputs written in place: compared
+            # through the (-2, -1) argument slots
+            out.append((f"FA bwd dK/dV {tag} fp16 b8 h32 s1024 d64", E.flashattn_bwd, (B, H, S, D, causal),
+                        dict(dq_mode="none", **E._tiles(D, D, "bwd", causal)), (q, k, v, do, lse, delta, dk, dv),
+                        4 * fl, (-2, -1)))
+            out.append((f"FA bwd dQ {tag} fp16 b8 h32 s1024 d64", E.flashattn_bwd_dq, (B, H, S, D, causal),
+                        dict(E._tiles(D, D, "dq", causal)), (q, k, v, do, lse, delta), 3 * fl, None))
+    if only in (None, "smla"):
+        from tilelang.ops.dsa import sparse_mla_fwd
+        Bs, Ss, SKV, Hs, topk = 1, 4096, 8192, 128, 2048
+        qs = torch.randn(Bs, Ss, Hs, 576, device="cuda", dtype=torch.bfloat16)
+        kvs = torch.randn(Bs, SKV, 1, 576, device="cuda", dtype=torch.bfloat16)
+        r = torch.rand(Ss, SKV, device="cuda")
+        pos = torch.arange(Ss, device="cuda")[:, None] + SKV - Ss
+        r = torch.where(torch.arange(SKV, device="cuda")[None, :] <= pos, r, torch.full_like(r, -1.0))
+        idx = r.topk(topk, dim=-1).indices.int().view(Bs, Ss, 1, topk)
+        out.append(("sparse MLA fwd b1 s4096 h128 topk2048", sparse_mla_fwd, (Bs, Ss, SKV, Hs, 512, 64, topk), {},
+                    (qs, kvs, idx), 2.0 * Bs * Ss * Hs * topk * (576 + 512), None))
+    if only in (None, "mamba"):
+        from example_mamba_chunk_scan import chunk_scan_fwd, make_inputs
+        L = 4096
+        margs = make_inputs(8, L, 256, 1, 80, 64, 128)
+        out.append(("Mamba-2 chunk scan 4K", chunk_scan_fwd, (8, L, 256, 1, 80, 64, 128),
+                    dict(block_M=128, block_N=64, block_K=32, threads=256), margs, None, None))
     return out
+
+
+def _outs(res, inputs, slots):
+    if slots is not None:
+        return [inputs[i].clone() for i in slots]
+    return list(res) if isinstance(res, (list, tuple)) else [res]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--unroll", type=int, default=2)
+    ap.add_argument("--only", choices=["fa_bwd", "smla", "mamba"], default=None)
     a = ap.parse_args()
     torch.manual_seed(0)
     runs = []
-    for name, fn, args, kw, inputs, flops in cases():
+    for name, fn, args, kw, inputs, flops, slots in cases(a.only):
         ks = []
         for tag, extra in (("base", {}), (f"unroll{a.unroll}", {"tl.pipeline_unroll": a.unroll})):
             try:
                 kern = build(fn, args, kw, extra)
-                res = kern(*inputs)
-                ks.append((tag, kern, res))
+                ks.append((tag, kern, _outs(kern(*inputs), inputs, slots)))
             except Exception as e:  # noqa: BLE001
                 print(f"{name} {tag}: FAILED {type(e).__name__}: {str(e)[:300]}", flush=True)
         if len(ks) == 2:
             r0, r1 = ks[0][2], ks[1][2]
-            same = all(torch.equal(x, y) for x, y in zip(r0 if isinstance(r0, (list, tuple)) else [r0],
-                                                          r1 if isinstance(r1, (list, tuple)) else [r1])) \
-                if r0 is not None else "n/a (in-place outputs)"
+            same = all(torch.equal(x, y) for x, y in zip(r0, r1))
             print(f"{name}: outputs identical: {same}", flush=True)
+            if not same:
+                d = max((x.float() - y.float()).abs().max().item() for x, y in zip(r0, r1))
+                print(f"{name}: max abs diff {d:.3g} (fp contraction under the unrolled body)", flush=True)
         for tag, kern, _ in ks:
             runs.append((name, tag, kern, inputs, flops))
     t0 = time.perf_counter()
