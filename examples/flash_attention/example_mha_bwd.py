@@ -164,7 +164,7 @@ def flashattn_bwd_postprocess(batch, heads, seq_len, dim, blk=64, threads=256, d
 
 @tilelang.jit(pass_configs=FAST_MATH)
 def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=512, num_stages=2,
-                  dtype="float16", dq_mode="atomic", groups=1, dim_v=None, kv_split=1):
+                  dtype="float16", dq_mode="atomic", groups=1, dim_v=None, kv_split=1, unroll=None):
     """``dq_mode``: "atomic" (fp32 atomics into dQ, one kernel) or "none" (dK/dV only; dQ comes from
     ``flashattn_bwd_dq``) -- the dQ atomics were 85% of the single-kernel time on MI355X.
     GQA (``groups`` query heads per KV head): one block per KV head walks the Q/dO tiles of all
@@ -220,7 +220,7 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
             loop_st = T.floordiv(by * block_M, block_N) if is_causal else 0
             loop_ed = T.ceildiv(seq_len, block_N)
             n_q = loop_ed - loop_st
-            for it in T.Pipelined(n_q * gps, num_stages=num_stages):
+            for it in T.Pipelined(n_q * gps, num_stages=num_stages, unroll=unroll):
                 # clamped into range: provably in bounds, so the Q / dO / lse / Delta tiles are LDS-DMA
                 # producers (division / modulo by a runtime count hides the range from the prover)
                 hq0 = bx * groups + sp * gps if kv_split > 1 else bx * groups
@@ -279,7 +279,7 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
 
 @tilelang.jit(out_idx=[6], pass_configs=FAST_MATH)
 def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=256, num_stages=2,
-                     dtype="float16", groups=1, dim_v=None):
+                     dtype="float16", groups=1, dim_v=None, unroll=None):
     """dQ without atomics: one block per (query tile, head, batch) walks the KV tiles, recomputing
     P and dP (2 extra GEMMs) and accumulating dQ = dS K in registers -- on MI355X this is ~4x
     faster than fp32 atomics from every KV block (measured: docs/RESULTS.md)."""
@@ -317,7 +317,7 @@ def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N
             T.copy(Delta[bz, bx, by * block_M:(by + 1) * block_M], delta_f)
             T.clear(dq)
             loop_ed = T.ceildiv((by + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N)
-            for k in T.Pipelined(loop_ed, num_stages=num_stages):
+            for k in T.Pipelined(loop_ed, num_stages=num_stages, unroll=unroll):
                 T.copy(K[bz, k * block_N:(k + 1) * block_N, bx // groups, :], K_shared)
                 T.copy(V[bz, k * block_N:(k + 1) * block_N, bx // groups, :], V_shared)
                 T.clear(s)
@@ -344,13 +344,16 @@ def _tiles(D, Dv, kind, causal=False):
     defaults are sized for D = Dv <= 128; wider heads (e.g. D=192 / Dv=128) halve the streamed tile.
     d64 heads use the winners of scripts/sweep_fa_bwd.py (b8 h32 s1024, profiles/r3/s3/bwd/):
     non-causal dK/dV 256x64 over 8 waves (209 -> 182 us), dQ 128x64 over 8 waves (150 -> 130 us);
-    causal 64x32 / 64x64 over 4 waves (more, shorter workgroups balance the triangle)."""
+    causal 64x32 / 64x64 over 4 waves (more, shorter workgroups balance the triangle).  The lowered
+    main loops run under #pragma unroll (the ring slot of each copy a constant; outputs bitwise
+    unchanged): non-causal dK/dV 173 -> 156-160 us, dQ -1 %, causal dK/dV -2 %
+    (profiles/r6/fa_bwd_unroll_ab.log)."""
     if D + Dv <= 128:
         if causal:
-            return {"fwd": {}, "bwd": dict(block_M=64, block_N=32, threads=256),
+            return {"fwd": {}, "bwd": dict(block_M=64, block_N=32, threads=256, unroll=2),
                     "dq": dict(block_M=64, block_N=64, threads=256)}[kind]
-        return {"fwd": {}, "bwd": dict(block_M=256, block_N=64, threads=512),
-                "dq": dict(block_M=128, block_N=64, threads=512)}[kind]
+        return {"fwd": {}, "bwd": dict(block_M=256, block_N=64, threads=512, unroll=4),
+                "dq": dict(block_M=128, block_N=64, threads=512, unroll=4)}[kind]
     if D + Dv <= 256:
         return {}
     return {"fwd": dict(block_M=128), "bwd": dict(block_N=32), "dq": dict(block_N=32)}[kind]

@@ -24,6 +24,11 @@ def build(jitfn, args, kwargs, extra):
     return tilelang.compile(f, out_idx=getattr(jitfn, "out_idx", None), target="hip", pass_configs=pc)
 
 
+def _base(tiles):
+    """A tile config without its own unroll (the A/B sets it through the pass config)."""
+    return {k: v for k, v in tiles.items() if k != "unroll"}
+
+
 def cases(only=None):
     out = []
     if only in (None, "fa_bwd"):
@@ -40,10 +45,10 @@ def cases(only=None):
             # the autograd path's tiles (example_mha_bwd._tiles); outputs written in place: compared
             # through the (-2, -1) argument slots
             out.append((f"FA bwd dK/dV {tag} fp16 b8 h32 s1024 d64", E.flashattn_bwd, (B, H, S, D, causal),
-                        dict(dq_mode="none", **E._tiles(D, D, "bwd", causal)), (q, k, v, do, lse, delta, dk, dv),
+                        dict(dq_mode="none", **_base(E._tiles(D, D, "bwd", causal))), (q, k, v, do, lse, delta, dk, dv),
                         4 * fl, (-2, -1)))
             out.append((f"FA bwd dQ {tag} fp16 b8 h32 s1024 d64", E.flashattn_bwd_dq, (B, H, S, D, causal),
-                        dict(E._tiles(D, D, "dq", causal)), (q, k, v, do, lse, delta), 3 * fl, None))
+                        _base(E._tiles(D, D, "dq", causal)), (q, k, v, do, lse, delta), 3 * fl, None))
     if only in (None, "smla"):
         from tilelang.ops.dsa import sparse_mla_fwd
         Bs, Ss, SKV, Hs, topk = 1, 4096, 8192, 128, 2048
