@@ -6,6 +6,10 @@ the 256 CUs idle; splitting K multiplies the block count.  Each block finishes w
 tile-wide ``T.atomic_add`` into C (``global_atomic_add_f32`` per element for fp32 output; for
 fp16 / bf16 output the lowering pairs the two adjacent columns each lane holds into one
 ``global_atomic_pk_add_{f16,bf16}`` -- AtomicAddVectorize, tests/test_language_atomic.py).
+For fp32 output the accumulator tile goes through a row-padded LDS tile first, so each wave
+instruction adds 64 consecutive floats (lower_tile_op.lower_atomic_staged): at 1024x1024x16384
+split 8 that took the kernel from 0.162 to 0.088 ms (0.074 ms with the 64-deep K tile default,
+0.068 ms at split 4; torch 0.109 ms -- profiles/r6/splitk_sweep.log).
 """
 import argparse
 
@@ -14,7 +18,7 @@ import tilelang.language as T
 
 
 @tilelang.jit
-def matmul_splitk(M, N, K, block_M=128, block_N=128, block_K=32, split_k=4, threads=256, num_stages=2,
+def matmul_splitk(M, N, K, block_M=128, block_N=128, block_K=64, split_k=4, threads=256, num_stages=2,
                   dtype="float16", accum_dtype="float", out_dtype="float32"):
     splitK = K // split_k
 

@@ -314,6 +314,28 @@ def test_splitk_fp16_output_uses_pk_add_hip():
     assert "global_atomic_pk_add_f16" in isa and "global_atomic_cmpswap" not in isa
 
 
+def test_splitk_fp32_atomics_staged_hip():
+    """fp32 tile atomics from an MFMA accumulator go through a row-padded LDS tile so each wave
+    instruction adds 64 consecutive floats (lower_tile_op.lower_atomic_staged); a tile over the LDS
+    budget keeps the per-element form."""
+    from example_tilelang_gemm_splitk import matmul_splitk
+    src = tilelang.lower(matmul_splitk.get_tir(1024, 1024, 8192, split_k=8), target="hip").kernel_source
+    assert re.search(r"tl::atomic_add\(&C\[[^;]*\], red_ws\d+\[", src), "atomics read the LDS tile"
+    assert "* 132)" in src  # 128 floats + 4 of padding per row
+    big = tilelang.lower(matmul_splitk.get_tir(1024, 1024, 8192, block_M=256, block_N=256, block_K=64, threads=512,
+                                               split_k=8), target="hip").kernel_source
+    assert "red_ws" not in big and "tl::atomic_add(&C[" in big
+
+
+def test_f32_atomic_nest_one_element_per_lane_hip():
+    """An element-form f32 atomic nest maps one element per lane (no vector f32 atomic exists, so a
+    4-wide mapping would only spread each wave instruction over every fourth float)."""
+    src = tilelang.lower(tile_atomic_add_program(4, 64, 64, 16, 16, "float32"), target="hip").kernel_source
+    adds = [ln for ln in src.splitlines() if "tl::atomic_add(" in ln]
+    assert len(adds) == 16 * 16 // TH and "tl::atomic_addx" not in src
+    assert all("tid_ * 4" not in ln for ln in adds)
+
+
 def test_addx2_addx4_codegen_hip():
     k = tilelang.compile(addx2_program(32, 64, 8, 16, "bfloat16"), target="hip")
     assert "global_atomic_pk_add_bf16" in _isa(k)
@@ -398,6 +420,19 @@ def test_atomic_return_prev_gpu():
 @pytest.mark.gpu
 def test_lds_histogram_gpu():
     _check_hist("cuda")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N", [(1024, 1024), (1000, 904)])
+def test_splitk_fp32_staged_atomics_gpu(M, N):
+    from example_tilelang_gemm_splitk import matmul_splitk
+    K = 4096
+    k = matmul_splitk(M, N, K, split_k=8, block_K=64)
+    a = torch.randn(M, K, device="cuda", dtype=torch.float16)
+    b = torch.randn(K, N, device="cuda", dtype=torch.float16)
+    c = torch.zeros(M, N, device="cuda")
+    k(a, b, c)
+    torch.testing.assert_close(c, a.float() @ b.float(), rtol=1e-3, atol=2e-2)
 
 
 @pytest.mark.gpu

@@ -182,7 +182,7 @@ def lower(func: S.PrimFunc, target="auto", target_host=None, pass_configs: Optio
     target.gemm_interleave = cfg.get("tl.gemm_interleave")  # its 1 MFMA : 1 ds_read sched_group_barrier
     target.gemm_rs_pipe = cfg.get("tl.gemm_rs_pipe")        # register-A GEMM: B fragments streamed in groups
     # default unroll of lowered pipelined loops; TL_PIPELINE_UNROLL is the process-wide A/B switch
-    target.pipeline_unroll = cfg.get("tl.pipeline_unroll") or int(os.environ.get("TL_PIPELINE_UNROLL", "0") or 0) or None
+    target.pipeline_unroll = cfg.get("tl.pipeline_unroll") or int(os.environ.get("TL_PIPELINE_UNROLL") or 0) or None
     timings: Dict[str, float] = {}
     dks = []
     for i, k in enumerate(kernels):
@@ -190,12 +190,20 @@ def lower(func: S.PrimFunc, target="auto", target_host=None, pass_configs: Optio
         try:
             dks.append(_lower_one(func, k, target, cfg, name, timings))
         except LDSPlanError:
-            if target.kind != "hip" or getattr(target, "disable_small_dma", False):
+            if target.kind != "hip":
                 raise
-            # the padded slots of small-tile LDS-DMA (transform/pipeline.py _small_dma_plan)
-            # pushed the arena past 160 KiB: this kernel stages its small tiles through registers
-            t1 = copy.copy(target)
-            t1.disable_small_dma = True
-            dks.append(_lower_one(func, k, t1, cfg, name, timings))
+            # the arena went past 160 KiB: retry without the LDS staging of fragment f32 atomics
+            # (lower_tile_op.lower_atomic_staged), then also without the padded slots of small-tile
+            # LDS-DMA (transform/pipeline.py _small_dma_plan: small tiles through registers)
+            for flag in ("no_atomic_stage", "disable_small_dma"):
+                t1 = copy.copy(target)
+                t1.no_atomic_stage = True
+                t1.disable_small_dma = flag == "disable_small_dma"
+                try:
+                    dks.append(_lower_one(func, k, t1, cfg, name, timings))
+                    break
+                except LDSPlanError:
+                    if flag == "disable_small_dma":
+                        raise
     timings["total"] = time.perf_counter() - t0
     return CompiledArtifact(func=func, target=target, kernels=dks, is_cpu=target.kind == "cpu", timings=timings)

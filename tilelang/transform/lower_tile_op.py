@@ -1041,7 +1041,10 @@ class TileOpLowerer(Mutator):
         accs = nest.accesses()
         max_eb = max([b.dtype.bytes for b, _, _ in accs] or [4])
         cand = cw if cw else max(1, 16 // max_eb)
-        if ctx.no_vectorize:
+        ac = _atomic_add_call(nest.body)
+        if ctx.no_vectorize or (ac is not None and not cw and str(ac.args[0].buffer.dtype) == "float32"):
+            # f32 atomics have no vector form: one element per lane keeps each wave instruction on
+            # 64 consecutive floats (256 bytes) instead of every fourth float of 1 KiB
             cand = 1
         while cand > 1:
             if exts[-1] % cand == 0 and total // cand >= 1 and self._vec_ok(nest, cand):
@@ -1795,6 +1798,9 @@ class TileOpLowerer(Mutator):
         mo = {"memory_order": op.memory_order} if op.memory_order else {}
         if isinstance(op.src, BufferRegion):
             src = op.src
+            staged = self.lower_atomic_staged(op, mo)
+            if staged is not None:
+                return staged
             nest = _copy_nest(src, dst, None, atomic=op.op, atomic_attrs=mo)
             lay = None
             if src.buffer.scope == "fragment":
@@ -1803,6 +1809,59 @@ class TileOpLowerer(Mutator):
         val = op.src
         nest = _region_nest(dst, lambda idx: None, atomic=(op.op, val), atomic_attrs=mo)
         return self.lower_nest(nest)
+
+    # LDS budget of the row-contiguous staging of a fragment's f32 atomic adds
+    ATOMIC_STAGE_BYTES = 96 * 1024
+
+    def lower_atomic_staged(self, op: O.AtomicOp, mo):
+        """``T.atomic_add(global_f32[...], fragment)``: the fragment goes through an LDS tile first so
+        each wave instruction adds 64 consecutive floats of one row (256 contiguous bytes).  In the
+        MFMA accumulator layout a wave instruction adds four 64-byte row pieces instead, and gfx950
+        has no vector f32 atomic; global float atomics run at one chip-wide byte rate only when each
+        instruction covers 256 contiguous bytes (cdna_hip_programming.md Guideline 12).  The LDS
+        row pitch is padded by 4 floats so the accumulator layout's writes (lanes 16 apart are 4 rows
+        apart) fall on disjoint bank halves.  None: the plain per-element lowering applies (other
+        ops or dtypes, a thread-range partition, a tile over the budget, or the retry after an LDS
+        plan that did not fit: target.no_atomic_stage)."""
+        ctx, src, dst = self.ctx, op.src, op.dst
+        if ctx.is_cpu or getattr(ctx.target, "no_atomic_stage", False) or op.op != "add" or \
+                ctx.thread_range is not None:
+            return None
+        if src.buffer.scope != "fragment" or dst.buffer.scope != "global" or str(dst.buffer.dtype) != "float32":
+            return None
+        lay = getattr(src.buffer, "layout", None)
+        sext = src.static_extents()
+        if lay is None or sext is None or not _full(src) or len(sext) < 2 or sext[-1] < 64:
+            return None
+        sd, dd = _squeeze_pairs(src, dst)
+        if len(sd) != len(sext):
+            return None
+        pitch = sext[-1] + 4 if sext[-1] % 8 == 0 else sext[-1]
+        rows = _prod(sext[:-1])
+        if rows * pitch * 4 > self.ATOMIC_STAGE_BYTES:
+            return None
+        ws = ctx.new_workspace(rows * pitch, "float32")
+
+        def ws_at(idx):
+            return binop("+", binop("*", _row_major(list(idx[:-1]), sext[:-1]), pitch), idx[-1])
+
+        lb = ctx.local_of(src.buffer)
+        out = [L.CallStmt("tl::sync_threads", [])] if ctx.self_sync else []
+        out += [S.StoreStmt(ws, [ws_at(lay.inverse(ctx.tid, i))], cast(BufferLoad(lb, [IntImm(i)]), "float32"))
+                for i in range(lay.local_size)]
+        out.append(L.CallStmt("tl::sync_threads", []))
+        vars_ = [Var(f"sa{i}") for i in range(len(sext))]
+        didx = list(dst.mins)
+        for v, d in zip(vars_, dd):
+            didx[d] = binop("+", didx[d], v)
+        body = S.EvaluateStmt(call("tl.atomic_add", [BufferLoad(dst.buffer, didx), BufferLoad(ws, [ws_at(vars_)])],
+                                   dst.buffer.dtype, **mo))
+        for v, e in reversed(list(zip(vars_, sext))):
+            body = S.ForStmt(v, 0, e, "parallel", body, {"coalesced_width": 1})
+        out.append(self.lower_nest(body))
+        if ctx.self_sync:
+            out.append(L.CallStmt("tl::sync_threads", []))
+        return S.SeqStmt(out)
 
     def lower_FinalizeReducerOp(self, op):
         b = op.buf.buffer
