@@ -1825,7 +1825,7 @@ class TileOpLowerer(Mutator):
         plan that did not fit: target.no_atomic_stage)."""
         ctx, src, dst = self.ctx, op.src, op.dst
         if ctx.is_cpu or getattr(ctx.target, "no_atomic_stage", False) or op.op != "add" or \
-                ctx.thread_range is not None:
+                ctx.thread_range is not None or ctx.pass_cfg.get("tl.atomic_stage", True) is False:
             return None
         if src.buffer.scope != "fragment" or dst.buffer.scope != "global" or str(dst.buffer.dtype) != "float32":
             return None

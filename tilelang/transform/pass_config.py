@@ -51,6 +51,7 @@ class PassConfigKey(str, Enum):
     TL_GEMM_RS_PIPE = "tl.gemm_rs_pipe"            # register-A GEMM: B fragments streamed in groups of N
     TL_PACK_F32 = "tl.pack_f32"                    # fp32 register pairs as packed v_pk_* math
     TL_PIPELINE_UNROLL = "tl.pipeline_unroll"      # default #pragma unroll N of lowered pipelined loops
+    TL_ATOMIC_STAGE = "tl.atomic_stage"            # fragment f32 tile atomics through a row-contiguous LDS tile
 
     def __str__(self):
         return self.value
@@ -109,6 +110,9 @@ EFFECT = {
                           "prefetched GEMM (the compiler schedules the two streams itself)",
     "tl.pipeline_unroll": "N > 1: every lowered T.Pipelined main loop without its own unroll= is emitted under "
                           "#pragma unroll N (N a multiple of the ring depth: the stage slots become constants)",
+    "tl.atomic_stage": "default on; False keeps T.atomic_add(global_f32, fragment) in the accumulator layout "
+                       "(per-element atomics, four 64-byte row pieces per wave instruction) instead of staging "
+                       "the tile through LDS for 256-byte row-contiguous atomics (lower_tile_op.lower_atomic_staged)",
 }
 
 # NVIDIA-only features / TVM passes that do not exist here: the value meaning "off" is what
