@@ -3,7 +3,8 @@ definition on random data AND on data whose logits move the row max by far more 
 threshold (q scaled x8: the rescale branch fires), then warm and cold TFLOPS.
 
     python scripts/fa_variants.py '[{"sum_mfma": true}, {"sum_mfma": true, "fold_max": true}]' [--causal]
-    (a variant's "_pc" entry adds pass configs: {"fold_max": true, "_pc": {"tl.gemm_rs_pipe": 4}})
+    (a variant's "_pc" entry adds pass configs: {"fold_max": true, "_pc": {"tl.gemm_rs_pipe": 4}}; "_cf" adds
+    hipcc flags: {"_cf": ["-fno-slp-vectorize"]})
 """
 import json
 import os
@@ -46,10 +47,11 @@ for kw in variants:
     kw = dict(kw)
     pc = dict(flashattn_pipelined.pass_configs)
     pc.update(kw.pop("_pc", {}))  # extra pass configs, e.g. {"tl.gemm_rs_pipe": 4}
+    cf = kw.pop("_cf", None)      # extra hipcc flags
     a.update(kw)
     try:
         f = flashattn_pipelined.get_tir(B, H, S, D, causal, 1, **a)
-        kern = tilelang.compile(f, out_idx=[3], target="hip", pass_configs=pc)
+        kern = tilelang.compile(f, out_idx=[3], target="hip", pass_configs=pc, compile_flags=cf)
         errs = []
         for name, qq in (("rand", q), ("hot", q_hot)):
             o = kern(qq, k, v)
