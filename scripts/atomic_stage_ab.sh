@@ -6,6 +6,7 @@ set -o pipefail
 OUT=${1:-gpurun_out/atomic_ab}
 mkdir -p $OUT
 export TMPDIR=/tmp
+export PYTHONPATH=$PWD:${PYTHONPATH:-}
 FA='import sys; sys.path.insert(0, "examples/flash_attention"); import example_mha_bwd as m; m.BWD_DQ_MODE = "atomic"; m.main()'
 SK='import sys; sys.path.insert(0, "examples/gemm_streamk"); import example_tilelang_gemm_streamk as m; m.main(1024, 1024, 8192)'
 for st in 0 1; do
