@@ -24,8 +24,8 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[7], pass_configs=FAST_MATH)
 def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, block_M=128, block_N=64,
-                   block_K=32, num_stages=2, threads=256, dtype="float16", xcd_group=False, lean=False,
-                   factored=False):
+                   block_K=64, num_stages=2, threads=256, dtype="float16", xcd_group=False, lean=False,
+                   factored=False, xscale=False):
     """``factored``: the decay ``exp(a_i - b_j)`` (a = row, b = key cumulative dA) of every
     (row, key) element as ``exp(a_i - c) * exp(c - b_j)`` with ``c`` the key window's last (smallest)
     ``b``: one exp per row and one per key per K step instead of one per element (the kernel is
@@ -38,6 +38,16 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
     mask: no index compare / select per element) and the diagonal tiles, with the row decays in
     log2 units precomputed once -- the kernel is VALU-bound (PMC: 20x more VALU than MFMA
     instructions), this trims the per-element decay arithmetic.
+    ``xscale``: the key tiles wholly below the row tile (every key precedes every row) take the
+    decay off the per-element path: with ``c`` the cumulative dA of the last key before the row tile,
+    ``exp(a_i - b_j) = exp(a_i - c) * exp(c - b_j)`` and both factors are <= 1 (dA_cumsum is
+    non-increasing), so the key factor (times dt_j) scales the x tile's rows in LDS (block_K x
+    headdim elements instead of block_M x block_K), cb feeds the MFMA straight from LDS, and the
+    row factor multiplies that partial sum once at the end.  A key factor that underflows belongs to
+    a product that is smaller still.  The diagonal tiles keep the per-element exponent (there the
+    factors can leave the fp16 range).  Measured (profiles/r6/mamba_xscale_ab.log): 205 TF against
+    231 for the plain 128x64x64 tile -- the workgroup's 2-4 key tiles make the split into two short
+    pipelined loops (as in ``lean``) cost more than the per-element exponentials it saves.
     ``xcd_group``: every workgroup of one (batch, chunk) -- all heads and row tiles, which share
     that chunk's ``cb`` and ``C`` tiles (one group) -- is placed on the same XCD (workgroups go
     round-robin over the 8 XCDs by dispatch id), so the shared tiles are fetched into one XCD's L2
@@ -117,6 +127,32 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
                         cb_local[i, j] = T.Cast(accum_dtype, cb_shared[i, j]) * T.exp2(
                             am[i] - T.Cast(accum_dtype, dA_k[j]) * LOG2E) * T.Cast(accum_dtype, dt_k[j])
                     T.gemm(cb_local, x_shared, acc_o)
+                for k in T.Pipelined(n_full, n_tot, num_stages=num_stages):
+                    load_k(cb, x, dA_cumsum, dt, cb_shared, x_shared, dA_k, dt_k, b, c, g, bz, m_idx, n_idx, k)
+                    for i, j in T.Parallel(block_M, block_K):
+                        cb_local[i, j] = T.Cast(accum_dtype, cb_shared[i, j]) * T.exp2(
+                            T.if_then_else(m_idx * block_M + i >= k * block_K + j,
+                                           am[i] - T.Cast(accum_dtype, dA_k[j]) * LOG2E,
+                                           -T.infinity(accum_dtype))) * T.Cast(accum_dtype, dt_k[j])
+                    T.gemm(cb_local, x_shared, acc_o)
+            elif xscale:
+                am = T.alloc_fragment((block_M, ), accum_dtype)
+                xs_shared = T.alloc_shared((block_K, block_N), dtype)
+                acc_f = T.alloc_fragment((block_M, block_N), accum_dtype)
+                cref = T.alloc_var(accum_dtype)
+                for i in T.Parallel(block_M):
+                    am[i] = dA_m[i] * LOG2E
+                n_full = (m_idx * block_M) // block_K  # tiles whose every key precedes every row
+                cref = T.Cast(accum_dtype, dA_cumsum[b, bz, c, T.max(m_idx * block_M - 1, 0)]) * LOG2E
+                T.clear(acc_f)
+                for k in T.Pipelined(n_full, num_stages=num_stages):
+                    load_k(cb, x, dA_cumsum, dt, cb_shared, x_shared, dA_k, dt_k, b, c, g, bz, m_idx, n_idx, k)
+                    for j, n in T.Parallel(block_K, block_N):  # one key row per thread's vector
+                        xs_shared[j, n] = T.Cast(dtype, T.Cast(accum_dtype, x_shared[j, n]) * (T.exp2(
+                            cref - T.Cast(accum_dtype, dA_k[j]) * LOG2E) * T.Cast(accum_dtype, dt_k[j])))
+                    T.gemm(cb_shared, xs_shared, acc_f)
+                for i, j in T.Parallel(block_M, block_N):
+                    acc_o[i, j] += acc_f[i, j] * T.exp2(am[i] - cref)
                 for k in T.Pipelined(n_full, n_tot, num_stages=num_stages):
                     load_k(cb, x, dA_cumsum, dt, cb_shared, x_shared, dA_k, dt_k, b, c, g, bz, m_idx, n_idx, k)
                     for i, j in T.Parallel(block_M, block_K):

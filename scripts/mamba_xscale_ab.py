@@ -1,0 +1,71 @@
+"""A/B of the Mamba-2 chunk-scan variants (examples/linear_attention/example_mamba_chunk_scan.py) in one
+process: the plain per-element-decay tile, ``lean`` and ``xscale`` (key decays on the x tile for the
+key tiles below the row tile), checked against the fp32 reference on the benchmark's inputs and on
+strong decays (dA down to -1.6 per step, Mamba-2's A = -16 with dt = 0.1), then timed round-robin.
+
+    python scripts/mamba_xscale_ab.py [--seq 4096]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "examples", "linear_attention")]
+
+import torch  # noqa: E402
+
+from tilelang.profiler import do_bench  # noqa: E402
+from example_mamba_chunk_scan import chunk_scan_fwd, flops, make_inputs, ref_program  # noqa: E402
+
+VARIANTS = [
+    ("plain 128x64x32", dict(block_M=128, block_N=64, block_K=32)),
+    ("plain 128x64x64", dict(block_M=128, block_N=64, block_K=64)),
+    ("lean 128x64x64", dict(block_M=128, block_N=64, block_K=64, lean=True)),
+    ("xscale 128x64x32", dict(block_M=128, block_N=64, block_K=32, xscale=True)),
+    ("xscale 128x64x64", dict(block_M=128, block_N=64, block_K=64, xscale=True)),
+    ("xscale 64x64x64", dict(block_M=64, block_N=64, block_K=64, xscale=True)),
+    ("xscale 64x64x32", dict(block_M=64, block_N=64, block_K=32, xscale=True)),
+]
+
+
+def strong(args):
+    cb, x, dt, dA, C, st, D = args
+    g = torch.Generator(device="cuda").manual_seed(1)
+    dt2 = (torch.rand(dt.shape, device="cuda", generator=g) * 0.1)
+    A = -torch.empty(dt.shape[1], device="cuda").uniform_(1, 16, generator=g)
+    dA2 = (dt2 * A[None, :, None, None]).cumsum(-1)
+    return [cb, x, dt2.half(), dA2.half(), C, st, D]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seq", type=int, default=4096)
+    a = ap.parse_args()
+    B, H, P, N, CS = 8, 80, 64, 128, 256
+    args = make_inputs(B, a.seq, CS, 1, H, P, N)
+    sargs = strong(args)
+    refs = [ref_program(*args), ref_program(*sargs)]
+    ks = []
+    for name, kw in VARIANTS:
+        try:
+            k = chunk_scan_fwd(B, a.seq, CS, 1, H, P, N, **kw)
+            errs = []
+            for inp, ref in zip((args, sargs), refs):
+                out = k(*inp).float()
+                errs.append(((out - ref).abs().max() / ref.abs().max()).item())
+            print(f"{name}: rel max err bench-inputs {errs[0]:.2e} strong-decay {errs[1]:.2e}", flush=True)
+            ks.append((name, k))
+        except Exception as e:  # noqa: BLE001
+            print(f"{name}: FAILED {type(e).__name__}: {str(e)[:300]}", flush=True)
+    res = {n: [] for n, _ in ks}
+    for _ in range(3):
+        for n, k in ks:
+            res[n].append(do_bench(lambda: k(*args)))
+    fl = flops(B, a.seq, CS, H, P, N)
+    for n, _ in ks:
+        ms = min(res[n])
+        print(f"{n}: {ms:.4f} ms, {fl / ms * 1e-9:.1f} TF (best of 3)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

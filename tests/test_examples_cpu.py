@@ -145,16 +145,17 @@ def test_linear_attention_fwd():
     torch.testing.assert_close(h, rh, rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("xcd_group,lean,factored", [(False, False, False), (True, False, False),
-                                                     (True, True, False), (False, False, True)])
-def test_mamba_chunk_scan(xcd_group, lean, factored):
+@pytest.mark.parametrize("xcd_group,lean,factored,xscale", [(False, False, False, False), (True, False, False, False),
+                                                            (True, True, False, False), (False, False, True, False),
+                                                            (False, False, False, True)])
+def test_mamba_chunk_scan(xcd_group, lean, factored, xscale):
     """xcd_group: the grid decoded so every workgroup of a (batch, chunk) shares one XCD."""
     import example_mamba_chunk_scan as m
     B = 2 if xcd_group else 1
     args = m.make_inputs(B, 2048, 128, 1, 2, 64, 64, device="cpu") if xcd_group else \
         m.make_inputs(1, 512, 128, 1, 2, 64, 64, device="cpu")
     k = _both(m.chunk_scan_fwd, B, 2048 if xcd_group else 512, 128, 1, 2, 64, 64, xcd_group=xcd_group, lean=lean,
-              factored=factored)
+              factored=factored, xscale=xscale, **({"block_M": 64, "block_K": 32} if xscale else {}))
     torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=1e-2, atol=2e-2)
 
 
@@ -166,10 +167,11 @@ def test_mamba_chunk_scan_factored_strong_decay():
     args = m.make_inputs(1, 512, 128, 1, 2, 64, 64, device="cpu")
     dA = -torch.rand(1, 2, 4, 128) * 4.0
     args[3] = dA.cumsum(-1).half()
-    k = _both(m.chunk_scan_fwd, 1, 512, 128, 1, 2, 64, 64, factored=True)
-    out = k(*args).float()
-    assert torch.isfinite(out).all()
-    torch.testing.assert_close(out, m.ref_program(*args), rtol=1e-2, atol=2e-2)
+    for kw in (dict(factored=True), dict(xscale=True, block_M=64, block_K=32)):
+        k = _both(m.chunk_scan_fwd, 1, 512, 128, 1, 2, 64, 64, **kw)
+        out = k(*args).float()
+        assert torch.isfinite(out).all()
+        torch.testing.assert_close(out, m.ref_program(*args), rtol=1e-2, atol=2e-2)
 
 
 def test_dequant_gemm_w4a16():

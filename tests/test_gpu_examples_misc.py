@@ -150,12 +150,14 @@ def test_linear_attention_fwd():
     torch.testing.assert_close(h, rh, rtol=1e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("xcd_group,lean,factored", [(False, False, False), (True, False, False),
-                                                     (True, True, False), (True, False, True)])
-def test_mamba_chunk_scan(xcd_group, lean, factored):
+@pytest.mark.parametrize("xcd_group,lean,factored,xscale", [(False, False, False, False), (True, False, False, False),
+                                                            (True, True, False, False), (True, False, True, False),
+                                                            (False, False, False, True)])
+def test_mamba_chunk_scan(xcd_group, lean, factored, xscale):
     import example_mamba_chunk_scan as m
     args = m.make_inputs(2, 4096, 256, 1, 8, 64, 128)
-    k = m.chunk_scan_fwd(2, 4096, 256, 1, 8, 64, 128, block_K=64, xcd_group=xcd_group, lean=lean, factored=factored)
+    k = m.chunk_scan_fwd(2, 4096, 256, 1, 8, 64, 128, block_K=64, xcd_group=xcd_group, lean=lean, factored=factored,
+                         xscale=xscale)
     torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=2e-2, atol=5e-2)
 
 
@@ -163,10 +165,11 @@ def test_mamba_chunk_scan_factored_strong_decay():
     import example_mamba_chunk_scan as m
     args = m.make_inputs(1, 1024, 256, 1, 4, 64, 128)
     args[3] = (-torch.rand(1, 4, 4, 256, device="cuda") * 4.0).cumsum(-1).half()
-    k = m.chunk_scan_fwd(1, 1024, 256, 1, 4, 64, 128, block_K=64, factored=True)
-    out = k(*args).float()
-    assert torch.isfinite(out).all()
-    torch.testing.assert_close(out, m.ref_program(*args), rtol=2e-2, atol=5e-2)
+    for kw in (dict(factored=True), dict(xscale=True)):
+        k = m.chunk_scan_fwd(1, 1024, 256, 1, 4, 64, 128, block_K=64, **kw)
+        out = k(*args).float()
+        assert torch.isfinite(out).all()
+        torch.testing.assert_close(out, m.ref_program(*args), rtol=2e-2, atol=5e-2)
 
 
 def test_dequant_gemm_w4a16():
