@@ -25,7 +25,7 @@ LOG2E = 1.44269504
 @tilelang.jit(out_idx=[7], pass_configs=FAST_MATH)
 def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, block_M=128, block_N=64,
                    block_K=64, num_stages=2, threads=256, dtype="float16", xcd_group=False, lean=False,
-                   factored=False, xscale=False):
+                   factored=False, xscale=False, ds_blk=None):
     """``factored``: the decay ``exp(a_i - b_j)`` (a = row, b = key cumulative dA) of every
     (row, key) element as ``exp(a_i - c) * exp(c - b_j)`` with ``c`` the key window's last (smallest)
     ``b``: one exp per row and one per key per K step instead of one per element (the kernel is
@@ -48,6 +48,9 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
     factors can leave the fp16 range).  Measured (profiles/r6/mamba_xscale_ab.log): 205 TF against
     231 for the plain 128x64x64 tile -- the workgroup's 2-4 key tiles make the split into two short
     pipelined loops (as in ``lean``) cost more than the per-element exponentials it saves.
+    ``ds_blk``: the inter-chunk GEMM C x prev_state^T streamed over dstate in ds_blk-wide slices
+    (serial, one LDS slice of each) instead of staging the whole [block_M + block_N, dstate] pair:
+    the workgroup's LDS peak falls to the main loop's ring, so more workgroups fit on a CU.
     ``xcd_group``: every workgroup of one (batch, chunk) -- all heads and row tiles, which share
     that chunk's ``cb`` and ``C`` tiles (one group) -- is placed on the same XCD (workgroups go
     round-robin over the 8 XCDs by dispatch id), so the shared tiles are fetched into one XCD's L2
@@ -91,8 +94,9 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
             cb_shared = T.alloc_shared((block_M, block_K), dtype)
             cb_local = T.alloc_fragment((block_M, block_K), dtype)
             x_shared = T.alloc_shared((block_K, block_N), dtype)
-            C_shared = T.alloc_shared((block_M, dstate), dtype)
-            st_shared = T.alloc_shared((block_N, dstate), dtype)
+            dsb = ds_blk or dstate
+            C_shared = T.alloc_shared((block_M, dsb), dtype)
+            st_shared = T.alloc_shared((block_N, dsb), dtype)
             dA_m = T.alloc_fragment((block_M, ), accum_dtype)
             scale_m = T.alloc_fragment((block_M, ), accum_dtype)
             dA_k = T.alloc_shared((block_K, ), dtype)
@@ -109,10 +113,17 @@ def chunk_scan_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, 
             T.copy(dA_cumsum[b, bz, c, m_idx * block_M:(m_idx + 1) * block_M], dA_m)
             for i in T.Parallel(block_M):
                 scale_m[i] = T.exp2(dA_m[i] * LOG2E)
-            T.copy(C[b, row0:row0 + block_M, g, :], C_shared)
-            T.copy(prev_states[b, c, bz, n_idx * block_N:(n_idx + 1) * block_N, :], st_shared)
             T.clear(acc_o)
-            T.gemm(C_shared, st_shared, acc_o, transpose_B=True)
+            if dsb == dstate:
+                T.copy(C[b, row0:row0 + block_M, g, :], C_shared)
+                T.copy(prev_states[b, c, bz, n_idx * block_N:(n_idx + 1) * block_N, :], st_shared)
+                T.gemm(C_shared, st_shared, acc_o, transpose_B=True)
+            else:
+                for s in T.serial(dstate // dsb):
+                    T.copy(C[b, row0:row0 + block_M, g, s * dsb:(s + 1) * dsb], C_shared)
+                    T.copy(prev_states[b, c, bz, n_idx * block_N:(n_idx + 1) * block_N, s * dsb:(s + 1) * dsb],
+                           st_shared)
+                    T.gemm(C_shared, st_shared, acc_o, transpose_B=True)
             for i, j in T.Parallel(block_M, block_N):
                 acc_o[i, j] *= scale_m[i]
             n_tot = T.ceildiv((m_idx + 1) * block_M, block_K)

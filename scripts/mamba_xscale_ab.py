@@ -14,17 +14,20 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "examples", "linear_attention")]
 
 import torch  # noqa: E402
 
+import tilelang  # noqa: E402
 from tilelang.profiler import do_bench  # noqa: E402
-from example_mamba_chunk_scan import chunk_scan_fwd, flops, make_inputs, ref_program  # noqa: E402
+from example_mamba_chunk_scan import chunk_scan_fwd, chunk_scan_fwd_fused, flops, make_inputs, ref_program  # noqa: E402,E501
 
-VARIANTS = [
-    ("plain 128x64x32", dict(block_M=128, block_N=64, block_K=32)),
+VARIANTS = [  # name, kernel kwargs (a "_pc" entry: pass configs; "_fused": chunk_scan_fwd_fused)
     ("plain 128x64x64", dict(block_M=128, block_N=64, block_K=64)),
-    ("lean 128x64x64", dict(block_M=128, block_N=64, block_K=64, lean=True)),
-    ("xscale 128x64x32", dict(block_M=128, block_N=64, block_K=32, xscale=True)),
+    ("plain 128x64x32", dict(block_M=128, block_N=64, block_K=32)),
     ("xscale 128x64x64", dict(block_M=128, block_N=64, block_K=64, xscale=True)),
-    ("xscale 64x64x64", dict(block_M=64, block_N=64, block_K=64, xscale=True)),
-    ("xscale 64x64x32", dict(block_M=64, block_N=64, block_K=32, xscale=True)),
+    ("ds64 128x64x32 mw4", dict(block_M=128, block_N=64, block_K=32, ds_blk=64, _pc={"tl.min_waves_per_eu": 4})),
+    ("plain 128x64x128", dict(block_M=128, block_N=64, block_K=128)),
+    ("ds64 128x64x128 st1", dict(block_M=128, block_N=64, block_K=128, num_stages=1, ds_blk=64)),
+    ("plain 256x64x64 t512", dict(block_M=256, block_N=64, block_K=64, threads=512)),
+    ("ds64 256x64x64 t512", dict(block_M=256, block_N=64, block_K=64, threads=512, ds_blk=64)),
+    ("fused k64 t512", dict(_fused=True, block_K=64)),
 ]
 
 
@@ -48,7 +51,12 @@ def main():
     ks = []
     for name, kw in VARIANTS:
         try:
-            k = chunk_scan_fwd(B, a.seq, CS, 1, H, P, N, **kw)
+            kw = dict(kw)
+            fn = chunk_scan_fwd_fused if kw.pop("_fused", False) else chunk_scan_fwd
+            pc = dict(fn.pass_configs)
+            pc.update(kw.pop("_pc", {}))
+            k = tilelang.compile(fn.get_tir(B, a.seq, CS, 1, H, P, N, **kw), out_idx=[7], target="hip",
+                                 pass_configs=pc)
             errs = []
             for inp, ref in zip((args, sargs), refs):
                 out = k(*inp).float()
