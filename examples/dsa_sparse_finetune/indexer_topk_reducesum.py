@@ -76,7 +76,7 @@ def index_logits(seq_len, heads, dim, block_N=64, threads=256, sm_scale=None, dt
     return main
 
 
-@tilelang.jit(out_idx=[3, 4, 5])
+@tilelang.jit(out_idx=[3, 4, 5], pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True})
 def topk_softmax(seq_len, N, topk, threads=64):
     """Selected logits -> softmax; picks of masked keys (logit -inf) get score 0 and index -1."""
 

@@ -15,7 +15,7 @@ import tilelang.language as T
 LOG2E = 1.44269504
 
 
-@tilelang.jit(out_idx=[4])
+@tilelang.jit(out_idx=[4], pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True})
 def sparse_mla_topk_reducesum(seq_len, heads, dqk, topk, sm_scale=None, block_I=32, threads=256,
                               dtype="bfloat16"):
     scale = (dqk**-0.5 if sm_scale is None else sm_scale) * LOG2E

@@ -5,6 +5,7 @@ pre-warm; outputs compared bitwise between the builds (the unroll changes no ari
     python scripts/unroll_ab.py [--unroll 2]
 """
 import argparse
+import json
 import os
 import sys
 import time
@@ -79,12 +80,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--unroll", type=int, default=2)
     ap.add_argument("--only", choices=["fa_bwd", "smla", "mamba"], default=None)
+    ap.add_argument("--pc", default=None, help='B variant pass configs instead of the unroll, e.g. \'{"tl.enable_fast_math": true}\'')
     a = ap.parse_args()
     torch.manual_seed(0)
     runs = []
     for name, fn, args, kw, inputs, flops, slots in cases(a.only):
         ks = []
-        for tag, extra in (("base", {}), (f"unroll{a.unroll}", {"tl.pipeline_unroll": a.unroll})):
+        bvar = ("pc", json.loads(a.pc)) if a.pc else (f"unroll{a.unroll}", {"tl.pipeline_unroll": a.unroll})
+        for tag, extra in (("base", {}), bvar):
             try:
                 kern = build(fn, args, kw, extra)
                 ks.append((tag, kern, _outs(kern(*inputs), inputs, slots)))

@@ -13,7 +13,11 @@ from tilelang.layout import PaddedLayout
 LOG2E = 1.44269504
 
 
-@tilelang.jit(out_idx=[3, 4], pass_configs={tilelang.PassConfigKey.TL_GEMM_FOLD_DEFAULT_GUARD: False})
+# exp2 straight on v_exp_f32 (differs from the OCML expansion only below 2^-126): 772 -> 826 TF at the
+# reference's benchmark shape (profiles/r6/smla_fast_math_ab.log; the expansion's range checks were
+# 3 VALU per exponential in a VALU-issue-bound loop)
+@tilelang.jit(out_idx=[3, 4], pass_configs={tilelang.PassConfigKey.TL_GEMM_FOLD_DEFAULT_GUARD: False,
+                                            tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True})
 def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_group=1, sm_scale=None, block_I=64,
                    threads=None, dtype="bfloat16", num_stages=2, block_H=None, xcd_pair=True, lazy_rescale=True,
                    wide=None, staged_out=True):
