@@ -305,7 +305,8 @@ def test_gather_rows_cpu():
     _gather_rows_check("cpu", "cpu")
     # the HIP lowering is a lane-addressed buffer LDS-DMA inside the pipeline
     src = _gather_rows_kernel(300, 256, 64, 4, "hip").get_kernel_source()
-    assert "tl::buffer_lds16" in src and "4294967280u" in src
+    # invalid indices clamp (unsigned) to the row count: an offset at or past num_records reads zeros
+    assert "tl::buffer_lds16" in src and "tl::min_(((uint32_t)(" in src and ", 300u)" in src
 
 
 def test_nsa_fwd_cpu():

@@ -2056,9 +2056,14 @@ class TileOpLowerer(Mutator):
                 iv = BufferLoad(regs, [IntImm(i)])
             else:
                 iv = self.expr(_gather_index(op.idx, row))
-            ok = logical_and(binop(">=", iv, 0), binop("<", iv, nrows))
-            off = binop("*", binop("+", binop("*", iv, stride_r), binop("*", lch, epc)), p["eb"])
-            voff = select(ok, cast(off, _dt.uint32), IntImm(0xFFFFFFF0, _dt.uint32))
+            # invalid rows (negative or past the tensor) clamp to row ``nrows`` as unsigned: their
+            # offset is at or past num_records, so the hardware writes zeros -- one v_min_u32
+            # instead of two compares, a select and the exec-mask juggling around the offset
+            u32 = _dt.uint32
+            iu = binop("min", cast(iv, u32), cast(nrows, u32))
+            off = binop("*", binop("+", binop("*", iu, cast(stride_r, u32)), cast(binop("*", lch, epc), u32)),
+                        IntImm(p["eb"], u32))
+            voff = off
             lds_off = binop("+", base_off, binop("*", chunk_base, epc))
             out.append(L.CallStmt("tl::buffer_lds16", [rsrc, voff, L.BufferPtr(ctx.flat_of(NB), lds_off)]))
         return S.SeqStmt(out)
