@@ -26,9 +26,11 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[-1], pass_configs=FAST_MATH)
 def nsa_fwd(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=None, block_size=64, groups=16,
-            selected_blocks=16, num_stages=2, block_T=32, dtype="bfloat16"):
+            selected_blocks=16, num_stages=2, block_T=32, dtype="bfloat16", unroll=2):
     """``block_T`` rows of a selected block per pipeline step (a 64-token block in two 32-row
-    steps keeps LDS at ~36 KB, so 4 blocks share a CU)."""
+    steps keeps LDS at ~36 KB, so 4 blocks share a CU).  ``unroll``: the lowered main loop is
+    emitted twice per trip (the LDS ring slot of each copy a constant): 2.135 -> 1.777 ms at
+    B4 SQ4096 HQ64 H4 D128 S16x64 (profiles/r6/secondary_sweep.log)."""
     scale = ((1.0 / dim)**0.5 if scale is None else scale) * LOG2E
     head_kv = heads // groups
     G, BS, S, D = groups, block_size, selected_blocks, dim
@@ -65,7 +67,7 @@ def nsa_fwd(batch, heads, seq_len, seq_len_kv, dim, is_causal=True, scale=None, 
             T.fill(acc_o, 0)
             T.fill(l_sum, 0)
             T.fill(m, -(2.0**30))
-            for i in T.Pipelined(S * NT, num_stages=num_stages):
+            for i in T.Pipelined(S * NT, num_stages=num_stages, unroll=unroll):
                 blk = BlockIndices[b, bx, h, i // NT]
                 # clamped into the tensor, so the copies are provably in bounds (LDS-DMA)
                 i_s = T.min(T.max(blk, 0), seq_len_kv // BS - 1) * BS + (i % NT) * BT
