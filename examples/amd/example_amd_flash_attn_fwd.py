@@ -18,12 +18,14 @@ FAST_MATH = {tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True}
 
 @tilelang.jit(out_idx=[3], pass_configs=FAST_MATH)
 def fast_flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_M=256, block_N=64, num_split_q=None,
-                   threads=512, num_stages=2, dtype="float16", mfma="16x16"):
+                   threads=512, num_stages=2, dtype="float16", mfma="16x16", unroll=2):
     """``num_split_q`` resident workgroups per (batch, head) (default: enough to put one 8-wave
     workgroup on each of the 256 CUs).  Work assignment in cost order: query tiles are ranked
     longest-first (causal: the last tiles see the most keys) and dealt to the workgroups of a head
     in a snake (``s, 2S-1-s, 2S+s, ...``), so every workgroup of a causal head gets the same number
-    of KV blocks (tile pairs (i, n-1-i)) and no CU idles at the end."""
+    of KV blocks (tile pairs (i, n-1-i)) and no CU idles at the end.  ``unroll``: the KV loop is
+    emitted twice per trip (constant LDS ring slots): 506 -> 539 TF at b1 h8 s4096 d128
+    (profiles/r6/unroll_sweep_examples.log)."""
     scale = (1.0 / dim)**0.5 * 1.44269504
     head_kv = heads // groups
     q_shape = [batch, seq_len, heads, dim]
@@ -71,7 +73,7 @@ def fast_flashattn(batch, heads, seq_len, dim, is_causal=False, groups=1, block_
                     loop_end = (T.min(T.ceildiv((bx + 1) * block_M, block_N), T.ceildiv(seq_len, block_N))
                                 if is_causal else T.ceildiv(seq_len, block_N))
                     for k in T.Pipelined(loop_end, num_stages=num_stages, order=[-1, 0, 3, 1, -1, 2],
-                                         stage=[-1, 0, 0, 1, -1, 1], group=group):
+                                         stage=[-1, 0, 0, 1, -1, 1], group=group, unroll=unroll):
                         T.copy(K[bz, k * block_N:(k + 1) * block_N, by // groups, :], K_shared)
                         if is_causal:
                             if (k + 1) * block_N <= bx * block_M + 1:  # block fully visible: no mask

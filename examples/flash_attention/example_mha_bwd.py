@@ -31,7 +31,7 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[3, 4], pass_configs=FAST_MATH)
 def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=256, block_N=64, threads=None, dtype="float16",
-                  groups=1, num_stages=2, dim_v=None):
+                  groups=1, num_stages=2, dim_v=None, unroll=None):
     """Forward that also writes the base-2 LSE (the training forward).  Schedule as the sink
     kernel (examples/attention_sink): heads on the fastest grid axis and the heaviest causal
     query tiles first, KV tiles below the diagonal in an unmasked loop and the diagonal ones
@@ -108,7 +108,7 @@ def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=256, block_N=64
             else:
                 end = T.ceildiv(seq_len, block_N)
                 full_end = seq_len // block_N
-            for k in T.Pipelined(full_end, num_stages=num_stages):
+            for k in T.Pipelined(full_end, num_stages=num_stages, unroll=unroll):
                 step(K, V, Q_shared, K_shared, V_shared, acc_s, acc_s_cast, acc_o, m, m_prev, alpha, r_sum, l_sum, k,
                      qt, by, bz, False)
             for k in T.Pipelined(full_end, end, num_stages=num_stages):
@@ -345,18 +345,20 @@ def _tiles(D, Dv, kind, causal=False):
     d64 heads use the winners of scripts/sweep_fa_bwd.py (b8 h32 s1024, profiles/r3/s3/bwd/):
     non-causal dK/dV 256x64 over 8 waves (209 -> 182 us), dQ 128x64 over 8 waves (150 -> 130 us);
     causal 64x32 / 64x64 over 4 waves (more, shorter workgroups balance the triangle).  The lowered
-    main loops run under #pragma unroll (the ring slot of each copy a constant; outputs bitwise
-    unchanged): non-causal dK/dV 173 -> 156-160 us, dQ -1 %, causal dK/dV -2 %
-    (profiles/r6/fa_bwd_unroll_ab.log)."""
+    main loops run under #pragma unroll where that measured faster (the ring slot of each copy a
+    constant; outputs bitwise identical; profiles/r6/fa_bwd_unroll_ab.log, fa_train_unroll_ab.log):
+    d64 dK/dV 173 -> 156 us, d128 dK/dV / dQ +8.5 / +9.4 %, forward +2-7 % non-causal; the causal
+    d128 forward and dK/dV and the GQA d192 dK/dV lose 0.5-1.7 % and keep the plain loop."""
+    fwd = {} if causal else dict(unroll=2)
     if D + Dv <= 128:
         if causal:
-            return {"fwd": {}, "bwd": dict(block_M=64, block_N=32, threads=256, unroll=2),
-                    "dq": dict(block_M=64, block_N=64, threads=256)}[kind]
-        return {"fwd": {}, "bwd": dict(block_M=256, block_N=64, threads=512, unroll=4),
+            return {"fwd": fwd, "bwd": dict(block_M=64, block_N=32, threads=256, unroll=2),
+                    "dq": dict(block_M=64, block_N=64, threads=256, unroll=2)}[kind]
+        return {"fwd": fwd, "bwd": dict(block_M=256, block_N=64, threads=512, unroll=4),
                 "dq": dict(block_M=128, block_N=64, threads=512, unroll=4)}[kind]
     if D + Dv <= 256:
-        return {}
-    return {"fwd": dict(block_M=128), "bwd": dict(block_N=32), "dq": dict(block_N=32)}[kind]
+        return {"fwd": fwd, "bwd": {} if causal else dict(unroll=2), "dq": dict(unroll=2)}[kind]
+    return {"fwd": dict(block_M=128, **fwd), "bwd": dict(block_N=32), "dq": dict(block_N=32, unroll=2)}[kind]
 
 
 def _kv_split(B, S, HKV, G, block_M, target_wgs=512):
@@ -385,7 +387,8 @@ class _attention:
                     G = H // k.shape[2]
                     dt = "bfloat16" if q.dtype == torch.bfloat16 else "float16"
                     Dv = v.shape[-1]
-                    fwd = flashattn_fwd(B, H, S, D, causal, dtype=dt, groups=G, dim_v=Dv, **_tiles(D, Dv, "fwd"))
+                    fwd = flashattn_fwd(B, H, S, D, causal, dtype=dt, groups=G, dim_v=Dv,
+                                        **_tiles(D, Dv, "fwd", causal))
                     o, lse = fwd(q, k, v)
                     ctx.save_for_backward(q, k, v, o, lse)
                     ctx.causal = causal
