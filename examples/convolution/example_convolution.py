@@ -14,7 +14,7 @@ import tilelang.language as T
 
 @tilelang.jit(out_idx=[2])
 def convolution(N, C, H, W, F, K, S, D, P, block_M=128, block_N=128, block_K=64, num_stages=2, threads=256,
-                dtype="float16", accum_dtype="float"):
+                dtype="float16", accum_dtype="float", unroll=2):
     KH = KW = K
     OH = (H + 2 * P - D * (K - 1) - 1) // S + 1
     OW = (W + 2 * P - D * (K - 1) - 1) // S + 1
@@ -31,7 +31,8 @@ def convolution(N, C, H, W, F, K, S, D, P, block_M=128, block_N=128, block_K=64,
             kernel_flat = T.Tensor((KH * KW * C, F), dtype, kernel.data)
             out_flat = T.Tensor((N * OH * OW, F), dtype, out.data)
             T.clear(out_local)
-            for k_iter in T.Pipelined(KH * KW * C // block_K, num_stages=num_stages):
+            # unrolled (constant ring slots): 2.015 -> 1.962 ms at the example's shape
+            for k_iter in T.Pipelined(KH * KW * C // block_K, num_stages=num_stages, unroll=unroll):
                 T.c2d_im2col(data, data_shared, by, k_iter, KH, S, D, P)
                 T.copy(kernel_flat[k_iter * block_K, bx * block_N], kernel_shared)
                 T.gemm(data_shared, kernel_shared, out_local)

@@ -306,9 +306,10 @@ def sparse_mla_bwd(q, kv, o, do, indices, lse, sm_scale=None, target=None, dkv="
     The gather path holds one bf16 partial row per (token, slot): B*S*topk*576*2 bytes (4.8 GB
     at S=4096, topk=2048) plus a sort of B*S*topk keys.  Past ``gather_budget_bytes`` (default: a
     quarter of the device's free memory; a fixed 4 GiB had sent the reference shape to the atomic
-    path, 9.3 -> 19.9 ms) it falls back to the atomic path, whose footprint is the O(SKV*576) fp32 dKV alone.  Numerics: each
-    partial row is rounded to bf16 before the fp32 sum (the atomic path adds fp32 partials), an
-    extra ~2^-9 relative error per partial that averages out over the rows a KV row collects;
+    path, 9.3 -> 19.9 ms) it falls back to the atomic path, whose footprint is the O(SKV*576) fp32
+    dKV alone.  Numerics: each partial row is rounded to bf16 before the fp32 sum (the atomic path
+    adds fp32 partials), an extra ~2^-9 relative error per partial that averages out over the rows
+    a KV row collects;
     tests/test_examples_cpu.py and test_gpu_examples_misc.py check both paths against fp32."""
     import torch
     B, S, H, DQK = q.shape

@@ -21,7 +21,7 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[4], pass_configs=FAST_MATH)
 def chunk_state_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate, block_M=None, block_N=None,
-                    block_K=64, num_stages=2, threads=256, dtype="float16"):
+                    block_K=64, num_stages=2, threads=256, dtype="float16", unroll=2):
     accum_dtype = "float"
     block_M = headdim if block_M is None else block_M
     block_N = dstate if block_N is None else block_N
@@ -53,7 +53,7 @@ def chunk_state_fwd(batch, seqlen, chunk_size, ngroups, nheads, headdim, dstate,
             g = bz // hpg
             last = T.Cast(accum_dtype, dA_cumsum[b, bz, c, chunk_size - 1]) * LOG2E
             T.clear(acc)
-            for k in T.Pipelined(chunk_size // block_K, num_stages=num_stages):
+            for k in T.Pipelined(chunk_size // block_K, num_stages=num_stages, unroll=unroll):  # 0.212 -> 0.206 ms
                 r0 = c * chunk_size + k * block_K
                 T.copy(x[b, r0:r0 + block_K, bz, m_idx * block_M:(m_idx + 1) * block_M], x_s)
                 T.copy(B[b, r0:r0 + block_K, g, n_idx * block_N:(n_idx + 1) * block_N], B_s)
