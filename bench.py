@@ -57,7 +57,10 @@ GEMM_CFG = dict(M=4096, N=4096, K=4096, block_M=256, block_N=256, block_K=64, th
 # unroll=2: the main loop as two copies, so both LDS ring slots are compile-time offsets (no per-tile
 # address VALU): 1089 -> 1094 TF, same process, round-robin (profiles/r6/fa_unroll_ab.log)
 ATTN_CFG = dict(batch=1, heads=64, seq_len=4096, dim=128, block_M=256, block_N=64, threads=512, num_stages=2,
-                q_in_regs=True, sum_mfma=True, fold_max=True, young_prio=True, xcd_heads=True, unroll=2)
+                q_in_regs=True, sum_mfma=True, fold_max=True, young_prio=True, xcd_heads=True, unroll=2,
+                # P V's B fragments streamed through the MFMAs in groups of 4 (tl::gemm_rs PIPE): +1.3 %
+                # non-causal and causal, same process (profiles/r6/fa_rs_pipe_ab.log)
+                pass_configs={"tl.gemm_rs_pipe": 4})
 MOE_CFG = dict(tokens=2048, hidden=4096, ffn=2048, experts=8, topk=2)
 # expert row tiles of 256 + MOE_EXT_M rows, every expert's rows spread evenly over its tiles
 # (ops/moe.py expert_gemm_sk_kernel ext_M): a random-routing expert of ~529 rows is two units, not three
