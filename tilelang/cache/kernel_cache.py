@@ -76,7 +76,8 @@ def kernel_key(func, target, out_idx, pass_configs, compile_flags) -> str:
     blob = json.dumps({"hooks": hook_fingerprint(), "ir": func.script(), "target": str(target),
                        "env": {"TL_GEMM_QUAD": os.environ.get("TL_GEMM_QUAD", "1"),
                                "TL_PIPELINE_UNROLL": os.environ.get("TL_PIPELINE_UNROLL", "0"),
-                               "TL_ATOMIC_STAGE": os.environ.get("TL_ATOMIC_STAGE", "1")},  # lower.py A/B switches
+                               "TL_ATOMIC_STAGE": os.environ.get("TL_ATOMIC_STAGE", "1"),
+                               "TL_GEMM_RS_PIPE": os.environ.get("TL_GEMM_RS_PIPE", "")},  # lower.py A/B switches
                        "out_idx": _freeze(out_idx),
                        "pass_configs": _freeze(pass_configs or {}), "flags": _freeze(compile_flags or []),
                        "compiler": compiler_fingerprint()}, sort_keys=True)

@@ -181,6 +181,8 @@ def lower(func: S.PrimFunc, target="auto", target_host=None, pass_configs: Optio
     target.gemm_prefetch = cfg.get("tl.gemm_prefetch")      # register-prefetched K-half GEMM schedule
     target.gemm_interleave = cfg.get("tl.gemm_interleave")  # its 1 MFMA : 1 ds_read sched_group_barrier
     target.gemm_rs_pipe = cfg.get("tl.gemm_rs_pipe")        # register-A GEMM: B fragments streamed in groups
+    if target.gemm_rs_pipe is None and os.environ.get("TL_GEMM_RS_PIPE"):  # process-wide A/B switch
+        target.gemm_rs_pipe = int(os.environ["TL_GEMM_RS_PIPE"]) or None
     target.no_atomic_stage = os.environ.get("TL_ATOMIC_STAGE", "1") == "0"  # process-wide A/B switch
     # default unroll of lowered pipelined loops; TL_PIPELINE_UNROLL is the process-wide A/B switch
     target.pipeline_unroll = cfg.get("tl.pipeline_unroll") or int(os.environ.get("TL_PIPELINE_UNROLL") or 0) or None
