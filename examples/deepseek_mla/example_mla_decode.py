@@ -14,11 +14,17 @@ import tilelang.language as T
 
 @tilelang.jit(out_idx=[6], pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True})
 def mla_decode(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, block_H=64, num_split=4,
-               threads=None, num_stages=2, dtype="float16", wide=None):
+               threads=None, num_stages=2, dtype="float16", wide=None, sum_mfma=None):
     """``wide`` (default for 64-head blocks): 8 waves, S on a 4x2 wave grid, P through LDS and
-    O = P KV split over the 512 latent columns (see tilelang/ops/dsa.py sparse_mla_fwd)."""
+    O = P KV split over the 512 latent columns (see tilelang/ops/dsa.py sparse_mla_fwd).
+    ``sum_mfma`` (wide): the softmax row sums come from the matrix cores -- P (already in LDS for
+    P KV) times a ones tile accumulates next to O and is rescaled with it -- instead of a per-tile
+    cross-wave reduction through LDS (its barrier and shuffles leave the loop): b128 h128 kv8192
+    727 -> 756 TF (default with ``wide``; profiles/r6/mla_sum_mfma_ab.log)."""
     if wide is None:
         wide = block_H == 64
+    if sum_mfma is None:
+        sum_mfma = wide
     if threads is None:
         threads = 512 if wide else 256
     s_policy = T.GemmWarpPolicy.Square if wide else T.GemmWarpPolicy.FullRow
@@ -50,6 +56,12 @@ def mla_decode(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, bl
             T.copy(Q[bx, by * VALID_BLOCK_H:(by + 1) * VALID_BLOCK_H, :], Q_local)
             T.copy(Q_pe[bx, by * VALID_BLOCK_H:(by + 1) * VALID_BLOCK_H, :], Q_pe_local)
             any_s = T.alloc_shared([2], "int32")
+            use_sm = wide and sum_mfma
+            if use_sm:
+                ones_s = T.alloc_shared([block_N, 32], dtype)
+                acc_l = T.alloc_fragment([block_H, 32], accum_dtype)
+                T.fill(ones_s, 1.0)
+                T.clear(acc_l)
             T.fill(acc_o, 0)
             T.fill(logsum, 0)
             # wide: lazy rescale (a row keeps its max until a score beats it by 2^8, P <= 256), so
@@ -86,22 +98,36 @@ def mla_decode(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, bl
                         scores_scale[i] = T.exp2(scores_max_prev[i] * scale - scores_max[i] * scale)
                 for i, j in T.Parallel(block_H, block_N):
                     acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
-                T.reduce_sum(acc_s, scores_sum, dim=1)
-                for i in T.Parallel(block_H):
-                    logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
+                if not use_sm:
+                    T.reduce_sum(acc_s, scores_sum, dim=1)
+                    for i in T.Parallel(block_H):
+                        logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
                 if wide:
                     T.copy(scores_scale, sc_shared)
                     T.copy(acc_s, P_shared)
                     if any_s[k % 2] != 0:
                         for i, j in T.Parallel(block_H, dim):
                             acc_o[i, j] *= sc_shared[i]
+                        if use_sm:
+                            for i, j in T.Parallel(block_H, 32):
+                                acc_l[i, j] *= sc_shared[i]
                     T.gemm(P_shared, KV_shared, acc_o)
+                    if use_sm:
+                        T.gemm(P_shared, ones_s, acc_l)
                 else:
                     T.copy(acc_s, acc_s_cast)
                     for i, j in T.Parallel(block_H, dim):
                         acc_o[i, j] *= scores_scale[i]
                     T.gemm(acc_s_cast, KV_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
-            if wide:
+            if use_sm:
+                for i, j in T.Parallel(block_H, 32):  # every column of P x ones is the row sum
+                    if j == 0:
+                        sc_shared[i] = acc_l[i, j]
+                for i in T.Parallel(block_H):
+                    logsum[i] = sc_shared[i]
+                for i, j in T.Parallel(block_H, dim):
+                    acc_o[i, j] /= sc_shared[i]
+            elif wide:
                 T.copy(logsum, sc_shared)
                 for i, j in T.Parallel(block_H, dim):
                     acc_o[i, j] /= sc_shared[i]

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--kv", type=int, default=8192)
     ap.add_argument("--variants", default="qk8_pv16_64_1,qk8_pv8_64_1,qk8_pv8_64_2,qk8_pv8_128_1")
     ap.add_argument("--splits", default="1")
-    ap.add_argument("--bf16-variants", default="", help="extra bf16 configs block_N_stages_split[_blockH], e.g. 64_2_2")
+    ap.add_argument("--bf16-variants", default="", help="extra bf16 configs block_N_stages_split[_blockH[_summfma]], e.g. 64_2_2 or 64_2_1_64_1")
     a = ap.parse_args()
     B, H, S, D, P = a.batch, a.heads, a.kv, 512, 64
     torch.manual_seed(0)
@@ -49,8 +49,10 @@ def main():
         parts = [int(x) for x in v.split("_")]
         bn, st, ns = parts[:3]
         bh = parts[3] if len(parts) > 3 else 64
+        sm = bool(parts[4]) if len(parts) > 4 else False  # sum_mfma
         try:
-            kb = mla_decode(B, H, 1, S, D, P, block_N=bn, block_H=bh, num_split=ns, num_stages=st, dtype="bfloat16")
+            kb = mla_decode(B, H, 1, S, D, P, block_N=bn, block_H=bh, num_split=ns, num_stages=st, dtype="bfloat16",
+                            sum_mfma=sm)
             gb, pb = torch.empty(B, H, ns, device="cuda"), torch.empty(B, H, ns, D, device="cuda")
             o = kb(q, qpe, kv16, kpe, gb, pb)
             print(f"bf16 {v}: rel err {((o.float() - r).norm() / r.norm()).item():.2e}", flush=True)

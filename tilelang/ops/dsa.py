@@ -20,7 +20,7 @@ LOG2E = 1.44269504
                                             tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True})
 def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_group=1, sm_scale=None, block_I=64,
                    threads=None, dtype="bfloat16", num_stages=2, block_H=None, xcd_pair=True, lazy_rescale=True,
-                   wide=None, staged_out=True):
+                   wide=None, staged_out=True, sum_mfma=None):
     """Sparse MLA forward over the ``topk`` selected latent rows of every query token.
 
     Schedule (MI355X): one block per (token, 64-head slice); Q stays in registers (it is the
@@ -30,7 +30,10 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
     ``wide`` (default for 64-head slices): 8 waves, S = Q K^T on a 4x2 wave grid, P through
     LDS and O = P V split over the 512 latent columns, so each wave holds a quarter of the O
     accumulator and two waves share every SIMD (656 TF vs 531 TF for the 4-wave FullRow
-    form, where every wave owns 16 head rows and P never leaves registers)."""
+    form, where every wave owns 16 head rows and P never leaves registers).
+    ``sum_mfma`` (default with ``wide``): the softmax row sums come from P (already in LDS for P V)
+    times a ones tile on the MFMA, rescaled with O, instead of a per-tile cross-wave reduction
+    through LDS and its barrier (examples/deepseek_mla/example_mla_decode.py, +4 % there)."""
     assert topk % block_I == 0
     if sm_scale is None:
         sm_scale = (1.0 / (dim + tail_dim))**0.5
@@ -44,6 +47,7 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
     valid_h = min(H, H_blk)
     if wide is None:
         wide = H_blk == 64  # measured: 656 TF wide vs 531 TF FullRow at the reference's shape
+    use_sm = wide and (sum_mfma is None or sum_mfma)
     if threads is None:
         threads = 64 * (H_blk // 16) * (2 if wide else 1)  # FullRow: 16 head rows per wave
     # wide: 8 waves per 64-head slice -- S = Q K^T on a 4x2 wave grid, P through LDS, O = P V
@@ -96,6 +100,11 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
             T.clear(Qt_frag)
             T.copy(Q[b, bx, h0:h0 + valid_h, 0:D], Q_frag[0:valid_h, :])
             T.copy(Q[b, bx, h0:h0 + valid_h, D:D + DT], Qt_frag[0:valid_h, :])
+            if use_sm:
+                ones_s = T.alloc_shared([block_I, 32], dtype)
+                acc_l = T.alloc_fragment([H_blk, 32], accum_dtype)
+                T.fill(ones_s, 1.0)
+                T.clear(acc_l)
             T.fill(acc_o, 0)
             T.fill(l_sum, 0)
             T.fill(m_cur, -(2.0**30))
@@ -134,9 +143,10 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
                         alpha[h] = 1.0
                 for h, r in T.Parallel(H_blk, block_I):
                     acc_s[h, r] = T.exp2(acc_s[h, r] * scale - m_cur[h] * scale)
-                T.reduce_sum(acc_s, r_sum, dim=1)
-                for h in T.Parallel(H_blk):
-                    l_sum[h] = l_sum[h] * alpha[h] + r_sum[h]
+                if not use_sm:
+                    T.reduce_sum(acc_s, r_sum, dim=1)
+                    for h in T.Parallel(H_blk):
+                        l_sum[h] = l_sum[h] * alpha[h] + r_sum[h]
                 if wide:
                     # O is partitioned over D, not over heads: alpha reaches its waves through LDS
                     T.copy(alpha, alpha_s)
@@ -146,14 +156,27 @@ def sparse_mla_fwd(batch, seq_len, seq_len_kv, heads, dim, tail_dim, topk, kv_gr
                     if any_s[i % 2] != 0:
                         for h, d in T.Parallel(H_blk, D):
                             acc_o[h, d] *= alpha_s[h]
+                        if use_sm:
+                            for h, j in T.Parallel(H_blk, 32):
+                                acc_l[h, j] *= alpha_s[h]
                     T.gemm(P_shared, KV_shared, acc_o)
+                    if use_sm:
+                        T.gemm(P_shared, ones_s, acc_l)
                 else:
                     if rescale != 0:  # per-thread flag: waves whose rows all kept their max skip it
                         for h, d in T.Parallel(H_blk, D):
                             acc_o[h, d] *= alpha[h]
                     T.copy(acc_s, acc_s_cast)
                     T.gemm(acc_s_cast, KV_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
-            if wide:
+            if use_sm:
+                for h, j in T.Parallel(H_blk, 32):  # every column of P x ones is the row sum
+                    if j == 0:
+                        alpha_s[h] = acc_l[h, j]
+                for h in T.Parallel(H_blk):
+                    l_sum[h] = alpha_s[h]
+                for h, d in T.Parallel(H_blk, D):
+                    o_cast[h, d] = acc_o[h, d] / alpha_s[h]
+            elif wide:
                 T.copy(l_sum, alpha_s)
                 for h, d in T.Parallel(H_blk, D):
                     o_cast[h, d] = acc_o[h, d] / alpha_s[h]
