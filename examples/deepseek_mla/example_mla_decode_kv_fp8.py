@@ -38,13 +38,15 @@ FP8_MAX = 448.0
 
 @tilelang.jit(out_idx=[7], pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True})
 def mla_decode_kv_fp8(batch, heads, seqlen_kv, dim, pe_dim, block_N=128, block_H=64, num_split=2, threads=512,
-                      num_stages=1, dtype="bfloat16", qk_fp8=True, pv_fp8=None):
+                      num_stages=1, dtype="bfloat16", qk_fp8=True, pv_fp8=None, sum_mfma=True):
     """``qk_fp8``: scores on the fp8 MFMA with Q quantised per head row (default); False keeps Q in
     ``dtype`` and runs both GEMMs on the widened tile (the reference's numerics).
     ``pv_fp8`` (default: with ``qk_fp8``): O += P V on the fp8 MFMA too -- P in e4m3 (the lazy
     rescale bounds it by 2^8, inside e4m3's range, so no scale is needed; 3 mantissa bits per
     probability), V read straight from the fp8 cache tile with ds_read_b64_tr_b8: no widened copy
-    of the tile, half the LDS bytes per PV operand."""
+    of the tile, half the LDS bytes per PV operand.
+    ``sum_mfma``: the softmax row sums are P x ones on the MFMA (P as P V consumes it: e4m3 with
+    ``pv_fp8``), rescaled with O, instead of a per-tile cross-wave reduction (example_mla_decode.py)."""
     if pv_fp8 is None:
         pv_fp8 = qk_fp8
     scale = (1.0 / (dim + pe_dim))**0.5 * 1.44269504  # softmax in base 2
@@ -94,6 +96,11 @@ def mla_decode_kv_fp8(batch, heads, seqlen_kv, dim, pe_dim, block_N=128, block_H
             else:
                 T.copy(Q[bx, by * VALID_BLOCK_H:(by + 1) * VALID_BLOCK_H, :], Q_local)
             T.copy(Q_pe[bx, by * VALID_BLOCK_H:(by + 1) * VALID_BLOCK_H, :], Q_pe_local)
+            if sum_mfma:
+                ones_s = T.alloc_shared([block_N, 32], FP8 if pv_fp8 else dtype)
+                acc_l = T.alloc_fragment([block_H, 32], accum_dtype)
+                T.fill(ones_s, 1.0)
+                T.clear(acc_l)
             T.fill(acc_o, 0)
             T.fill(logsum, 0)
             # lazy rescale: a row keeps its max until a score beats it by 2^8 (P <= 256); the O
@@ -134,18 +141,30 @@ def mla_decode_kv_fp8(batch, heads, seqlen_kv, dim, pe_dim, block_N=128, block_H
                         scores_scale[i] = 1.0
                 for i, j in T.Parallel(block_H, block_N):
                     acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
-                T.reduce_sum(acc_s, scores_sum, dim=1)
-                for i in T.Parallel(block_H):
-                    logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
+                if not sum_mfma:
+                    T.reduce_sum(acc_s, scores_sum, dim=1)
+                    for i in T.Parallel(block_H):
+                        logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
                 T.copy(scores_scale, sc_shared)
                 T.copy(acc_s, P_shared)
                 if any_s[k % 2] != 0:
                     for i, j in T.Parallel(block_H, dim):
                         acc_o[i, j] *= sc_shared[i]
+                    if sum_mfma:
+                        for i, j in T.Parallel(block_H, 32):
+                            acc_l[i, j] *= sc_shared[i]
                 if pv_fp8:
                     T.gemm(P_shared, KV8_shared, acc_o)  # e4m3 x e4m3, B [keys, dim]: transposed reads
                 else:
                     T.gemm(P_shared, V_shared, acc_o)
+                if sum_mfma:
+                    T.gemm(P_shared, ones_s, acc_l)
+            if sum_mfma:
+                for i, j in T.Parallel(block_H, 32):  # every column of P x ones is the row sum
+                    if j == 0:
+                        sc_shared[i] = acc_l[i, j]
+                for i in T.Parallel(block_H):
+                    logsum[i] = sc_shared[i]
             for i in T.Parallel(block_H):
                 sc_shared[i] = kv_scale / logsum[i]
             for i, j in T.Parallel(block_H, dim):

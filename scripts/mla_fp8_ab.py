@@ -62,10 +62,10 @@ def main():
     ref = ref8(q, qpe, kv8, s, kpe)
     for ns in (int(x) for x in a.splits.split(",")):
         for v in a.variants.split(","):
-            qk, pv, bn, st = v.split("_")
+            qk, pv, bn, st, *rest = v.split("_")  # optional 5th field "nosum": reduce_sum row sums
             try:
                 k = mla_decode_kv_fp8(B, H, S, D, P, block_N=int(bn), num_split=ns, num_stages=int(st),
-                                      qk_fp8=qk == "qk8", pv_fp8=pv == "pv8")
+                                      qk_fp8=qk == "qk8", pv_fp8=pv == "pv8", sum_mfma=rest != ["nosum"])
                 g, pp = torch.empty(B, H, ns, device="cuda"), torch.empty(B, H, ns, D, device="cuda")
                 o = k(q, qpe, kv8, kpe, s, g, pp)
                 err = ((o.float() - ref).norm() / ref.norm()).item()
