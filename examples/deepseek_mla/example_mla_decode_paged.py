@@ -21,9 +21,11 @@ FAST_MATH = {tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True}
 
 @tilelang.jit(out_idx=[8], pass_configs=FAST_MATH)
 def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe_dim=64, block_N=64, block_H=64,
-                     num_split=4, threads=None, num_stages=2, dtype="bfloat16", wide=None):
+                     num_split=4, threads=None, num_stages=2, dtype="bfloat16", wide=None, sum_mfma=None):
+    """``sum_mfma`` (default with ``wide``): row sums as P x ones on the MFMA (example_mla_decode.py)."""
     if wide is None:
         wide = block_H == 64  # 8 waves, O split over the latent columns (example_mla_decode.py)
+    use_sm = wide and (sum_mfma is None or sum_mfma)
     if threads is None:
         threads = 512 if wide else 256
     s_policy = T.GemmWarpPolicy.Square if wide else T.GemmWarpPolicy.FullRow
@@ -64,6 +66,11 @@ def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe
             t_end = T.min(t_begin + per_split, n_tiles)
             T.copy(Q[bx, by * VALID_H:(by + 1) * VALID_H, :], Q_local)
             T.copy(Q_pe[bx, by * VALID_H:(by + 1) * VALID_H, :], Q_pe_local)
+            if use_sm:
+                ones_s = T.alloc_shared([block_N, 32], dtype)
+                acc_l = T.alloc_fragment([block_H, 32], accum_dtype)
+                T.fill(ones_s, 1.0)
+                T.clear(acc_l)
             T.fill(acc_o, 0)
             T.fill(l_sum, 0)
             T.fill(m, -(2.0**30))
@@ -100,22 +107,36 @@ def mla_decode_paged(batch, heads, max_seqlen, num_pages, page_size, dim=512, pe
                         alpha[i] = T.exp2((m_prev[i] - m[i]) * scale)
                 for i, j in T.Parallel(block_H, block_N):
                     acc_s[i, j] = T.exp2(acc_s[i, j] * scale - m[i] * scale)
-                T.reduce_sum(acc_s, r_sum, dim=1)
-                for i in T.Parallel(block_H):
-                    l_sum[i] = l_sum[i] * alpha[i] + r_sum[i]
+                if not use_sm:
+                    T.reduce_sum(acc_s, r_sum, dim=1)
+                    for i in T.Parallel(block_H):
+                        l_sum[i] = l_sum[i] * alpha[i] + r_sum[i]
                 if wide:
                     T.copy(alpha, sc_shared)
                     T.copy(acc_s, P_shared)
                     if any_s[t % 2] != 0:
                         for i, j in T.Parallel(block_H, dim):
                             acc_o[i, j] *= sc_shared[i]
+                        if use_sm:
+                            for i, j in T.Parallel(block_H, 32):
+                                acc_l[i, j] *= sc_shared[i]
                     T.gemm(P_shared, KV_shared, acc_o)
+                    if use_sm:
+                        T.gemm(P_shared, ones_s, acc_l)
                 else:
                     T.copy(acc_s, acc_s_cast)
                     for i, j in T.Parallel(block_H, dim):
                         acc_o[i, j] *= alpha[i]
                     T.gemm(acc_s_cast, KV_shared, acc_o, policy=T.GemmWarpPolicy.FullRow)
-            if wide:
+            if use_sm:
+                for i, j in T.Parallel(block_H, 32):  # every column of P x ones is the row sum
+                    if j == 0:
+                        sc_shared[i] = acc_l[i, j]
+                for i in T.Parallel(block_H):
+                    l_sum[i] = sc_shared[i]
+                for i, j in T.Parallel(block_H, dim):
+                    acc_o[i, j] /= T.max(sc_shared[i], 1e-30)
+            elif wide:
                 T.copy(l_sum, sc_shared)
                 for i, j in T.Parallel(block_H, dim):
                     acc_o[i, j] /= T.max(sc_shared[i], 1e-30)

@@ -18,7 +18,8 @@ from example_mla_decode import ref_program, flops
 
 @tilelang.jit(out_idx=[6], pass_configs={tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True})
 def mla_decode_persistent(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, block_N=64, block_H=64, num_split=4,
-                          num_cu=256, threads=512, num_stages=2, dtype="float16"):
+                          num_cu=256, threads=512, num_stages=2, dtype="float16", sum_mfma=True):
+    """``sum_mfma``: row sums as P x ones on the MFMA (example_mla_decode.py)."""
     scale = (1.0 / (dim + pe_dim))**0.5 * 1.44269504
     accum_dtype = "float"
     assert kv_head_num == 1, "MLA decode expects one latent KV head"
@@ -51,6 +52,10 @@ def mla_decode_persistent(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, blo
             sc_shared = T.alloc_shared([block_H], accum_dtype)
             any_s = T.alloc_shared([2], "int32")
             acc_o = T.alloc_fragment([block_H, dim], accum_dtype)
+            if sum_mfma:
+                ones_s = T.alloc_shared([block_N, 32], dtype)
+                acc_l = T.alloc_fragment([block_H, 32], accum_dtype)
+                T.fill(ones_s, 1.0)
             scores_max = T.alloc_fragment([block_H], accum_dtype)
             scores_max_prev = T.alloc_fragment([block_H], accum_dtype)
             scores_scale = T.alloc_fragment([block_H], accum_dtype)
@@ -72,6 +77,8 @@ def mla_decode_persistent(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, blo
                     T.copy(Q_pe[bid, hid * VALID_BLOCK_H:(hid + 1) * VALID_BLOCK_H, :], Q_pe_local)
                     T.fill(acc_o, 0)
                     T.fill(logsum, 0)
+                    if sum_mfma:
+                        T.clear(acc_l)
                     T.fill(scores_max, -(2.0**30))  # lazy rescale (example_mla_decode.py)
                     # lazy-rescale flag, double-buffered by iteration parity: iteration t resets the slot
                     # of t + 1 (ordered by the stage barrier against t - 1's readers and t + 1's setters)
@@ -97,15 +104,27 @@ def mla_decode_persistent(batch, heads, kv_head_num, seqlen_kv, dim, pe_dim, blo
                                 scores_scale[i] = 1.0
                         for i, j in T.Parallel(block_H, block_N):
                             acc_s[i, j] = T.exp2(acc_s[i, j] * scale - scores_max[i] * scale)
-                        T.reduce_sum(acc_s, scores_sum, dim=1)
-                        for i in T.Parallel(block_H):
-                            logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
+                        if not sum_mfma:
+                            T.reduce_sum(acc_s, scores_sum, dim=1)
+                            for i in T.Parallel(block_H):
+                                logsum[i] = logsum[i] * scores_scale[i] + scores_sum[i]
                         T.copy(scores_scale, sc_shared)
                         T.copy(acc_s, P_shared)
                         if any_s[k % 2] != 0:
                             for i, j in T.Parallel(block_H, dim):
                                 acc_o[i, j] *= sc_shared[i]
+                            if sum_mfma:
+                                for i, j in T.Parallel(block_H, 32):
+                                    acc_l[i, j] *= sc_shared[i]
                         T.gemm(P_shared, KV_shared, acc_o)
+                        if sum_mfma:
+                            T.gemm(P_shared, ones_s, acc_l)
+                    if sum_mfma:
+                        for i, j in T.Parallel(block_H, 32):  # every column of P x ones is the row sum
+                            if j == 0:
+                                sc_shared[i] = acc_l[i, j]
+                        for i in T.Parallel(block_H):
+                            logsum[i] = sc_shared[i]
                     T.copy(logsum, sc_shared)
                     for i, j in T.Parallel(block_H, dim):
                         acc_o[i, j] /= sc_shared[i]
