@@ -5,8 +5,8 @@ Each head keeps a few *slash* lines (key = query - s) and *vertical* lines (key 
 causal attention matrix.  Per query block of ``block_M`` rows the pattern becomes
   * ``block_offset``: the ``block_N``-aligned key blocks any slash line crosses (dense tiles),
   * ``column_index``: the vertical columns not already inside those blocks (gathered rows),
-computed on the device with vectorised PyTorch ops (``convert_vertical_slash_indexes``; the
-reference ships a CUDA extension for this).  The attention kernel (one workgroup per query
+computed on the device by a tilelang kernel (``vs_convert``: LDS bitmap + prefix-sum compaction,
+no host synchronisation; the reference ships a CUDA extension for this).  The attention kernel (one workgroup per query
 block, head, batch) runs the online softmax over the dense key blocks (K/V tiles at data-dependent
 offsets through the LDS-DMA ring) and then over the column chunks (``T.gather_rows``: per-lane row
 addresses, LDS-DMA), causal-masked in both phases.
@@ -23,9 +23,81 @@ LOG2E = 1.44269504
 FAST_MATH = {tilelang.PassConfigKey.TL_ENABLE_FAST_MATH: True}
 
 
+@tilelang.jit(out_idx=[2, 3, 4, 5])
+def vs_convert(batch, heads, seq_len, nv, ns, block_M=64, block_N=64, threads=256):
+    """The index conversion on the device (the reference ships a CUDA extension for it), one
+    workgroup per (query block, head, batch): the key blocks any slash line crosses are marked in an
+    LDS bitmap and compacted in ascending order by a prefix sum; the vertical columns outside those
+    blocks (and not past the block's last query) are compacted in input order the same way.  Output
+    shapes are the static bounds (a 64-row segment of a slash crosses at most
+    ceil((block_M - 1) / block_N) + 1 key blocks), so there is no host synchronisation."""
+    NQ = (seq_len + block_M - 1) // block_M
+    NK = (seq_len + block_N - 1) // block_N
+    span = (block_M - 1) // block_N + 2
+    MAXB = max(1, min(NK, span * ns))
+    MAXC = max(block_N, (nv + block_N - 1) // block_N * block_N)
+
+    @T.prim_func
+    def main(Vidx: T.Tensor([batch, heads, nv], "int32"), Sidx: T.Tensor([batch, heads, ns], "int32"),
+             BlockCount: T.Tensor([batch, heads, NQ], "int32"), BlockOffset: T.Tensor([batch, heads, NQ, MAXB], "int32"),
+             ColumnCount: T.Tensor([batch, heads, NQ], "int32"),
+             ColumnIndex: T.Tensor([batch, heads, NQ, MAXC], "int32")):
+        with T.Kernel(NQ, heads, batch, threads=threads) as (bx, by, bz):
+            cover = T.alloc_shared([NK], "int32")
+            csum = T.alloc_shared([NK], "int32")
+            vflag = T.alloc_shared([MAXC], "int32")
+            vpos = T.alloc_shared([MAXC], "int32")
+            m0 = bx * block_M
+            m1 = T.min(m0 + block_M - 1, seq_len - 1)
+            for j in T.Parallel(NK):
+                cover[j] = 0
+            for t in T.Parallel(ns):
+                sv = Sidx[bz, by, t]
+                lo = T.max(m0 - sv, 0)
+                hi = T.min(m0 + block_M - 1 - sv, m1)
+                for d in T.serial(span):
+                    if (hi >= lo) & (lo // block_N + d <= hi // block_N):
+                        cover[lo // block_N + d] = 1
+            for j in T.Parallel(NK):
+                csum[j] = cover[j]
+            T.cumsum(csum, dim=0)
+            for j in T.Parallel(NK):
+                if cover[j] != 0:
+                    BlockOffset[bz, by, bx, csum[j] - 1] = j * block_N
+            for i in T.Parallel(MAXB):
+                if i >= csum[NK - 1]:
+                    BlockOffset[bz, by, bx, i] = -1
+            for t in T.Parallel(MAXC):
+                vv = T.if_then_else(t < nv, Vidx[bz, by, T.min(t, nv - 1)], -1)
+                ok = (vv >= 0) & (vv <= m1)
+                vflag[t] = T.if_then_else(ok, 1 - cover[T.max(T.min(vv, seq_len - 1), 0) // block_N], 0)
+                vpos[t] = vflag[t]
+            T.cumsum(vpos, dim=0)
+            for t in T.Parallel(MAXC):
+                if vflag[t] != 0:
+                    ColumnIndex[bz, by, bx, vpos[t] - 1] = Vidx[bz, by, T.min(t, nv - 1)]
+            for i in T.Parallel(MAXC):
+                if i >= vpos[MAXC - 1]:
+                    ColumnIndex[bz, by, bx, i] = -1
+            for z in T.Parallel(1):
+                BlockCount[bz, by, bx] = csum[NK - 1] + z
+                ColumnCount[bz, by, bx] = vpos[MAXC - 1] + z
+
+    return main
+
+
 def convert_vertical_slash_indexes(v_idx, s_idx, seq_len, block_M=64, block_N=64):
-    """v_idx [B, H, NV], s_idx [B, H, NS] -> (block_count [B,H,NQ], block_offset [B,H,NQ,MAXB],
-    column_count [B,H,NQ], column_index [B,H,NQ,MAXC]) int32; unused slots are -1."""
+    """(block_count, block_offset, column_count, column_index) int32 from the device kernel
+    ``vs_convert`` (block offsets ascending, columns in input order, unused slots -1)."""
+    B, H, NV = v_idx.shape
+    k = vs_convert(B, H, seq_len, NV, s_idx.shape[-1], block_M, block_N)
+    return k(v_idx.int().contiguous(), s_idx.int().contiguous())
+
+
+def convert_vertical_slash_indexes_torch(v_idx, s_idx, seq_len, block_M=64, block_N=64):
+    """Vectorised-PyTorch form of the conversion (the test's reference): v_idx [B, H, NV], s_idx
+    [B, H, NS] -> (block_count [B,H,NQ], block_offset [B,H,NQ,MAXB], column_count [B,H,NQ],
+    column_index [B,H,NQ,MAXC]) int32; unused slots are -1, columns sorted."""
     import torch
     dev = v_idx.device
     B, H, _ = v_idx.shape
@@ -142,12 +214,12 @@ def vs_sparse_flashattn(batch, heads, seq_len, dim, max_blocks, max_cols, block_
     return main
 
 
-def vertical_slash_sparse_attention(q, k, v, v_idx, s_idx, block_M=64, block_N=64):
+def vertical_slash_sparse_attention(q, k, v, v_idx, s_idx, block_M=64, block_N=64, threads=256, num_stages=2):
     """q/k/v [B, H, S, D]; v_idx [B, H, NV]; s_idx [B, H, NS] -> output [B, H, S, D]."""
     B, H, S, D = q.shape
     bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, S, block_M, block_N)
-    k_ = vs_sparse_flashattn(B, H, S, D, bo.shape[-1], ci.shape[-1], block_M, block_N,
-                             dtype=str(q.dtype).replace("torch.", ""))
+    k_ = vs_sparse_flashattn(B, H, S, D, bo.shape[-1], ci.shape[-1], block_M, block_N, threads=threads,
+                             num_stages=num_stages, dtype=str(q.dtype).replace("torch.", ""))
     return k_(q, k, v, bc, bo, cc, ci)
 
 

@@ -31,6 +31,32 @@ def test_vertical_slash_cpu():
     torch.testing.assert_close(o.float(), ref_program(q, k, v, v_idx, s_idx, 64, 32), rtol=2e-2, atol=2e-2)
 
 
+def _check_convert(device):
+    from example_vertical_slash_sparse_attn import convert_vertical_slash_indexes, convert_vertical_slash_indexes_torch
+    for S, nv, slashes, bm, bn in ((512, 40, [[0, 300], [0, 100]], 64, 32), (1024, 100, [[0, 7, 300], [0, 64, 513]], 64, 64)):
+        _, _, _, v_idx, s_idx = _vs_inputs(1, 2, S, device, nv, slashes)
+        bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, S, bm, bn)
+        rbc, rbo, rcc, rci = convert_vertical_slash_indexes_torch(v_idx, s_idx, S, bm, bn)
+        assert torch.equal(bc.cpu(), rbc.cpu()) and torch.equal(cc.cpu(), rcc.cpu())
+        for h in range(2):
+            for qb in range(bc.shape[2]):
+                n, c = int(bc[0, h, qb]), int(cc[0, h, qb])
+                assert bo[0, h, qb, :n].tolist() == rbo[0, h, qb, :n].tolist()  # ascending in both
+                assert sorted(ci[0, h, qb, :c].tolist()) == rci[0, h, qb, :c].tolist()  # input order vs sorted
+                assert (bo[0, h, qb, n:] == -1).all() and (ci[0, h, qb, c:] == -1).all()
+
+
+def test_vertical_slash_convert_cpu():
+    """The device index conversion (vs_convert) selects exactly the blocks / columns of the
+    vectorised-PyTorch form."""
+    _check_convert("cpu")
+
+
+@pytest.mark.gpu
+def test_vertical_slash_convert_gpu():
+    _check_convert("cuda")
+
+
 @pytest.mark.gpu
 def test_vertical_slash_gpu():
     from example_vertical_slash_sparse_attn import ref_program, vertical_slash_sparse_attention
