@@ -39,7 +39,8 @@ def vs_convert(batch, heads, seq_len, nv, ns, block_M=64, block_N=64, threads=25
 
     @T.prim_func
     def main(Vidx: T.Tensor([batch, heads, nv], "int32"), Sidx: T.Tensor([batch, heads, ns], "int32"),
-             BlockCount: T.Tensor([batch, heads, NQ], "int32"), BlockOffset: T.Tensor([batch, heads, NQ, MAXB], "int32"),
+             BlockCount: T.Tensor([batch, heads, NQ], "int32"),
+             BlockOffset: T.Tensor([batch, heads, NQ, MAXB], "int32"),
              ColumnCount: T.Tensor([batch, heads, NQ], "int32"),
              ColumnIndex: T.Tensor([batch, heads, NQ, MAXC], "int32")):
         with T.Kernel(NQ, heads, batch, threads=threads) as (bx, by, bz):
@@ -130,9 +131,13 @@ def convert_vertical_slash_indexes_torch(v_idx, s_idx, seq_len, block_M=64, bloc
     return block_count.contiguous(), block_offset.contiguous(), column_count.contiguous(), column_index.contiguous()
 
 
-@tilelang.jit(out_idx=[7], pass_configs=FAST_MATH)
+@tilelang.jit(out_idx=[-1], pass_configs=FAST_MATH)
 def vs_sparse_flashattn(batch, heads, seq_len, dim, max_blocks, max_cols, block_M=64, block_N=64, threads=256,
-                        num_stages=2, dtype="float16"):
+                        num_stages=2, dtype="float16", num_split=1):
+    """``num_split`` > 1: each query block's key work (dense blocks, then column chunks) is divided
+    over ``num_split`` workgroups, which write fp32 partial outputs and base-2 LSEs; a second kernel
+    of the program combines them (short / lightly populated sequences at B1 H1 otherwise leave most
+    CUs idle: 64 workgroups at 8K)."""
     scale = dim**-0.5 * LOG2E
     NQ = (seq_len + block_M - 1) // block_M
     NC = max_cols // block_N
@@ -163,64 +168,133 @@ def vs_sparse_flashattn(batch, heads, seq_len, dim, max_blocks, max_cols, block_
         T.copy(acc_s, acc_s_cast)
         T.gemm(acc_s_cast, V_s, acc_o, policy=T.GemmWarpPolicy.FullRow)
 
-    @T.prim_func
-    def main(Q: T.Tensor([batch, heads, seq_len, dim], dtype), K: T.Tensor([batch, heads, seq_len, dim], dtype),
-             V: T.Tensor([batch, heads, seq_len, dim], dtype), BlockCount: T.Tensor([batch, heads, NQ], "int32"),
-             BlockOffset: T.Tensor([batch, heads, NQ, max_blocks], "int32"),
-             ColumnCount: T.Tensor([batch, heads, NQ], "int32"),
-             ColumnIndex: T.Tensor([batch, heads, NQ, max_cols], "int32"),
-             Output: T.Tensor([batch, heads, seq_len, dim], dtype)):
-        with T.Kernel(NQ, heads, batch, threads=threads) as (bx, by, bz):
-            Q_s = T.alloc_shared([block_M, dim], dtype)
-            K_s = T.alloc_shared([block_N, dim], dtype)
-            V_s = T.alloc_shared([block_N, dim], dtype)
-            cidx = T.alloc_shared([block_N], "int32")
-            acc_s = T.alloc_fragment([block_M, block_N], accum)
-            acc_s_cast = T.alloc_fragment([block_M, block_N], dtype)
-            acc_o = T.alloc_fragment([block_M, dim], accum)
-            m = T.alloc_fragment([block_M], accum)
-            m_prev = T.alloc_fragment([block_M], accum)
-            alpha = T.alloc_fragment([block_M], accum)
-            l_sum = T.alloc_fragment([block_M], accum)
-            r_sum = T.alloc_fragment([block_M], accum)
-            T.copy(Q[bz, by, bx * block_M:(bx + 1) * block_M, :], Q_s)
-            T.fill(acc_o, 0)
-            T.fill(l_sum, 0)
-            T.fill(m, -(2.0**30))
-            nb = BlockCount[bz, by, bx]
-            for i in T.Pipelined(nb, num_stages=num_stages):
-                k0 = T.max(BlockOffset[bz, by, bx, i], 0)
-                T.copy(K[bz, by, k0:k0 + block_N, :], K_s)
-                T.copy(V[bz, by, k0:k0 + block_N, :], V_s)
-                for r, c in T.Parallel(block_M, block_N):
-                    acc_s[r, c] = T.if_then_else((k0 + c <= bx * block_M + r) & (k0 + c < seq_len), 0,
-                                                 -T.infinity(accum))
-                T.gemm(Q_s, K_s, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                softmax_step(acc_s, acc_s_cast, acc_o, m, m_prev, alpha, l_sum, r_sum, V_s)
-            nc = T.ceildiv(ColumnCount[bz, by, bx], block_N)
-            for j in T.Pipelined(nc, num_stages=num_stages):
-                T.gather_rows(K[bz, by, :, :], ColumnIndex[bz, by, bx, j * block_N:(j + 1) * block_N], K_s)
-                T.gather_rows(V[bz, by, :, :], ColumnIndex[bz, by, bx, j * block_N:(j + 1) * block_N], V_s)
-                T.copy(ColumnIndex[bz, by, bx, j * block_N:(j + 1) * block_N], cidx)
-                for r, c in T.Parallel(block_M, block_N):
-                    acc_s[r, c] = T.if_then_else((cidx[c] >= 0) & (cidx[c] <= bx * block_M + r), 0,
-                                                 -T.infinity(accum))
-                T.gemm(Q_s, K_s, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                softmax_step(acc_s, acc_s_cast, acc_o, m, m_prev, alpha, l_sum, r_sum, V_s)
-            for i, d in T.Parallel(block_M, dim):
-                acc_o[i, d] /= T.max(l_sum[i], 1e-30)
-            T.copy(acc_o, Output[bz, by, bx * block_M:(bx + 1) * block_M, :])
+    P = num_split
+
+    @T.macro
+    def attend(Q, K, V, BlockCount, BlockOffset, ColumnCount, ColumnIndex, bx, by, bz, sp, acc_o, m, l_sum):
+        Q_s = T.alloc_shared([block_M, dim], dtype)
+        K_s = T.alloc_shared([block_N, dim], dtype)
+        V_s = T.alloc_shared([block_N, dim], dtype)
+        cidx = T.alloc_shared([block_N], "int32")
+        acc_s = T.alloc_fragment([block_M, block_N], accum)
+        acc_s_cast = T.alloc_fragment([block_M, block_N], dtype)
+        m_prev = T.alloc_fragment([block_M], accum)
+        alpha = T.alloc_fragment([block_M], accum)
+        r_sum = T.alloc_fragment([block_M], accum)
+        T.copy(Q[bz, by, bx * block_M:(bx + 1) * block_M, :], Q_s)
+        T.fill(acc_o, 0)
+        T.fill(l_sum, 0)
+        T.fill(m, -(2.0**30))
+        nb_all = BlockCount[bz, by, bx]
+        nb0 = nb_all * sp // P
+        nb1 = nb_all * (sp + 1) // P
+        for i in T.Pipelined(nb1 - nb0, num_stages=num_stages):
+            k0 = T.max(BlockOffset[bz, by, bx, nb0 + i], 0)
+            T.copy(K[bz, by, k0:k0 + block_N, :], K_s)
+            T.copy(V[bz, by, k0:k0 + block_N, :], V_s)
+            for r, c in T.Parallel(block_M, block_N):
+                acc_s[r, c] = T.if_then_else((k0 + c <= bx * block_M + r) & (k0 + c < seq_len), 0,
+                                             -T.infinity(accum))
+            T.gemm(Q_s, K_s, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+            softmax_step(acc_s, acc_s_cast, acc_o, m, m_prev, alpha, l_sum, r_sum, V_s)
+        nc_all = T.ceildiv(ColumnCount[bz, by, bx], block_N)
+        nc0 = nc_all * sp // P
+        nc1 = nc_all * (sp + 1) // P
+        for j in T.Pipelined(nc1 - nc0, num_stages=num_stages):
+            T.gather_rows(K[bz, by, :, :], ColumnIndex[bz, by, bx, (nc0 + j) * block_N:(nc0 + j + 1) * block_N], K_s)
+            T.gather_rows(V[bz, by, :, :], ColumnIndex[bz, by, bx, (nc0 + j) * block_N:(nc0 + j + 1) * block_N], V_s)
+            T.copy(ColumnIndex[bz, by, bx, (nc0 + j) * block_N:(nc0 + j + 1) * block_N], cidx)
+            for r, c in T.Parallel(block_M, block_N):
+                acc_s[r, c] = T.if_then_else((cidx[c] >= 0) & (cidx[c] <= bx * block_M + r), 0,
+                                             -T.infinity(accum))
+            T.gemm(Q_s, K_s, acc_s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
+            softmax_step(acc_s, acc_s_cast, acc_o, m, m_prev, alpha, l_sum, r_sum, V_s)
+
+    if P == 1:
+
+        @T.prim_func
+        def main(Q: T.Tensor([batch, heads, seq_len, dim], dtype), K: T.Tensor([batch, heads, seq_len, dim], dtype),
+                 V: T.Tensor([batch, heads, seq_len, dim], dtype), BlockCount: T.Tensor([batch, heads, NQ], "int32"),
+                 BlockOffset: T.Tensor([batch, heads, NQ, max_blocks], "int32"),
+                 ColumnCount: T.Tensor([batch, heads, NQ], "int32"),
+                 ColumnIndex: T.Tensor([batch, heads, NQ, max_cols], "int32"),
+                 Output: T.Tensor([batch, heads, seq_len, dim], dtype)):
+            with T.Kernel(NQ, heads, batch, threads=threads) as (bx, by, bz):
+                acc_o = T.alloc_fragment([block_M, dim], accum)
+                m = T.alloc_fragment([block_M], accum)
+                l_sum = T.alloc_fragment([block_M], accum)
+                attend(Q, K, V, BlockCount, BlockOffset, ColumnCount, ColumnIndex, bx, by, bz, 0, acc_o, m, l_sum)
+                for i, d in T.Parallel(block_M, dim):
+                    acc_o[i, d] /= T.max(l_sum[i], 1e-30)
+                T.copy(acc_o, Output[bz, by, bx * block_M:(bx + 1) * block_M, :])
+    else:
+
+        @T.prim_func
+        def main(Q: T.Tensor([batch, heads, seq_len, dim], dtype), K: T.Tensor([batch, heads, seq_len, dim], dtype),
+                 V: T.Tensor([batch, heads, seq_len, dim], dtype), BlockCount: T.Tensor([batch, heads, NQ], "int32"),
+                 BlockOffset: T.Tensor([batch, heads, NQ, max_blocks], "int32"),
+                 ColumnCount: T.Tensor([batch, heads, NQ], "int32"),
+                 ColumnIndex: T.Tensor([batch, heads, NQ, max_cols], "int32"),
+                 Opart: T.Tensor([batch, heads, P, seq_len, dim], accum),
+                 Lse: T.Tensor([batch, heads, P, seq_len], accum),
+                 Output: T.Tensor([batch, heads, seq_len, dim], dtype)):
+            with T.Kernel(NQ, heads, batch * P, threads=threads) as (bx, by, bzp):
+                bz = bzp // P
+                sp = bzp % P
+                acc_o = T.alloc_fragment([block_M, dim], accum)
+                m = T.alloc_fragment([block_M], accum)
+                l_sum = T.alloc_fragment([block_M], accum)
+                attend(Q, K, V, BlockCount, BlockOffset, ColumnCount, ColumnIndex, bx, by, bz, sp, acc_o, m, l_sum)
+                for i, d in T.Parallel(block_M, dim):
+                    acc_o[i, d] /= T.max(l_sum[i], 1e-30)
+                for i in T.Parallel(block_M):  # base-2 LSE; an empty split gets -inf weight
+                    l_sum[i] = T.if_then_else(l_sum[i] > 0, T.log2(l_sum[i]) + m[i] * scale, -T.infinity(accum))
+                T.copy(acc_o, Opart[bz, by, sp, bx * block_M:(bx + 1) * block_M, :])
+                T.copy(l_sum, Lse[bz, by, sp, bx * block_M:(bx + 1) * block_M])
+            with T.Kernel(T.ceildiv(seq_len, 64), heads, batch, threads=256) as (rx, hy, bz):
+                for r, d in T.Parallel(64, dim):
+                    row = rx * 64 + r
+                    if row < seq_len:
+                        mx = T.alloc_var(accum)
+                        mx = -T.infinity(accum)
+                        for q in T.serial(P):
+                            mx = T.max(mx, Lse[bz, hy, q, row])
+                        num = T.alloc_var(accum)
+                        den = T.alloc_var(accum)
+                        num = 0.0
+                        den = 0.0
+                        for q in T.serial(P):
+                            w = T.exp2(Lse[bz, hy, q, row] - mx)
+                            num = num + w * Opart[bz, hy, q, row, d]
+                            den = den + w
+                        Output[bz, hy, row, d] = T.Cast(dtype, num / T.max(den, 1e-30))
 
     return main
 
 
-def vertical_slash_sparse_attention(q, k, v, v_idx, s_idx, block_M=64, block_N=64, threads=256, num_stages=2):
-    """q/k/v [B, H, S, D]; v_idx [B, H, NV]; s_idx [B, H, NS] -> output [B, H, S, D]."""
+def vertical_slash_sparse_attention(q, k, v, v_idx, s_idx, block_M=128, block_N=None, threads=512, num_stages=2,
+                                    num_split=None):
+    """q/k/v [B, H, S, D]; v_idx [B, H, NV]; s_idx [B, H, NS] -> output [B, H, S, D].
+    Tiles from scripts/minference_sweep.py at the reference's B1 H1 D64 (profiles/r6/minference_sweep*.log):
+    128-row query blocks over 8 waves; 128-key blocks up to 32K keys (fewer, fuller pipeline steps:
+    8K 0.279 -> 0.167 ms against the 64x64 / 4-wave tile), 64-key blocks beyond (finer slash coverage:
+    64K 2.00 -> 1.40 ms).  ``num_split`` (default: enough splits for ~512 workgroups, at most 8) divides
+    each query block's key work over several workgroups (combined by LSE)."""
+    import torch
     B, H, S, D = q.shape
+    if block_N is None:
+        block_N = 128 if S <= 32768 else 64
+    NQ = (S + block_M - 1) // block_M
+    if num_split is None:
+        num_split = max(1, min(8, 512 // max(1, NQ * H * B)))
     bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, S, block_M, block_N)
     k_ = vs_sparse_flashattn(B, H, S, D, bo.shape[-1], ci.shape[-1], block_M, block_N, threads=threads,
-                             num_stages=num_stages, dtype=str(q.dtype).replace("torch.", ""))
-    return k_(q, k, v, bc, bo, cc, ci)
+                             num_stages=num_stages, dtype=str(q.dtype).replace("torch.", ""), num_split=num_split)
+    if num_split == 1:
+        return k_(q, k, v, bc, bo, cc, ci)
+    opart = torch.empty(B, H, num_split, S, D, device=q.device, dtype=torch.float32)
+    lse = torch.empty(B, H, num_split, S, device=q.device, dtype=torch.float32)
+    return k_(q, k, v, bc, bo, cc, ci, opart, lse)
 
 
 def ref_program(q, k, v, v_idx, s_idx, block_M=64, block_N=64):

@@ -20,20 +20,25 @@ def _vs_inputs(B, H, S, device, nv, slashes):
     return q, k, v, v_idx, s_idx
 
 
-def test_vertical_slash_cpu():
+@pytest.mark.parametrize("num_split", [1, 3])
+def test_vertical_slash_cpu(num_split):
+    """num_split 3: each query block's key work over three workgroups + the LSE combine (some
+    splits of the short blocks are empty: weight 0)."""
     from example_vertical_slash_sparse_attn import ref_program, vs_sparse_flashattn, convert_vertical_slash_indexes
     q, k, v, v_idx, s_idx = _vs_inputs(1, 2, 512, "cpu", 40, [[0, 300], [0, 100]])
     bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, 512, 64, 32)
     assert int(cc.sum()) > 0 and int(bc.sum()) > 0  # both phases exercised
-    f = vs_sparse_flashattn.get_tir(1, 2, 512, 64, bo.shape[-1], ci.shape[-1], 64, 32, 128)
-    kern = tilelang.compile(f, out_idx=[7], target="cpu", pass_configs={"tl.enable_fast_math": True})
-    o = kern(q, k, v, bc, bo, cc, ci)
+    f = vs_sparse_flashattn.get_tir(1, 2, 512, 64, bo.shape[-1], ci.shape[-1], 64, 32, 128, num_split=num_split)
+    kern = tilelang.compile(f, out_idx=[-1], target="cpu", pass_configs={"tl.enable_fast_math": True})
+    extra = () if num_split == 1 else (torch.empty(1, 2, num_split, 512, 64), torch.empty(1, 2, num_split, 512))
+    o = kern(q, k, v, bc, bo, cc, ci, *extra)
     torch.testing.assert_close(o.float(), ref_program(q, k, v, v_idx, s_idx, 64, 32), rtol=2e-2, atol=2e-2)
 
 
 def _check_convert(device):
     from example_vertical_slash_sparse_attn import convert_vertical_slash_indexes, convert_vertical_slash_indexes_torch
-    for S, nv, slashes, bm, bn in ((512, 40, [[0, 300], [0, 100]], 64, 32), (1024, 100, [[0, 7, 300], [0, 64, 513]], 64, 64)):
+    cases = ((512, 40, [[0, 300], [0, 100]], 64, 32), (1024, 100, [[0, 7, 300], [0, 64, 513]], 64, 64))
+    for S, nv, slashes, bm, bn in cases:
         _, _, _, v_idx, s_idx = _vs_inputs(1, 2, S, device, nv, slashes)
         bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, S, bm, bn)
         rbc, rbo, rcc, rci = convert_vertical_slash_indexes_torch(v_idx, s_idx, S, bm, bn)
@@ -61,8 +66,9 @@ def test_vertical_slash_convert_gpu():
 def test_vertical_slash_gpu():
     from example_vertical_slash_sparse_attn import ref_program, vertical_slash_sparse_attention
     q, k, v, v_idx, s_idx = _vs_inputs(2, 2, 1024, "cuda", 100, [[0, 7, 300], [0, 64, 513]])
-    o = vertical_slash_sparse_attention(q, k, v, v_idx, s_idx)
-    torch.testing.assert_close(o.float(), ref_program(q, k, v, v_idx, s_idx), rtol=2e-2, atol=2e-2)
+    for bm, bn, th, ns in ((64, 64, 256, 1), (128, 128, 512, None), (128, 64, 512, 1), (128, 64, 512, 4)):
+        o = vertical_slash_sparse_attention(q, k, v, v_idx, s_idx, bm, bn, th, num_split=ns)
+        torch.testing.assert_close(o.float(), ref_program(q, k, v, v_idx, s_idx, bm, bn), rtol=2e-2, atol=2e-2)
 
 
 @pytest.mark.parametrize("variant", ["varlen_indice", "varlen_mask", "paged"])
