@@ -40,7 +40,7 @@ def _check_convert(device):
     cases = ((512, 40, [[0, 300], [0, 100]], 64, 32), (1024, 100, [[0, 7, 300], [0, 64, 513]], 64, 64))
     for S, nv, slashes, bm, bn in cases:
         _, _, _, v_idx, s_idx = _vs_inputs(1, 2, S, device, nv, slashes)
-        bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, S, bm, bn)
+        bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, S, bm, bn, merged=False)
         rbc, rbo, rcc, rci = convert_vertical_slash_indexes_torch(v_idx, s_idx, S, bm, bn)
         assert torch.equal(bc.cpu(), rbc.cpu()) and torch.equal(cc.cpu(), rcc.cpu())
         for h in range(2):
@@ -49,6 +49,31 @@ def _check_convert(device):
                 assert bo[0, h, qb, :n].tolist() == rbo[0, h, qb, :n].tolist()  # ascending in both
                 assert sorted(ci[0, h, qb, :c].tolist()) == rci[0, h, qb, :c].tolist()  # input order vs sorted
                 assert (bo[0, h, qb, n:] == -1).all() and (ci[0, h, qb, c:] == -1).all()
+
+
+def _check_convert_merged(device):
+    from example_vertical_slash_sparse_attn import convert_vertical_slash_indexes, convert_vertical_slash_merged_py
+    g = torch.Generator().manual_seed(3)
+    for S, nv, ns, bm, bn in ((512, 40, 6, 64, 32), (2048, 200, 60, 128, 64), (1000, 50, 9, 128, 128)):
+        v_idx = torch.stack([torch.randperm(S, generator=g)[:nv] for _ in range(2)]).view(1, 2, -1).int().to(device)
+        s_idx = torch.stack([torch.randperm(S, generator=g)[:ns] for _ in range(2)]).view(1, 2, -1).int()
+        s_idx[..., 0] = 0
+        s_idx = s_idx.to(device)
+        bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, S, bm, bn)
+        for b, h, qb, offs, cols in convert_vertical_slash_merged_py(v_idx.cpu(), s_idx.cpu(), S, bm, bn):
+            n, c = int(bc[b, h, qb]), int(cc[b, h, qb])
+            assert bo[b, h, qb, :n].tolist() == offs
+            assert sorted(ci[b, h, qb, :c].tolist()) == sorted(cols)
+
+
+def test_vertical_slash_convert_merged_cpu():
+    """Merged unaligned slash segments (the default conversion) against its Python definition."""
+    _check_convert_merged("cpu")
+
+
+@pytest.mark.gpu
+def test_vertical_slash_convert_merged_gpu():
+    _check_convert_merged("cuda")
 
 
 def test_vertical_slash_convert_cpu():
