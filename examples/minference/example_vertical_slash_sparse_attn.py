@@ -218,13 +218,15 @@ def convert_vertical_slash_merged_py(v_idx, s_idx, seq_len, block_M=64, block_N=
     return out
 
 
-def convert_vertical_slash_indexes(v_idx, s_idx, seq_len, block_M=64, block_N=64, merged=True):
+def convert_vertical_slash_indexes(v_idx, s_idx, seq_len, block_M=64, block_N=64, merged=None):
     """(block_count, block_offset, column_count, column_index) int32 from a device kernel: ``merged``
-    (default) unaligned dense ranges over merged slash segments (``vs_convert_merged``), else
-    ``block_N``-aligned key blocks (``vs_convert``); block offsets ascending, columns in input
+    (default past 16K keys) unaligned dense ranges over merged slash segments (``vs_convert_merged``),
+    else ``block_N``-aligned key blocks (``vs_convert``); block offsets ascending, columns in input
     order, unused slots -1."""
     import torch
     B, H, NV = v_idx.shape
+    if merged is None:
+        merged = seq_len > 16384
     if merged:
         k = vs_convert_merged(B, H, seq_len, NV, s_idx.shape[-1], block_M, block_N)
         return k(v_idx.int().contiguous(), torch.sort(s_idx.int(), dim=-1, descending=True).values.contiguous())
@@ -424,6 +426,10 @@ def vertical_slash_sparse_attention(q, k, v, v_idx, s_idx, block_M=128, block_N=
     NQ = (S + block_M - 1) // block_M
     if num_split is None:
         num_split = max(1, min(8, 512 // max(1, NQ * H * B)))
+    # merged unaligned slash segments attend fewer keys, which pays past 16K keys (32K / 64K:
+    # -6..-13 % end to end); below that nearly every key block is covered anyway and the aligned
+    # conversion's two serial prefix sums (instead of four) are the cheaper index pass
+    # (profiles/r6/minference_table_merged.md against minference_table_split.md)
     bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, S, block_M, block_N)
     k_ = vs_sparse_flashattn(B, H, S, D, bo.shape[-1], ci.shape[-1], block_M, block_N, threads=threads,
                              num_stages=num_stages, dtype=str(q.dtype).replace("torch.", ""), num_split=num_split)
@@ -434,11 +440,11 @@ def vertical_slash_sparse_attention(q, k, v, v_idx, s_idx, block_M=128, block_N=
     return k_(q, k, v, bc, bo, cc, ci, opart, lse)
 
 
-def ref_program(q, k, v, v_idx, s_idx, block_M=64, block_N=64):
+def ref_program(q, k, v, v_idx, s_idx, block_M=64, block_N=64, merged=None):
     """Dense fp32 softmax over exactly the keys selected by convert_vertical_slash_indexes."""
     import torch
     B, H, S, D = q.shape
-    bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, S, block_M, block_N)
+    bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, S, block_M, block_N, merged)
     allowed = torch.zeros(B, H, S, S, dtype=torch.bool, device=q.device)
     NQ = bo.shape[2]
     for qb in range(NQ):

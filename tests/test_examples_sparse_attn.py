@@ -59,11 +59,23 @@ def _check_convert_merged(device):
         s_idx = torch.stack([torch.randperm(S, generator=g)[:ns] for _ in range(2)]).view(1, 2, -1).int()
         s_idx[..., 0] = 0
         s_idx = s_idx.to(device)
-        bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, S, bm, bn)
+        bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, S, bm, bn, merged=True)
         for b, h, qb, offs, cols in convert_vertical_slash_merged_py(v_idx.cpu(), s_idx.cpu(), S, bm, bn):
             n, c = int(bc[b, h, qb]), int(cc[b, h, qb])
             assert bo[b, h, qb, :n].tolist() == offs
             assert sorted(ci[b, h, qb, :c].tolist()) == sorted(cols)
+
+
+def test_vertical_slash_merged_attention_cpu():
+    """The attention kernel over merged unaligned segments (dense tiles at arbitrary key offsets)."""
+    from example_vertical_slash_sparse_attn import ref_program, vs_sparse_flashattn, convert_vertical_slash_indexes
+    q, k, v, v_idx, s_idx = _vs_inputs(1, 2, 512, "cpu", 40, [[0, 300, 37], [0, 100, 7]])
+    bc, bo, cc, ci = convert_vertical_slash_indexes(v_idx, s_idx, 512, 64, 32, merged=True)
+    f = vs_sparse_flashattn.get_tir(1, 2, 512, 64, bo.shape[-1], ci.shape[-1], 64, 32, 128, num_split=2)
+    kern = tilelang.compile(f, out_idx=[-1], target="cpu", pass_configs={"tl.enable_fast_math": True})
+    o = kern(q, k, v, bc, bo, cc, ci, torch.empty(1, 2, 2, 512, 64), torch.empty(1, 2, 2, 512))
+    torch.testing.assert_close(o.float(), ref_program(q, k, v, v_idx, s_idx, 64, 32, merged=True), rtol=2e-2,
+                               atol=2e-2)
 
 
 def test_vertical_slash_convert_merged_cpu():
