@@ -10,9 +10,9 @@ import torch  # noqa: E402
 from tilelang.profiler import do_bench  # noqa: E402
 from example_vertical_slash_sparse_attn import vertical_slash_sparse_attention, ref_program  # noqa: E402
 
-CFGS = [(64, 64, 256, 2), (64, 64, 256, 3), (64, 64, 256, 4), (32, 64, 256, 3), (64, 128, 256, 2), (128, 64, 256, 2),
-        (128, 64, 512, 2), (64, 32, 256, 3)]
-for S, nv, ns in ((8192, 1000, 200), (65536, 1000, 600)):
+CFGS = [(64, 64, 256, 2), (64, 128, 256, 2), (128, 64, 512, 2), (128, 128, 512, 2), (128, 32, 512, 3),
+        (128, 64, 512, 3), (64, 32, 256, 3), (64, 64, 128, 2), (128, 128, 256, 2)]
+for S, nv, ns in ((8192, 1000, 200), (32768, 1000, 600), (65536, 1000, 600)):
     g = torch.Generator(device="cuda").manual_seed(0)
     q, k, v = (torch.randn(1, 1, S, 64, device="cuda", dtype=torch.float16) for _ in range(3))
     v_idx = torch.randperm(S, device="cuda", generator=g)[:nv].view(1, 1, -1)
