@@ -12,7 +12,7 @@ and contributes nothing to the output.  MI355X schedule:
 * causal masking is applied only on the diagonal tiles: the KV loop is split into an unmasked
   main loop and a short masked tail, so the main loop has no per-element selects;
 * query tiles are issued longest-first across ALL heads (grid = (heads, q-tiles) with the
-  tile index reversed), so the tail of the grid is the cheap tiles (causal work is
+  tile index reversed; the q-tile axis slowest -- across batches too -- when there are <= 4), so the tail of the grid is the cheap tiles (causal work is
   triangular; measured 0.75 -> see docs/RESULTS.md).
 """
 import argparse
@@ -120,8 +120,12 @@ def flashattn_sink(batch, heads, seq_q, seq_kv, dim, groups=1, window_size=None,
     def main(Q: T.Tensor(q_shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(kv_shape, dtype),
              Output: T.Tensor(q_shape, dtype), Sinks: T.Tensor([heads], dtype)):
         # heads on the fastest grid axis: every head's heaviest (last) query tile is dispatched
-        # before any lighter one -- global longest-first order for the triangular causal work
-        with T.Kernel(heads, n_qt, batch, threads=threads) as (by, bx, bz):
+        # before any lighter one -- global longest-first order for the triangular causal work; with
+        # few query tiles (<= 4) across batches too (the tile axis slowest), with more the batch
+        # stays slowest for L2 reuse of K/V (the measured split of example_mha_fwd_pipelined)
+        lpt = n_qt <= 4
+        with T.Kernel(heads, *((batch, n_qt) if lpt else (n_qt, batch)), threads=threads) as (by, g1, g2):
+            bx, bz = (g2, g1) if lpt else (g1, g2)
             Q_shared = T.alloc_shared([block_M, dim], dtype)
             K_shared = T.alloc_shared([block_N, dim], dtype)
             V_shared = T.alloc_shared([block_N, dim], dtype)

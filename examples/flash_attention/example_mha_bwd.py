@@ -31,11 +31,12 @@ LOG2E = 1.44269504
 
 @tilelang.jit(out_idx=[3, 4], pass_configs=FAST_MATH)
 def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=256, block_N=64, threads=None, dtype="float16",
-                  groups=1, num_stages=2, dim_v=None, unroll=None):
+                  groups=1, num_stages=2, dim_v=None, unroll=None, lpt=None):
     """Forward that also writes the base-2 LSE (the training forward).  Schedule as the sink
     kernel (examples/attention_sink): heads on the fastest grid axis and the heaviest causal
     query tiles first, KV tiles below the diagonal in an unmasked loop and the diagonal ones
     in a masked loop, lazy O rescale, 8 waves x 32 rows."""
+    lpt = is_causal if lpt is None else lpt
     if threads is None:
         threads = min(512, 64 * (block_M // 16))  # FullRow: >= 16 query rows per wave
     scale = (1.0 / dim)**0.5 * LOG2E
@@ -84,7 +85,10 @@ def flashattn_fwd(batch, heads, seq_len, dim, is_causal, block_M=256, block_N=64
     @T.prim_func
     def flash_fwd(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(v_shape, dtype),
                   Output: T.Tensor(o_shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype)):
-        with T.Kernel(heads, n_qt, batch, threads=threads) as (by, bx, bz):
+        # causal: the query-tile axis is the SLOWEST grid axis, so the heaviest tiles of every
+        # (batch, head) are dispatched before any lighter one (longest-processing-time-first)
+        with T.Kernel(heads, *((batch, n_qt) if lpt else (n_qt, batch)), threads=threads) as (by, g1, g2):
+            bx, bz = (g2, g1) if lpt else (g1, g2)
             Q_shared = T.alloc_shared([block_M, dim], dtype)
             K_shared = T.alloc_shared([block_N, dim], dtype)
             V_shared = T.alloc_shared([block_N, dv_], dtype)
@@ -164,7 +168,7 @@ def flashattn_bwd_postprocess(batch, heads, seq_len, dim, blk=64, threads=256, d
 
 @tilelang.jit(pass_configs=FAST_MATH)
 def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=512, num_stages=2,
-                  dtype="float16", dq_mode="atomic", groups=1, dim_v=None, kv_split=1, unroll=None):
+                  dtype="float16", dq_mode="atomic", groups=1, dim_v=None, kv_split=1, unroll=None, lpt=None):
     """``dq_mode``: "atomic" (fp32 atomics into dQ, one kernel) or "none" (dK/dV only; dQ comes from
     ``flashattn_bwd_dq``) -- the dQ atomics were 85% of the single-kernel time on MI355X.
     GQA (``groups`` query heads per KV head): one block per KV head walks the Q/dO tiles of all
@@ -174,6 +178,7 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
     256 CUs): each KV head's query heads are split over ``kv_split`` workgroups that write fp32
     partial dK/dV [kv_split, batch, seq, head_kv, d] (summed by the caller), so the grid fills
     the chip instead of serialising all ``groups`` heads in one workgroup."""
+    lpt = is_causal if lpt is None else lpt
     sm_scale = (1.0 / dim)**0.5
     scale = sm_scale * LOG2E
     shape = [batch, seq_len, heads, dim]
@@ -194,7 +199,12 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
 
     @T.macro
     def body(Q, K, V, dO, lse, Delta, dQ, dK, dV):
-        with T.Kernel(head_kv * kv_split, T.ceildiv(seq_len, block_M), batch, threads=threads) as (bxs, by, bz):
+        # causal: key tile on the SLOWEST grid axis -- tile 0 (the longest walk) of every (batch, head)
+        # is dispatched first (longest-processing-time-first over the whole grid, not per batch)
+        n_kt = (seq_len + block_M - 1) // block_M
+        with T.Kernel(head_kv * kv_split, *((batch, n_kt) if lpt else (n_kt, batch)), threads=threads) as (
+                bxs, g1, g2):
+            by, bz = (g2, g1) if lpt else (g1, g2)
             bx, sp = (bxs // kv_split, bxs % kv_split) if kv_split > 1 else (bxs, 0)  # KV head, query-head slice
             K_shared = T.alloc_shared([block_M, dim], dtype)
             V_shared = T.alloc_shared([block_M, dv_], dtype)
@@ -279,10 +289,11 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
 
 @tilelang.jit(out_idx=[6], pass_configs=FAST_MATH)
 def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=256, num_stages=2,
-                     dtype="float16", groups=1, dim_v=None, unroll=None):
+                     dtype="float16", groups=1, dim_v=None, unroll=None, lpt=None):
     """dQ without atomics: one block per (query tile, head, batch) walks the KV tiles, recomputing
     P and dP (2 extra GEMMs) and accumulating dQ = dS K in registers -- on MI355X this is ~4x
     faster than fp32 atomics from every KV block (measured: docs/RESULTS.md)."""
+    lpt = is_causal if lpt is None else lpt
     sm_scale = (1.0 / dim)**0.5
     scale = sm_scale * LOG2E
     shape = [batch, seq_len, heads, dim]
@@ -297,8 +308,10 @@ def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N
                      dO: T.Tensor(o_shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
                      Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dQ: T.Tensor(shape, dtype)):
         n_t = (seq_len + block_M - 1) // block_M
-        with T.Kernel(heads, n_t, batch, threads=threads) as (bx, by_raw, bz):
-            # causal: the longest rows of dQ (last query tiles) are dispatched first
+        # causal: the query-tile axis is the slowest, so the longest dQ rows (last query tiles) of
+        # every (batch, head) are dispatched first
+        with T.Kernel(heads, *((batch, n_t) if lpt else (n_t, batch)), threads=threads) as (bx, g1, g2):
+            by_raw, bz = (g2, g1) if lpt else (g1, g2)
             by = (n_t - 1 - by_raw) if is_causal else by_raw
             q = T.alloc_shared([block_M, dim], dtype)
             do = T.alloc_shared([block_M, dv_], dtype)
@@ -339,7 +352,7 @@ BWD_DQ_MODE = "separate"  # or "atomic" (single kernel, fp32 atomics into dQ)
 BWD_OVERLAP = False  # dQ on a side stream: measured slower (0.374 -> 0.509 ms, profiles/r3/s3/bwd/)
 
 
-def _tiles(D, Dv, kind, causal=False):
+def _tiles(D, Dv, kind, causal=False, S=None):
     """Tile sizes that keep each kernel's LDS (operand tiles + 2-stage rings) under 160 KiB: the
     defaults are sized for D = Dv <= 128; wider heads (e.g. D=192 / Dv=128) halve the streamed tile.
     d64 heads use the winners of scripts/sweep_fa_bwd.py (b8 h32 s1024, profiles/r3/s3/bwd/):
@@ -348,12 +361,18 @@ def _tiles(D, Dv, kind, causal=False):
     main loops run under #pragma unroll where that measured faster (the ring slot of each copy a
     constant; outputs bitwise identical; profiles/r6/fa_bwd_unroll_ab.log, fa_train_unroll_ab.log):
     d64 dK/dV 173 -> 156 us, d128 dK/dV / dQ +8.5 / +9.4 %, forward +2-7 % non-causal; the causal
-    d128 forward and dK/dV and the GQA d192 dK/dV lose 0.5-1.7 % and keep the plain loop."""
+    d128 forward and dK/dV and the GQA d192 dK/dV lose 0.5-1.7 % and keep the plain loop.
+    Causal d64 with the tile axis slowest in the grid (longest walks of every (batch, head) first,
+    ``lpt``; profiles/r6/fa_bwd_lpt_ab*.log): dK/dV 128x32 over 4 waves up to S = 1024 (139.5 ->
+    130.7 us at b8 h32 s1024), the non-causal 256x64 / 8-wave tile beyond (b2 h32 s4096 430 ->
+    349 us); dQ 128x64 over 4 waves (98 -> 93 us, 304 -> 277 us)."""
     fwd = {} if causal else dict(unroll=2)
     if D + Dv <= 128:
         if causal:
-            return {"fwd": fwd, "bwd": dict(block_M=64, block_N=32, threads=256, unroll=2),
-                    "dq": dict(block_M=64, block_N=64, threads=256, unroll=2)}[kind]
+            long_s = S is not None and S >= 2048
+            bwd = dict(block_M=256, block_N=64, threads=512, unroll=4) if long_s else \
+                dict(block_M=128, block_N=32, threads=256, unroll=2)
+            return {"fwd": fwd, "bwd": bwd, "dq": dict(block_M=128, block_N=64, threads=256, unroll=2)}[kind]
         return {"fwd": fwd, "bwd": dict(block_M=256, block_N=64, threads=512, unroll=4),
                 "dq": dict(block_M=128, block_N=64, threads=512, unroll=4)}[kind]
     if D + Dv <= 256:
@@ -388,7 +407,7 @@ class _attention:
                     dt = "bfloat16" if q.dtype == torch.bfloat16 else "float16"
                     Dv = v.shape[-1]
                     fwd = flashattn_fwd(B, H, S, D, causal, dtype=dt, groups=G, dim_v=Dv,
-                                        **_tiles(D, Dv, "fwd", causal))
+                                        **_tiles(D, Dv, "fwd", causal, S))
                     o, lse = fwd(q, k, v)
                     ctx.save_for_backward(q, k, v, o, lse)
                     ctx.causal = causal
@@ -405,19 +424,19 @@ class _attention:
                     delta = flashattn_bwd_preprocess(B, H, S, Dv, dtype=dt)(o, do)
                     dk = torch.empty_like(k)
                     dv = torch.empty_like(v)
-                    bw = _tiles(D, Dv, "bwd", ctx.causal)
+                    bw = _tiles(D, Dv, "bwd", ctx.causal, S)
                     split = _kv_split(B, S, k.shape[2], G, bw.get("block_M", 128))
                     if BWD_DQ_MODE == "atomic":
                         dq = torch.zeros(B, S, H, D, dtype=torch.float32, device=q.device)
                         bwd = flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv,
-                                            **_tiles(D, Dv, "bwd", ctx.causal))
+                                            **bw)
                         bwd(q, k, v, do, lse, delta, dq, dk, dv)
                         return flashattn_bwd_postprocess(B, H, S, D, dtype=dt)(dq), dk, dv, None
                     # dK/dV kernel without dQ + an atomic-free dQ kernel; they only share read-only
                     # inputs, so with BWD_OVERLAP the dQ kernel runs on a side stream and fills the
                     # CUs the dK/dV grid's tail leaves idle
                     bdq = flashattn_bwd_dq(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv,
-                                           **_tiles(D, Dv, "dq", ctx.causal))
+                                           **_tiles(D, Dv, "dq", ctx.causal, S))
                     side = None
                     if BWD_OVERLAP and q.is_cuda:
                         main_s = torch.cuda.current_stream()

@@ -94,14 +94,21 @@ def flashattn_pipelined(batch, heads, seq_len, dim, is_causal=False, groups=1, b
 
     @T.macro
     def body(Q, K, V, Output, Sinks):
-        # causal: heads on the fastest grid axis and the longest (last) query tiles dispatched first
-        grid = (heads, n_qt, batch) if is_causal else (n_qt, heads, batch)
+        # causal: heads on the fastest grid axis and the longest (last) query tiles first.  With few
+        # query tiles (<= 4) the tile axis is the slowest, so the longest tiles of EVERY (batch, head)
+        # go before any shorter one (b16 h16 s1024: 499 -> 604 TF); with more, the batch stays the
+        # slowest axis, keeping a head's K/V shared by more co-resident tiles in L2 (b4 h32 s4096:
+        # 1018 vs 995 TF, b8 h32 s2048: 863 vs 834; profiles/r6/fa_lpt_fwd_ab.log)
+        lpt = is_causal and n_qt <= 4
+        grid = (heads, batch, n_qt) if lpt else (heads, n_qt, batch) if is_causal else (n_qt, heads, batch)
         with T.Kernel(*grid, threads=threads) as (g0_, g1_, bz_):
             if xcd_h:
                 pid = g0_ + n_qt * (g1_ + heads * bz_)  # dispatch id: XCD = pid % 8
                 jj = pid // 8
                 hb = (jj // n_qt) * 8 + pid % 8  # (batch, head) of this slot
                 g0, g1, bz = jj % n_qt, hb % heads, hb // heads
+            elif lpt:
+                g0, g1, bz = g0_, bz_, g1_
             else:
                 g0, g1, bz = g0_, g1_, bz_
             bx = (n_qt - 1 - g1) if is_causal else g0
