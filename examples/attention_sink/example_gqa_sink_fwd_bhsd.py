@@ -12,7 +12,8 @@ and contributes nothing to the output.  MI355X schedule:
 * causal masking is applied only on the diagonal tiles: the KV loop is split into an unmasked
   main loop and a short masked tail, so the main loop has no per-element selects;
 * query tiles are issued longest-first across ALL heads (grid = (heads, q-tiles) with the
-  tile index reversed; the q-tile axis slowest -- across batches too -- when there are <= 4), so the tail of the grid is the cheap tiles (causal work is
+  tile index reversed; the q-tile axis slowest -- across batches too -- when there are <= 4),
+  so the tail of the grid is the cheap tiles (causal work is
   triangular; measured 0.75 -> see docs/RESULTS.md).
 """
 import argparse

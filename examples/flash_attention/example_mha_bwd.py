@@ -289,10 +289,13 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
 
 @tilelang.jit(out_idx=[6], pass_configs=FAST_MATH)
 def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=256, num_stages=2,
-                     dtype="float16", groups=1, dim_v=None, unroll=None, lpt=None):
+                     dtype="float16", groups=1, dim_v=None, unroll=None, lpt=None, fuse_delta=False):
     """dQ without atomics: one block per (query tile, head, batch) walks the KV tiles, recomputing
     P and dP (2 extra GEMMs) and accumulating dQ = dS K in registers -- on MI355X this is ~4x
-    faster than fp32 atomics from every KV block (measured: docs/RESULTS.md)."""
+    faster than fp32 atomics from every KV block (measured: docs/RESULTS.md).
+    ``fuse_delta``: the preprocess (Delta = rowsum(O * dO)) is done here for the block's own rows
+    from its dO tile and an O tile (an extra trailing input ``O``), and Delta is written out for the
+    dK/dV kernel, which then runs after this one -- one launch and one pass over dO fewer."""
     lpt = is_causal if lpt is None else lpt
     sm_scale = (1.0 / dim)**0.5
     scale = sm_scale * LOG2E
@@ -303,10 +306,8 @@ def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N
     o_shape = [batch, seq_len, heads, dv_]
     accum_dtype = "float"
 
-    @T.prim_func
-    def flash_bwd_dq(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(v_shape, dtype),
-                     dO: T.Tensor(o_shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
-                     Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dQ: T.Tensor(shape, dtype)):
+    @T.macro
+    def body(Q, K, V, dO, lse, Delta, dQ, O):
         n_t = (seq_len + block_M - 1) // block_M
         # causal: the query-tile axis is the slowest, so the longest dQ rows (last query tiles) of
         # every (batch, head) are dispatched first
@@ -327,7 +328,22 @@ def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N
             T.copy(Q[bz, by * block_M:(by + 1) * block_M, bx, :], q)
             T.copy(dO[bz, by * block_M:(by + 1) * block_M, bx, :], do)
             T.copy(lse[bz, bx, by * block_M:(by + 1) * block_M], lse_f)
-            T.copy(Delta[bz, bx, by * block_M:(by + 1) * block_M], delta_f)
+            if fuse_delta:
+                # Delta of this block's rows (the preprocess kernel's work), staged through LDS so the
+                # reduction's row layout and the score tile's are each inferred on their own
+                o_f = T.alloc_fragment([block_M, dv_], dtype)
+                prod = T.alloc_fragment([block_M, dv_], accum_dtype)
+                d_red = T.alloc_fragment([block_M], accum_dtype)
+                d_s = T.alloc_shared([block_M], accum_dtype)
+                T.copy(O[bz, by * block_M:(by + 1) * block_M, bx, :], o_f)
+                for i, j in T.Parallel(block_M, dv_):
+                    prod[i, j] = T.Cast(accum_dtype, o_f[i, j]) * T.Cast(accum_dtype, do[i, j])
+                T.reduce_sum(prod, d_red, dim=1)
+                T.copy(d_red, d_s)
+                T.copy(d_s, delta_f)
+                T.copy(d_s, Delta[bz, bx, by * block_M:(by + 1) * block_M])
+            else:
+                T.copy(Delta[bz, bx, by * block_M:(by + 1) * block_M], delta_f)
             T.clear(dq)
             loop_ed = T.ceildiv((by + 1) * block_M, block_N) if is_causal else T.ceildiv(seq_len, block_N)
             for k in T.Pipelined(loop_ed, num_stages=num_stages, unroll=unroll):
@@ -345,10 +361,27 @@ def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N
             T.copy(dq, dq_cast)
             T.copy(dq_cast, dQ[bz, by * block_M:(by + 1) * block_M, bx, :])
 
+    if fuse_delta:
+
+        @T.prim_func
+        def flash_bwd_dq(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(v_shape, dtype),
+                         dO: T.Tensor(o_shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
+                         Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dQ: T.Tensor(shape, dtype),
+                         O: T.Tensor(o_shape, dtype)):
+            body(Q, K, V, dO, lse, Delta, dQ, O)
+    else:
+
+        @T.prim_func
+        def flash_bwd_dq(Q: T.Tensor(shape, dtype), K: T.Tensor(kv_shape, dtype), V: T.Tensor(v_shape, dtype),
+                         dO: T.Tensor(o_shape, dtype), lse: T.Tensor([batch, heads, seq_len], accum_dtype),
+                         Delta: T.Tensor([batch, heads, seq_len], accum_dtype), dQ: T.Tensor(shape, dtype)):
+            body(Q, K, V, dO, lse, Delta, dQ, None)
+
     return flash_bwd_dq
 
 
 BWD_DQ_MODE = "separate"  # or "atomic" (single kernel, fp32 atomics into dQ)
+BWD_FUSE_DELTA = True  # Delta computed inside the dQ kernel, which then runs before dK/dV
 BWD_OVERLAP = False  # dQ on a side stream: measured slower (0.374 -> 0.509 ms, profiles/r3/s3/bwd/)
 
 
@@ -421,7 +454,14 @@ class _attention:
                     dt = "bfloat16" if q.dtype == torch.bfloat16 else "float16"
                     Dv = v.shape[-1]
                     do = do.contiguous()
-                    delta = flashattn_bwd_preprocess(B, H, S, Dv, dtype=dt)(o, do)
+                    fuse = BWD_FUSE_DELTA and BWD_DQ_MODE != "atomic" and not BWD_OVERLAP
+                    if fuse:
+                        # the dQ kernel computes Delta for its rows and runs first (no preprocess)
+                        delta = torch.empty(B, H, S, dtype=torch.float32, device=q.device)
+                        dq = flashattn_bwd_dq(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv, fuse_delta=True,
+                                              **_tiles(D, Dv, "dq", ctx.causal, S))(q, k, v, do, lse, delta, o)
+                    else:
+                        delta = flashattn_bwd_preprocess(B, H, S, Dv, dtype=dt)(o, do)
                     dk = torch.empty_like(k)
                     dv = torch.empty_like(v)
                     bw = _tiles(D, Dv, "bwd", ctx.causal, S)
@@ -435,8 +475,8 @@ class _attention:
                     # dK/dV kernel without dQ + an atomic-free dQ kernel; they only share read-only
                     # inputs, so with BWD_OVERLAP the dQ kernel runs on a side stream and fills the
                     # CUs the dK/dV grid's tail leaves idle
-                    bdq = flashattn_bwd_dq(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv,
-                                           **_tiles(D, Dv, "dq", ctx.causal, S))
+                    bdq = None if fuse else flashattn_bwd_dq(B, H, S, D, ctx.causal, dtype=dt, groups=G, dim_v=Dv,
+                                                             **_tiles(D, Dv, "dq", ctx.causal, S))
                     side = None
                     if BWD_OVERLAP and q.is_cuda:
                         main_s = torch.cuda.current_stream()
@@ -453,7 +493,9 @@ class _attention:
                     else:
                         flashattn_bwd(B, H, S, D, ctx.causal, dtype=dt, dq_mode="none", groups=G, dim_v=Dv,
                                       **bw)(q, k, v, do, lse, delta, dk, dv)
-                    if side is None:
+                    if fuse:
+                        pass  # dQ came out of the fused kernel above
+                    elif side is None:
                         dq = bdq(q, k, v, do, lse, delta)
                     else:
                         main_s.wait_stream(side)

@@ -209,6 +209,22 @@ def test_flash_attention_bwd_atomic_free_dq(causal):
         torch.testing.assert_close(a.float(), r, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("causal", [False, True])
+def test_flash_attention_bwd_dq_fused_delta(causal):
+    """dQ kernel computing Delta = rowsum(O * dO) itself (no preprocess kernel): Delta and dQ match
+    the separate preprocess + dQ kernels."""
+    import example_mha_bwd as m
+    B, S, H, D = 1, 256, 2, 64
+    q, k, v, do = [torch.randn(B, S, H, D).half() for _ in range(4)]
+    o, lse = _both(m.flashattn_fwd, B, H, S, D, causal, 64, 64)(q, k, v)
+    delta_ref = _both(m.flashattn_bwd_preprocess, B, H, S, D)(o, do)
+    dq_ref = _both(m.flashattn_bwd_dq, B, H, S, D, causal, 64, 64, 256)(q, k, v, do, lse, delta_ref)
+    delta = torch.full((B, H, S), float("nan"))
+    dq = _both(m.flashattn_bwd_dq, B, H, S, D, causal, 64, 64, 256, fuse_delta=True)(q, k, v, do, lse, delta, o)
+    torch.testing.assert_close(delta, delta_ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dq.float(), dq_ref.float(), rtol=1e-2, atol=1e-2)
+
+
 def test_fused_moe_shared_plus_routed():
     import example_fusedmoe_tilelang as m
     w = m.init_weights(256, 128, 4, 1, device="cpu")
