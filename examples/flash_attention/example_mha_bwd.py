@@ -168,7 +168,8 @@ def flashattn_bwd_postprocess(batch, heads, seq_len, dim, blk=64, threads=256, d
 
 @tilelang.jit(pass_configs=FAST_MATH)
 def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=512, num_stages=2,
-                  dtype="float16", dq_mode="atomic", groups=1, dim_v=None, kv_split=1, unroll=None, lpt=None):
+                  dtype="float16", dq_mode="atomic", groups=1, dim_v=None, kv_split=1, unroll=None, lpt=None,
+                  mask_split=True):
     """``dq_mode``: "atomic" (fp32 atomics into dQ, one kernel) or "none" (dK/dV only; dQ comes from
     ``flashattn_bwd_dq``) -- the dQ atomics were 85% of the single-kernel time on MI355X.
     GQA (``groups`` query heads per KV head): one block per KV head walks the Q/dO tiles of all
@@ -240,10 +241,22 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
                 T.clear(qkT)
                 T.gemm(K_shared, q, qkT, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 T.copy(lse[bz, hq, k * block_N:(k + 1) * block_N], lse_shared)
-                # the causal mask selects the exponent (exp2(-inf) = 0): one pass, no branch
-                for i, j in T.Parallel(block_M, block_N):
-                    qkT[i, j] = T.exp2(T.if_then_else((by * block_M + i <= k * block_N + j) | (not is_causal),
-                                                      qkT[i, j] * scale - lse_shared[j], -T.infinity(accum_dtype)))
+                # the causal mask selects the exponent (exp2(-inf) = 0); ``mask_split``: only tiles that
+                # cross the diagonal take the select (a uniform branch: key tile and query tile are
+                # workgroup-uniform), the ones wholly past it run the plain exponent
+                if is_causal and mask_split:
+                    if by * block_M + block_M - 1 <= k * block_N:
+                        for i, j in T.Parallel(block_M, block_N):
+                            qkT[i, j] = T.exp2(qkT[i, j] * scale - lse_shared[j])
+                    else:
+                        for i, j in T.Parallel(block_M, block_N):
+                            qkT[i, j] = T.exp2(T.if_then_else(by * block_M + i <= k * block_N + j,
+                                                              qkT[i, j] * scale - lse_shared[j],
+                                                              -T.infinity(accum_dtype)))
+                else:
+                    for i, j in T.Parallel(block_M, block_N):
+                        qkT[i, j] = T.exp2(T.if_then_else((by * block_M + i <= k * block_N + j) | (not is_causal),
+                                                          qkT[i, j] * scale - lse_shared[j], -T.infinity(accum_dtype)))
                 T.copy(dO[bz, k * block_N:(k + 1) * block_N, hq, :], do)
                 T.clear(dsT)
                 T.gemm(V_shared, do, dsT, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
@@ -289,7 +302,7 @@ def flashattn_bwd(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64
 
 @tilelang.jit(out_idx=[6], pass_configs=FAST_MATH)
 def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N=64, threads=256, num_stages=2,
-                     dtype="float16", groups=1, dim_v=None, unroll=None, lpt=None, fuse_delta=False):
+                     dtype="float16", groups=1, dim_v=None, unroll=None, lpt=None, fuse_delta=False, mask_split=True):
     """dQ without atomics: one block per (query tile, head, batch) walks the KV tiles, recomputing
     P and dP (2 extra GEMMs) and accumulating dQ = dS K in registers -- on MI355X this is ~4x
     faster than fp32 atomics from every KV block (measured: docs/RESULTS.md).
@@ -353,10 +366,20 @@ def flashattn_bwd_dq(batch, heads, seq_len, dim, is_causal, block_M=128, block_N
                 T.gemm(q, K_shared, s, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
                 T.clear(dp)
                 T.gemm(do, V_shared, dp, transpose_B=True, policy=T.GemmWarpPolicy.FullRow)
-                for i, j in T.Parallel(block_M, block_N):
-                    ds_cast[i, j] = T.exp2(T.if_then_else(
-                        (by * block_M + i >= k * block_N + j) | (not is_causal),
-                        s[i, j] * scale - lse_f[i], -T.infinity(accum_dtype))) * (dp[i, j] - delta_f[i]) * sm_scale
+                if is_causal and mask_split:  # uniform branch: only diagonal tiles take the select
+                    if by * block_M >= k * block_N + block_N - 1:
+                        for i, j in T.Parallel(block_M, block_N):
+                            ds_cast[i, j] = T.exp2(s[i, j] * scale - lse_f[i]) * (dp[i, j] - delta_f[i]) * sm_scale
+                    else:
+                        for i, j in T.Parallel(block_M, block_N):
+                            pe = T.exp2(T.if_then_else(by * block_M + i >= k * block_N + j, s[i, j] * scale - lse_f[i],
+                                                       -T.infinity(accum_dtype)))
+                            ds_cast[i, j] = pe * (dp[i, j] - delta_f[i]) * sm_scale
+                else:
+                    for i, j in T.Parallel(block_M, block_N):
+                        ds_cast[i, j] = T.exp2(T.if_then_else(
+                            (by * block_M + i >= k * block_N + j) | (not is_causal),
+                            s[i, j] * scale - lse_f[i], -T.infinity(accum_dtype))) * (dp[i, j] - delta_f[i]) * sm_scale
                 T.gemm(ds_cast, K_shared, dq, policy=T.GemmWarpPolicy.FullRow)
             T.copy(dq, dq_cast)
             T.copy(dq_cast, dQ[bz, by * block_M:(by + 1) * block_M, bx, :])
