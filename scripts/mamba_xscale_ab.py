@@ -20,6 +20,10 @@ from example_mamba_chunk_scan import chunk_scan_fwd, chunk_scan_fwd_fused, flops
 
 VARIANTS = [  # name, kernel kwargs (a "_pc" entry: pass configs; "_fused": chunk_scan_fwd_fused)
     ("plain 128x64x64", dict(block_M=128, block_N=64, block_K=64)),
+    ("mask_split 128x64x64", dict(block_M=128, block_N=64, block_K=64, mask_split=True)),
+    ("heavy_first 128x64x64", dict(block_M=128, block_N=64, block_K=64, heavy_first=True)),
+    ("mask_split+heavy_first 128x64x64", dict(block_M=128, block_N=64, block_K=64, mask_split=True, heavy_first=True)),
+    ("mask_split 128x64x32", dict(block_M=128, block_N=64, block_K=32, mask_split=True)),
     ("plain 128x64x32", dict(block_M=128, block_N=64, block_K=32)),
     ("xscale 128x64x64", dict(block_M=128, block_N=64, block_K=64, xscale=True)),
     ("ds64 128x64x32 mw4", dict(block_M=128, block_N=64, block_K=32, ds_blk=64, _pc={"tl.min_waves_per_eu": 4})),

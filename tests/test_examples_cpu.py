@@ -159,6 +159,16 @@ def test_mamba_chunk_scan(xcd_group, lean, factored, xscale):
     torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=1e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("mask_split,heavy_first", [(True, False), (False, True), (True, True)])
+def test_mamba_chunk_scan_mask_split(mask_split, heavy_first):
+    """Diagonal-only causal select (uniform branch) and reversed row-tile order."""
+    import example_mamba_chunk_scan as m
+    args = m.make_inputs(1, 512, 128, 1, 2, 64, 64, device="cpu")
+    k = _both(m.chunk_scan_fwd, 1, 512, 128, 1, 2, 64, 64, block_M=64, block_K=32, mask_split=mask_split,
+              heavy_first=heavy_first)
+    torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=1e-2, atol=2e-2)
+
+
 def test_mamba_chunk_scan_factored_strong_decay():
     """The factored decay exp(a_i - c) exp(c - b_j) where the per-element decays span far beyond
     fp32's exponent range inside a chunk (dA down to -4 per step: -500 over a chunk): the row

@@ -161,6 +161,15 @@ def test_mamba_chunk_scan(xcd_group, lean, factored, xscale):
     torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=2e-2, atol=5e-2)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mask_split,heavy_first", [(True, False), (True, True)])
+def test_mamba_chunk_scan_mask_split(mask_split, heavy_first):
+    import example_mamba_chunk_scan as m
+    args = m.make_inputs(2, 4096, 256, 1, 8, 64, 128)
+    k = m.chunk_scan_fwd(2, 4096, 256, 1, 8, 64, 128, block_K=64, mask_split=mask_split, heavy_first=heavy_first)
+    torch.testing.assert_close(k(*args).float(), m.ref_program(*args), rtol=2e-2, atol=5e-2)
+
+
 def test_mamba_chunk_scan_factored_strong_decay():
     import example_mamba_chunk_scan as m
     args = m.make_inputs(1, 1024, 256, 1, 4, 64, 128)
