@@ -101,11 +101,13 @@ class _SinkAttn:
                     G = H // k.shape[2]
                     dt = "bfloat16" if q.dtype == torch.bfloat16 else "float16"
                     do = do.contiguous()
-                    delta = fa.flashattn_bwd_preprocess(B, H, S, D, dtype=dt)(o, do)
+                    # Delta' = rowsum(o' dO) inside the dQ kernel (fuse_delta), which runs first
+                    delta = torch.empty(B, H, S, dtype=torch.float32, device=q.device)
+                    dq = fa.flashattn_bwd_dq(B, H, S, D, True, dtype=dt, groups=G, fuse_delta=True)(q, k, v, do, lse,
+                                                                                                   delta, o)
                     dk, dv = torch.empty_like(k), torch.empty_like(v)
                     fa.flashattn_bwd(B, H, S, D, True, dtype=dt, dq_mode="none", groups=G)(q, k, v, do, lse, delta,
                                                                                             dk, dv)
-                    dq = fa.flashattn_bwd_dq(B, H, S, D, True, dtype=dt, groups=G)(q, k, v, do, lse, delta)
                     ds = sink_grad(B, S, H)(lse, delta, sinks.float().contiguous())
                     return dq, dk, dv, ds.to(sinks.dtype)
 
